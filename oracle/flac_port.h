@@ -1,0 +1,75 @@
+/*
+ * flac_port.h — CPU restatement of python-audio-tools' FLAC encoder
+ * (src/encoders/flac.c) and a FLAC decoder (semantics of src/decoders/flac.c).
+ *
+ * TEST INFRASTRUCTURE ONLY.  This library is the parity checker and the
+ * "port" CPU baseline; the product path (libatgpu.so) never links, loads or
+ * calls it.  Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline
+ * leg may use it.
+ *
+ * Parity pinning: checked byte-for-byte against the reference C encoder built
+ * from /root/reference/src (oracle/_ref/flacenc, see oracle/Makefile) and
+ * against the reference's own known-answer fixture test/tone.flac
+ * (tests/golden/).
+ */
+#ifndef FLAC_PORT_H
+#define FLAC_PORT_H
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* Encoder options, same meaning as the keyword arguments of
+   audiotools.encoders.encode_flac (reference src/encoders/flac.c:52-108). */
+typedef struct {
+    uint32_t block_size;
+    uint32_t max_lpc_order;
+    uint32_t min_residual_partition_order; /* accepted, unused (as reference) */
+    uint32_t max_residual_partition_order;
+    int32_t mid_side;
+    int32_t adaptive_mid_side;
+    int32_t exhaustive_model_search;
+    int32_t disable_verbatim_subframes;
+    int32_t disable_constant_subframes;
+    int32_t disable_fixed_subframes;
+    int32_t disable_lpc_subframes;
+    uint32_t padding_size;
+} flacport_options;
+
+/* Encode one whole stream.  pcm is interleaved int32 [pcm_frames][channels].
+   Writes a complete .flac file image into out (capacity out_cap).
+   frame_offsets / frame_lengths (optional, capacity max_frames) receive the
+   (byte offset from first frame, pcm frames) list that encode_flac returns.
+   Returns 0 on success, negative on error. */
+int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
+                    uint32_t channels, uint32_t bits_per_sample,
+                    uint32_t sample_rate, const flacport_options *opts,
+                    uint8_t *out, size_t out_cap, size_t *out_len,
+                    uint64_t *frame_offsets, uint32_t *frame_lengths,
+                    size_t max_frames, size_t *n_frames);
+
+/* Worst-case output size for flacport_encode / the GPU engine. */
+size_t flacport_max_stream_bytes(uint64_t pcm_frames, uint32_t channels,
+                                 uint32_t bits_per_sample, uint32_t block_size,
+                                 uint32_t padding_size);
+
+/* MD5 of the little-endian signed PCM bytes (STREAMINFO md5). */
+void flacport_pcm_md5(const int32_t *pcm, uint64_t pcm_frames,
+                      uint32_t channels, uint32_t bits_per_sample,
+                      uint8_t digest[16]);
+
+/* Decode a .flac image.  On success returns 0 and fills the stream
+   parameters; pcm (capacity pcm_cap samples, may be NULL to query) receives
+   interleaved int32 samples.  Verifies CRC-8/CRC-16 and, when present,
+   the STREAMINFO MD5 (returns -5 on MD5 mismatch). */
+int flacport_decode(const uint8_t *flac, size_t len,
+                    uint32_t *channels, uint32_t *bits_per_sample,
+                    uint32_t *sample_rate, uint64_t *total_frames,
+                    int32_t *pcm, size_t pcm_cap);
+
+#ifdef __cplusplus
+}
+#endif
+#endif
