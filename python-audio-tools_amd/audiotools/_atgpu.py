@@ -1,0 +1,258 @@
+"""ctypes binding of libatgpu.so — the C ABI declared in include/atgpu.h.
+
+The library holds the HIP kernels (gfx950) and the batch engine.  This
+module only marshals arguments; it never encodes anything itself.  Missing
+library => ImportError, missing GPU => ATGError(ATG_ERR_DEVICE): there is no
+CPU fallback on the product path.
+"""
+
+import ctypes
+import os
+import threading
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("ATGPU_LIB", os.path.join(_HERE, "libatgpu.so"))
+
+ATG_OK = 0
+ATG_ERR_INVALID = -1
+ATG_ERR_UNSUPPORTED = -2
+ATG_ERR_DEVICE = -3
+ATG_ERR_NOMEM = -4
+ATG_ERR_CAPACITY = -5
+
+PCM_S16 = 0
+PCM_S32 = 1
+
+# every function include/atgpu.h declares (tests check the .so exports them)
+EXPORTS = (
+    "atg_abi_version", "atg_last_error", "atg_engine_create",
+    "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
+    "atg_flac_encode_device", "atg_engine_kernel_times", "atg_device_alloc",
+    "atg_device_free", "atg_copy_to_device", "atg_copy_to_host",
+)
+
+c_u32, c_i32, c_u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+
+
+class FlacOptions(ctypes.Structure):
+    _fields_ = [("block_size", c_u32), ("max_lpc_order", c_u32),
+                ("min_residual_partition_order", c_u32),
+                ("max_residual_partition_order", c_u32),
+                ("mid_side", c_i32), ("adaptive_mid_side", c_i32),
+                ("exhaustive_model_search", c_i32),
+                ("disable_verbatim_subframes", c_i32),
+                ("disable_constant_subframes", c_i32),
+                ("disable_fixed_subframes", c_i32),
+                ("disable_lpc_subframes", c_i32), ("padding_size", c_u32)]
+
+
+class Track(ctypes.Structure):
+    _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64),
+                ("frame_sizes", ctypes.POINTER(c_u32)), ("n_frame_sizes", c_u64)]
+
+
+class TrackResult(ctypes.Structure):
+    _fields_ = [("out_offset", c_u64), ("bytes", c_u64),
+                ("first_frame", c_u32), ("n_frames", c_u32),
+                ("min_frame_bytes", c_u32), ("max_frame_bytes", c_u32),
+                ("md5", ctypes.c_uint8 * 16), ("status", c_i32),
+                ("reserved", c_u32)]
+
+
+class ATGError(RuntimeError):
+    """failure reported by libatgpu (status code + message)"""
+
+    def __init__(self, status, message):
+        RuntimeError.__init__(self, "%s (atg status %d)" % (message, status))
+        self.status = status
+        self.message = message
+
+
+_lib = None
+_lib_lock = threading.Lock()
+
+
+def load_library():
+    """dlopen libatgpu.so (built in-tree by __graft_entry__.build())"""
+    global _lib
+    with _lib_lock:
+        if _lib is not None:
+            return _lib
+        if not os.path.exists(LIB_PATH):
+            raise ImportError("libatgpu.so not found at %s: build it with "
+                              "`make -C python-audio-tools_amd/csrc` or "
+                              "__graft_entry__.build()" % LIB_PATH)
+        lib = ctypes.CDLL(LIB_PATH)
+        P = ctypes.c_void_p
+        lib.atg_abi_version.restype = ctypes.c_int
+        lib.atg_last_error.restype = ctypes.c_char_p
+        lib.atg_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        lib.atg_engine_create.restype = ctypes.c_int
+        lib.atg_engine_destroy.argtypes = [P]
+        lib.atg_engine_destroy.restype = None
+        lib.atg_flac_batch_bounds.argtypes = [
+            ctypes.POINTER(FlacOptions), ctypes.POINTER(Track), c_u32, c_u32, c_u32,
+            ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
+        lib.atg_flac_batch_bounds.restype = ctypes.c_int
+        lib.atg_flac_encode_host.argtypes = [
+            P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
+            c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult),
+            P, P]
+        lib.atg_flac_encode_host.restype = ctypes.c_int
+        lib.atg_flac_encode_device.argtypes = [
+            P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
+            c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult)]
+        lib.atg_flac_encode_device.restype = ctypes.c_int
+        lib.atg_engine_kernel_times.argtypes = [
+            P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
+            ctypes.c_int]
+        lib.atg_engine_kernel_times.restype = ctypes.c_int
+        lib.atg_device_alloc.argtypes = [P, c_u64, ctypes.POINTER(P)]
+        lib.atg_device_alloc.restype = ctypes.c_int
+        lib.atg_device_free.argtypes = [P, P]
+        lib.atg_device_free.restype = ctypes.c_int
+        lib.atg_copy_to_device.argtypes = [P, P, P, c_u64]
+        lib.atg_copy_to_device.restype = ctypes.c_int
+        lib.atg_copy_to_host.argtypes = [P, P, P, c_u64]
+        lib.atg_copy_to_host.restype = ctypes.c_int
+        _lib = lib
+        return lib
+
+
+def _check(lib, status):
+    if status != ATG_OK:
+        raise ATGError(status, lib.atg_last_error().decode("utf-8", "replace"))
+
+
+def make_options(block_size, max_lpc_order, min_residual_partition_order,
+                 max_residual_partition_order, mid_side=0, adaptive_mid_side=0,
+                 exhaustive_model_search=0, disable_verbatim_subframes=0,
+                 disable_constant_subframes=0, disable_fixed_subframes=0,
+                 disable_lpc_subframes=0, padding_size=4096):
+    return FlacOptions(int(block_size), int(max_lpc_order),
+                       int(min_residual_partition_order),
+                       int(max_residual_partition_order), int(bool(mid_side)),
+                       int(bool(adaptive_mid_side)),
+                       int(bool(exhaustive_model_search)),
+                       int(bool(disable_verbatim_subframes)),
+                       int(bool(disable_constant_subframes)),
+                       int(bool(disable_fixed_subframes)),
+                       int(bool(disable_lpc_subframes)), int(padding_size))
+
+
+def _track_array(tracks):
+    """tracks: iterable of (pcm_offset, pcm_frames[, frame_sizes])"""
+    tracks = list(tracks)
+    arr = (Track * max(1, len(tracks)))()
+    keep = []
+    for i, t in enumerate(tracks):
+        arr[i].pcm_offset = int(t[0])
+        arr[i].pcm_frames = int(t[1])
+        sizes = t[2] if len(t) > 2 else None
+        if sizes is not None:
+            s = np.ascontiguousarray(sizes, dtype=np.uint32)
+            keep.append(s)
+            arr[i].frame_sizes = s.ctypes.data_as(ctypes.POINTER(c_u32))
+            arr[i].n_frame_sizes = len(s)
+        else:
+            arr[i].frame_sizes = None
+            arr[i].n_frame_sizes = 0
+    return arr, len(tracks), keep
+
+
+class Engine(object):
+    """one libatgpu engine (two HIP streams + workspace) on one device"""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        _check(self.lib, self.lib.atg_engine_create(int(device), ctypes.byref(h)))
+        self.handle = h
+
+    def close(self):
+        if self.handle:
+            self.lib.atg_engine_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def bounds(self, options, tracks, channels, bits_per_sample):
+        arr, n, _keep = _track_array(tracks)
+        nf, nb = c_u64(), c_u64()
+        _check(self.lib, self.lib.atg_flac_batch_bounds(
+            ctypes.byref(options), arr, n, channels, bits_per_sample,
+            ctypes.byref(nf), ctypes.byref(nb)))
+        return nf.value, nb.value
+
+    def encode(self, options, pcm, tracks, channels, bits_per_sample,
+               sample_rate):
+        """encode a batch held in host memory.
+
+        pcm: numpy int16 (bits <= 16) or int32 interleaved samples.
+        Returns (out: uint8 array, results: list of TrackResult,
+                 frame_offsets: uint64 array, frame_pcm: uint32 array)."""
+        pcm = np.ascontiguousarray(pcm)
+        if pcm.dtype == np.int16:
+            fmt = PCM_S16
+        elif pcm.dtype == np.int32:
+            fmt = PCM_S32
+        else:
+            raise TypeError("pcm must be int16 or int32")
+        tracks = list(tracks)
+        nf, nb = self.bounds(options, tracks, channels, bits_per_sample)
+        arr, n, keep = _track_array(tracks)
+        out = np.empty(max(1, nb), dtype=np.uint8)
+        res = (TrackResult * max(1, n))()
+        offs = np.zeros(max(1, nf), dtype=np.uint64)
+        fpcm = np.zeros(max(1, nf), dtype=np.uint32)
+        _check(self.lib, self.lib.atg_flac_encode_host(
+            self.handle, ctypes.byref(options), pcm.ctypes.data_as(ctypes.c_void_p),
+            fmt, arr, n, channels, bits_per_sample, sample_rate,
+            out.ctypes.data_as(ctypes.c_void_p), nb, res,
+            offs.ctypes.data_as(ctypes.c_void_p), fpcm.ctypes.data_as(ctypes.c_void_p)))
+        return out, [res[i] for i in range(n)], offs[:nf], fpcm[:nf]
+
+    def encode_device(self, options, d_pcm, fmt, tracks, channels,
+                      bits_per_sample, sample_rate, d_out, out_cap):
+        """encode a batch whose PCM is already in device memory; the .flac
+        images stay in device memory at d_out.  Returns the TrackResults."""
+        arr, n, keep = _track_array(tracks)
+        res = (TrackResult * max(1, n))()
+        _check(self.lib, self.lib.atg_flac_encode_device(
+            self.handle, ctypes.byref(options), ctypes.c_void_p(d_pcm), fmt, arr, n,
+            channels, bits_per_sample, sample_rate, ctypes.c_void_p(d_out),
+            out_cap, res))
+        return [res[i] for i in range(n)]
+
+    def kernel_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self.lib.atg_engine_kernel_times(self.handle, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
+_engine = None
+_engine_lock = threading.Lock()
+
+
+def default_device():
+    for var in ("ATG_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(var, "") != "":
+            return int(os.environ[var])
+    return 0
+
+
+def engine():
+    """process-wide engine on ATG_DEVICE / LOCAL_RANK / device 0"""
+    global _engine
+    with _engine_lock:
+        if _engine is None:
+            _engine = Engine(default_device())
+        return _engine

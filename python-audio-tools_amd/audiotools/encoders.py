@@ -1,0 +1,126 @@
+"""audiotools.encoders — FLAC encoding on the MI355X engine.
+
+`encode_flac` keeps the reference's Python-visible contract
+(reference src/encoders/flac.c:44-121, registered src/encoders.h:65-67):
+
+    encode_flac(filename, pcmreader, block_size, max_lpc_order,
+                min_residual_partition_order, max_residual_partition_order,
+                mid_side=0, adaptive_mid_side=0, exhaustive_model_search=0,
+                disable_verbatim_subframes=0, disable_constant_subframes=0,
+                disable_fixed_subframes=0, disable_lpc_subframes=0,
+                padding_size=4096) -> [(byte_offset, pcm_frames), ...]
+
+* the output file is opened first; failure raises OSError/IOError carrying
+  errno and filename (flac.c:114-116);
+* PCM is pulled with pcmreader.read(block_size) until an empty FrameList,
+  and every read becomes one FLAC frame, exactly as the reference frame loop
+  does (flac.c:244-274) — with a BufferedPCMReader that is block_size
+  frames plus a shorter final frame;
+* read() must return pcm.FrameList objects (TypeError otherwise,
+  pcmconv.c:244-248); exceptions raised by read() propagate;
+* on success the reader is closed (flac.c:282) and the list of
+  (offset of the frame from the first frame, pcm frames) is returned.
+
+`encode_flac_batch` is the batch form the engine is built for: many tracks
+in one GPU pass (what track2track -j N achieves with N processes).
+"""
+
+import numpy as np
+
+from . import pcm as _pcm
+from . import _atgpu
+
+
+def _collect(pcmreader, block_size):
+    """drain a PCMReader the way the reference frame loop does"""
+    chunks, sizes = [], []
+    while True:
+        fl = pcmreader.read(block_size)
+        if not isinstance(fl, _pcm.FrameList):
+            raise TypeError("results from pcmreader.read() must be FrameLists")
+        if fl.frames == 0:
+            break
+        if fl.channels != pcmreader.channels:
+            raise ValueError("FrameList channel count does not match pcmreader")
+        chunks.append(fl.samples)
+        sizes.append(fl.frames)
+    samples = (np.concatenate(chunks) if chunks else np.zeros(0, dtype=np.int32))
+    return samples, sizes
+
+
+def _frame_sizes_or_none(sizes, block_size):
+    """None when the chunks are plain block_size blocking (+ short tail)"""
+    if all(s == block_size for s in sizes[:-1]) and (not sizes or sizes[-1] <= block_size):
+        return None
+    return np.asarray(sizes, dtype=np.uint32)
+
+
+def encode_flac_batch(filenames, pcmreaders, block_size, max_lpc_order,
+                      min_residual_partition_order, max_residual_partition_order,
+                      mid_side=0, adaptive_mid_side=0, exhaustive_model_search=0,
+                      disable_verbatim_subframes=0, disable_constant_subframes=0,
+                      disable_fixed_subframes=0, disable_lpc_subframes=0,
+                      padding_size=4096):
+    """encode several PCMReaders (same channels / bits / rate) to several
+    .flac files in one GPU batch; returns one offsets list per file"""
+    filenames = list(filenames)
+    pcmreaders = list(pcmreaders)
+    if len(filenames) != len(pcmreaders):
+        raise ValueError("filenames and pcmreaders differ in length")
+    if not pcmreaders:
+        return []
+    r0 = pcmreaders[0]
+    channels, bps, rate = r0.channels, r0.bits_per_sample, r0.sample_rate
+    for r in pcmreaders:
+        if (r.channels, r.bits_per_sample, r.sample_rate) != (channels, bps, rate):
+            raise ValueError("all pcmreaders of a batch must share channels, "
+                             "bits-per-sample and sample rate")
+    files = [open(fn, "wb") for fn in filenames]
+    try:
+        opts = _atgpu.make_options(
+            block_size, max_lpc_order, min_residual_partition_order,
+            max_residual_partition_order, mid_side, adaptive_mid_side,
+            exhaustive_model_search, disable_verbatim_subframes,
+            disable_constant_subframes, disable_fixed_subframes,
+            disable_lpc_subframes, padding_size)
+        parts, tracks, start = [], [], 0
+        for r in pcmreaders:
+            samples, sizes = _collect(r, block_size)
+            frames = len(samples) // channels
+            tracks.append((start, frames, _frame_sizes_or_none(sizes, block_size)))
+            parts.append(samples)
+            start += frames
+        pcm = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
+        if bps <= 16:
+            pcm = pcm.astype(np.int16)
+        out, results, offsets, pcm_frames = _atgpu.engine().encode(
+            opts, pcm, tracks, channels, bps, rate)
+        lists = []
+        for f, res in zip(files, results):
+            f.write(memoryview(out[res.out_offset:res.out_offset + res.bytes]))
+            lo, n = res.first_frame, res.n_frames
+            lists.append([(int(offsets[lo + i]), int(pcm_frames[lo + i]))
+                          for i in range(n)])
+        for r in pcmreaders:
+            r.close()
+        return lists
+    finally:
+        for f in files:
+            f.close()
+
+
+def encode_flac(filename, pcmreader, block_size, max_lpc_order,
+                min_residual_partition_order, max_residual_partition_order,
+                mid_side=0, adaptive_mid_side=0, exhaustive_model_search=0,
+                disable_verbatim_subframes=0, disable_constant_subframes=0,
+                disable_fixed_subframes=0, disable_lpc_subframes=0,
+                padding_size=4096):
+    """encode_flac(filename, pcmreader, block_size, max_lpc_order,
+    min_residual_partition_order, max_residual_partition_order, ...)
+    -> [(byte_offset, pcm_frames), ...]"""
+    return encode_flac_batch(
+        [filename], [pcmreader], block_size, max_lpc_order,
+        min_residual_partition_order, max_residual_partition_order, mid_side,
+        adaptive_mid_side, exhaustive_model_search, disable_verbatim_subframes,
+        disable_constant_subframes, disable_fixed_subframes,
+        disable_lpc_subframes, padding_size)[0]

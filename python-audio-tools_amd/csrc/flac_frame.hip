@@ -1,0 +1,554 @@
+// flac_frame.hip — frame-level stages of the FLAC encoder.
+//
+//   K3 k_frame_decide   stereo decorrelation choice + frame header + size
+//                       (reference flacenc_write_frame / _write_frame_header,
+//                       src/encoders/flac.c:412-671)
+//   K4 k_track_scan     per-track byte offsets of frames, STREAMINFO min/max
+//                       frame size (flac.c:244-279)
+//   K5 k_frame_pack     serialise the chosen subframes MSB-first into an LDS
+//                       frame image, CRC-16 it, copy it to its final place
+//                       (flac.c:813-1016, 1406-1434; bit writer semantics
+//                       src/bitstream.c:1904-1945, 2234-2313)
+//   K6 k_stream_header  "fLaC" + STREAMINFO + VORBIS_COMMENT + PADDING
+//                       (flac.c:208-238, 376-409)
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+#include "launch.h"
+#include "pcm_read.h"
+#include "wave.h"
+
+__constant__ uint16_t c_crc_adv[24][16]; // advance CRC-16 state by 2^m zero bytes
+__constant__ uint32_t c_crc16[256];
+__constant__ uint32_t c_crc8[256];
+
+#define VENDOR "Python Audio Tools 2.22alpha1"
+#define VENDOR_LEN 29
+
+hipError_t upload_crc_tables(const uint16_t *adv, const uint32_t *crc16_tab,
+                             const uint32_t *crc8_tab)
+{
+    hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_adv), adv, sizeof(uint16_t) * 24 * 16);
+    if (e != hipSuccess)
+        return e;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), crc16_tab, sizeof(uint32_t) * 256);
+    if (e != hipSuccess)
+        return e;
+    return hipMemcpyToSymbol(HIP_SYMBOL(c_crc8), crc8_tab, sizeof(uint32_t) * 256);
+}
+
+// ---------------------------------------------------------------- K3
+struct HdrWriter {
+    uint8_t b[16];
+    uint32_t pos;
+    __device__ void put(uint32_t n, uint32_t v)
+    {
+        for (uint32_t i = n; i-- > 0;) {
+            const uint32_t byte = pos >> 3;
+            if ((pos & 7u) == 0u)
+                b[byte] = 0;
+            if ((v >> i) & 1u)
+                b[byte] |= (uint8_t)(0x80u >> (pos & 7u));
+            pos++;
+        }
+    }
+};
+
+__device__ uint32_t frame_header(uint8_t *out, uint32_t block, uint32_t rate, uint32_t bps,
+                                 uint32_t assign, uint32_t number)
+{
+    uint32_t bsc, src, bpc;
+    switch (block) {
+    case 192: bsc = 1; break;
+    case 576: bsc = 2; break;
+    case 1152: bsc = 3; break;
+    case 2304: bsc = 4; break;
+    case 4608: bsc = 5; break;
+    case 256: bsc = 8; break;
+    case 512: bsc = 9; break;
+    case 1024: bsc = 10; break;
+    case 2048: bsc = 11; break;
+    case 4096: bsc = 12; break;
+    case 8192: bsc = 13; break;
+    case 16384: bsc = 14; break;
+    case 32768: bsc = 15; break;
+    default: bsc = block <= 0xFFu ? 6u : (block <= 0xFFFFu ? 7u : 0u);
+    }
+    switch (rate) {
+    case 88200: src = 1; break;
+    case 176400: src = 2; break;
+    case 192000: src = 3; break;
+    case 8000: src = 4; break;
+    case 16000: src = 5; break;
+    case 22050: src = 6; break;
+    case 24000: src = 7; break;
+    case 32000: src = 8; break;
+    case 44100: src = 9; break;
+    case 48000: src = 10; break;
+    case 96000: src = 11; break;
+    default:
+        if (rate <= 255000u && rate % 1000u == 0u)
+            src = 12;
+        else if (rate <= 655350u && rate % 10u == 0u)
+            src = 14;
+        else if (rate <= 0xFFFFu)
+            src = 13;
+        else
+            src = 0;
+    }
+    switch (bps) {
+    case 8: bpc = 1; break;
+    case 12: bpc = 2; break;
+    case 16: bpc = 4; break;
+    case 20: bpc = 5; break;
+    case 24: bpc = 6; break;
+    default: bpc = 0;
+    }
+    HdrWriter w;
+    w.pos = 0;
+    w.put(14, 0x3FFE);
+    w.put(2, 0);
+    w.put(4, bsc);
+    w.put(4, src);
+    w.put(4, assign);
+    w.put(3, bpc);
+    w.put(1, 0);
+    // UTF-8-style frame number (flac.c:1531-1566)
+    if (number <= 0x7Fu) {
+        w.put(8, number);
+    } else {
+        const uint32_t nb = number <= 0x7FFu ? 2 : number <= 0xFFFFu ? 3 : number <= 0x1FFFFFu ? 4
+                          : number <= 0x3FFFFFFu ? 5 : 6;
+        int shift = (int)(nb - 1) * 6;
+        w.put(nb + 1, ((1u << nb) - 1u) << 1);
+        w.put(7 - nb, number >> shift);
+        for (shift -= 6; shift >= 0; shift -= 6) {
+            w.put(2, 2);
+            w.put(6, (number >> shift) & 0x3Fu);
+        }
+    }
+    if (bsc == 6)
+        w.put(8, block - 1);
+    else if (bsc == 7)
+        w.put(16, block - 1);
+    if (src == 12)
+        w.put(8, rate / 1000u);
+    else if (src == 13)
+        w.put(16, rate);
+    else if (src == 14)
+        w.put(16, rate / 10u);
+    const uint32_t n = w.pos >> 3;
+    uint32_t crc = 0;
+    for (uint32_t i = 0; i < n; ++i)
+        crc = c_crc8[crc ^ w.b[i]];
+    w.put(8, crc);
+    for (uint32_t i = 0; i <= n; ++i)
+        out[i] = w.b[i];
+    return n + 1;
+}
+
+__global__ void k_frame_decide(FlacParams p, const FrameInfo *__restrict__ frames,
+                               const SubDesc *__restrict__ sub, FrameDesc *__restrict__ fd)
+{
+    const uint32_t f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= p.n_frames)
+        return;
+    const FrameInfo fi = frames[f];
+    const SubDesc *s = sub + (size_t)f * p.n_cand;
+    FrameDesc d;
+    uint64_t bits = 0;
+    if (p.n_cand == 4u && p.channels == 2u) {
+        const uint32_t L = s[0].bits, R = s[1].bits, A = s[2].bits, D = s[3].bits;
+        uint32_t assign, s0, s1;
+        if (p.mid_side) {
+            uint32_t m = L + D < D + R ? L + D : D + R;
+            m = m < A + D ? m : A + D;
+            if (L + R < m) {
+                assign = 1; s0 = 0; s1 = 1;
+            } else if (L < (R < A ? R : A)) {
+                assign = 8; s0 = 0; s1 = 3;
+            } else if (R < A) {
+                assign = 9; s0 = 3; s1 = 1;
+            } else {
+                assign = 10; s0 = 2; s1 = 3;
+            }
+        } else if (L + R < A + D) {
+            assign = 1; s0 = 0; s1 = 1;
+        } else {
+            assign = 10; s0 = 2; s1 = 3;
+        }
+        d.assign = (uint8_t)assign;
+        d.nsub = 2;
+        d.sub[0] = (uint8_t)s0;
+        d.sub[1] = (uint8_t)s1;
+        bits = (uint64_t)s[s0].bits + s[s1].bits;
+    } else {
+        d.assign = (uint8_t)(p.channels - 1u);
+        d.nsub = (uint8_t)p.channels;
+        for (uint32_t c = 0; c < p.channels; ++c) {
+            d.sub[c] = (uint8_t)c;
+            bits += s[c].bits;
+        }
+    }
+    d.hdr_len = (uint8_t)frame_header(d.hdr, fi.n, p.sample_rate, p.bps, d.assign, fi.index);
+    d.bytes = (uint32_t)(d.hdr_len + (bits + 7u) / 8u + 2u);
+    d.out_off = 0;
+    d.pad = 0;
+    fd[f] = d;
+}
+
+// ---------------------------------------------------------------- K4
+__global__ void k_track_scan(FlacParams p, const TrackInfo *__restrict__ tracks,
+                             const uint32_t *__restrict__ order, FrameDesc *__restrict__ fd,
+                             TrackOut *__restrict__ tout)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.n_tracks)
+        return;
+    const TrackInfo ti = tracks[t];
+    uint64_t off = 0;
+    uint32_t mn = 0xFFFFFFu, mx = 0;
+    for (uint32_t i = 0; i < ti.n_frames; ++i) {
+        const uint32_t f = order[ti.first_pos + i];
+        const uint32_t b = fd[f].bytes;
+        fd[f].out_off = (uint32_t)off;
+        off += b;
+        mn = b < mn ? b : mn;
+        mx = b > mx ? b : mx;
+    }
+    tout[t].bytes = p.header_bytes + off;
+    tout[t].min_fs = mn;
+    tout[t].max_fs = mx;
+}
+
+// ---------------------------------------------------------------- K5
+#define PK_PRE 48
+#define PK_WORDS (PK_PRE + ATG_MAX_BLOCK + ATG_MAX_BLOCK / 64 + 16)
+__device__ __forceinline__ int paddr(int i) { return PK_PRE + i + (i >> 6); }
+
+// OR `n` (1..32) bits of v into the big-endian bit image at bit position pos
+__device__ __forceinline__ void put_bits(uint32_t *fb, uint32_t pos, uint32_t n, uint32_t v)
+{
+    if (n == 0)
+        return;
+    const uint64_t val = (uint64_t)(n >= 32 ? v : (v & ((1u << n) - 1u)));
+    const uint32_t w = pos >> 5, off = pos & 31u;
+    const uint64_t x = val << (64u - off - n);
+    const uint32_t hi = (uint32_t)(x >> 32), lo = (uint32_t)x;
+    if (hi)
+        atomicOr(&fb[w], hi);
+    if (lo)
+        atomicOr(&fb[w + 1], lo);
+}
+
+__device__ __forceinline__ uint32_t fb_byte(const uint32_t *fb, uint32_t b)
+{
+    return (fb[b >> 2] >> (24u - 8u * (b & 3u))) & 0xFFu;
+}
+
+__device__ __forceinline__ uint32_t crc_adv(uint32_t c, int m)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        r ^= ((c >> i) & 1u) ? (uint32_t)c_crc_adv[m][i] : 0u;
+    return r;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_frame_pack(
+    FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
+    const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
+    const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
+{
+    extern __shared__ __attribute__((aligned(16))) uint32_t fb[];
+    __shared__ int32_t sl[PK_WORDS];
+    __shared__ int32_t cfs[ATG_MAX_LPC];
+    __shared__ uint32_t crc_tab[256];
+
+    const uint32_t f = blockIdx.x;
+    const int lane = threadIdx.x;
+    const FrameInfo fi = frames[f];
+    const FrameDesc fd = fdesc[f];
+    const uint32_t N = fi.n;
+    const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
+    const uint32_t words = (fd.bytes + 3u) / 4u + 1u;
+
+    for (uint32_t i = lane; i < words; i += 64)
+        fb[i] = 0;
+    for (uint32_t i = lane; i < 256; i += 64)
+        crc_tab[i] = c_crc16[i];
+    for (int i = lane; i < PK_PRE; i += 64)
+        sl[i] = 0;
+    __syncthreads();
+    if (lane < fd.hdr_len)
+        put_bits(fb, 8u * lane, 8, fd.hdr[lane]);
+    uint32_t pos = 8u * fd.hdr_len;
+
+    // lane run mapping (same as the search kernel)
+    const uint32_t tz = N ? (uint32_t)__builtin_ctz(N) : 0u;
+    uint32_t P = p.max_porder < tz ? p.max_porder : tz;
+    P = P > ATG_MAX_PORDER ? ATG_MAX_PORDER : P;
+    const uint32_t G = 64u >> P, S = N >> P, R = (S + G - 1u) / G;
+    const uint32_t jf = (uint32_t)lane / G, qf = (uint32_t)lane % G;
+    uint32_t ra = jf * S + qf * R, re = ra + R;
+    re = re < (jf + 1u) * S ? re : (jf + 1u) * S;
+    ra = ra < re ? ra : re;
+
+    for (uint32_t si = 0; si < fd.nsub; ++si) {
+        const uint32_t cand = fd.sub[si];
+        const SubDesc d = sub[(size_t)f * p.n_cand + cand];
+        const uint32_t start = pos;
+        const uint32_t w = d.wasted;
+        for (uint32_t i = lane; i < N; i += 64)
+            sl[paddr((int)i)] = cand_sample(pcm, fi.pcm_start + i, p.channels, cand, ms) >> w;
+        if (lane < (int)d.order && d.type == SF_LPC)
+            cfs[lane] = d.coef[lane];
+        if (d.type == SF_FIXED && lane < 4) {
+            const int o = d.order;
+            cfs[lane] = o == 1 ? (lane == 0 ? 1 : 0)
+                      : o == 2 ? (lane == 0 ? 2 : lane == 1 ? -1 : 0)
+                      : o == 3 ? (lane == 0 ? 3 : lane == 1 ? -3 : lane == 2 ? 1 : 0)
+                      : (lane == 0 ? 4 : lane == 1 ? -6 : lane == 2 ? 4 : lane == 3 ? -1 : 0);
+        }
+        __syncthreads();
+        const uint32_t rb = d.sbps - w;
+        if (d.type == SF_CONSTANT) {
+            // 8 zero header bits, then the raw first sample (flac.c:813-830)
+            if (lane == 0)
+                put_bits(fb, pos + 8u, d.sbps, (uint32_t)sl[paddr(0)]);
+            pos += 8u + d.sbps;
+        } else {
+            const uint32_t code = d.type == SF_VERBATIM ? 1u
+                                : d.type == SF_FIXED ? 8u + d.order : 32u + d.order - 1u;
+            if (lane == 0) {
+                put_bits(fb, pos, 7, code);
+                if (w)
+                    put_bits(fb, pos + 7u, w + 1u, (1u << w) | 1u);
+            }
+            const uint32_t hb = 7u + (w ? w + 1u : 1u);
+            if (d.type == SF_VERBATIM) {
+                for (uint32_t i = lane; i < N; i += 64)
+                    put_bits(fb, pos + hb + i * rb, rb, (uint32_t)sl[paddr((int)i)]);
+                pos += hb + N * rb;
+            } else {
+                const uint32_t order = d.order;
+                if ((uint32_t)lane < order)
+                    put_bits(fb, pos + hb + lane * rb, rb, (uint32_t)sl[paddr(lane)]);
+                uint32_t q = pos + hb + order * rb;
+                int shift = 0;
+                if (d.type == SF_LPC) {
+                    shift = d.shift;
+                    if (lane == 0) {
+                        put_bits(fb, q, 4, d.precision - 1u);
+                        put_bits(fb, q + 4u, 5, (uint32_t)shift & 31u);
+                    }
+                    if ((uint32_t)lane < order)
+                        put_bits(fb, q + 9u + lane * d.precision, d.precision,
+                                 (uint32_t)cfs[lane]);
+                    q += 9u + order * d.precision;
+                }
+                if (lane == 0) {
+                    put_bits(fb, q, 2, d.method);
+                    put_bits(fb, q + 2u, 4, d.porder);
+                }
+                const uint32_t rs = q + 6u;
+                const uint32_t po = d.porder;
+                const uint32_t pbits = d.method ? 5u : 4u;
+                const bool degen = (N >> po) < order;
+                const uint32_t jp = (uint32_t)lane >> (6u - po);
+                const uint32_t k = degen ? d.rice[0] : d.rice[jp];
+                // pass 1: code bits of this lane's residuals
+                const int i0 = max((int)ra, (int)order);
+                uint32_t cb = 0;
+                for (int i = i0; i < (int)re; ++i) {
+                    int64_t acc = 0;
+                    for (uint32_t j = 0; j < order; ++j)
+                        acc += (int64_t)cfs[j] * (int64_t)sl[paddr(i - 1 - (int)j)];
+                    const int r = (int)((uint32_t)sl[paddr(i)] - (uint32_t)(int32_t)(acc >> shift));
+                    const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+                    cb += (u >> k) + 1u + k;
+                }
+                const uint32_t excl = wave_excl_scan_u32(cb, lane);
+                const uint32_t total = wave_sum_u32(cb);
+                uint32_t pp;
+                if (!degen) {
+                    pp = rs + pbits * (jp + 1u) + excl;
+                    if (((uint32_t)lane & ((64u >> po) - 1u)) == 0u)
+                        put_bits(fb, rs + pbits * jp + excl, pbits, k);
+                } else {
+                    pp = rs + pbits + excl;
+                    const uint32_t np = 1u << po;
+                    for (uint32_t j = lane; j < np; j += 64)
+                        put_bits(fb, j == 0 ? rs : rs + pbits + total + (j - 1u) * pbits,
+                                 pbits, d.rice[j]);
+                }
+                for (int i = i0; i < (int)re; ++i) {
+                    int64_t acc = 0;
+                    for (uint32_t j = 0; j < order; ++j)
+                        acc += (int64_t)cfs[j] * (int64_t)sl[paddr(i - 1 - (int)j)];
+                    const int r = (int)((uint32_t)sl[paddr(i)] - (uint32_t)(int32_t)(acc >> shift));
+                    const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+                    const uint32_t msb = u >> k;
+                    put_bits(fb, pp + msb, k + 1u, (1u << k) | (k ? (u & ((1u << k) - 1u)) : 0u));
+                    pp += msb + 1u + k;
+                }
+                pos = rs + (1u << po) * pbits + total;
+            }
+        }
+        if (pos - start != d.bits && lane == 0)
+            atomicOr(err, 2u);
+        __syncthreads();
+    }
+    __syncthreads();
+    // CRC-16 of bytes [0, L): 64 chunks of Lc bytes (virtual leading zeros,
+    // which leave a zero-init CRC unchanged), tree-combined with the
+    // "advance by 2^m zero bytes" matrices.
+    const uint32_t L = fd.bytes - 2u;
+    uint32_t lc_log = 2;
+    while ((64u << lc_log) < L)
+        lc_log++;
+    const uint32_t Lc = 1u << lc_log;
+    const int64_t z = (int64_t)(64u << lc_log) - (int64_t)L;
+    int64_t b0 = (int64_t)lane * Lc - z;
+    const int64_t b1 = b0 + Lc;
+    b0 = b0 < 0 ? 0 : b0;
+    uint32_t crc = 0;
+    for (int64_t b = b0; b < b1; ++b)
+        crc = ((crc << 8) ^ crc_tab[((crc >> 8) ^ fb_byte(fb, (uint32_t)b)) & 0xFFu]) & 0xFFFFu;
+#pragma unroll
+    for (int s = 0; s < 6; ++s) {
+        const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << s, 64);
+        if ((lane & ((2 << s) - 1)) == 0)
+            crc = crc_adv(crc, (int)lc_log + s) ^ other;
+    }
+    if (lane == 0)
+        put_bits(fb, 8u * L, 16, crc);
+    __syncthreads();
+
+    // copy the image to its place: aligned dwords inside, bytes at the ends
+    const TrackInfo ti = tracks[fi.track];
+    uint8_t *dst = out + ti.out_base + p.header_bytes + fd.out_off;
+    const uintptr_t d0 = (uintptr_t)dst;
+    const uint32_t head = (uint32_t)((4u - (d0 & 3u)) & 3u);
+    const uint32_t nb = fd.bytes;
+    const uint32_t h = head < nb ? head : nb;
+    if ((uint32_t)lane < h)
+        dst[lane] = (uint8_t)fb_byte(fb, lane);
+    const uint32_t body = (nb - h) / 4u;
+    uint32_t *dw = (uint32_t *)(dst + h);
+    for (uint32_t i = lane; i < body; i += 64) {
+        const uint32_t b = h + 4u * i;
+        dw[i] = fb_byte(fb, b) | (fb_byte(fb, b + 1u) << 8) | (fb_byte(fb, b + 2u) << 16) |
+                (fb_byte(fb, b + 3u) << 24);
+    }
+    const uint32_t tail0 = h + 4u * body;
+    if (tail0 + (uint32_t)lane < nb)
+        dst[tail0 + lane] = (uint8_t)fb_byte(fb, tail0 + lane);
+}
+
+// ---------------------------------------------------------------- K6
+__global__ __launch_bounds__(64) void k_stream_header(FlacParams p,
+                                                      const TrackInfo *__restrict__ tracks,
+                                                      const TrackOut *__restrict__ tout,
+                                                      uint8_t *__restrict__ out)
+{
+    __shared__ uint8_t hdr[128];
+    const uint32_t t = blockIdx.x;
+    const int lane = threadIdx.x;
+    const TrackInfo ti = tracks[t];
+    const TrackOut to = tout[t];
+    uint8_t *dst = out + ti.out_base;
+    if (lane == 0) {
+        uint32_t n = 0;
+        hdr[n++] = 'f'; hdr[n++] = 'L'; hdr[n++] = 'a'; hdr[n++] = 'C';
+        hdr[n++] = 0x00; hdr[n++] = 0; hdr[n++] = 0; hdr[n++] = 34;
+        HdrWriter w; // reuse as a 34-byte STREAMINFO writer in two halves
+        const uint32_t bs = p.block_size > 0xFFFFu ? 0xFFFFu : p.block_size;
+        const uint32_t mn = to.min_fs > 0xFFFFFFu ? 0xFFFFFFu : to.min_fs;
+        const uint32_t mx = to.max_fs > 0xFFFFFFu ? 0xFFFFFFu : to.max_fs;
+        const uint32_t rate = p.sample_rate > 0xFFFFFu ? 0xFFFFFu : p.sample_rate;
+        const uint64_t total = ti.pcm_frames;
+        w.pos = 0;
+        w.put(16, bs);
+        w.put(16, bs);
+        w.put(24, mn);
+        w.put(24, mx);
+        w.put(20, rate);
+        w.put(3, p.channels - 1u > 7u ? 7u : p.channels - 1u);
+        w.put(5, p.bps - 1u > 31u ? 31u : p.bps - 1u);
+        w.put(4, (uint32_t)(total >> 32) & 0xFu);
+        for (int i = 0; i < 14; ++i)
+            hdr[n++] = w.b[i];
+        const uint32_t lo = (uint32_t)total;
+        hdr[n++] = (uint8_t)(lo >> 24); hdr[n++] = (uint8_t)(lo >> 16);
+        hdr[n++] = (uint8_t)(lo >> 8); hdr[n++] = (uint8_t)lo;
+        for (int i = 0; i < 16; ++i)
+            hdr[n++] = to.md5[i];
+        const uint32_t vc = 4u + VENDOR_LEN + 4u;
+        hdr[n++] = 0x04; hdr[n++] = (uint8_t)(vc >> 16); hdr[n++] = (uint8_t)(vc >> 8);
+        hdr[n++] = (uint8_t)vc;
+        hdr[n++] = VENDOR_LEN; hdr[n++] = 0; hdr[n++] = 0; hdr[n++] = 0;
+        const char *v = VENDOR;
+        for (int i = 0; i < VENDOR_LEN; ++i)
+            hdr[n++] = (uint8_t)v[i];
+        hdr[n++] = 0; hdr[n++] = 0; hdr[n++] = 0; hdr[n++] = 0;
+        hdr[n++] = 0x81; hdr[n++] = (uint8_t)(p.padding_size >> 16);
+        hdr[n++] = (uint8_t)(p.padding_size >> 8); hdr[n++] = (uint8_t)p.padding_size;
+    }
+    __syncthreads();
+    const uint32_t fixed = p.header_bytes - p.padding_size;
+    for (uint32_t i = lane; i < fixed; i += 64)
+        dst[i] = hdr[i];
+    for (uint32_t i = fixed + lane; i < p.header_bytes; i += 64)
+        dst[i] = 0;
+}
+
+// ---------------------------------------------------------------- launchers
+hipError_t launch_frame_decide(const FlacParams &p, const FrameInfo *frames, const SubDesc *sub,
+                               FrameDesc *fd, hipStream_t s)
+{
+    if (!p.n_frames)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_frame_decide, dim3((p.n_frames + 255u) / 256u), dim3(256), 0, s, p,
+                       frames, sub, fd);
+    return hipGetLastError();
+}
+
+hipError_t launch_track_scan(const FlacParams &p, const TrackInfo *tracks,
+                             const uint32_t *order, FrameDesc *fd, TrackOut *tout,
+                             hipStream_t s)
+{
+    if (!p.n_tracks)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_track_scan, dim3((p.n_tracks + 63u) / 64u), dim3(64), 0, s, p, tracks,
+                       order, fd, tout);
+    return hipGetLastError();
+}
+
+hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
+                             const FrameInfo *frames, const TrackInfo *tracks,
+                             const SubDesc *sub, const FrameDesc *fd, uint8_t *out,
+                             uint32_t *err, hipStream_t s)
+{
+    if (!p.n_frames)
+        return hipSuccess;
+    const size_t lds = (size_t)p.frame_lds_words * 4u;
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_frame_pack<int16_t>), dim3(p.n_frames), dim3(64), lds, s, p,
+                           (const int16_t *)pcm, frames, tracks, sub, fd, out, err);
+    else
+        hipLaunchKernelGGL((k_frame_pack<int32_t>), dim3(p.n_frames), dim3(64), lds, s, p,
+                           (const int32_t *)pcm, frames, tracks, sub, fd, out, err);
+    return hipGetLastError();
+}
+
+hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
+                                const TrackOut *tout, uint8_t *out, hipStream_t s)
+{
+    if (!p.n_tracks)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_stream_header, dim3(p.n_tracks), dim3(64), 0, s, p, tracks, tout, out);
+    return hipGetLastError();
+}

@@ -1,0 +1,247 @@
+// flac_lpc.hip — K1: LPC analysis of every subframe candidate.
+//
+// Reference: flacenc_best_lpc_coefficients and helpers,
+// src/encoders/flac.c:1018-1324.  Byte-exactness hinges on fp64 order:
+//   * windowed sample  x[n] = (double)s[n] * window[n]       (flac.c:1164-1166)
+//   * autocorrelation  R[L] = sum_{i<N-L} x[i]*x[i+L], ONE accumulator added
+//                      left to right, no fused multiply-add (flac.c:1178-1187)
+//   * Levinson-Durbin, quantisation with frexp/round        (flac.c:1190-1324)
+// This file is compiled with -ffp-contract=off and `#pragma clang fp
+// contract(off)`, so every product is rounded before its add.
+//
+// Mapping: one lane = one subframe candidate of one frame (64 frames per
+// wave, a wave per candidate channel).  Each lane streams its samples once
+// and keeps all LAGS+1 accumulators plus a circular history of the last
+// LAGS windowed samples in registers: 13 independent fp64 add chains per
+// lane, each bit-identical to the reference's sequential loop.  The
+// sequential sum forbids tree/MFMA reductions inside a subframe, so the
+// parallelism is across subframes.
+//
+// The window is applied to the UNSHIFTED candidate samples.  Shifting out
+// w wasted bits scales every x[n] by 2^-w exactly, every R[L] by 4^-w
+// exactly, and leaves the Levinson coefficients bit-identical (all
+// operations are scale-invariant under powers of two in the normal range),
+// so K1 does not need to know the wasted bits.
+#include <hip/hip_runtime.h>
+#include <math.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+#include "launch.h"
+#include "pcm_read.h"
+#include "wave.h"
+
+#pragma clang fp contract(off)
+
+// (int)x on the reference's x86-64 build is cvttsd2si: NaN and out-of-range
+// inputs produce INT_MIN.  v_cvt_i32_f64 saturates instead, so spell it out.
+__device__ __forceinline__ int32_t d2i_x86(double x)
+{
+    if (!(x > -2147483649.0 && x < 2147483648.0))
+        return INT32_MIN;
+    return (int32_t)x;
+}
+
+template <int LAGS>
+__device__ __forceinline__ void quantize_store(const double (&lp)[LAGS],
+                                               int order, int prec,
+                                               int16_t *__restrict__ q,
+                                               int8_t *__restrict__ shift_out)
+{
+    // flacenc_quantize_coefficients (flac.c:1270-1324)
+    double l = 2.2250738585072014e-308; // DBL_MIN
+#pragma unroll
+    for (int i = 0; i < LAGS; ++i) {
+        if (i < order) {
+            const double a = fabs(lp[i]);
+            l = a > l ? a : l;
+        }
+    }
+    int log2cmax;
+    frexp(l, &log2cmax);
+    int shift = (prec - 1) - (log2cmax - 1) - 1;
+    shift = shift < -16 ? -16 : shift;
+    shift = shift > 15 ? 15 : shift;
+    const int qmax = (1 << (prec - 1)) - 1;
+    const int qmin = -(1 << (prec - 1));
+    double err = 0.0;
+#pragma unroll
+    for (int i = 0; i < LAGS; ++i) {
+        if (i < order) {
+            if (shift >= 0)
+                err += lp[i] * (double)(1 << shift);
+            else
+                err += lp[i] / (double)(1 << -shift);
+            const int32_t ei = d2i_x86(round(err));
+            q[i] = (int16_t)(ei < qmin ? qmin : (ei > qmax ? qmax : ei));
+            err -= (double)ei;
+        }
+    }
+    *shift_out = (int8_t)(shift >= 0 ? shift : 0);
+}
+
+template <typename T, int LAGS>
+__global__ __launch_bounds__(64) void k_lpc_analyze(
+    FlacParams p, const T *__restrict__ pcm,
+    const FrameInfo *__restrict__ frames, const double *__restrict__ windows,
+    int16_t *__restrict__ coef_tab, int8_t *__restrict__ shift_tab,
+    uint8_t *__restrict__ est_tab)
+{
+    constexpr int K = LAGS + 1;
+    uint32_t group, cand;
+    xcd_unit_map(blockIdx.x, p.n_cand, &group, &cand);
+    const uint32_t f = group * 64u + threadIdx.x;
+    const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
+    const bool active = f < p.n_frames;
+    const FrameInfo fi = frames[active ? f : 0u];
+    const int M = (int)p.max_lpc_order;
+    const uint32_t N = active ? fi.n : 0u;
+    const bool do_lpc = active && N > (uint32_t)M + 1u;
+    const uint32_t n_loop = do_lpc ? N : 0u;
+    const uint32_t n_max = wave_max_u32(n_loop);
+    if (n_max == 0u)
+        return;
+
+    double acc[K];
+    double hist[K];
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+        acc[k] = 0.0;
+        hist[k] = 0.0;
+    }
+    const double *__restrict__ win = windows + fi.win_off;
+
+    // Stream samples; positions past this lane's N contribute x = 0, which
+    // adds +-0.0 to accumulators that are never -0.0 (exact no-op).
+    for (uint32_t j0 = 0; j0 < n_max; j0 += K) {
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t j = j0 + (uint32_t)u;
+            double x = 0.0;
+            if (j < n_loop) {
+                const int32_t s = cand_sample(pcm, fi.pcm_start + j, p.channels,
+                                              cand, ms);
+                x = (double)s * win[j];
+            }
+            hist[u] = x;
+#pragma unroll
+            for (int L = 0; L < K; ++L) {
+                const double prod = hist[(u - L + K) % K] * x;
+                acc[L] = acc[L] + prod;
+            }
+        }
+    }
+    if (!do_lpc)
+        return;
+
+    // Levinson-Durbin (flac.c:1190-1231), one row at a time.
+    const size_t sub = (size_t)f * p.n_cand + cand;
+    int16_t *__restrict__ qout = coef_tab + sub * p.coef_stride;
+    int8_t *__restrict__ sout = shift_tab + sub * (size_t)M;
+    const int prec = (int)p.qlp_precision;
+
+    double prev[LAGS], cur[LAGS], errv[LAGS];
+#pragma unroll
+    for (int k = 0; k < LAGS; ++k) {
+        prev[k] = 0.0;
+        cur[k] = 0.0;
+        errv[k] = 0.0;
+    }
+    double k0 = acc[1] / acc[0];
+    cur[0] = k0;
+    errv[0] = acc[0] * (1.0 - (k0 * k0));
+    quantize_store<LAGS>(cur, 1, prec, qout, sout);
+#pragma unroll
+    for (int i = 1; i < LAGS; ++i) {
+        if (i < M) {
+#pragma unroll
+            for (int j = 0; j < LAGS; ++j)
+                prev[j] = cur[j];
+            double q = acc[i + 1];
+#pragma unroll
+            for (int j = 0; j < LAGS; ++j)
+                if (j < i)
+                    q -= (prev[j] * acc[i - j]);
+            const double kk = q / errv[i - 1];
+#pragma unroll
+            for (int j = 0; j < LAGS; ++j)
+                if (j < i)
+                    cur[j] = prev[j] - (kk * prev[i - j - 1]);
+            cur[i] = kk;
+            errv[i] = errv[i - 1] * (1.0 - (kk * kk));
+            quantize_store<LAGS>(cur, i + 1, prec, qout + (i * (i + 1)) / 2,
+                                 sout + i);
+        }
+    }
+
+    if (!p.exhaustive) {
+        // flacenc_estimate_best_lpc_order (flac.c:1233-1268)
+        const double ln2 = 0.69314718055994530942;
+        const double error_scale = (ln2 * ln2) / ((double)N * 2.0);
+        int best = 0;
+        double best_bits = 1.7976931348623157e308;
+        bool done = false;
+#pragma unroll
+        for (int i = 0; i < LAGS; ++i) {
+            if (i < M && !done) {
+                const int order = i + 1;
+                if (errv[i] > 0.0) {
+                    const unsigned header = (unsigned)order * (p.bps + p.qlp_precision);
+                    double bpr = log(errv[i] * error_scale) / (ln2 * 2);
+                    bpr = bpr > 0.0 ? bpr : 0.0;
+                    const double est = (double)header + bpr * (double)(N - (unsigned)order);
+                    if (est < best_bits) {
+                        best = order;
+                        best_bits = est;
+                    }
+                } else {
+                    best = order;
+                    done = true;
+                }
+            }
+        }
+        est_tab[sub] = (uint8_t)best;
+    }
+}
+
+template <typename T, int LAGS>
+static hipError_t launch_t(const FlacParams &p, const T *pcm, const FrameInfo *frames,
+                           const double *windows, int16_t *coef_tab,
+                           int8_t *shift_tab, uint8_t *est_tab, hipStream_t s)
+{
+    const uint32_t groups = (p.n_frames + 63u) / 64u;
+    const uint32_t groups8 = (groups + 7u) / 8u * 8u;
+    dim3 grid(groups8 * p.n_cand);
+    hipLaunchKernelGGL((k_lpc_analyze<T, LAGS>), grid, dim3(64), 0, s, p, pcm,
+                       frames, windows, coef_tab, shift_tab, est_tab);
+    return hipGetLastError();
+}
+
+template <typename T>
+static hipError_t launch_lags(const FlacParams &p, const T *pcm,
+                              const FrameInfo *frames, const double *windows,
+                              int16_t *coef_tab, int8_t *shift_tab,
+                              uint8_t *est_tab, hipStream_t s)
+{
+    const uint32_t M = p.max_lpc_order;
+    if (M <= 8)
+        return launch_t<T, 8>(p, pcm, frames, windows, coef_tab, shift_tab, est_tab, s);
+    if (M <= 12)
+        return launch_t<T, 12>(p, pcm, frames, windows, coef_tab, shift_tab, est_tab, s);
+    return launch_t<T, ATG_MAX_LPC>(p, pcm, frames, windows, coef_tab, shift_tab,
+                                    est_tab, s);
+}
+
+hipError_t launch_lpc_analyze(const FlacParams &p, const void *pcm, int fmt,
+                              const FrameInfo *frames, const double *windows,
+                              int16_t *coef_tab, int8_t *shift_tab,
+                              uint8_t *est_tab, hipStream_t s)
+{
+    if (p.max_lpc_order == 0 || !p.try_lpc || p.n_frames == 0)
+        return hipSuccess;
+    if (fmt == 0)
+        return launch_lags<int16_t>(p, (const int16_t *)pcm, frames, windows,
+                                    coef_tab, shift_tab, est_tab, s);
+    return launch_lags<int32_t>(p, (const int32_t *)pcm, frames, windows,
+                                coef_tab, shift_tab, est_tab, s);
+}

@@ -1,0 +1,39 @@
+// launch.h — host-side launchers exported by each kernel translation unit.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+
+// flac_lpc.hip
+hipError_t launch_lpc_analyze(const FlacParams &p, const void *pcm, int fmt,
+                              const FrameInfo *frames, const double *windows,
+                              int16_t *coef_tab, int8_t *shift_tab,
+                              uint8_t *est_tab, hipStream_t s);
+// flac_search.hip
+hipError_t launch_subframe_search(const FlacParams &p, const void *pcm, int fmt,
+                                  const FrameInfo *frames,
+                                  const int16_t *coef_tab,
+                                  const int8_t *shift_tab,
+                                  const uint8_t *est_tab, SubDesc *sub,
+                                  uint32_t *err, hipStream_t s);
+// flac_frame.hip
+hipError_t launch_frame_decide(const FlacParams &p, const FrameInfo *frames,
+                               const SubDesc *sub, FrameDesc *fd, hipStream_t s);
+hipError_t launch_track_scan(const FlacParams &p, const TrackInfo *tracks,
+                             const uint32_t *order, FrameDesc *fd, TrackOut *tout,
+                             hipStream_t s);
+hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
+                             const FrameInfo *frames, const TrackInfo *tracks,
+                             const SubDesc *sub, const FrameDesc *fd,
+                             uint8_t *out, uint32_t *err, hipStream_t s);
+hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
+                                const TrackOut *tout, uint8_t *out,
+                                hipStream_t s);
+hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
+                             const uint32_t *crc16_tab /*[256]*/,
+                             const uint32_t *crc8_tab /*[256]*/);
+// md5.hip
+hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
+                            const TrackInfo *tracks, TrackOut *tout,
+                            hipStream_t s);

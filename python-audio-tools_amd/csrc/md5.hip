@@ -1,0 +1,182 @@
+// md5.hip — STREAMINFO MD5 of each track's PCM (reference: MD5 of the
+// little-endian signed sample bytes fed by the PCM reader callback,
+// src/encoders/flac.c:187-188, 1570-1576; src/pcmconv.c:266-291).
+//
+// MD5 is one serial chain per track, so the kernel runs one lane per track
+// and is launched on its own stream, concurrently with the encoder kernels
+// (it occupies a handful of SIMDs).  Round functions use v_bfi/v_xor3 forms
+// and v_alignbit rotates; message words are fetched 16 per block.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+#include "launch.h"
+
+__device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
+
+#define MD5_STEP(f, a, b, c, d, x, t, s) \
+    a = b + rotl(a + f(b, c, d) + x + t, s)
+#define F1(x, y, z) (z ^ (x & (y ^ z)))
+#define F2(x, y, z) (y ^ (z & (x ^ y)))
+#define F3(x, y, z) (x ^ y ^ z)
+#define F4(x, y, z) (y ^ (x | ~z))
+
+__device__ __forceinline__ void md5_compress(uint32_t h[4], const uint32_t X[16])
+{
+    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
+    MD5_STEP(F1, a, b, c, d, X[0], 0xd76aa478, 7);
+    MD5_STEP(F1, d, a, b, c, X[1], 0xe8c7b756, 12);
+    MD5_STEP(F1, c, d, a, b, X[2], 0x242070db, 17);
+    MD5_STEP(F1, b, c, d, a, X[3], 0xc1bdceee, 22);
+    MD5_STEP(F1, a, b, c, d, X[4], 0xf57c0faf, 7);
+    MD5_STEP(F1, d, a, b, c, X[5], 0x4787c62a, 12);
+    MD5_STEP(F1, c, d, a, b, X[6], 0xa8304613, 17);
+    MD5_STEP(F1, b, c, d, a, X[7], 0xfd469501, 22);
+    MD5_STEP(F1, a, b, c, d, X[8], 0x698098d8, 7);
+    MD5_STEP(F1, d, a, b, c, X[9], 0x8b44f7af, 12);
+    MD5_STEP(F1, c, d, a, b, X[10], 0xffff5bb1, 17);
+    MD5_STEP(F1, b, c, d, a, X[11], 0x895cd7be, 22);
+    MD5_STEP(F1, a, b, c, d, X[12], 0x6b901122, 7);
+    MD5_STEP(F1, d, a, b, c, X[13], 0xfd987193, 12);
+    MD5_STEP(F1, c, d, a, b, X[14], 0xa679438e, 17);
+    MD5_STEP(F1, b, c, d, a, X[15], 0x49b40821, 22);
+    MD5_STEP(F2, a, b, c, d, X[1], 0xf61e2562, 5);
+    MD5_STEP(F2, d, a, b, c, X[6], 0xc040b340, 9);
+    MD5_STEP(F2, c, d, a, b, X[11], 0x265e5a51, 14);
+    MD5_STEP(F2, b, c, d, a, X[0], 0xe9b6c7aa, 20);
+    MD5_STEP(F2, a, b, c, d, X[5], 0xd62f105d, 5);
+    MD5_STEP(F2, d, a, b, c, X[10], 0x02441453, 9);
+    MD5_STEP(F2, c, d, a, b, X[15], 0xd8a1e681, 14);
+    MD5_STEP(F2, b, c, d, a, X[4], 0xe7d3fbc8, 20);
+    MD5_STEP(F2, a, b, c, d, X[9], 0x21e1cde6, 5);
+    MD5_STEP(F2, d, a, b, c, X[14], 0xc33707d6, 9);
+    MD5_STEP(F2, c, d, a, b, X[3], 0xf4d50d87, 14);
+    MD5_STEP(F2, b, c, d, a, X[8], 0x455a14ed, 20);
+    MD5_STEP(F2, a, b, c, d, X[13], 0xa9e3e905, 5);
+    MD5_STEP(F2, d, a, b, c, X[2], 0xfcefa3f8, 9);
+    MD5_STEP(F2, c, d, a, b, X[7], 0x676f02d9, 14);
+    MD5_STEP(F2, b, c, d, a, X[12], 0x8d2a4c8a, 20);
+    MD5_STEP(F3, a, b, c, d, X[5], 0xfffa3942, 4);
+    MD5_STEP(F3, d, a, b, c, X[8], 0x8771f681, 11);
+    MD5_STEP(F3, c, d, a, b, X[11], 0x6d9d6122, 16);
+    MD5_STEP(F3, b, c, d, a, X[14], 0xfde5380c, 23);
+    MD5_STEP(F3, a, b, c, d, X[1], 0xa4beea44, 4);
+    MD5_STEP(F3, d, a, b, c, X[4], 0x4bdecfa9, 11);
+    MD5_STEP(F3, c, d, a, b, X[7], 0xf6bb4b60, 16);
+    MD5_STEP(F3, b, c, d, a, X[10], 0xbebfbc70, 23);
+    MD5_STEP(F3, a, b, c, d, X[13], 0x289b7ec6, 4);
+    MD5_STEP(F3, d, a, b, c, X[0], 0xeaa127fa, 11);
+    MD5_STEP(F3, c, d, a, b, X[3], 0xd4ef3085, 16);
+    MD5_STEP(F3, b, c, d, a, X[6], 0x04881d05, 23);
+    MD5_STEP(F3, a, b, c, d, X[9], 0xd9d4d039, 4);
+    MD5_STEP(F3, d, a, b, c, X[12], 0xe6db99e5, 11);
+    MD5_STEP(F3, c, d, a, b, X[15], 0x1fa27cf8, 16);
+    MD5_STEP(F3, b, c, d, a, X[2], 0xc4ac5665, 23);
+    MD5_STEP(F4, a, b, c, d, X[0], 0xf4292244, 6);
+    MD5_STEP(F4, d, a, b, c, X[7], 0x432aff97, 10);
+    MD5_STEP(F4, c, d, a, b, X[14], 0xab9423a7, 15);
+    MD5_STEP(F4, b, c, d, a, X[5], 0xfc93a039, 21);
+    MD5_STEP(F4, a, b, c, d, X[12], 0x655b59c3, 6);
+    MD5_STEP(F4, d, a, b, c, X[3], 0x8f0ccc92, 10);
+    MD5_STEP(F4, c, d, a, b, X[10], 0xffeff47d, 15);
+    MD5_STEP(F4, b, c, d, a, X[1], 0x85845dd1, 21);
+    MD5_STEP(F4, a, b, c, d, X[8], 0x6fa87e4f, 6);
+    MD5_STEP(F4, d, a, b, c, X[15], 0xfe2ce6e0, 10);
+    MD5_STEP(F4, c, d, a, b, X[6], 0xa3014314, 15);
+    MD5_STEP(F4, b, c, d, a, X[13], 0x4e0811a1, 21);
+    MD5_STEP(F4, a, b, c, d, X[4], 0xf7537e82, 6);
+    MD5_STEP(F4, d, a, b, c, X[11], 0xbd3af235, 10);
+    MD5_STEP(F4, c, d, a, b, X[2], 0x2ad7d2bb, 15);
+    MD5_STEP(F4, b, c, d, a, X[9], 0xeb86d391, 21);
+    h[0] += a;
+    h[1] += b;
+    h[2] += c;
+    h[3] += d;
+}
+
+// byte j of the track's little-endian PCM byte stream (generic formats)
+template <typename T>
+__device__ __forceinline__ uint32_t pcm_byte(const T *s, uint64_t j, uint32_t bb)
+{
+    const uint64_t k = j / bb;
+    const uint32_t r = (uint32_t)(j - k * bb);
+    return ((uint32_t)(int32_t)s[k] >> (8u * r)) & 0xFFu;
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restrict__ pcm,
+                                                  const TrackInfo *__restrict__ tracks,
+                                                  TrackOut *__restrict__ tout)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.n_tracks)
+        return;
+    const TrackInfo ti = tracks[t];
+    const uint32_t bb = p.bps / 8u;
+    const T *s = pcm + ti.pcm_start * p.channels;
+    const uint64_t nbytes = ti.pcm_frames * p.channels * bb;
+    // fast path: the sample container IS the byte stream (S16 at 16 bits)
+    const bool raw = sizeof(T) == 2 && bb == 2 && (((uintptr_t)s) & 15u) == 0;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    uint32_t X[16];
+    const uint64_t full = nbytes / 64u;
+    if (raw) {
+        const uint4 *q = (const uint4 *)s;
+        for (uint64_t blk = 0; blk < full; ++blk) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                const uint4 v = q[blk * 4 + i];
+                X[4 * i] = v.x;
+                X[4 * i + 1] = v.y;
+                X[4 * i + 2] = v.z;
+                X[4 * i + 3] = v.w;
+            }
+            md5_compress(h, X);
+        }
+    } else {
+        for (uint64_t blk = 0; blk < full; ++blk) {
+            for (int i = 0; i < 16; ++i) {
+                const uint64_t j = blk * 64u + 4u * (uint32_t)i;
+                X[i] = pcm_byte(s, j, bb) | (pcm_byte(s, j + 1, bb) << 8) |
+                       (pcm_byte(s, j + 2, bb) << 16) | (pcm_byte(s, j + 3, bb) << 24);
+            }
+            md5_compress(h, X);
+        }
+    }
+    // tail + padding (0x80, zeros, 64-bit little-endian bit length)
+    uint8_t tail[128];
+    const uint32_t rem = (uint32_t)(nbytes - full * 64u);
+    for (uint32_t i = 0; i < rem; ++i)
+        tail[i] = (uint8_t)pcm_byte(s, full * 64u + i, bb);
+    tail[rem] = 0x80;
+    const uint32_t tl = rem < 56u ? 64u : 128u;
+    for (uint32_t i = rem + 1; i < tl - 8u; ++i)
+        tail[i] = 0;
+    const uint64_t bits = nbytes * 8u;
+    for (int i = 0; i < 8; ++i)
+        tail[tl - 8u + i] = (uint8_t)(bits >> (8 * i));
+    for (uint32_t o = 0; o < tl; o += 64) {
+        for (int i = 0; i < 16; ++i)
+            X[i] = tail[o + 4 * i] | ((uint32_t)tail[o + 4 * i + 1] << 8) |
+                   ((uint32_t)tail[o + 4 * i + 2] << 16) | ((uint32_t)tail[o + 4 * i + 3] << 24);
+        md5_compress(h, X);
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            tout[t].md5[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
+hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
+                            const TrackInfo *tracks, TrackOut *tout, hipStream_t s)
+{
+    if (!p.n_tracks)
+        return hipSuccess;
+    dim3 grid((p.n_tracks + 63u) / 64u);
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_track_md5<int16_t>), grid, dim3(64), 0, s, p,
+                           (const int16_t *)pcm, tracks, tout);
+    else
+        hipLaunchKernelGGL((k_track_md5<int32_t>), grid, dim3(64), 0, s, p,
+                           (const int32_t *)pcm, tracks, tout);
+    return hipGetLastError();
+}

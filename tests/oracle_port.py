@@ -1,0 +1,166 @@
+"""ctypes wrapper of oracle/libflacport.so — the CPU restatement of the
+reference FLAC encoder/decoder.  TEST INFRASTRUCTURE ONLY: used by tests/,
+__graft_entry__.smoke() and bench.py's cpu_baseline leg, never by the
+product path.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_DIR = os.path.join(ROOT, "oracle")
+LIB = os.path.join(ORACLE_DIR, "libflacport.so")
+REF_FLACENC = os.path.join(ORACLE_DIR, "_ref", "flacenc")
+
+c_u32, c_i32, c_u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
+
+
+class PortOptions(ctypes.Structure):
+    _fields_ = [("block_size", c_u32), ("max_lpc_order", c_u32),
+                ("min_residual_partition_order", c_u32),
+                ("max_residual_partition_order", c_u32),
+                ("mid_side", c_i32), ("adaptive_mid_side", c_i32),
+                ("exhaustive_model_search", c_i32),
+                ("disable_verbatim_subframes", c_i32),
+                ("disable_constant_subframes", c_i32),
+                ("disable_fixed_subframes", c_i32),
+                ("disable_lpc_subframes", c_i32), ("padding_size", c_u32)]
+
+
+# reference FLAC presets (audiotools/flac.py:1719-1764)
+PRESETS = {
+    "0": dict(block_size=1152, max_lpc_order=0, min_residual_partition_order=0,
+              max_residual_partition_order=3),
+    "1": dict(block_size=1152, max_lpc_order=0, adaptive_mid_side=True,
+              min_residual_partition_order=0, max_residual_partition_order=3),
+    "2": dict(block_size=1152, max_lpc_order=0, exhaustive_model_search=True,
+              min_residual_partition_order=0, max_residual_partition_order=3),
+    "3": dict(block_size=4096, max_lpc_order=6, min_residual_partition_order=0,
+              max_residual_partition_order=4),
+    "4": dict(block_size=4096, max_lpc_order=8, adaptive_mid_side=True,
+              min_residual_partition_order=0, max_residual_partition_order=4),
+    "5": dict(block_size=4096, max_lpc_order=8, mid_side=True,
+              min_residual_partition_order=0, max_residual_partition_order=5),
+    "6": dict(block_size=4096, max_lpc_order=8, mid_side=True,
+              min_residual_partition_order=0, max_residual_partition_order=6),
+    "7": dict(block_size=4096, max_lpc_order=8, mid_side=True,
+              exhaustive_model_search=True, min_residual_partition_order=0,
+              max_residual_partition_order=6),
+    "8": dict(block_size=4096, max_lpc_order=12, mid_side=True,
+              exhaustive_model_search=True, min_residual_partition_order=0,
+              max_residual_partition_order=6),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            subprocess.check_call(["make", "-C", ORACLE_DIR, "port"],
+                                  stdout=subprocess.DEVNULL)
+        lib = ctypes.CDLL(LIB)
+        lib.flacport_max_stream_bytes.restype = ctypes.c_size_t
+        lib.flacport_max_stream_bytes.argtypes = [c_u64, c_u32, c_u32, c_u32, c_u32]
+        lib.flacport_encode.restype = ctypes.c_int
+        lib.flacport_encode.argtypes = [
+            ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32, ctypes.POINTER(PortOptions),
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_size_t)]
+        lib.flacport_decode.restype = ctypes.c_int
+        lib.flacport_decode.argtypes = [
+            ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(c_u32),
+            ctypes.POINTER(c_u32), ctypes.POINTER(c_u32), ctypes.POINTER(c_u64),
+            ctypes.c_void_p, ctypes.c_size_t]
+        lib.flacport_pcm_md5.restype = None
+        lib.flacport_pcm_md5.argtypes = [ctypes.c_void_p, c_u64, c_u32, c_u32,
+                                         ctypes.c_void_p]
+        _lib = lib
+    return _lib
+
+
+def options(**kw):
+    d = dict(mid_side=0, adaptive_mid_side=0, exhaustive_model_search=0,
+             disable_verbatim_subframes=0, disable_constant_subframes=0,
+             disable_fixed_subframes=0, disable_lpc_subframes=0,
+             padding_size=4096)
+    d.update(kw)
+    return PortOptions(d["block_size"], d["max_lpc_order"],
+                       d.get("min_residual_partition_order", 0),
+                       d["max_residual_partition_order"], int(bool(d["mid_side"])),
+                       int(bool(d["adaptive_mid_side"])),
+                       int(bool(d["exhaustive_model_search"])),
+                       int(bool(d["disable_verbatim_subframes"])),
+                       int(bool(d["disable_constant_subframes"])),
+                       int(bool(d["disable_fixed_subframes"])),
+                       int(bool(d["disable_lpc_subframes"])), int(d["padding_size"]))
+
+
+def encode(pcm, channels, bps, rate, **opts):
+    """-> (flac bytes, [(offset, pcm_frames), ...])"""
+    lib = load()
+    o = options(**opts)
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames = len(a) // channels
+    cap = lib.flacport_max_stream_bytes(frames, channels, bps, o.block_size,
+                                        o.padding_size)
+    out = np.empty(cap, dtype=np.uint8)
+    olen = ctypes.c_size_t()
+    nfmax = frames // max(1, o.block_size) + 2
+    offs = np.zeros(nfmax, dtype=np.uint64)
+    lens = np.zeros(nfmax, dtype=np.uint32)
+    nf = ctypes.c_size_t()
+    rc = lib.flacport_encode(a.ctypes.data_as(ctypes.c_void_p), frames, channels, bps,
+                             rate, ctypes.byref(o), out.ctypes.data_as(ctypes.c_void_p),
+                             cap, ctypes.byref(olen),
+                             offs.ctypes.data_as(ctypes.c_void_p),
+                             lens.ctypes.data_as(ctypes.c_void_p), nfmax,
+                             ctypes.byref(nf))
+    if rc != 0:
+        raise RuntimeError("flacport_encode failed: %d" % rc)
+    n = nf.value
+    return out[:olen.value].tobytes(), [(int(offs[i]), int(lens[i])) for i in range(n)]
+
+
+def decode(data):
+    """-> (pcm int32 interleaved, channels, bps, rate); raises on CRC/MD5 error"""
+    lib = load()
+    ch, bps, rate, tot = c_u32(), c_u32(), c_u32(), c_u64()
+    rc = lib.flacport_decode(data, len(data), ctypes.byref(ch), ctypes.byref(bps),
+                             ctypes.byref(rate), ctypes.byref(tot), None, 0)
+    if rc != 0:
+        raise ValueError("flacport_decode header failed: %d" % rc)
+    pcm = np.zeros(tot.value * ch.value, dtype=np.int32)
+    rc = lib.flacport_decode(data, len(data), ctypes.byref(ch), ctypes.byref(bps),
+                             ctypes.byref(rate), ctypes.byref(tot),
+                             pcm.ctypes.data_as(ctypes.c_void_p), len(pcm))
+    if rc != 0:
+        raise ValueError("flacport_decode failed: %d" % rc)
+    return pcm, ch.value, bps.value, rate.value
+
+
+def pcm_md5(pcm, channels, bps):
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    d = np.zeros(16, dtype=np.uint8)
+    lib.flacport_pcm_md5(a.ctypes.data_as(ctypes.c_void_p), len(a) // channels,
+                         channels, bps, d.ctypes.data_as(ctypes.c_void_p))
+    return d.tobytes()
+
+
+def split_flac(data):
+    """-> (list of (block_type, payload bytes), frame region bytes)"""
+    assert data[:4] == b"fLaC"
+    i, blocks = 4, []
+    while True:
+        last, btype = data[i] & 0x80, data[i] & 0x7F
+        n = int.from_bytes(data[i + 1:i + 4], "big")
+        blocks.append((btype, data[i + 4:i + 4 + n]))
+        i += 4 + n
+        if last:
+            break
+    return blocks, data[i:]

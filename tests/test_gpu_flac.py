@@ -1,0 +1,166 @@
+"""GPU parity: libatgpu's FLAC encoder vs the CPU oracle (byte-identical).
+
+Runs on the MI355X box (`pytest -m gpu`).  Every case encodes the same
+seeded PCM with the GPU engine (through the C ABI) and with the oracle
+(oracle/flac_port.c, itself byte-identical to the reference encoder), and
+requires identical .flac images, identical frame offset lists, and a clean
+oracle decode round trip.
+"""
+import hashlib
+import os
+
+import numpy as np
+import pytest
+
+import oracle_port
+import signals
+
+pytestmark = pytest.mark.gpu
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def gpu_encode_tracks(engine, pcms, channels, bps, rate, opts, frame_sizes=None):
+    from audiotools import _atgpu
+    o = _atgpu.make_options(**opts)
+    tracks, parts, start = [], [], 0
+    for i, p in enumerate(pcms):
+        n = len(p) // channels
+        fs = None if frame_sizes is None else frame_sizes[i]
+        tracks.append((start, n, fs))
+        parts.append(p)
+        start += n
+    pcm = np.concatenate(parts) if parts else np.zeros(0, np.int32)
+    pcm = pcm.astype(np.int16 if bps <= 16 else np.int32)
+    out, res, offs, fpcm = engine.encode(o, pcm, tracks, channels, bps, rate)
+    images = []
+    for r in res:
+        img = out[r.out_offset:r.out_offset + r.bytes].tobytes()
+        lst = [(int(offs[r.first_frame + i]), int(fpcm[r.first_frame + i]))
+               for i in range(r.n_frames)]
+        images.append((img, lst))
+    return images
+
+
+def check_batch(engine, pcms, channels, bps, opts, rate=44100):
+    got = gpu_encode_tracks(engine, pcms, channels, bps, rate, opts)
+    for p, (img, lst) in zip(pcms, got):
+        want, wlst = oracle_port.encode(p, channels, bps, rate, **opts)
+        assert img == want, ("GPU/oracle mismatch: %d vs %d bytes, ch=%d bps=%d opts=%r"
+                             % (len(img), len(want), channels, bps, opts))
+        assert lst == wlst
+        dec, ch, b, r = oracle_port.decode(img)
+        assert np.array_equal(dec, p)
+
+
+@pytest.mark.parametrize("preset", ["8", "0", "1", "2", "3", "4", "5", "6", "7"])
+@pytest.mark.parametrize("channels,bps", [(2, 16), (1, 16), (2, 24), (6, 16), (1, 8)])
+def test_presets_vs_oracle(gpu_engine, preset, channels, bps):
+    opts = dict(oracle_port.PRESETS[preset])
+    B = opts["block_size"]
+    rng = np.random.default_rng(int(preset) * 1000 + channels * 100 + bps)
+    pcms = []
+    for kind in ["tone", "sine", "noise", "silence", "chirp", "wasted"]:
+        if kind == "wasted" and bps == 8:
+            continue
+        n = int(rng.integers(1, 3 * B)) if kind != "tone" else 3 * B + 17
+        pcms.append(signals.make(kind, n, channels, bps, seed=int(rng.integers(1 << 30))))
+    check_batch(gpu_engine, pcms, channels, bps, opts)
+
+
+def test_small_and_fsd_streams(gpu_engine):
+    opts = dict(block_size=1152, max_lpc_order=16, min_residual_partition_order=0,
+                max_residual_partition_order=3, mid_side=True, adaptive_mid_side=True,
+                exhaustive_model_search=True)
+    for samples, ch, bps in signals.SHORT_STREAMS:
+        check_batch(gpu_engine, [np.array(samples, np.int32)], ch, bps, opts)
+    for bps in (8, 16, 24):
+        pcms = [signals.fsd(p, 100, bps) for p in signals.PATTERNS]
+        check_batch(gpu_engine, pcms, 1, bps, opts)
+    check_batch(gpu_engine, [signals.wasted_bps16(1000)], 2, 16, opts)
+
+
+@pytest.mark.parametrize("block_size", [16, 17, 19, 24, 32, 33, 192, 576, 1000, 4096])
+def test_block_sizes_lpc_orders(gpu_engine, block_size):
+    rng = np.random.default_rng(block_size)
+    noise = rng.integers(-32768, 32768, 32).astype(np.int32)
+    for disable in [{}, dict(disable_verbatim_subframes=True, disable_constant_subframes=True),
+                    dict(disable_verbatim_subframes=True, disable_constant_subframes=True,
+                         disable_fixed_subframes=True)]:
+        for lpc in [0, 1, 2, 4, 8, 9, 12, 15, 16, 17, 31, 32]:
+            opts = dict(block_size=block_size, max_lpc_order=lpc,
+                        min_residual_partition_order=0, max_residual_partition_order=6,
+                        mid_side=True, adaptive_mid_side=True, exhaustive_model_search=True)
+            opts.update(disable)
+            pcms = [np.tile(noise, 400)[:n] for n in (block_size * 3 + 1, 200, 7)]
+            check_batch(gpu_engine, pcms, 1, 16, opts)
+
+
+def test_fractional_lengths(gpu_engine):
+    opts = dict(block_size=256, max_lpc_order=8, min_residual_partition_order=0,
+                max_residual_partition_order=6)
+    lens = [254, 255, 256, 257, 258, 510, 511, 512, 513, 1022, 1023, 1024, 1025, 4095, 4097]
+    pcms = [signals.noise(n, 2, 16, n) for n in lens]
+    check_batch(gpu_engine, pcms, 2, 16, opts)
+
+
+def test_rates_and_headers(gpu_engine):
+    opts = dict(oracle_port.PRESETS["8"])
+    for rate in [8000, 9, 90, 12345, 44100, 90000, 96000, 192000, 700000]:
+        pcms = [signals.make("tone", 9000, 2, 16, seed=rate)]
+        got = gpu_encode_tracks(gpu_engine, pcms, 2, 16, rate, opts)
+        want, _ = oracle_port.encode(pcms[0], 2, 16, rate, **opts)
+        assert got[0][0] == want
+
+
+def test_tone_flac_kat(gpu_engine):
+    """reference known-answer fixture test/tone.flac (FLAC-8 frames)"""
+    data = open(os.path.join(GOLDEN, "tone.flac"), "rb").read()
+    pcm, ch, bps, rate = oracle_port.decode(data)
+    blocks, frames = oracle_port.split_flac(data)
+    img, _ = gpu_encode_tracks(gpu_engine, [pcm], ch, bps, rate,
+                               oracle_port.PRESETS["8"])[0]
+    gblocks, gframes = oracle_port.split_flac(img)
+    assert gblocks[0][1] == blocks[0][1]          # STREAMINFO incl. MD5
+    assert hashlib.sha256(gframes).hexdigest() == hashlib.sha256(frames).hexdigest()
+
+
+def test_many_tracks_one_batch(gpu_engine):
+    opts = dict(oracle_port.PRESETS["8"])
+    pcms = [signals.make("tone", 4096 * 3 + k * 131, 2, 16, seed=k) for k in range(40)]
+    check_batch(gpu_engine, pcms, 2, 16, opts)
+
+
+def test_explicit_frame_sizes(gpu_engine):
+    """frames cut exactly where pcmreader.read() returned (flac.c:244-274)"""
+    opts = dict(oracle_port.PRESETS["8"])
+    pcm = signals.make("tone", 10000, 2, 16, seed=3)
+    sizes = [4096, 1000, 4096, 808]
+    got = gpu_encode_tracks(gpu_engine, [pcm], 2, 16, 44100, opts, frame_sizes=[sizes])
+    img, lst = got[0]
+    assert [n for _, n in lst] == sizes
+    dec, ch, b, r = oracle_port.decode(img)
+    assert np.array_equal(dec, pcm)
+
+
+def test_unsupported_options_raise(gpu_engine):
+    from audiotools import _atgpu
+    o = _atgpu.make_options(block_size=8192, max_lpc_order=8,
+                            min_residual_partition_order=0, max_residual_partition_order=6)
+    pcm = np.zeros(20000, np.int16)
+    with pytest.raises(_atgpu.ATGError) as e:
+        gpu_engine.encode(o, pcm, [(0, 10000)], 2, 16, 44100)
+    assert e.value.status == _atgpu.ATG_ERR_UNSUPPORTED
+
+
+def test_encode_flac_api(tmp_path):
+    """audiotools.encoders.encode_flac: reference signature and return value"""
+    import audiotools
+    from audiotools.encoders import encode_flac
+    pcm = signals.make("tone", 30000, 2, 16, seed=9)
+    reader = audiotools.BufferedPCMReader(audiotools.FrameListReader(pcm, 44100, 2, 16))
+    fn = str(tmp_path / "a.flac")
+    offsets = encode_flac(fn, reader, **oracle_port.PRESETS["8"])
+    want, wlst = oracle_port.encode(pcm, 2, 16, 44100, **oracle_port.PRESETS["8"])
+    assert open(fn, "rb").read() == want
+    assert offsets == wlst
