@@ -1,0 +1,264 @@
+#!/usr/bin/env python3
+"""bench.py — FLAC-8 batch encode throughput on MI355X (BASELINE.json config 2).
+
+One step = one pass of the hot path over one batch: FLAC-8 encode of
+`--tracks` synthetic 44.1 kHz / 16-bit stereo tracks x `--frames` FLAC
+frames of 4096 PCM frames, PCM resident in HBM, complete .flac images
+(STREAMINFO with MD5, VORBIS_COMMENT, PADDING, frames) left in HBM.
+
+Multi-GPU: one process per GPU (torchrun); each rank encodes its own batch
+of `--tracks` tracks (tracks are independent, no collective on the data
+path) -> "scaling": "weak"; value = frames of all ranks / max-over-ranks time.
+
+Prints ONE JSON line on rank 0.  The roofline block is for the dominant
+kernel (timed with HIP events on the stream it runs on, inside libatgpu);
+cpu_baseline times the CPU oracle (oracle/flac_port.c) on a bounded sample
+of the same batch on this host's cores.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import threading
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "python-audio-tools_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+METRIC = "FLAC-8 encode frames/s (4096-sample 44.1k stereo) at 1/2/4/8 GPUs; bit-exact"
+BLOCK = 4096
+PCM_BYTES_PER_FRAME = BLOCK * 2 * 2
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+FLAC8 = dict(block_size=4096, max_lpc_order=12, min_residual_partition_order=0,
+             max_residual_partition_order=6, mid_side=True,
+             exhaustive_model_search=True)
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--tracks", type=int, default=1024)
+    ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
+    ap.add_argument("--cpu-sample-tracks", type=int, default=64)
+    ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    return ap.parse_args(argv)
+
+
+def shard(n_total_ranks, rank, tracks_per_rank):
+    """global track ids owned by `rank` (weak scaling: a full batch per rank)"""
+    return list(range(rank * tracks_per_rank, (rank + 1) * tracks_per_rank))
+
+
+def synth_batch(torch, track_ids, n_samples, device):
+    """seeded synthetic PCM, int16 interleaved stereo, generated on device.
+
+    SURVEY §8(d): per track two sines (f1 in [100,2000] Hz, f2 in [2k,12k] Hz,
+    a1 + a2 <= 0.9) + gaussian noise sigma 64 LSB, right channel with
+    frequencies x1.3; 5% white-noise tracks, 2% silent tracks."""
+    T = len(track_ids)
+    rs = [np.random.RandomState(0x5EED0000 + t) for t in track_ids]
+    f1 = torch.tensor([r.uniform(100, 2000) for r in rs], dtype=torch.float64, device=device)
+    f2 = torch.tensor([r.uniform(2000, 12000) for r in rs], dtype=torch.float64, device=device)
+    a1 = torch.tensor([r.uniform(0.05, 0.6) for r in rs], dtype=torch.float64, device=device)
+    a2 = torch.tensor([r.uniform(0.0, 0.3) for r in rs], dtype=torch.float64, device=device)
+    kind = torch.tensor([(t * 2654435761) % 100 for t in track_ids], device=device)
+    gen = torch.Generator(device=device)
+    gen.manual_seed(0x5EED + track_ids[0])
+    out = torch.empty((T, n_samples, 2), dtype=torch.int16, device=device)
+    chunk = 64
+    n = torch.arange(n_samples, dtype=torch.float64, device=device)
+    for c0 in range(0, T, chunk):
+        sl = slice(c0, min(T, c0 + chunk))
+        ph = 2 * np.pi * n[None, :] / 44100.0
+        for ch, fm in ((0, 1.0), (1, 1.3)):
+            x = (a1[sl, None] * torch.sin(ph * f1[sl, None] * fm) +
+                 a2[sl, None] * torch.sin(ph * f2[sl, None] * fm)) * 32767.0
+            x = x + torch.randn(x.shape, generator=gen, device=device,
+                                dtype=torch.float64) * 64.0
+            x = torch.round(x).clamp_(-32768, 32767)
+            wn = kind[sl] < 5
+            if bool(wn.any()):
+                u = torch.randint(-32768, 32768, x.shape, generator=gen, device=device)
+                x = torch.where(wn[:, None], u.to(x.dtype), x)
+            sil = (kind[sl] >= 5) & (kind[sl] < 7)
+            x = torch.where(sil[:, None], torch.zeros_like(x), x)
+            out[sl, :, ch] = x.to(torch.int16)
+    return out.reshape(-1)
+
+
+def cpu_baseline(pcm_host, n_tracks, samples_per_track, threads):
+    """oracle FLAC-8 encode of `n_tracks` tracks on `threads` host threads
+    (one track per thread at a time, like track2track -j N)"""
+    import oracle_port
+    oracle_port.load()
+    work = list(range(n_tracks))
+    lock = threading.Lock()
+
+    def run():
+        while True:
+            with lock:
+                if not work:
+                    return
+                t = work.pop()
+            p = pcm_host[t * samples_per_track * 2:(t + 1) * samples_per_track * 2]
+            oracle_port.encode(p.astype(np.int32), 2, 16, 44100, **FLAC8)
+
+    th = [threading.Thread(target=run) for _ in range(threads)]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    dt = time.perf_counter() - t0
+    frames = n_tracks * (samples_per_track // BLOCK)
+    return frames / dt, dt
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    device = torch.device("cuda", local)
+    os.environ["ATG_DEVICE"] = str(local)
+
+    from audiotools import _atgpu
+    eng = _atgpu.Engine(local)
+    opts = _atgpu.make_options(**FLAC8)
+
+    n_samples = args.frames * BLOCK
+    ids = shard(world, rank, args.tracks)
+    pcm = synth_batch(torch, ids, n_samples, device)
+    tracks = [(i * n_samples, n_samples) for i in range(args.tracks)]
+    n_frames, out_cap = eng.bounds(opts, tracks, 2, 16)
+    out = torch.empty(out_cap, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+
+    def step():
+        return eng.encode_device(opts, pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16,
+                                 44100, out.data_ptr(), out_cap)
+
+    for _ in range(args.warmup):
+        res = step()
+
+    def barrier():
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+
+    kt_sum = {}
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res = step()
+        for k, v in eng.kernel_times().items():
+            kt_sum[k] = kt_sum.get(k, 0.0) + v
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    kt = {k: v / args.steps for k, v in kt_sum.items()}
+    out_bytes = sum(int(r.bytes) for r in res)
+    header = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + 4096
+    frame_bytes = out_bytes - header * len(res)
+
+    verified = None
+    if not args.no_verify:
+        # parity spot check outside the timed region: a few tracks vs oracle
+        import oracle_port
+        host_out = out.cpu().numpy()
+        host_pcm = pcm[:4 * n_samples * 2].cpu().numpy()
+        verified = True
+        for t in range(min(4, args.tracks)):
+            r = res[t]
+            img = host_out[r.out_offset:r.out_offset + r.bytes].tobytes()
+            want, _ = oracle_port.encode(
+                host_pcm[t * n_samples * 2:(t + 1) * n_samples * 2].astype(np.int32),
+                2, 16, 44100, **FLAC8)
+            verified = verified and (img == want)
+
+    if rank != 0:
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
+    total_frames = n_frames * world * args.steps
+    value = total_frames / elapsed
+    # dominant kernel and its roofline (algorithmic bytes: PCM in + FLAC out)
+    kernels = {k: v for k, v in kt.items() if k != "total"}
+    dom = max(kernels, key=kernels.get)
+    dom_ms = kernels[dom]
+    alg_bytes = n_frames * PCM_BYTES_PER_FRAME + frame_bytes
+    achieved = alg_bytes / (dom_ms / 1e3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom)
+        except Exception:
+            traffic = None
+
+    cpu = None
+    if not args.no_cpu_baseline:
+        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+        nt = min(args.cpu_sample_tracks, args.tracks)
+        sample_frames = args.frames
+        sps = sample_frames * BLOCK
+        host = pcm.reshape(args.tracks, n_samples * 2)[:nt, :sps * 2].cpu().numpy().reshape(-1)
+        fps, dt = cpu_baseline(host, nt, sps, threads)
+        cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
+               "sample": "%d tracks x %d FLAC-8 frames of the same synthetic batch, "
+                         "%d threads (one track per thread), %.1f s" % (nt, sample_frames,
+                                                                        threads, dt)}
+
+    line = {
+        "metric": METRIC,
+        "value": round(value, 1),
+        "unit": "frames/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "int32 residuals / f64 LPC analysis (s16 PCM in)",
+        "data": "synthetic (seeded sine+noise, 5% white noise, 2% silent tracks)",
+        "config": {"workload": "FLAC-8 batch encode, %d tracks x %d frames x 4096 samples "
+                               "per GPU, 44.1 kHz 16-bit stereo, PCM and .flac images in HBM"
+                               % (args.tracks, args.frames),
+                   "tracks_per_gpu": args.tracks, "frames_per_track": args.frames,
+                   "block_size": 4096, "preset": "FLAC-8 (-l 12 -m -e -R 6)",
+                   "parallelism": "dp%d (tracks sharded per GPU)" % world},
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                     "alg_bytes_per_launch": alg_bytes, "launch_ms": round(dom_ms, 4)},
+        "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+        "compressed_bytes_per_frame": round(frame_bytes / n_frames, 1),
+        "verified_vs_oracle": verified,
+        "cpu_baseline": cpu,
+    }
+    print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()
