@@ -67,8 +67,9 @@ const char *kTimedNames[kNumTimed] = {"lpc_analyze", "subframe_search", "frame_d
                                       "track_scan",  "frame_pack",      "track_md5",
                                       "stream_header", "total"};
 
-// CRC-16 (0x8005) byte table and "advance by 2^m zero bytes" matrices
-void build_crc_tables(uint32_t *t16, uint32_t *t8, uint16_t adv[24][16])
+// CRC-16 (0x8005) slicing tables t16[k][b] = CRC of byte b followed by k
+// zero bytes, the CRC-8 table, and "advance by 2^m zero bytes" matrices
+void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16])
 {
     for (uint32_t b = 0; b < 256; ++b) {
         uint32_t c = b << 8, c8 = b;
@@ -76,13 +77,18 @@ void build_crc_tables(uint32_t *t16, uint32_t *t8, uint16_t adv[24][16])
             c = (c & 0x8000u) ? ((c << 1) ^ 0x8005u) : (c << 1);
             c8 = (c8 & 0x80u) ? ((c8 << 1) ^ 0x07u) : (c8 << 1);
         }
-        t16[b] = c & 0xFFFFu;
+        t16[0][b] = c & 0xFFFFu;
         t8[b] = c8 & 0xFFu;
     }
+    for (int k = 1; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) {
+            const uint32_t c = t16[k - 1][b];
+            t16[k][b] = ((c << 8) ^ t16[0][(c >> 8) & 0xFFu]) & 0xFFFFu;
+        }
     // m = 0: one zero byte
     for (int i = 0; i < 16; ++i) {
         uint32_t s = 1u << i;
-        s = ((s << 8) ^ t16[(s >> 8) & 0xFFu]) & 0xFFFFu;
+        s = ((s << 8) ^ t16[0][(s >> 8) & 0xFFu]) & 0xFFFFu;
         adv[0][i] = (uint16_t)s;
     }
     for (int m = 1; m < 24; ++m) {
@@ -474,10 +480,10 @@ atg_status atg_engine_create(int device, atg_engine **out)
         HIP_TRY(hipEventCreate(&ev));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_tables, hipEventDisableTiming));
     HIP_TRY(hipEventCreateWithFlags(&e->ev_md5, hipEventDisableTiming));
-    static uint32_t t16[256], t8[256];
+    static uint32_t t16[4][256], t8[256];
     static uint16_t adv[24][16];
     build_crc_tables(t16, t8, adv);
-    HIP_TRY(upload_crc_tables(&adv[0][0], t16, t8));
+    HIP_TRY(upload_crc_tables(&adv[0][0], &t16[0][0], t8));
     *out = e;
     return ATG_OK;
 }

@@ -17,10 +17,11 @@
 #include "flac_dev.h"
 #include "launch.h"
 #include "pcm_read.h"
+#include "residual.h"
 #include "wave.h"
 
 __constant__ uint16_t c_crc_adv[24][16]; // advance CRC-16 state by 2^m zero bytes
-__constant__ uint32_t c_crc16[256];
+__constant__ uint32_t c_crc16[4][256]; // slicing tables: byte + k zero bytes
 __constant__ uint32_t c_crc8[256];
 
 #define VENDOR "Python Audio Tools 2.22alpha1"
@@ -32,7 +33,7 @@ hipError_t upload_crc_tables(const uint16_t *adv, const uint32_t *crc16_tab,
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_adv), adv, sizeof(uint16_t) * 24 * 16);
     if (e != hipSuccess)
         return e;
-    e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), crc16_tab, sizeof(uint32_t) * 256);
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), crc16_tab, sizeof(uint32_t) * 1024);
     if (e != hipSuccess)
         return e;
     return hipMemcpyToSymbol(HIP_SYMBOL(c_crc8), crc8_tab, sizeof(uint32_t) * 256);
@@ -223,9 +224,12 @@ __global__ void k_track_scan(FlacParams p, const TrackInfo *__restrict__ tracks,
 }
 
 // ---------------------------------------------------------------- K5
-#define PK_PRE 48
-#define PK_WORDS (PK_PRE + ATG_MAX_BLOCK + ATG_MAX_BLOCK / 64 + 16)
-__device__ __forceinline__ int paddr(int i) { return PK_PRE + i + (i >> 6); }
+// One wave per frame.  The frame image is built MSB-first in a zeroed LDS
+// buffer of big-endian words: lane l streams its own run of residual codes
+// through a 64-bit register window and stores whole words (ds_write), only
+// the first and last word of each run (shared with a neighbour) use ds_or.
+// Residuals are recomputed with the search kernel's arithmetic
+// (residual.h), so they are the same integers the bit counts came from.
 
 // OR `n` (1..32) bits of v into the big-endian bit image at bit position pos
 __device__ __forceinline__ void put_bits(uint32_t *fb, uint32_t pos, uint32_t n, uint32_t v)
@@ -242,9 +246,70 @@ __device__ __forceinline__ void put_bits(uint32_t *fb, uint32_t pos, uint32_t n,
         atomicOr(&fb[w + 1], lo);
 }
 
+// per-lane MSB-first bit stream into the zeroed LDS image
+struct LaneWriter {
+    uint32_t *fb;
+    uint64_t acc; // bits of words cw (high half) and cw + 1 (low half)
+    uint32_t cw, w0, bp;
+
+    __device__ __forceinline__ void begin(uint32_t *f, uint32_t pos)
+    {
+        fb = f;
+        acc = 0;
+        cw = pos >> 5;
+        w0 = cw;
+        bp = pos;
+    }
+    __device__ __forceinline__ void emit(uint32_t w, uint32_t v)
+    {
+        if (v) {
+            if (w == w0)
+                atomicOr(&fb[w], v); // may be shared with the previous run
+            else
+                fb[w] = v;           // wholly this lane's
+        }
+    }
+    // `zeros` 0-bits, then the low n (1..32) bits of v (v < 2^n)
+    __device__ __forceinline__ void put(uint32_t zeros, uint32_t n, uint32_t v)
+    {
+        bp += zeros;
+        const uint32_t nw = bp >> 5;
+        if (nw != cw) {
+            emit(cw, (uint32_t)(acc >> 32));
+            if (nw == cw + 1u) {
+                acc <<= 32;
+            } else {
+                emit(cw + 1u, (uint32_t)acc);
+                acc = 0;
+            }
+            cw = nw;
+        }
+        acc |= (uint64_t)v << (64u - (bp & 31u) - n);
+        bp += n;
+    }
+    __device__ __forceinline__ void end()
+    {
+        const uint32_t hi = (uint32_t)(acc >> 32), lo = (uint32_t)acc;
+        if (hi)
+            atomicOr(&fb[cw], hi);
+        if (lo)
+            atomicOr(&fb[cw + 1u], lo);
+    }
+};
+
 __device__ __forceinline__ uint32_t fb_byte(const uint32_t *fb, uint32_t b)
 {
     return (fb[b >> 2] >> (24u - 8u * (b & 3u))) & 0xFFu;
+}
+
+// big-endian 32 bits starting at image byte q (q >= 0) = alignbyte of two words
+__device__ __forceinline__ uint32_t fb_be32(const uint32_t *fb, uint32_t q)
+{
+    const uint32_t hi = fb[q >> 2];
+    const uint32_t r = q & 3u;
+    if (r == 0u)
+        return hi;
+    return __builtin_amdgcn_alignbyte(hi, fb[(q >> 2) + 1u], 4u - r);
 }
 
 __device__ __forceinline__ uint32_t crc_adv(uint32_t c, int m)
@@ -256,6 +321,17 @@ __device__ __forceinline__ uint32_t crc_adv(uint32_t c, int m)
     return r;
 }
 
+// rice-coded residual section of one lane from its kept zig-zag codes
+__device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[ATG_RUN], int lo,
+                                           int hi, uint32_t k)
+{
+    const uint32_t kmask = (1u << k) - 1u;
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; ++t)
+        if (t >= lo && t < hi)
+            w.put(u[t] >> k, k + 1u, (1u << k) | (u[t] & kmask));
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void k_frame_pack(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
@@ -263,23 +339,23 @@ __global__ __launch_bounds__(64) void k_frame_pack(
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t fb[];
-    __shared__ int32_t sl[PK_WORDS];
+    __shared__ __attribute__((aligned(16))) int32_t sl[SL_WORDS];
     __shared__ int32_t cfs[ATG_MAX_LPC];
-    __shared__ uint32_t crc_tab[256];
+    __shared__ uint32_t crc_tab[4][256];
 
     const uint32_t f = blockIdx.x;
     const int lane = threadIdx.x;
     const FrameInfo fi = frames[f];
-    const FrameDesc fd = fdesc[f];
+    const FrameDesc &fd = fdesc[f]; // by reference: hdr[]/sub[] indexed per lane
     const uint32_t N = fi.n;
     const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
     const uint32_t words = (fd.bytes + 3u) / 4u + 1u;
 
     for (uint32_t i = lane; i < words; i += 64)
         fb[i] = 0;
-    for (uint32_t i = lane; i < 256; i += 64)
-        crc_tab[i] = c_crc16[i];
-    for (int i = lane; i < PK_PRE; i += 64)
+    for (uint32_t i = lane; i < 1024u; i += 64)
+        (&crc_tab[0][0])[i] = (&c_crc16[0][0])[i];
+    for (int i = lane; i < SL_PRE; i += 64)
         sl[i] = 0;
     __syncthreads();
     if (lane < fd.hdr_len)
@@ -295,50 +371,61 @@ __global__ __launch_bounds__(64) void k_frame_pack(
     uint32_t ra = jf * S + qf * R, re = ra + R;
     re = re < (jf + 1u) * S ? re : (jf + 1u) * S;
     ra = ra < re ? ra : re;
+    const int len = (int)(re - ra);
 
     for (uint32_t si = 0; si < fd.nsub; ++si) {
         const uint32_t cand = fd.sub[si];
-        const SubDesc d = sub[(size_t)f * p.n_cand + cand];
+        const SubDesc &d = sub[(size_t)f * p.n_cand + cand];
+        const uint32_t type = d.type, order = d.order, w = d.wasted, sbps = d.sbps;
         const uint32_t start = pos;
-        const uint32_t w = d.wasted;
-        for (uint32_t i = lane; i < N; i += 64)
-            sl[paddr((int)i)] = cand_sample(pcm, fi.pcm_start + i, p.channels, cand, ms) >> w;
-        if (lane < (int)d.order && d.type == SF_LPC)
-            cfs[lane] = d.coef[lane];
-        if (d.type == SF_FIXED && lane < 4) {
-            const int o = d.order;
-            cfs[lane] = o == 1 ? (lane == 0 ? 1 : 0)
-                      : o == 2 ? (lane == 0 ? 2 : lane == 1 ? -1 : 0)
-                      : o == 3 ? (lane == 0 ? 3 : lane == 1 ? -3 : lane == 2 ? 1 : 0)
-                      : (lane == 0 ? 4 : lane == 1 ? -6 : lane == 2 ? 4 : lane == 3 ? -1 : 0);
+        uint32_t maxabs = 0;
+        for (uint32_t i = lane; i < N; i += 64) {
+            const int32_t s = cand_sample(pcm, fi.pcm_start + i, p.channels, cand, ms) >> w;
+            sl[saddr((int)i)] = s;
+            maxabs = max(maxabs, iabs_u(s));
+        }
+        maxabs = wave_max_u32(maxabs);
+        if (lane < (int)order) {
+            int c;
+            if (type == SF_LPC)
+                c = d.coef[lane];
+            else // FIXED predictors as coefficient sets (flac.c:918-1016)
+                c = order == 1 ? 1
+                  : order == 2 ? (lane == 0 ? 2 : -1)
+                  : order == 3 ? (lane == 0 ? 3 : lane == 1 ? -3 : 1)
+                  : (lane == 0 ? 4 : lane == 1 ? -6 : lane == 2 ? 4 : -1);
+            cfs[lane] = c;
         }
         __syncthreads();
-        const uint32_t rb = d.sbps - w;
-        if (d.type == SF_CONSTANT) {
+        const uint32_t rb = sbps - w;
+        if (type == SF_CONSTANT) {
             // 8 zero header bits, then the raw first sample (flac.c:813-830)
             if (lane == 0)
-                put_bits(fb, pos + 8u, d.sbps, (uint32_t)sl[paddr(0)]);
-            pos += 8u + d.sbps;
+                put_bits(fb, pos + 8u, sbps, (uint32_t)sl[saddr(0)]);
+            pos += 8u + sbps;
         } else {
-            const uint32_t code = d.type == SF_VERBATIM ? 1u
-                                : d.type == SF_FIXED ? 8u + d.order : 32u + d.order - 1u;
+            const uint32_t code = type == SF_VERBATIM ? 1u
+                                : type == SF_FIXED ? 8u + order : 32u + order - 1u;
             if (lane == 0) {
                 put_bits(fb, pos, 7, code);
                 if (w)
                     put_bits(fb, pos + 7u, w + 1u, (1u << w) | 1u);
             }
             const uint32_t hb = 7u + (w ? w + 1u : 1u);
-            if (d.type == SF_VERBATIM) {
-                for (uint32_t i = lane; i < N; i += 64)
-                    put_bits(fb, pos + hb + i * rb, rb, (uint32_t)sl[paddr((int)i)]);
+            const uint32_t rmask = rb >= 32u ? 0xFFFFFFFFu : (1u << rb) - 1u;
+            if (type == SF_VERBATIM) {
+                LaneWriter wr;
+                wr.begin(fb, pos + hb + ra * rb);
+                for (int t = 0; t < len; ++t)
+                    wr.put(0, rb, (uint32_t)sl[saddr((int)ra + t)] & rmask);
+                wr.end();
                 pos += hb + N * rb;
             } else {
-                const uint32_t order = d.order;
                 if ((uint32_t)lane < order)
-                    put_bits(fb, pos + hb + lane * rb, rb, (uint32_t)sl[paddr(lane)]);
+                    put_bits(fb, pos + hb + lane * rb, rb, (uint32_t)sl[saddr(lane)]);
                 uint32_t q = pos + hb + order * rb;
                 int shift = 0;
-                if (d.type == SF_LPC) {
+                if (type == SF_LPC) {
                     shift = d.shift;
                     if (lane == 0) {
                         put_bits(fb, q, 4, d.precision - 1u);
@@ -359,40 +446,76 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                 const bool degen = (N >> po) < order;
                 const uint32_t jp = (uint32_t)lane >> (6u - po);
                 const uint32_t k = degen ? d.rice[0] : d.rice[jp];
-                // pass 1: code bits of this lane's residuals
-                const int i0 = max((int)ra, (int)order);
-                uint32_t cb = 0;
-                for (int i = i0; i < (int)re; ++i) {
-                    int64_t acc = 0;
-                    for (uint32_t j = 0; j < order; ++j)
-                        acc += (int64_t)cfs[j] * (int64_t)sl[paddr(i - 1 - (int)j)];
-                    const int r = (int)((uint32_t)sl[paddr(i)] - (uint32_t)(int32_t)(acc >> shift));
-                    const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
-                    cb += (u >> k) + 1u + k;
-                }
-                const uint32_t excl = wave_excl_scan_u32(cb, lane);
-                const uint32_t total = wave_sum_u32(cb);
-                uint32_t pp;
-                if (!degen) {
-                    pp = rs + pbits * (jp + 1u) + excl;
-                    if (((uint32_t)lane & ((64u >> po) - 1u)) == 0u)
-                        put_bits(fb, rs + pbits * jp + excl, pbits, k);
+                const bool part_head = !degen && ((uint32_t)lane & ((64u >> po) - 1u)) == 0u;
+
+                uint64_t csum = 0;
+                for (uint32_t j = 0; j < order; ++j)
+                    csum += (uint64_t)(cfs[j] < 0 ? -(int64_t)cfs[j] : cfs[j]);
+                const int kind = residual_kernel(csum, maxabs, (int)order);
+                uint32_t total, excl;
+                LaneWriter wr;
+                if (kind != RES_GENERIC) {
+                    int cf[ATG_FAST_ORDER];
+#pragma unroll
+                    for (int j = 0; j < ATG_FAST_ORDER; ++j)
+                        cf[j] = uniform_i32(j < (int)order ? cfs[j] : 0);
+                    uint32_t u[ATG_RUN];
+                    uint64_t asum;
+                    const bool full = N == ATG_MAX_BLOCK;
+                    if (kind == RES_DOT2)
+                        asum = full ? lane_residuals<true, true>(sl, (int)ra, len, cf, shift, u)
+                                    : lane_residuals<true, false>(sl, (int)ra, len, cf, shift, u);
+                    else
+                        asum = full ? lane_residuals<false, true>(sl, (int)ra, len, cf, shift, u)
+                                    : lane_residuals<false, false>(sl, (int)ra, len, cf, shift, u);
+                    const int warm = drop_warmup((int)ra, len, (int)order, u, asum);
+                    uint32_t cb = (uint32_t)(len - warm) * (1u + k);
+#pragma unroll
+                    for (int t = 0; t < ATG_RUN; ++t)
+                        cb += u[t] >> k;
+                    excl = wave_excl_scan_u32(cb, lane);
+                    total = wave_sum_u32(cb);
+                    wr.begin(fb, degen ? rs + pbits + excl
+                                       : rs + pbits * (jp + (part_head ? 0u : 1u)) + excl);
+                    if (part_head)
+                        wr.put(0, pbits, k);
+                    emit_codes(wr, u, warm, len, k);
                 } else {
-                    pp = rs + pbits + excl;
+                    // any order <= 32 / wide samples: 64-bit accumulator
+                    const int i0 = max((int)ra, (int)order);
+                    uint32_t cb = 0;
+                    for (int i = i0; i < (int)re; ++i) {
+                        int64_t acc = 0;
+                        for (uint32_t j = 0; j < order; ++j)
+                            acc += (int64_t)cfs[j] * (int64_t)sl[saddr(i - 1 - (int)j)];
+                        const int r = (int)((uint32_t)sl[saddr(i)] -
+                                            (uint32_t)(int32_t)(acc >> shift));
+                        cb += (zigzag(r) >> k) + 1u + k;
+                    }
+                    excl = wave_excl_scan_u32(cb, lane);
+                    total = wave_sum_u32(cb);
+                    wr.begin(fb, degen ? rs + pbits + excl
+                                       : rs + pbits * (jp + (part_head ? 0u : 1u)) + excl);
+                    if (part_head)
+                        wr.put(0, pbits, k);
+                    const uint32_t kmask = (1u << k) - 1u;
+                    for (int i = i0; i < (int)re; ++i) {
+                        int64_t acc = 0;
+                        for (uint32_t j = 0; j < order; ++j)
+                            acc += (int64_t)cfs[j] * (int64_t)sl[saddr(i - 1 - (int)j)];
+                        const int r = (int)((uint32_t)sl[saddr(i)] -
+                                            (uint32_t)(int32_t)(acc >> shift));
+                        const uint32_t uu = zigzag(r);
+                        wr.put(uu >> k, k + 1u, (1u << k) | (uu & kmask));
+                    }
+                }
+                wr.end();
+                if (degen) {
+                    // partition 0 holds every residual; the others are empty
                     const uint32_t np = 1u << po;
                     for (uint32_t j = lane; j < np; j += 64)
                         put_bits(fb, j == 0 ? rs : rs + pbits + total + (j - 1u) * pbits,
                                  pbits, d.rice[j]);
-                }
-                for (int i = i0; i < (int)re; ++i) {
-                    int64_t acc = 0;
-                    for (uint32_t j = 0; j < order; ++j)
-                        acc += (int64_t)cfs[j] * (int64_t)sl[paddr(i - 1 - (int)j)];
-                    const int r = (int)((uint32_t)sl[paddr(i)] - (uint32_t)(int32_t)(acc >> shift));
-                    const uint32_t u = ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
-                    const uint32_t msb = u >> k;
-                    put_bits(fb, pp + msb, k + 1u, (1u << k) | (k ? (u & ((1u << k) - 1u)) : 0u));
-                    pp += msb + 1u + k;
                 }
                 pos = rs + (1u << po) * pbits + total;
             }
@@ -402,21 +525,37 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         __syncthreads();
     }
     __syncthreads();
-    // CRC-16 of bytes [0, L): 64 chunks of Lc bytes (virtual leading zeros,
-    // which leave a zero-init CRC unchanged), tree-combined with the
-    // "advance by 2^m zero bytes" matrices.
+
+    // CRC-16 of bytes [0, L): 64 chunks of Lc = 2^m >= 4 bytes over a
+    // virtually zero-prefixed image (leading zeros leave a zero-init CRC
+    // unchanged), 4 bytes per step with slicing tables, tree-combined with
+    // the "advance by 2^m zero bytes" matrices.
     const uint32_t L = fd.bytes - 2u;
     uint32_t lc_log = 2;
     while ((64u << lc_log) < L)
         lc_log++;
     const uint32_t Lc = 1u << lc_log;
-    const int64_t z = (int64_t)(64u << lc_log) - (int64_t)L;
-    int64_t b0 = (int64_t)lane * Lc - z;
-    const int64_t b1 = b0 + Lc;
-    b0 = b0 < 0 ? 0 : b0;
+    const int z = (int)(64u << lc_log) - (int)L;
     uint32_t crc = 0;
-    for (int64_t b = b0; b < b1; ++b)
-        crc = ((crc << 8) ^ crc_tab[((crc >> 8) ^ fb_byte(fb, (uint32_t)b)) & 0xFFu]) & 0xFFFFu;
+    {
+        int q = lane * (int)Lc - z; // image byte of this lane's first group
+        const int qe = q + (int)Lc;
+        if (q < 0) {
+            // groups wholly in the zero prefix leave crc = 0: skip them
+            q += ((-q) >> 2) << 2; // now -4 < q <= 0
+            if (q < 0 && q < qe) {
+                const uint32_t t = fb[0] >> (8u * (uint32_t)(-q));
+                crc = crc_tab[3][t >> 24] ^ crc_tab[2][(t >> 16) & 0xFFu] ^
+                      crc_tab[1][(t >> 8) & 0xFFu] ^ crc_tab[0][t & 0xFFu];
+                q += 4;
+            }
+        }
+        for (; q < qe; q += 4) {
+            const uint32_t t = fb_be32(fb, (uint32_t)q) ^ (crc << 16);
+            crc = crc_tab[3][t >> 24] ^ crc_tab[2][(t >> 16) & 0xFFu] ^
+                  crc_tab[1][(t >> 8) & 0xFFu] ^ crc_tab[0][t & 0xFFu];
+        }
+    }
 #pragma unroll
     for (int s = 0; s < 6; ++s) {
         const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << s, 64);
@@ -438,11 +577,8 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         dst[lane] = (uint8_t)fb_byte(fb, lane);
     const uint32_t body = (nb - h) / 4u;
     uint32_t *dw = (uint32_t *)(dst + h);
-    for (uint32_t i = lane; i < body; i += 64) {
-        const uint32_t b = h + 4u * i;
-        dw[i] = fb_byte(fb, b) | (fb_byte(fb, b + 1u) << 8) | (fb_byte(fb, b + 2u) << 16) |
-                (fb_byte(fb, b + 3u) << 24);
-    }
+    for (uint32_t i = lane; i < body; i += 64)
+        dw[i] = __builtin_bswap32(fb_be32(fb, h + 4u * i));
     const uint32_t tail0 = h + 4u * body;
     if (tail0 + (uint32_t)lane < nb)
         dst[tail0 + lane] = (uint8_t)fb_byte(fb, tail0 + lane);

@@ -9,8 +9,8 @@
 // This file is compiled with -ffp-contract=off and `#pragma clang fp
 // contract(off)`, so every product is rounded before its add.
 //
-// Mapping: one lane = one subframe candidate of one frame (64 frames per
-// wave, a wave per candidate channel).  Each lane streams its samples once
+// Mapping: one lane = one subframe candidate of one frame; the candidates of
+// a frame sit in adjacent lanes (16 frames per wave for stereo mid/side).  Each lane streams its samples once
 // and keeps all LAGS+1 accumulators plus a circular history of the last
 // LAGS windowed samples in registers: 13 independent fp64 add chains per
 // lane, each bit-identical to the reference's sequential loop.  The
@@ -80,6 +80,50 @@ __device__ __forceinline__ void quantize_store(const double (&lp)[LAGS],
     *shift_out = (int8_t)(shift >= 0 ? shift : 0);
 }
 
+// Autocorrelation of one candidate, streamed K samples at a time: all loads
+// of a group are issued together (indices clamped, no branches), then the K
+// accumulator chains run.  Positions past this lane's N contribute x = 0, which adds +-0.0
+// to accumulators that are never -0.0 (exact no-op).
+template <int MODE, typename T, int K>
+__device__ __forceinline__ void autocorr(const T *__restrict__ src, const double *__restrict__ win,
+                                         uint32_t ch, uint32_t cand, uint32_t n_loop,
+                                         uint32_t nlast, uint32_t n_max, double (&acc)[K],
+                                         double (&hist)[K])
+{
+    // software pipeline: the loads of group g+1 are in flight while the
+    // chains of group g run
+    int32_t sv[K];
+    double wv[K];
+#pragma unroll
+    for (int u = 0; u < K; ++u) {
+        const uint32_t j = min((uint32_t)u, nlast);
+        sv[u] = cand_at<MODE>(src, j, ch, cand);
+        wv[u] = win[j];
+    }
+    for (uint32_t j0 = 0; j0 < n_max; j0 += K) {
+        double xv[K];
+#pragma unroll
+        for (int u = 0; u < K; ++u)
+            xv[u] = (j0 + (uint32_t)u < n_loop) ? (double)sv[u] * wv[u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t j = min(j0 + K + (uint32_t)u, nlast);
+            sv[u] = cand_at<MODE>(src, j, ch, cand);
+            wv[u] = win[j];
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const double x = xv[u];
+            hist[u] = x;
+#pragma unroll
+            for (int L = 0; L < K; ++L) {
+                const double prod = hist[(u - L + K) % K] * x;
+                acc[L] = acc[L] + prod;
+            }
+        }
+    }
+}
+
 template <typename T, int LAGS>
 __global__ __launch_bounds__(64) void k_lpc_analyze(
     FlacParams p, const T *__restrict__ pcm,
@@ -88,11 +132,14 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
     uint8_t *__restrict__ est_tab)
 {
     constexpr int K = LAGS + 1;
-    uint32_t group, cand;
-    xcd_unit_map(blockIdx.x, p.n_cand, &group, &cand);
-    const uint32_t f = group * 64u + threadIdx.x;
+    // lanes [c*k, c*k + c) = the c candidates of one frame: they read the
+    // same interleaved PCM, so a load touches 64 / c frames' lines
+    const uint32_t fpw = 64u / p.n_cand;
+    const uint32_t fl = threadIdx.x / p.n_cand;
+    const uint32_t cand = threadIdx.x - fl * p.n_cand;
+    const uint32_t f = blockIdx.x * fpw + fl;
     const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
-    const bool active = f < p.n_frames;
+    const bool active = fl < fpw && f < p.n_frames;
     const FrameInfo fi = frames[active ? f : 0u];
     const int M = (int)p.max_lpc_order;
     const uint32_t N = active ? fi.n : 0u;
@@ -110,26 +157,17 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
         hist[k] = 0.0;
     }
     const double *__restrict__ win = windows + fi.win_off;
-
-    // Stream samples; positions past this lane's N contribute x = 0, which
-    // adds +-0.0 to accumulators that are never -0.0 (exact no-op).
-    for (uint32_t j0 = 0; j0 < n_max; j0 += K) {
-#pragma unroll
-        for (int u = 0; u < K; ++u) {
-            const uint32_t j = j0 + (uint32_t)u;
-            double x = 0.0;
-            if (j < n_loop) {
-                const int32_t s = cand_sample(pcm, fi.pcm_start + j, p.channels,
-                                              cand, ms);
-                x = (double)s * win[j];
-            }
-            hist[u] = x;
-#pragma unroll
-            for (int L = 0; L < K; ++L) {
-                const double prod = hist[(u - L + K) % K] * x;
-                acc[L] = acc[L] + prod;
-            }
-        }
+    const T *__restrict__ src = pcm + fi.pcm_start * p.channels;
+    const uint32_t nlast = n_loop ? n_loop - 1u : 0u;
+    switch (pcm_mode(pcm, ms)) {
+    case PCM_MS16:
+        autocorr<PCM_MS16, T, K>(src, win, p.channels, cand, n_loop, nlast, n_max, acc, hist);
+        break;
+    case PCM_MS:
+        autocorr<PCM_MS, T, K>(src, win, p.channels, cand, n_loop, nlast, n_max, acc, hist);
+        break;
+    default:
+        autocorr<PCM_CH, T, K>(src, win, p.channels, cand, n_loop, nlast, n_max, acc, hist);
     }
     if (!do_lpc)
         return;
@@ -209,9 +247,8 @@ static hipError_t launch_t(const FlacParams &p, const T *pcm, const FrameInfo *f
                            const double *windows, int16_t *coef_tab,
                            int8_t *shift_tab, uint8_t *est_tab, hipStream_t s)
 {
-    const uint32_t groups = (p.n_frames + 63u) / 64u;
-    const uint32_t groups8 = (groups + 7u) / 8u * 8u;
-    dim3 grid(groups8 * p.n_cand);
+    const uint32_t fpw = 64u / p.n_cand;
+    dim3 grid((p.n_frames + fpw - 1u) / fpw);
     hipLaunchKernelGGL((k_lpc_analyze<T, LAGS>), grid, dim3(64), 0, s, p, pcm,
                        frames, windows, coef_tab, shift_tab, est_tab);
     return hipGetLastError();

@@ -28,26 +28,8 @@
 #include "flac_dev.h"
 #include "launch.h"
 #include "pcm_read.h"
+#include "residual.h"
 #include "wave.h"
-
-// LDS sample layout: 4 pad words after every 64 samples, so lane runs
-// (64 samples apart) start 68 words apart: 16-byte aligned for ds_read_b128
-// and bank-conflict-free across each 16-lane b128 group.  Indices -12..-1
-// (history before sample 0) read zeros.
-#define SL_PRE 48
-#define SL_WORDS (SL_PRE + ATG_MAX_BLOCK + 4 * (ATG_MAX_BLOCK / 64) + 64 + 8)
-
-__device__ __forceinline__ int saddr(int i) { return SL_PRE + i + 4 * (i >> 6); }
-
-__device__ __forceinline__ uint32_t zigzag(int32_t r)
-{
-    return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
-}
-
-__device__ __forceinline__ uint32_t iabs_u(int32_t r)
-{
-    return r < 0 ? 0u - (uint32_t)r : (uint32_t)r;
-}
 
 // Rice parameter of one partition: the reference's loop
 //   while ((uint64_t)(plength << Rice) < sum) if (Rice < max) Rice++; else break;
@@ -156,134 +138,21 @@ struct Eval {
     PartSel sel;
 };
 
-// Fast path: order <= 12 with exact 32-bit accumulation.  One code path for
-// every order: the predictor always has 12 taps, taps >= order carry 0
-// (adding 0 * s changes nothing).  Two kernels of arithmetic:
-//   DOT2  samples fit int16: v_dot2_i32_i16 takes two taps per instruction
-//         on packed pairs Q_m = (s_m, s_{m-1}); pred_t = sum_j C_j . Q_{t-1-2j}
-//         -> 1 v_perm + 6 v_dot2 per residual;
-//   MAD24 samples fit 24 bits: v_mad_i32_i24, 12 per residual.
-// Samples are read from LDS 16 at a time (ds_read_b128 for full aligned
-// runs); the 64 zig-zag codes of the lane's run stay in VGPRs for pass 2.
-typedef short short2_t __attribute__((ext_vector_type(2)));
-
+// Fast path: order <= 12 with exact 32-bit accumulation (residual.h); the 64
+// zig-zag codes of the lane's run stay in VGPRs for pass 2.
 template <bool DOT2, bool FULL>
 __device__ __forceinline__ Eval eval_fast(const int32_t *__restrict__ sl, const RunCtx &c,
                                           const int *__restrict__ cf_lds, int order,
                                           int shift)
 {
-    constexpr int W = ATG_FAST_ORDER;
-    int cf[W];
+    int cf[ATG_FAST_ORDER];
 #pragma unroll
-    for (int k = 0; k < W; ++k)
+    for (int k = 0; k < ATG_FAST_ORDER; ++k)
         cf[k] = uniform_i32(k < order ? cf_lds[k] : 0);
-    int cp[W / 2]; // packed coefficient pairs (c_2j, c_2j+1)
-#pragma unroll
-    for (int j = 0; j < W / 2; ++j)
-        cp[j] = uniform_i32((int)(((uint32_t)cf[2 * j] & 0xFFFFu) |
-                                  ((uint32_t)cf[2 * j + 1] << 16)));
     uint32_t u[ATG_RUN];
-    uint64_t sum = 0;
-    int base = c.a;
-    // history: win[k] = s[i-1-k] (MAD24), qw[k] = Q_{i-1-k} (DOT2)
-    int win[W];
-    int h[W + 1]; // s[a-13 .. a-1]
-    if (FULL) {
-        const int4 *hp = (const int4 *)&sl[saddr(base - W)];
-#pragma unroll
-        for (int q = 0; q < W / 4; ++q) {
-            const int4 v = hp[q];
-            h[1 + 4 * q] = v.x;
-            h[2 + 4 * q] = v.y;
-            h[3 + 4 * q] = v.z;
-            h[4 + 4 * q] = v.w;
-        }
-        h[0] = sl[saddr(base - W - 1)];
-    } else {
-#pragma unroll
-        for (int k = 0; k <= W; ++k)
-            h[k] = sl[saddr(base - W - 1 + k)];
-    }
-    int qw[W];
-#pragma unroll
-    for (int k = 0; k < W; ++k) {
-        win[k] = h[W - k];                                     // s[a-1-k]
-        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)h[W - 1 - k], (uint32_t)h[W - k],
-                                           0x05040100u);       // (s[a-1-k], s[a-2-k])
-    }
-#pragma unroll
-    for (int ch = 0; ch < ATG_RUN / 16; ++ch) {
-        // keep each chunk's loads inside the chunk (bounds live registers)
-        asm volatile("" : "+v"(base)::"memory");
-        int x[16];
-        if (FULL) {
-            const int4 *p4 = (const int4 *)&sl[saddr(base + 16 * ch)];
-#pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const int4 v = p4[q];
-                x[4 * q] = v.x;
-                x[4 * q + 1] = v.y;
-                x[4 * q + 2] = v.z;
-                x[4 * q + 3] = v.w;
-            }
-        } else {
-#pragma unroll
-            for (int t = 0; t < 16; ++t)
-                x[t] = sl[saddr(base + 16 * ch + t)];
-        }
-#pragma unroll
-        for (int tt = 0; tt < 16; ++tt) {
-            const int t = 16 * ch + tt;
-            const int s = x[tt];
-            int acc;
-            if (DOT2) {
-                acc = 0;
-#pragma unroll
-                for (int j = 0; j < W / 2; ++j) {
-                    short2_t a = __builtin_bit_cast(short2_t, qw[2 * j]);
-                    short2_t b = __builtin_bit_cast(short2_t, cp[j]);
-                    acc = __builtin_amdgcn_sdot2(a, b, acc, false);
-                }
-                const int prev = win[0];
-#pragma unroll
-                for (int k = W - 1; k > 0; --k)
-                    qw[k] = qw[k - 1];
-                qw[0] = (int)__builtin_amdgcn_perm((uint32_t)prev, (uint32_t)s, 0x05040100u);
-                win[0] = s;
-            } else {
-                acc = 0;
-#pragma unroll
-                for (int k = 0; k < W; ++k)
-                    acc = mad24(win[k], cf[k], acc);
-#pragma unroll
-                for (int k = W - 1; k > 0; --k)
-                    win[k] = win[k - 1];
-                win[0] = s;
-            }
-            const int r = (int)((uint32_t)s - (uint32_t)(acc >> shift));
-            uint32_t uu = zigzag(r);
-            uint32_t ar = iabs_u(r);
-            if (!FULL) {
-                const bool v = t < c.len;
-                uu = v ? uu : 0u;
-                ar = v ? ar : 0u;
-            }
-            u[t] = uu;
-            sum += ar;
-        }
-    }
-    // residuals exist only from sample `order` on (warm-up samples excluded)
-    const int warm = min(max(order - c.a, 0), c.len);
+    uint64_t sum = lane_residuals<DOT2, FULL>(sl, c.a, c.len, cf, shift, u);
+    const int warm = drop_warmup(c.a, c.len, order, u, sum);
     const int cnt = c.len - warm;
-    if (warm > 0) {
-#pragma unroll
-        for (int t = 0; t < W; ++t) {
-            if (t < warm) {
-                sum -= ((uint64_t)u[t] + 1u) >> 1;
-                u[t] = 0u;
-            }
-        }
-    }
     Eval ev;
     ev.sel = select_partitions(sum, (uint32_t)order, c);
     const uint32_t k = ev.sel.k_lane;
@@ -330,20 +199,17 @@ __device__ __forceinline__ Eval eval_any(const int32_t *sl, const RunCtx &c,
                                          const int *cf_lds, int order, int shift,
                                          uint32_t maxabs)
 {
-    // 32-bit accumulation is exact when every partial sum fits in int32.
     uint64_t csum = 0;
     for (int k = 0; k < order; ++k)
         csum += (uint64_t)(cf_lds[k] < 0 ? -(int64_t)cf_lds[k] : cf_lds[k]);
-    const bool narrow = csum * (uint64_t)maxabs < (1ull << 31);
-    if (narrow && order <= ATG_FAST_ORDER) {
-        const bool full = c.N == ATG_MAX_BLOCK;
-        if (maxabs <= 32767u && csum <= 32767u * 12u)
-            return full ? eval_fast<true, true>(sl, c, cf_lds, order, shift)
-                        : eval_fast<true, false>(sl, c, cf_lds, order, shift);
-        if (maxabs < (1u << 23))
-            return full ? eval_fast<false, true>(sl, c, cf_lds, order, shift)
-                        : eval_fast<false, false>(sl, c, cf_lds, order, shift);
-    }
+    const int kind = residual_kernel(csum, maxabs, order);
+    const bool full = c.N == ATG_MAX_BLOCK;
+    if (kind == RES_DOT2)
+        return full ? eval_fast<true, true>(sl, c, cf_lds, order, shift)
+                    : eval_fast<true, false>(sl, c, cf_lds, order, shift);
+    if (kind == RES_MAD24)
+        return full ? eval_fast<false, true>(sl, c, cf_lds, order, shift)
+                    : eval_fast<false, false>(sl, c, cf_lds, order, shift);
     return eval_generic(sl, c, cf_lds, order, shift);
 }
 

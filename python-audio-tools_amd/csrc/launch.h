@@ -31,7 +31,7 @@ hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
                                 const TrackOut *tout, uint8_t *out,
                                 hipStream_t s);
 hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
-                             const uint32_t *crc16_tab /*[256]*/,
+                             const uint32_t *crc16_tab /*[4][256] slicing tables*/,
                              const uint32_t *crc8_tab /*[256]*/);
 // md5.hip
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,

@@ -12,6 +12,8 @@
 #include "flac_dev.h"
 #include "launch.h"
 
+#define MD5_D 4
+
 __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_amdgcn_alignbit(x, x, 32 - s); }
 
 #define MD5_STEP(f, a, b, c, d, x, t, s) \
@@ -108,6 +110,9 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
                                                   const TrackInfo *__restrict__ tracks,
                                                   TrackOut *__restrict__ tout)
 {
+    // the hash chains are the longest serial path of a batch: let their
+    // waves issue ahead of the encoder kernels sharing the SIMD
+    __builtin_amdgcn_s_setprio(3);
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
     if (t >= p.n_tracks)
         return;
@@ -120,20 +125,50 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
     uint32_t X[16];
     const uint64_t full = nbytes / 64u;
-    if (raw) {
+    if (raw && full > 0) {
+        // MD5_D blocks in flight per lane: the loads of block b + MD5_D are
+        // issued before block b is hashed, so HBM latency hides behind
+        // ~MD5_D x 320 dependent VALU ops (one chain per lane, 4 cyc each)
         const uint4 *q = (const uint4 *)s;
-        for (uint64_t blk = 0; blk < full; ++blk) {
+        uint4 buf[MD5_D][4];
 #pragma unroll
-            for (int i = 0; i < 4; ++i) {
-                const uint4 v = q[blk * 4 + i];
-                X[4 * i] = v.x;
-                X[4 * i + 1] = v.y;
-                X[4 * i + 2] = v.z;
-                X[4 * i + 3] = v.w;
+        for (int j = 0; j < MD5_D; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                buf[j][i] = q[(uint64_t)min((uint64_t)j, full - 1u) * 4u + i];
+        uint64_t blk = 0;
+        for (; blk + MD5_D <= full; blk += MD5_D) {
+#pragma unroll
+            for (int j = 0; j < MD5_D; ++j) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    X[4 * i] = buf[j][i].x;
+                    X[4 * i + 1] = buf[j][i].y;
+                    X[4 * i + 2] = buf[j][i].z;
+                    X[4 * i + 3] = buf[j][i].w;
+                }
+                // refill (clamped: past the end it re-reads the last block)
+                const uint64_t nb = min(blk + (uint64_t)(j + MD5_D), full - 1u);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    buf[j][i] = q[nb * 4u + i];
+                md5_compress(h, X);
             }
-            md5_compress(h, X);
         }
-    } else {
+#pragma unroll
+        for (int j = 0; j < MD5_D; ++j) {
+            if (blk + (uint64_t)j < full) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    X[4 * i] = buf[j][i].x;
+                    X[4 * i + 1] = buf[j][i].y;
+                    X[4 * i + 2] = buf[j][i].z;
+                    X[4 * i + 3] = buf[j][i].w;
+                }
+                md5_compress(h, X);
+            }
+        }
+    } else if (!raw) {
         for (uint64_t blk = 0; blk < full; ++blk) {
             for (int i = 0; i < 16; ++i) {
                 const uint64_t j = blk * 64u + 4u * (uint32_t)i;

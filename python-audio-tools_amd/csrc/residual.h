@@ -1,0 +1,179 @@
+// residual.h — a lane's LPC/FIXED residuals over its run of samples held in
+// LDS; shared by the subframe search (K2) and the frame packer (K5) so both
+// see the very same integers (reference residual loop: src/encoders/flac.c
+// flacenc_encode_lpc_subframe 1060-1126, fixed 918-1016).
+//
+// LDS sample layout: 4 pad words after every 64 samples, so lane runs (64
+// samples apart) start 68 words apart: 16-byte aligned for ds_read_b128 and
+// bank-conflict-free across each 16-lane b128 group.  Indices -12..-1
+// (history before sample 0) read zeros.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+#include "wave.h"
+
+#define SL_PRE 48
+#define SL_WORDS (SL_PRE + ATG_MAX_BLOCK + 4 * (ATG_MAX_BLOCK / 64) + 64 + 8)
+
+__device__ __forceinline__ int saddr(int i) { return SL_PRE + i + 4 * (i >> 6); }
+
+__device__ __forceinline__ uint32_t zigzag(int32_t r)
+{
+    return ((uint32_t)r << 1) ^ (uint32_t)(r >> 31);
+}
+
+__device__ __forceinline__ uint32_t iabs_u(int32_t r)
+{
+    return r < 0 ? 0u - (uint32_t)r : (uint32_t)r;
+}
+
+typedef short short2_t __attribute__((ext_vector_type(2)));
+
+// Residuals of samples [a, a+len) (len <= 64) with a 12-tap predictor whose
+// taps >= order are 0, exact in 32 bits (caller checks sum|c| * max|s| <
+// 2^31).  cf[] must be wave-uniform.  Two kernels of arithmetic:
+//   DOT2  samples fit int16: v_dot2_i32_i16 takes two taps per instruction
+//         on packed pairs Q_m = (s_m, s_{m-1}); pred_t = sum_j C_j . Q_{t-1-2j}
+//         -> 1 v_perm + 6 v_dot2 per residual;
+//   MAD24 samples fit 24 bits: v_mad_i32_i24, 12 per residual.
+// FULL: len == 64 and a % 64 == 0 (N == 4096), samples read 16 at a time
+// with ds_read_b128.  Writes the zig-zag codes to u[] (0 past len) and
+// returns sum |r| over the run; warm-up positions (< order) are NOT yet
+// excluded.
+template <bool DOT2, bool FULL>
+__device__ __forceinline__ uint64_t lane_residuals(const int32_t *__restrict__ sl, int a, int len,
+                                                   const int (&cf)[ATG_FAST_ORDER], int shift,
+                                                   uint32_t (&u)[ATG_RUN])
+{
+    constexpr int W = ATG_FAST_ORDER;
+    int cp[W / 2]; // packed coefficient pairs (c_2j, c_2j+1)
+#pragma unroll
+    for (int j = 0; j < W / 2; ++j)
+        cp[j] = uniform_i32((int)(((uint32_t)cf[2 * j] & 0xFFFFu) |
+                                  ((uint32_t)cf[2 * j + 1] << 16)));
+    uint64_t sum = 0;
+    int base = a;
+    // history: win[k] = s[i-1-k] (MAD24), qw[k] = Q_{i-1-k} (DOT2)
+    int win[W];
+    int h[W + 1]; // s[a-13 .. a-1]
+    if (FULL) {
+        const int4 *hp = (const int4 *)&sl[saddr(base - W)];
+#pragma unroll
+        for (int q = 0; q < W / 4; ++q) {
+            const int4 v = hp[q];
+            h[1 + 4 * q] = v.x;
+            h[2 + 4 * q] = v.y;
+            h[3 + 4 * q] = v.z;
+            h[4 + 4 * q] = v.w;
+        }
+        h[0] = sl[saddr(base - W - 1)];
+    } else {
+#pragma unroll
+        for (int k = 0; k <= W; ++k)
+            h[k] = sl[saddr(base - W - 1 + k)];
+    }
+    int qw[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        win[k] = h[W - k];                                     // s[a-1-k]
+        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)h[W - 1 - k], (uint32_t)h[W - k],
+                                           0x05040100u);       // (s[a-1-k], s[a-2-k])
+    }
+#pragma unroll
+    for (int ch = 0; ch < ATG_RUN / 16; ++ch) {
+        // keep each chunk's loads inside the chunk (bounds live registers)
+        asm volatile("" : "+v"(base)::"memory");
+        int x[16];
+        if (FULL) {
+            const int4 *p4 = (const int4 *)&sl[saddr(base + 16 * ch)];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int4 v = p4[q];
+                x[4 * q] = v.x;
+                x[4 * q + 1] = v.y;
+                x[4 * q + 2] = v.z;
+                x[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                x[t] = sl[saddr(base + 16 * ch + t)];
+        }
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+            const int t = 16 * ch + tt;
+            const int s = x[tt];
+            int acc;
+            if (DOT2) {
+                acc = 0;
+#pragma unroll
+                for (int j = 0; j < W / 2; ++j) {
+                    short2_t av = __builtin_bit_cast(short2_t, qw[2 * j]);
+                    short2_t bv = __builtin_bit_cast(short2_t, cp[j]);
+                    acc = __builtin_amdgcn_sdot2(av, bv, acc, false);
+                }
+                const int prev = win[0];
+#pragma unroll
+                for (int k = W - 1; k > 0; --k)
+                    qw[k] = qw[k - 1];
+                qw[0] = (int)__builtin_amdgcn_perm((uint32_t)prev, (uint32_t)s, 0x05040100u);
+                win[0] = s;
+            } else {
+                acc = 0;
+#pragma unroll
+                for (int k = 0; k < W; ++k)
+                    acc = mad24(win[k], cf[k], acc);
+#pragma unroll
+                for (int k = W - 1; k > 0; --k)
+                    win[k] = win[k - 1];
+                win[0] = s;
+            }
+            const int r = (int)((uint32_t)s - (uint32_t)(acc >> shift));
+            uint32_t uu = zigzag(r);
+            uint32_t ar = iabs_u(r);
+            if (!FULL) {
+                const bool v = t < len;
+                uu = v ? uu : 0u;
+                ar = v ? ar : 0u;
+            }
+            u[t] = uu;
+            sum += ar;
+        }
+    }
+    return sum;
+}
+
+// Exclude warm-up positions (< order) from a run's codes and |r| sum.
+// |r| = (u + 1) >> 1 for a zig-zag code u.
+__device__ __forceinline__ int drop_warmup(int a, int len, int order, uint32_t (&u)[ATG_RUN],
+                                           uint64_t &sum)
+{
+    const int warm = min(max(order - a, 0), len);
+    if (warm > 0) {
+#pragma unroll
+        for (int t = 0; t < ATG_FAST_ORDER; ++t) {
+            if (t < warm) {
+                sum -= ((uint64_t)u[t] + 1u) >> 1;
+                u[t] = 0u;
+            }
+        }
+    }
+    return warm;
+}
+
+// 32-bit accumulation is exact when every partial sum fits in int32
+// (sum |c| * max |s| < 2^31); which arithmetic kernel applies.
+enum { RES_GENERIC = 0, RES_DOT2 = 1, RES_MAD24 = 2 };
+__device__ __forceinline__ int residual_kernel(uint64_t csum, uint32_t maxabs, int order)
+{
+    const bool narrow = csum * (uint64_t)maxabs < (1ull << 31);
+    if (narrow && order <= ATG_FAST_ORDER) {
+        if (maxabs <= 32767u && csum <= 32767u * 12u)
+            return RES_DOT2;
+        if (maxabs < (1u << 23))
+            return RES_MAD24;
+    }
+    return RES_GENERIC;
+}
