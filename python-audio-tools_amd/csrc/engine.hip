@@ -178,7 +178,8 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
     p.n_cand = (channels == 2 && (p.mid_side || p.adaptive_mid_side)) ? 4 : channels;
     p.n_tracks = n_tracks;
     const uint32_t M = p.max_lpc_order;
-    p.coef_stride = std::max<uint32_t>(2, (M * (M + 1) / 2 + 1) & ~1u);
+    p.coef_row = std::max<uint32_t>(2, (M + 1u) & ~1u);
+    p.coef_stride = std::max<uint32_t>(1, M) * p.coef_row;
     p.padding_size = o->padding_size;
     p.header_bytes = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + o->padding_size;
 

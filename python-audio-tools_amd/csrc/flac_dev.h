@@ -42,6 +42,7 @@ struct FlacParams {
     uint32_t n_frames;
     uint32_t n_tracks;
     uint32_t coef_stride;    // int16 entries per candidate in the lpc table
+    uint32_t coef_row;       // int16 entries per order row (even; zero past the order)
     uint32_t padding_size;
     uint32_t header_bytes;   // bytes before the first frame of every track
     uint32_t frame_lds_words;// pack kernel frame buffer (32-bit words)

@@ -45,7 +45,7 @@ __device__ __forceinline__ int32_t d2i_x86(double x)
 template <int LAGS>
 __device__ __forceinline__ void quantize_store(const double (&lp)[LAGS],
                                                int order, int prec,
-                                               int16_t *__restrict__ q,
+                                               int16_t *__restrict__ q, uint32_t row,
                                                int8_t *__restrict__ shift_out)
 {
     // flacenc_quantize_coefficients (flac.c:1270-1324)
@@ -77,6 +77,9 @@ __device__ __forceinline__ void quantize_store(const double (&lp)[LAGS],
             err -= (double)ei;
         }
     }
+    // rows are zero past the order: fixed-width readers use them as taps
+    for (uint32_t i = (uint32_t)order; i < row; ++i)
+        q[i] = 0;
     *shift_out = (int8_t)(shift >= 0 ? shift : 0);
 }
 
@@ -188,7 +191,7 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
     double k0 = acc[1] / acc[0];
     cur[0] = k0;
     errv[0] = acc[0] * (1.0 - (k0 * k0));
-    quantize_store<LAGS>(cur, 1, prec, qout, sout);
+    quantize_store<LAGS>(cur, 1, prec, qout, p.coef_row, sout);
 #pragma unroll
     for (int i = 1; i < LAGS; ++i) {
         if (i < M) {
@@ -207,7 +210,7 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
                     cur[j] = prev[j] - (kk * prev[i - j - 1]);
             cur[i] = kk;
             errv[i] = errv[i - 1] * (1.0 - (kk * kk));
-            quantize_store<LAGS>(cur, i + 1, prec, qout + (i * (i + 1)) / 2,
+            quantize_store<LAGS>(cur, i + 1, prec, qout + i * p.coef_row, p.coef_row,
                                  sout + i);
         }
     }

@@ -76,55 +76,95 @@ struct PartSel {
     uint32_t hdr_bits;
 };
 
+// Estimated bits of one partition (flac.c:1437-1505), 64-bit as the
+// reference's accumulator.
+__device__ __forceinline__ uint64_t part_estimate(uint32_t plen, uint64_t sum, uint32_t k)
+{
+    if (k > 0)
+        return 4ull + (sum >> (k - 1)) + (uint64_t)(uint32_t)((1u + k) * plen) -
+               (uint64_t)(plen / 2u);
+    return 4ull + (sum << 1) + (uint64_t)plen - (uint64_t)(plen / 2u);
+}
+
+// Rice parameter and estimate of partition j at level lv (sum = its |r| sum)
+__device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, uint64_t S, uint64_t total,
+                                          uint32_t order, const RunCtx &c, uint32_t &k,
+                                          uint64_t &e)
+{
+    const uint32_t Sp = c.N >> lv;
+    const bool degen = Sp < order; // partition 0 takes every residual
+    const uint32_t plen = j == 0 ? Sp - order : Sp;
+    const uint64_t sum = degen ? (j == 0 ? total : 0ull) : S;
+    k = rice_param(plen, sum, c.max_rice);
+    e = part_estimate(plen, sum, k);
+}
+
 // flacenc_encode_residuals' partition-order search (flac.c:1362-1402) from
-// per-lane |r| sums.  Level lv partition of lane l is l >> (6 - lv).
+// per-lane |r| sums; level lv partition of lane l is l >> (6 - lv).
+// All 127 (level, partition) pairs are evaluated in two lane-parallel
+// passes instead of seven:
+//   pass A  level 6, partition = lane;
+//   pass B  levels 5..0 packed into lanes [64 - 2^(lv+1), 64 - 2^lv):
+//           lanes 0-31 level 5, 32-47 level 4, 48-55 level 3, 56-59 level 2,
+//           60-61 level 1, 62 level 0 (63 idle).
+// Partition sums come from one inclusive prefix scan of the lane sums; the
+// level totals from a full butterfly (A) and a segmented one (B) whose
+// segments are aligned to their power-of-two sizes.
 __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order, const RunCtx &c)
 {
-    uint64_t S[7];
-    S[6] = lane_sum;
+    const int lane = c.lane;
+    uint64_t pre = lane_sum;
 #pragma unroll
-    for (int b = 0; b < 6; ++b)
-        S[5 - b] = S[6 - b] + shfl_xor_u64(S[6 - b], 1 << b);
-    const uint64_t total = S[0];
+    for (int d = 1; d < 64; d <<= 1) {
+        const uint64_t t = shfl_up_u64(pre, d);
+        pre += lane >= d ? t : 0ull;
+    }
+    const uint64_t total = readlane_u64(pre, 63);
+
+    const uint32_t lvB = lane < 32 ? 5u : lane < 48 ? 4u : lane < 56 ? 3u
+                       : lane < 60 ? 2u : lane < 62 ? 1u : 0u;
+    const uint32_t offB = 64u - (2u << lvB);
+    const uint32_t jB = (uint32_t)lane - offB;
+    const uint32_t wB = 64u >> lvB; // lanes per partition at level lvB
+    const int first = (int)((jB * wB) & 63u), last = (int)((jB * wB + wB - 1u) & 63u);
+    const uint64_t p_last = shfl_u64(pre, last);
+    const uint64_t p_prev = shfl_u64(pre, (first + 63) & 63);
+    const uint64_t SB = p_last - (first ? p_prev : 0ull);
+
+    uint32_t kA, kB;
+    uint64_t eA, eB;
+    part_eval(6, (uint32_t)lane, lane_sum, total, order, c, kA, eA);
+    part_eval(lvB, jB, SB, total, order, c, kB, eB);
+#pragma unroll
+    for (int m = 1; m < 64; m <<= 1)
+        eA += shfl_xor_u64(eA, m);
+    const uint32_t segB = lane == 63 ? 1u : (1u << lvB);
+#pragma unroll
+    for (int m = 1; m < 32; m <<= 1) {
+        const uint64_t o = shfl_xor_u64(eB, m);
+        eB += (uint32_t)m < segB ? o : 0ull;
+    }
 
     uint64_t best_tot = ~0ull;
     uint32_t best_p = 0;
-    uint32_t kown[7];
 #pragma unroll
     for (int lv = 0; lv <= 6; ++lv) {
-        kown[lv] = 0;
-        if (lv <= c.P) {
-            const uint32_t Sp = c.N >> lv;
-            const bool degen = Sp < order;
-            const uint32_t jp = (uint32_t)c.lane >> (6 - lv);
-            const uint32_t plen = jp == 0 ? Sp - order : Sp;
-            const uint64_t sum = degen ? (jp == 0 ? total : 0ull) : S[lv];
-            const uint32_t k = rice_param(plen, sum, c.max_rice);
-            kown[lv] = k;
-            uint64_t e;
-            if (k > 0)
-                e = 4ull + (sum >> (k - 1)) + (uint64_t)(uint32_t)((1u + k) * plen) -
-                    (uint64_t)(plen / 2u);
-            else
-                e = 4ull + (sum << 1) + (uint64_t)plen - (uint64_t)(plen / 2u);
-#pragma unroll
-            for (int b = 6 - lv; b < 6; ++b)
-                e += shfl_xor_u64(e, 1 << b);
-            if (e < best_tot) {
-                best_tot = e;
-                best_p = (uint32_t)lv;
-            }
+        const uint64_t T = lv == 6 ? readlane_u64(eA, 0) : readlane_u64(eB, 64 - (2 << lv));
+        if (lv <= c.P && T < best_tot) {
+            best_tot = T;
+            best_p = (uint32_t)lv;
         }
     }
     PartSel r;
     r.porder = best_p;
-    uint32_t ko = kown[0];
-#pragma unroll
-    for (int lv = 1; lv <= 6; ++lv)
-        ko = best_p == (uint32_t)lv ? kown[lv] : ko;
+    uint32_t ko;
+    if (best_p == 6u)
+        ko = kA;
+    else
+        ko = (uint32_t)__shfl((int)kB, (int)(64u - (2u << best_p) + ((uint32_t)lane >> (6u - best_p))), 64);
     r.k_own = ko;
     const bool degen_best = (c.N >> best_p) < order;
-    const uint32_t k0 = (uint32_t)__shfl((int)ko, 0, 64);
+    const uint32_t k0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)ko);
     r.k_lane = degen_best ? k0 : ko;
     r.method = 0;
     if (c.max_rice > 14u)
@@ -138,31 +178,121 @@ struct Eval {
     PartSel sel;
 };
 
-// Fast path: order <= 12 with exact 32-bit accumulation (residual.h); the 64
-// zig-zag codes of the lane's run stay in VGPRs for pass 2.
+// v_dot2_i32_i16 with a zero accumulator (VOP3 form: no v_mov to clear it)
+__device__ __forceinline__ int dot2_first(int a, int b_uniform)
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "s"(b_uniform));
+    return d;
+}
+
+// Hot path (N = 4096, samples fit int16, |u| < 2^26): residuals of the
+// lane's 64-sample run with TAPS taps (the order rounded up to even),
+// v_dot2 on packed sample pairs.  Sums are kept in 32 bits, two samples
+// per v_add3:  su = sum u (zig-zag codes), sn = -#(r < 0); the reference's
+// sum |r| is then (su + #neg) / 2 exactly, since |r| = (u + (u & 1)) / 2.
+// Warm-up positions (lane 0, t < order) are masked to u = 0.
+template <int TAPS>
+__device__ __forceinline__ uint64_t residuals_full_dot2(const int32_t *__restrict__ sl,
+                                                        const RunCtx &c,
+                                                        const int (&cfu)[ATG_FAST_ORDER],
+                                                        int order, int shift,
+                                                        uint32_t (&u)[ATG_RUN])
+{
+    constexpr int NP = TAPS / 2;
+    constexpr int W = ATG_FAST_ORDER;
+    int cp[NP];
+#pragma unroll
+    for (int j = 0; j < NP; ++j)
+        cp[j] = uniform_i32((int)(((uint32_t)cfu[2 * j] & 0xFFFFu) |
+                                  ((uint32_t)cfu[2 * j + 1] << 16)));
+    int base = c.a;
+    int h[W + 1]; // s[a-13 .. a-1]
+    {
+        const int4 *hp = (const int4 *)&sl[saddr(base - W)];
+#pragma unroll
+        for (int q = 0; q < W / 4; ++q) {
+            const int4 v = hp[q];
+            h[1 + 4 * q] = v.x;
+            h[2 + 4 * q] = v.y;
+            h[3 + 4 * q] = v.z;
+            h[4 + 4 * q] = v.w;
+        }
+        h[0] = sl[saddr(base - W - 1)];
+    }
+    int qw[TAPS]; // qw[k] = Q_{t-1-k} = (s[t-1-k], s[t-2-k])
+#pragma unroll
+    for (int k = 0; k < TAPS; ++k)
+        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)h[W - 1 - k], (uint32_t)h[W - k],
+                                           0x05040100u);
+    int prev = h[W];
+    const int warm = c.a < order ? order - c.a : 0; // lane 0 only
+    uint32_t su = 0, sn = 0, pu = 0, pn = 0;
+#pragma unroll
+    for (int ch = 0; ch < ATG_RUN / 16; ++ch) {
+        asm volatile("" : "+v"(base)::"memory");
+        int x[16];
+        const int4 *p4 = (const int4 *)&sl[saddr(base + 16 * ch)];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int4 v = p4[q];
+            x[4 * q] = v.x;
+            x[4 * q + 1] = v.y;
+            x[4 * q + 2] = v.z;
+            x[4 * q + 3] = v.w;
+        }
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+            const int t = 16 * ch + tt;
+            const int s = x[tt];
+            int acc = dot2_first(qw[0], cp[0]);
+#pragma unroll
+            for (int j = 1; j < NP; ++j) {
+                short2_t av = __builtin_bit_cast(short2_t, qw[2 * j]);
+                short2_t bv = __builtin_bit_cast(short2_t, cp[j]);
+                acc = __builtin_amdgcn_sdot2(av, bv, acc, false);
+            }
+#pragma unroll
+            for (int k = TAPS - 1; k > 0; --k)
+                qw[k] = qw[k - 1];
+            qw[0] = (int)__builtin_amdgcn_perm((uint32_t)prev, (uint32_t)s, 0x05040100u);
+            prev = s;
+            const int r = (int)((uint32_t)s - (uint32_t)(acc >> shift));
+            uint32_t neg = (uint32_t)(r >> 31);
+            uint32_t uu = ((uint32_t)r << 1) ^ neg;
+            if (t < W) {
+                const bool w = t < warm;
+                uu = w ? 0u : uu;
+                neg = w ? 0u : neg;
+            }
+            u[t] = uu;
+            if (tt & 1) {
+                su = su + pu + uu; // v_add3_u32
+                sn = sn + pn + neg;
+            } else {
+                pu = uu;
+                pn = neg;
+            }
+        }
+    }
+    return ((uint64_t)su + (uint64_t)(0u - sn)) >> 1;
+}
+
+// Other fast cases: 12 taps (residual.h), 64-bit |r| sums, warm-up dropped
+// afterwards.
 template <bool DOT2, bool FULL>
-__device__ __forceinline__ Eval eval_fast(const int32_t *__restrict__ sl, const RunCtx &c,
-                                          const int *__restrict__ cf_lds, int order,
-                                          int shift)
+__device__ __forceinline__ uint64_t residuals_fast(const int32_t *__restrict__ sl,
+                                                   const RunCtx &c,
+                                                   const int (&cfu)[ATG_FAST_ORDER], int order,
+                                                   int shift, uint32_t (&u)[ATG_RUN])
 {
     int cf[ATG_FAST_ORDER];
 #pragma unroll
     for (int k = 0; k < ATG_FAST_ORDER; ++k)
-        cf[k] = uniform_i32(k < order ? cf_lds[k] : 0);
-    uint32_t u[ATG_RUN];
+        cf[k] = uniform_i32(cfu[k]);
     uint64_t sum = lane_residuals<DOT2, FULL>(sl, c.a, c.len, cf, shift, u);
-    const int warm = drop_warmup(c.a, c.len, order, u, sum);
-    const int cnt = c.len - warm;
-    Eval ev;
-    ev.sel = select_partitions(sum, (uint32_t)order, c);
-    const uint32_t k = ev.sel.k_lane;
-    uint32_t lb = 0;
-#pragma unroll
-    for (int t = 0; t < ATG_RUN; ++t)
-        lb += u[t] >> k;
-    lb += (uint32_t)cnt * (1u + k);
-    ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
-    return ev;
+    drop_warmup(c.a, c.len, order, u, sum);
+    return sum;
 }
 
 // Generic path: any order <= 32, 64-bit accumulator, recompute in pass 2.
@@ -195,28 +325,67 @@ __device__ __forceinline__ Eval eval_generic(const int32_t *__restrict__ sl, con
     return ev;
 }
 
-__device__ __forceinline__ Eval eval_any(const int32_t *sl, const RunCtx &c,
-                                         const int *cf_lds, int order, int shift,
-                                         uint32_t maxabs)
+// One predictor on the fast paths (order <= 12, exact 32-bit arithmetic):
+// residuals with the 64 zig-zag codes of the lane's run kept in VGPRs,
+// partition search, exact bits.  cfu[] = wave-uniform taps (0 past order).
+__device__ __forceinline__ Eval eval_fast_any(const int32_t *sl, const RunCtx &c,
+                                              const int (&cfu)[ATG_FAST_ORDER], int order,
+                                              int shift, uint32_t maxabs, uint64_t csum,
+                                              int kind)
 {
-    uint64_t csum = 0;
-    for (int k = 0; k < order; ++k)
-        csum += (uint64_t)(cf_lds[k] < 0 ? -(int64_t)cf_lds[k] : cf_lds[k]);
-    const int kind = residual_kernel(csum, maxabs, order);
     const bool full = c.N == ATG_MAX_BLOCK;
-    if (kind == RES_DOT2)
-        return full ? eval_fast<true, true>(sl, c, cf_lds, order, shift)
-                    : eval_fast<true, false>(sl, c, cf_lds, order, shift);
-    if (kind == RES_MAD24)
-        return full ? eval_fast<false, true>(sl, c, cf_lds, order, shift)
-                    : eval_fast<false, false>(sl, c, cf_lds, order, shift);
-    return eval_generic(sl, c, cf_lds, order, shift);
+    // |r| <= max|s| + (sum|c| max|s| >> shift) + 1; 32-bit sums of 64 codes
+    // u <= 2|r| + 1 are exact below 2^26 per code
+    const uint64_t rbound = (uint64_t)maxabs + ((csum * (uint64_t)maxabs) >> shift) + 1u;
+    const bool sum32 = 2u * rbound + 1u < (1ull << 26);
+    uint32_t u[ATG_RUN];
+    uint64_t sum;
+    if (kind == RES_DOT2 && full && sum32) {
+        switch ((order + 1) >> 1) {
+        case 0:
+        case 1: sum = residuals_full_dot2<2>(sl, c, cfu, order, shift, u); break;
+        case 2: sum = residuals_full_dot2<4>(sl, c, cfu, order, shift, u); break;
+        case 3: sum = residuals_full_dot2<6>(sl, c, cfu, order, shift, u); break;
+        case 4: sum = residuals_full_dot2<8>(sl, c, cfu, order, shift, u); break;
+        case 5: sum = residuals_full_dot2<10>(sl, c, cfu, order, shift, u); break;
+        default: sum = residuals_full_dot2<12>(sl, c, cfu, order, shift, u); break;
+        }
+    } else if (kind == RES_DOT2) {
+        sum = full ? residuals_fast<true, true>(sl, c, cfu, order, shift, u)
+                   : residuals_fast<true, false>(sl, c, cfu, order, shift, u);
+    } else {
+        sum = full ? residuals_fast<false, true>(sl, c, cfu, order, shift, u)
+                   : residuals_fast<false, false>(sl, c, cfu, order, shift, u);
+    }
+    const int warm = min(max(order - c.a, 0), c.len);
+    const int cnt = c.len - warm;
+    Eval ev;
+    ev.sel = select_partitions(sum, (uint32_t)order, c);
+    const uint32_t k = ev.sel.k_lane;
+    uint32_t lb = (uint32_t)cnt * (1u + k);
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; t += 2)
+        lb = lb + (u[t] >> k) + (u[t + 1] >> k); // v_add3_u32
+    ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
+    return ev;
+}
+
+// FIXED predictor of order o as LPC taps (flac.c:918-1016)
+__device__ __forceinline__ int fixed_tap(uint32_t o, int j)
+{
+    switch (o) {
+    case 1: return j == 0 ? 1 : 0;
+    case 2: return j == 0 ? 2 : j == 1 ? -1 : 0;
+    case 3: return j == 0 ? 3 : j == 1 ? -3 : j == 2 ? 1 : 0;
+    case 4: return j == 0 ? 4 : j == 1 ? -6 : j == 2 ? 4 : j == 3 ? -1 : 0;
+    default: return 0;
+    }
 }
 
 __device__ __forceinline__ uint32_t wasted_field(uint32_t w) { return w ? w + 1u : 1u; }
 
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_subframe_search(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_subframe_search(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
@@ -373,26 +542,36 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
         const uint32_t o = is_fixed ? fixed_order : lo + pi - (p.try_fixed ? 1u : 0u);
         int shift = 0;
         uint32_t prec = 0;
-        if (is_fixed) {
-            // FIXED predictors as integer coefficient sets, shift 0
-            const int fc = o == 1 ? (lane == 0 ? 1 : 0)
-                         : o == 2 ? (lane == 0 ? 2 : lane == 1 ? -1 : 0)
-                         : o == 3 ? (lane == 0 ? 3 : lane == 1 ? -3 : lane == 2 ? 1 : 0)
-                         : (lane == 0 ? 4 : lane == 1 ? -6 : lane == 2 ? 4 : lane == 3 ? -1 : 0);
-            if (lane < 4)
-                cf_lds[lane] = fc;
-        } else if (dummy) {
-            if (lane == 0)
-                cf_lds[0] = 1;
-            prec = 2;
-        } else {
-            if (lane < (int)o)
-                cf_lds[lane] = qtab[(o * (o - 1u)) / 2u + (uint32_t)lane];
+        // this predictor's taps, wave-uniform (scalar loads of the LPC row)
+        const int16_t *__restrict__ row = qtab + (size_t)(o ? o - 1u : 0u) * p.coef_row;
+        if (!is_fixed && !dummy) {
             shift = stab[o - 1u];
             prec = p.qlp_precision;
+        } else if (dummy) {
+            prec = 2;
         }
-        __syncthreads();
-        const Eval ev = eval_any(sl, c, cf_lds, (int)o, shift, maxabs);
+        int cfu[ATG_FAST_ORDER];
+        uint64_t csum = 0;
+#pragma unroll
+        for (int j = 0; j < ATG_FAST_ORDER; ++j) {
+            const int cj = is_fixed ? fixed_tap(o, j)
+                         : dummy ? (j == 0 ? 1 : 0)
+                         : ((uint32_t)j < o ? (int)row[j] : 0);
+            cfu[j] = cj;
+            csum += (uint64_t)(cj < 0 ? -cj : cj);
+        }
+        const int kind = o <= ATG_FAST_ORDER ? residual_kernel(csum, maxabs, (int)o)
+                                             : RES_GENERIC;
+        Eval ev;
+        if (kind == RES_GENERIC) {
+            if ((uint32_t)lane < o)
+                cf_lds[lane] = is_fixed ? fixed_tap(o, lane) : dummy ? 1 : (int)row[lane];
+            __syncthreads();
+            ev = eval_generic(sl, c, cf_lds, (int)o, shift);
+            __syncthreads();
+        } else {
+            ev = eval_fast_any(sl, c, cfu, (int)o, shift, maxabs, csum, kind);
+        }
         if (is_fixed) {
             fixed_bits = 7u + wf + o * rb + ev.bits;
             fixed_sel = ev.sel;
@@ -406,7 +585,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
                 lpc_sel = ev.sel;
             }
         }
-        __syncthreads();
     }
 
     // ---- subframe choice (flac.c:727-809)
@@ -441,7 +619,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(3))) void k_
     if (pick == SF_LPC) {
         if (lane < (int)lpc_order)
             d->coef[lane] = (int16_t)(N > p.max_lpc_order + 1u
-                                          ? qtab[(lpc_order * (lpc_order - 1u)) / 2u + lane]
+                                          ? qtab[(lpc_order - 1u) * p.coef_row + lane]
                                           : 1);
     }
     if (lane == 0) {
