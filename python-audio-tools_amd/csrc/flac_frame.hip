@@ -379,11 +379,12 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         const uint32_t type = d.type, order = d.order, w = d.wasted, sbps = d.sbps;
         const uint32_t start = pos;
         uint32_t maxabs = 0;
-        for (uint32_t i = lane; i < N; i += 64) {
-            const int32_t s = cand_sample(pcm, fi.pcm_start + i, p.channels, cand, ms) >> w;
-            sl[saddr((int)i)] = s;
-            maxabs = max(maxabs, iabs_u(s));
-        }
+        stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
+                            [&](uint32_t i, int32_t s) {
+                                s >>= w;
+                                sl[saddr((int)i)] = s;
+                                maxabs = max(maxabs, iabs_u(s));
+                            });
         maxabs = wave_max_u32(maxabs);
         if (lane < (int)order) {
             int c;

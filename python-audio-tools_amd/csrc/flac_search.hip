@@ -31,6 +31,11 @@
 #include "residual.h"
 #include "wave.h"
 
+// timing experiments only (tools/gpu_exp.sh); 0 in every product build
+#ifndef ATG_EXP
+#define ATG_EXP 0
+#endif
+
 // Rice parameter of one partition: the reference's loop
 //   while ((uint64_t)(plength << Rice) < sum) if (Rice < max) Rice++; else break;
 // including its 32-bit shift (flac.c:1477-1484).
@@ -112,6 +117,10 @@ __device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, uint64_t S, u
 // segments are aligned to their power-of-two sizes.
 __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order, const RunCtx &c)
 {
+#if ATG_EXP == 2
+    { PartSel r; r.porder = 6; r.method = 0; r.k_own = r.k_lane = (uint32_t)(lane_sum >> 6) & 7u;
+      r.hdr_bits = 6u + 64u * 4u; return r; }
+#endif
     const int lane = c.lane;
     uint64_t pre = lane_sum;
 #pragma unroll
@@ -363,9 +372,13 @@ __device__ __forceinline__ Eval eval_fast_any(const int32_t *sl, const RunCtx &c
     ev.sel = select_partitions(sum, (uint32_t)order, c);
     const uint32_t k = ev.sel.k_lane;
     uint32_t lb = (uint32_t)cnt * (1u + k);
+#if ATG_EXP == 4
+    lb += u[(k + 3) & 63];
+#else
 #pragma unroll
     for (int t = 0; t < ATG_RUN; t += 2)
         lb = lb + (u[t] >> k) + (u[t + 1] >> k); // v_add3_u32
+#endif
     ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
     return ev;
 }
@@ -416,14 +429,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     for (int i = lane; i < SL_PRE; i += 64)
         sl[i] = 0;
     const int32_t first = cand_sample(pcm, fi.pcm_start, p.channels, cand, ms);
-    uint32_t orv = 0;
+    uint32_t orv = 0, amax = 0;
     bool same = true;
-    for (uint32_t i = lane; i < N; i += 64) {
-        const int32_t s = cand_sample(pcm, fi.pcm_start + i, p.channels, cand, ms);
-        sl[saddr((int)i)] = s;
-        orv |= (uint32_t)s;
-        same = same && (s == first);
-    }
+    stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
+                        [&](uint32_t i, int32_t s) {
+                            sl[saddr((int)i)] = s;
+                            orv |= (uint32_t)s;
+                            amax = max(amax, iabs_u(s));
+                            same = same && (s == first);
+                        });
     orv = wave_or_u32(orv);
     same = wave_all(same);
     __syncthreads();
@@ -443,14 +457,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         return;
     }
     const uint32_t w = orv ? (uint32_t)__builtin_ctz(orv) : 0u;
-    uint32_t maxabs = 0;
-    for (uint32_t i = lane; i < N; i += 64) {
-        const int32_t s = sl[saddr((int)i)] >> w;
-        sl[saddr((int)i)] = s;
-        maxabs = max(maxabs, iabs_u(s));
+    // every sample is a multiple of 2^w, so max|s >> w| = max|s| >> w
+    const uint32_t maxabs = wave_max_u32(amax) >> w;
+    if (w) {
+        for (uint32_t i = lane; i < N; i += 64)
+            sl[saddr((int)i)] >>= w;
+        __syncthreads();
     }
-    maxabs = wave_max_u32(maxabs);
-    __syncthreads();
 
     // ---- lane run inside one finest partition
     RunCtx c;
@@ -479,24 +492,73 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 
     // ---- FIXED order by |residual| sums over samples [4,N) (flac.c:856-916)
     uint32_t fixed_order = 0;
+#if ATG_EXP == 1
+    fixed_order = 2;
+    if (0) {
+#else
     if (p.try_fixed) {
+#endif
         uint64_t s5[5] = {0, 0, 0, 0, 0};
-        const int st = max(c.a, 4);
-        for (int i = st; i < c.a + c.len; ++i) {
-            const uint32_t x0 = (uint32_t)sl[saddr(i)], x1 = (uint32_t)sl[saddr(i - 1)],
-                           x2 = (uint32_t)sl[saddr(i - 2)], x3 = (uint32_t)sl[saddr(i - 3)],
-                           x4 = (uint32_t)sl[saddr(i - 4)];
-            const int32_t d0 = (int32_t)x0;
-            const int32_t d1 = (int32_t)(x0 - x1);
-            const int32_t d2 = (int32_t)(x0 - 2u * x1 + x2);
-            const int32_t d3 = (int32_t)(x0 - 3u * x1 + 3u * x2 - x3);
-            const int32_t d4 = (int32_t)(x0 - 4u * x1 + 6u * x2 - 4u * x3 + x4);
-            // accumulator += abs(int): abs(INT_MIN) stays negative (flac.c:1628)
-            s5[0] += (uint64_t)(int64_t)(int32_t)iabs_u(d0);
-            s5[1] += (uint64_t)(int64_t)(int32_t)iabs_u(d1);
-            s5[2] += (uint64_t)(int64_t)(int32_t)iabs_u(d2);
-            s5[3] += (uint64_t)(int64_t)(int32_t)iabs_u(d3);
-            s5[4] += (uint64_t)(int64_t)(int32_t)iabs_u(d4);
+        if (N == ATG_MAX_BLOCK && maxabs < (1u << 21)) {
+            // the lane's 64 samples from LDS, differences carried in
+            // registers, |d| summed in 32 bits (16 max|s| * 64 < 2^31)
+            uint32_t a5[5] = {0, 0, 0, 0, 0};
+            const int4 *hp = (const int4 *)&sl[saddr(c.a - 4)];
+            const int4 h4 = hp[0];
+            int x1 = h4.w, d1p = h4.w - h4.z, d2p = d1p - (h4.z - h4.y);
+            int d3p = d2p - ((h4.z - h4.y) - (h4.y - h4.x));
+            int base = c.a;
+#pragma unroll
+            for (int chn = 0; chn < ATG_RUN / 16; ++chn) {
+                asm volatile("" : "+v"(base)::"memory");
+                const int4 *p4 = (const int4 *)&sl[saddr(base + 16 * chn)];
+                int x[16];
+#pragma unroll
+                for (int q = 0; q < 4; ++q) {
+                    const int4 v = p4[q];
+                    x[4 * q] = v.x;
+                    x[4 * q + 1] = v.y;
+                    x[4 * q + 2] = v.z;
+                    x[4 * q + 3] = v.w;
+                }
+#pragma unroll
+                for (int tt = 0; tt < 16; ++tt) {
+                    const int x0 = x[tt];
+                    const int d1 = x0 - x1, d2 = d1 - d1p, d3 = d2 - d2p, d4 = d3 - d3p;
+                    x1 = x0;
+                    d1p = d1;
+                    d2p = d2;
+                    d3p = d3;
+                    // samples 0..3 are outside the sums (lane 0 only)
+                    const bool v = chn > 0 || tt >= 4 || c.a > 0;
+                    a5[0] += v ? iabs_u(x0) : 0u;
+                    a5[1] += v ? iabs_u(d1) : 0u;
+                    a5[2] += v ? iabs_u(d2) : 0u;
+                    a5[3] += v ? iabs_u(d3) : 0u;
+                    a5[4] += v ? iabs_u(d4) : 0u;
+                }
+            }
+#pragma unroll
+            for (int k = 0; k < 5; ++k)
+                s5[k] = a5[k];
+        } else {
+            const int st = max(c.a, 4);
+            for (int i = st; i < c.a + c.len; ++i) {
+                const uint32_t x0 = (uint32_t)sl[saddr(i)], x1 = (uint32_t)sl[saddr(i - 1)],
+                               x2 = (uint32_t)sl[saddr(i - 2)], x3 = (uint32_t)sl[saddr(i - 3)],
+                               x4 = (uint32_t)sl[saddr(i - 4)];
+                const int32_t d0 = (int32_t)x0;
+                const int32_t d1 = (int32_t)(x0 - x1);
+                const int32_t d2 = (int32_t)(x0 - 2u * x1 + x2);
+                const int32_t d3 = (int32_t)(x0 - 3u * x1 + 3u * x2 - x3);
+                const int32_t d4 = (int32_t)(x0 - 4u * x1 + 6u * x2 - 4u * x3 + x4);
+                // accumulator += abs(int): abs(INT_MIN) stays negative (flac.c:1628)
+                s5[0] += (uint64_t)(int64_t)(int32_t)iabs_u(d0);
+                s5[1] += (uint64_t)(int64_t)(int32_t)iabs_u(d1);
+                s5[2] += (uint64_t)(int64_t)(int32_t)iabs_u(d2);
+                s5[3] += (uint64_t)(int64_t)(int32_t)iabs_u(d3);
+                s5[4] += (uint64_t)(int64_t)(int32_t)iabs_u(d4);
+            }
         }
 #pragma unroll
         for (int k = 0; k < 5; ++k)
@@ -536,7 +598,14 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     uint32_t lpc_bits = 0xFFFFFFFFu, lpc_order = 0, lpc_prec = 0;
     int lpc_shift = 0;
     PartSel lpc_sel = {};
+#if ATG_EXP == 3
+    lo = hi = M;
+#endif
+#if ATG_EXP == 6
+    const uint32_t n_pred = 0;
+#else
     const uint32_t n_pred = (p.try_fixed ? 1u : 0u) + (p.try_lpc ? hi - lo + 1u : 0u);
+#endif
     for (uint32_t pi = 0; pi < n_pred; ++pi) {
         const bool is_fixed = p.try_fixed && pi == 0;
         const uint32_t o = is_fixed ? fixed_order : lo + pi - (p.try_fixed ? 1u : 0u);

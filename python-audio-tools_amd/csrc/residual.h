@@ -12,6 +12,7 @@
 #include <stdint.h>
 
 #include "flac_dev.h"
+#include "pcm_read.h"
 #include "wave.h"
 
 #define SL_PRE 48
@@ -176,4 +177,43 @@ __device__ __forceinline__ int residual_kernel(uint64_t csum, uint32_t maxabs, i
             return RES_MAD24;
     }
     return RES_GENERIC;
+}
+
+// Stage candidate `cand` of a frame (samples [0, N)) through registers:
+// lane l takes samples l, l + 64, ...; STAGE_U loads per lane are issued
+// before any is consumed (one memory latency per STAGE_U x 64 samples
+// instead of one per 64).  f(i, s) consumes sample i.
+#define STAGE_U 32
+template <int MODE, typename T, typename F>
+__device__ __forceinline__ void stage_candidate(const T *__restrict__ src, uint32_t N, uint32_t ch,
+                                                uint32_t cand, int lane, F &&f)
+{
+    const uint32_t nlast = N ? N - 1u : 0u;
+    for (uint32_t m0 = 0; m0 * 64u < N; m0 += STAGE_U) {
+        int32_t v[STAGE_U];
+#pragma unroll
+        for (int u = 0; u < STAGE_U; ++u) {
+            const uint32_t i = (uint32_t)lane + 64u * (m0 + (uint32_t)u);
+            v[u] = cand_at<MODE>(src, min(i, nlast), ch, cand);
+        }
+#pragma unroll
+        for (int u = 0; u < STAGE_U; ++u) {
+            const uint32_t i = (uint32_t)lane + 64u * (m0 + (uint32_t)u);
+            if (i < N)
+                f(i, v[u]);
+        }
+    }
+}
+
+template <typename T, typename F>
+__device__ __forceinline__ void stage_candidate_any(const T *__restrict__ pcm, uint64_t pcm_start,
+                                                    uint32_t N, uint32_t ch, uint32_t cand,
+                                                    bool ms, int lane, F &&f)
+{
+    const T *__restrict__ src = pcm + pcm_start * ch;
+    switch (pcm_mode(pcm, ms)) {
+    case PCM_MS16: stage_candidate<PCM_MS16>(src, N, ch, cand, lane, f); break;
+    case PCM_MS: stage_candidate<PCM_MS>(src, N, ch, cand, lane, f); break;
+    default: stage_candidate<PCM_CH>(src, N, ch, cand, lane, f); break;
+    }
 }
