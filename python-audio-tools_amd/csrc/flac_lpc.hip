@@ -29,6 +29,7 @@
 #include "flac_dev.h"
 #include "launch.h"
 #include "pcm_read.h"
+#include "residual.h"
 #include "wave.h"
 
 #pragma clang fp contract(off)
@@ -127,6 +128,63 @@ __device__ __forceinline__ void autocorr(const T *__restrict__ src, const double
     }
 }
 
+// Hot path: 16-bit stereo pairs, mid/side candidates, every active lane of
+// the wave on the same frame length N (one shared window, read with scalar
+// loads).  The candidate is one v_dot2 of the (l, r) pair with per-lane
+// weights and a shift: L (1,0)>>0, R (0,1)>>0, mid (1,1)>>1, side (1,-1)>>0.
+// Full groups of K samples use immediate-offset loads; only the last
+// partial group clamps and masks.
+template <int K>
+__device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs,
+                                              const double *__restrict__ win, uint32_t cand,
+                                              uint32_t N, double (&acc)[K], double (&hist)[K])
+{
+    const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
+                       : cand == 2u ? 0x00010001u : 0xFFFF0001u;
+    const int gsh = cand == 2u ? 1 : 0;
+    const uint32_t nfull = N / K * K;
+    uint32_t j0 = 0;
+    for (; j0 < nfull; j0 += K) {
+        double xv[K];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const int v = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pairs[j0 + u]),
+                                                 __builtin_bit_cast(short2_t, wts), 0, false);
+            xv[u] = (double)(v >> gsh) * win[j0 + u];
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const double x = xv[u];
+            hist[u] = x;
+#pragma unroll
+            for (int L = 0; L < K; ++L) {
+                const double prod = hist[(u - L + K) % K] * x;
+                acc[L] = acc[L] + prod;
+            }
+        }
+    }
+    if (j0 < N) {
+        double xv[K];
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const uint32_t j = min(j0 + (uint32_t)u, N - 1u);
+            const int v = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pairs[j]),
+                                                 __builtin_bit_cast(short2_t, wts), 0, false);
+            xv[u] = j0 + (uint32_t)u < N ? (double)(v >> gsh) * win[j] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < K; ++u) {
+            const double x = xv[u];
+            hist[u] = x;
+#pragma unroll
+            for (int L = 0; L < K; ++L) {
+                const double prod = hist[(u - L + K) % K] * x;
+                acc[L] = acc[L] + prod;
+            }
+        }
+    }
+}
+
 template <typename T, int LAGS>
 __global__ __launch_bounds__(64) void k_lpc_analyze(
     FlacParams p, const T *__restrict__ pcm,
@@ -162,7 +220,15 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
     const double *__restrict__ win = windows + fi.win_off;
     const T *__restrict__ src = pcm + fi.pcm_start * p.channels;
     const uint32_t nlast = n_loop ? n_loop - 1u : 0u;
-    switch (pcm_mode(pcm, ms)) {
+    const int mode = pcm_mode(pcm, ms);
+    // uniform frame length over the active lanes -> shared window
+    const uint32_t n_first = uniform_u32(do_lpc ? N : 0u);
+    const bool uniform_n = wave_all(!active || (do_lpc ? N : 0u) == n_first) && n_first > 0u;
+    if (mode == PCM_MS16 && uniform_n) {
+        const double *__restrict__ wu =
+            windows + uniform_u32(active ? fi.win_off : 0u);
+        autocorr_ms16<K>((const uint32_t *)src, wu, cand, n_first, acc, hist);
+    } else switch (mode) {
     case PCM_MS16:
         autocorr<PCM_MS16, T, K>(src, win, p.channels, cand, n_loop, nlast, n_max, acc, hist);
         break;
