@@ -16,7 +16,6 @@ cpu_baseline times the CPU oracle (oracle/flac_port.c) on a bounded sample
 of the same batch on this host's cores.
 """
 import argparse
-import ctypes
 import json
 import os
 import sys
@@ -53,8 +52,16 @@ def parse_args(argv=None):
 
 
 def shard(n_total_ranks, rank, tracks_per_rank):
-    """global track ids owned by `rank` (weak scaling: a full batch per rank)"""
+    """global track ids owned by `rank` (weak scaling: a full batch per rank;
+    tracks are independent, so ranks share nothing on the data path)"""
     return list(range(rank * tracks_per_rank, (rank + 1) * tracks_per_rank))
+
+
+def reduce_max(torch, dist, value, device):
+    """max of a host float over all ranks (the step clock: max over ranks)"""
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
 
 
 def synth_batch(torch, track_ids, n_samples, device):
@@ -170,9 +177,7 @@ def main(argv=None):
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
-        tt = torch.tensor([elapsed], dtype=torch.float64, device=device)
-        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
-        elapsed = float(tt.item())
+        elapsed = reduce_max(torch, dist, elapsed, device)
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     out_bytes = sum(int(r.bytes) for r in res)
     header = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + 4096

@@ -1,0 +1,71 @@
+"""CPU, world_size 2 over gloo: the multi-GPU bench path.  Each rank owns a
+disjoint set of whole tracks (weak scaling, no data-path collective); the
+only collective is the max-over-ranks step clock.  Also checks that two
+ranks encoding their shards produce exactly what one process encoding the
+union produces (tracks are independent), using the oracle on CPU."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        ids = bench.shard(world, rank, 3)
+        import hashlib
+        import oracle_port
+        import signals
+        digests = {}
+        for t in ids:
+            pcm = signals.make("tone", 4096 + 37 * t, 2, 16, seed=t)
+            data, _ = oracle_port.encode(pcm, 2, 16, 44100, **oracle_port.PRESETS["8"])
+            digests[t] = hashlib.sha256(data).hexdigest()
+        elapsed = 1.0 + rank            # rank-specific clock
+        mx = bench.reduce_max(torch, dist, elapsed, torch.device("cpu"))
+        q.put((rank, ids, digests, mx))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_shards_and_clock():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    res.sort()
+    all_ids = [t for _, ids, _, _ in res for t in ids]
+    assert sorted(all_ids) == list(range(6)) and len(set(all_ids)) == 6
+    assert all(mx == 2.0 for _, _, _, mx in res)
+    # union of the shards == single-process encode of every track
+    import hashlib
+    import oracle_port
+    import signals
+    for _, _, digests, _ in res:
+        for t, h in digests.items():
+            pcm = signals.make("tone", 4096 + 37 * t, 2, 16, seed=t)
+            data, _ = oracle_port.encode(pcm, 2, 16, 44100, **oracle_port.PRESETS["8"])
+            assert hashlib.sha256(data).hexdigest() == h
