@@ -1,0 +1,22 @@
+#!/usr/bin/env python3
+"""profiles/pmc_traffic.json from a tools/gpu_pmc.sh run: HBM bytes per
+launch per kernel = FETCH_SIZE x 2 (gfx950 reports half of wide streaming
+reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both KiB -> bytes."""
+import json
+import subprocess
+import sys
+
+src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
+dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
+pmc = json.loads(subprocess.check_output([sys.executable, "tools/pmc_summary.py", src]))
+names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
+         "k_frame_decide": "frame_decide", "k_track_scan": "track_scan",
+         "k_frame_pack": "frame_pack", "k_track_md5": "track_md5",
+         "k_stream_header": "stream_header"}
+out = {}
+for k, v in pmc.items():
+    base = k.split("<")[0]
+    if base in names and "HBM_read_bytes" in v and "HBM_write_bytes" in v:
+        out[names[base]] = int(v["HBM_read_bytes"] + v["HBM_write_bytes"])
+json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
+print(json.dumps(out, indent=1, sort_keys=True))
