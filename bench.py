@@ -44,7 +44,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--tracks", type=int, default=1024)
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
-    ap.add_argument("--cpu-sample-tracks", type=int, default=64)
+    ap.add_argument("--cpu-sample-tracks", type=int, default=128)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -205,11 +205,18 @@ def main(argv=None):
 
     total_frames = n_frames * world * args.steps
     value = total_frames / elapsed
-    # dominant kernel and its roofline (algorithmic bytes: PCM in + FLAC out)
+    # dominant kernel and its roofline.  Algorithmic bytes per launch
+    # (DESIGN.md section 4): every kernel that reads the batch reads its
+    # PCM once (16,384 B per 4096-sample stereo frame); the packer also
+    # writes the compressed frames.
+    pcm_bytes = args.tracks * n_samples * 2 * 2
+    alg = {"lpc_analyze": pcm_bytes, "subframe_search": pcm_bytes,
+           "frame_pack": pcm_bytes + frame_bytes, "track_md5": pcm_bytes,
+           "frame_decide": 0, "track_scan": 0, "stream_header": out_bytes - frame_bytes}
     kernels = {k: v for k, v in kt.items() if k != "total"}
     dom = max(kernels, key=kernels.get)
     dom_ms = kernels[dom]
-    alg_bytes = n_frames * PCM_BYTES_PER_FRAME + frame_bytes
+    alg_bytes = alg.get(dom, pcm_bytes)
     achieved = alg_bytes / (dom_ms / 1e3) / 1e9
     traffic = None
     tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
