@@ -152,11 +152,12 @@ def main(argv=None):
     pcm = synth_batch(torch, ids, n_samples, device)
     tracks = [(i * n_samples, n_samples) for i in range(args.tracks)]
     n_frames, out_cap = eng.bounds(opts, tracks, 2, 16)
+    table = _atgpu.TrackTable(tracks)
     out = torch.empty(out_cap, dtype=torch.uint8, device=device)
     torch.cuda.synchronize()
 
     def step():
-        return eng.encode_device(opts, pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16,
+        return eng.encode_device(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16,
                                  44100, out.data_ptr(), out_cap)
 
     for _ in range(args.warmup):

@@ -162,6 +162,13 @@ def _track_array(tracks):
     return arr, len(tracks), keep
 
 
+class TrackTable(object):
+    """a batch's atg_track array, built once (batches repeat in pipelines)"""
+
+    def __init__(self, tracks):
+        self.arr, self.n, self._keep = _track_array(tracks)
+
+
 class Engine(object):
     """one libatgpu engine (two HIP streams + workspace) on one device"""
 
@@ -222,8 +229,12 @@ class Engine(object):
     def encode_device(self, options, d_pcm, fmt, tracks, channels,
                       bits_per_sample, sample_rate, d_out, out_cap):
         """encode a batch whose PCM is already in device memory; the .flac
-        images stay in device memory at d_out.  Returns the TrackResults."""
-        arr, n, keep = _track_array(tracks)
+        images stay in device memory at d_out.  Returns the TrackResults.
+        `tracks` may be a TrackTable (prepared once, reused across calls)."""
+        if isinstance(tracks, TrackTable):
+            arr, n = tracks.arr, tracks.n
+        else:
+            arr, n, keep = _track_array(tracks)
         res = (TrackResult * max(1, n))()
         _check(self.lib, self.lib.atg_flac_encode_device(
             self.handle, ctypes.byref(options), ctypes.c_void_p(d_pcm), fmt, arr, n,

@@ -117,6 +117,10 @@ struct atg_engine {
     size_t win_uploaded = 0;
     float times[kNumTimed] = {};
     bool have_times = false;
+    // plan cache: a batch with the same geometry as the previous call reuses
+    // the plan and the frame/track tables already on the device
+    std::vector<uint8_t> plan_key, plan_key_pending;
+    void *plan_cached = nullptr; // Plan*
 };
 
 namespace {
@@ -323,8 +327,8 @@ atg_status prepare_windows(atg_engine *e, Plan &pl)
     return ATG_OK;
 }
 
-atg_status run_batch(atg_engine *e, Plan &pl, const void *d_pcm, int fmt, uint8_t *d_out,
-                     uint64_t out_cap, std::vector<TrackOut> &tout_h,
+atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, int fmt,
+                     uint8_t *d_out, uint64_t out_cap, std::vector<TrackOut> &tout_h,
                      std::vector<FrameDesc> *fdesc_h)
 {
     FlacParams &p = pl.p;
@@ -335,9 +339,14 @@ atg_status run_batch(atg_engine *e, Plan &pl, const void *d_pcm, int fmt, uint8_
     if (st != ATG_OK)
         return st;
     const size_t nf = pl.frames.size(), nt = pl.tracks.size();
-    HIP_TRY(e->frames.ensure(nf * sizeof(FrameInfo)));
-    HIP_TRY(e->tracks.ensure(nt * sizeof(TrackInfo)));
-    HIP_TRY(e->order.ensure(nf * sizeof(uint32_t)));
+    {
+        void *f0 = e->frames.p, *t0 = e->tracks.p, *o0 = e->order.p;
+        HIP_TRY(e->frames.ensure(nf * sizeof(FrameInfo)));
+        HIP_TRY(e->tracks.ensure(nt * sizeof(TrackInfo)));
+        HIP_TRY(e->order.ensure(nf * sizeof(uint32_t)));
+        if (f0 != e->frames.p || t0 != e->tracks.p || o0 != e->order.p)
+            upload = true;
+    }
     HIP_TRY(e->coef.ensure(nf * p.n_cand * p.coef_stride * sizeof(int16_t)));
     HIP_TRY(e->shift.ensure(nf * p.n_cand * std::max<uint32_t>(1, p.max_lpc_order)));
     HIP_TRY(e->est.ensure(nf * p.n_cand));
@@ -345,13 +354,13 @@ atg_status run_batch(atg_engine *e, Plan &pl, const void *d_pcm, int fmt, uint8_
     HIP_TRY(e->fdesc.ensure(nf * sizeof(FrameDesc)));
     HIP_TRY(e->tout.ensure(nt * sizeof(TrackOut)));
     HIP_TRY(e->err.ensure(sizeof(uint32_t)));
-    if (nf)
+    if (upload && nf)
         HIP_TRY(hipMemcpyAsync(e->frames.p, pl.frames.data(), nf * sizeof(FrameInfo),
                                hipMemcpyHostToDevice, e->s_main));
-    if (nt)
+    if (upload && nt)
         HIP_TRY(hipMemcpyAsync(e->tracks.p, pl.tracks.data(), nt * sizeof(TrackInfo),
                                hipMemcpyHostToDevice, e->s_main));
-    if (nf)
+    if (upload && nf)
         HIP_TRY(hipMemcpyAsync(e->order.p, pl.order.data(), nf * sizeof(uint32_t),
                                hipMemcpyHostToDevice, e->s_main));
     HIP_TRY(hipMemsetAsync(e->err.p, 0, sizeof(uint32_t), e->s_main));
@@ -454,6 +463,62 @@ void fill_results(const Plan &pl, const std::vector<TrackOut> &to, atg_track_res
     }
 }
 
+std::vector<uint8_t> plan_key(const atg_flac_options *o, const atg_track *tracks,
+                              uint32_t n_tracks, uint32_t channels, uint32_t bps, uint32_t rate)
+{
+    std::vector<uint8_t> k;
+    auto put = [&k](const void *p, size_t n) {
+        const uint8_t *b = (const uint8_t *)p;
+        k.insert(k.end(), b, b + n);
+    };
+    put(o, sizeof(*o));
+    put(&n_tracks, 4);
+    put(&channels, 4);
+    put(&bps, 4);
+    put(&rate, 4);
+    for (uint32_t t = 0; t < n_tracks; ++t) {
+        put(&tracks[t].pcm_offset, 8);
+        put(&tracks[t].pcm_frames, 8);
+        put(&tracks[t].n_frame_sizes, 8);
+        if (tracks[t].frame_sizes)
+            put(tracks[t].frame_sizes, tracks[t].n_frame_sizes * 4);
+    }
+    return k;
+}
+
+// plan for this call: the cached one when the geometry repeats (fresh=false:
+// device tables are current), else a new plan that replaces the cache
+atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *tracks,
+                    uint32_t n_tracks, uint32_t channels, uint32_t bps, uint32_t rate,
+                    Plan *&pl, bool &fresh)
+{
+    std::vector<uint8_t> key = plan_key(o, tracks, n_tracks, channels, bps, rate);
+    if (e->plan_cached && key == e->plan_key) {
+        pl = (Plan *)e->plan_cached;
+        fresh = false;
+        return ATG_OK;
+    }
+    Plan *np = new Plan();
+    atg_status st = make_plan(o, tracks, n_tracks, channels, bps, rate, *np);
+    if (st != ATG_OK) {
+        delete np;
+        return st;
+    }
+    delete (Plan *)e->plan_cached;
+    e->plan_cached = np;
+    e->plan_key.clear();            // valid only once its tables are uploaded
+    e->plan_key_pending.swap(key);  // committed by commit_plan()
+    pl = np;
+    fresh = true;
+    return ATG_OK;
+}
+
+void commit_plan(atg_engine *e, bool fresh)
+{
+    if (fresh)
+        e->plan_key.swap(e->plan_key_pending);
+}
+
 } // namespace
 
 extern "C" {
@@ -503,6 +568,7 @@ void atg_engine_destroy(atg_engine *e)
         (void)hipEventDestroy(ev);
     (void)hipEventDestroy(e->ev_tables);
     (void)hipEventDestroy(e->ev_md5);
+    delete (Plan *)e->plan_cached;
     (void)hipStreamDestroy(e->s_main);
     (void)hipStreamDestroy(e->s_aux);
     delete e;
@@ -533,15 +599,19 @@ atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    Plan pl;
-    atg_status st = make_plan(opts, tracks, n_tracks, channels, bps, rate, pl);
+    Plan *pl = nullptr;
+    bool fresh = true;
+    atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, pl, fresh);
     if (st != ATG_OK)
         return st;
     std::vector<TrackOut> to;
-    st = run_batch(e, pl, d_pcm, (int)format, (uint8_t *)d_out, out_cap, to, nullptr);
-    if (st != ATG_OK)
+    st = run_batch(e, *pl, fresh, d_pcm, (int)format, (uint8_t *)d_out, out_cap, to, nullptr);
+    if (st != ATG_OK) {
+        e->plan_key.clear(); // tables may not be on the device
         return st;
-    fill_results(pl, to, results, nullptr, nullptr, nullptr);
+    }
+    commit_plan(e, fresh);
+    fill_results(*pl, to, results, nullptr, nullptr, nullptr);
     return ATG_OK;
 }
 
@@ -556,12 +626,16 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    Plan pl;
-    atg_status st = make_plan(opts, tracks, n_tracks, channels, bps, rate, pl);
+    Plan *plp = nullptr;
+    bool fresh = true;
+    atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, plp, fresh);
     if (st != ATG_OK)
         return st;
-    if (pl.out_bytes > out_cap)
+    Plan &pl = *plp;
+    if (pl.out_bytes > out_cap) {
+        e->plan_key.clear();
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
+    }
     uint64_t samples = 0;
     for (uint32_t t = 0; t < n_tracks; ++t)
         samples = std::max<uint64_t>(samples, (tracks[t].pcm_offset + tracks[t].pcm_frames) *
@@ -575,15 +649,19 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
                                e->s_main));
     std::vector<TrackOut> to;
     std::vector<FrameDesc> fd;
-    st = run_batch(e, pl, e->h_pcm.p, (int)format, (uint8_t *)e->h_out.p, e->h_out.cap, to, &fd);
-    if (st != ATG_OK)
+    st = run_batch(e, pl, fresh, e->h_pcm.p, (int)format, (uint8_t *)e->h_out.p, e->h_out.cap,
+                   to, &fd);
+    if (st != ATG_OK) {
+        e->plan_key.clear(); // tables may not be on the device
         return st;
+    }
     for (size_t t = 0; t < pl.tracks.size(); ++t)
         if (to[t].bytes)
             HIP_TRY(hipMemcpyAsync(out + pl.tracks[t].out_base,
                                    (uint8_t *)e->h_out.p + pl.tracks[t].out_base, to[t].bytes,
                                    hipMemcpyDeviceToHost, e->s_main));
     HIP_TRY(hipStreamSynchronize(e->s_main));
+    commit_plan(e, fresh);
     fill_results(pl, to, results, &fd, frame_offsets, frame_pcm_frames);
     return ATG_OK;
 }

@@ -134,7 +134,7 @@ __device__ __forceinline__ void autocorr(const T *__restrict__ src, const double
 // weights and a shift: L (1,0)>>0, R (0,1)>>0, mid (1,1)>>1, side (1,-1)>>0.
 // Full groups of K samples use immediate-offset loads; only the last
 // partial group clamps and masks.
-template <int K>
+template <int K, bool VEC4>
 __device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs,
                                               const double *__restrict__ win, uint32_t cand,
                                               uint32_t N, double (&acc)[K], double (&hist)[K])
@@ -144,6 +144,42 @@ __device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs
     const int gsh = cand == 2u ? 1 : 0;
     const uint32_t nfull = N / K * K;
     uint32_t j0 = 0;
+    if (VEC4) {
+        // groups of 4K samples: 13 dwordx4 loads (4 pairs each) per lane
+        const uint4 *__restrict__ q4 = (const uint4 *)pairs;
+        for (; j0 + 4u * K <= N; j0 += 4u * K) {
+            uint32_t pv[4 * K];
+#pragma unroll
+            for (int i = 0; i < K; ++i) {
+                const uint4 v = q4[(j0 >> 2) + (uint32_t)i];
+                pv[4 * i] = v.x;
+                pv[4 * i + 1] = v.y;
+                pv[4 * i + 2] = v.z;
+                pv[4 * i + 3] = v.w;
+            }
+#pragma unroll
+            for (int sub = 0; sub < 4; ++sub) {
+                double xv[K];
+#pragma unroll
+                for (int u = 0; u < K; ++u) {
+                    const int v = __builtin_amdgcn_sdot2(
+                        __builtin_bit_cast(short2_t, pv[sub * K + u]),
+                        __builtin_bit_cast(short2_t, wts), 0, false);
+                    xv[u] = (double)(v >> gsh) * win[j0 + (uint32_t)(sub * K + u)];
+                }
+#pragma unroll
+                for (int u = 0; u < K; ++u) {
+                    const double x = xv[u];
+                    hist[u] = x;
+#pragma unroll
+                    for (int L = 0; L < K; ++L) {
+                        const double prod = hist[(u - L + K) % K] * x;
+                        acc[L] = acc[L] + prod;
+                    }
+                }
+            }
+        }
+    }
     for (; j0 < nfull; j0 += K) {
         double xv[K];
 #pragma unroll
@@ -227,7 +263,12 @@ __global__ __launch_bounds__(64) void k_lpc_analyze(
     if (mode == PCM_MS16 && uniform_n) {
         const double *__restrict__ wu =
             windows + uniform_u32(active ? fi.win_off : 0u);
-        autocorr_ms16<K>((const uint32_t *)src, wu, cand, n_first, acc, hist);
+        // 16-byte aligned frame starts in every lane: 4 pairs per load
+        const bool al16 = wave_all(((uintptr_t)src & 15u) == 0u);
+        if (al16)
+            autocorr_ms16<K, true>((const uint32_t *)src, wu, cand, n_first, acc, hist);
+        else
+            autocorr_ms16<K, false>((const uint32_t *)src, wu, cand, n_first, acc, hist);
     } else switch (mode) {
     case PCM_MS16:
         autocorr<PCM_MS16, T, K>(src, win, p.channels, cand, n_loop, nlast, n_max, acc, hist);
