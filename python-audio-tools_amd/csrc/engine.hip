@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <string>
@@ -371,19 +372,22 @@ atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, in
     TrackOut *dto = (TrackOut *)e->tout.p;
     uint32_t *derr = (uint32_t *)e->err.p;
 
-    // MD5 chain on the aux stream, concurrent with the encoder
-    HIP_TRY(hipStreamWaitEvent(e->s_aux, e->ev_tables, 0));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5], e->s_aux));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, e->s_aux));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5 + 1], e->s_aux));
-    HIP_TRY(hipEventRecord(e->ev_md5, e->s_aux));
-
     HIP_TRY(hipEventRecord(e->ev[14], e->s_main));
     HIP_TRY(hipEventRecord(e->ev[0], e->s_main));
     HIP_TRY(launch_lpc_analyze(p, d_pcm, fmt, dfr, (const double *)e->windows.p,
                                (int16_t *)e->coef.p, (int8_t *)e->shift.p,
                                (uint8_t *)e->est.p, e->s_main));
     HIP_TRY(hipEventRecord(e->ev[1], e->s_main));
+    // MD5 chains on the aux stream, concurrent with the search and pack
+    // kernels.  They start after the LPC kernel: its grid is only ~1.3
+    // waves per SIMD deep, so a SIMD shared with a (high-priority) chain
+    // would leave straggler waves; the search/pack grids are >60 deep and
+    // absorb it.
+    HIP_TRY(hipStreamWaitEvent(e->s_aux, e->ev[1], 0));
+    HIP_TRY(hipEventRecord(e->ev[2 * 5], e->s_aux));
+    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, e->s_aux));
+    HIP_TRY(hipEventRecord(e->ev[2 * 5 + 1], e->s_aux));
+    HIP_TRY(hipEventRecord(e->ev_md5, e->s_aux));
     HIP_TRY(hipEventRecord(e->ev[2], e->s_main));
     HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)e->coef.p,
                                    (const int8_t *)e->shift.p, (const uint8_t *)e->est.p,

@@ -81,27 +81,47 @@ struct PartSel {
     uint32_t hdr_bits;
 };
 
-// Estimated bits of one partition (flac.c:1437-1505), 64-bit as the
-// reference's accumulator.
-__device__ __forceinline__ uint64_t part_estimate(uint32_t plen, uint64_t sum, uint32_t k)
+// wave primitives on 32- or 64-bit values
+__device__ __forceinline__ uint32_t wshfl_up(uint32_t v, int d)
+{
+    return (uint32_t)__shfl_up((int)v, d, 64);
+}
+__device__ __forceinline__ uint64_t wshfl_up(uint64_t v, int d) { return shfl_up_u64(v, d); }
+__device__ __forceinline__ uint32_t wshfl(uint32_t v, int src)
+{
+    return (uint32_t)__shfl((int)v, src, 64);
+}
+__device__ __forceinline__ uint64_t wshfl(uint64_t v, int src) { return shfl_u64(v, src); }
+__device__ __forceinline__ uint32_t wshfl_xor(uint32_t v, int m) { return shfl_xor_u32(v, m); }
+__device__ __forceinline__ uint64_t wshfl_xor(uint64_t v, int m) { return shfl_xor_u64(v, m); }
+__device__ __forceinline__ uint32_t wreadlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t wreadlane(uint64_t v, int l) { return readlane_u64(v, l); }
+
+// Estimated bits of one partition (flac.c:1437-1505).  S = uint64_t is the
+// reference's accumulator; S = uint32_t gives the same values whenever the
+// subframe's sum |r| < 2^31 (then no term or total reaches 2^32).
+template <typename S>
+__device__ __forceinline__ S part_estimate(uint32_t plen, S sum, uint32_t k)
 {
     if (k > 0)
-        return 4ull + (sum >> (k - 1)) + (uint64_t)(uint32_t)((1u + k) * plen) -
-               (uint64_t)(plen / 2u);
-    return 4ull + (sum << 1) + (uint64_t)plen - (uint64_t)(plen / 2u);
+        return (S)4u + (sum >> (k - 1)) + (S)(uint32_t)((1u + k) * plen) - (S)(plen / 2u);
+    return (S)4u + (sum << 1) + (S)plen - (S)(plen / 2u);
 }
 
 // Rice parameter and estimate of partition j at level lv (sum = its |r| sum)
-__device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, uint64_t S, uint64_t total,
-                                          uint32_t order, const RunCtx &c, uint32_t &k,
-                                          uint64_t &e)
+template <typename S>
+__device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, S Sj, S total,
+                                          uint32_t order, const RunCtx &c, uint32_t &k, S &e)
 {
     const uint32_t Sp = c.N >> lv;
     const bool degen = Sp < order; // partition 0 takes every residual
     const uint32_t plen = j == 0 ? Sp - order : Sp;
-    const uint64_t sum = degen ? (j == 0 ? total : 0ull) : S;
-    k = rice_param(plen, sum, c.max_rice);
-    e = part_estimate(plen, sum, k);
+    const S sum = degen ? (j == 0 ? total : (S)0) : Sj;
+    k = rice_param(plen, (uint64_t)sum, c.max_rice);
+    e = part_estimate<S>(plen, sum, k);
 }
 
 // flacenc_encode_residuals' partition-order search (flac.c:1362-1402) from
@@ -115,20 +135,18 @@ __device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, uint64_t S, u
 // Partition sums come from one inclusive prefix scan of the lane sums; the
 // level totals from a full butterfly (A) and a segmented one (B) whose
 // segments are aligned to their power-of-two sizes.
-__device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order, const RunCtx &c)
+template <typename S>
+__device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t order,
+                                                       const RunCtx &c)
 {
-#if ATG_EXP == 2
-    { PartSel r; r.porder = 6; r.method = 0; r.k_own = r.k_lane = (uint32_t)(lane_sum >> 6) & 7u;
-      r.hdr_bits = 6u + 64u * 4u; return r; }
-#endif
     const int lane = c.lane;
-    uint64_t pre = lane_sum;
+    S pre = lane_sum;
 #pragma unroll
     for (int d = 1; d < 64; d <<= 1) {
-        const uint64_t t = shfl_up_u64(pre, d);
-        pre += lane >= d ? t : 0ull;
+        const S t = wshfl_up(pre, d);
+        pre += lane >= d ? t : (S)0;
     }
-    const uint64_t total = readlane_u64(pre, 63);
+    const S total = wreadlane(pre, 63);
 
     const uint32_t lvB = lane < 32 ? 5u : lane < 48 ? 4u : lane < 56 ? 3u
                        : lane < 60 ? 2u : lane < 62 ? 1u : 0u;
@@ -136,29 +154,29 @@ __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t
     const uint32_t jB = (uint32_t)lane - offB;
     const uint32_t wB = 64u >> lvB; // lanes per partition at level lvB
     const int first = (int)((jB * wB) & 63u), last = (int)((jB * wB + wB - 1u) & 63u);
-    const uint64_t p_last = shfl_u64(pre, last);
-    const uint64_t p_prev = shfl_u64(pre, (first + 63) & 63);
-    const uint64_t SB = p_last - (first ? p_prev : 0ull);
+    const S p_last = wshfl(pre, last);
+    const S p_prev = wshfl(pre, (first + 63) & 63);
+    const S SB = p_last - (first ? p_prev : (S)0);
 
     uint32_t kA, kB;
-    uint64_t eA, eB;
-    part_eval(6, (uint32_t)lane, lane_sum, total, order, c, kA, eA);
-    part_eval(lvB, jB, SB, total, order, c, kB, eB);
+    S eA, eB;
+    part_eval<S>(6, (uint32_t)lane, lane_sum, total, order, c, kA, eA);
+    part_eval<S>(lvB, jB, SB, total, order, c, kB, eB);
 #pragma unroll
     for (int m = 1; m < 64; m <<= 1)
-        eA += shfl_xor_u64(eA, m);
+        eA += wshfl_xor(eA, m);
     const uint32_t segB = lane == 63 ? 1u : (1u << lvB);
 #pragma unroll
     for (int m = 1; m < 32; m <<= 1) {
-        const uint64_t o = shfl_xor_u64(eB, m);
-        eB += (uint32_t)m < segB ? o : 0ull;
+        const S o = wshfl_xor(eB, m);
+        eB += (uint32_t)m < segB ? o : (S)0;
     }
 
-    uint64_t best_tot = ~0ull;
+    S best_tot = (S)~(S)0;
     uint32_t best_p = 0;
 #pragma unroll
     for (int lv = 0; lv <= 6; ++lv) {
-        const uint64_t T = lv == 6 ? readlane_u64(eA, 0) : readlane_u64(eB, 64 - (2 << lv));
+        const S T = lv == 6 ? wreadlane(eA, 0) : wreadlane(eB, 64 - (2 << lv));
         if (lv <= c.P && T < best_tot) {
             best_tot = T;
             best_p = (uint32_t)lv;
@@ -182,6 +200,19 @@ __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t
     return r;
 }
 
+// `small`: the subframe's sum |r| is known to be < 2^31 (32-bit search)
+__device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order,
+                                                     const RunCtx &c, bool small = false)
+{
+#if ATG_EXP == 2
+    { PartSel r; r.porder = 6; r.method = 0; r.k_own = r.k_lane = (uint32_t)(lane_sum >> 6) & 7u;
+      r.hdr_bits = 6u + 64u * 4u; return r; }
+#endif
+    if (small)
+        return select_partitions_t<uint32_t>((uint32_t)lane_sum, order, c);
+    return select_partitions_t<uint64_t>(lane_sum, order, c);
+}
+
 struct Eval {
     uint32_t bits;    // residual section bits
     PartSel sel;
@@ -197,16 +228,18 @@ __device__ __forceinline__ int dot2_first(int a, int b_uniform)
 
 // Hot path (N = 4096, samples fit int16, |u| < 2^26): residuals of the
 // lane's 64-sample run with TAPS taps (the order rounded up to even),
-// v_dot2 on packed sample pairs.  Sums are kept in 32 bits, two samples
-// per v_add3:  su = sum u (zig-zag codes), sn = -#(r < 0); the reference's
-// sum |r| is then (su + #neg) / 2 exactly, since |r| = (u + (u & 1)) / 2.
-// Warm-up positions (lane 0, t < order) are masked to u = 0.
+// v_dot2 on packed sample pairs.  Keeps v = r ^ (r >> 31) = |r| - [r < 0]
+// per sample instead of the zig-zag code u = 2v + [r < 0]: |r| = v + [r<0]
+// and u >> k = v >> (k - 1) for k >= 1, so the partition search and the
+// exact bit count need only v, sum v and #neg.  Sums are 32-bit, two
+// samples per v_add3.  Warm-up positions (lane 0, t < order) are masked.
 template <int TAPS>
 __device__ __forceinline__ uint64_t residuals_full_dot2(const int32_t *__restrict__ sl,
                                                         const RunCtx &c,
                                                         const int (&cfu)[ATG_FAST_ORDER],
                                                         int order, int shift,
-                                                        uint32_t (&u)[ATG_RUN])
+                                                        uint32_t (&u)[ATG_RUN], uint32_t &sv,
+                                                        uint32_t &nneg)
 {
     constexpr int NP = TAPS / 2;
     constexpr int W = ATG_FAST_ORDER;
@@ -268,23 +301,25 @@ __device__ __forceinline__ uint64_t residuals_full_dot2(const int32_t *__restric
             prev = s;
             const int r = (int)((uint32_t)s - (uint32_t)(acc >> shift));
             uint32_t neg = (uint32_t)(r >> 31);
-            uint32_t uu = ((uint32_t)r << 1) ^ neg;
+            uint32_t vv = (uint32_t)r ^ neg; // |r| - [r < 0]
             if (t < W) {
                 const bool w = t < warm;
-                uu = w ? 0u : uu;
+                vv = w ? 0u : vv;
                 neg = w ? 0u : neg;
             }
-            u[t] = uu;
+            u[t] = vv;
             if (tt & 1) {
-                su = su + pu + uu; // v_add3_u32
+                su = su + pu + vv; // v_add3_u32
                 sn = sn + pn + neg;
             } else {
-                pu = uu;
+                pu = vv;
                 pn = neg;
             }
         }
     }
-    return ((uint64_t)su + (uint64_t)(0u - sn)) >> 1;
+    sv = su;
+    nneg = 0u - sn;
+    return (uint64_t)su + (uint64_t)nneg;
 }
 
 // Other fast cases: 12 taps (residual.h), 64-bit |r| sums, warm-up dropped
@@ -349,15 +384,18 @@ __device__ __forceinline__ Eval eval_fast_any(const int32_t *sl, const RunCtx &c
     const bool sum32 = 2u * rbound + 1u < (1ull << 26);
     uint32_t u[ATG_RUN];
     uint64_t sum;
+    bool vform = false;      // u[] holds v = |r| - [r<0] instead of zig-zag codes
+    uint32_t sv = 0, nneg = 0;
     if (kind == RES_DOT2 && full && sum32) {
+        vform = true;
         switch ((order + 1) >> 1) {
         case 0:
-        case 1: sum = residuals_full_dot2<2>(sl, c, cfu, order, shift, u); break;
-        case 2: sum = residuals_full_dot2<4>(sl, c, cfu, order, shift, u); break;
-        case 3: sum = residuals_full_dot2<6>(sl, c, cfu, order, shift, u); break;
-        case 4: sum = residuals_full_dot2<8>(sl, c, cfu, order, shift, u); break;
-        case 5: sum = residuals_full_dot2<10>(sl, c, cfu, order, shift, u); break;
-        default: sum = residuals_full_dot2<12>(sl, c, cfu, order, shift, u); break;
+        case 1: sum = residuals_full_dot2<2>(sl, c, cfu, order, shift, u, sv, nneg); break;
+        case 2: sum = residuals_full_dot2<4>(sl, c, cfu, order, shift, u, sv, nneg); break;
+        case 3: sum = residuals_full_dot2<6>(sl, c, cfu, order, shift, u, sv, nneg); break;
+        case 4: sum = residuals_full_dot2<8>(sl, c, cfu, order, shift, u, sv, nneg); break;
+        case 5: sum = residuals_full_dot2<10>(sl, c, cfu, order, shift, u, sv, nneg); break;
+        default: sum = residuals_full_dot2<12>(sl, c, cfu, order, shift, u, sv, nneg); break;
         }
     } else if (kind == RES_DOT2) {
         sum = full ? residuals_fast<true, true>(sl, c, cfu, order, shift, u)
@@ -369,16 +407,24 @@ __device__ __forceinline__ Eval eval_fast_any(const int32_t *sl, const RunCtx &c
     const int warm = min(max(order - c.a, 0), c.len);
     const int cnt = c.len - warm;
     Eval ev;
-    ev.sel = select_partitions(sum, (uint32_t)order, c);
+    // every lane's sum |r| < 2^25 -> the subframe's < 2^31: 32-bit search
+    const bool small = wave_all(sum < (1ull << 25));
+    ev.sel = select_partitions(sum, (uint32_t)order, c, small);
     const uint32_t k = ev.sel.k_lane;
     uint32_t lb = (uint32_t)cnt * (1u + k);
-#if ATG_EXP == 4
-    lb += u[(k + 3) & 63];
-#else
+    if (vform) {
+        // k = 0: sum u = 2 sum v + #neg;  k >= 1: sum (v >> (k - 1))
+        const uint32_t kv = k ? k - 1u : 0u;
+        uint32_t sh = 0;
 #pragma unroll
-    for (int t = 0; t < ATG_RUN; t += 2)
-        lb = lb + (u[t] >> k) + (u[t + 1] >> k); // v_add3_u32
-#endif
+        for (int t = 0; t < ATG_RUN; t += 2)
+            sh = sh + (u[t] >> kv) + (u[t + 1] >> kv); // v_add3_u32
+        lb += k ? sh : 2u * sv + nneg;
+    } else {
+#pragma unroll
+        for (int t = 0; t < ATG_RUN; t += 2)
+            lb = lb + (u[t] >> k) + (u[t + 1] >> k); // v_add3_u32
+    }
     ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
     return ev;
 }
