@@ -134,6 +134,7 @@ struct Plan {
     std::vector<uint32_t> order;           // track-order position -> frame id
     uint64_t frame_bound = 0;               // worst-case frame bytes
     uint64_t out_bytes = 0;
+    uint32_t n_reg_prefix = 0; // leading frame ids of 4096 samples at 4-frame-aligned starts
 };
 
 uint32_t qlp_precision_for(uint32_t n)
@@ -280,6 +281,13 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
     }
     p.n_frames = (uint32_t)pl.frames.size();
     pl.out_bytes = out;
+    // register-staged packer (K5): 16-bit stereo mid/side, 4096-sample
+    // frames whose first pair is 16-byte aligned (with an aligned base)
+    pl.n_reg_prefix = 0;
+    if (channels == 2 && p.n_cand == 4 && bps <= 16 && B == ATG_MAX_BLOCK)
+        while (pl.n_reg_prefix < p.n_frames && pl.frames[pl.n_reg_prefix].n == ATG_MAX_BLOCK &&
+               (pl.frames[pl.n_reg_prefix].pcm_start & 3u) == 0)
+            pl.n_reg_prefix++;
     return ATG_OK;
 }
 
@@ -335,6 +343,7 @@ atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, in
     FlacParams &p = pl.p;
     if (pl.out_bytes > out_cap)
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
+    p.n_reg_frames = (fmt == ATG_PCM_S16 && ((uintptr_t)d_pcm & 15u) == 0) ? pl.n_reg_prefix : 0u;
     HIP_TRY(hipSetDevice(e->device));
     atg_status st = prepare_windows(e, pl);
     if (st != ATG_OK)

@@ -43,6 +43,7 @@ struct FlacParams {
     uint32_t n_tracks;
     uint32_t coef_stride;    // int16 entries per candidate in the lpc table
     uint32_t coef_row;       // int16 entries per order row (even; zero past the order)
+    uint32_t n_reg_frames;   // leading frames the register-staged packer takes (see K5)
     uint32_t padding_size;
     uint32_t header_bytes;   // bytes before the first frame of every track
     uint32_t frame_lds_words;// pack kernel frame buffer (32-bit words)

@@ -332,18 +332,23 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
             w.put(u[t] >> k, k + 1u, (1u << k) | (u[t] & kmask));
 }
 
-template <typename T>
+// REG = false: samples staged in LDS (any frame).  REG = true: the lane's
+// 64-sample run (+16 predecessors) held in VGPRs, read as 16-bit stereo
+// pairs with 16-byte loads: no sample LDS, twice the occupancy.  Used for
+// the leading full-length (4096) frames of a 16-bit mid/side batch whose
+// frame starts are 16-byte aligned (engine.hip counts them: n_reg_frames).
+template <typename T, bool REG>
 __global__ __launch_bounds__(64) void k_frame_pack(
-    FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
+    FlacParams p, uint32_t f0, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
 {
     extern __shared__ __attribute__((aligned(16))) uint32_t fb[];
-    __shared__ __attribute__((aligned(16))) int32_t sl[SL_WORDS];
+    __shared__ __attribute__((aligned(16))) int32_t sl[REG ? 4 : SL_WORDS];
     __shared__ int32_t cfs[ATG_MAX_LPC];
-    __shared__ uint32_t crc_tab[4][256];
+    __shared__ uint16_t crc_tab[4][256];
 
-    const uint32_t f = blockIdx.x;
+    const uint32_t f = f0 + blockIdx.x;
     const int lane = threadIdx.x;
     const FrameInfo fi = frames[f];
     const FrameDesc &fd = fdesc[f]; // by reference: hdr[]/sub[] indexed per lane
@@ -354,15 +359,16 @@ __global__ __launch_bounds__(64) void k_frame_pack(
     for (uint32_t i = lane; i < words; i += 64)
         fb[i] = 0;
     for (uint32_t i = lane; i < 1024u; i += 64)
-        (&crc_tab[0][0])[i] = (&c_crc16[0][0])[i];
-    for (int i = lane; i < SL_PRE; i += 64)
-        sl[i] = 0;
+        (&crc_tab[0][0])[i] = (uint16_t)(&c_crc16[0][0])[i];
+    if (!REG)
+        for (int i = lane; i < SL_PRE; i += 64)
+            sl[i] = 0;
     __syncthreads();
     if (lane < fd.hdr_len)
         put_bits(fb, 8u * lane, 8, fd.hdr[lane]);
     uint32_t pos = 8u * fd.hdr_len;
 
-    // lane run mapping (same as the search kernel)
+    // lane run mapping (same as the search kernel; REG: N = 4096 -> 64l..64l+63)
     const uint32_t tz = N ? (uint32_t)__builtin_ctz(N) : 0u;
     uint32_t P = p.max_porder < tz ? p.max_porder : tz;
     P = P > ATG_MAX_PORDER ? ATG_MAX_PORDER : P;
@@ -373,19 +379,56 @@ __global__ __launch_bounds__(64) void k_frame_pack(
     ra = ra < re ? ra : re;
     const int len = (int)(re - ra);
 
+    // REG: the frame's 16-bit stereo pairs for samples [ra - 16, ra + 64)
+    uint32_t pr[80];
+    if (REG) {
+        const uint4 *q4 = (const uint4 *)((const uint32_t *)pcm + fi.pcm_start);
+        const int b4 = ((int)ra - 16) / 4;
+#pragma unroll
+        for (int q = 0; q < 20; ++q) {
+            const uint4 v = q4[max(b4 + q, 0)];
+            const bool ok = b4 + q >= 0;
+            pr[4 * q] = ok ? v.x : 0u;
+            pr[4 * q + 1] = ok ? v.y : 0u;
+            pr[4 * q + 2] = ok ? v.z : 0u;
+            pr[4 * q + 3] = ok ? v.w : 0u;
+        }
+    }
+
     for (uint32_t si = 0; si < fd.nsub; ++si) {
         const uint32_t cand = fd.sub[si];
         const SubDesc &d = sub[(size_t)f * p.n_cand + cand];
         const uint32_t type = d.type, order = d.order, w = d.wasted, sbps = d.sbps;
         const uint32_t start = pos;
         uint32_t maxabs = 0;
-        stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
-                            [&](uint32_t i, int32_t s) {
-                                s >>= w;
-                                sl[saddr((int)i)] = s;
-                                maxabs = max(maxabs, iabs_u(s));
-                            });
+        int xs[80];
+        if (REG) {
+            const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
+                               : cand == 2u ? 0x00010001u : 0xFFFF0001u;
+            const int gsh = cand == 2u ? 1 : 0;
+#pragma unroll
+            for (int i = 0; i < 80; ++i) {
+                const int v = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr[i]),
+                                                     __builtin_bit_cast(short2_t, wts), 0, false);
+                xs[i] = (v >> gsh) >> w;
+                if (i >= 16)
+                    maxabs = max(maxabs, iabs_u(xs[i]));
+            }
+        } else {
+            stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
+                                [&](uint32_t i, int32_t s) {
+                                    s >>= w;
+                                    sl[saddr((int)i)] = s;
+                                    maxabs = max(maxabs, iabs_u(s));
+                                });
+        }
         maxabs = wave_max_u32(maxabs);
+        // sample i of this subframe (generic paths; REG reads PCM directly)
+        auto sample = [&](int i) -> int32_t {
+            if (REG)
+                return i < 0 ? 0 : cand_sample(pcm, fi.pcm_start + (uint32_t)i, p.channels, cand, ms) >> w;
+            return sl[saddr(i)];
+        };
         if (lane < (int)order) {
             int c;
             if (type == SF_LPC)
@@ -399,10 +442,13 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         }
         __syncthreads();
         const uint32_t rb = sbps - w;
+        const uint32_t rmask = rb >= 32u ? 0xFFFFFFFFu : (1u << rb) - 1u;
         if (type == SF_CONSTANT) {
             // 8 zero header bits, then the raw first sample (flac.c:813-830)
+            const uint32_t s0 = REG ? (uint32_t)__builtin_amdgcn_readfirstlane(xs[16])
+                                    : (uint32_t)sl[saddr(0)];
             if (lane == 0)
-                put_bits(fb, pos + 8u, sbps, (uint32_t)sl[saddr(0)]);
+                put_bits(fb, pos + 8u, sbps, s0);
             pos += 8u + sbps;
         } else {
             const uint32_t code = type == SF_VERBATIM ? 1u
@@ -413,17 +459,34 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                     put_bits(fb, pos + 7u, w + 1u, (1u << w) | 1u);
             }
             const uint32_t hb = 7u + (w ? w + 1u : 1u);
-            const uint32_t rmask = rb >= 32u ? 0xFFFFFFFFu : (1u << rb) - 1u;
             if (type == SF_VERBATIM) {
                 LaneWriter wr;
                 wr.begin(fb, pos + hb + ra * rb);
-                for (int t = 0; t < len; ++t)
-                    wr.put(0, rb, (uint32_t)sl[saddr((int)ra + t)] & rmask);
+                if (REG) {
+#pragma unroll
+                    for (int t = 0; t < 64; ++t)
+                        wr.put(0, rb, (uint32_t)xs[16 + t] & rmask);
+                } else {
+                    for (int t = 0; t < len; ++t)
+                        wr.put(0, rb, (uint32_t)sl[saddr((int)ra + t)] & rmask);
+                }
                 wr.end();
                 pos += hb + N * rb;
             } else {
-                if ((uint32_t)lane < order)
+                // warm-up samples
+                if (REG) {
+                    if (lane == 0) {
+                        LaneWriter ww;
+                        ww.begin(fb, pos + hb);
+#pragma unroll
+                        for (int j = 0; j < ATG_MAX_LPC; ++j)
+                            if ((uint32_t)j < order)
+                                ww.put(0, rb, (uint32_t)xs[16 + j] & rmask);
+                        ww.end();
+                    }
+                } else if ((uint32_t)lane < order) {
                     put_bits(fb, pos + hb + lane * rb, rb, (uint32_t)sl[saddr(lane)]);
+                }
                 uint32_t q = pos + hb + order * rb;
                 int shift = 0;
                 if (type == SF_LPC) {
@@ -461,15 +524,27 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                     for (int j = 0; j < ATG_FAST_ORDER; ++j)
                         cf[j] = uniform_i32(j < (int)order ? cfs[j] : 0);
                     uint32_t u[ATG_RUN];
-                    uint64_t asum;
-                    const bool full = N == ATG_MAX_BLOCK;
-                    if (kind == RES_DOT2)
-                        asum = full ? lane_residuals<true, true>(sl, (int)ra, len, cf, shift, u)
-                                    : lane_residuals<true, false>(sl, (int)ra, len, cf, shift, u);
-                    else
-                        asum = full ? lane_residuals<false, true>(sl, (int)ra, len, cf, shift, u)
-                                    : lane_residuals<false, false>(sl, (int)ra, len, cf, shift, u);
-                    const int warm = drop_warmup((int)ra, len, (int)order, u, asum);
+                    int warm;
+                    if (REG) {
+                        if (kind == RES_DOT2)
+                            lane_residuals_regs<true>(xs, cf, shift, u);
+                        else
+                            lane_residuals_regs<false>(xs, cf, shift, u);
+                        warm = lane == 0 ? (int)order : 0;
+#pragma unroll
+                        for (int t = 0; t < ATG_FAST_ORDER; ++t)
+                            u[t] = t < warm ? 0u : u[t];
+                    } else {
+                        uint64_t asum;
+                        const bool full = N == ATG_MAX_BLOCK;
+                        if (kind == RES_DOT2)
+                            asum = full ? lane_residuals<true, true>(sl, (int)ra, len, cf, shift, u)
+                                        : lane_residuals<true, false>(sl, (int)ra, len, cf, shift, u);
+                        else
+                            asum = full ? lane_residuals<false, true>(sl, (int)ra, len, cf, shift, u)
+                                        : lane_residuals<false, false>(sl, (int)ra, len, cf, shift, u);
+                        warm = drop_warmup((int)ra, len, (int)order, u, asum);
+                    }
                     uint32_t cb = (uint32_t)(len - warm) * (1u + k);
 #pragma unroll
                     for (int t = 0; t < ATG_RUN; ++t)
@@ -488,9 +563,8 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                     for (int i = i0; i < (int)re; ++i) {
                         int64_t acc = 0;
                         for (uint32_t j = 0; j < order; ++j)
-                            acc += (int64_t)cfs[j] * (int64_t)sl[saddr(i - 1 - (int)j)];
-                        const int r = (int)((uint32_t)sl[saddr(i)] -
-                                            (uint32_t)(int32_t)(acc >> shift));
+                            acc += (int64_t)cfs[j] * (int64_t)sample(i - 1 - (int)j);
+                        const int r = (int)((uint32_t)sample(i) - (uint32_t)(int32_t)(acc >> shift));
                         cb += (zigzag(r) >> k) + 1u + k;
                     }
                     excl = wave_excl_scan_u32(cb, lane);
@@ -503,9 +577,8 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                     for (int i = i0; i < (int)re; ++i) {
                         int64_t acc = 0;
                         for (uint32_t j = 0; j < order; ++j)
-                            acc += (int64_t)cfs[j] * (int64_t)sl[saddr(i - 1 - (int)j)];
-                        const int r = (int)((uint32_t)sl[saddr(i)] -
-                                            (uint32_t)(int32_t)(acc >> shift));
+                            acc += (int64_t)cfs[j] * (int64_t)sample(i - 1 - (int)j);
+                        const int r = (int)((uint32_t)sample(i) - (uint32_t)(int32_t)(acc >> shift));
                         const uint32_t uu = zigzag(r);
                         wr.put(uu >> k, k + 1u, (1u << k) | (uu & kmask));
                     }
@@ -672,11 +745,18 @@ hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
     if (!p.n_frames)
         return hipSuccess;
     const size_t lds = (size_t)p.frame_lds_words * 4u;
+    const uint32_t nreg = fmt == 0 ? p.n_reg_frames : 0u;
+    if (nreg)
+        hipLaunchKernelGGL((k_frame_pack<int16_t, true>), dim3(nreg), dim3(64), lds, s, p, 0u,
+                           (const int16_t *)pcm, frames, tracks, sub, fd, out, err);
+    const uint32_t rest = p.n_frames - nreg;
+    if (rest == 0)
+        return hipGetLastError();
     if (fmt == 0)
-        hipLaunchKernelGGL((k_frame_pack<int16_t>), dim3(p.n_frames), dim3(64), lds, s, p,
+        hipLaunchKernelGGL((k_frame_pack<int16_t, false>), dim3(rest), dim3(64), lds, s, p, nreg,
                            (const int16_t *)pcm, frames, tracks, sub, fd, out, err);
     else
-        hipLaunchKernelGGL((k_frame_pack<int32_t>), dim3(p.n_frames), dim3(64), lds, s, p,
+        hipLaunchKernelGGL((k_frame_pack<int32_t, false>), dim3(rest), dim3(64), lds, s, p, nreg,
                            (const int32_t *)pcm, frames, tracks, sub, fd, out, err);
     return hipGetLastError();
 }

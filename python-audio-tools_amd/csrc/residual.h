@@ -217,3 +217,54 @@ __device__ __forceinline__ void stage_candidate_any(const T *__restrict__ pcm, u
     default: stage_candidate<PCM_CH>(src, N, ch, cand, lane, f); break;
     }
 }
+
+// Register-staged variant of lane_residuals for a full 64-sample run:
+// xs[i] = sample (a - 16 + i), i.e. xs[16] is the run's first sample and
+// xs[3..15] its 13 predecessors.  Writes zig-zag codes only.
+template <bool DOT2>
+__device__ __forceinline__ void lane_residuals_regs(const int (&xs)[80],
+                                                    const int (&cf)[ATG_FAST_ORDER], int shift,
+                                                    uint32_t (&u)[ATG_RUN])
+{
+    constexpr int W = ATG_FAST_ORDER;
+    int cp[W / 2];
+#pragma unroll
+    for (int j = 0; j < W / 2; ++j)
+        cp[j] = uniform_i32((int)(((uint32_t)cf[2 * j] & 0xFFFFu) |
+                                  ((uint32_t)cf[2 * j + 1] << 16)));
+    int win[W], qw[W];
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        win[k] = xs[15 - k];                                              // s[a-1-k]
+        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)xs[14 - k], (uint32_t)xs[15 - k],
+                                           0x05040100u);                  // (s[a-1-k], s[a-2-k])
+    }
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; ++t) {
+        const int s = xs[16 + t];
+        int acc = 0;
+        if (DOT2) {
+#pragma unroll
+            for (int j = 0; j < W / 2; ++j) {
+                short2_t av = __builtin_bit_cast(short2_t, qw[2 * j]);
+                short2_t bv = __builtin_bit_cast(short2_t, cp[j]);
+                acc = __builtin_amdgcn_sdot2(av, bv, acc, false);
+            }
+            const int prev = win[0];
+#pragma unroll
+            for (int k = W - 1; k > 0; --k)
+                qw[k] = qw[k - 1];
+            qw[0] = (int)__builtin_amdgcn_perm((uint32_t)prev, (uint32_t)s, 0x05040100u);
+            win[0] = s;
+        } else {
+#pragma unroll
+            for (int k = 0; k < W; ++k)
+                acc = mad24(win[k], cf[k], acc);
+#pragma unroll
+            for (int k = W - 1; k > 0; --k)
+                win[k] = win[k - 1];
+            win[0] = s;
+        }
+        u[t] = zigzag((int)((uint32_t)s - (uint32_t)(acc >> shift)));
+    }
+}
