@@ -20,6 +20,11 @@
 #include "residual.h"
 #include "wave.h"
 
+// timing experiments only (tools/gpu_exp.sh); 0 in every product build
+#ifndef ATG_EXP
+#define ATG_EXP 0
+#endif
+
 __constant__ uint16_t c_crc_adv[24][16]; // advance CRC-16 state by 2^m zero bytes
 __constant__ uint32_t c_crc16[4][256]; // slicing tables: byte + k zero bytes
 __constant__ uint32_t c_crc8[256];
@@ -338,7 +343,7 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
 // the leading full-length (4096) frames of a 16-bit mid/side batch whose
 // frame starts are 16-byte aligned (engine.hip counts them: n_reg_frames).
 template <typename T, bool REG>
-__global__ __launch_bounds__(64) void k_frame_pack(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_frame_pack(
     FlacParams p, uint32_t f0, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
@@ -379,41 +384,41 @@ __global__ __launch_bounds__(64) void k_frame_pack(
     ra = ra < re ? ra : re;
     const int len = (int)(re - ra);
 
-    // REG: the frame's 16-bit stereo pairs for samples [ra - 16, ra + 64)
-    uint32_t pr[80];
-    if (REG) {
-        const uint4 *q4 = (const uint4 *)((const uint32_t *)pcm + fi.pcm_start);
-        const int b4 = ((int)ra - 16) / 4;
-#pragma unroll
-        for (int q = 0; q < 20; ++q) {
-            const uint4 v = q4[max(b4 + q, 0)];
-            const bool ok = b4 + q >= 0;
-            pr[4 * q] = ok ? v.x : 0u;
-            pr[4 * q + 1] = ok ? v.y : 0u;
-            pr[4 * q + 2] = ok ? v.z : 0u;
-            pr[4 * q + 3] = ok ? v.w : 0u;
-        }
-    }
-
     for (uint32_t si = 0; si < fd.nsub; ++si) {
+        // REG: the frame's 16-bit stereo pairs for samples [ra - 16, ra + 64),
+        // (re)loaded per subframe so they are not live across the emission
+        uint32_t pr[80];
+        if (REG) {
+            const uint4 *q4 = (const uint4 *)((const uint32_t *)pcm + fi.pcm_start);
+            const int b4 = ((int)ra - 16) / 4;
+#pragma unroll
+            for (int q = 0; q < 20; ++q) {
+                const uint4 v = q4[max(b4 + q, 0)];
+                const bool ok = b4 + q >= 0;
+                pr[4 * q] = ok ? v.x : 0u;
+                pr[4 * q + 1] = ok ? v.y : 0u;
+                pr[4 * q + 2] = ok ? v.z : 0u;
+                pr[4 * q + 3] = ok ? v.w : 0u;
+            }
+        }
         const uint32_t cand = fd.sub[si];
         const SubDesc &d = sub[(size_t)f * p.n_cand + cand];
         const uint32_t type = d.type, order = d.order, w = d.wasted, sbps = d.sbps;
         const uint32_t start = pos;
         uint32_t maxabs = 0;
-        int xs[80];
+        // REG: candidate sample (ra - 16 + i) from the staged pairs, computed
+        // where used (one v_dot2 + one shift) instead of held in 80 VGPRs
+        const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
+                           : cand == 2u ? 0x00010001u : 0xFFFF0001u;
+        const int xsh = (cand == 2u ? 1 : 0) + (int)w;
+        auto xs = [&](int i) -> int {
+            return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr[i]),
+                                          __builtin_bit_cast(short2_t, wts), 0, false) >> xsh;
+        };
         if (REG) {
-            const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
-                               : cand == 2u ? 0x00010001u : 0xFFFF0001u;
-            const int gsh = cand == 2u ? 1 : 0;
 #pragma unroll
-            for (int i = 0; i < 80; ++i) {
-                const int v = __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr[i]),
-                                                     __builtin_bit_cast(short2_t, wts), 0, false);
-                xs[i] = (v >> gsh) >> w;
-                if (i >= 16)
-                    maxabs = max(maxabs, iabs_u(xs[i]));
-            }
+            for (int i = 16; i < 80; ++i)
+                maxabs = max(maxabs, iabs_u(xs(i)));
         } else {
             stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
                                 [&](uint32_t i, int32_t s) {
@@ -445,7 +450,7 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         const uint32_t rmask = rb >= 32u ? 0xFFFFFFFFu : (1u << rb) - 1u;
         if (type == SF_CONSTANT) {
             // 8 zero header bits, then the raw first sample (flac.c:813-830)
-            const uint32_t s0 = REG ? (uint32_t)__builtin_amdgcn_readfirstlane(xs[16])
+            const uint32_t s0 = REG ? (uint32_t)__builtin_amdgcn_readfirstlane(xs(16))
                                     : (uint32_t)sl[saddr(0)];
             if (lane == 0)
                 put_bits(fb, pos + 8u, sbps, s0);
@@ -465,7 +470,7 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                 if (REG) {
 #pragma unroll
                     for (int t = 0; t < 64; ++t)
-                        wr.put(0, rb, (uint32_t)xs[16 + t] & rmask);
+                        wr.put(0, rb, (uint32_t)xs(16 + t) & rmask);
                 } else {
                     for (int t = 0; t < len; ++t)
                         wr.put(0, rb, (uint32_t)sl[saddr((int)ra + t)] & rmask);
@@ -481,7 +486,7 @@ __global__ __launch_bounds__(64) void k_frame_pack(
 #pragma unroll
                         for (int j = 0; j < ATG_MAX_LPC; ++j)
                             if ((uint32_t)j < order)
-                                ww.put(0, rb, (uint32_t)xs[16 + j] & rmask);
+                                ww.put(0, rb, (uint32_t)xs(16 + j) & rmask);
                         ww.end();
                     }
                 } else if ((uint32_t)lane < order) {
@@ -555,7 +560,9 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                                        : rs + pbits * (jp + (part_head ? 0u : 1u)) + excl);
                     if (part_head)
                         wr.put(0, pbits, k);
+#if ATG_EXP != 8
                     emit_codes(wr, u, warm, len, k);
+#endif
                 } else {
                     // any order <= 32 / wide samples: 64-bit accumulator
                     const int i0 = max((int)ra, (int)order);
@@ -624,6 +631,9 @@ __global__ __launch_bounds__(64) void k_frame_pack(
                 q += 4;
             }
         }
+#if ATG_EXP == 7
+        q = qe;
+#endif
         for (; q < qe; q += 4) {
             const uint32_t t = fb_be32(fb, (uint32_t)q) ^ (crc << 16);
             crc = crc_tab[3][t >> 24] ^ crc_tab[2][(t >> 16) & 0xFFu] ^
@@ -651,8 +661,10 @@ __global__ __launch_bounds__(64) void k_frame_pack(
         dst[lane] = (uint8_t)fb_byte(fb, lane);
     const uint32_t body = (nb - h) / 4u;
     uint32_t *dw = (uint32_t *)(dst + h);
+#if ATG_EXP != 9
     for (uint32_t i = lane; i < body; i += 64)
         dw[i] = __builtin_bswap32(fb_be32(fb, h + 4u * i));
+#endif
     const uint32_t tail0 = h + 4u * body;
     if (tail0 + (uint32_t)lane < nb)
         dst[tail0 + lane] = (uint8_t)fb_byte(fb, tail0 + lane);

@@ -219,12 +219,12 @@ __device__ __forceinline__ void stage_candidate_any(const T *__restrict__ pcm, u
 }
 
 // Register-staged variant of lane_residuals for a full 64-sample run:
-// xs[i] = sample (a - 16 + i), i.e. xs[16] is the run's first sample and
-// xs[3..15] its 13 predecessors.  Writes zig-zag codes only.
-template <bool DOT2>
-__device__ __forceinline__ void lane_residuals_regs(const int (&xs)[80],
-                                                    const int (&cf)[ATG_FAST_ORDER], int shift,
-                                                    uint32_t (&u)[ATG_RUN])
+// xs(i) = sample (a - 16 + i) (i a compile-time constant after unrolling),
+// i.e. xs(16) is the run's first sample and xs(3..15) its predecessors.
+// Writes zig-zag codes only.
+template <bool DOT2, typename X>
+__device__ __forceinline__ void lane_residuals_regs(X &&xs, const int (&cf)[ATG_FAST_ORDER],
+                                                    int shift, uint32_t (&u)[ATG_RUN])
 {
     constexpr int W = ATG_FAST_ORDER;
     int cp[W / 2];
@@ -235,13 +235,13 @@ __device__ __forceinline__ void lane_residuals_regs(const int (&xs)[80],
     int win[W], qw[W];
 #pragma unroll
     for (int k = 0; k < W; ++k) {
-        win[k] = xs[15 - k];                                              // s[a-1-k]
-        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)xs[14 - k], (uint32_t)xs[15 - k],
+        win[k] = xs(15 - k);                                              // s[a-1-k]
+        qw[k] = (int)__builtin_amdgcn_perm((uint32_t)xs(14 - k), (uint32_t)xs(15 - k),
                                            0x05040100u);                  // (s[a-1-k], s[a-2-k])
     }
 #pragma unroll
     for (int t = 0; t < ATG_RUN; ++t) {
-        const int s = xs[16 + t];
+        const int s = xs(16 + t);
         int acc = 0;
         if (DOT2) {
 #pragma unroll
