@@ -20,6 +20,11 @@
 #include "flac_dev.h"
 #include "launch.h"
 
+// timing experiments only (tools/gpu_exp.sh); 0 in every product build
+#ifndef ATG_EXP
+#define ATG_EXP 0
+#endif
+
 namespace {
 
 thread_local std::string g_err;
@@ -392,11 +397,16 @@ atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, in
     // waves per SIMD deep, so a SIMD shared with a (high-priority) chain
     // would leave straggler waves; the search/pack grids are >60 deep and
     // absorb it.
-    HIP_TRY(hipStreamWaitEvent(e->s_aux, e->ev[1], 0));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5], e->s_aux));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, e->s_aux));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5 + 1], e->s_aux));
-    HIP_TRY(hipEventRecord(e->ev_md5, e->s_aux));
+#if ATG_EXP == 10
+    hipStream_t s_md5 = e->s_main; // timing experiment: MD5 alone, serialized
+#else
+    hipStream_t s_md5 = e->s_aux;
+#endif
+    HIP_TRY(hipStreamWaitEvent(s_md5, e->ev[1], 0));
+    HIP_TRY(hipEventRecord(e->ev[2 * 5], s_md5));
+    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, s_md5));
+    HIP_TRY(hipEventRecord(e->ev[2 * 5 + 1], s_md5));
+    HIP_TRY(hipEventRecord(e->ev_md5, s_md5));
     HIP_TRY(hipEventRecord(e->ev[2], e->s_main));
     HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)e->coef.p,
                                    (const int8_t *)e->shift.p, (const uint8_t *)e->est.p,

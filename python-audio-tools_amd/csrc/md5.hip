@@ -20,7 +20,15 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_a
     a = b + rotl(a + f(b, c, d) + x + t, s)
 #define F1(x, y, z) (z ^ (x & (y ^ z)))
 #define F2(x, y, z) (y ^ (z & (x ^ y)))
-#define F3(x, y, z) (x ^ y ^ z)
+// x ^ y ^ z as one v_bitop3_b32 (truth table 0x96); the compiler emits two
+// v_xor_b32 otherwise
+__device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z)
+{
+    uint32_t r;
+    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+}
+#define F3(x, y, z) xor3(x, y, z)
 #define F4(x, y, z) (y ^ (x | ~z))
 
 __device__ __forceinline__ void md5_compress(uint32_t h[4], const uint32_t X[16])
@@ -140,19 +148,13 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
         for (; blk + MD5_D <= full; blk += MD5_D) {
 #pragma unroll
             for (int j = 0; j < MD5_D; ++j) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    X[4 * i] = buf[j][i].x;
-                    X[4 * i + 1] = buf[j][i].y;
-                    X[4 * i + 2] = buf[j][i].z;
-                    X[4 * i + 3] = buf[j][i].w;
-                }
-                // refill (clamped: past the end it re-reads the last block)
+                // hash straight from the load registers, then refill them
+                // (block blk + j + MD5_D, clamped) -- no message copies
+                md5_compress(h, (const uint32_t *)&buf[j][0]);
                 const uint64_t nb = min(blk + (uint64_t)(j + MD5_D), full - 1u);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
                     buf[j][i] = q[nb * 4u + i];
-                md5_compress(h, X);
             }
         }
 #pragma unroll
