@@ -26,6 +26,7 @@
  */
 #include "flac_port.h"
 
+#include <ctype.h>
 #include <float.h>
 #include <limits.h>
 #include <math.h>
@@ -1120,25 +1121,28 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
 }
 
 /* ------------------------------------------------------------------ */
-/* Decoder (FLAC format; semantics of src/decoders/flac.c)             */
+/* Decoder: restatement of src/decoders/flac.c (python-audio-tools     */
+/* 2.22alpha1), error for error.  Codes (FD_*) are the reference's     */
+/* flac_status values (src/decoders/flac.h:68-81) extended with the    */
+/* conditions FlacDecoder.read() raises itself (flac.c:204-265).       */
 /* ------------------------------------------------------------------ */
 typedef struct {
     const uint8_t *p;
-    size_t len;   /* bytes */
+    uint64_t len_bits;
     uint64_t pos; /* bits */
-    int err;
+    int eof;      /* a read went past the end (br_abort -> IOError) */
 } bitr;
 
 static uint32_t br_get(bitr *r, unsigned n)
 {
+    /* bitstream->read(n) for n <= 32 (src/bitstream.c FUNC_READ_BITS) */
     uint32_t v = 0;
     for (unsigned i = 0; i < n; i++) {
-        uint64_t byte = r->pos >> 3;
-        if (byte >= r->len) {
-            r->err = 1;
+        if (r->pos >= r->len_bits) {
+            r->eof = 1;
             return 0;
         }
-        v = (v << 1) | ((r->p[byte] >> (7 - (r->pos & 7))) & 1u);
+        v = (v << 1) | ((r->p[r->pos >> 3] >> (7 - (r->pos & 7))) & 1u);
         r->pos++;
     }
     return v;
@@ -1146,124 +1150,367 @@ static uint32_t br_get(bitr *r, unsigned n)
 
 static int32_t br_get_signed(bitr *r, unsigned n)
 {
-    if (n == 0)
+    /* br_read_signed_bits_be (src/bitstream.c:418-425): sign bit, then
+       count-1 magnitude bits; count 0 asks for 2^32-1 bits -> EOF */
+    if (n == 0) {
+        br_get(r, 1);
+        r->pos = r->len_bits;
+        r->eof = 1;
         return 0;
-    uint32_t v = br_get(r, n);
-    if (n < 32 && (v & (1u << (n - 1))))
-        v |= ~((1u << n) - 1u);
-    return (int32_t)v;
+    }
+    if (n > 33) { /* reads beyond 32 bits keep the low 32: only EOF matters */
+        r->pos += n;
+        if (r->pos > r->len_bits) { r->pos = r->len_bits; r->eof = 1; }
+        return 0;
+    }
+    uint32_t sign = br_get(r, 1);
+    uint32_t v = n > 1 ? br_get(r, n - 1) : 0;
+    return sign ? (int32_t)(v - (1u << (n - 1))) : (int32_t)v;
 }
 
-static uint32_t br_unary(bitr *r)
+/* read_unary(stop): count bits != stop until a stop bit */
+static uint32_t br_unary(bitr *r, unsigned stop)
 {
     uint32_t n = 0;
-    while (!r->err && br_get(r, 1) == 0)
+    while (!r->eof && br_get(r, 1) != stop)
         n++;
     return n;
 }
 
-static int dec_residual(bitr *r, unsigned N, unsigned order, int32_t *res)
+enum {
+    FD_OK = 0, FD_ERROR = 1, FD_SYNC = 2, FD_RESERVED = 3, FD_BPS = 4, FD_RATE = 5,
+    FD_HDR_CRC = 6, FD_RATE_MISMATCH = 7, FD_CH_MISMATCH = 8, FD_BPS_MISMATCH = 9,
+    FD_MAXBS = 10, FD_CODING = 11, FD_FIXED_ORDER = 12, FD_SUBFRAME_TYPE = 13,
+    FD_FRAME_CRC = 14, FD_EOF = 15, FD_MD5 = 16
+};
+
+#define FD_RET(r, code) return (r)->eof ? FD_EOF : (code)
+
+typedef struct {
+    unsigned block_size, sample_rate, assign, channels, bps;
+    uint32_t frame_number;
+} fd_header;
+
+/* flacdec_read_frame_header (src/decoders/flac.c:710-851) */
+static int fd_frame_header(bitr *r, const flacport_streaminfo *si, fd_header *h)
 {
-    unsigned method = br_get(r, 2);
-    if (method > 1)
-        return -1;
-    unsigned porder = br_get(r, 4);
-    unsigned pbits = method ? 5 : 4;
-    unsigned esc = method ? 31 : 15;
-    unsigned idx = 0;
-    for (unsigned part = 0; part < (1u << porder); part++) {
-        unsigned plen = (N >> porder) - (part == 0 ? order : 0);
-        unsigned k = br_get(r, pbits);
-        if (k == esc) {
-            unsigned raw = br_get(r, 5);
-            for (unsigned i = 0; i < plen; i++)
-                res[idx++] = br_get_signed(r, raw);
-        } else {
-            for (unsigned i = 0; i < plen; i++) {
-                uint32_t msb = br_unary(r);
-                uint32_t u = (msb << k) | (k ? br_get(r, k) : 0);
-                res[idx++] = (int32_t)(u >> 1) ^ -(int32_t)(u & 1);
-            }
-        }
-        if (r->err)
-            return -1;
+    const uint64_t start = r->pos;
+    if (br_get(r, 14) != 0x3FFE) FD_RET(r, FD_SYNC);
+    if (br_get(r, 1) != 0) FD_RET(r, FD_RESERVED);
+    br_get(r, 1); /* blocking strategy */
+    unsigned bs_bits = br_get(r, 4), sr_bits = br_get(r, 4);
+    h->assign = br_get(r, 4);
+    h->channels = (h->assign >= 8 && h->assign <= 10) ? 2 : h->assign + 1;
+    switch (br_get(r, 3)) {
+    case 0: h->bps = si->bits_per_sample; break;
+    case 1: h->bps = 8; break;
+    case 2: h->bps = 12; break;
+    case 4: h->bps = 16; break;
+    case 5: h->bps = 20; break;
+    case 6: h->bps = 24; break;
+    default: FD_RET(r, FD_BPS);
     }
-    return 0;
+    br_get(r, 1);
+    /* read_utf8 (flac.c:1310-1320) */
+    unsigned nbytes = br_unary(r, 0);
+    if (nbytes > 7) { r->pos = r->len_bits; r->eof = 1; return FD_EOF; }
+    uint32_t num = br_get(r, 7 - nbytes);
+    for (; nbytes > 1; nbytes--)
+        num = (num << 6) | (br_get(r, 8) & 0x3F);
+    h->frame_number = num;
+    static const unsigned bs_tab[16] = {0, 192, 576, 1152, 2304, 4608, 0, 0,
+                                        256, 512, 1024, 2048, 4096, 8192, 16384, 32768};
+    if (bs_bits == 0) h->block_size = si->max_block_size;
+    else if (bs_bits == 6) h->block_size = br_get(r, 8) + 1;
+    else if (bs_bits == 7) h->block_size = br_get(r, 16) + 1;
+    else h->block_size = bs_tab[bs_bits];
+    static const unsigned sr_tab[12] = {0, 88200, 176400, 192000, 8000, 16000,
+                                        22050, 24000, 32000, 44100, 48000, 96000};
+    if (sr_bits == 0) h->sample_rate = si->sample_rate;
+    else if (sr_bits < 12) h->sample_rate = sr_tab[sr_bits];
+    else if (sr_bits == 12) h->sample_rate = br_get(r, 8) * 1000;
+    else if (sr_bits == 13) h->sample_rate = br_get(r, 16);
+    else if (sr_bits == 14) h->sample_rate = br_get(r, 16) * 10;
+    else FD_RET(r, FD_RATE);
+    br_get(r, 8);
+    if (r->eof) return FD_EOF;
+    if (crc8_bytes(r->p + (start >> 3), (size_t)((r->pos - start) >> 3)) != 0)
+        return FD_HDR_CRC;
+    if (si->sample_rate != h->sample_rate) return FD_RATE_MISMATCH;
+    if (si->channels != h->channels) return FD_CH_MISMATCH;
+    if (si->bits_per_sample != h->bps) return FD_BPS_MISMATCH;
+    if (h->block_size > si->max_block_size) return FD_MAXBS;
+    return FD_OK;
 }
 
-static int dec_subframe(bitr *r, unsigned N, unsigned bps, int32_t *out,
-                        int32_t *res)
+/* flacdec_read_residual (flac.c:1135-1209): res[0 .. N-order) */
+static int fd_residual(bitr *r, unsigned order, unsigned N, int32_t *res)
 {
-    if (br_get(r, 1) != 0)
-        return -1;
-    unsigned type = br_get(r, 6);
+    const unsigned method = br_get(r, 2);
+    const unsigned porder = br_get(r, 4);
+    unsigned idx = 0;
+    /* a partition order that does not divide the block leaves residuals the
+       reference never reads (it would predict from a stale buffer); both
+       engines reject such streams (decoder limits) */
+    if (!r->eof && method <= 1 && ((N >> porder) << porder) != N)
+        return FD_ERROR;
+    for (unsigned part = 0; part < (1u << porder); part++) {
+        int plen;
+        if (part == 0) {
+            plen = (int)(N / (1u << porder)) - (int)order;
+            if (plen < 0) plen = 0;
+        } else {
+            plen = (int)(N / (1u << porder));
+        }
+        unsigned rice, esc;
+        if (method == 0) {
+            rice = br_get(r, 4);
+            esc = rice == 0xF ? br_get(r, 5) : 0;
+        } else if (method == 1) {
+            rice = br_get(r, 5);
+            esc = rice == 0x1F ? br_get(r, 5) : 0;
+        } else {
+            FD_RET(r, FD_CODING);
+        }
+        if (r->eof) return FD_EOF;
+        if (!esc) {
+            for (; plen; plen--) {
+                const uint32_t msb = br_unary(r, 1);
+                const uint32_t lsb = br_get(r, rice);
+                const uint32_t value = (msb << rice) | lsb;
+                const int32_t sv = (int32_t)value >> 1;
+                res[idx++] = (value & 1u) ? -sv - 1 : sv;
+                if (r->eof) return FD_EOF;
+            }
+        } else {
+            for (; plen; plen--)
+                res[idx++] = br_get_signed(r, esc);
+        }
+        if (r->eof) return FD_EOF;
+    }
+    return FD_OK;
+}
+
+/* flacdec_read_subframe and friends (flac.c:854-1132) */
+static int fd_subframe(bitr *r, unsigned N, unsigned bps, int32_t *s, int32_t *res)
+{
+    br_get(r, 1); /* padding, unchecked */
+    const unsigned t = br_get(r, 6);
+    unsigned kind, order;
+    if (t == 0) { kind = 0; order = 0; }
+    else if (t == 1) { kind = 1; order = 0; }
+    else if ((t & 0x38) == 0x08) { kind = 2; order = t & 7; }
+    else if ((t & 0x20) == 0x20) { kind = 3; order = (t & 0x1F) + 1; }
+    else FD_RET(r, FD_SUBFRAME_TYPE);
     unsigned wasted = 0;
     if (br_get(r, 1))
-        wasted = br_unary(r) + 1;
-    unsigned sbps = bps - wasted;
-    if (type == 0) {
-        int32_t v = br_get_signed(r, sbps);
-        for (unsigned i = 0; i < N; i++)
-            out[i] = v;
-    } else if (type == 1) {
-        for (unsigned i = 0; i < N; i++)
-            out[i] = br_get_signed(r, sbps);
-    } else if (type >= 8 && type <= 12) {
-        unsigned order = type - 8;
-        for (unsigned i = 0; i < order; i++)
-            out[i] = br_get_signed(r, sbps);
-        if (dec_residual(r, N, order, res))
-            return -1;
+        wasted = br_unary(r, 1) + 1;
+    if (r->eof) return FD_EOF;
+    bps -= wasted; /* unsigned, as the reference */
+    if (kind == 0) {
+        const int32_t v = br_get_signed(r, bps);
+        for (unsigned i = 0; i < N; i++) s[i] = v;
+    } else if (kind == 1) {
+        for (unsigned i = 0; i < N; i++) s[i] = br_get_signed(r, bps);
+    } else if (kind == 2) {
+        for (unsigned i = 0; i < order; i++) s[i] = br_get_signed(r, bps);
+        int rc = fd_residual(r, order, N, res);
+        if (rc) return rc;
+        if (order > 4) return FD_FIXED_ORDER;
         for (unsigned i = order; i < N; i++) {
-            int64_t pred;
+            const uint32_t *u = (const uint32_t *)s; /* int arithmetic wraps */
+            uint32_t v;
             switch (order) {
-            case 0: pred = 0; break;
-            case 1: pred = out[i - 1]; break;
-            case 2: pred = 2 * (int64_t)out[i - 1] - out[i - 2]; break;
-            case 3: pred = 3 * (int64_t)out[i - 1] - 3 * (int64_t)out[i - 2] + out[i - 3]; break;
-            default: pred = 4 * (int64_t)out[i - 1] - 6 * (int64_t)out[i - 2] +
-                            4 * (int64_t)out[i - 3] - out[i - 4];
+            case 0: v = 0; break;
+            case 1: v = u[i - 1]; break;
+            case 2: v = 2u * u[i - 1] - u[i - 2]; break;
+            case 3: v = 3u * u[i - 1] - 3u * u[i - 2] + u[i - 3]; break;
+            default: v = 4u * u[i - 1] - 6u * u[i - 2] + 4u * u[i - 3] - u[i - 4];
             }
-            out[i] = (int32_t)(pred + res[i - order]);
+            s[i] = (int32_t)(v + (uint32_t)res[i - order]);
         }
-    } else if (type >= 32) {
-        unsigned order = (type & 31) + 1;
+    } else {
         int32_t coef[32];
-        for (unsigned i = 0; i < order; i++)
-            out[i] = br_get_signed(r, sbps);
-        unsigned prec = br_get(r, 4) + 1;
-        int shift = br_get_signed(r, 5);
-        for (unsigned i = 0; i < order; i++)
-            coef[i] = br_get_signed(r, prec);
-        if (dec_residual(r, N, order, res))
-            return -1;
+        for (unsigned i = 0; i < order; i++) s[i] = br_get_signed(r, bps);
+        const unsigned prec = br_get(r, 4) + 1;
+        /* qlp_shift_needed is unsigned: MAX(x, 0) keeps a negative shift as a
+           huge count, and x86's 64-bit sar masks the count to 6 bits */
+        const unsigned shift = (unsigned)br_get_signed(r, 5) & 63u;
+        for (unsigned i = 0; i < order; i++) coef[i] = br_get_signed(r, prec);
+        int rc = fd_residual(r, order, N, res);
+        if (rc) return rc;
         for (unsigned i = order; i < N; i++) {
             int64_t acc = 0;
             for (unsigned j = 0; j < order; j++)
-                acc += (int64_t)coef[j] * out[i - j - 1];
-            out[i] = (int32_t)((acc >> (shift > 0 ? shift : 0)) + res[i - order]);
+                acc += (int64_t)coef[j] * (int64_t)s[i - j - 1];
+            s[i] = (int32_t)((uint32_t)(int32_t)(acc >> shift) + (uint32_t)res[i - order]);
         }
-    } else {
-        return -1;
     }
+    if (r->eof) return FD_EOF;
     if (wasted)
-        for (unsigned i = 0; i < N; i++)
-            out[i] = (int32_t)((uint32_t)out[i] << wasted);
-    return r->err ? -1 : 0;
+        for (unsigned i = 0; i < N; i++) s[i] = (int32_t)((uint32_t)s[i] << wasted);
+    return FD_OK;
 }
 
-static uint32_t dec_utf8(bitr *r)
+int flacport_read_metadata(const uint8_t *data, size_t len, flacport_streaminfo *si,
+                           flacport_seekpoint *sp, size_t sp_cap)
 {
-    uint32_t b = br_get(r, 8);
-    if (!(b & 0x80))
-        return b;
-    unsigned n = 0;
-    while (b & (0x80 >> n))
-        n++;
-    uint32_t v = b & (0xFF >> (n + 1));
-    for (unsigned i = 1; i < n; i++)
-        v = (v << 6) | (br_get(r, 8) & 0x3F);
-    return v;
+    /* flacdec_read_metadata (flac.c:568-707) */
+    static const uint32_t masks[9] = {0, 0x4, 0x3, 0x7, 0x33, 0x37, 0x3F, 0x70F, 0x63F};
+    memset(si, 0, sizeof(*si));
+    bitr r = {data, (uint64_t)len * 8, 0, 0};
+    uint32_t magic = br_get(&r, 32);
+    if (r.eof) return 2;
+    if (magic != 0x664C6143u) return 1;
+    unsigned last;
+    do {
+        last = br_get(&r, 1);
+        const unsigned type = br_get(&r, 7);
+        const uint32_t blen = br_get(&r, 24);
+        if (r.eof) return 2;
+        const uint64_t body = r.pos;
+        if (type == 0) {
+            si->min_block_size = br_get(&r, 16);
+            si->max_block_size = br_get(&r, 16);
+            si->min_frame_size = br_get(&r, 24);
+            si->max_frame_size = br_get(&r, 24);
+            si->sample_rate = br_get(&r, 20);
+            si->channels = br_get(&r, 3) + 1;
+            si->bits_per_sample = br_get(&r, 5) + 1;
+            si->total_samples = ((uint64_t)br_get(&r, 4) << 32) | br_get(&r, 32);
+            for (int i = 0; i < 16; i++) si->md5[i] = (uint8_t)br_get(&r, 8);
+            si->channel_mask = si->channels <= 8 ? masks[si->channels] : 0;
+            /* the reference reads exactly 34 bytes whatever the length says */
+        } else if (type == 3) {
+            const unsigned n = blen / 18;
+            for (unsigned k = 0; k < n; k++) {
+                flacport_seekpoint p;
+                p.sample_number = ((uint64_t)br_get(&r, 32) << 32) | br_get(&r, 32);
+                p.byte_offset = ((uint64_t)br_get(&r, 32) << 32) | br_get(&r, 32);
+                p.samples = br_get(&r, 16);
+                if (sp && k < sp_cap) sp[k] = p;
+            }
+            si->n_seekpoints = n;
+        } else if (type == 4) {
+            /* flacdec_read_vorbis_comment (flac.c:508-566): little-endian
+               lengths; a read error inside the block is swallowed */
+            if (body + (uint64_t)blen * 8 > r.len_bits) { r.eof = 1; return 2; }
+            const uint8_t *c = data + (body >> 3);
+            size_t cl = blen, i = 0;
+#define LE32(q) ((uint32_t)(q)[0] | ((uint32_t)(q)[1] << 8) | ((uint32_t)(q)[2] << 16) | ((uint32_t)(q)[3] << 24))
+            if (i + 4 <= cl) {
+                uint32_t vl = LE32(c + i);
+                i += 4;
+                if (vl <= cl - i) {
+                    i += vl;
+                    if (i + 4 <= cl) {
+                        uint32_t lines = LE32(c + i);
+                        i += 4;
+                        static const char pre[] = "WAVEFORMATEXTENSIBLE_CHANNEL_MASK=";
+                        for (; lines > 0; lines--) {
+                            if (i + 4 > cl) break;
+                            uint32_t ll = LE32(c + i);
+                            i += 4;
+                            if (ll > cl - i) break;
+                            char buf[256];
+                            size_t keep = ll < 255 ? ll : 255;
+                            for (size_t k = 0; k < keep; k++)
+                                buf[k] = (char)toupper(c[i + k]);
+                            buf[keep] = 0;
+                            /* the reference uppercases the line into a
+                               NUL-terminated buffer: strstr prefix test, then
+                               strtoul base 16 on the rest */
+                            if (strncmp(buf, pre, sizeof(pre) - 1) == 0) {
+                                unsigned long m = strtoul(buf + sizeof(pre) - 1, NULL, 16);
+                                unsigned mask = (unsigned)m, bits = 0;
+                                for (unsigned mm = mask; mm; mm >>= 1) bits += mm & 1u;
+                                if (bits == si->channels) si->channel_mask = mask;
+                            }
+                            i += ll;
+                        }
+                    }
+                }
+            }
+#undef LE32
+        }
+        if (type != 0 && type != 3) r.pos = body + (uint64_t)blen * 8;
+        if (r.pos > r.len_bits) { r.pos = r.len_bits; r.eof = 1; }
+        if (r.eof) return 2;
+    } while (!last);
+    si->frames_offset = r.pos >> 3;
+    return 0;
+}
+
+int flacport_decode_frames(const uint8_t *data, size_t len, const flacport_streaminfo *si,
+                           uint64_t remaining, int check_crc, int32_t *pcm, size_t pcm_cap,
+                           uint64_t *frame_offsets, uint32_t *frame_block_sizes,
+                           size_t frame_cap, size_t *n_frames, uint64_t *pcm_frames)
+{
+    /* the frame loop of FlacDecoder_read / offsets (flac.c:174-285, 365-443) */
+    crc_init();
+    const unsigned ch = si->channels;
+    const unsigned alloc = si->max_block_size ? si->max_block_size : 1;
+    const size_t stride = (size_t)alloc + 32; /* warm-up samples may exceed a tiny block */
+    int32_t *sub = malloc(sizeof(int32_t) * stride * 16);
+    int32_t *res = malloc(sizeof(int32_t) * stride);
+    bitr r = {data, (uint64_t)len * 8, 0, 0};
+    size_t nf = 0;
+    uint64_t done = 0;
+    int rc = FD_OK;
+    while (remaining != 0) {
+        const uint64_t fstart = r.pos;
+        fd_header h;
+        rc = fd_frame_header(&r, si, &h);
+        if (rc) break;
+        const unsigned N = (unsigned)(h.block_size < remaining ? h.block_size : remaining);
+        for (unsigned c = 0; c < h.channels && !rc; c++) {
+            unsigned sbps = h.bps;
+            if ((h.assign == 8 && c == 1) || (h.assign == 9 && c == 0) ||
+                (h.assign == 10 && c == 1))
+                sbps = h.bps + 1;
+            rc = fd_subframe(&r, N, sbps, sub + (size_t)c * stride, res);
+        }
+        if (rc) break;
+        if (r.pos & 7) br_get(&r, 8 - (unsigned)(r.pos & 7));
+        br_get(&r, 16);
+        if (r.eof) { rc = FD_EOF; break; }
+        if (check_crc && crc16_bytes(data + (fstart >> 3), (size_t)((r.pos - fstart) >> 3)) != 0) {
+            rc = FD_FRAME_CRC;
+            break;
+        }
+        if (nf >= frame_cap || (done + N) * ch > pcm_cap) { rc = -1; break; } /* capacity */
+        frame_offsets[nf] = fstart >> 3;
+        frame_block_sizes[nf] = h.block_size;
+        nf++;
+        /* flacdec_decorrelate_channels (flac.c:1212-1269) */
+        int32_t *a = sub, *b = sub + stride;
+        int32_t *o = pcm + done * ch;
+        for (unsigned k = 0; k < N; k++) {
+            if (h.assign == 8) {
+                o[2 * k] = a[k];
+                o[2 * k + 1] = (int32_t)((uint32_t)a[k] - (uint32_t)b[k]);
+            } else if (h.assign == 9) {
+                o[2 * k] = (int32_t)((uint32_t)a[k] + (uint32_t)b[k]);
+                o[2 * k + 1] = b[k];
+            } else if (h.assign == 10) {
+                int64_t mid = a[k];
+                int32_t side = b[k];
+                mid = (int64_t)((uint64_t)mid << 1) | (side & 1);
+                o[2 * k] = (int32_t)((mid + side) >> 1);
+                o[2 * k + 1] = (int32_t)((mid - side) >> 1);
+            } else {
+                for (unsigned c = 0; c < ch; c++)
+                    o[(size_t)k * ch + c] = sub[(size_t)c * stride + k];
+            }
+        }
+        done += N;
+        remaining -= h.block_size; /* uint64, wraps as the reference's */
+    }
+    free(sub);
+    free(res);
+    *n_frames = nf;
+    *pcm_frames = done;
+    return rc;
 }
 
 int flacport_decode(const uint8_t *flac, size_t len, uint32_t *channels,
@@ -1278,112 +1525,36 @@ int flacport_decode(const uint8_t *flac, size_t len, uint32_t *channels,
                     ((size_t)(flac[8] & 0x7F) << 7) | (flac[9] & 0x7F);
         i = 10 + sz;
     }
-    if (len < i + 8 || memcmp(flac + i, "fLaC", 4) != 0)
+    if (i > len)
         return -1;
-    i += 4;
-    uint32_t ch = 0, bps = 0, rate = 0, maxbs = 0;
-    uint64_t total = 0;
-    uint8_t md5[16] = {0};
-    int last = 0;
-    while (!last) {
-        if (i + 4 > len)
-            return -1;
-        last = flac[i] >> 7;
-        unsigned type = flac[i] & 0x7F;
-        size_t blen = ((size_t)flac[i + 1] << 16) | ((size_t)flac[i + 2] << 8) | flac[i + 3];
-        i += 4;
-        if (i + blen > len)
-            return -1;
-        if (type == 0) {
-            bitr r = {flac + i, blen, 0, 0};
-            br_get(&r, 16);
-            maxbs = br_get(&r, 16);
-            br_get(&r, 24);
-            br_get(&r, 24);
-            rate = br_get(&r, 20);
-            ch = br_get(&r, 3) + 1;
-            bps = br_get(&r, 5) + 1;
-            total = ((uint64_t)br_get(&r, 4) << 32) | br_get(&r, 32);
-            memcpy(md5, flac + i + 18, 16);
-        }
-        i += blen;
-    }
-    if (channels) *channels = ch;
-    if (bits_per_sample) *bits_per_sample = bps;
-    if (sample_rate) *sample_rate = rate;
-    if (total_frames) *total_frames = total;
+    flacport_streaminfo si;
+    if (flacport_read_metadata(flac + i, len - i, &si, NULL, 0))
+        return -1;
+    if (channels) *channels = si.channels;
+    if (bits_per_sample) *bits_per_sample = si.bits_per_sample;
+    if (sample_rate) *sample_rate = si.sample_rate;
+    if (total_frames) *total_frames = si.total_samples;
     if (!pcm)
         return 0;
-    if (pcm_cap < total * ch)
+    if (pcm_cap < si.total_samples * si.channels)
         return -2;
-
-    size_t alloc = maxbs ? maxbs : 65536;
-    int32_t *sub = malloc(sizeof(int32_t) * alloc * 8);
-    int32_t *res = malloc(sizeof(int32_t) * alloc);
-    uint64_t done = 0;
-    int rc = 0;
-    bitr r = {flac, len, (uint64_t)i * 8, 0};
-    while (done < total) {
-        uint64_t fstart = r.pos >> 3;
-        if (br_get(&r, 14) != 0x3FFE) { rc = -3; break; }
-        br_get(&r, 2);
-        unsigned bs_code = br_get(&r, 4);
-        unsigned sr_code = br_get(&r, 4);
-        unsigned assign = br_get(&r, 4);
-        unsigned bps_code = br_get(&r, 3);
-        br_get(&r, 1);
-        (void)bps_code;
-        dec_utf8(&r);
-        unsigned N;
-        if (bs_code == 1) N = 192;
-        else if (bs_code >= 2 && bs_code <= 5) N = 576u << (bs_code - 2);
-        else if (bs_code == 6) N = br_get(&r, 8) + 1;
-        else if (bs_code == 7) N = br_get(&r, 16) + 1;
-        else if (bs_code >= 8) N = 256u << (bs_code - 8);
-        else { rc = -3; break; }
-        if (sr_code == 12) br_get(&r, 8);
-        else if (sr_code == 13 || sr_code == 14) br_get(&r, 16);
-        unsigned hdr_bytes = (unsigned)((r.pos >> 3) - fstart);
-        unsigned crc8 = br_get(&r, 8);
-        if (r.err || N > alloc || crc8 != crc8_bytes(flac + fstart, hdr_bytes)) { rc = -3; break; }
-        unsigned nch = assign < 8 ? assign + 1 : 2;
-        if (nch != ch) { rc = -3; break; }
-        for (unsigned c = 0; c < nch; c++) {
-            unsigned sbps = bps;
-            if ((assign == 8 && c == 1) || (assign == 9 && c == 0) || (assign == 10 && c == 1))
-                sbps = bps + 1;
-            if (dec_subframe(&r, N, sbps, sub + (size_t)c * alloc, res)) { rc = -4; break; }
-        }
-        if (rc) break;
-        if (r.pos & 7) br_get(&r, 8 - (unsigned)(r.pos & 7));
-        uint16_t want = crc16_bytes(flac + fstart, (size_t)((r.pos >> 3) - fstart));
-        if (br_get(&r, 16) != want || r.err) { rc = -3; break; }
-        int32_t *a = sub, *b = sub + alloc;
-        for (unsigned k = 0; k < N; k++) {
-            if (assign == 8) b[k] = a[k] - b[k];
-            else if (assign == 9) a[k] = a[k] + b[k];
-            else if (assign == 10) {
-                int32_t mid = (int32_t)(((uint32_t)a[k] << 1) | ((uint32_t)b[k] & 1u));
-                int32_t side = b[k];
-                a[k] = (mid + side) >> 1;
-                b[k] = (mid - side) >> 1;
-            }
-        }
-        if (done + N > total) N = (unsigned)(total - done);
-        for (unsigned k = 0; k < N; k++)
-            for (unsigned c = 0; c < nch; c++)
-                pcm[(done + k) * ch + c] = sub[(size_t)c * alloc + k];
-        done += N;
-    }
-    free(sub);
-    free(res);
+    size_t cap = (size_t)(si.total_samples / (si.min_block_size ? si.min_block_size : 1)) + 2;
+    uint64_t *offs = malloc(sizeof(uint64_t) * cap);
+    uint32_t *bss = malloc(sizeof(uint32_t) * cap);
+    size_t nf;
+    uint64_t got;
+    const size_t start = i + si.frames_offset;
+    int rc = flacport_decode_frames(flac + start, len - start, &si, si.total_samples, 1, pcm,
+                                    pcm_cap, offs, bss, cap, &nf, &got);
+    free(offs);
+    free(bss);
     if (rc)
-        return rc;
+        return rc == FD_EOF ? -4 : -3;
     static const uint8_t zero[16] = {0};
-    if (memcmp(md5, zero, 16) != 0) {
-        uint8_t got[16];
-        flacport_pcm_md5(pcm, total, ch, bps, got);
-        if (memcmp(got, md5, 16) != 0)
+    if (memcmp(si.md5, zero, 16) != 0) {
+        uint8_t d[16];
+        flacport_pcm_md5(pcm, got, si.channels, si.bits_per_sample, d);
+        if (memcmp(d, si.md5, 16) != 0)
             return -5;
     }
     return 0;

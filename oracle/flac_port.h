@@ -60,6 +60,39 @@ void flacport_pcm_md5(const int32_t *pcm, uint64_t pcm_frames,
                       uint32_t channels, uint32_t bits_per_sample,
                       uint8_t digest[16]);
 
+/* STREAMINFO + the parts of the other metadata blocks the reference decoder
+   keeps (src/decoders/flac.c:568-707). */
+typedef struct {
+    uint32_t min_block_size, max_block_size, min_frame_size, max_frame_size;
+    uint32_t sample_rate, channels, bits_per_sample, channel_mask;
+    uint64_t total_samples;
+    uint8_t md5[16];
+    uint64_t frames_offset; /* byte offset of the first frame */
+    uint32_t n_seekpoints;
+    uint32_t reserved;
+} flacport_streaminfo;
+
+typedef struct {
+    uint64_t sample_number, byte_offset;
+    uint32_t samples, reserved;
+} flacport_seekpoint;
+
+/* 0 = ok, 1 = not a FLAC file (ValueError), 2 = EOF (IOError) */
+int flacport_read_metadata(const uint8_t *data, size_t len, flacport_streaminfo *si,
+                           flacport_seekpoint *sp, size_t sp_cap);
+
+/* Decode frames from data (the first frame at data[0]) until `remaining`
+   (uint64, decremented by each frame's block size with wrap-around, as the
+   reference's remaining_samples) reaches 0 or an error ends the stream.
+   Returns the FD_* code that ended decoding: 0 ok, 1..13 the reference's
+   flac_status values, 14 frame CRC-16 mismatch, 15 EOF; -1 when pcm_cap or
+   frame_cap is too small.  pcm receives the
+   interleaved int32 samples of the frames decoded before the error. */
+int flacport_decode_frames(const uint8_t *data, size_t len, const flacport_streaminfo *si,
+                           uint64_t remaining, int check_crc, int32_t *pcm, size_t pcm_cap,
+                           uint64_t *frame_offsets, uint32_t *frame_block_sizes,
+                           size_t frame_cap, size_t *n_frames, uint64_t *pcm_frames);
+
 /* Decode a .flac image.  On success returns 0 and fills the stream
    parameters; pcm (capacity pcm_cap samples, may be NULL to query) receives
    interleaved int32 samples.  Verifies CRC-8/CRC-16 and, when present,

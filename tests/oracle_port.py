@@ -164,3 +164,123 @@ def split_flac(data):
         if last:
             break
     return blocks, data[i:]
+
+
+# ---------------------------------------------------------------- decoder
+class PortStreamInfo(ctypes.Structure):
+    _fields_ = [("min_block_size", c_u32), ("max_block_size", c_u32),
+                ("min_frame_size", c_u32), ("max_frame_size", c_u32),
+                ("sample_rate", c_u32), ("channels", c_u32),
+                ("bits_per_sample", c_u32), ("channel_mask", c_u32),
+                ("total_samples", c_u64), ("md5", ctypes.c_uint8 * 16),
+                ("frames_offset", c_u64), ("n_seekpoints", c_u32),
+                ("reserved", c_u32)]
+
+
+class PortSeekPoint(ctypes.Structure):
+    _fields_ = [("sample_number", c_u64), ("byte_offset", c_u64),
+                ("samples", c_u32), ("reserved", c_u32)]
+
+
+# decoder status codes: the reference's flac_status values
+# (src/decoders/flac.h:68-81) plus the conditions FlacDecoder.read raises
+FD_OK, FD_ERROR, FD_FRAME_CRC, FD_EOF, FD_MD5 = 0, 1, 14, 15, 16
+FD_MESSAGES = {
+    1: "Error", 2: "invalid sync code", 3: "invalid reserved bit",
+    4: "invalid bits per sample", 5: "invalid sample rate",
+    6: "invalid checksum in frame header",
+    7: "frame sample rate does not match STREAMINFO sample rate",
+    8: "frame channel count does not match STREAMINFO channel count",
+    9: "frame bits-per-sample does not match STREAMINFO bits per sample",
+    10: "frame block size exceeds STREAMINFO's maximum block size",
+    11: "invalid residual partition coding method",
+    12: "invalid FIXED subframe order", 13: "invalid subframe type",
+    14: "invalid checksum in frame", 15: "EOF reading frame",
+    16: "MD5 mismatch at end of stream",
+}
+
+
+def _dec_lib():
+    lib = load()
+    if not hasattr(lib, "_dec_ready"):
+        lib.flacport_read_metadata.restype = ctypes.c_int
+        lib.flacport_read_metadata.argtypes = [
+            ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(PortStreamInfo),
+            ctypes.c_void_p, ctypes.c_size_t]
+        lib.flacport_decode_frames.restype = ctypes.c_int
+        lib.flacport_decode_frames.argtypes = [
+            ctypes.c_char_p, ctypes.c_size_t, ctypes.POINTER(PortStreamInfo), c_u64,
+            ctypes.c_int, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_void_p,
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+            ctypes.POINTER(c_u64)]
+        lib._dec_ready = True
+    return lib
+
+
+def read_metadata(data):
+    """-> (rc, streaminfo dict, [(sample, byte_offset, samples)]);
+    rc 0 ok, 1 not FLAC (ValueError), 2 EOF (IOError)"""
+    lib = _dec_lib()
+    si = PortStreamInfo()
+    sp = (PortSeekPoint * 4096)()
+    rc = lib.flacport_read_metadata(data, len(data), ctypes.byref(si),
+                                    ctypes.cast(sp, ctypes.c_void_p), 4096)
+    info = {f: getattr(si, f) for f, _ in PortStreamInfo._fields_ if f != "md5"}
+    info["md5"] = bytes(si.md5)
+    pts = [(sp[i].sample_number, sp[i].byte_offset, sp[i].samples)
+           for i in range(min(si.n_seekpoints, 4096))]
+    return rc, info, pts, si
+
+
+def decode_frames(data, si=None, start=None, remaining=None, check_crc=True,
+                  extra_frames=4):
+    """Frame loop of the reference decoder over a whole file image.
+    -> dict(code, pcm int32 interleaved, offsets [(byte offset from start,
+    block_size)], pcm_frames)"""
+    lib = _dec_lib()
+    if si is None:
+        rc, _, _, si = read_metadata(data)
+        if rc:
+            raise ValueError("metadata rc %d" % rc)
+    if start is None:
+        start = si.frames_offset
+    if remaining is None:
+        remaining = si.total_samples
+    bs = max(1, si.max_block_size)
+    minbs = max(1, min(si.min_block_size or 1, bs))
+    want = int(min(remaining, si.total_samples)) + bs * extra_frames
+    body = data[start:]
+    while True:  # a wrapped remaining count decodes past the total: grow
+        frame_cap = want // minbs + extra_frames + 2
+        cap = want * max(1, si.channels)
+        pcm = np.zeros(cap, dtype=np.int32)
+        offs = np.zeros(frame_cap, dtype=np.uint64)
+        bss = np.zeros(frame_cap, dtype=np.uint32)
+        nf, got = ctypes.c_size_t(), c_u64()
+        code = lib.flacport_decode_frames(body, len(body), ctypes.byref(si), remaining,
+                                          int(check_crc), pcm.ctypes.data_as(ctypes.c_void_p),
+                                          cap, offs.ctypes.data_as(ctypes.c_void_p),
+                                          bss.ctypes.data_as(ctypes.c_void_p), frame_cap,
+                                          ctypes.byref(nf), ctypes.byref(got))
+        if code != -1:
+            break
+        want *= 4
+    n = nf.value
+    return dict(code=code, pcm=pcm[:got.value * si.channels],
+                offsets=[(int(offs[i]), int(bss[i])) for i in range(n)],
+                pcm_frames=got.value)
+
+
+def pcm_bytes(pcm, bps):
+    """FrameList.to_bytes(little_endian, signed) for 8/16/24-bit samples"""
+    a = np.asarray(pcm, dtype=np.int32)
+    if a.size == 0:
+        return b""
+    if bps == 8:
+        return a.astype(np.int8).tobytes()
+    if bps == 16:
+        return a.astype("<i2").tobytes()
+    if bps == 24:
+        u = a.astype("<i4").view(np.uint8).reshape(-1, 4)[:, :3]
+        return u.tobytes()
+    raise ValueError("unsupported bps %d" % bps)
