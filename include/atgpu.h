@@ -148,6 +148,108 @@ atg_status atg_copy_to_device(atg_engine *eng, void *d_dst, const void *src,
 atg_status atg_copy_to_host(atg_engine *eng, void *dst, const void *d_src,
                             uint64_t bytes);
 
+/* ------------------------------------------------------------------ */
+/* FLAC decoder (trackverify / FlacDecoder path).                     */
+/* Replaces the body of the reference's audiotools.decoders.FlacDecoder */
+/* (src/decoders/flac.c:28-98 init + flacdec_read_metadata :568-707,   */
+/* read() :174-285 with its frame/subframe/residual readers :710-1269, */
+/* offsets() :365-443, MD5 verify :446-493) for a batch of images.      */
+/* ------------------------------------------------------------------ */
+
+/* Decode status per track: the reference's flac_status values
+   (src/decoders/flac.h:68-81) plus what read() raises itself. */
+enum {
+    ATG_FD_OK = 0, ATG_FD_ERROR = 1, ATG_FD_SYNC = 2, ATG_FD_RESERVED = 3,
+    ATG_FD_BPS = 4, ATG_FD_RATE = 5, ATG_FD_HDR_CRC = 6,
+    ATG_FD_RATE_MISMATCH = 7, ATG_FD_CH_MISMATCH = 8, ATG_FD_BPS_MISMATCH = 9,
+    ATG_FD_MAXBS = 10, ATG_FD_CODING = 11, ATG_FD_FIXED_ORDER = 12,
+    ATG_FD_SUBFRAME_TYPE = 13,
+    ATG_FD_FRAME_CRC = 14, /* "invalid checksum in frame" (flac.c:251-255) */
+    ATG_FD_EOF = 15,       /* IOError "EOF reading frame" (flac.c:259-264) */
+    ATG_FD_MD5 = 16        /* "MD5 mismatch at end of stream" (:199-207) */
+};
+
+/* STREAMINFO and the parts of the other metadata blocks the reference
+   decoder keeps (struct flac_STREAMINFO, src/decoders/flac.h:37-48). */
+typedef struct {
+    uint32_t min_block_size, max_block_size, min_frame_size, max_frame_size;
+    uint32_t sample_rate, channels, bits_per_sample, channel_mask;
+    uint64_t total_samples;
+    uint8_t md5[16];
+    uint64_t frames_offset; /* bytes from the image start to the first frame */
+    uint32_t n_seekpoints;
+    uint32_t reserved;
+} atg_flac_streaminfo;
+
+typedef struct {
+    uint64_t sample_number, byte_offset;
+    uint32_t samples, reserved;
+} atg_flac_seekpoint;
+
+/* flacdec_read_metadata (src/decoders/flac.c:568-707) over an in-memory
+   image.  Returns 0 ok, 1 not a FLAC stream (ValueError), 2 EOF (IOError).
+   Up to sp_cap SEEKTABLE points are stored into sp (may be NULL). */
+int atg_flac_read_metadata(const uint8_t *data, uint64_t len, atg_flac_streaminfo *si,
+                           atg_flac_seekpoint *sp, uint32_t sp_cap);
+
+/* One stream of a decode batch: its frames occupy
+   data[data_offset, data_offset + data_bytes) (data_offset = image start +
+   frames_offset); the remaining fields are its STREAMINFO. */
+typedef struct {
+    uint64_t data_offset;
+    uint64_t data_bytes;
+    uint64_t total_samples;
+    uint32_t sample_rate, channels, bits_per_sample, max_block_size;
+    uint8_t md5[16];
+} atg_flac_dec_track;
+
+/* Per-track decode result.  The frames before `status` stopped the stream
+   decoded: pcm_frames PCM frames (interleaved int32, FrameList layout) at
+   PCM-frame index pcm_offset of the batch output, n_frames FLAC frames
+   starting at first_frame of the frame arrays.  md5 = MD5 of their
+   little-endian PCM bytes. */
+typedef struct {
+    uint64_t pcm_offset;
+    uint64_t pcm_frames;
+    uint32_t first_frame;
+    uint32_t n_frames;
+    int32_t status;
+    uint32_t reserved;
+    uint8_t md5[16];
+} atg_flac_dec_result;
+
+typedef struct atg_decoder atg_decoder;
+
+atg_status atg_decoder_create(int device, atg_decoder **out);
+void atg_decoder_destroy(atg_decoder *dec);
+const char *atg_decoder_last_error(void);
+
+/* Decode a batch held in host memory; the PCM stays in the decoder until
+   atg_flac_decode_fetch.  total_samples = interleaved samples of the batch
+   output, total_frames = FLAC frames decoded. */
+atg_status atg_flac_decode_host(atg_decoder *dec, const uint8_t *data, uint64_t len,
+                                const atg_flac_dec_track *tracks, uint32_t n_tracks,
+                                atg_flac_dec_result *results, uint64_t *total_samples,
+                                uint64_t *total_frames);
+
+/* Copy the last decode's PCM (pcm_cap int32 samples) and, per FLAC frame,
+   its byte offset from the track's first frame and its header block size
+   (what FlacDecoder.offsets() reports, flac.c:365-443).  Any may be NULL. */
+atg_status atg_flac_decode_fetch(atg_decoder *dec, int32_t *pcm, uint64_t pcm_cap,
+                                 uint64_t *frame_offsets, uint32_t *frame_block_sizes,
+                                 uint64_t frame_cap);
+
+/* Decode a batch already in device memory (4-byte aligned, readable up to
+   len rounded up to 4).  *d_pcm receives the decoder-owned device PCM
+   (valid until the next call). */
+atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t len,
+                                  const atg_flac_dec_track *tracks, uint32_t n_tracks,
+                                  atg_flac_dec_result *results, const int32_t **d_pcm,
+                                  uint64_t *total_samples);
+
+/* Per-kernel device time of the decoder's most recent batch (HIP events). */
+int atg_decoder_kernel_times(atg_decoder *dec, const char **names, float *ms, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,6 +31,9 @@ EXPORTS = (
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_device", "atg_engine_kernel_times", "atg_device_alloc",
     "atg_device_free", "atg_copy_to_device", "atg_copy_to_host",
+    "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
+    "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
+    "atg_flac_decode_device", "atg_decoder_kernel_times",
 )
 
 c_u32, c_i32, c_u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
@@ -59,6 +62,53 @@ class TrackResult(ctypes.Structure):
                 ("min_frame_bytes", c_u32), ("max_frame_bytes", c_u32),
                 ("md5", ctypes.c_uint8 * 16), ("status", c_i32),
                 ("reserved", c_u32)]
+
+
+class StreamInfo(ctypes.Structure):
+    _fields_ = [("min_block_size", c_u32), ("max_block_size", c_u32),
+                ("min_frame_size", c_u32), ("max_frame_size", c_u32),
+                ("sample_rate", c_u32), ("channels", c_u32),
+                ("bits_per_sample", c_u32), ("channel_mask", c_u32),
+                ("total_samples", c_u64), ("md5", ctypes.c_uint8 * 16),
+                ("frames_offset", c_u64), ("n_seekpoints", c_u32),
+                ("reserved", c_u32)]
+
+
+class SeekPoint(ctypes.Structure):
+    _fields_ = [("sample_number", c_u64), ("byte_offset", c_u64),
+                ("samples", c_u32), ("reserved", c_u32)]
+
+
+class DecTrack(ctypes.Structure):
+    _fields_ = [("data_offset", c_u64), ("data_bytes", c_u64),
+                ("total_samples", c_u64), ("sample_rate", c_u32),
+                ("channels", c_u32), ("bits_per_sample", c_u32),
+                ("max_block_size", c_u32), ("md5", ctypes.c_uint8 * 16)]
+
+
+class DecResult(ctypes.Structure):
+    _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64),
+                ("first_frame", c_u32), ("n_frames", c_u32),
+                ("status", c_i32), ("reserved", c_u32),
+                ("md5", ctypes.c_uint8 * 16)]
+
+
+# decode status codes (include/atgpu.h ATG_FD_*) and the reference's
+# messages for them (src/decoders/flac.c FlacDecoder_strerror, read())
+FD_OK, FD_FRAME_CRC, FD_EOF, FD_MD5 = 0, 14, 15, 16
+FD_MESSAGES = {
+    1: "Error", 2: "invalid sync code", 3: "invalid reserved bit",
+    4: "invalid bits per sample", 5: "invalid sample rate",
+    6: "invalid checksum in frame header",
+    7: "frame sample rate does not match STREAMINFO sample rate",
+    8: "frame channel count does not match STREAMINFO channel count",
+    9: "frame bits-per-sample does not match STREAMINFO bits per sample",
+    10: "frame block size exceeds STREAMINFO's maximum block size",
+    11: "invalid residual partition coding method",
+    12: "invalid FIXED subframe order", 13: "invalid subframe type",
+    14: "invalid checksum in frame", 15: "EOF reading frame",
+    16: "MD5 mismatch at end of stream",
+}
 
 
 class ATGError(RuntimeError):
@@ -117,6 +167,28 @@ def load_library():
         lib.atg_copy_to_device.restype = ctypes.c_int
         lib.atg_copy_to_host.argtypes = [P, P, P, c_u64]
         lib.atg_copy_to_host.restype = ctypes.c_int
+        lib.atg_flac_read_metadata.argtypes = [
+            ctypes.c_char_p, c_u64, ctypes.POINTER(StreamInfo), P, c_u32]
+        lib.atg_flac_read_metadata.restype = ctypes.c_int
+        lib.atg_decoder_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        lib.atg_decoder_create.restype = ctypes.c_int
+        lib.atg_decoder_destroy.argtypes = [P]
+        lib.atg_decoder_destroy.restype = None
+        lib.atg_decoder_last_error.restype = ctypes.c_char_p
+        lib.atg_flac_decode_host.argtypes = [
+            P, P, c_u64, ctypes.POINTER(DecTrack), c_u32, ctypes.POINTER(DecResult),
+            ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
+        lib.atg_flac_decode_host.restype = ctypes.c_int
+        lib.atg_flac_decode_fetch.argtypes = [P, P, c_u64, P, P, c_u64]
+        lib.atg_flac_decode_fetch.restype = ctypes.c_int
+        lib.atg_flac_decode_device.argtypes = [
+            P, P, c_u64, ctypes.POINTER(DecTrack), c_u32, ctypes.POINTER(DecResult),
+            ctypes.POINTER(P), ctypes.POINTER(c_u64)]
+        lib.atg_flac_decode_device.restype = ctypes.c_int
+        lib.atg_decoder_kernel_times.argtypes = [
+            P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
+            ctypes.c_int]
+        lib.atg_decoder_kernel_times.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -249,8 +321,106 @@ class Engine(object):
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
+def read_metadata(data, sp_cap=4096):
+    """flacdec_read_metadata over an in-memory image (host C in libatgpu).
+    -> (rc, StreamInfo, [(sample_number, byte_offset, samples)]);
+    rc 0 ok, 1 not a FLAC stream, 2 EOF"""
+    lib = load_library()
+    si = StreamInfo()
+    sp = (SeekPoint * max(1, sp_cap))()
+    rc = lib.atg_flac_read_metadata(bytes(data), len(data), ctypes.byref(si),
+                                    ctypes.cast(sp, ctypes.c_void_p), sp_cap)
+    pts = [(sp[i].sample_number, sp[i].byte_offset, sp[i].samples)
+           for i in range(min(si.n_seekpoints, sp_cap))]
+    return rc, si, pts
+
+
+def dec_track(offset, nbytes, si):
+    """DecTrack for a stream whose first frame is at `offset` of the batch"""
+    t = DecTrack()
+    t.data_offset = offset
+    t.data_bytes = nbytes
+    t.total_samples = si.total_samples
+    t.sample_rate = si.sample_rate
+    t.channels = si.channels
+    t.bits_per_sample = si.bits_per_sample
+    t.max_block_size = si.max_block_size
+    t.md5[:] = bytes(si.md5)
+    return t
+
+
+class Decoder(object):
+    """one libatgpu FLAC decoder (HIP stream + workspace) on one device"""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        self._check(self.lib.atg_decoder_create(int(device), ctypes.byref(h)))
+        self.handle = h
+
+    def _check(self, status):
+        if status != ATG_OK:
+            raise ATGError(status, self.lib.atg_decoder_last_error().decode(
+                "utf-8", "replace"))
+
+    def close(self):
+        if self.handle:
+            self.lib.atg_decoder_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, data, tracks, fetch_pcm=True):
+        """decode a batch in host memory.  data: bytes-like holding every
+        stream; tracks: list of DecTrack.  -> (pcm int32 array, [DecResult],
+        frame byte offsets (uint64), frame block sizes (uint32)); pcm is
+        None when fetch_pcm is false (results carry the PCM MD5s)"""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        n = len(tracks)
+        arr = (DecTrack * max(1, n))(*tracks)
+        res = (DecResult * max(1, n))()
+        ns, nf = c_u64(), c_u64()
+        self._check(self.lib.atg_flac_decode_host(
+            self.handle, buf.ctypes.data_as(ctypes.c_void_p), len(buf), arr, n, res,
+            ctypes.byref(ns), ctypes.byref(nf)))
+        pcm = np.empty(max(1, ns.value), dtype=np.int32) if fetch_pcm else None
+        offs = np.empty(max(1, nf.value), dtype=np.uint64)
+        bss = np.empty(max(1, nf.value), dtype=np.uint32)
+        self._check(self.lib.atg_flac_decode_fetch(
+            self.handle, pcm.ctypes.data_as(ctypes.c_void_p) if fetch_pcm else None,
+            ns.value, offs.ctypes.data_as(ctypes.c_void_p),
+            bss.ctypes.data_as(ctypes.c_void_p), nf.value))
+        return (pcm[:ns.value] if fetch_pcm else None, [res[i] for i in range(n)],
+                offs[:nf.value], bss[:nf.value])
+
+    def decode_device(self, d_data, nbytes, tracks):
+        """decode a batch already in device memory -> ([DecResult],
+        device pointer of the int32 PCM, interleaved samples)"""
+        n = len(tracks)
+        arr = (DecTrack * max(1, n))(*tracks)
+        res = (DecResult * max(1, n))()
+        dp = ctypes.c_void_p()
+        ns = c_u64()
+        self._check(self.lib.atg_flac_decode_device(
+            self.handle, ctypes.c_void_p(d_data), nbytes, arr, n, res, ctypes.byref(dp),
+            ctypes.byref(ns)))
+        return [res[i] for i in range(n)], dp.value, ns.value
+
+    def kernel_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self.lib.atg_decoder_kernel_times(self.handle, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
 _engine = None
 _engine_lock = threading.Lock()
+_decoder = None
 
 
 def default_device():
@@ -267,3 +437,12 @@ def engine():
         if _engine is None:
             _engine = Engine(default_device())
         return _engine
+
+
+def decoder():
+    """process-wide FLAC decoder on ATG_DEVICE / LOCAL_RANK / device 0"""
+    global _decoder
+    with _engine_lock:
+        if _decoder is None:
+            _decoder = Decoder(default_device())
+        return _decoder

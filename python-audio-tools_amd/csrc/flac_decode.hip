@@ -1,0 +1,1268 @@
+// flac_decode.hip — MI355X batch FLAC decoder (SURVEY §8(a) rows D1–D5,
+// §8(f) rank 1): the frame loop of the reference's FlacDecoder.read()
+// (src/decoders/flac.c:174-285), its frame header / subframe / residual
+// readers (flac.c:710-1209) and channel decorrelation (flac.c:1212-1269),
+// error for error, for a whole batch of .flac images at once.
+//
+// A FLAC stream has no frame index, and a frame's length is only known once
+// its residuals are parsed, so the serial loop is split into passes that are
+// each parallel:
+//
+//   K1 k_dec_scan      thread per 4 input bytes: every byte that starts a
+//                      sync code gets a full frame-header parse (CRC-8 and
+//                      STREAMINFO consistency, flac.c:710-851); survivors are
+//                      "candidates" (cand_pos[i], cand_idx[byte] = i).
+//   K2 k_dec_parse     lane per candidate (grid-stride): parse the subframes
+//                      (Rice codes included) without reconstructing samples,
+//                      CRC-16 the frame; record status, length, and the bit
+//                      offset of every subframe.
+//   K3 k_dec_chain     lane per track: walk first frame -> frame end -> ...
+//                      exactly as the reference's read() loop (remaining
+//                      samples, uint64 wrap); a position that is not a
+//                      candidate, or a frame truncated by `remaining`, is
+//                      parsed inline.  Pass 1 counts, pass 2 (after a host
+//                      prefix over tracks) writes the frame and subframe jobs.
+//   K4 k_dec_subframe  lane per (frame, channel): restart at the recorded bit
+//                      offset, Rice-decode and restore FIXED/LPC samples with
+//                      the predictor history in registers (one instantiation
+//                      per order), planar output.
+//   K5 k_dec_interleave block per frame: decorrelate (L-S, S-R, mid-side),
+//                      interleave to the FrameList layout (int32), and emit
+//                      the little-endian PCM byte stream the MD5 hashes.
+//   K6 k_bytes_md5     lane per track (md5.hip): STREAMINFO MD5 check input.
+//
+// Only K2 and K4 do real work; K1 and K5 are HBM passes.  Status codes are
+// the FD_* values of include/atgpu.h (the reference's flac_status plus the
+// conditions read() raises itself).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/atgpu.h"
+#include "launch.h"
+
+namespace {
+
+enum {
+    FD_OK = 0, FD_ERROR = 1, FD_SYNC = 2, FD_RESERVED = 3, FD_BPS = 4, FD_RATE = 5,
+    FD_HDR_CRC = 6, FD_RATE_MISMATCH = 7, FD_CH_MISMATCH = 8, FD_BPS_MISMATCH = 9,
+    FD_MAXBS = 10, FD_CODING = 11, FD_FIXED_ORDER = 12, FD_SUBFRAME_TYPE = 13,
+    FD_FRAME_CRC = 14, FD_EOF = 15, FD_MD5 = 16
+};
+
+__constant__ uint8_t c_crc8[256];
+__constant__ uint16_t c_crc16[4][256];
+
+struct DecTrack {
+    uint64_t start;     // absolute byte of the first frame
+    uint64_t end;       // absolute byte end of the track image
+    uint64_t total;     // STREAMINFO total samples (remaining_samples)
+    uint32_t rate, channels, bps, max_bs;
+    uint64_t frame_base; // pass 2: first DecFrame slot
+    uint64_t pcm_base;   // pass 2: first interleaved sample of the output
+    uint64_t md5_base;   // pass 2: first byte of the track's PCM byte stream
+    uint64_t job_base;   // pass 2: first (frame, channel) job
+};
+
+struct DecCount {
+    uint64_t pcm_frames;
+    uint32_t n_frames;
+    int32_t status;
+};
+
+struct ParseRec {
+    int32_t status;
+    uint32_t bs;        // header block size
+    uint32_t bytes;     // whole frame incl. CRC-16
+    uint8_t assign, ch, bps, pad;
+    uint32_t sub_bit[8]; // bit offset of each subframe from the frame start
+};
+
+struct DecFrame {
+    uint64_t pos;       // absolute byte of the frame
+    uint64_t pcm_start; // first interleaved sample of the frame in the output
+    uint32_t n;         // samples per channel decoded (MIN(bs, remaining))
+    uint32_t track;
+    uint32_t bs;
+    uint8_t assign, ch, bps, pad;
+    uint32_t sub_bit[8];
+};
+
+struct Hdr {
+    uint32_t bs, rate, assign, ch, bps;
+};
+
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+
+// MSB-first bit reader over the batch buffer (big-endian 32-bit words).
+// `cache` holds bits [32*cw, 32*cw + 64); 0 <= off < 32 between calls, so
+// peek32() always has 32 valid bits.  The word after the cache is loaded one
+// refill ahead (`nxt`) to keep HBM latency off the decode chain.  Reading
+// past the track end is not trapped per bit: eof() compares the position
+// with the end (any read past the end makes the reference report EOF,
+// flac.c:1187-1209 br_abort), and loads are clamped to the buffer.
+struct BitR {
+    const uint32_t *w;
+    uint64_t nw;
+    uint64_t cw;
+    uint64_t cache;
+    uint32_t nxt;
+    uint32_t off;
+    uint64_t endbit;
+
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const
+    {
+        return bswap32(w[i < nw ? i : nw - 1]);
+    }
+    __device__ __forceinline__ void seek(uint64_t bit)
+    {
+        cw = bit >> 5;
+        off = (uint32_t)(bit & 31);
+        cache = ((uint64_t)ld(cw) << 32) | ld(cw + 1);
+        nxt = ld(cw + 2);
+    }
+    __device__ __forceinline__ uint64_t pos() const { return cw * 32 + off; }
+    __device__ __forceinline__ bool eof() const { return pos() > endbit; }
+    __device__ __forceinline__ uint32_t peek32() const { return (uint32_t)((cache << off) >> 32); }
+    __device__ __forceinline__ void adv()
+    {
+        cache = (cache << 32) | nxt;
+        ++cw;
+        nxt = ld(cw + 2);
+    }
+    __device__ __forceinline__ void skip(uint32_t n) // n <= 32
+    {
+        off += n;
+        if (off >= 32) {
+            off -= 32;
+            adv();
+        }
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t n) // n <= 32
+    {
+        const uint32_t v = n ? peek32() >> (32 - n) : 0u;
+        skip(n);
+        return v;
+    }
+    // br_read_signed_bits_be (src/bitstream.c:418-425)
+    __device__ __forceinline__ int32_t get_signed(uint32_t n)
+    {
+        if (n == 0) { // asks for 2^32-1 magnitude bits: always EOF
+            seek(endbit + 1);
+            return 0;
+        }
+        if (n > 33) {
+            seek(pos() + n);
+            return 0;
+        }
+        const uint32_t sign = get(1);
+        const uint32_t v = n > 1 ? get(n - 1) : 0u;
+        return sign ? (int32_t)(v - (1u << ((n - 1) & 31))) : (int32_t)v;
+    }
+    // read_unary(stop=1): number of 0 bits before a 1
+    __device__ __forceinline__ uint32_t zeros()
+    {
+        uint32_t q = 0;
+        for (;;) {
+            const uint32_t p = peek32();
+            if (p) {
+                const uint32_t z = __builtin_clz(p);
+                skip(z + 1);
+                return q + z;
+            }
+            q += 32;
+            skip(32);
+            if (eof())
+                return q;
+        }
+    }
+};
+
+__device__ __forceinline__ uint32_t byte_at(const uint32_t *w, uint64_t i)
+{
+    return (bswap32(w[i >> 2]) >> (24 - 8 * (uint32_t)(i & 3))) & 0xFFu;
+}
+
+#define RET(code) return r.eof() ? FD_EOF : (code)
+
+// flacdec_read_frame_header (flac.c:710-851)
+__device__ int dec_header(BitR &r, const DecTrack &t, Hdr &h)
+{
+    const uint64_t start = r.pos();
+    if (r.get(14) != 0x3FFEu) RET(FD_SYNC);
+    if (r.get(1)) RET(FD_RESERVED);
+    r.get(1); // blocking strategy
+    const uint32_t bs_bits = r.get(4), sr_bits = r.get(4);
+    h.assign = r.get(4);
+    h.ch = (h.assign >= 8 && h.assign <= 10) ? 2u : h.assign + 1u;
+    switch (r.get(3)) {
+    case 0: h.bps = t.bps; break;
+    case 1: h.bps = 8; break;
+    case 2: h.bps = 12; break;
+    case 4: h.bps = 16; break;
+    case 5: h.bps = 20; break;
+    case 6: h.bps = 24; break;
+    default: RET(FD_BPS);
+    }
+    r.get(1);
+    // read_utf8 (flac.c:1310-1320): leading 1 bits count the bytes
+    uint32_t nbytes = __builtin_clz(~r.peek32() | 1u);
+    if (nbytes > 7)
+        return FD_EOF;
+    r.skip(nbytes + 1);
+    r.get(7 - nbytes);
+    for (; nbytes > 1; nbytes--)
+        r.get(8);
+    switch (bs_bits) {
+    case 0: h.bs = t.max_bs; break;
+    case 6: h.bs = r.get(8) + 1; break;
+    case 7: h.bs = r.get(16) + 1; break;
+    case 1: h.bs = 192; break;
+    case 2: case 3: case 4: case 5: h.bs = 576u << (bs_bits - 2); break;
+    default: h.bs = 256u << (bs_bits - 8); break;
+    }
+    switch (sr_bits) {
+    case 0: h.rate = t.rate; break;
+    case 1: h.rate = 88200; break;
+    case 2: h.rate = 176400; break;
+    case 3: h.rate = 192000; break;
+    case 4: h.rate = 8000; break;
+    case 5: h.rate = 16000; break;
+    case 6: h.rate = 22050; break;
+    case 7: h.rate = 24000; break;
+    case 8: h.rate = 32000; break;
+    case 9: h.rate = 44100; break;
+    case 10: h.rate = 48000; break;
+    case 11: h.rate = 96000; break;
+    case 12: h.rate = r.get(8) * 1000; break;
+    case 13: h.rate = r.get(16); break;
+    case 14: h.rate = r.get(16) * 10; break;
+    default: RET(FD_RATE);
+    }
+    r.get(8);
+    if (r.eof())
+        return FD_EOF;
+    uint32_t crc = 0;
+    for (uint64_t i = start >> 3; i < (r.pos() >> 3); ++i)
+        crc = c_crc8[crc ^ byte_at(r.w, i)];
+    if (crc)
+        return FD_HDR_CRC;
+    if (t.rate != h.rate) return FD_RATE_MISMATCH;
+    if (t.channels != h.ch) return FD_CH_MISMATCH;
+    if (t.bps != h.bps) return FD_BPS_MISMATCH;
+    if (h.bs > t.max_bs) return FD_MAXBS;
+    return FD_OK;
+}
+
+// sample sinks for the residual reader: NullPred only parses (K2), the
+// Fixed/Lpc predictors restore samples with their history in registers (K4)
+struct NullPred {
+    __device__ __forceinline__ void operator()(int32_t) {}
+};
+
+template <int O>
+struct FixedPred {
+    int32_t *out;
+    uint32_t i, n, wasted;
+    uint32_t h[O > 0 ? O : 1]; // h[0] newest
+    __device__ __forceinline__ void operator()(int32_t rv)
+    {
+        uint32_t v;
+        if (O == 0) v = 0;
+        else if (O == 1) v = h[0];
+        else if (O == 2) v = 2u * h[0] - h[1];
+        else if (O == 3) v = 3u * h[0] - 3u * h[1] + h[2];
+        else v = 4u * h[0] - 6u * h[1] + 4u * h[2] - h[3];
+        const uint32_t s = v + (uint32_t)rv;
+#pragma unroll
+        for (int j = O - 1; j > 0; --j)
+            h[j] = h[j - 1];
+        if (O > 0)
+            h[0] = s;
+        if (i < n)
+            out[i] = (int32_t)(s << wasted);
+        ++i;
+    }
+};
+
+template <int O>
+struct LpcPred {
+    int32_t *out;
+    uint32_t i, n, wasted, shift;
+    int32_t c[O];
+    int32_t h[O]; // h[0] newest
+    __device__ __forceinline__ void operator()(int32_t rv)
+    {
+        int64_t acc = 0;
+#pragma unroll
+        for (int j = 0; j < O; ++j)
+            acc += (int64_t)c[j] * (int64_t)h[j];
+        const int32_t s = (int32_t)((uint32_t)(int32_t)(acc >> shift) + (uint32_t)rv);
+#pragma unroll
+        for (int j = O - 1; j > 0; --j)
+            h[j] = h[j - 1];
+        h[0] = s;
+        if (i < n)
+            out[i] = (int32_t)((uint32_t)s << wasted);
+        ++i;
+    }
+};
+
+// flacdec_read_residual (flac.c:1135-1209), samples handed to `pred`
+template <class P>
+__device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &pred)
+{
+    const uint32_t method = r.get(2);
+    const uint32_t porder = r.get(4);
+    // a partition order that does not divide the block: rejected (the
+    // reference would predict from a stale buffer), as the oracle does
+    if (!r.eof() && method <= 1 && ((N >> porder) << porder) != N)
+        return FD_ERROR;
+    const uint32_t parts = 1u << porder;
+    for (uint32_t part = 0; part < parts; ++part) {
+        int plen = (int)(N >> porder);
+        if (part == 0) {
+            plen -= (int)order;
+            if (plen < 0)
+                plen = 0;
+        }
+        uint32_t rice, esc;
+        if (method == 0) {
+            rice = r.get(4);
+            esc = rice == 0xF ? r.get(5) : 0u;
+        } else if (method == 1) {
+            rice = r.get(5);
+            esc = rice == 0x1F ? r.get(5) : 0u;
+        } else {
+            RET(FD_CODING);
+        }
+        if (r.eof())
+            return FD_EOF;
+        if (!esc) {
+            for (; plen; --plen) {
+                const uint32_t msb = r.zeros();
+                const uint32_t lsb = r.get(rice);
+                const uint32_t value = (msb << rice) | lsb;
+                const int32_t sv = (int32_t)value >> 1;
+                pred((value & 1u) ? -sv - 1 : sv);
+            }
+        } else {
+            for (; plen; --plen)
+                pred(r.get_signed(esc));
+        }
+        if (r.eof())
+            return FD_EOF;
+    }
+    return FD_OK;
+}
+
+struct SubHdr {
+    uint32_t kind, order, wasted;
+};
+
+// subframe header (flac.c:854-905)
+__device__ __forceinline__ int dec_subhdr(BitR &r, SubHdr &s)
+{
+    r.get(1);
+    const uint32_t t = r.get(6);
+    if (t == 0) { s.kind = 0; s.order = 0; }
+    else if (t == 1) { s.kind = 1; s.order = 0; }
+    else if ((t & 0x38) == 0x08) { s.kind = 2; s.order = t & 7; }
+    else if ((t & 0x20) == 0x20) { s.kind = 3; s.order = (t & 0x1F) + 1; }
+    else RET(FD_SUBFRAME_TYPE);
+    s.wasted = 0;
+    if (r.get(1))
+        s.wasted = r.zeros() + 1;
+    if (r.eof())
+        return FD_EOF;
+    return FD_OK;
+}
+
+// parse-only subframe (K2 and the chain's inline path)
+__device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps)
+{
+    SubHdr sh;
+    int rc = dec_subhdr(r, sh);
+    if (rc)
+        return rc;
+    bps -= sh.wasted; // unsigned, as the reference
+    NullPred np;
+    if (sh.kind == 0) {
+        r.get_signed(bps);
+    } else if (sh.kind == 1) {
+        for (uint32_t i = 0; i < N; ++i) {
+            r.get_signed(bps);
+            if ((i & 255) == 255 && r.eof())
+                break;
+        }
+    } else {
+        for (uint32_t i = 0; i < sh.order; ++i)
+            r.get_signed(bps);
+        if (sh.kind == 3) {
+            const uint32_t prec = r.get(4) + 1;
+            r.get_signed(5);
+            for (uint32_t i = 0; i < sh.order; ++i)
+                r.get_signed(prec);
+        }
+        rc = dec_residual(r, sh.order, N, np);
+        if (rc)
+            return rc;
+        if (sh.kind == 2 && sh.order > 4)
+            return FD_FIXED_ORDER;
+    }
+    if (r.eof())
+        return FD_EOF;
+    return FD_OK;
+}
+
+__device__ __forceinline__ uint32_t sub_bps(uint32_t assign, uint32_t c, uint32_t bps)
+{
+    return ((assign == 8 && c == 1) || (assign == 9 && c == 0) || (assign == 10 && c == 1))
+               ? bps + 1 : bps;
+}
+
+// CRC-16 (0x8005) of bytes [b0, b1), slicing by 4 with tables in LDS
+__device__ uint32_t crc16_range(const uint32_t *w, uint64_t b0, uint64_t b1,
+                                const uint16_t (*T)[256])
+{
+    uint32_t crc = 0;
+    uint64_t i = b0;
+    for (; i < b1 && (i & 3); ++i)
+        crc = ((crc << 8) & 0xFFFFu) ^ T[0][(crc >> 8) ^ byte_at(w, i)];
+    for (; i + 4 <= b1; i += 4) {
+        const uint32_t x = bswap32(w[i >> 2]) ^ (crc << 16);
+        crc = (uint32_t)T[3][x >> 24] ^ T[2][(x >> 16) & 0xFF] ^ T[1][(x >> 8) & 0xFF] ^
+              T[0][x & 0xFF];
+    }
+    for (; i < b1; ++i)
+        crc = ((crc << 8) & 0xFFFFu) ^ T[0][(crc >> 8) ^ byte_at(w, i)];
+    return crc;
+}
+
+// one frame of the reference's read() loop, parse only: header, subframes
+// with N = MIN(block size, nlimit), byte align, CRC-16
+__device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const DecTrack &t,
+                            uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec)
+{
+    BitR r;
+    r.w = w;
+    r.nw = nw;
+    r.endbit = t.end * 8;
+    r.seek(pos * 8);
+    Hdr h;
+    rec.bytes = 0;
+    rec.status = dec_header(r, t, h);
+    if (rec.status)
+        return;
+    rec.bs = h.bs;
+    rec.assign = (uint8_t)h.assign;
+    rec.ch = (uint8_t)h.ch;
+    rec.bps = (uint8_t)h.bps;
+    const uint32_t N = (uint32_t)((uint64_t)h.bs < nlimit ? (uint64_t)h.bs : nlimit);
+    for (uint32_t c = 0; c < h.ch; ++c) {
+        rec.sub_bit[c] = (uint32_t)(r.pos() - pos * 8);
+        const int rc = parse_subframe(r, N, sub_bps(h.assign, c, h.bps));
+        if (rc) {
+            rec.status = rc;
+            return;
+        }
+    }
+    const uint32_t a = (uint32_t)(r.pos() & 7);
+    if (a)
+        r.skip(8 - a);
+    r.get(16);
+    if (r.eof()) {
+        rec.status = FD_EOF;
+        return;
+    }
+    const uint64_t endb = r.pos() >> 3;
+    rec.bytes = (uint32_t)(endb - pos);
+    rec.status = crc16_range(w, pos, endb, T) ? FD_FRAME_CRC : FD_OK;
+}
+
+__device__ __forceinline__ void load_crc_lds(uint16_t (*T)[256])
+{
+    for (uint32_t i = threadIdx.x; i < 4 * 256; i += blockDim.x)
+        T[i >> 8][i & 255] = c_crc16[i >> 8][i & 255];
+    __syncthreads();
+}
+
+__device__ __forceinline__ uint32_t find_track(const DecTrack *tr, uint32_t nt, uint64_t p)
+{
+    // last track with start <= p (tracks sorted by start)
+    uint32_t lo = 0, hi = nt;
+    while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (tr[mid].start <= p) lo = mid;
+        else hi = mid;
+    }
+    return lo;
+}
+
+// K1: sync-code candidates.  Thread per 32-bit word; a position needs byte
+// 0xFF followed by 0xF8/0xF9 (14-bit sync 0x3FFE, reserved bit 0).
+__global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w, uint64_t nw,
+                                                  uint64_t len, const DecTrack *__restrict__ tr,
+                                                  uint32_t nt, uint32_t *__restrict__ ncand,
+                                                  uint64_t *__restrict__ cand_pos,
+                                                  uint32_t *__restrict__ cand_idx)
+{
+    const uint64_t gw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (gw >= nw)
+        return;
+    const uint32_t a = bswap32(w[gw]);
+    const uint32_t b = gw + 1 < nw ? bswap32(w[gw + 1]) : 0u;
+    const uint64_t pair = ((uint64_t)a << 32) | b;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t hi = (uint32_t)(pair >> (48 - 8 * k)) & 0xFFFFu;
+        if ((hi & 0xFFFEu) != 0xFFF8u)
+            continue;
+        const uint64_t p = gw * 4 + k;
+        if (p + 1 >= len)
+            continue;
+        const uint32_t t = find_track(tr, nt, p);
+        const DecTrack T = tr[t];
+        if (p < T.start || p >= T.end)
+            continue;
+        BitR r;
+        r.w = w;
+        r.nw = nw;
+        r.endbit = T.end * 8;
+        r.seek(p * 8);
+        Hdr h;
+        if (dec_header(r, T, h) != FD_OK)
+            continue;
+        const uint32_t i = atomicAdd(ncand, 1u);
+        cand_pos[i] = p;
+        cand_idx[p] = i;
+    }
+}
+
+// K2: parse every candidate frame (grid-stride; the count lives on device)
+__global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w, uint64_t nw,
+                                                  const DecTrack *__restrict__ tr, uint32_t nt,
+                                                  const uint32_t *__restrict__ ncand,
+                                                  const uint64_t *__restrict__ cand_pos,
+                                                  ParseRec *__restrict__ recs)
+{
+    __shared__ uint16_t T[4][256];
+    load_crc_lds(T);
+    const uint32_t n = *ncand;
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
+        const uint64_t p = cand_pos[i];
+        const DecTrack t = tr[find_track(tr, nt, p)];
+        ParseRec rec;
+        parse_frame(w, nw, p, t, ~0ull, T, rec);
+        recs[i] = rec;
+    }
+}
+
+// K3: the read() loop per track (flac.c:196-258); pass 1 counts, pass 2
+// writes frames and subframe jobs
+__global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w, uint64_t nw,
+                                                  const DecTrack *__restrict__ tr, uint32_t nt,
+                                                  const uint32_t *__restrict__ ncand,
+                                                  const uint64_t *__restrict__ cand_pos,
+                                                  const uint32_t *__restrict__ cand_idx,
+                                                  const ParseRec *__restrict__ recs,
+                                                  DecCount *__restrict__ counts, int pass,
+                                                  DecFrame *__restrict__ frames,
+                                                  uint2 *__restrict__ jobs)
+{
+    __shared__ uint16_t T[4][256];
+    load_crc_lds(T);
+    const uint32_t ti = blockIdx.x * blockDim.x + threadIdx.x;
+    if (ti >= nt)
+        return;
+    const DecTrack t = tr[ti];
+    const uint32_t nc = *ncand;
+    uint64_t pos = t.start, remaining = t.total, pcm = 0;
+    uint32_t nf = 0;
+    int status = FD_OK;
+    while (remaining != 0) {
+        ParseRec rec;
+        uint32_t ci = 0xFFFFFFFFu;
+        if (pos < t.end) {
+            const uint32_t c = cand_idx[pos];
+            if (c < nc && cand_pos[c] == pos)
+                ci = c;
+        }
+        if (ci != 0xFFFFFFFFu && (uint64_t)recs[ci].bs <= remaining)
+            rec = recs[ci];
+        else // not a candidate (its header fails), or truncated by remaining
+            parse_frame(w, nw, pos, t, remaining, T, rec);
+        if (rec.status) {
+            status = rec.status;
+            break;
+        }
+        const uint32_t N = (uint32_t)((uint64_t)rec.bs < remaining ? (uint64_t)rec.bs : remaining);
+        if (pass == 2) {
+            const uint64_t slot = t.frame_base + nf;
+            DecFrame f;
+            f.pos = pos;
+            f.pcm_start = t.pcm_base + pcm * t.channels;
+            f.n = N;
+            f.track = ti;
+            f.bs = rec.bs;
+            f.assign = rec.assign;
+            f.ch = rec.ch;
+            f.bps = rec.bps;
+            f.pad = 0;
+            for (int c = 0; c < 8; ++c)
+                f.sub_bit[c] = rec.sub_bit[c];
+            frames[slot] = f;
+            for (uint32_t c = 0; c < rec.ch; ++c)
+                jobs[t.job_base + (uint64_t)nf * rec.ch + c] = make_uint2((uint32_t)slot, c);
+        }
+        ++nf;
+        pcm += N;
+        pos += rec.bytes;
+        remaining -= rec.bs; // uint64, wraps as the reference's
+    }
+    if (pass == 1) {
+        DecCount dc;
+        dc.pcm_frames = pcm;
+        dc.n_frames = nf;
+        dc.status = status;
+        counts[ti] = dc;
+    }
+}
+
+template <int O>
+__device__ __noinline__ void restore_lpc(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
+                                         int32_t *out)
+{
+    LpcPred<O> p;
+    p.out = out;
+    p.n = N;
+    p.wasted = wasted;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const int32_t v = r.get_signed(bps);
+        if ((uint32_t)j < N)
+            out[j] = (int32_t)((uint32_t)v << wasted);
+        p.h[O - 1 - j] = v;
+    }
+    const uint32_t prec = r.get(4) + 1;
+    p.shift = (uint32_t)r.get_signed(5) & 63u;
+#pragma unroll
+    for (int j = 0; j < O; ++j)
+        p.c[j] = r.get_signed(prec);
+    p.i = O;
+    dec_residual(r, O, N, p);
+}
+
+template <int O>
+__device__ __noinline__ void restore_fixed(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
+                                           int32_t *out)
+{
+    FixedPred<O> p;
+    p.out = out;
+    p.n = N;
+    p.wasted = wasted;
+#pragma unroll
+    for (int j = 0; j < O; ++j) {
+        const int32_t v = r.get_signed(bps);
+        if ((uint32_t)j < N)
+            out[j] = (int32_t)((uint32_t)v << wasted);
+        p.h[O - 1 - j] = (uint32_t)v;
+    }
+    p.i = O;
+    dec_residual(r, O, N, p);
+}
+
+// K4: one subframe per lane, samples restored into the planar scratch
+__global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict__ w, uint64_t nw,
+                                                     const DecTrack *__restrict__ tr,
+                                                     const DecFrame *__restrict__ frames,
+                                                     const uint2 *__restrict__ jobs,
+                                                     uint64_t njobs, int32_t *__restrict__ planar)
+{
+    const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= njobs)
+        return;
+    const uint2 jb = jobs[j];
+    const DecFrame f = frames[jb.x];
+    const uint32_t c = jb.y;
+    BitR r;
+    r.w = w;
+    r.nw = nw;
+    r.endbit = tr[f.track].end * 8;
+    r.seek(f.pos * 8 + f.sub_bit[c]);
+    const uint32_t N = f.n;
+    int32_t *out = planar + f.pcm_start + (uint64_t)c * N;
+    SubHdr sh;
+    if (dec_subhdr(r, sh))
+        return;
+    const uint32_t bps = sub_bps(f.assign, c, f.bps) - sh.wasted;
+    const uint32_t ws = sh.wasted;
+    if (sh.kind == 0) {
+        const uint32_t v = (uint32_t)r.get_signed(bps) << ws;
+        for (uint32_t i = 0; i < N; ++i)
+            out[i] = (int32_t)v;
+    } else if (sh.kind == 1) {
+        for (uint32_t i = 0; i < N; ++i)
+            out[i] = (int32_t)((uint32_t)r.get_signed(bps) << ws);
+    } else if (sh.kind == 2) {
+        switch (sh.order) {
+        case 0: restore_fixed<0>(r, N, bps, ws, out); break;
+        case 1: restore_fixed<1>(r, N, bps, ws, out); break;
+        case 2: restore_fixed<2>(r, N, bps, ws, out); break;
+        case 3: restore_fixed<3>(r, N, bps, ws, out); break;
+        default: restore_fixed<4>(r, N, bps, ws, out); break;
+        }
+    } else {
+        switch (sh.order) {
+#define LPC_CASE(k) case k: restore_lpc<k>(r, N, bps, ws, out); break;
+            LPC_CASE(1) LPC_CASE(2) LPC_CASE(3) LPC_CASE(4) LPC_CASE(5) LPC_CASE(6)
+            LPC_CASE(7) LPC_CASE(8) LPC_CASE(9) LPC_CASE(10) LPC_CASE(11) LPC_CASE(12)
+            LPC_CASE(13) LPC_CASE(14) LPC_CASE(15) LPC_CASE(16) LPC_CASE(17) LPC_CASE(18)
+            LPC_CASE(19) LPC_CASE(20) LPC_CASE(21) LPC_CASE(22) LPC_CASE(23) LPC_CASE(24)
+            LPC_CASE(25) LPC_CASE(26) LPC_CASE(27) LPC_CASE(28) LPC_CASE(29) LPC_CASE(30)
+            LPC_CASE(31) LPC_CASE(32)
+#undef LPC_CASE
+        default: break;
+        }
+    }
+}
+
+// K5: flacdec_decorrelate_channels (flac.c:1212-1269) + interleave + the
+// little-endian signed byte stream of FrameList.to_bytes (MD5 input)
+__global__ __launch_bounds__(256) void k_dec_interleave(const DecTrack *__restrict__ tr,
+                                                        const DecFrame *__restrict__ frames,
+                                                        const int32_t *__restrict__ planar,
+                                                        int32_t *__restrict__ pcm,
+                                                        uint8_t *__restrict__ bytes)
+{
+    const DecFrame f = frames[blockIdx.x];
+    const DecTrack t = tr[f.track];
+    const uint32_t N = f.n, ch = f.ch;
+    const uint32_t bb = (t.bps + 7) / 8;
+    const int32_t *src = planar + f.pcm_start;
+    int32_t *dst = pcm + f.pcm_start;
+    uint8_t *bdst = bytes + t.md5_base + (f.pcm_start - t.pcm_base) * bb;
+    for (uint32_t k = threadIdx.x; k < N; k += blockDim.x) {
+        int32_t o[8];
+        if (f.assign >= 8 && f.assign <= 10) {
+            const int32_t a = src[k], b = src[N + k];
+            if (f.assign == 8) {
+                o[0] = a;
+                o[1] = (int32_t)((uint32_t)a - (uint32_t)b);
+            } else if (f.assign == 9) {
+                o[0] = (int32_t)((uint32_t)a + (uint32_t)b);
+                o[1] = b;
+            } else {
+                const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
+                o[0] = (int32_t)((mid + b) >> 1);
+                o[1] = (int32_t)((mid - b) >> 1);
+            }
+        } else {
+            for (uint32_t c = 0; c < ch && c < 8; ++c)
+                o[c] = src[(uint64_t)c * N + k];
+        }
+        for (uint32_t c = 0; c < ch && c < 8; ++c) {
+            const uint64_t s = (uint64_t)k * ch + c;
+            dst[s] = o[c];
+            if (bb == 2) {
+                ((int16_t *)bdst)[s] = (int16_t)o[c];
+            } else {
+                for (uint32_t q = 0; q < bb; ++q)
+                    bdst[s * bb + q] = (uint8_t)((uint32_t)o[c] >> (8 * q));
+            }
+        }
+    }
+}
+
+const int kDecTimed = 7;
+const char *kDecNames[kDecTimed] = {"dec_scan", "dec_parse", "dec_chain", "dec_subframe",
+                                    "dec_interleave", "dec_md5", "dec_total"};
+
+} // namespace
+
+thread_local std::string g_dec_err;
+
+static atg_status dfail(atg_status s, const std::string &m)
+{
+    g_dec_err = m;
+    return s;
+}
+
+#define DHIP(expr)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return dfail(ATG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct DBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    hipError_t ensure(size_t bytes)
+    {
+        if (bytes <= cap && p)
+            return hipSuccess;
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t want = std::max<size_t>(bytes, 256);
+        hipError_t e = hipMalloc(&p, want);
+        if (e == hipSuccess)
+            cap = want;
+        return e;
+    }
+    void release()
+    {
+        if (p)
+            (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct atg_decoder {
+    int device = 0;
+    hipStream_t s = nullptr;
+    hipEvent_t ev[kDecTimed + 1] = {};
+    float times[kDecTimed] = {};
+    bool have_times = false;
+    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, planar, pcm,
+        bytes, md5, md5meta;
+    // results of the last decode
+    std::vector<DecTrack> tr;
+    std::vector<DecCount> cnt;
+    uint64_t total_samples = 0, total_frames = 0;
+};
+
+static void build_dec_tables(uint8_t *t8, uint16_t t16[4][256])
+{
+    for (uint32_t b = 0; b < 256; ++b) {
+        uint32_t c8 = b;
+        for (int i = 0; i < 8; ++i)
+            c8 = (c8 & 0x80) ? ((c8 << 1) ^ 0x07) : (c8 << 1);
+        t8[b] = (uint8_t)c8;
+        uint32_t c = b << 8;
+        for (int i = 0; i < 8; ++i)
+            c = (c & 0x8000) ? ((c << 1) ^ 0x8005) : (c << 1);
+        t16[0][b] = (uint16_t)c;
+    }
+    for (int k = 1; k < 4; ++k)
+        for (uint32_t b = 0; b < 256; ++b) {
+            const uint32_t p = t16[k - 1][b];
+            t16[k][b] = (uint16_t)(((p << 8) & 0xFFFF) ^ t16[0][p >> 8]);
+        }
+}
+
+static const uint32_t kMasks[9] = {0, 0x4, 0x3, 0x7, 0x33, 0x37, 0x3F, 0x70F, 0x63F};
+
+extern "C" {
+
+const char *atg_decoder_last_error(void) { return g_dec_err.c_str(); }
+
+int atg_flac_read_metadata(const uint8_t *data, uint64_t len, atg_flac_streaminfo *si,
+                           atg_flac_seekpoint *sp, uint32_t sp_cap)
+{
+    // flacdec_read_metadata (src/decoders/flac.c:568-707) over an in-memory
+    // image: STREAMINFO, SEEKTABLE, the VORBIS_COMMENT channel-mask tag
+    if (!si || (!data && len))
+        return 1;
+    std::memset(si, 0, sizeof(*si));
+    uint64_t pos = 0; // bits
+    const uint64_t lb = len * 8;
+    bool eof = false;
+    auto get = [&](unsigned n) -> uint32_t {
+        uint32_t v = 0;
+        for (unsigned i = 0; i < n; ++i) {
+            if (pos >= lb) {
+                eof = true;
+                return 0;
+            }
+            v = (v << 1) | ((data[pos >> 3] >> (7 - (pos & 7))) & 1u);
+            ++pos;
+        }
+        return v;
+    };
+    const uint32_t magic = get(32);
+    if (eof)
+        return 2;
+    if (magic != 0x664C6143u)
+        return 1;
+    unsigned last;
+    do {
+        last = get(1);
+        const unsigned type = get(7);
+        const uint32_t blen = get(24);
+        if (eof)
+            return 2;
+        const uint64_t body = pos;
+        if (type == 0) {
+            si->min_block_size = get(16);
+            si->max_block_size = get(16);
+            si->min_frame_size = get(24);
+            si->max_frame_size = get(24);
+            si->sample_rate = get(20);
+            si->channels = get(3) + 1;
+            si->bits_per_sample = get(5) + 1;
+            si->total_samples = ((uint64_t)get(4) << 32);
+            si->total_samples |= get(32);
+            for (int i = 0; i < 16; ++i)
+                si->md5[i] = (uint8_t)get(8);
+            si->channel_mask = si->channels <= 8 ? kMasks[si->channels] : 0;
+        } else if (type == 3) {
+            const uint32_t n = blen / 18;
+            for (uint32_t k = 0; k < n; ++k) {
+                atg_flac_seekpoint p;
+                p.sample_number = (uint64_t)get(32) << 32;
+                p.sample_number |= get(32);
+                p.byte_offset = (uint64_t)get(32) << 32;
+                p.byte_offset |= get(32);
+                p.samples = get(16);
+                p.reserved = 0;
+                if (sp && k < sp_cap)
+                    sp[k] = p;
+            }
+            si->n_seekpoints = n;
+        } else if (type == 4) {
+            // flacdec_read_vorbis_comment (flac.c:508-566): little-endian
+            // lengths; a read error inside the block is swallowed
+            if (body + (uint64_t)blen * 8 > lb)
+                return 2;
+            const uint8_t *c = data + (body >> 3);
+            const size_t cl = blen;
+            size_t i = 0;
+            auto le32 = [](const uint8_t *q) {
+                return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16) |
+                       ((uint32_t)q[3] << 24);
+            };
+            if (i + 4 <= cl) {
+                const uint32_t vl = le32(c + i);
+                i += 4;
+                if (vl <= cl - i) {
+                    i += vl;
+                    if (i + 4 <= cl) {
+                        uint32_t lines = le32(c + i);
+                        i += 4;
+                        static const char pre[] = "WAVEFORMATEXTENSIBLE_CHANNEL_MASK=";
+                        for (; lines > 0; --lines) {
+                            if (i + 4 > cl)
+                                break;
+                            const uint32_t ll = le32(c + i);
+                            i += 4;
+                            if (ll > cl - i)
+                                break;
+                            char buf[256];
+                            const size_t keep = ll < 255 ? ll : 255;
+                            for (size_t k = 0; k < keep; ++k) {
+                                const char ch = (char)c[i + k];
+                                buf[k] = (ch >= 'a' && ch <= 'z') ? (char)(ch - 32) : ch;
+                            }
+                            buf[keep] = 0;
+                            if (std::strncmp(buf, pre, sizeof(pre) - 1) == 0) {
+                                const unsigned long m =
+                                    std::strtoul(buf + sizeof(pre) - 1, nullptr, 16);
+                                const unsigned mask = (unsigned)m;
+                                unsigned bits = 0;
+                                for (unsigned mm = mask; mm; mm >>= 1)
+                                    bits += mm & 1u;
+                                if (bits == si->channels)
+                                    si->channel_mask = mask;
+                            }
+                            i += ll;
+                        }
+                    }
+                }
+            }
+        }
+        if (type != 0 && type != 3)
+            pos = body + (uint64_t)blen * 8;
+        if (pos > lb)
+            return 2;
+        if (eof)
+            return 2;
+    } while (!last);
+    si->frames_offset = pos >> 3;
+    return 0;
+}
+
+atg_status atg_decoder_create(int device, atg_decoder **out)
+{
+    if (!out)
+        return dfail(ATG_ERR_INVALID, "out is NULL");
+    *out = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return dfail(ATG_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n)
+        return dfail(ATG_ERR_INVALID, "device index out of range");
+    DHIP(hipSetDevice(device));
+    static uint8_t t8[256];
+    static uint16_t t16[4][256];
+    build_dec_tables(t8, t16);
+    DHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_crc8), t8, sizeof(t8)));
+    DHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), t16, sizeof(t16)));
+    atg_decoder *d = new atg_decoder();
+    d->device = device;
+    DHIP(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
+    for (auto &e : d->ev)
+        DHIP(hipEventCreate(&e));
+    *out = d;
+    return ATG_OK;
+}
+
+void atg_decoder_destroy(atg_decoder *d)
+{
+    if (!d)
+        return;
+    (void)hipSetDevice(d->device);
+    (void)hipStreamSynchronize(d->s);
+    for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
+                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->pcm, &d->bytes, &d->md5, &d->md5meta})
+        b->release();
+    for (auto &e : d->ev)
+        (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(d->s);
+    delete d;
+}
+
+} // extern "C"
+
+// the device-resident decode of a batch already in d->data (or caller HBM)
+static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len,
+                             const atg_flac_dec_track *tracks, uint32_t n,
+                             atg_flac_dec_result *res)
+{
+    hipStream_t s = d->s;
+    d->tr.assign(n, DecTrack());
+    for (uint32_t t = 0; t < n; ++t) {
+        const atg_flac_dec_track &a = tracks[t];
+        DecTrack &b = d->tr[t];
+        if (a.data_offset > len || a.data_bytes > len - a.data_offset)
+            return dfail(ATG_ERR_INVALID, "track data range outside the buffer");
+        if (t && a.data_offset < tracks[t - 1].data_offset)
+            return dfail(ATG_ERR_INVALID, "tracks must be ordered by data_offset");
+        if (a.channels < 1 || a.channels > 8)
+            return dfail(ATG_ERR_UNSUPPORTED, "channels must be 1..8");
+        b.start = a.data_offset;
+        b.end = a.data_offset + a.data_bytes;
+        b.total = a.total_samples;
+        b.rate = a.sample_rate;
+        b.channels = a.channels;
+        b.bps = a.bits_per_sample;
+        b.max_bs = a.max_block_size;
+    }
+    const uint64_t nw = std::max<uint64_t>(1, (len + 3) / 4);
+    DHIP(d->tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
+    DHIP(d->counts.ensure(sizeof(DecCount) * std::max<uint32_t>(n, 1)));
+    DHIP(d->ncand.ensure(sizeof(uint32_t)));
+    // a frame is at least 10 bytes (header 6 + subframe 1 + CRC 2 ...), so
+    // at most len/2 positions can start candidates; sized for the worst case
+    const uint64_t max_cand = len / 2 + 1;
+    DHIP(d->cand_pos.ensure(sizeof(uint64_t) * max_cand));
+    DHIP(d->cand_idx.ensure(sizeof(uint32_t) * (len + 4)));
+    DHIP(d->recs.ensure(sizeof(ParseRec) * max_cand));
+    DHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
+    DHIP(hipMemsetAsync(d->ncand.p, 0, sizeof(uint32_t), s));
+    const uint32_t *w = (const uint32_t *)d_data;
+    DecTrack *dtr = (DecTrack *)d->tracks.p;
+    DHIP(hipEventRecord(d->ev[0], s));
+    if (n && len)
+        hipLaunchKernelGGL(k_dec_scan, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, nw,
+                           len, dtr, n, (uint32_t *)d->ncand.p, (uint64_t *)d->cand_pos.p,
+                           (uint32_t *)d->cand_idx.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[1], s));
+    hipLaunchKernelGGL(k_dec_parse, dim3(4096), dim3(64), 0, s, w, nw, dtr, n,
+                       (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
+                       (ParseRec *)d->recs.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[2], s));
+    const dim3 tg((n + 63) / 64);
+    if (n)
+        hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, dtr, n,
+                           (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
+                           (const uint32_t *)d->cand_idx.p, (const ParseRec *)d->recs.p,
+                           (DecCount *)d->counts.p, 1, (DecFrame *)nullptr, (uint2 *)nullptr);
+    DHIP(hipGetLastError());
+    d->cnt.assign(n, DecCount());
+    DHIP(hipMemcpyAsync(d->cnt.data(), d->counts.p, sizeof(DecCount) * n, hipMemcpyDeviceToHost,
+                        s));
+    DHIP(hipStreamSynchronize(s));
+    // host prefix over tracks: frame slots, PCM placement, MD5 byte streams
+    uint64_t fb = 0, pb = 0, mb = 0, jb = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        DecTrack &b = d->tr[t];
+        b.frame_base = fb;
+        b.pcm_base = pb;
+        b.md5_base = mb;
+        b.job_base = jb;
+        fb += d->cnt[t].n_frames;
+        jb += (uint64_t)d->cnt[t].n_frames * b.channels;
+        const uint64_t ns = d->cnt[t].pcm_frames * b.channels;
+        pb += ns;
+        mb += (ns * ((b.bps + 7) / 8) + 63) & ~63ull;
+    }
+    d->total_samples = pb;
+    d->total_frames = fb;
+    DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
+    DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
+    DHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    DHIP(d->pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    DHIP(d->bytes.ensure(std::max<uint64_t>(mb, 64)));
+    DHIP(d->md5.ensure(16 * std::max<uint32_t>(n, 1)));
+    DHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
+    if (n)
+        hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, dtr, n,
+                           (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
+                           (const uint32_t *)d->cand_idx.p, (const ParseRec *)d->recs.p,
+                           (DecCount *)d->counts.p, 2, (DecFrame *)d->frames.p,
+                           (uint2 *)d->jobs.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[3], s));
+    if (jb)
+        hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
+                           nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
+                           (int32_t *)d->planar.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[4], s));
+    if (fb)
+        hipLaunchKernelGGL(k_dec_interleave, dim3((unsigned)fb), dim3(256), 0, s, dtr,
+                           (const DecFrame *)d->frames.p, (const int32_t *)d->planar.p,
+                           (int32_t *)d->pcm.p, (uint8_t *)d->bytes.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[5], s));
+    std::vector<uint64_t> md5_off(n), md5_len(n);
+    for (uint32_t t = 0; t < n; ++t) {
+        md5_off[t] = d->tr[t].md5_base;
+        md5_len[t] = d->cnt[t].pcm_frames * d->tr[t].channels * ((d->tr[t].bps + 7) / 8);
+    }
+    DBuf &mb_buf = d->md5meta;
+    DHIP(mb_buf.ensure(sizeof(uint64_t) * 2 * std::max<uint32_t>(n, 1)));
+    DHIP(hipMemcpyAsync(mb_buf.p, md5_off.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
+    DHIP(hipMemcpyAsync((uint64_t *)mb_buf.p + n, md5_len.data(), sizeof(uint64_t) * n,
+                        hipMemcpyHostToDevice, s));
+    DHIP(launch_bytes_md5((const uint8_t *)d->bytes.p, (const uint64_t *)mb_buf.p,
+                          (const uint64_t *)mb_buf.p + n, n, (uint8_t *)d->md5.p, s));
+    DHIP(hipEventRecord(d->ev[6], s));
+    std::vector<uint8_t> md5(16 * (size_t)n);
+    if (n)
+        DHIP(hipMemcpyAsync(md5.data(), d->md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s));
+    DHIP(hipStreamSynchronize(s));
+    // timings: scan, parse, chain (both passes + the host prefix), subframe,
+    // interleave, md5, total
+    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
+    for (int k = 0; k < kDecTimed; ++k)
+        (void)hipEventElapsedTime(&d->times[k], d->ev[map[k][0]], d->ev[map[k][1]]);
+    d->have_times = true;
+    static const uint8_t zero[16] = {0};
+    uint64_t fbase = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        atg_flac_dec_result &r = res[t];
+        r.pcm_offset = d->tr[t].pcm_base / d->tr[t].channels;
+        r.pcm_frames = d->cnt[t].pcm_frames;
+        r.first_frame = (uint32_t)fbase;
+        r.n_frames = d->cnt[t].n_frames;
+        fbase += r.n_frames;
+        std::memcpy(r.md5, &md5[16 * (size_t)t], 16);
+        r.status = d->cnt[t].status;
+        // FlacDecoder_verify_okay (flac.c:479-493) once remaining reaches 0
+        if (r.status == FD_OK && std::memcmp(tracks[t].md5, zero, 16) != 0 &&
+            std::memcmp(tracks[t].md5, r.md5, 16) != 0)
+            r.status = FD_MD5;
+        r.reserved = 0;
+    }
+    return ATG_OK;
+}
+
+extern "C" {
+
+atg_status atg_flac_decode_device(atg_decoder *d, const void *d_data, uint64_t len,
+                                  const atg_flac_dec_track *tracks, uint32_t n,
+                                  atg_flac_dec_result *results, const int32_t **d_pcm,
+                                  uint64_t *total_samples)
+{
+    if (!d || (!tracks && n) || (!results && n) || (!d_data && len))
+        return dfail(ATG_ERR_INVALID, "NULL argument");
+    if (((uintptr_t)d_data) & 3)
+        return dfail(ATG_ERR_INVALID, "d_data must be 4-byte aligned");
+    DHIP(hipSetDevice(d->device));
+    atg_status st = run_decode(d, (const uint8_t *)d_data, len, tracks, n, results);
+    if (st != ATG_OK)
+        return st;
+    if (d_pcm)
+        *d_pcm = (const int32_t *)d->pcm.p;
+    if (total_samples)
+        *total_samples = d->total_samples;
+    return ATG_OK;
+}
+
+atg_status atg_flac_decode_host(atg_decoder *d, const uint8_t *data, uint64_t len,
+                                const atg_flac_dec_track *tracks, uint32_t n,
+                                atg_flac_dec_result *results, uint64_t *total_samples,
+                                uint64_t *total_frames)
+{
+    if (!d || (!tracks && n) || (!results && n) || (!data && len))
+        return dfail(ATG_ERR_INVALID, "NULL argument");
+    DHIP(hipSetDevice(d->device));
+    DHIP(d->data.ensure(len + 64));
+    DHIP(hipMemsetAsync((uint8_t *)d->data.p + (len & ~3ull), 0, 64, d->s));
+    if (len)
+        DHIP(hipMemcpyAsync(d->data.p, data, len, hipMemcpyHostToDevice, d->s));
+    atg_status st = run_decode(d, (const uint8_t *)d->data.p, len, tracks, n, results);
+    if (st != ATG_OK)
+        return st;
+    if (total_samples)
+        *total_samples = d->total_samples;
+    if (total_frames)
+        *total_frames = d->total_frames;
+    return ATG_OK;
+}
+
+atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
+                                 uint64_t *frame_offsets, uint32_t *frame_block_sizes,
+                                 uint64_t frame_cap)
+{
+    if (!d)
+        return dfail(ATG_ERR_INVALID, "NULL decoder");
+    if ((pcm && pcm_cap < d->total_samples) ||
+        ((frame_offsets || frame_block_sizes) && frame_cap < d->total_frames))
+        return dfail(ATG_ERR_CAPACITY, "output buffer too small for the decoded batch");
+    DHIP(hipSetDevice(d->device));
+    if (pcm && d->total_samples)
+        DHIP(hipMemcpyAsync(pcm, d->pcm.p, sizeof(int32_t) * d->total_samples,
+                            hipMemcpyDeviceToHost, d->s));
+    std::vector<DecFrame> fr;
+    if ((frame_offsets || frame_block_sizes) && d->total_frames) {
+        fr.resize(d->total_frames);
+        DHIP(hipMemcpyAsync(fr.data(), d->frames.p, sizeof(DecFrame) * d->total_frames,
+                            hipMemcpyDeviceToHost, d->s));
+    }
+    DHIP(hipStreamSynchronize(d->s));
+    for (uint64_t i = 0; i < fr.size(); ++i) {
+        const DecTrack &t = d->tr[fr[i].track];
+        if (frame_offsets)
+            frame_offsets[i] = fr[i].pos - t.start;
+        if (frame_block_sizes)
+            frame_block_sizes[i] = fr[i].bs;
+    }
+    return ATG_OK;
+}
+
+int atg_decoder_kernel_times(atg_decoder *d, const char **names, float *ms, int cap)
+{
+    if (!d || !d->have_times)
+        return 0;
+    const int n = cap < kDecTimed ? cap : kDecTimed;
+    for (int k = 0; k < n; ++k) {
+        if (names)
+            names[k] = kDecNames[k];
+        if (ms)
+            ms[k] = d->times[k];
+    }
+    return n;
+}
+
+} // extern "C"

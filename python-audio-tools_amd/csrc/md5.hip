@@ -203,6 +203,78 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
             tout[t].md5[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
 }
 
+// MD5 of a plain byte stream per lane (the decoder hashes the little-endian
+// PCM bytes K5 of flac_decode.hip wrote; streams start 64-byte aligned)
+__global__ __launch_bounds__(64) void k_bytes_md5(const uint8_t *__restrict__ base,
+                                                  const uint64_t *__restrict__ off,
+                                                  const uint64_t *__restrict__ len, uint32_t n,
+                                                  uint8_t *__restrict__ md5)
+{
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n)
+        return;
+    const uint8_t *s = base + off[t];
+    const uint64_t nbytes = len[t];
+    const uint64_t full = nbytes / 64u;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    uint32_t X[16];
+    if (full > 0) {
+        const uint4 *q = (const uint4 *)s;
+        uint4 buf[MD5_D][4];
+#pragma unroll
+        for (int j = 0; j < MD5_D; ++j)
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                buf[j][i] = q[(uint64_t)min((uint64_t)j, full - 1u) * 4u + i];
+        uint64_t blk = 0;
+        for (; blk + MD5_D <= full; blk += MD5_D) {
+#pragma unroll
+            for (int j = 0; j < MD5_D; ++j) {
+                md5_compress(h, (const uint32_t *)&buf[j][0]);
+                const uint64_t nb = min(blk + (uint64_t)(j + MD5_D), full - 1u);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    buf[j][i] = q[nb * 4u + i];
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < MD5_D; ++j)
+            if (blk + (uint64_t)j < full)
+                md5_compress(h, (const uint32_t *)&buf[j][0]);
+    }
+    uint8_t tail[128];
+    const uint32_t rem = (uint32_t)(nbytes - full * 64u);
+    for (uint32_t i = 0; i < rem; ++i)
+        tail[i] = s[full * 64u + i];
+    tail[rem] = 0x80;
+    const uint32_t tl = rem < 56u ? 64u : 128u;
+    for (uint32_t i = rem + 1; i < tl - 8u; ++i)
+        tail[i] = 0;
+    const uint64_t bits = nbytes * 8u;
+    for (int i = 0; i < 8; ++i)
+        tail[tl - 8u + i] = (uint8_t)(bits >> (8 * i));
+    for (uint32_t o = 0; o < tl; o += 64) {
+        for (int i = 0; i < 16; ++i)
+            X[i] = tail[o + 4 * i] | ((uint32_t)tail[o + 4 * i + 1] << 8) |
+                   ((uint32_t)tail[o + 4 * i + 2] << 16) | ((uint32_t)tail[o + 4 * i + 3] << 24);
+        md5_compress(h, X);
+    }
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            md5[16 * t + 4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
+hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                            uint32_t n, uint8_t *md5, hipStream_t s)
+{
+    if (!n)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_bytes_md5, dim3((n + 63u) / 64u), dim3(64), 0, s, base, off, len, n,
+                       md5);
+    return hipGetLastError();
+}
+
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                             const TrackInfo *tracks, TrackOut *tout, hipStream_t s)
 {

@@ -1,0 +1,164 @@
+"""GPU parity: libatgpu's FLAC decoder (flac_decode.hip) vs the reference
+decoder's recorded behaviour and vs the CPU oracle decoder.
+
+* every golden case of tests/golden/flac_decode_vectors.json (the
+  reference's own FLAC fixtures plus seeded corruptions, recorded with the
+  reference decoder by tests/golden/make_decode_golden.py): same status code,
+  same number of PCM bytes before it, same PCM MD5 -- one GPU batch per
+  fixture (33 streams);
+* GPU encode -> GPU decode round trips across presets, channel counts and
+  bit depths (bit-exact PCM, STREAMINFO MD5 verified on the GPU), and
+  offsets() equal to the encoder's frame list;
+* the FlacDecoder interface: one frame per read(), errors raised at the
+  frame where the reference raises them.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+import decode_cases
+import oracle_port
+import signals
+
+pytestmark = pytest.mark.gpu
+
+CASES = decode_cases.load_cases()
+FILES = sorted(set(c["file"] for c in CASES))
+
+
+def _batch(datas):
+    from audiotools import _atgpu
+    tracks, parts, infos, pos = [], [], [], 0
+    for d in datas:
+        rc, si, _ = _atgpu.read_metadata(d)
+        infos.append((rc, si))
+        if rc:
+            continue
+        body = d[si.frames_offset:]
+        pad = (-len(body)) % 4
+        tracks.append(_atgpu.dec_track(pos, len(body), si))
+        parts.append(body + b"\0" * pad)
+        pos += len(body) + pad
+    return tracks, b"".join(parts), infos
+
+
+@pytest.mark.parametrize("fname", FILES)
+def test_golden_cases_batch(fname):
+    from audiotools import _atgpu
+    cases = [c for c in CASES if c["file"] == fname]
+    datas = [decode_cases.case_bytes(c) for c in cases]
+    tracks, blob, infos = _batch(datas)
+    _, res, _, _ = _atgpu.decoder().decode(blob, tracks, fetch_pcm=False)
+    k = 0
+    for c, (rc, si) in zip(cases, infos):
+        if rc:
+            assert c["code"] == 100, c["name"]
+            continue
+        r = res[k]
+        k += 1
+        bb = (si.bits_per_sample + 7) // 8
+        assert r.status == c["code"], (c["name"], r.status, c["code"])
+        assert r.pcm_frames * si.channels * bb == c["pcm_bytes"], c["name"]
+        assert bytes(r.md5).hex() == c["pcm_md5"], c["name"]
+
+
+def test_golden_pcm_matches_oracle():
+    """PCM samples (not only their MD5) of the uncorrupted fixtures"""
+    from audiotools import _atgpu
+    datas = [decode_cases.case_bytes(c) for c in CASES
+             if not c["xor"] and c["cut"] is None and c["file"] != "1h.flac"]
+    tracks, blob, infos = _batch(datas)
+    pcm, res, offs, bss = _atgpu.decoder().decode(blob, tracks)
+    k = 0
+    for d, (rc, si) in zip(datas, infos):
+        if rc:
+            continue
+        r = res[k]
+        k += 1
+        want = oracle_port.decode_frames(d)
+        got = pcm[r.pcm_offset * si.channels:(r.pcm_offset + r.pcm_frames) * si.channels]
+        assert np.array_equal(got, np.asarray(want["pcm"], dtype=np.int32))
+        got_offs = [(int(o), int(b)) for o, b in
+                    zip(offs[r.first_frame:r.first_frame + r.n_frames],
+                        bss[r.first_frame:r.first_frame + r.n_frames])]
+        assert got_offs == [tuple(x) for x in want["offsets"]]
+
+
+@pytest.mark.parametrize("preset", ["8", "5", "0", "2"])
+@pytest.mark.parametrize("channels,bps", [(2, 16), (1, 16), (2, 24), (6, 16), (1, 8), (2, 8)])
+def test_encode_decode_round_trip(gpu_engine, preset, channels, bps):
+    from audiotools import _atgpu
+    opts = dict(oracle_port.PRESETS[preset])
+    B = opts["block_size"]
+    kinds = ["tone", "noise", "silence", "chirp", "sine", "wasted"]
+    pcms = [signals.make(k, B * (1 + i % 3) + 37 * i, channels, bps, seed=i)
+            for i, k in enumerate(kinds)]
+    o = _atgpu.make_options(**opts)
+    tracks, start = [], 0
+    for p in pcms:
+        tracks.append((start, len(p) // channels))
+        start += len(p) // channels
+    allpcm = np.concatenate(pcms).astype(np.int16 if bps <= 16 else np.int32)
+    out, res, eoffs, efp = gpu_engine.encode(o, allpcm, tracks, channels, bps, 44100)
+    images = [out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res]
+    dtracks, blob, infos = _batch(images)
+    pcm, dres, offs, bss = _atgpu.decoder().decode(blob, dtracks)
+    for i, (p, r, er) in enumerate(zip(pcms, dres, res)):
+        si = infos[i][1]
+        assert r.status == 0, (i, r.status)
+        got = pcm[r.pcm_offset * channels:(r.pcm_offset + r.pcm_frames) * channels]
+        assert np.array_equal(got, p.astype(np.int32))
+        assert bytes(r.md5) == bytes(si.md5)
+        got_offs = [int(x) for x in offs[r.first_frame:r.first_frame + r.n_frames]]
+        want_offs = [int(x) for x in eoffs[er.first_frame:er.first_frame + er.n_frames]]
+        assert got_offs == want_offs
+
+
+def test_flacdecoder_interface(tmp_path):
+    from audiotools import decoders
+    data = open(decode_cases.FIX + "/tone2.flac", "rb").read()
+    fn = tmp_path / "t.flac"
+    fn.write_bytes(data)
+    want = oracle_port.decode_frames(data)
+    with open(fn, "rb") as f:
+        dec = decoders.FlacDecoder(f)
+    frames = []
+    while True:
+        fl = dec.read(4096)
+        if not len(fl):
+            break
+        frames.append(fl)
+    assert len(frames) == len(want["offsets"])
+    got = np.concatenate([f.samples for f in frames]).astype(np.int32)
+    assert np.array_equal(got, np.asarray(want["pcm"], dtype=np.int32))
+    assert dec.offsets() == [tuple(x) for x in want["offsets"]]
+    dec.close()
+    with pytest.raises(ValueError):
+        dec.read(1)
+
+
+def test_flacdecoder_raises_at_bad_frame():
+    from audiotools import decoders
+    bad = [c for c in CASES if c["code"] == 14 and c["file"] == "tone3.flac"][0]
+    data = decode_cases.case_bytes(bad)
+    dec = decoders.FlacDecoder(data)
+    n = 0
+    with pytest.raises(ValueError) as e:
+        while True:
+            fl = dec.read(4096)
+            n += fl.frames
+            if not len(fl):
+                break
+    assert "invalid checksum in frame" in str(e.value)
+    bb = (dec.bits_per_sample + 7) // 8
+    assert n * dec.channels * bb == bad["pcm_bytes"]
+
+
+def test_truncated_stream_raises_ioerror():
+    from audiotools import decoders
+    bad = [c for c in CASES if c["code"] == 15][0]
+    dec = decoders.FlacDecoder(decode_cases.case_bytes(bad))
+    with pytest.raises(IOError):
+        while len(dec.read(4096)):
+            pass
