@@ -44,6 +44,13 @@
 #include "../../include/atgpu.h"
 #include "launch.h"
 
+#ifndef ATG_DEC_EXP
+#define ATG_DEC_EXP 0 // timing experiments only (exp/ builds); 0 in the product
+#endif
+#ifndef ATG_DEC_READER
+#define ATG_DEC_READER 1 // residual loop reader: 0 random access, 1 register window
+#endif
+
 namespace {
 
 enum {
@@ -97,65 +104,76 @@ struct Hdr {
 
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
-// MSB-first bit reader over the batch buffer (big-endian 32-bit words).
-// `cache` holds bits [32*cw, 32*cw + 64); 0 <= off < 32 between calls, so
-// peek32() always has 32 valid bits.  The word after the cache is loaded one
-// refill ahead (`nxt`) to keep HBM latency off the decode chain.  Reading
-// past the track end is not trapped per bit: eof() compares the position
-// with the end (any read past the end makes the reference report EOF,
-// flac.c:1187-1209 br_abort), and loads are clamped to the buffer.
+// MSB-first random-access bit reader over the batch buffer (big-endian
+// 32-bit words).  Position = 32-bit bit offset from a base word, so the
+// decode loops do 32-bit arithmetic and carry no refill state: every peek
+// loads the two words under the position (L1 hits: a lane walks its own
+// frame sequentially).  Keeping the loops free of data-dependent branches is
+// what matters here -- the lanes of a wave hold different frames, and a
+// per-lane refill branch diverges on almost every code.  Reading past the
+// track end is not trapped per bit: eof() compares the position with the
+// end (any read past the end makes the reference report EOF, flac.c
+// br_abort), and loads are clamped to the buffer.
 struct BitR {
     const uint32_t *w;
-    uint64_t nw;
-    uint64_t cw;
-    uint64_t cache;
-    uint32_t nxt;
-    uint32_t off;
-    uint64_t endbit;
+    uint64_t last;  // last valid word index
+    uint64_t bw;    // base word
+    uint32_t pos;   // bits from 32 * bw
+    uint32_t end;   // track end, bits from 32 * bw (saturated)
 
-    __device__ __forceinline__ uint32_t ld(uint64_t i) const
+    __device__ __forceinline__ void init(const uint32_t *w_, uint64_t nw, uint64_t bit,
+                                         uint64_t endbit)
     {
-        return bswap32(w[i < nw ? i : nw - 1]);
+        w = w_;
+        last = nw - 1;
+        bw = bit >> 5;
+        pos = (uint32_t)(bit & 31);
+        const uint64_t e = endbit - bw * 32; // endbit >= bit - 31 for every caller
+        end = endbit < bw * 32 ? 0u : (e > 0xF0000000ull ? 0xF0000000u : (uint32_t)e);
     }
-    __device__ __forceinline__ void seek(uint64_t bit)
+    __device__ __forceinline__ uint64_t abspos() const { return bw * 32 + pos; }
+    __device__ __forceinline__ bool eof() const { return pos > end; }
+    // the two words under the position (raw, big-endian)
+    __device__ __forceinline__ void words(uint32_t &a, uint32_t &b) const
     {
-        cw = bit >> 5;
-        off = (uint32_t)(bit & 31);
-        cache = ((uint64_t)ld(cw) << 32) | ld(cw + 1);
-        nxt = ld(cw + 2);
+        const uint64_t i = bw + (pos >> 5);
+        a = w[i < last ? i : last];
+        b = w[i + 1 < last ? i + 1 : last];
     }
-    __device__ __forceinline__ uint64_t pos() const { return cw * 32 + off; }
-    __device__ __forceinline__ bool eof() const { return pos() > endbit; }
-    __device__ __forceinline__ uint32_t peek32() const { return (uint32_t)((cache << off) >> 32); }
-    __device__ __forceinline__ void adv()
+    __device__ __forceinline__ uint32_t window(uint32_t a, uint32_t b) const
     {
-        cache = (cache << 32) | nxt;
-        ++cw;
-        nxt = ld(cw + 2);
+        a = bswap32(a);
+        b = bswap32(b);
+        const uint32_t sh = pos & 31;
+        return sh ? (a << sh) | (b >> (32 - sh)) : a;
     }
-    __device__ __forceinline__ void skip(uint32_t n) // n <= 32
+    __device__ __forceinline__ uint32_t peek32() const
     {
-        off += n;
-        if (off >= 32) {
-            off -= 32;
-            adv();
-        }
+        uint32_t a, b;
+        words(a, b);
+        return window(a, b);
+    }
+    __device__ __forceinline__ void skip(uint32_t n) { pos += n; }
+    __device__ __forceinline__ void skip_far(uint64_t n)
+    {
+        const uint64_t p = (uint64_t)pos + n;
+        pos = p > 0xF0000001ull ? 0xF0000001u : (uint32_t)p; // saturate past any end
     }
     __device__ __forceinline__ uint32_t get(uint32_t n) // n <= 32
     {
         const uint32_t v = n ? peek32() >> (32 - n) : 0u;
-        skip(n);
+        pos += n;
         return v;
     }
     // br_read_signed_bits_be (src/bitstream.c:418-425)
     __device__ __forceinline__ int32_t get_signed(uint32_t n)
     {
         if (n == 0) { // asks for 2^32-1 magnitude bits: always EOF
-            seek(endbit + 1);
+            skip_far(1ull << 33);
             return 0;
         }
         if (n > 33) {
-            seek(pos() + n);
+            skip_far(n);
             return 0;
         }
         const uint32_t sign = get(1);
@@ -170,11 +188,11 @@ struct BitR {
             const uint32_t p = peek32();
             if (p) {
                 const uint32_t z = __builtin_clz(p);
-                skip(z + 1);
+                pos += z + 1;
                 return q + z;
             }
             q += 32;
-            skip(32);
+            pos += 32;
             if (eof())
                 return q;
         }
@@ -191,7 +209,7 @@ __device__ __forceinline__ uint32_t byte_at(const uint32_t *w, uint64_t i)
 // flacdec_read_frame_header (flac.c:710-851)
 __device__ int dec_header(BitR &r, const DecTrack &t, Hdr &h)
 {
-    const uint64_t start = r.pos();
+    const uint64_t start = r.abspos();
     if (r.get(14) != 0x3FFEu) RET(FD_SYNC);
     if (r.get(1)) RET(FD_RESERVED);
     r.get(1); // blocking strategy
@@ -246,7 +264,7 @@ __device__ int dec_header(BitR &r, const DecTrack &t, Hdr &h)
     if (r.eof())
         return FD_EOF;
     uint32_t crc = 0;
-    for (uint64_t i = start >> 3; i < (r.pos() >> 3); ++i)
+    for (uint64_t i = start >> 3; i < (r.abspos() >> 3); ++i)
         crc = c_crc8[crc ^ byte_at(r.w, i)];
     if (crc)
         return FD_HDR_CRC;
@@ -257,63 +275,84 @@ __device__ int dec_header(BitR &r, const DecTrack &t, Hdr &h)
     return FD_OK;
 }
 
-// sample sinks for the residual reader: NullPred only parses (K2), the
-// Fixed/Lpc predictors restore samples with their history in registers (K4)
-struct NullPred {
-    __device__ __forceinline__ void operator()(int32_t) {}
-};
+// Every FIXED and LPC subframe is restored by one W-tap window predictor
+// (W = 12 for orders <= 12, 32 beyond): coefficients zero-padded past the
+// order, FIXED orders as LPC coefficients with shift 0 (flac.c:1090-1132;
+// the reference's wrapping int arithmetic equals the int64 sum truncated to
+// 32 bits).  One code path for all orders keeps the lanes of a wave, which
+// hold subframes of different orders, in lockstep.
+//
+// `fast`: the int64 sum of the reference is computed as int32 with
+// v_mad_i32_i24 when that is exact -- Σ|c|·2^(bps-1) < 2^31, |c| and
+// samples within 24 bits -- and every restored sample stays inside the
+// bps range (checked per sample into `bad`; a lane that trips it re-decodes
+// the subframe with the int64 path).
+// v_mad_i32_i24: 24-bit signed multiply, 32-bit add, one full-rate op
+__device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
+{
+    int32_t d;
+    asm("v_mad_i32_i24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
 
-template <int O>
-struct FixedPred {
+template <int W>
+struct WinPred {
     int32_t *out;
-    uint32_t i, n, wasted;
-    uint32_t h[O > 0 ? O : 1]; // h[0] newest
-    __device__ __forceinline__ void operator()(int32_t rv)
+    int32_t *dummy; // per-job slot for the stores of non-sample iterations
+    uint32_t i, n, wasted, shift, half;
+    bool fast, bad;
+    int32_t c[W];
+    int32_t h[W]; // h[0] newest sample
+    __device__ __forceinline__ void push(int32_t s, bool commit)
     {
-        uint32_t v;
-        if (O == 0) v = 0;
-        else if (O == 1) v = h[0];
-        else if (O == 2) v = 2u * h[0] - h[1];
-        else if (O == 3) v = 3u * h[0] - 3u * h[1] + h[2];
-        else v = 4u * h[0] - 6u * h[1] + 4u * h[2] - h[3];
-        const uint32_t s = v + (uint32_t)rv;
 #pragma unroll
-        for (int j = O - 1; j > 0; --j)
-            h[j] = h[j - 1];
-        if (O > 0)
-            h[0] = s;
-        if (i < n)
-            out[i] = (int32_t)(s << wasted);
-        ++i;
+        for (int j = W - 1; j > 0; --j)
+            h[j] = commit ? h[j - 1] : h[j];
+        h[0] = commit ? s : h[0];
+        // unconditional store: a store under a per-lane branch makes the
+        // next load wait for it (vmcnt counts stores on CDNA)
+#if ATG_DEC_EXP == 1 // timing experiment: no sample stores
+        if (i == n)
+            *dummy = s;
+#else
+        *(commit && i < n ? out + i : dummy) = (int32_t)((uint32_t)s << wasted);
+#endif
+        i += commit ? 1u : 0u;
+    }
+    __device__ __forceinline__ void step(int32_t rv, bool commit)
+    {
+        int32_t p;
+        if (fast) {
+            int32_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                acc = mad24(c[j], h[j], acc);
+            p = acc >> (shift < 31 ? shift : 31);
+        } else {
+            int64_t acc = 0;
+#pragma unroll
+            for (int j = 0; j < W; ++j)
+                acc += (int64_t)c[j] * (int64_t)h[j];
+            p = (int32_t)(acc >> shift);
+        }
+        const int32_t s = (int32_t)((uint32_t)p + (uint32_t)rv);
+        bad |= commit && ((uint32_t)(s + (int32_t)half) >= 2u * half);
+        push(s, commit);
     }
 };
 
-template <int O>
-struct LpcPred {
-    int32_t *out;
-    uint32_t i, n, wasted, shift;
-    int32_t c[O];
-    int32_t h[O]; // h[0] newest
-    __device__ __forceinline__ void operator()(int32_t rv)
-    {
-        int64_t acc = 0;
-#pragma unroll
-        for (int j = 0; j < O; ++j)
-            acc += (int64_t)c[j] * (int64_t)h[j];
-        const int32_t s = (int32_t)((uint32_t)(int32_t)(acc >> shift) + (uint32_t)rv);
-#pragma unroll
-        for (int j = O - 1; j > 0; --j)
-            h[j] = h[j - 1];
-        h[0] = s;
-        if (i < n)
-            out[i] = (int32_t)((uint32_t)s << wasted);
-        ++i;
-    }
+struct NullSink {
+    __device__ __forceinline__ void step(int32_t, bool) {}
 };
 
-// flacdec_read_residual (flac.c:1135-1209), samples handed to `pred`
+// flacdec_read_residual (flac.c:1135-1209), residuals handed to `sink`.
+// One flat loop whose iterations each consume either a partition header or
+// one residual, both decoded from the same 32-bit peek and merged with
+// selects: lanes holding different partition orders and Rice parameters
+// never branch apart (long unary codes, > 32 bits with their LSBs, take a
+// rare slow path).
 template <class P>
-__device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &pred)
+__device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &sink)
 {
     const uint32_t method = r.get(2);
     const uint32_t porder = r.get(4);
@@ -321,41 +360,99 @@ __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N,
     // reference would predict from a stale buffer), as the oracle does
     if (!r.eof() && method <= 1 && ((N >> porder) << porder) != N)
         return FD_ERROR;
+    if (method > 1)
+        RET(FD_CODING); // raised at the first partition (flac.c:1160-1170)
+    const uint32_t plen_all = N >> porder;
+    const uint32_t p0 = plen_all > order ? plen_all - order : 0u;
     const uint32_t parts = 1u << porder;
-    for (uint32_t part = 0; part < parts; ++part) {
-        int plen = (int)(N >> porder);
-        if (part == 0) {
-            plen -= (int)order;
-            if (plen < 0)
-                plen = 0;
+    const uint32_t total = p0 + (parts - 1u) * plen_all;
+    const uint32_t pbits = method ? 5u : 4u, escv = method ? 0x1Fu : 0xFu;
+    uint32_t k = 0, hdrs = 0, left = 0, rice = 0, esc = 0;
+#if ATG_DEC_READER == 0
+    uint32_t wa, wb;
+    r.words(wa, wb);
+#else
+    // register window: hi:lo = words cw, cw+1; nx = word cw+2 (raw), reloaded
+    // every iteration (one L1-resident load, issued before the MACs)
+    uint64_t cw = r.bw + (r.pos >> 5);
+    uint32_t off = r.pos & 31;
+    uint32_t hi = bswap32(r.w[cw < r.last ? cw : r.last]);
+    uint32_t lo = bswap32(r.w[cw + 1 < r.last ? cw + 1 : r.last]);
+    uint32_t nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+#endif
+    while (k < total || hdrs < parts) {
+#if ATG_DEC_READER == 0
+        const uint32_t p = r.window(wa, wb);
+#else
+        const uint32_t p = off ? (hi << off) | (lo >> (32 - off)) : hi;
+#endif
+        const bool hdr = left == 0;
+        // partition header: Rice parameter (+ escape width)
+        const uint32_t hr = p >> (32 - pbits);
+        const bool hesc = hr == escv;
+        const uint32_t hlen = pbits + (hesc ? 5u : 0u);
+        const uint32_t hbits = (p >> (27 - pbits)) & 31u;
+        // residual: Rice code (unary MSBs, stop bit, LSBs) or escaped raw
+        const uint32_t z = __builtin_clz(p | 1u);
+        const uint32_t clen = z + 1 + rice;
+        const uint32_t lsb = __builtin_amdgcn_ubfe(p, 31 - z - rice, rice);
+        const uint32_t value = (z << rice) | lsb;
+        int32_t v = (int32_t)(value >> 1) ^ -(int32_t)(value & 1u);
+        uint32_t len = clen;
+        if (esc) {
+            v = (int32_t)p >> (32 - esc);
+            len = esc;
         }
-        uint32_t rice, esc;
-        if (method == 0) {
-            rice = r.get(4);
-            esc = rice == 0xF ? r.get(5) : 0u;
-        } else if (method == 1) {
-            rice = r.get(5);
-            esc = rice == 0x1F ? r.get(5) : 0u;
+        const uint32_t step = hdr ? hlen : len;
+#if ATG_DEC_READER == 0
+        if (!hdr && !esc && (p == 0 || clen > 32)) { // rare: long code
+            const uint32_t msb = r.zeros();
+            const uint32_t val = (msb << rice) | r.get(rice);
+            v = (int32_t)(val >> 1) ^ -(int32_t)(val & 1u);
         } else {
-            RET(FD_CODING);
+            r.skip(step);
         }
-        if (r.eof())
-            return FD_EOF;
-        if (!esc) {
-            for (; plen; --plen) {
-                const uint32_t msb = r.zeros();
-                const uint32_t lsb = r.get(rice);
-                const uint32_t value = (msb << rice) | lsb;
-                const int32_t sv = (int32_t)value >> 1;
-                pred((value & 1u) ? -sv - 1 : sv);
-            }
+        // the next code's words are requested before this sample's
+        // prediction, whose MACs then cover the load latency
+        r.words(wa, wb);
+#else
+        if (!hdr && !esc && (p == 0 || clen > 32)) { // rare: long code
+            r.pos = (uint32_t)((cw - r.bw) * 32) + off;
+            const uint32_t msb = r.zeros();
+            const uint32_t val = (msb << rice) | r.get(rice);
+            v = (int32_t)(val >> 1) ^ -(int32_t)(val & 1u);
+            cw = r.bw + (r.pos >> 5);
+            off = r.pos & 31;
+            hi = bswap32(r.w[cw < r.last ? cw : r.last]);
+            lo = bswap32(r.w[cw + 1 < r.last ? cw + 1 : r.last]);
         } else {
-            for (; plen; --plen)
-                pred(r.get_signed(esc));
+            off += step;
+            const bool need = off >= 32;
+            hi = need ? lo : hi;
+            lo = need ? bswap32(nx) : lo;
+            cw += need ? 1u : 0u;
+            off -= need ? 32u : 0u;
         }
-        if (r.eof())
+        nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+#endif
+        sink.step(v, !hdr);
+        k += hdr ? 0u : 1u;
+        left = hdr ? (hdrs == 0 ? p0 : plen_all) : left - 1u;
+        rice = hdr ? hr : rice;
+        esc = hdr ? (hesc ? hbits : 0u) : esc;
+        hdrs += hdr ? 1u : 0u;
+#if ATG_DEC_READER != 0
+        if (hdr)
+            r.pos = (uint32_t)((cw - r.bw) * 32) + off;
+#endif
+        if (hdr && r.eof())
             return FD_EOF;
     }
+#if ATG_DEC_READER != 0
+    r.pos = (uint32_t)((cw - r.bw) * 32) + off;
+#endif
+    if (r.eof())
+        return FD_EOF;
     return FD_OK;
 }
 
@@ -389,7 +486,7 @@ __device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps)
     if (rc)
         return rc;
     bps -= sh.wasted; // unsigned, as the reference
-    NullPred np;
+    NullSink np;
     if (sh.kind == 0) {
         r.get_signed(bps);
     } else if (sh.kind == 1) {
@@ -432,6 +529,7 @@ __device__ uint32_t crc16_range(const uint32_t *w, uint64_t b0, uint64_t b1,
     uint64_t i = b0;
     for (; i < b1 && (i & 3); ++i)
         crc = ((crc << 8) & 0xFFFFu) ^ T[0][(crc >> 8) ^ byte_at(w, i)];
+#pragma unroll 8
     for (; i + 4 <= b1; i += 4) {
         const uint32_t x = bswap32(w[i >> 2]) ^ (crc << 16);
         crc = (uint32_t)T[3][x >> 24] ^ T[2][(x >> 16) & 0xFF] ^ T[1][(x >> 8) & 0xFF] ^
@@ -448,10 +546,7 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
                             uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec)
 {
     BitR r;
-    r.w = w;
-    r.nw = nw;
-    r.endbit = t.end * 8;
-    r.seek(pos * 8);
+    r.init(w, nw, pos * 8, t.end * 8);
     Hdr h;
     rec.bytes = 0;
     rec.status = dec_header(r, t, h);
@@ -463,14 +558,14 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
     rec.bps = (uint8_t)h.bps;
     const uint32_t N = (uint32_t)((uint64_t)h.bs < nlimit ? (uint64_t)h.bs : nlimit);
     for (uint32_t c = 0; c < h.ch; ++c) {
-        rec.sub_bit[c] = (uint32_t)(r.pos() - pos * 8);
+        rec.sub_bit[c] = (uint32_t)(r.abspos() - pos * 8);
         const int rc = parse_subframe(r, N, sub_bps(h.assign, c, h.bps));
         if (rc) {
             rec.status = rc;
             return;
         }
     }
-    const uint32_t a = (uint32_t)(r.pos() & 7);
+    const uint32_t a = (uint32_t)(r.abspos() & 7);
     if (a)
         r.skip(8 - a);
     r.get(16);
@@ -478,7 +573,7 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
         rec.status = FD_EOF;
         return;
     }
-    const uint64_t endb = r.pos() >> 3;
+    const uint64_t endb = r.abspos() >> 3;
     rec.bytes = (uint32_t)(endb - pos);
     rec.status = crc16_range(w, pos, endb, T) ? FD_FRAME_CRC : FD_OK;
 }
@@ -529,10 +624,7 @@ __global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w
         if (p < T.start || p >= T.end)
             continue;
         BitR r;
-        r.w = w;
-        r.nw = nw;
-        r.endbit = T.end * 8;
-        r.seek(p * 8);
+        r.init(w, nw, p * 8, T.end * 8);
         Hdr h;
         if (dec_header(r, T, h) != FD_OK)
             continue;
@@ -632,47 +724,53 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
     }
 }
 
-template <int O>
-__device__ __noinline__ void restore_lpc(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
-                                         int32_t *out)
+template <int W>
+__device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
+                                            uint32_t kind, uint32_t order, int32_t *out,
+                                            int32_t *dummy, bool allow_fast)
 {
-    LpcPred<O> p;
+    WinPred<W> p;
     p.out = out;
+    p.dummy = dummy;
     p.n = N;
+    p.i = 0;
     p.wasted = wasted;
+    p.shift = 0;
+    p.bad = false;
 #pragma unroll
-    for (int j = 0; j < O; ++j) {
-        const int32_t v = r.get_signed(bps);
-        if ((uint32_t)j < N)
-            out[j] = (int32_t)((uint32_t)v << wasted);
-        p.h[O - 1 - j] = v;
+    for (int j = 0; j < W; ++j) {
+        p.c[j] = 0;
+        p.h[j] = 0;
     }
-    const uint32_t prec = r.get(4) + 1;
-    p.shift = (uint32_t)r.get_signed(5) & 63u;
+    for (uint32_t j = 0; j < order; ++j) // warm-up samples enter the window
+        p.push(r.get_signed(bps), true);
+    uint32_t sum_abs = 0;
+    if (kind == 3) {
+        const uint32_t prec = r.get(4) + 1;
+        p.shift = (uint32_t)r.get_signed(5) & 63u;
+        for (uint32_t k = 0; k < order; ++k) {
+            const int32_t v = r.get_signed(prec);
+            sum_abs += (uint32_t)(v < 0 ? -v : v);
 #pragma unroll
-    for (int j = 0; j < O; ++j)
-        p.c[j] = r.get_signed(prec);
-    p.i = O;
-    dec_residual(r, O, N, p);
-}
-
-template <int O>
-__device__ __noinline__ void restore_fixed(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
-                                           int32_t *out)
-{
-    FixedPred<O> p;
-    p.out = out;
-    p.n = N;
-    p.wasted = wasted;
-#pragma unroll
-    for (int j = 0; j < O; ++j) {
-        const int32_t v = r.get_signed(bps);
-        if ((uint32_t)j < N)
-            out[j] = (int32_t)((uint32_t)v << wasted);
-        p.h[O - 1 - j] = (uint32_t)v;
+            for (int j = 0; j < W; ++j)
+                p.c[j] = (uint32_t)j == k ? v : p.c[j];
+        }
+    } else { // FIXED order 0..4: coefficients of the difference polynomial
+        const int32_t o = (int32_t)(order < 5 ? order : 4);
+        p.c[0] = o;                                  // 0, 1, 2, 3, 4
+        p.c[1] = o == 2 ? -1 : o == 3 ? -3 : o == 4 ? -6 : 0;
+        p.c[2] = o == 3 ? 1 : o == 4 ? 4 : 0;
+        p.c[3] = o == 4 ? -1 : 0;
+        sum_abs = o == 4 ? 15u : o == 3 ? 7u : o == 2 ? 3u : (uint32_t)o;
     }
-    p.i = O;
-    dec_residual(r, O, N, p);
+    // int32 is exact while every sample is inside the bps range (see WinPred)
+    p.half = bps >= 1 && bps <= 24 ? 1u << (bps - 1) : 0u;
+    p.fast = allow_fast && p.half && (uint64_t)sum_abs * p.half < 0x80000000ull;
+#if ATG_DEC_EXP == 2 // timing experiment: int64 sums only
+    p.fast = false;
+#endif
+    dec_residual(r, order, N, p);
+    return p.fast && p.bad;
 }
 
 // K4: one subframe per lane, samples restored into the planar scratch
@@ -680,7 +778,8 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
                                                      const DecTrack *__restrict__ tr,
                                                      const DecFrame *__restrict__ frames,
                                                      const uint2 *__restrict__ jobs,
-                                                     uint64_t njobs, int32_t *__restrict__ planar)
+                                                     uint64_t njobs, int32_t *__restrict__ planar,
+                                                     int32_t *__restrict__ dummies)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= njobs)
@@ -689,12 +788,10 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     const DecFrame f = frames[jb.x];
     const uint32_t c = jb.y;
     BitR r;
-    r.w = w;
-    r.nw = nw;
-    r.endbit = tr[f.track].end * 8;
-    r.seek(f.pos * 8 + f.sub_bit[c]);
+    r.init(w, nw, f.pos * 8 + f.sub_bit[c], tr[f.track].end * 8);
     const uint32_t N = f.n;
     int32_t *out = planar + f.pcm_start + (uint64_t)c * N;
+    int32_t *dummy = dummies + j;
     SubHdr sh;
     if (dec_subhdr(r, sh))
         return;
@@ -707,26 +804,14 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     } else if (sh.kind == 1) {
         for (uint32_t i = 0; i < N; ++i)
             out[i] = (int32_t)((uint32_t)r.get_signed(bps) << ws);
-    } else if (sh.kind == 2) {
-        switch (sh.order) {
-        case 0: restore_fixed<0>(r, N, bps, ws, out); break;
-        case 1: restore_fixed<1>(r, N, bps, ws, out); break;
-        case 2: restore_fixed<2>(r, N, bps, ws, out); break;
-        case 3: restore_fixed<3>(r, N, bps, ws, out); break;
-        default: restore_fixed<4>(r, N, bps, ws, out); break;
+    } else if (sh.order <= 12) {
+        const uint32_t at = r.pos;
+        if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, dummy, true)) {
+            r.pos = at; // a sample left the bps range: redo with int64 sums
+            restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, dummy, false);
         }
     } else {
-        switch (sh.order) {
-#define LPC_CASE(k) case k: restore_lpc<k>(r, N, bps, ws, out); break;
-            LPC_CASE(1) LPC_CASE(2) LPC_CASE(3) LPC_CASE(4) LPC_CASE(5) LPC_CASE(6)
-            LPC_CASE(7) LPC_CASE(8) LPC_CASE(9) LPC_CASE(10) LPC_CASE(11) LPC_CASE(12)
-            LPC_CASE(13) LPC_CASE(14) LPC_CASE(15) LPC_CASE(16) LPC_CASE(17) LPC_CASE(18)
-            LPC_CASE(19) LPC_CASE(20) LPC_CASE(21) LPC_CASE(22) LPC_CASE(23) LPC_CASE(24)
-            LPC_CASE(25) LPC_CASE(26) LPC_CASE(27) LPC_CASE(28) LPC_CASE(29) LPC_CASE(30)
-            LPC_CASE(31) LPC_CASE(32)
-#undef LPC_CASE
-        default: break;
-        }
+        restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, dummy, false);
     }
 }
 
@@ -1109,7 +1194,7 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     d->total_frames = fb;
     DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
     DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
-    DHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    DHIP(d->planar.ensure(sizeof(int32_t) * (std::max<uint64_t>(pb, 1) + jb)));
     DHIP(d->pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
     DHIP(d->bytes.ensure(std::max<uint64_t>(mb, 64)));
     DHIP(d->md5.ensure(16 * std::max<uint32_t>(n, 1)));
@@ -1125,7 +1210,7 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     if (jb)
         hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
                            nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
-                           (int32_t *)d->planar.p);
+                           (int32_t *)d->planar.p, (int32_t *)d->planar.p + pb);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(d->ev[4], s));
     if (fb)
