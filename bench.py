@@ -196,11 +196,12 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
     comp = sum(int(r.bytes) - header for r in res)
     pcm32 = args.tracks * args.frames * BLOCK * 2 * 4
     # algorithmic bytes per launch: the parsers read the compressed frames
-    # once; the subframe decoder also writes the int32 planar samples; the
-    # interleaver reads them and writes int32 PCM + the s16 byte stream
+    # once; the subframe decoder also writes its int32 row scratch, which
+    # the row transposer reads and writes as planar samples; the
+    # interleaver reads those and writes int32 PCM + the s16 byte stream
     alg = {"dec_scan": comp, "dec_parse": comp, "dec_chain": 0,
-           "dec_subframe": comp + pcm32, "dec_interleave": pcm32 * 2 + pcm32 // 2,
-           "dec_md5": pcm32 // 2}
+           "dec_subframe": comp + pcm32, "dec_unrow": 2 * pcm32,
+           "dec_interleave": pcm32 * 2 + pcm32 // 2, "dec_md5": pcm32 // 2}
     kernels = {k: v for k, v in kt.items() if k in alg}
     dom = max(kernels, key=kernels.get)
     achieved = alg[dom] / (kernels[dom] / 1e3) / 1e9

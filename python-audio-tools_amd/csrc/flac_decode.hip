@@ -102,6 +102,17 @@ struct Hdr {
     uint32_t bs, rate, assign, ch, bps;
 };
 
+// what K4 leaves for the row transposer (K4b) per subframe job
+struct JobMeta {
+    uint8_t kind;   // 0 CONSTANT, 1 VERBATIM (rows = samples), 2 FIXED/LPC, 3 none
+    uint8_t order;
+    uint8_t porder;
+    uint8_t pad;
+    int32_t value;  // CONSTANT sample (already shifted by wasted bits)
+    uint32_t iters; // rows written
+    uint32_t pad2;
+};
+
 __device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
 
 // MSB-first random-access bit reader over the batch buffer (big-endian
@@ -297,28 +308,27 @@ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
 
 template <int W>
 struct WinPred {
-    int32_t *out;
-    int32_t *dummy; // per-job slot for the stores of non-sample iterations
-    uint32_t i, n, wasted, shift, half;
+    int32_t *out;   // planar samples (warm-up only)
+    int32_t *row;   // this lane's column of the wave's row scratch
+    uint32_t i, n, t, wasted, shift, half, porder;
     bool fast, bad;
     int32_t c[W];
     int32_t h[W]; // h[0] newest sample
-    __device__ __forceinline__ void push(int32_t s, bool commit)
+    __device__ __forceinline__ void warm(int32_t s)
     {
 #pragma unroll
         for (int j = W - 1; j > 0; --j)
-            h[j] = commit ? h[j - 1] : h[j];
-        h[0] = commit ? s : h[0];
-        // unconditional store: a store under a per-lane branch makes the
-        // next load wait for it (vmcnt counts stores on CDNA)
-#if ATG_DEC_EXP == 1 // timing experiment: no sample stores
-        if (i == n)
-            *dummy = s;
-#else
-        *(commit && i < n ? out + i : dummy) = (int32_t)((uint32_t)s << wasted);
-#endif
-        i += commit ? 1u : 0u;
+            h[j] = h[j - 1];
+        h[0] = s;
+        if (i < n)
+            out[i] = (int32_t)((uint32_t)s << wasted);
+        ++i;
     }
+    __device__ __forceinline__ void partition_order(uint32_t p) { porder = p; }
+    // one residual-loop iteration (a partition header when !commit): the
+    // value goes to row t of the lane's column -- every lane of the wave
+    // stores to the same row, one 256-byte coalesced store per iteration
+    // (per-lane sample addresses would make 64 scattered line writes)
     __device__ __forceinline__ void step(int32_t rv, bool commit)
     {
         int32_t p;
@@ -337,12 +347,18 @@ struct WinPred {
         }
         const int32_t s = (int32_t)((uint32_t)p + (uint32_t)rv);
         bad |= commit && ((uint32_t)(s + (int32_t)half) >= 2u * half);
-        push(s, commit);
+#pragma unroll
+        for (int j = W - 1; j > 0; --j)
+            h[j] = commit ? h[j - 1] : h[j];
+        h[0] = commit ? s : h[0];
+        row[(uint64_t)t * 64] = (int32_t)((uint32_t)s << wasted);
+        ++t;
     }
 };
 
 struct NullSink {
     __device__ __forceinline__ void step(int32_t, bool) {}
+    __device__ __forceinline__ void partition_order(uint32_t) {}
 };
 
 // flacdec_read_residual (flac.c:1135-1209), residuals handed to `sink`.
@@ -356,6 +372,7 @@ __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N,
 {
     const uint32_t method = r.get(2);
     const uint32_t porder = r.get(4);
+    sink.partition_order(porder);
     // a partition order that does not divide the block: rejected (the
     // reference would predict from a stale buffer), as the oracle does
     if (!r.eof() && method <= 1 && ((N >> porder) << porder) != N)
@@ -727,11 +744,13 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
 template <int W>
 __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
                                             uint32_t kind, uint32_t order, int32_t *out,
-                                            int32_t *dummy, bool allow_fast)
+                                            int32_t *row, JobMeta &m, bool allow_fast)
 {
     WinPred<W> p;
     p.out = out;
-    p.dummy = dummy;
+    p.row = row;
+    p.t = 0;
+    p.porder = 0;
     p.n = N;
     p.i = 0;
     p.wasted = wasted;
@@ -743,7 +762,7 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
         p.h[j] = 0;
     }
     for (uint32_t j = 0; j < order; ++j) // warm-up samples enter the window
-        p.push(r.get_signed(bps), true);
+        p.warm(r.get_signed(bps));
     uint32_t sum_abs = 0;
     if (kind == 3) {
         const uint32_t prec = r.get(4) + 1;
@@ -770,16 +789,21 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
     p.fast = false;
 #endif
     dec_residual(r, order, N, p);
+    m.porder = (uint8_t)p.porder;
+    m.iters = p.t;
     return p.fast && p.bad;
 }
 
-// K4: one subframe per lane, samples restored into the planar scratch
+// K4: one subframe per lane.  Warm-up samples go straight to the planar
+// scratch; every residual-loop iteration stores to its row of the wave's
+// [row][lane] scratch (coalesced); K4b maps rows back to samples.
 __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict__ w, uint64_t nw,
                                                      const DecTrack *__restrict__ tr,
                                                      const DecFrame *__restrict__ frames,
                                                      const uint2 *__restrict__ jobs,
                                                      uint64_t njobs, int32_t *__restrict__ planar,
-                                                     int32_t *__restrict__ dummies)
+                                                     int32_t *__restrict__ rows, uint32_t nrows,
+                                                     JobMeta *__restrict__ meta)
 {
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= njobs)
@@ -791,27 +815,134 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     r.init(w, nw, f.pos * 8 + f.sub_bit[c], tr[f.track].end * 8);
     const uint32_t N = f.n;
     int32_t *out = planar + f.pcm_start + (uint64_t)c * N;
-    int32_t *dummy = dummies + j;
+    int32_t *row = rows + (uint64_t)blockIdx.x * nrows * 64 + threadIdx.x;
+    JobMeta m;
+    m.kind = 3;
+    m.order = 0;
+    m.porder = 0;
+    m.pad = 0;
+    m.value = 0;
+    m.iters = 0;
+    m.pad2 = 0;
     SubHdr sh;
-    if (dec_subhdr(r, sh))
-        return;
-    const uint32_t bps = sub_bps(f.assign, c, f.bps) - sh.wasted;
-    const uint32_t ws = sh.wasted;
-    if (sh.kind == 0) {
-        const uint32_t v = (uint32_t)r.get_signed(bps) << ws;
-        for (uint32_t i = 0; i < N; ++i)
-            out[i] = (int32_t)v;
-    } else if (sh.kind == 1) {
-        for (uint32_t i = 0; i < N; ++i)
-            out[i] = (int32_t)((uint32_t)r.get_signed(bps) << ws);
-    } else if (sh.order <= 12) {
-        const uint32_t at = r.pos;
-        if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, dummy, true)) {
-            r.pos = at; // a sample left the bps range: redo with int64 sums
-            restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, dummy, false);
+    if (dec_subhdr(r, sh) == FD_OK) {
+        const uint32_t bps = sub_bps(f.assign, c, f.bps) - sh.wasted;
+        const uint32_t ws = sh.wasted;
+        if (sh.kind == 0) {
+            m.kind = 0;
+            m.value = (int32_t)((uint32_t)r.get_signed(bps) << ws);
+        } else if (sh.kind == 1) {
+            m.kind = 1;
+            m.iters = N;
+            for (uint32_t i = 0; i < N; ++i)
+                row[(uint64_t)i * 64] = (int32_t)((uint32_t)r.get_signed(bps) << ws);
+        } else {
+            m.kind = 2;
+            m.order = (uint8_t)sh.order;
+            if (sh.order <= 12) {
+                const uint32_t at = r.pos;
+                if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, true)) {
+                    r.pos = at; // a sample left the bps range: redo with int64 sums
+                    restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false);
+                }
+            } else {
+                restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false);
+            }
         }
-    } else {
-        restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, dummy, false);
+    }
+    meta[j] = m;
+}
+
+// K4b: rows -> samples.  Block = (wave slot of 64 jobs, tile of 64 rows):
+// the tile is read with coalesced row loads into LDS, then each job's
+// samples are written as contiguous runs.  Row t of a FIXED/LPC job is
+// partition header 0 (t = 0), residual t-1 of partition 0 (t <= p0), or,
+// past that, header/residual m of partition 1 + (t-p0-1)/(plen+1) -- the
+// residual loop reads a header before every partition (flac.c:1150-1209).
+__global__ __launch_bounds__(256) void k_dec_unrow(const DecFrame *__restrict__ frames,
+                                                   const uint2 *__restrict__ jobs, uint64_t njobs,
+                                                   const JobMeta *__restrict__ meta,
+                                                   const int32_t *__restrict__ rows,
+                                                   uint32_t nrows, int32_t *__restrict__ planar)
+{
+    __shared__ int32_t tile[64 * 65];
+    __shared__ JobMeta jm[64];
+    __shared__ uint64_t joff[64];
+    __shared__ uint32_t jn[64];
+    __shared__ uint32_t maxit;
+    const uint32_t slot = blockIdx.x, t0 = blockIdx.y * 64;
+    const uint32_t tid = threadIdx.x;
+    if (tid == 0)
+        maxit = 0;
+    __syncthreads();
+    if (tid < 64) {
+        const uint64_t j = (uint64_t)slot * 64 + tid;
+        JobMeta m;
+        m.kind = 3;
+        m.iters = 0;
+        if (j < njobs) {
+            m = meta[j];
+            const uint2 jb = jobs[j];
+            const DecFrame f = frames[jb.x];
+            joff[tid] = f.pcm_start + (uint64_t)jb.y * f.n;
+            jn[tid] = f.n;
+        } else {
+            joff[tid] = 0;
+            jn[tid] = 0;
+        }
+        jm[tid] = m;
+        const uint32_t need = m.kind == 0 ? jn[tid] : (m.kind == 3 ? 0u : m.iters);
+        atomicMax(&maxit, need);
+    }
+    __syncthreads();
+    if (t0 >= maxit)
+        return;
+    const int32_t *src = rows + ((uint64_t)slot * nrows + t0) * 64;
+    for (uint32_t k = tid; k < 64 * 64; k += 256) {
+        const uint32_t x = k >> 6, l = k & 63;
+        tile[x * 65 + l] = t0 + x < nrows ? src[(uint64_t)x * 64 + l] : 0;
+    }
+    __syncthreads();
+    for (uint32_t k = tid; k < 64 * 64; k += 256) {
+        const uint32_t l = k >> 6, x = k & 63;
+        const JobMeta m = jm[l];
+        const uint32_t t = t0 + x, n = jn[l];
+        uint32_t i;
+        int32_t v = tile[x * 65 + l];
+        if (m.kind == 0) {
+            i = t;
+            v = m.value;
+        } else if (m.kind == 1) {
+            i = t;
+        } else if (m.kind == 2) {
+            if (t >= m.iters)
+                continue;
+            const uint32_t order = m.order;
+            const uint32_t plen = n >> m.porder;
+            const uint32_t p0 = plen > order ? plen - order : 0u;
+            uint32_t rr;
+            if (t == 0)
+                continue;
+            if (t <= p0) {
+                rr = t - 1;
+            } else {
+                const uint32_t tp = t - p0 - 1, L = plen + 1;
+                uint32_t q = (uint32_t)((float)tp * (1.0f / (float)L));
+                while (q * L > tp)
+                    --q;
+                while ((q + 1) * L <= tp)
+                    ++q;
+                const uint32_t mm = tp - q * L;
+                if (mm == 0)
+                    continue;
+                rr = p0 + q * plen + mm - 1;
+            }
+            i = order + rr;
+        } else {
+            continue;
+        }
+        if (i < n)
+            planar[joff[l] + i] = v;
     }
 }
 
@@ -862,9 +993,9 @@ __global__ __launch_bounds__(256) void k_dec_interleave(const DecTrack *__restri
     }
 }
 
-const int kDecTimed = 7;
-const char *kDecNames[kDecTimed] = {"dec_scan", "dec_parse", "dec_chain", "dec_subframe",
-                                    "dec_interleave", "dec_md5", "dec_total"};
+const int kDecTimed = 8;
+const char *kDecNames[kDecTimed] = {"dec_scan",  "dec_parse",      "dec_chain", "dec_subframe",
+                                    "dec_unrow", "dec_interleave", "dec_md5",   "dec_total"};
 
 } // namespace
 
@@ -916,7 +1047,7 @@ struct atg_decoder {
     float times[kDecTimed] = {};
     bool have_times = false;
     DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, planar, pcm,
-        bytes, md5, md5meta;
+        bytes, md5, md5meta, rows, meta;
     // results of the last decode
     std::vector<DecTrack> tr;
     std::vector<DecCount> cnt;
@@ -1105,7 +1236,7 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->pcm, &d->bytes, &d->md5, &d->md5meta})
+                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->pcm, &d->bytes, &d->md5, &d->md5meta, &d->rows, &d->meta})
         b->release();
     for (auto &e : d->ev)
         (void)hipEventDestroy(e);
@@ -1194,7 +1325,16 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     d->total_frames = fb;
     DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
     DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
-    DHIP(d->planar.ensure(sizeof(int32_t) * (std::max<uint64_t>(pb, 1) + jb)));
+    DHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    // row scratch: a residual loop runs at most N + 2^porder <= 2N iterations
+    uint32_t max_bs = 1;
+    for (uint32_t t = 0; t < n; ++t)
+        if (d->cnt[t].n_frames)
+            max_bs = std::max(max_bs, d->tr[t].max_bs);
+    const uint32_t nrows = 2 * max_bs + 1;
+    const uint64_t nslots = (jb + 63) / 64;
+    DHIP(d->rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
+    DHIP(d->meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
     DHIP(d->pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
     DHIP(d->bytes.ensure(std::max<uint64_t>(mb, 64)));
     DHIP(d->md5.ensure(16 * std::max<uint32_t>(n, 1)));
@@ -1210,15 +1350,23 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     if (jb)
         hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
                            nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
-                           (int32_t *)d->planar.p, (int32_t *)d->planar.p + pb);
+                           (int32_t *)d->planar.p, (int32_t *)d->rows.p, nrows,
+                           (JobMeta *)d->meta.p);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(d->ev[4], s));
+    if (jb)
+        hipLaunchKernelGGL(k_dec_unrow, dim3((unsigned)nslots, (nrows + 63) / 64), dim3(256), 0,
+                           s, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
+                           (const JobMeta *)d->meta.p, (const int32_t *)d->rows.p, nrows,
+                           (int32_t *)d->planar.p);
+    DHIP(hipGetLastError());
+    DHIP(hipEventRecord(d->ev[5], s));
     if (fb)
         hipLaunchKernelGGL(k_dec_interleave, dim3((unsigned)fb), dim3(256), 0, s, dtr,
                            (const DecFrame *)d->frames.p, (const int32_t *)d->planar.p,
                            (int32_t *)d->pcm.p, (uint8_t *)d->bytes.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[5], s));
+    DHIP(hipEventRecord(d->ev[6], s));
     std::vector<uint64_t> md5_off(n), md5_len(n);
     for (uint32_t t = 0; t < n; ++t) {
         md5_off[t] = d->tr[t].md5_base;
@@ -1231,14 +1379,14 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
                         hipMemcpyHostToDevice, s));
     DHIP(launch_bytes_md5((const uint8_t *)d->bytes.p, (const uint64_t *)mb_buf.p,
                           (const uint64_t *)mb_buf.p + n, n, (uint8_t *)d->md5.p, s));
-    DHIP(hipEventRecord(d->ev[6], s));
+    DHIP(hipEventRecord(d->ev[7], s));
     std::vector<uint8_t> md5(16 * (size_t)n);
     if (n)
         DHIP(hipMemcpyAsync(md5.data(), d->md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s));
     DHIP(hipStreamSynchronize(s));
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
     // interleave, md5, total
-    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {0, 6}};
+    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {0, 7}};
     for (int k = 0; k < kDecTimed; ++k)
         (void)hipEventElapsedTime(&d->times[k], d->ev[map[k][0]], d->ev[map[k][1]]);
     d->have_times = true;
