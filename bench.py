@@ -44,7 +44,7 @@ def parse_args(argv=None):
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--tracks", type=int, default=1024)
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
-    ap.add_argument("--cpu-sample-tracks", type=int, default=128)
+    ap.add_argument("--cpu-sample-tracks", type=int, default=1024)
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -205,6 +205,13 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
     kernels = {k: v for k, v in kt.items() if k in alg}
     dom = max(kernels, key=kernels.get)
     achieved = alg[dom] / (kernels[dom] / 1e3) / 1e9
+    traffic = None
+    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if os.path.exists(tf):
+        try:
+            traffic = json.load(open(tf)).get(dom)
+        except Exception:
+            traffic = None
     dec.close()
     return {
         "metric": "FLAC-8 decode frames/s (GPU decode of the encoded batch, MD5-verified)",
@@ -213,7 +220,7 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": None,
+                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4)},
         "verified_md5_round_trip": ok,
     }

@@ -9,6 +9,7 @@ import collections
 import csv
 import glob
 import json
+import re
 import sys
 
 root = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
@@ -16,10 +17,10 @@ agg = collections.defaultdict(lambda: collections.defaultdict(float))
 cnt = collections.defaultdict(lambda: collections.defaultdict(int))
 for f in glob.glob(root + "/*/run_counter_collection.csv"):
     for r in csv.DictReader(open(f)):
-        name = r["Kernel_Name"]
-        if "k_" not in name:
+        m = re.search(r"\b(k_[A-Za-z0-9_]+(?:<[^>(]*>)?)", r["Kernel_Name"])
+        if not m:
             continue
-        short = name.replace("void ", "").split("(")[0]
+        short = m.group(1)
         agg[short][r["Counter_Name"]] += float(r["Counter_Value"])
         cnt[short][r["Counter_Name"]] += 1
 out = {}

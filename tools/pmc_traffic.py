@@ -12,11 +12,16 @@ pmc = json.loads(subprocess.check_output([sys.executable, "tools/pmc_summary.py"
 names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
          "k_frame_decide": "frame_decide", "k_track_scan": "track_scan",
          "k_frame_pack": "frame_pack", "k_track_md5": "track_md5",
-         "k_stream_header": "stream_header"}
+         "k_stream_header": "stream_header",
+         # decoder (flac_decode.hip, md5.hip)
+         "k_dec_scan": "dec_scan", "k_dec_parse": "dec_parse", "k_dec_chain": "dec_chain",
+         "k_dec_subframe": "dec_subframe", "k_dec_unrow": "dec_unrow",
+         "k_dec_interleave": "dec_interleave", "k_bytes_md5": "dec_md5"}
 out = {}
 for k, v in pmc.items():
     base = k.split("<")[0]
     if base in names and "HBM_read_bytes" in v and "HBM_write_bytes" in v:
+        # k_dec_chain runs twice per step (count + write passes): per step
         out[names[base]] = int(v["HBM_read_bytes"] + v["HBM_write_bytes"])
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
 print(json.dumps(out, indent=1, sort_keys=True))

@@ -5,6 +5,7 @@ usage: prof_summary.py <run_results.db | kernel_stats.csv> [out.txt]
 Keeps the libatgpu kernels (k_*) and the runtime copies, drops torch's
 synthetic-data kernels.  Durations are microseconds per dispatch."""
 import csv
+import re
 import sqlite3
 import sys
 
@@ -27,10 +28,11 @@ def rows_from_csv(path):
 def main():
     src = sys.argv[1]
     rows = list(rows_from_db(src) if src.endswith(".db") else rows_from_csv(src))
-    keep = [r for r in rows if r[0].startswith(("void k_", "k_", "__amd_rocclr"))]
+    keep = [r for r in rows if re.search(r"\bk_[a-z]", r[0]) or "__amd_rocclr" in r[0]]
     lines = ["%-44s %6s %12s %12s" % ("kernel", "calls", "total_us", "avg_us")]
     for name, calls, total, avg, _ in keep:
-        short = name.replace("void ", "").split("(")[0]
+        m = re.search(r"\b(k_[A-Za-z0-9_]+(?:<[^>(]*>)?)", name)
+        short = m.group(1) if m else name.replace("void ", "").split("(")[0]
         lines.append("%-44s %6d %12.1f %12.1f" % (short[:44], calls, total, avg))
     text = "\n".join(lines) + "\n"
     if len(sys.argv) > 2:
