@@ -250,6 +250,38 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
 /* Per-kernel device time of the decoder's most recent batch (HIP events). */
 int atg_decoder_kernel_times(atg_decoder *dec, const char **names, float *ms, int cap);
 
+/* ------------------------------------------------------------------ */
+/* Integer PCM converters (track2track --bits-per-sample / --channels). */
+/* Replace the read() bodies of the reference's pcmconverter types:     */
+/* BPSConverter (src/pcmconverter.c:667-747, dither src/dither.c:73-89),*/
+/* Downmixer (:220-342) and Averager (:64-97), over whole tracks.       */
+/* PCM is interleaved int32 (FrameList layout) in and out.              */
+/* ------------------------------------------------------------------ */
+enum {
+    ATG_CONV_BPS = 0,     /* in_bps -> out_bps; dither bits when reducing */
+    ATG_CONV_DOWNMIX = 1, /* -> 2 channels (channel_mask 0 = invented mask) */
+    ATG_CONV_AVERAGE = 2  /* -> 1 channel */
+};
+
+const char *atg_pcm_convert_last_error(void);
+uint32_t atg_pcm_convert_out_channels(int kind, uint32_t in_channels);
+
+/* Device buffers; `stream` is a hipStream_t (NULL = default stream); the
+   call returns after the launch.  Reducing bits reads one dither bit per
+   sample from d_dither, starting at bit dither_bit0, MSB first, in the
+   reference's order: per 4096-frame read(), channel by channel. */
+atg_status atg_pcm_convert_device(int kind, const int32_t *d_in, int32_t *d_out,
+                                  uint64_t frames, uint32_t channels, uint32_t channel_mask,
+                                  uint32_t in_bps, uint32_t out_bps, const uint8_t *d_dither,
+                                  uint64_t dither_bit0, void *stream);
+
+/* Host buffers (staged through the device); out holds
+   frames x atg_pcm_convert_out_channels() samples. */
+atg_status atg_pcm_convert_host(int device, int kind, const int32_t *in, int32_t *out,
+                                uint64_t frames, uint32_t channels, uint32_t channel_mask,
+                                uint32_t in_bps, uint32_t out_bps, const uint8_t *dither,
+                                uint64_t dither_bytes, uint64_t dither_bit0);
+
 #ifdef __cplusplus
 }
 #endif

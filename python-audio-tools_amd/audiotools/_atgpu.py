@@ -34,7 +34,11 @@ EXPORTS = (
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
     "atg_flac_decode_device", "atg_decoder_kernel_times",
+    "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
+    "atg_pcm_convert_device", "atg_pcm_convert_host",
 )
+
+CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
 
 c_u32, c_i32, c_u64 = ctypes.c_uint32, ctypes.c_int32, ctypes.c_uint64
 
@@ -189,6 +193,16 @@ def load_library():
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
         lib.atg_decoder_kernel_times.restype = ctypes.c_int
+        lib.atg_pcm_convert_last_error.restype = ctypes.c_char_p
+        lib.atg_pcm_convert_out_channels.argtypes = [ctypes.c_int, c_u32]
+        lib.atg_pcm_convert_out_channels.restype = c_u32
+        lib.atg_pcm_convert_device.argtypes = [
+            ctypes.c_int, P, P, c_u64, c_u32, c_u32, c_u32, c_u32, P, c_u64, P]
+        lib.atg_pcm_convert_device.restype = ctypes.c_int
+        lib.atg_pcm_convert_host.argtypes = [
+            ctypes.c_int, ctypes.c_int, P, P, c_u64, c_u32, c_u32, c_u32, c_u32, P, c_u64,
+            c_u64]
+        lib.atg_pcm_convert_host.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -446,3 +460,24 @@ def decoder():
         if _decoder is None:
             _decoder = Decoder(default_device())
         return _decoder
+
+
+def pcm_convert(kind, pcm, channels, in_bps, out_bps=None, channel_mask=0,
+                dither=b"", dither_bit0=0, device=None):
+    """one GPU conversion of interleaved int32 PCM held in host memory
+    (atg_pcm_convert_host) -> int32 numpy array"""
+    lib = load_library()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames = len(a) // channels
+    oc = lib.atg_pcm_convert_out_channels(kind, channels)
+    out = np.empty(max(1, frames * oc), dtype=np.int32)
+    d = np.frombuffer(bytes(dither), dtype=np.uint8) if dither else None
+    st = lib.atg_pcm_convert_host(
+        default_device() if device is None else device, kind,
+        a.ctypes.data_as(ctypes.c_void_p), out.ctypes.data_as(ctypes.c_void_p), frames,
+        channels, channel_mask, in_bps, in_bps if out_bps is None else out_bps,
+        d.ctypes.data_as(ctypes.c_void_p) if d is not None else None,
+        0 if d is None else len(d), dither_bit0)
+    if st != ATG_OK:
+        raise ATGError(st, lib.atg_pcm_convert_last_error().decode("utf-8", "replace"))
+    return out[:frames * oc]

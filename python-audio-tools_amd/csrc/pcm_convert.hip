@@ -1,0 +1,215 @@
+// pcm_convert.hip — the integer PCM converters of the reference's
+// pcmconverter module, elementwise over whole tracks:
+//
+//   BPS      BPSConverter_read (src/pcmconverter.c:667-747): fewer bits =
+//            (x >> shift) ^ dither_bit, the bits read MSB first from a byte
+//            stream (the reference's os.urandom reader, src/dither.c:73-89),
+//            one per sample in the order the reference consumes them: per
+//            4096-frame read(), channel by channel; more bits = x << shift.
+//   DOWNMIX  Downmixer_read (:220-342): 6-channel layout from the channel
+//            mask (missing channels silent), then
+//            L = round(fL + 0.6·0.7·(bL+bR) + 0.7·fC), R likewise with −,
+//            clamped to the sample range; fp64, no contraction.
+//   AVERAGE  Averager_read (:64-97): int64 sum / channels (C truncation).
+//
+// Input and output are interleaved int32 (the FrameList layout).  One
+// thread per PCM frame; the kernels are HBM streams (4-24 B in, 4-8 B out
+// per frame).  The caller supplies the dither bytes, so a conversion is
+// reproducible and testable; the reference draws them from os.urandom.
+#include <hip/hip_runtime.h>
+
+#include <string>
+
+#include "../../include/atgpu.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+thread_local std::string g_conv_err;
+
+atg_status cfail(atg_status s, const std::string &m)
+{
+    g_conv_err = m;
+    return s;
+}
+
+#define CHIP(expr)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return cfail(ATG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+__global__ __launch_bounds__(256) void k_pcm_bps(const int32_t *__restrict__ in,
+                                                 int32_t *__restrict__ out, uint64_t frames,
+                                                 uint32_t ch, uint32_t in_bps, uint32_t out_bps,
+                                                 const uint8_t *__restrict__ dither,
+                                                 uint64_t bit0)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= frames)
+        return;
+    const uint64_t chunk = f / 4096u * 4096u;
+    const uint64_t clen = frames - chunk < 4096u ? frames - chunk : 4096u;
+    for (uint32_t c = 0; c < ch; ++c) {
+        const int32_t x = in[f * ch + c];
+        int32_t y;
+        if (out_bps < in_bps) {
+            const uint64_t b = bit0 + chunk * ch + (uint64_t)c * clen + (f - chunk);
+            const int32_t bit = (dither[b >> 3] >> (7 - (uint32_t)(b & 7))) & 1;
+            y = (x >> (in_bps - out_bps)) ^ bit;
+        } else {
+            y = (int32_t)((uint32_t)x << (out_bps - in_bps));
+        }
+        out[f * ch + c] = y;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_pcm_downmix(const int32_t *__restrict__ in,
+                                                     int32_t *__restrict__ out, uint64_t frames,
+                                                     uint32_t ch, uint32_t mask, uint32_t bps)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= frames)
+        return;
+    int32_t six[6];
+    uint32_t k = 0;
+    for (uint32_t m = 0; m < 6; ++m) {
+        if (mask & (1u << m))
+            six[m] = in[f * ch + k++];
+        else
+            six[m] = 0;
+    }
+    const double REAR_GAIN = 0.6, CENTER_GAIN = 0.7;
+    const int32_t smin = -(1 << (bps - 1)), smax = (1 << (bps - 1)) - 1;
+    const double mono_rear = 0.7 * (double)(six[4] + six[5]);
+    const int32_t l = (int32_t)round((double)six[0] + REAR_GAIN * mono_rear +
+                                     CENTER_GAIN * (double)six[2]);
+    const int32_t r = (int32_t)round((double)six[1] - REAR_GAIN * mono_rear +
+                                     CENTER_GAIN * (double)six[2]);
+    out[2 * f] = l > smax ? smax : (l < smin ? smin : l);
+    out[2 * f + 1] = r > smax ? smax : (r < smin ? smin : r);
+}
+
+__global__ __launch_bounds__(256) void k_pcm_average(const int32_t *__restrict__ in,
+                                                     int32_t *__restrict__ out, uint64_t frames,
+                                                     uint32_t ch)
+{
+    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= frames)
+        return;
+    int64_t acc = 0;
+    for (uint32_t c = 0; c < ch; ++c)
+        acc += in[f * ch + c];
+    out[f] = (int32_t)(acc / (int64_t)ch);
+}
+
+uint32_t default_mask(uint32_t ch)
+{
+    // Downmixer_read's invented masks (pcmconverter.c:256-290)
+    static const uint32_t m[7] = {0x0, 0x4, 0x3, 0x7, 0x33, 0x37, 0x3F};
+    return ch <= 6 ? m[ch] : 0x3F;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *atg_pcm_convert_last_error(void) { return g_conv_err.c_str(); }
+
+uint32_t atg_pcm_convert_out_channels(int kind, uint32_t in_channels)
+{
+    return kind == ATG_CONV_DOWNMIX ? 2u : kind == ATG_CONV_AVERAGE ? 1u : in_channels;
+}
+
+atg_status atg_pcm_convert_device(int kind, const int32_t *d_in, int32_t *d_out,
+                                  uint64_t frames, uint32_t channels, uint32_t channel_mask,
+                                  uint32_t in_bps, uint32_t out_bps, const uint8_t *d_dither,
+                                  uint64_t dither_bit0, void *stream)
+{
+    if ((!d_in || !d_out) && frames)
+        return cfail(ATG_ERR_INVALID, "NULL buffer");
+    if (channels < 1 || in_bps < 1 || in_bps > 32)
+        return cfail(ATG_ERR_INVALID, "bad channels / bits per sample");
+    hipStream_t s = (hipStream_t)stream;
+    const dim3 grid((unsigned)((frames + 255) / 256)), blk(256);
+    if (!frames)
+        return ATG_OK;
+    switch (kind) {
+    case ATG_CONV_BPS:
+        if (out_bps < 1 || out_bps > 32)
+            return cfail(ATG_ERR_INVALID, "bad output bits per sample");
+        if (out_bps < in_bps && !d_dither)
+            return cfail(ATG_ERR_INVALID, "dither bytes required to reduce bits per sample");
+        hipLaunchKernelGGL(k_pcm_bps, grid, blk, 0, s, d_in, d_out, frames, channels, in_bps,
+                           out_bps, d_dither, dither_bit0);
+        break;
+    case ATG_CONV_DOWNMIX: {
+        uint32_t mask = channel_mask ? channel_mask : default_mask(channels);
+        // the reference links input channels to mask bits 0x1..0x20 in order
+        uint32_t bits = 0;
+        for (uint32_t m = mask & 0x3F; m; m >>= 1)
+            bits += m & 1u;
+        if (bits > channels)
+            return cfail(ATG_ERR_INVALID, "channel mask names more channels than present");
+        hipLaunchKernelGGL(k_pcm_downmix, grid, blk, 0, s, d_in, d_out, frames, channels,
+                           mask & 0x3Fu, in_bps);
+        break;
+    }
+    case ATG_CONV_AVERAGE:
+        hipLaunchKernelGGL(k_pcm_average, grid, blk, 0, s, d_in, d_out, frames, channels);
+        break;
+    default:
+        return cfail(ATG_ERR_INVALID, "unknown conversion");
+    }
+    CHIP(hipGetLastError());
+    return ATG_OK;
+}
+
+atg_status atg_pcm_convert_host(int device, int kind, const int32_t *in, int32_t *out,
+                                uint64_t frames, uint32_t channels, uint32_t channel_mask,
+                                uint32_t in_bps, uint32_t out_bps, const uint8_t *dither,
+                                uint64_t dither_bytes, uint64_t dither_bit0)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return cfail(ATG_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n)
+        return cfail(ATG_ERR_INVALID, "device index out of range");
+    CHIP(hipSetDevice(device));
+    const uint32_t oc = atg_pcm_convert_out_channels(kind, channels);
+    const uint64_t need_bits = frames * channels;
+    if (kind == ATG_CONV_BPS && out_bps < in_bps && dither_bytes * 8 < need_bits + dither_bit0)
+        return cfail(ATG_ERR_INVALID, "not enough dither bytes");
+    void *di = nullptr, *dout = nullptr, *dd = nullptr;
+    const size_t ib = sizeof(int32_t) * (frames * channels ? frames * channels : 1);
+    const size_t ob = sizeof(int32_t) * (frames * oc ? frames * oc : 1);
+    if (hipMalloc(&di, ib) != hipSuccess || hipMalloc(&dout, ob) != hipSuccess ||
+        hipMalloc(&dd, dither_bytes ? dither_bytes : 1) != hipSuccess) {
+        (void)hipFree(di);
+        (void)hipFree(dout);
+        (void)hipFree(dd);
+        return cfail(ATG_ERR_NOMEM, "device allocation failed");
+    }
+    atg_status st = ATG_OK;
+    if (hipMemcpy(di, in, sizeof(int32_t) * frames * channels, hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        (dither_bytes && hipMemcpy(dd, dither, dither_bytes, hipMemcpyHostToDevice) != hipSuccess))
+        st = cfail(ATG_ERR_DEVICE, "copy to device failed");
+    if (st == ATG_OK)
+        st = atg_pcm_convert_device(kind, (const int32_t *)di, (int32_t *)dout, frames, channels,
+                                    channel_mask, in_bps, out_bps,
+                                    dither_bytes ? (const uint8_t *)dd : nullptr, dither_bit0,
+                                    nullptr);
+    if (st == ATG_OK &&
+        (hipDeviceSynchronize() != hipSuccess ||
+         hipMemcpy(out, dout, sizeof(int32_t) * frames * oc, hipMemcpyDeviceToHost) != hipSuccess))
+        st = cfail(ATG_ERR_DEVICE, "conversion failed on the device");
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    (void)hipFree(dd);
+    return st;
+}
+
+} // extern "C"

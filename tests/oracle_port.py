@@ -284,3 +284,32 @@ def pcm_bytes(pcm, bps):
         u = a.astype("<i4").view(np.uint8).reshape(-1, 4)[:, :3]
         return u.tobytes()
     raise ValueError("unsupported bps %d" % bps)
+
+
+# --- PCM converters (oracle/pcmconv_port.c; parity unpinned, see header) ---
+CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
+
+
+def convert(kind, pcm, channels, in_bps, out_bps=None, mask=0, dither=b""):
+    """oracle conversion of interleaved int32 PCM -> int32 array"""
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames = len(a) // channels
+    P = ctypes.c_void_p
+    if kind == CONV_BPS:
+        out = np.empty(max(1, frames * channels), dtype=np.int32)
+        d = np.frombuffer(bytes(dither) or b"\0", dtype=np.uint8)
+        lib.pcmconvport_bps.argtypes = [P, P, c_u64, c_u32, c_u32, c_u32, P]
+        lib.pcmconvport_bps(a.ctypes.data, out.ctypes.data, frames, channels, in_bps,
+                            out_bps, d.ctypes.data)
+        return out[:frames * channels]
+    if kind == CONV_DOWNMIX:
+        out = np.empty(max(1, frames * 2), dtype=np.int32)
+        lib.pcmconvport_downmix.argtypes = [P, P, c_u64, c_u32, c_u32, c_u32]
+        lib.pcmconvport_downmix(a.ctypes.data, out.ctypes.data, frames, channels, mask,
+                                in_bps)
+        return out[:frames * 2]
+    out = np.empty(max(1, frames), dtype=np.int32)
+    lib.pcmconvport_average.argtypes = [P, P, c_u64, c_u32]
+    lib.pcmconvport_average(a.ctypes.data, out.ctypes.data, frames, channels)
+    return out[:frames]
