@@ -226,6 +226,46 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
     }
 
 
+def convert_leg(args, torch, device, pcm):
+    """BPSConverter 16 -> 8 bits with dither over the whole batch
+    (pcm_convert.hip): an HBM stream -- 4 B in + 4 B out +
+    1/8 B of dither per sample.  Timed with torch's default-stream sync
+    around the launches (the converter runs on the default stream)."""
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    x = pcm.to(torch.int32)
+    y = torch.empty_like(x)
+    dither = torch.randint(0, 256, ((x.numel() + 7) // 8,), dtype=torch.uint8,
+                           device=device)
+    frames = x.numel() // 2
+
+    def run():
+        st = lib.atg_pcm_convert_device(_atgpu.CONV_BPS, x.data_ptr(), y.data_ptr(), frames,
+                                        2, 0, 16, 8, dither.data_ptr(), 0, None)
+        if st != _atgpu.ATG_OK:
+            raise RuntimeError(lib.atg_pcm_convert_last_error())
+
+    for _ in range(args.warmup):
+        run()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        run()
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / args.steps
+    ok = bool((((y ^ (x >> 8)) & ~1) == 0).all().item())
+    alg = x.numel() * 8 + dither.numel()
+    del x, y, dither
+    return {"metric": "BPSConverter 16->8 dither, samples/s", "value": round(frames * 2 / dt, 1),
+            "unit": "samples/s", "ms_per_step": round(dt * 1e3, 4),
+            "roofline": {"bound": "hbm", "kernel": "k_pcm_bps",
+                         "achieved": round(alg / dt / 1e9, 2), "peak": HBM_PEAK_GBS,
+                         "unit": "GB/s", "frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 4),
+                         "traffic": None, "alg_bytes_per_launch": alg,
+                         "launch_ms": round(dt * 1e3, 4)},
+            "verified_dither_invariant": ok}
+
+
 def main(argv=None):
     args = parse_args(argv)
     import torch
@@ -300,6 +340,10 @@ def main(argv=None):
     if not args.no_decode:
         decode = decode_leg(args, torch, dist, world, device, out, res, header, n_frames,
                             barrier)
+
+    convert = None
+    if not args.no_decode and rank == 0:
+        convert = convert_leg(args, torch, device, pcm)
 
     if rank != 0:
         if world > 1:
@@ -380,6 +424,7 @@ def main(argv=None):
         "verified_vs_oracle": verified,
         "cpu_baseline": cpu,
         "decode": decode,
+        "convert": convert,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -12,9 +12,10 @@
 //            clamped to the sample range; fp64, no contraction.
 //   AVERAGE  Averager_read (:64-97): int64 sum / channels (C truncation).
 //
-// Input and output are interleaved int32 (the FrameList layout).  One
-// thread per PCM frame; the kernels are HBM streams (4-24 B in, 4-8 B out
-// per frame).  The caller supplies the dither bytes, so a conversion is
+// Input and output are interleaved int32 (the FrameList layout).  The
+// kernels are HBM streams (4-24 B in, 4-8 B out per frame): BPS runs a
+// lane per 4 samples with 16-byte vector loads/stores (buffers 16-byte
+// aligned), downmix/average a thread per frame.  The caller supplies the dither bytes, so a conversion is
 // reproducible and testable; the reference draws them from os.urandom.
 #include <hip/hip_runtime.h>
 
@@ -41,28 +42,62 @@ atg_status cfail(atg_status s, const std::string &m)
             return cfail(ATG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
     } while (0)
 
+__device__ __forceinline__ int32_t bps_one(int32_t x, uint64_t f, uint32_t c, uint64_t frames,
+                                           uint32_t ch, uint32_t in_bps, uint32_t out_bps,
+                                           const uint8_t *__restrict__ dither, uint64_t bit0)
+{
+    if (out_bps < in_bps) {
+        const uint64_t chunk = f / 4096u * 4096u;
+        const uint64_t clen = frames - chunk < 4096u ? frames - chunk : 4096u;
+        const uint64_t b = bit0 + chunk * ch + (uint64_t)c * clen + (f - chunk);
+        const int32_t bit = (dither[b >> 3] >> (7 - (uint32_t)(b & 7))) & 1;
+        return (x >> (in_bps - out_bps)) ^ bit;
+    }
+    return (int32_t)((uint32_t)x << (out_bps - in_bps));
+}
+
+// lane per 4 consecutive samples (one 16-byte load/store, adjacent lanes
+// adjacent): coalesced; the frame/channel of the first sample costs one
+// division per lane
 __global__ __launch_bounds__(256) void k_pcm_bps(const int32_t *__restrict__ in,
                                                  int32_t *__restrict__ out, uint64_t frames,
                                                  uint32_t ch, uint32_t in_bps, uint32_t out_bps,
                                                  const uint8_t *__restrict__ dither,
                                                  uint64_t bit0)
 {
-    const uint64_t f = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= frames)
+    const uint64_t q0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const uint64_t n = frames * ch;
+    if (q0 >= n)
         return;
-    const uint64_t chunk = f / 4096u * 4096u;
-    const uint64_t clen = frames - chunk < 4096u ? frames - chunk : 4096u;
-    for (uint32_t c = 0; c < ch; ++c) {
-        const int32_t x = in[f * ch + c];
-        int32_t y;
-        if (out_bps < in_bps) {
-            const uint64_t b = bit0 + chunk * ch + (uint64_t)c * clen + (f - chunk);
-            const int32_t bit = (dither[b >> 3] >> (7 - (uint32_t)(b & 7))) & 1;
-            y = (x >> (in_bps - out_bps)) ^ bit;
-        } else {
-            y = (int32_t)((uint32_t)x << (out_bps - in_bps));
+    uint64_t f;
+    uint32_t c;
+    if (n < 0xFFFFFFFFull) {
+        f = (uint32_t)q0 / ch;
+        c = (uint32_t)q0 - (uint32_t)f * ch;
+    } else {
+        f = q0 / ch;
+        c = (uint32_t)(q0 - f * ch);
+    }
+    if (q0 + 4 <= n) {
+        int4 v = *(const int4 *)(in + q0);
+        int32_t *e = (int32_t *)&v;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            e[k] = bps_one(e[k], f, c, frames, ch, in_bps, out_bps, dither, bit0);
+            if (++c == ch) {
+                c = 0;
+                ++f;
+            }
         }
-        out[f * ch + c] = y;
+        *(int4 *)(out + q0) = v;
+    } else {
+        for (uint64_t q = q0; q < n; ++q) {
+            out[q] = bps_one(in[q], f, c, frames, ch, in_bps, out_bps, dither, bit0);
+            if (++c == ch) {
+                c = 0;
+                ++f;
+            }
+        }
     }
 }
 
@@ -142,8 +177,10 @@ atg_status atg_pcm_convert_device(int kind, const int32_t *d_in, int32_t *d_out,
             return cfail(ATG_ERR_INVALID, "bad output bits per sample");
         if (out_bps < in_bps && !d_dither)
             return cfail(ATG_ERR_INVALID, "dither bytes required to reduce bits per sample");
-        hipLaunchKernelGGL(k_pcm_bps, grid, blk, 0, s, d_in, d_out, frames, channels, in_bps,
-                           out_bps, d_dither, dither_bit0);
+        if (((uintptr_t)d_in | (uintptr_t)d_out) & 15)
+            return cfail(ATG_ERR_INVALID, "PCM buffers must be 16-byte aligned");
+        hipLaunchKernelGGL(k_pcm_bps, dim3((unsigned)((frames * channels + 1023) / 1024)), blk, 0, s, d_in,
+                           d_out, frames, channels, in_bps, out_bps, d_dither, dither_bit0);
         break;
     case ATG_CONV_DOWNMIX: {
         uint32_t mask = channel_mask ? channel_mask : default_mask(channels);
