@@ -282,6 +282,44 @@ atg_status atg_pcm_convert_host(int device, int kind, const int32_t *in, int32_t
                                 uint32_t in_bps, uint32_t out_bps, const uint8_t *dither,
                                 uint64_t dither_bytes, uint64_t dither_bit0);
 
+/* ------------------------------------------------------------------ */
+/* ReplayGain analysis (tracktag/track2track --replay-gain).           */
+/* Replaces ReplayGain(rate).title_gain(pcmreader) for every track of a */
+/* batch and album_gain() per album (src/replaygain.c:115-322,         */
+/* :566-807).  PCM is interleaved int32 (FrameList layout), 1 or 2      */
+/* channels, 8/16/24 bits, one of the 20 supported sample rates.        */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t pcm_offset; /* first PCM frame of the track in d_pcm */
+    uint64_t pcm_frames;
+    uint32_t channels, bits_per_sample, sample_rate;
+    uint32_t album;      /* album index (tracks grouped by album) */
+} atg_rg_track;
+
+typedef struct {
+    double title_gain;   /* dB; 0.0 when no 50 ms window completed */
+    double title_peak;   /* max |x| / 2^(bps-1) */
+    int32_t status;      /* 0 ok, 1 not enough samples */
+    uint32_t reserved;
+} atg_rg_result;
+
+const char *atg_replaygain_last_error(void);
+
+/* Title gains/peaks of all tracks; when n_albums > 0 also each album's
+   12000-bin window histogram (the reference's B array) into d_album_hist
+   (device, n_albums x 12000 uint32; NULL = internal) and album peaks into
+   album_peaks (host, may be NULL).  Album gains follow from
+   atg_replaygain_hist_gain -- after an RCCL all-reduce of the histograms
+   when an album spans several GPUs. */
+atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *tracks,
+                                 uint32_t n_tracks, uint32_t n_albums, atg_rg_result *results,
+                                 uint32_t *d_album_hist, double *album_peaks, void *stream);
+
+/* analyzeResult (replaygain.c:754-776) of n device histograms -> gains
+   (host); NaN = not enough samples (album_gain raises ValueError). */
+atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *gains,
+                                    void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -36,6 +36,7 @@ EXPORTS = (
     "atg_flac_decode_device", "atg_decoder_kernel_times",
     "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
     "atg_pcm_convert_device", "atg_pcm_convert_host",
+    "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
 )
 
 CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
@@ -113,6 +114,16 @@ FD_MESSAGES = {
     14: "invalid checksum in frame", 15: "EOF reading frame",
     16: "MD5 mismatch at end of stream",
 }
+
+
+class RgTrack(ctypes.Structure):
+    _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64), ("channels", c_u32),
+                ("bits_per_sample", c_u32), ("sample_rate", c_u32), ("album", c_u32)]
+
+
+class RgResult(ctypes.Structure):
+    _fields_ = [("title_gain", ctypes.c_double), ("title_peak", ctypes.c_double),
+                ("status", c_i32), ("reserved", c_u32)]
 
 
 class ATGError(RuntimeError):
@@ -203,6 +214,13 @@ def load_library():
             ctypes.c_int, ctypes.c_int, P, P, c_u64, c_u32, c_u32, c_u32, c_u32, P, c_u64,
             c_u64]
         lib.atg_pcm_convert_host.restype = ctypes.c_int
+        lib.atg_replaygain_last_error.restype = ctypes.c_char_p
+        lib.atg_replaygain_device.argtypes = [
+            P, ctypes.POINTER(RgTrack), c_u32, c_u32, ctypes.POINTER(RgResult), P,
+            ctypes.POINTER(ctypes.c_double), P]
+        lib.atg_replaygain_device.restype = ctypes.c_int
+        lib.atg_replaygain_hist_gain.argtypes = [P, c_u32, ctypes.POINTER(ctypes.c_double), P]
+        lib.atg_replaygain_hist_gain.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -481,3 +499,60 @@ def pcm_convert(kind, pcm, channels, in_bps, out_bps=None, channel_mask=0,
     if st != ATG_OK:
         raise ATGError(st, lib.atg_pcm_convert_last_error().decode("utf-8", "replace"))
     return out[:frames * oc]
+
+
+def _rg_check(lib, st):
+    if st != ATG_OK:
+        raise ATGError(st, lib.atg_replaygain_last_error().decode("utf-8", "replace"))
+
+
+def replaygain_device(d_pcm, tracks, n_albums=0, d_album_hist=None):
+    """ReplayGain of a batch whose int32 PCM is in device memory.
+    tracks: list of RgTrack.  -> ([RgResult], [album peak])"""
+    lib = load_library()
+    n = len(tracks)
+    arr = (RgTrack * max(1, n))(*tracks)
+    res = (RgResult * max(1, n))()
+    peaks = (ctypes.c_double * max(1, n_albums))()
+    _rg_check(lib, lib.atg_replaygain_device(
+        ctypes.c_void_p(d_pcm), arr, n, n_albums, res,
+        ctypes.c_void_p(d_album_hist) if d_album_hist else None, peaks, None))
+    return [res[i] for i in range(n)], [peaks[i] for i in range(n_albums)]
+
+
+def replaygain_hist_gain(d_hist, n):
+    """analyzeResult of n device histograms -> list of gains (NaN = none)"""
+    lib = load_library()
+    g = (ctypes.c_double * max(1, n))()
+    _rg_check(lib, lib.atg_replaygain_hist_gain(ctypes.c_void_p(d_hist), n, g, None))
+    return [g[i] for i in range(n)]
+
+
+def replaygain_host(pcm, tracks, n_albums=0, return_hist=False):
+    """same as replaygain_device for int32 PCM in host memory
+    -> (results, album_peaks, album_gains[, album histograms uint32])"""
+    lib = load_library()
+    eng = engine()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    d_pcm, d_hist = ctypes.c_void_p(), ctypes.c_void_p()
+    _check(lib, lib.atg_device_alloc(eng.handle, max(4, a.nbytes), ctypes.byref(d_pcm)))
+    _check(lib, lib.atg_device_alloc(eng.handle, max(4, 48000 * n_albums),
+                                     ctypes.byref(d_hist)))
+    try:
+        if a.nbytes:
+            _check(lib, lib.atg_copy_to_device(eng.handle, d_pcm,
+                                               a.ctypes.data_as(ctypes.c_void_p), a.nbytes))
+        res, peaks = replaygain_device(d_pcm.value, tracks, n_albums, d_hist.value)
+        gains = replaygain_hist_gain(d_hist.value, n_albums) if n_albums else []
+        hist = None
+        if return_hist:
+            hist = np.zeros((max(1, n_albums), 12000), dtype=np.uint32)
+            if n_albums:
+                _check(lib, lib.atg_copy_to_host(eng.handle, hist.ctypes.data_as(ctypes.c_void_p),
+                                                 d_hist, hist.nbytes))
+    finally:
+        lib.atg_device_free(eng.handle, d_pcm)
+        lib.atg_device_free(eng.handle, d_hist)
+    if return_hist:
+        return res, peaks, gains, hist[:n_albums]
+    return res, peaks, gains

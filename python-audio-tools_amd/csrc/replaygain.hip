@@ -1,0 +1,343 @@
+// replaygain.hip — ReplayGain title and album analysis (SURVEY §8(a)
+// G1–G5) for a batch of tracks: the reference's ReplayGain_title_gain /
+// analyze_samples / analyzeResult / get_album_gain (src/replaygain.c
+// :186-322, :566-807).
+//
+//   k_rg_title   lane per track: the Yule-Walker (10th order) + Butterworth
+//                (2nd order) IIR pair per channel is a serial recurrence, so
+//                each lane runs it over its whole track from zero state, in
+//                the reference's exact fp64 operation order (no contraction),
+//                summing squared outputs with the reference's batch grouping
+//                (4096-frame reads, 10-sample prebuffer batch, 50 ms windows;
+//                singles for batch % 16, then 16-term groups) and binning
+//                each window as (int)(1000·log10(mean/2 + 1e-37)) into the
+//                track's 12000-bin histogram; title peak = max |x| / 2^(bps-1).
+//   k_rg_album   thread per bin: album histogram = sum of its tracks'.
+//   k_rg_gain    lane per histogram: 95th-percentile scan -> 64.82 - i/100.
+//
+// Multi-GPU: an album split across ranks all-reduces its uint32 histogram
+// (sum, exact) and peak (max) -- the caller does that over RCCL between
+// atg_replaygain_device and atg_replaygain_hist_gain (bench.py).
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/atgpu.h"
+#include "rg_coeffs.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kBins = 12000;
+
+__constant__ double c_yule[20][21];
+__constant__ double c_butter[20][5];
+
+thread_local std::string g_rg_err;
+
+atg_status rfail(atg_status s, const std::string &m)
+{
+    g_rg_err = m;
+    return s;
+}
+
+#define RHIP(expr)                                                                         \
+    do {                                                                                   \
+        hipError_t e_ = (expr);                                                            \
+        if (e_ != hipSuccess)                                                              \
+            return rfail(ATG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+int freq_index(unsigned rate)
+{
+    static const unsigned rates[20] = {48000, 44100, 32000, 24000, 22050, 16000, 12000,
+                                       11025, 8000,  18900, 37800, 56000, 64000, 88200,
+                                       96000, 112000, 128000, 144000, 176400, 192000};
+    for (int i = 0; i < 20; i++)
+        if (rates[i] == rate)
+            return i;
+    return -1;
+}
+
+struct RgTrack {
+    uint64_t off;    // first interleaved sample
+    uint64_t frames;
+    uint32_t ch, bps, fi, window;
+};
+
+struct Chan {
+    double in[10], yo[10], bo0, bo1; // newest first
+};
+
+// filterYule then filterButter for one sample (replaygain.c:566-610):
+// left-to-right sums exactly as the reference's expressions
+__device__ __forceinline__ double filt(Chan &s, double x, const double *ky, const double *kb)
+{
+    double y = 1e-10 + x * ky[0];
+#pragma unroll
+    for (int k = 1; k <= 10; ++k) {
+        y = y - s.yo[k - 1] * ky[2 * k - 1];
+        y = y + s.in[k - 1] * ky[2 * k];
+    }
+    const double b = y * kb[0] - s.bo0 * kb[1] + s.yo[0] * kb[2] - s.bo1 * kb[3] + s.yo[1] * kb[4];
+#pragma unroll
+    for (int k = 9; k > 0; --k) {
+        s.in[k] = s.in[k - 1];
+        s.yo[k] = s.yo[k - 1];
+    }
+    s.in[0] = x;
+    s.yo[0] = y;
+    s.bo1 = s.bo0;
+    s.bo0 = b;
+    return b;
+}
+
+__global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm,
+                                                 const RgTrack *__restrict__ tracks, uint32_t n,
+                                                 uint32_t *__restrict__ hist,
+                                                 double *__restrict__ peaks)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n)
+        return;
+    const RgTrack T = tracks[t];
+    const double *ky = c_yule[T.fi], *kb = c_butter[T.fi];
+    uint32_t *A = hist + (uint64_t)t * kBins;
+    const int32_t *p = pcm + T.off;
+    const long window = T.window;
+    const double peak_shift = (double)(1 << (T.bps - 1));
+    Chan L = {}, R = {};
+    double lsum = 0, rsum = 0, peak = 0;
+    long totsamp = 0;
+    for (uint64_t c0 = 0; c0 < T.frames; c0 += 4096) {
+        const long n4 = (long)(T.frames - c0 < 4096 ? T.frames - c0 : 4096);
+        long pos = 0, batch = n4;
+        while (batch > 0) {
+            long cur = batch > window - totsamp ? window - totsamp : batch;
+            if (pos < 10 && cur > 10 - pos)
+                cur = 10 - pos;
+            const long singles = cur % 16;
+            double gl = 0, gr = 0;
+            for (long k = 0; k < cur; ++k) {
+                const uint64_t f = c0 + (uint64_t)(pos + k);
+                const int32_t il = p[f * T.ch];
+                const int32_t ir = T.ch == 2 ? p[f * T.ch + 1] : il;
+                double xl, xr;
+                if (T.bps == 8) {
+                    xl = (double)(il << 8);
+                    xr = (double)(ir << 8);
+                } else if (T.bps == 16) {
+                    xl = (double)il;
+                    xr = (double)ir;
+                } else {
+                    xl = (double)(il >> 8);
+                    xr = (double)(ir >> 8);
+                }
+                peak = fmax(peak, (double)abs(il) / peak_shift);
+                peak = fmax(peak, (double)abs(ir) / peak_shift);
+                const double ol = filt(L, xl, ky, kb);
+                const double orr = filt(R, xr, ky, kb);
+                if (k < singles) {
+                    lsum += ol * ol;
+                    rsum += orr * orr;
+                } else {
+                    const long g = (k - singles) & 15;
+                    gl = g == 0 ? ol * ol : gl + ol * ol;
+                    gr = g == 0 ? orr * orr : gr + orr * orr;
+                    if (g == 15) {
+                        lsum += gl;
+                        rsum += gr;
+                    }
+                }
+            }
+            batch -= cur;
+            pos += cur;
+            totsamp += cur;
+            if (totsamp == window) {
+                const double val = 100. * 10. * log10((lsum + rsum) / totsamp * 0.5 + 1.e-37);
+                int ival = (int)val;
+                ival = ival < 0 ? 0 : (ival >= kBins ? kBins - 1 : ival);
+                A[ival] += 1u;
+                lsum = rsum = 0.;
+                totsamp = 0;
+            }
+        }
+    }
+    peaks[t] = peak;
+}
+
+// album histogram = sum of its tracks' histograms (tracks [first, first+count))
+__global__ __launch_bounds__(256) void k_rg_album(const uint32_t *__restrict__ hist,
+                                                  const uint32_t *__restrict__ first,
+                                                  const uint32_t *__restrict__ count,
+                                                  uint32_t *__restrict__ album)
+{
+    const uint32_t a = blockIdx.y;
+    for (uint32_t b = blockIdx.x * blockDim.x + threadIdx.x; b < kBins; b += gridDim.x * blockDim.x) {
+        uint32_t s = 0;
+        for (uint32_t t = first[a]; t < first[a] + count[a]; ++t)
+            s += hist[(uint64_t)t * kBins + b];
+        album[(uint64_t)a * kBins + b] = s;
+    }
+}
+
+// analyzeResult (replaygain.c:754-776): NaN = not enough samples
+__global__ __launch_bounds__(64) void k_rg_gain(const uint32_t *__restrict__ hist, uint32_t n,
+                                                double *__restrict__ gain)
+{
+    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h >= n)
+        return;
+    const uint32_t *A = hist + (uint64_t)h * kBins;
+    uint32_t elems = 0;
+    for (int i = 0; i < kBins; ++i)
+        elems += A[i];
+    if (elems == 0) {
+        gain[h] = NAN;
+        return;
+    }
+    int32_t upper = (int32_t)ceil(elems * (1. - 0.95));
+    int i;
+    for (i = kBins - 1; i >= 0; --i)
+        if ((upper -= (int32_t)A[i]) <= 0)
+            break;
+    gain[h] = 64.82 - (double)i / 100.;
+}
+
+struct RgCtx {
+    std::mutex mu;
+    int device = -1;
+    void *tracks = nullptr, *hist = nullptr, *peaks = nullptr, *gains = nullptr, *alb = nullptr,
+         *meta = nullptr;
+    size_t cap_tracks = 0, cap_albums = 0;
+};
+RgCtx g_ctx;
+
+} // namespace
+
+extern "C" {
+
+const char *atg_replaygain_last_error(void) { return g_rg_err.c_str(); }
+
+atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *tracks, uint32_t n,
+                                 uint32_t n_albums, atg_rg_result *results,
+                                 uint32_t *d_album_hist, double *album_peaks, void *stream)
+{
+    if ((!tracks || !results) && n)
+        return rfail(ATG_ERR_INVALID, "NULL argument");
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    hipStream_t s = (hipStream_t)stream;
+    int dev = 0;
+    RHIP(hipGetDevice(&dev));
+    if (g_ctx.device != dev) {
+        RHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_yule), RG_YULE, sizeof(RG_YULE)));
+        RHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_butter), RG_BUTTER, sizeof(RG_BUTTER)));
+        g_ctx.device = dev;
+    }
+    std::vector<RgTrack> tr(n);
+    std::vector<uint32_t> first(n_albums, 0), count(n_albums, 0);
+    for (uint32_t t = 0; t < n; ++t) {
+        const atg_rg_track &a = tracks[t];
+        const int fi = freq_index(a.sample_rate);
+        if (fi < 0)
+            return rfail(ATG_ERR_INVALID, "unsupported sample rate");
+        if (a.channels != 1 && a.channels != 2)
+            return rfail(ATG_ERR_INVALID, "FrameList must contain only 1 or 2 channels");
+        if (a.bits_per_sample != 8 && a.bits_per_sample != 16 && a.bits_per_sample != 24)
+            return rfail(ATG_ERR_INVALID, "unsupported bits per sample");
+        if (n_albums && a.album >= n_albums)
+            return rfail(ATG_ERR_INVALID, "album index out of range");
+        if (n_albums && t && a.album < tracks[t - 1].album)
+            return rfail(ATG_ERR_INVALID, "tracks must be grouped by album");
+        tr[t] = RgTrack{a.pcm_offset * a.channels, a.pcm_frames, a.channels, a.bits_per_sample,
+                        (uint32_t)fi, (uint32_t)std::ceil(a.sample_rate * 0.050)};
+        if (n_albums) {
+            if (!count[a.album])
+                first[a.album] = t;
+            ++count[a.album];
+        }
+    }
+    if (n > g_ctx.cap_tracks) {
+        for (void *p : {g_ctx.tracks, g_ctx.hist, g_ctx.peaks, g_ctx.gains})
+            (void)hipFree(p);
+        RHIP(hipMalloc(&g_ctx.tracks, sizeof(RgTrack) * n));
+        RHIP(hipMalloc(&g_ctx.hist, sizeof(uint32_t) * kBins * (size_t)n));
+        RHIP(hipMalloc(&g_ctx.peaks, sizeof(double) * n));
+        RHIP(hipMalloc(&g_ctx.gains, sizeof(double) * (n + n_albums + 1)));
+        g_ctx.cap_tracks = n;
+    }
+    if (n_albums > g_ctx.cap_albums) {
+        (void)hipFree(g_ctx.alb);
+        (void)hipFree(g_ctx.meta);
+        RHIP(hipMalloc(&g_ctx.alb, sizeof(uint32_t) * kBins * (size_t)n_albums));
+        RHIP(hipMalloc(&g_ctx.meta, sizeof(uint32_t) * 2 * n_albums));
+        (void)hipFree(g_ctx.gains);
+        RHIP(hipMalloc(&g_ctx.gains, sizeof(double) * (g_ctx.cap_tracks + n_albums + 1)));
+        g_ctx.cap_albums = n_albums;
+    }
+    if (!n)
+        return ATG_OK;
+    RHIP(hipMemcpyAsync(g_ctx.tracks, tr.data(), sizeof(RgTrack) * n, hipMemcpyHostToDevice, s));
+    RHIP(hipMemsetAsync(g_ctx.hist, 0, sizeof(uint32_t) * kBins * (size_t)n, s));
+    hipLaunchKernelGGL(k_rg_title, dim3((n + 63) / 64), dim3(64), 0, s, d_pcm,
+                       (const RgTrack *)g_ctx.tracks, n, (uint32_t *)g_ctx.hist,
+                       (double *)g_ctx.peaks);
+    RHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_rg_gain, dim3((n + 63) / 64), dim3(64), 0, s,
+                       (const uint32_t *)g_ctx.hist, n, (double *)g_ctx.gains);
+    RHIP(hipGetLastError());
+    uint32_t *album = d_album_hist ? d_album_hist : (uint32_t *)g_ctx.alb;
+    if (n_albums) {
+        RHIP(hipMemcpyAsync(g_ctx.meta, first.data(), sizeof(uint32_t) * n_albums,
+                            hipMemcpyHostToDevice, s));
+        RHIP(hipMemcpyAsync((uint32_t *)g_ctx.meta + n_albums, count.data(),
+                            sizeof(uint32_t) * n_albums, hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_rg_album, dim3((kBins + 255) / 256, n_albums), dim3(256), 0, s,
+                           (const uint32_t *)g_ctx.hist, (const uint32_t *)g_ctx.meta,
+                           (const uint32_t *)g_ctx.meta + n_albums, album);
+        RHIP(hipGetLastError());
+    }
+    std::vector<double> gains(n), peaks(n);
+    RHIP(hipMemcpyAsync(gains.data(), g_ctx.gains, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    RHIP(hipMemcpyAsync(peaks.data(), g_ctx.peaks, sizeof(double) * n, hipMemcpyDeviceToHost, s));
+    RHIP(hipStreamSynchronize(s));
+    if (album_peaks)
+        for (uint32_t a = 0; a < n_albums; ++a)
+            album_peaks[a] = 0.0; // album_peak starts at 0.0 (replaygain.c:180)
+    for (uint32_t t = 0; t < n; ++t) {
+        // title_gain returns 0.0 when no window completed (replaygain.c:311-318)
+        results[t].status = std::isnan(gains[t]) ? 1 : 0;
+        results[t].title_gain = std::isnan(gains[t]) ? 0.0 : gains[t];
+        results[t].title_peak = peaks[t];
+        if (album_peaks && n_albums)
+            album_peaks[tracks[t].album] = std::max(album_peaks[tracks[t].album], peaks[t]);
+    }
+    return ATG_OK;
+}
+
+atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *gains,
+                                    void *stream)
+{
+    if (!n)
+        return ATG_OK;
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    hipStream_t s = (hipStream_t)stream;
+    double *d_g = nullptr;
+    RHIP(hipMalloc(&d_g, sizeof(double) * n));
+    hipLaunchKernelGGL(k_rg_gain, dim3((n + 63) / 64), dim3(64), 0, s, d_hist, n, d_g);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(gains, d_g, sizeof(double) * n, hipMemcpyDeviceToHost, s);
+    if (e == hipSuccess)
+        e = hipStreamSynchronize(s);
+    (void)hipFree(d_g);
+    if (e != hipSuccess)
+        return rfail(ATG_ERR_DEVICE, hipGetErrorString(e));
+    return ATG_OK;
+}
+
+} // extern "C"

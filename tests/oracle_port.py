@@ -313,3 +313,25 @@ def convert(kind, pcm, channels, in_bps, out_bps=None, mask=0, dither=b""):
     lib.pcmconvport_average.argtypes = [P, P, c_u64, c_u32]
     lib.pcmconvport_average(a.ctypes.data, out.ctypes.data, frames, channels)
     return out[:frames]
+
+
+# --- ReplayGain (oracle/replaygain_port.c; parity unpinned, see header) ---
+def rg_title(pcm, channels, bps, rate):
+    """-> (histogram uint32[12000], title peak)"""
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    A = np.zeros(12000, dtype=np.uint32)
+    P = ctypes.c_void_p
+    lib.rgport_title.argtypes = [P, c_u64, c_u32, c_u32, c_u32, P]
+    lib.rgport_title.restype = ctypes.c_double
+    peak = lib.rgport_title(a.ctypes.data, len(a) // channels, channels, bps, rate,
+                            A.ctypes.data)
+    return A, peak
+
+
+def rg_gain(A):
+    lib = load()
+    A = np.ascontiguousarray(A, dtype=np.uint32)
+    lib.rgport_gain.argtypes = [ctypes.c_void_p]
+    lib.rgport_gain.restype = ctypes.c_double
+    return lib.rgport_gain(A.ctypes.data)

@@ -1,0 +1,78 @@
+"""GPU parity: replaygain.hip vs the CPU oracle (oracle/replaygain_port.c):
+identical per-track 12000-bin window histograms (each track its own album),
+identical peaks, title gains and album gain; the ReplayGain class contract.
+Parity unpinned (no reference fixtures; see the oracle header)."""
+import math
+
+import numpy as np
+import pytest
+
+import oracle_port as op
+import signals
+
+pytestmark = pytest.mark.gpu
+
+CASES = [(44100, 2, 16, 441000), (48000, 1, 16, 100000), (8000, 2, 8, 30000),
+         (96000, 2, 24, 200000), (44100, 2, 16, 4095), (44100, 2, 16, 2205 * 3),
+         (22050, 1, 24, 12345), (192000, 2, 16, 9600 * 5 + 17), (44100, 2, 16, 100)]
+
+
+def make(rate, ch, bps, n, seed):
+    kind = ["tone", "noise", "chirp", "sine"][seed % 4]
+    x = signals.make(kind, n, ch, bps, seed=seed)
+    return np.asarray(x, dtype=np.int32)
+
+
+@pytest.mark.parametrize("rate,ch,bps,n", CASES)
+def test_track_histogram_matches_oracle(rate, ch, bps, n):
+    from audiotools import _atgpu
+    pcms = [make(rate, ch, bps, n + 7 * k, k) for k in range(3)]
+    tracks, off = [], 0
+    for k, p in enumerate(pcms):
+        tracks.append(_atgpu.RgTrack(off, len(p) // ch, ch, bps, rate, k))
+        off += len(p) // ch
+    res, peaks, gains, hist = _atgpu.replaygain_host(np.concatenate(pcms), tracks, len(pcms),
+                                                     return_hist=True)
+    for k, p in enumerate(pcms):
+        A, peak = op.rg_title(p, ch, bps, rate)
+        assert np.array_equal(hist[k], A), k
+        assert res[k].title_peak == peak and peaks[k] == peak
+        g = op.rg_gain(A)
+        if math.isnan(g):
+            assert res[k].status == 1 and res[k].title_gain == 0.0
+        else:
+            assert res[k].title_gain == g and gains[k] == g
+
+
+def test_album_gain_is_percentile_of_summed_histograms():
+    from audiotools import _atgpu
+    pcms = [make(44100, 2, 16, 50000 + 1000 * k, k) for k in range(6)]
+    tracks, off = [], 0
+    for k, p in enumerate(pcms):
+        tracks.append(_atgpu.RgTrack(off, len(p) // 2, 2, 16, 44100, k // 3))
+        off += len(p) // 2
+    res, peaks, gains, hist = _atgpu.replaygain_host(np.concatenate(pcms), tracks, 2,
+                                                     return_hist=True)
+    for a in range(2):
+        B = sum(op.rg_title(p, 2, 16, 44100)[0].astype(np.uint64)
+                for p in pcms[3 * a:3 * a + 3]).astype(np.uint32)
+        assert np.array_equal(hist[a], B)
+        assert gains[a] == op.rg_gain(B)
+        assert peaks[a] == max(op.rg_title(p, 2, 16, 44100)[1] for p in pcms[3 * a:3 * a + 3])
+
+
+def test_replaygain_class_contract():
+    import audiotools
+    from audiotools import replaygain
+    with pytest.raises(ValueError):
+        replaygain.ReplayGain(12345)
+    rg = replaygain.ReplayGain(44100)
+    with pytest.raises(ValueError):
+        rg.album_gain()
+    p1, p2 = make(44100, 2, 16, 60000, 1), make(44100, 2, 16, 70000, 2)
+    g1 = rg.title_gain(audiotools.FrameListReader(p1, 44100, 2, 16))
+    g2 = rg.title_gain(audiotools.FrameListReader(p2, 44100, 2, 16))
+    A1, pk1 = op.rg_title(p1, 2, 16, 44100)
+    A2, pk2 = op.rg_title(p2, 2, 16, 44100)
+    assert g1 == (op.rg_gain(A1), pk1) and g2 == (op.rg_gain(A2), pk2)
+    assert rg.album_gain() == (op.rg_gain(A1 + A2), max(pk1, pk2))
