@@ -266,6 +266,53 @@ def convert_leg(args, torch, device, pcm):
             "verified_dither_invariant": ok}
 
 
+def replaygain_leg(args, torch, dist, world, rank, device, pcm, barrier):
+    """ReplayGain title analysis of every track of the batch (replaygain.hip,
+    SURVEY 8(a) G1-G5) plus one album over ALL ranks' tracks: each rank sums
+    its tracks' window histograms on the GPU, then the 12000-bin uint32
+    histogram is all-reduced (SUM, exact) and the album peak (MAX) over RCCL
+    -- the one real exchange step of the path.  Returns the
+    JSON object (rank 0) and per-track results for the CPU check."""
+    from audiotools import _atgpu
+    x = pcm.to(torch.int32)
+    n_samples = args.frames * BLOCK
+    tracks = [_atgpu.RgTrack(t * n_samples, n_samples, 2, 16, 44100, 0)
+              for t in range(args.tracks)]
+    hist = torch.zeros(12000, dtype=torch.int32, device=device)
+
+    def step():
+        res, peaks = _atgpu.replaygain_device(x.data_ptr(), tracks, 1, hist.data_ptr())
+        pk = torch.tensor([peaks[0]], dtype=torch.float64, device=device)
+        if world > 1:
+            dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+        gain = _atgpu.replaygain_hist_gain(hist.data_ptr(), 1)[0]
+        return res, gain, float(pk.item())
+
+    for _ in range(args.warmup):
+        step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        res, album_gain, album_peak = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, device)
+    host = pcm[:4 * n_samples * 2].cpu().numpy().astype(np.int32)
+    del x
+    frames = args.tracks * args.frames * world * args.steps
+    out = {"metric": "ReplayGain title analysis, FLAC-frame-equivalents/s (4096 PCM frames)",
+           "value": round(frames / elapsed, 1), "unit": "frames/s",
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "album": {"tracks": args.tracks * world, "gain_db": album_gain,
+                     "peak": album_peak,
+                     "collective": "all_reduce SUM uint32[12000] + MAX f64 (RCCL)"
+                                   if world > 1 else "none (1 rank)"},
+           "bound": "serial fp64 IIR per channel (lane per track-channel, 32 waves)"}
+    return out, res, host
+
+
 def main(argv=None):
     args = parse_args(argv)
     import torch
@@ -344,6 +391,10 @@ def main(argv=None):
     convert = None
     if not args.no_decode and rank == 0:
         convert = convert_leg(args, torch, device, pcm)
+    rg = rg_res = rg_host = None
+    if not args.no_decode:
+        rg, rg_res, rg_host = replaygain_leg(args, torch, dist, world, rank, device, pcm,
+                                             barrier)
 
     if rank != 0:
         if world > 1:
@@ -385,6 +436,22 @@ def main(argv=None):
                "sample": "%d tracks x %d FLAC-8 frames of the same synthetic batch, "
                          "%d threads (one track per thread), %.1f s" % (nt, sample_frames,
                                                                         threads, dt)}
+        if rg is not None:
+            # oracle on the first 4 tracks: exact title gains/peaks, timed
+            import oracle_port
+            t0 = time.perf_counter()
+            ok = True
+            for t in range(min(4, args.tracks)):
+                A, pk = oracle_port.rg_title(
+                    rg_host[t * n_samples * 2:(t + 1) * n_samples * 2], 2, 16, 44100)
+                ok = ok and oracle_port.rg_gain(A) == rg_res[t].title_gain and \
+                    pk == rg_res[t].title_peak
+            dt = time.perf_counter() - t0
+            rg["verified_vs_oracle"] = ok
+            rg["cpu_baseline"] = {"value": round(min(4, args.tracks) * args.frames / dt, 2),
+                                  "unit": "frames/s", "cores": 1, "kind": "port",
+                                  "sample": "oracle title analysis of 4 tracks, 1 thread, "
+                                            "%.1f s" % dt}
         if decode is not None:
             host_out = out.cpu().numpy()
             imgs = [host_out[r.out_offset:r.out_offset + r.bytes].tobytes()
@@ -425,6 +492,7 @@ def main(argv=None):
         "cpu_baseline": cpu,
         "decode": decode,
         "convert": convert,
+        "replaygain": rg,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

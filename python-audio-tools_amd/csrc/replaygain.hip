@@ -3,15 +3,16 @@
 // analyze_samples / analyzeResult / get_album_gain (src/replaygain.c
 // :186-322, :566-807).
 //
-//   k_rg_title   lane per track: the Yule-Walker (10th order) + Butterworth
-//                (2nd order) IIR pair per channel is a serial recurrence, so
-//                each lane runs it over its whole track from zero state, in
+//   k_rg_title   lane per (track, channel): the Yule-Walker (10th order) +
+//                Butterworth (2nd order) IIR pair is a serial recurrence, so
+//                each lane runs it over its whole channel from zero state, in
 //                the reference's exact fp64 operation order (no contraction),
 //                summing squared outputs with the reference's batch grouping
 //                (4096-frame reads, 10-sample prebuffer batch, 50 ms windows;
-//                singles for batch % 16, then 16-term groups) and binning
-//                each window as (int)(1000·log10(mean/2 + 1e-37)) into the
-//                track's 12000-bin histogram; title peak = max |x| / 2^(bps-1).
+//                singles for batch % 16, then 16-term groups) into one sum
+//                per closed window; title peak = max |x| / 2^(bps-1).
+//   k_rg_bin     thread per window: (int)(1000·log10((l+r)/n/2 + 1e-37))
+//                into the track's 12000-bin histogram.
 //   k_rg_album   thread per bin: album histogram = sum of its tracks'.
 //   k_rg_gain    lane per histogram: 95th-percentile scan -> 64.82 - i/100.
 //
@@ -96,23 +97,36 @@ __device__ __forceinline__ double filt(Chan &s, double x, const double *ky, cons
     return b;
 }
 
+// lane per (track, channel): the reference keeps separate accumulators for
+// the two channels (lsum, rsum) and only adds them when a window closes, so
+// each lane filters one channel and writes its per-window sums; k_rg_bin
+// bins (lsum + rsum) / window / 2 per window.  Mono tracks filter once and
+// use the same sums for both channels (the reference duplicates the channel).
 __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm,
                                                  const RgTrack *__restrict__ tracks, uint32_t n,
-                                                 uint32_t *__restrict__ hist,
+                                                 const uint64_t *__restrict__ win_base,
+                                                 double *__restrict__ wsum,
                                                  double *__restrict__ peaks)
 {
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= n)
+    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= 2 * n)
         return;
+    const uint32_t t = g >> 1, chan = g & 1;
     const RgTrack T = tracks[t];
+    if (chan == 1 && T.ch == 1)
+        return; // mono: channel 0's sums stand for both
     const double *ky = c_yule[T.fi], *kb = c_butter[T.fi];
-    uint32_t *A = hist + (uint64_t)t * kBins;
-    const int32_t *p = pcm + T.off;
+    const int32_t *p = pcm + T.off + chan;
+    double *W = wsum + 2 * win_base[t] + chan;
     const long window = T.window;
     const double peak_shift = (double)(1 << (T.bps - 1));
-    Chan L = {}, R = {};
-    double lsum = 0, rsum = 0, peak = 0;
-    long totsamp = 0;
+    Chan S = {};
+    double sum = 0, peak = 0;
+    long totsamp = 0, nwin = 0;
+    const uint64_t last = T.frames ? T.frames - 1 : 0;
+    const uint32_t stride = T.ch;
+    int32_t nx = T.frames ? p[0] : 0;
+    uint32_t pf = 0;
     for (uint64_t c0 = 0; c0 < T.frames; c0 += 4096) {
         const long n4 = (long)(T.frames - c0 < 4096 ? T.frames - c0 : 4096);
         long pos = 0, batch = n4;
@@ -121,53 +135,74 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
             if (pos < 10 && cur > 10 - pos)
                 cur = 10 - pos;
             const long singles = cur % 16;
-            double gl = 0, gr = 0;
+            double gs = 0;
             for (long k = 0; k < cur; ++k) {
                 const uint64_t f = c0 + (uint64_t)(pos + k);
-                const int32_t il = p[f * T.ch];
-                const int32_t ir = T.ch == 2 ? p[f * T.ch + 1] : il;
-                double xl, xr;
-                if (T.bps == 8) {
-                    xl = (double)(il << 8);
-                    xr = (double)(ir << 8);
-                } else if (T.bps == 16) {
-                    xl = (double)il;
-                    xr = (double)ir;
-                } else {
-                    xl = (double)(il >> 8);
-                    xr = (double)(ir >> 8);
-                }
-                peak = fmax(peak, (double)abs(il) / peak_shift);
-                peak = fmax(peak, (double)abs(ir) / peak_shift);
-                const double ol = filt(L, xl, ky, kb);
-                const double orr = filt(R, xr, ky, kb);
+                const int32_t iv = nx;
+                const uint64_t f1 = f + 1 < last ? f + 1 : last;
+                nx = p[f1 * stride];
+                const uint64_t f64 = f + 64 < last ? f + 64 : last;
+                pf ^= (uint32_t)p[f64 * stride];
+                double x;
+                if (T.bps == 8)
+                    x = (double)(iv << 8);
+                else if (T.bps == 16)
+                    x = (double)iv;
+                else
+                    x = (double)(iv >> 8);
+                peak = fmax(peak, (double)abs(iv) / peak_shift);
+                const double o = filt(S, x, ky, kb);
                 if (k < singles) {
-                    lsum += ol * ol;
-                    rsum += orr * orr;
+                    sum += o * o;
                 } else {
-                    const long g = (k - singles) & 15;
-                    gl = g == 0 ? ol * ol : gl + ol * ol;
-                    gr = g == 0 ? orr * orr : gr + orr * orr;
-                    if (g == 15) {
-                        lsum += gl;
-                        rsum += gr;
-                    }
+                    const long gi = (k - singles) & 15;
+                    gs = gi == 0 ? o * o : gs + o * o;
+                    if (gi == 15)
+                        sum += gs;
                 }
             }
             batch -= cur;
             pos += cur;
             totsamp += cur;
             if (totsamp == window) {
-                const double val = 100. * 10. * log10((lsum + rsum) / totsamp * 0.5 + 1.e-37);
-                int ival = (int)val;
-                ival = ival < 0 ? 0 : (ival >= kBins ? kBins - 1 : ival);
-                A[ival] += 1u;
-                lsum = rsum = 0.;
+                W[2 * nwin] = sum;
+                if (T.ch == 1)
+                    W[2 * nwin + 1] = sum;
+                ++nwin;
+                sum = 0.;
                 totsamp = 0;
             }
         }
     }
-    peaks[t] = peak;
+    asm volatile("" ::"v"(pf)); // keep the prefetch loads
+    peaks[2 * t + chan] = peak;
+    if (T.ch == 1)
+        peaks[2 * t + 1] = peak;
+}
+
+// bin every closed window: (int)(1000 log10((lsum + rsum) / n * 0.5 + 1e-37))
+// (replaygain.c:713-724), one thread per window
+__global__ __launch_bounds__(256) void k_rg_bin(const RgTrack *__restrict__ tracks, uint32_t n,
+                                                const uint64_t *__restrict__ win_base,
+                                                const double *__restrict__ wsum,
+                                                const double *__restrict__ peak2,
+                                                uint32_t *__restrict__ hist,
+                                                double *__restrict__ peaks)
+{
+    const uint32_t t = blockIdx.y;
+    if (t >= n)
+        return;
+    const uint64_t nw = win_base[t + 1] - win_base[t];
+    const double window = (double)tracks[t].window;
+    for (uint64_t w = blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += gridDim.x * blockDim.x) {
+        const double *ws = wsum + 2 * (win_base[t] + w);
+        const double val = 100. * 10. * log10((ws[0] + ws[1]) / window * 0.5 + 1.e-37);
+        int ival = (int)val;
+        ival = ival < 0 ? 0 : (ival >= kBins ? kBins - 1 : ival);
+        atomicAdd(&hist[(uint64_t)t * kBins + ival], 1u);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0)
+        peaks[t] = fmax(peak2[2 * t], peak2[2 * t + 1]);
 }
 
 // album histogram = sum of its tracks' histograms (tracks [first, first+count))
@@ -212,8 +247,8 @@ struct RgCtx {
     std::mutex mu;
     int device = -1;
     void *tracks = nullptr, *hist = nullptr, *peaks = nullptr, *gains = nullptr, *alb = nullptr,
-         *meta = nullptr;
-    size_t cap_tracks = 0, cap_albums = 0;
+         *meta = nullptr, *wsum = nullptr, *wbase = nullptr, *peak2 = nullptr;
+    size_t cap_tracks = 0, cap_albums = 0, cap_win = 0, cap_wbase = 0, cap_peak2 = 0;
 };
 RgCtx g_ctx;
 
@@ -239,6 +274,7 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
         g_ctx.device = dev;
     }
     std::vector<RgTrack> tr(n);
+    std::vector<uint64_t> wbase(n + 1, 0);
     std::vector<uint32_t> first(n_albums, 0), count(n_albums, 0);
     for (uint32_t t = 0; t < n; ++t) {
         const atg_rg_track &a = tracks[t];
@@ -255,6 +291,7 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
             return rfail(ATG_ERR_INVALID, "tracks must be grouped by album");
         tr[t] = RgTrack{a.pcm_offset * a.channels, a.pcm_frames, a.channels, a.bits_per_sample,
                         (uint32_t)fi, (uint32_t)std::ceil(a.sample_rate * 0.050)};
+        wbase[t + 1] = wbase[t] + a.pcm_frames / tr[t].window;
         if (n_albums) {
             if (!count[a.album])
                 first[a.album] = t;
@@ -281,10 +318,35 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
     }
     if (!n)
         return ATG_OK;
+    if (wbase[n] + 1 > g_ctx.cap_win) {
+        (void)hipFree(g_ctx.wsum);
+        (void)hipFree(g_ctx.wbase);
+        RHIP(hipMalloc(&g_ctx.wsum, sizeof(double) * 2 * (wbase[n] + 1)));
+        RHIP(hipMalloc(&g_ctx.wbase, sizeof(uint64_t) * (n + 1)));
+        g_ctx.cap_win = wbase[n] + 1;
+        g_ctx.cap_wbase = n + 1;
+    }
+    if (n + 1 > g_ctx.cap_wbase) {
+        (void)hipFree(g_ctx.wbase);
+        RHIP(hipMalloc(&g_ctx.wbase, sizeof(uint64_t) * (n + 1)));
+        g_ctx.cap_wbase = n + 1;
+    }
+    if (!g_ctx.peak2 || n > g_ctx.cap_peak2) {
+        (void)hipFree(g_ctx.peak2);
+        RHIP(hipMalloc(&g_ctx.peak2, sizeof(double) * 2 * n));
+        g_ctx.cap_peak2 = n;
+    }
     RHIP(hipMemcpyAsync(g_ctx.tracks, tr.data(), sizeof(RgTrack) * n, hipMemcpyHostToDevice, s));
+    RHIP(hipMemcpyAsync(g_ctx.wbase, wbase.data(), sizeof(uint64_t) * (n + 1),
+                        hipMemcpyHostToDevice, s));
     RHIP(hipMemsetAsync(g_ctx.hist, 0, sizeof(uint32_t) * kBins * (size_t)n, s));
-    hipLaunchKernelGGL(k_rg_title, dim3((n + 63) / 64), dim3(64), 0, s, d_pcm,
-                       (const RgTrack *)g_ctx.tracks, n, (uint32_t *)g_ctx.hist,
+    hipLaunchKernelGGL(k_rg_title, dim3((2 * n + 63) / 64), dim3(64), 0, s, d_pcm,
+                       (const RgTrack *)g_ctx.tracks, n, (const uint64_t *)g_ctx.wbase,
+                       (double *)g_ctx.wsum, (double *)g_ctx.peak2);
+    RHIP(hipGetLastError());
+    hipLaunchKernelGGL(k_rg_bin, dim3(4, n), dim3(256), 0, s, (const RgTrack *)g_ctx.tracks, n,
+                       (const uint64_t *)g_ctx.wbase, (const double *)g_ctx.wsum,
+                       (const double *)g_ctx.peak2, (uint32_t *)g_ctx.hist,
                        (double *)g_ctx.peaks);
     RHIP(hipGetLastError());
     hipLaunchKernelGGL(k_rg_gain, dim3((n + 63) / 64), dim3(64), 0, s,
