@@ -266,6 +266,15 @@ def convert_leg(args, torch, device, pcm):
             "verified_dither_invariant": ok}
 
 
+def album_reduce(dist, world, hist, peak):
+    """an album spread over ranks: SUM of the uint32 window histograms (held
+    as int32; two's-complement sums are the same bits) and MAX of the peak,
+    in place -- exact and order-independent (SURVEY 8(e) ReplayGain row)"""
+    if world > 1:
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
+        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+
+
 def replaygain_leg(args, torch, dist, world, rank, device, pcm, barrier):
     """ReplayGain title analysis of every track of the batch (replaygain.hip,
     SURVEY 8(a) G1-G5) plus one album over ALL ranks' tracks: each rank sums
@@ -283,9 +292,7 @@ def replaygain_leg(args, torch, dist, world, rank, device, pcm, barrier):
     def step():
         res, peaks = _atgpu.replaygain_device(x.data_ptr(), tracks, 1, hist.data_ptr())
         pk = torch.tensor([peaks[0]], dtype=torch.float64, device=device)
-        if world > 1:
-            dist.all_reduce(hist, op=dist.ReduceOp.SUM)
-            dist.all_reduce(pk, op=dist.ReduceOp.MAX)
+        album_reduce(dist, world, hist, pk)
         gain = _atgpu.replaygain_hist_gain(hist.data_ptr(), 1)[0]
         return res, gain, float(pk.item())
 

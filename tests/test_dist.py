@@ -69,3 +69,54 @@ def test_two_rank_shards_and_clock():
             pcm = signals.make("tone", 4096 + 37 * t, 2, 16, seed=t)
             data, _ = oracle_port.encode(pcm, 2, 16, 44100, **oracle_port.PRESETS["8"])
             assert hashlib.sha256(data).hexdigest() == h
+
+
+def _rg_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      RANK=str(rank), WORLD_SIZE=str(world))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import oracle_port
+        import signals
+        # this rank's tracks of one album: histograms summed locally, then
+        # the album reduce of bench.py over the ranks
+        local = np.zeros(12000, dtype=np.uint64)
+        peak = 0.0
+        for t in bench.shard(world, rank, 2):
+            pcm = signals.make("tone", 30000 + 1000 * t, 2, 16, seed=t)
+            A, pk = oracle_port.rg_title(pcm, 2, 16, 44100)
+            local += A
+            peak = max(peak, pk)
+        hist = torch.tensor(local.astype(np.int64), dtype=torch.int32)
+        pkt = torch.tensor([peak], dtype=torch.float64)
+        bench.album_reduce(dist, world, hist, pkt)
+        q.put((rank, hist.numpy().astype(np.uint32), float(pkt.item())))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_two_rank_album_reduce_matches_single_process():
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_rg_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    import oracle_port
+    import signals
+    B = np.zeros(12000, dtype=np.uint64)
+    peak = 0.0
+    for t in range(4):
+        A, pk = oracle_port.rg_title(signals.make("tone", 30000 + 1000 * t, 2, 16, seed=t),
+                                     2, 16, 44100)
+        B += A
+        peak = max(peak, pk)
+    for _, hist, pk in res:
+        assert np.array_equal(hist, B.astype(np.uint32))
+        assert pk == peak
+        assert oracle_port.rg_gain(hist) == oracle_port.rg_gain(B.astype(np.uint32))
