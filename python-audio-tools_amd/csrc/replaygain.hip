@@ -121,7 +121,10 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
     const long window = T.window;
     const double peak_shift = (double)(1 << (T.bps - 1));
     Chan S = {};
-    double sum = 0, peak = 0;
+    double sum = 0;
+    // max |x| as an integer: dividing by 2^(bps-1) is exact and monotonic,
+    // so max(|x|) / 2^(bps-1) == max(|x| / 2^(bps-1)) bit for bit
+    uint32_t amax = 0;
     long totsamp = 0, nwin = 0;
     const uint64_t last = T.frames ? T.frames - 1 : 0;
     const uint32_t stride = T.ch;
@@ -150,7 +153,8 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
                     x = (double)iv;
                 else
                     x = (double)(iv >> 8);
-                peak = fmax(peak, (double)abs(iv) / peak_shift);
+                const uint32_t av = (uint32_t)(iv < 0 ? -(int64_t)iv : iv);
+                amax = av > amax ? av : amax;
                 const double o = filt(S, x, ky, kb);
                 if (k < singles) {
                     sum += o * o;
@@ -175,6 +179,7 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
         }
     }
     asm volatile("" ::"v"(pf)); // keep the prefetch loads
+    const double peak = (double)amax / peak_shift;
     peaks[2 * t + chan] = peak;
     if (T.ch == 1)
         peaks[2 * t + 1] = peak;
