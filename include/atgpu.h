@@ -320,6 +320,23 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
 atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *gains,
                                     void *stream);
 
+/* ReplayGainReader (src/replaygain.c:820-925): multiplier from (gain, peak)
+   as ReplayGainReader_init computes it (long double pow; 1/peak when the
+   gain would amplify), then per sample lround(x * multiplier), clamp to
+   bits_per_sample, XOR one dither bit (consumed per read(chunk_frames)
+   call, channel by channel, MSB first, starting at dither_bit0). */
+double atg_replaygain_multiplier(double replaygain, double peak);
+atg_status atg_pcm_apply_gain_device(const int32_t *d_in, int32_t *d_out, uint64_t frames,
+                                     uint32_t channels, uint32_t bits_per_sample,
+                                     double multiplier, uint32_t chunk_frames,
+                                     const uint8_t *d_dither, uint64_t dither_bit0,
+                                     void *stream);
+atg_status atg_pcm_apply_gain_host(int device, const int32_t *in, int32_t *out,
+                                   uint64_t frames, uint32_t channels,
+                                   uint32_t bits_per_sample, double multiplier,
+                                   uint32_t chunk_frames, const uint8_t *dither,
+                                   uint64_t dither_bytes, uint64_t dither_bit0);
+
 #ifdef __cplusplus
 }
 #endif

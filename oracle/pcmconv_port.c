@@ -74,3 +74,32 @@ void pcmconvport_average(const int32_t *in, int32_t *out, uint64_t frames, uint3
         out[f] = (int)(acc / ch);
     }
 }
+
+/* ReplayGainReader_init / _read (src/replaygain.c:820-925) over a track read
+   in chunks of chunk_frames (the caller's read(pcm_frames) size) */
+double pcmconvport_rg_multiplier(double replaygain, double peak)
+{
+    double m = (double)powl(10.0L, (long double)replaygain / 20.0L);
+    if (m > 1.0)
+        m = (double)(1.0L / (long double)peak);
+    return m;
+}
+
+void pcmconvport_apply_gain(const int32_t *in, int32_t *out, uint64_t frames, uint32_t ch,
+                            uint32_t bps, double multiplier, uint32_t chunk_frames,
+                            const uint8_t *dither)
+{
+    const int max_value = (1 << (bps - 1)) - 1, min_value = -(1 << (bps - 1));
+    uint64_t bit = 0;
+    for (uint64_t f0 = 0; f0 < frames; f0 += chunk_frames) {
+        const uint64_t n = frames - f0 < chunk_frames ? frames - f0 : chunk_frames;
+        for (uint32_t c = 0; c < ch; c++)
+            for (uint64_t i = 0; i < n; i++) {
+                int v = (int)lround(in[(f0 + i) * ch + c] * multiplier);
+                v = v < min_value ? min_value : (v > max_value ? max_value : v);
+                const int b = (dither[bit >> 3] >> (7 - (bit & 7))) & 1;
+                bit++;
+                out[(f0 + i) * ch + c] = v ^ b;
+            }
+    }
+}

@@ -37,6 +37,7 @@ EXPORTS = (
     "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
+    "atg_replaygain_multiplier", "atg_pcm_apply_gain_device", "atg_pcm_apply_gain_host",
 )
 
 CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
@@ -221,6 +222,14 @@ def load_library():
         lib.atg_replaygain_device.restype = ctypes.c_int
         lib.atg_replaygain_hist_gain.argtypes = [P, c_u32, ctypes.POINTER(ctypes.c_double), P]
         lib.atg_replaygain_hist_gain.restype = ctypes.c_int
+        lib.atg_replaygain_multiplier.argtypes = [ctypes.c_double, ctypes.c_double]
+        lib.atg_replaygain_multiplier.restype = ctypes.c_double
+        lib.atg_pcm_apply_gain_device.argtypes = [
+            P, P, c_u64, c_u32, c_u32, ctypes.c_double, c_u32, P, c_u64, P]
+        lib.atg_pcm_apply_gain_device.restype = ctypes.c_int
+        lib.atg_pcm_apply_gain_host.argtypes = [
+            ctypes.c_int, P, P, c_u64, c_u32, c_u32, ctypes.c_double, c_u32, P, c_u64, c_u64]
+        lib.atg_pcm_apply_gain_host.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -556,3 +565,19 @@ def replaygain_host(pcm, tracks, n_albums=0, return_hist=False):
     if return_hist:
         return res, peaks, gains, hist[:n_albums]
     return res, peaks, gains
+
+
+def apply_gain(pcm, channels, bits_per_sample, multiplier, chunk_frames, dither,
+               dither_bit0=0, device=None):
+    """ReplayGainReader sample transform on the GPU (atg_pcm_apply_gain_host)"""
+    lib = load_library()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    out = np.empty(max(1, len(a)), dtype=np.int32)
+    d = np.frombuffer(bytes(dither) or b"\0", dtype=np.uint8)
+    st = lib.atg_pcm_apply_gain_host(
+        default_device() if device is None else device, a.ctypes.data_as(ctypes.c_void_p),
+        out.ctypes.data_as(ctypes.c_void_p), len(a) // channels, channels, bits_per_sample,
+        multiplier, chunk_frames, d.ctypes.data_as(ctypes.c_void_p), len(d), dither_bit0)
+    if st != ATG_OK:
+        raise ATGError(st, lib.atg_pcm_convert_last_error().decode("utf-8", "replace"))
+    return out[:len(a)]

@@ -11,6 +11,7 @@ No CPU path.
 """
 
 import math
+import os
 
 import numpy as np
 
@@ -82,3 +83,44 @@ def batch_gains(pcm_i32, tracks, n_albums):
     -> ([(title_gain, title_peak)], [(album_gain, album_peak)])"""
     res, peaks, gains = _atgpu.replaygain_host(pcm_i32, tracks, n_albums)
     return ([(r.title_gain, r.title_peak) for r in res], list(zip(gains, peaks)))
+
+
+class ReplayGainReader(object):
+    """reference replaygain.ReplayGainReader(pcmreader, replaygain, peak)
+    (src/replaygain.c:820-925): a PCMReader applying the gain with
+    lround, clamping and one XOR dither bit per sample (os.urandom, or
+    `dither=` callable n -> bytes for reproducible output)"""
+
+    def __init__(self, pcmreader, replaygain, peak, dither=None):
+        self.pcmreader = pcmreader
+        self.sample_rate = pcmreader.sample_rate
+        self.channels = pcmreader.channels
+        self.channel_mask = pcmreader.channel_mask
+        self.bits_per_sample = pcmreader.bits_per_sample
+        self.multiplier = _atgpu.load_library().atg_replaygain_multiplier(
+            float(replaygain), float(peak))
+        self._rand = dither if dither is not None else os.urandom
+        self._bits = b""
+        self._bitpos = 0
+
+    def read(self, pcm_frames):
+        if pcm_frames <= 0:
+            raise ValueError("pcm_frames must be positive")
+        fl = self.pcmreader.read(pcm_frames)
+        if not isinstance(fl, pcm.FrameList):
+            raise TypeError("pcmreader.read() must return a FrameList")
+        if not fl.frames:
+            return fl
+        n = len(fl)
+        have = len(self._bits) * 8 - self._bitpos
+        if have < n:
+            self._bits = self._bits[self._bitpos // 8:] + self._rand(
+                max((n - have + 7) // 8, 4096))
+            self._bitpos %= 8
+        out = _atgpu.apply_gain(fl.samples, self.channels, self.bits_per_sample,
+                                self.multiplier, fl.frames, self._bits, self._bitpos)
+        self._bitpos += n
+        return pcm.FrameList._wrap(out, self.channels, self.bits_per_sample)
+
+    def close(self):
+        self.pcmreader.close()

@@ -19,6 +19,7 @@
 // reproducible and testable; the reference draws them from os.urandom.
 #include <hip/hip_runtime.h>
 
+#include <cmath>
 #include <string>
 
 #include "../../include/atgpu.h"
@@ -97,6 +98,39 @@ __global__ __launch_bounds__(256) void k_pcm_bps(const int32_t *__restrict__ in,
                 c = 0;
                 ++f;
             }
+        }
+    }
+}
+
+// ReplayGainReader_read (src/replaygain.c:886-925): lround(x * multiplier),
+// clamp, XOR one dither bit; bits consumed per read(pcm_frames) chunk,
+// channel by channel (chunk = the caller's pcm_frames)
+__global__ __launch_bounds__(256) void k_pcm_gain(const int32_t *__restrict__ in,
+                                                  int32_t *__restrict__ out, uint64_t frames,
+                                                  uint32_t ch, uint32_t bps, double mult,
+                                                  uint32_t chunk_frames,
+                                                  const uint8_t *__restrict__ dither,
+                                                  uint64_t bit0)
+{
+    const uint64_t q0 = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    const uint64_t n = frames * ch;
+    if (q0 >= n)
+        return;
+    const int32_t maxv = (1 << (bps - 1)) - 1, minv = -(1 << (bps - 1));
+    uint64_t f = q0 / ch;
+    uint32_t c = (uint32_t)(q0 - f * ch);
+    const uint64_t qe = q0 + 4 < n ? q0 + 4 : n;
+    for (uint64_t q = q0; q < qe; ++q) {
+        const uint64_t chunk = f / chunk_frames * chunk_frames;
+        const uint64_t clen = frames - chunk < chunk_frames ? frames - chunk : chunk_frames;
+        const uint64_t b = bit0 + chunk * ch + (uint64_t)c * clen + (f - chunk);
+        const int32_t bit = (dither[b >> 3] >> (7 - (uint32_t)(b & 7))) & 1;
+        int32_t v = (int32_t)lround((double)in[q] * mult);
+        v = v < minv ? minv : (v > maxv ? maxv : v);
+        out[q] = v ^ bit;
+        if (++c == ch) {
+            c = 0;
+            ++f;
         }
     }
 }
@@ -243,6 +277,76 @@ atg_status atg_pcm_convert_host(int device, int kind, const int32_t *in, int32_t
         (hipDeviceSynchronize() != hipSuccess ||
          hipMemcpy(out, dout, sizeof(int32_t) * frames * oc, hipMemcpyDeviceToHost) != hipSuccess))
         st = cfail(ATG_ERR_DEVICE, "conversion failed on the device");
+    (void)hipFree(di);
+    (void)hipFree(dout);
+    (void)hipFree(dd);
+    return st;
+}
+
+double atg_replaygain_multiplier(double replaygain, double peak)
+{
+    // ReplayGainReader_init (replaygain.c:838-842): long double pow, stored
+    // in a double; gains above unity are replaced by 1 / peak
+    double m = (double)powl(10.0L, (long double)replaygain / 20.0L);
+    if (m > 1.0)
+        m = (double)(1.0L / (long double)peak);
+    return m;
+}
+
+atg_status atg_pcm_apply_gain_device(const int32_t *d_in, int32_t *d_out, uint64_t frames,
+                                     uint32_t channels, uint32_t bps, double multiplier,
+                                     uint32_t chunk_frames, const uint8_t *d_dither,
+                                     uint64_t dither_bit0, void *stream)
+{
+    if (((!d_in || !d_out) && frames) || !d_dither)
+        return cfail(ATG_ERR_INVALID, "NULL buffer");
+    if (channels < 1 || bps < 1 || bps > 32 || chunk_frames < 1)
+        return cfail(ATG_ERR_INVALID, "bad channels / bits per sample / chunk");
+    if (!frames)
+        return ATG_OK;
+    hipLaunchKernelGGL(k_pcm_gain, dim3((unsigned)((frames * channels + 1023) / 1024)),
+                       dim3(256), 0, (hipStream_t)stream, d_in, d_out, frames, channels, bps,
+                       multiplier, chunk_frames, d_dither, dither_bit0);
+    CHIP(hipGetLastError());
+    return ATG_OK;
+}
+
+atg_status atg_pcm_apply_gain_host(int device, const int32_t *in, int32_t *out, uint64_t frames,
+                                   uint32_t channels, uint32_t bps, double multiplier,
+                                   uint32_t chunk_frames, const uint8_t *dither,
+                                   uint64_t dither_bytes, uint64_t dither_bit0)
+{
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0)
+        return cfail(ATG_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n)
+        return cfail(ATG_ERR_INVALID, "device index out of range");
+    CHIP(hipSetDevice(device));
+    if (dither_bytes * 8 < frames * channels + dither_bit0)
+        return cfail(ATG_ERR_INVALID, "not enough dither bytes");
+    void *di = nullptr, *dout = nullptr, *dd = nullptr;
+    const size_t nb = sizeof(int32_t) * (frames * channels ? frames * channels : 1);
+    if (hipMalloc(&di, nb) != hipSuccess || hipMalloc(&dout, nb) != hipSuccess ||
+        hipMalloc(&dd, dither_bytes ? dither_bytes : 1) != hipSuccess) {
+        (void)hipFree(di);
+        (void)hipFree(dout);
+        (void)hipFree(dd);
+        return cfail(ATG_ERR_NOMEM, "device allocation failed");
+    }
+    atg_status st = ATG_OK;
+    if (hipMemcpy(di, in, sizeof(int32_t) * frames * channels, hipMemcpyHostToDevice) !=
+            hipSuccess ||
+        (dither_bytes && hipMemcpy(dd, dither, dither_bytes, hipMemcpyHostToDevice) != hipSuccess))
+        st = cfail(ATG_ERR_DEVICE, "copy to device failed");
+    if (st == ATG_OK)
+        st = atg_pcm_apply_gain_device((const int32_t *)di, (int32_t *)dout, frames, channels,
+                                       bps, multiplier, chunk_frames, (const uint8_t *)dd,
+                                       dither_bit0, nullptr);
+    if (st == ATG_OK &&
+        (hipDeviceSynchronize() != hipSuccess ||
+         hipMemcpy(out, dout, sizeof(int32_t) * frames * channels, hipMemcpyDeviceToHost) !=
+             hipSuccess))
+        st = cfail(ATG_ERR_DEVICE, "gain application failed on the device");
     (void)hipFree(di);
     (void)hipFree(dout);
     (void)hipFree(dd);

@@ -335,3 +335,23 @@ def rg_gain(A):
     lib.rgport_gain.argtypes = [ctypes.c_void_p]
     lib.rgport_gain.restype = ctypes.c_double
     return lib.rgport_gain(A.ctypes.data)
+
+
+def rg_multiplier(gain, peak):
+    lib = load()
+    lib.pcmconvport_rg_multiplier.argtypes = [ctypes.c_double, ctypes.c_double]
+    lib.pcmconvport_rg_multiplier.restype = ctypes.c_double
+    return lib.pcmconvport_rg_multiplier(gain, peak)
+
+
+def rg_apply(pcm, channels, bps, multiplier, chunk_frames, dither):
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    out = np.empty(max(1, len(a)), dtype=np.int32)
+    d = np.frombuffer(bytes(dither) or b"\0", dtype=np.uint8)
+    P = ctypes.c_void_p
+    lib.pcmconvport_apply_gain.argtypes = [P, P, c_u64, c_u32, c_u32, ctypes.c_double,
+                                           c_u32, P]
+    lib.pcmconvport_apply_gain(a.ctypes.data, out.ctypes.data, len(a) // channels, channels,
+                               bps, multiplier, chunk_frames, d.ctypes.data)
+    return out[:len(a)]

@@ -76,3 +76,44 @@ def test_replaygain_class_contract():
     A2, pk2 = op.rg_title(p2, 2, 16, 44100)
     assert g1 == (op.rg_gain(A1), pk1) and g2 == (op.rg_gain(A2), pk2)
     assert rg.album_gain() == (op.rg_gain(A1 + A2), max(pk1, pk2))
+
+
+@pytest.mark.parametrize("gain,peak,ch,bps,chunk", [(-6.5, 0.8, 2, 16, 4096), (4.0, 0.5, 2, 16, 1000),
+                                                    (-1.25, 0.99, 1, 24, 333), (2.0, 0.25, 2, 8, 4096)])
+def test_rg_reader_matches_oracle(gain, peak, ch, bps, chunk):
+    from audiotools import _atgpu
+    rng = np.random.RandomState(int(abs(gain) * 10) + ch)
+    n = 9001
+    x = rng.randint(-2 ** (bps - 1), 2 ** (bps - 1), size=n * ch).astype(np.int32)
+    d = rng.bytes(n * ch // 8 + 2)
+    m = _atgpu.load_library().atg_replaygain_multiplier(gain, peak)
+    assert m == op.rg_multiplier(gain, peak)
+    got = _atgpu.apply_gain(x, ch, bps, m, chunk, d)
+    assert np.array_equal(got, op.rg_apply(x, ch, bps, m, chunk, d))
+
+
+def test_rg_reader_class():
+    import audiotools
+    from audiotools import replaygain
+    rng = np.random.RandomState(9)
+    x = rng.randint(-32768, 32768, size=2 * 10000).astype(np.int32)
+    stream = rng.bytes(4096)
+    pos = [0]
+
+    def dither(k):
+        b = stream[pos[0]:pos[0] + k]
+        pos[0] += k
+        return b + b"\0" * (k - len(b))
+
+    r = replaygain.ReplayGainReader(audiotools.FrameListReader(x, 44100, 2, 16), -3.0, 0.9,
+                                    dither=dither)
+    with pytest.raises(ValueError):
+        r.read(0)
+    got = []
+    while True:
+        fl = r.read(3000)
+        if not len(fl):
+            break
+        got.append(fl.samples)
+    want = op.rg_apply(x, 2, 16, op.rg_multiplier(-3.0, 0.9), 3000, stream)
+    assert np.array_equal(np.concatenate(got), want)

@@ -45,3 +45,15 @@ def test_percentile_rule():
     A[5000] = 10                   # upper = ceil(100 * 0.05) = 5 -> bin 5000
     assert math.isclose(op.rg_gain(A), 64.82 - 50.0)
     assert math.isnan(op.rg_gain(np.zeros(12000, dtype=np.uint32)))
+
+
+def test_rg_reader_oracle_invariants():
+    m = op.rg_multiplier(-6.0, 0.9)
+    assert math.isclose(m, 10 ** (-6.0 / 20), rel_tol=1e-15)
+    assert op.rg_multiplier(3.0, 0.5) == 2.0          # amplifying gain -> 1 / peak
+    rng = np.random.RandomState(3)
+    x = rng.randint(-32768, 32768, size=2 * 5000).astype(np.int32)
+    d = rng.bytes(2 * 5000 // 8 + 1)
+    y = op.rg_apply(x, 2, 16, 2.0, 4096, d)
+    base = np.clip(np.round(x.astype(np.float64) * 2.0), -32768, 32767).astype(np.int32)
+    assert set(np.unique(y ^ base)) <= {0, 1}
