@@ -14,7 +14,7 @@
 //   k_rg_bin     thread per window: (int)(1000·log10((l+r)/n/2 + 1e-37))
 //                into the track's 12000-bin histogram.
 //   k_rg_album   thread per bin: album histogram = sum of its tracks'.
-//   k_rg_gain    lane per histogram: 95th-percentile scan -> 64.82 - i/100.
+//   k_rg_gain    block per histogram: 95th-percentile bin -> 64.82 - i/100.
 //
 // Multi-GPU: an album split across ranks all-reduces its uint32 histogram
 // (sum, exact) and peak (max) -- the caller does that over RCCL between
@@ -225,27 +225,50 @@ __global__ __launch_bounds__(256) void k_rg_album(const uint32_t *__restrict__ h
     }
 }
 
-// analyzeResult (replaygain.c:754-776): NaN = not enough samples
-__global__ __launch_bounds__(64) void k_rg_gain(const uint32_t *__restrict__ hist, uint32_t n,
-                                                double *__restrict__ gain)
+// analyzeResult (replaygain.c:754-776): NaN = not enough samples.  Block
+// per histogram: 256 threads own contiguous bin chunks; the answer is the
+// largest bin i whose suffix sum reaches upper = ceil(0.05 * total), which
+// is exactly where the reference's top-down `upper -= A[i]` loop stops.
+__global__ __launch_bounds__(256) void k_rg_gain(const uint32_t *__restrict__ hist, uint32_t n,
+                                                 double *__restrict__ gain)
 {
-    const uint32_t h = blockIdx.x * blockDim.x + threadIdx.x;
+    __shared__ uint32_t csum[256];
+    __shared__ uint32_t suffix[257];
+    const uint32_t h = blockIdx.x, tid = threadIdx.x;
     if (h >= n)
         return;
     const uint32_t *A = hist + (uint64_t)h * kBins;
-    uint32_t elems = 0;
-    for (int i = 0; i < kBins; ++i)
-        elems += A[i];
+    const uint32_t per = (kBins + 255) / 256;
+    const uint32_t lo = tid * per, hi = lo + per < (uint32_t)kBins ? lo + per : (uint32_t)kBins;
+    uint32_t c = 0;
+    for (uint32_t i = lo; i < hi; ++i)
+        c += A[i];
+    csum[tid] = c;
+    __syncthreads();
+    if (tid == 0) {
+        suffix[256] = 0;
+        for (int k = 255; k >= 0; --k)
+            suffix[k] = suffix[k + 1] + csum[k];
+    }
+    __syncthreads();
+    const uint32_t elems = suffix[0];
     if (elems == 0) {
-        gain[h] = NAN;
+        if (tid == 0)
+            gain[h] = NAN;
         return;
     }
-    int32_t upper = (int32_t)ceil(elems * (1. - 0.95));
-    int i;
-    for (i = kBins - 1; i >= 0; --i)
-        if ((upper -= (int32_t)A[i]) <= 0)
-            break;
-    gain[h] = 64.82 - (double)i / 100.;
+    const int64_t upper = (int32_t)ceil(elems * (1. - 0.95));
+    // the chunk where the suffix first reaches upper, scanning downward
+    if ((int64_t)suffix[tid] >= upper && (int64_t)suffix[tid + 1] < upper) {
+        int64_t run = suffix[tid + 1];
+        int i = (int)hi - 1;
+        for (; i >= (int)lo; --i) {
+            run += A[i];
+            if (run >= upper)
+                break;
+        }
+        gain[h] = 64.82 - (double)i / 100.;
+    }
 }
 
 struct RgCtx {
@@ -354,8 +377,8 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
                        (const double *)g_ctx.peak2, (uint32_t *)g_ctx.hist,
                        (double *)g_ctx.peaks);
     RHIP(hipGetLastError());
-    hipLaunchKernelGGL(k_rg_gain, dim3((n + 63) / 64), dim3(64), 0, s,
-                       (const uint32_t *)g_ctx.hist, n, (double *)g_ctx.gains);
+    hipLaunchKernelGGL(k_rg_gain, dim3(n), dim3(256), 0, s, (const uint32_t *)g_ctx.hist, n,
+                       (double *)g_ctx.gains);
     RHIP(hipGetLastError());
     uint32_t *album = d_album_hist ? d_album_hist : (uint32_t *)g_ctx.alb;
     if (n_albums) {
@@ -395,7 +418,7 @@ atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *
     hipStream_t s = (hipStream_t)stream;
     double *d_g = nullptr;
     RHIP(hipMalloc(&d_g, sizeof(double) * n));
-    hipLaunchKernelGGL(k_rg_gain, dim3((n + 63) / 64), dim3(64), 0, s, d_hist, n, d_g);
+    hipLaunchKernelGGL(k_rg_gain, dim3(n), dim3(256), 0, s, d_hist, n, d_g);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess)
         e = hipMemcpyAsync(gains, d_g, sizeof(double) * n, hipMemcpyDeviceToHost, s);
