@@ -51,28 +51,24 @@ class ReplayGain(object):
         return (res.title_gain, res.title_peak)
 
     def _run(self, titles, album):
-        tracks, off = [], 0
+        # the reference analyses mono as a duplicated stereo pair
+        # (replaygain.c:228-229), so mono titles are widened and every title
+        # of the album goes in one 2-channel batch
+        bufs, tracks, off = [], [], 0
         for s, ch, bps in titles:
-            t = _atgpu.RgTrack(off, len(s) // ch, ch, bps, self.sample_rate, 0)
-            tracks.append(t)
-            off += len(s) // ch
-        # tracks are addressed by PCM frame: pad mono to the batch layout
-        # by keeping one buffer per channel count
-        chans = set(ch for _, ch, _ in titles)
-        if len(chans) > 1:
-            # mixed mono/stereo: analyse one track at a time (album histogram
-            # summed on the host, exact integer sums)
-            outs = [self._run([t], album) for t in titles]
-            res = [o[0][0] for o in outs]
-            return res, [max([o[1][0] for o in outs] or [0.0])], None
-        buf = np.concatenate([s for s, _, _ in titles]) if titles else np.zeros(0, np.int32)
+            st = np.repeat(s, 2) if ch == 1 else s
+            frames = len(st) // 2
+            tracks.append(_atgpu.RgTrack(off, frames, 2, bps, self.sample_rate, 0))
+            bufs.append(st)
+            off += frames
+        buf = np.concatenate(bufs) if bufs else np.zeros(0, np.int32)
         return _atgpu.replaygain_host(buf, tracks, 1 if album else 0)
 
     def album_gain(self):
         if not self._titles:
             raise ValueError("Not enough samples to perform calculation")
         res, peaks, gains = self._run(self._titles, album=True)
-        if gains is None or math.isnan(gains[0]):
+        if not gains or math.isnan(gains[0]):
             raise ValueError("Not enough samples to perform calculation")
         return (gains[0], peaks[0])
 

@@ -117,3 +117,16 @@ def test_rg_reader_class():
         got.append(fl.samples)
     want = op.rg_apply(x, 2, 16, op.rg_multiplier(-3.0, 0.9), 3000, stream)
     assert np.array_equal(np.concatenate(got), want)
+
+
+def test_replaygain_class_mixed_mono_stereo():
+    import audiotools
+    from audiotools import replaygain
+    rg = replaygain.ReplayGain(48000)
+    m, st = make(48000, 1, 16, 50000, 3), make(48000, 2, 16, 40000, 1)
+    g1 = rg.title_gain(audiotools.FrameListReader(m, 48000, 1, 16))
+    g2 = rg.title_gain(audiotools.FrameListReader(st, 48000, 2, 16))
+    A1, p1 = op.rg_title(m, 1, 16, 48000)
+    A2, p2 = op.rg_title(st, 2, 16, 48000)
+    assert g1 == (op.rg_gain(A1), p1) and g2 == (op.rg_gain(A2), p2)
+    assert rg.album_gain() == (op.rg_gain(A1 + A2), max(p1, p2))
