@@ -309,7 +309,8 @@ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
 template <int W>
 struct WinPred {
     int32_t *out;   // planar samples (warm-up only)
-    int32_t *row;   // this lane's column of the wave's row scratch
+    int4 *row;      // wave row scratch, [row/4][lane][4]: lane column at row[.. * 64]
+    int32_t q0, q1, q2, q3; // the 4 rows stored together
     uint32_t i, n, t, wasted, shift, half, porder;
     bool fast, bad;
     int32_t c[W];
@@ -351,8 +352,22 @@ struct WinPred {
         for (int j = W - 1; j > 0; --j)
             h[j] = commit ? h[j - 1] : h[j];
         h[0] = commit ? s : h[0];
-        row[(uint64_t)t * 64] = (int32_t)((uint32_t)s << wasted);
+        const int32_t v = (int32_t)((uint32_t)s << wasted);
+        const uint32_t k = t & 3;
+        q0 = k == 0 ? v : q0;
+        q1 = k == 1 ? v : q1;
+        q2 = k == 2 ? v : q2;
+        q3 = k == 3 ? v : q3;
+        // one 16-byte store per 4 iterations (64 lanes: 1 KB contiguous):
+        // a store waits in the same in-order vmcnt queue as the next load
+        if (k == 3)
+            row[(uint64_t)(t >> 2) * 64] = make_int4(q0, q1, q2, q3);
         ++t;
+    }
+    __device__ __forceinline__ void flush()
+    {
+        if (t & 3)
+            row[(uint64_t)(t >> 2) * 64] = make_int4(q0, q1, q2, q3);
     }
 };
 
@@ -744,7 +759,7 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
 template <int W>
 __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
                                             uint32_t kind, uint32_t order, int32_t *out,
-                                            int32_t *row, JobMeta &m, bool allow_fast)
+                                            int4 *row, JobMeta &m, bool allow_fast)
 {
     WinPred<W> p;
     p.out = out;
@@ -788,7 +803,9 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
 #if ATG_DEC_EXP == 2 // timing experiment: int64 sums only
     p.fast = false;
 #endif
+    p.q0 = p.q1 = p.q2 = p.q3 = 0;
     dec_residual(r, order, N, p);
+    p.flush();
     m.porder = (uint8_t)p.porder;
     m.iters = p.t;
     return p.fast && p.bad;
@@ -815,7 +832,8 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     r.init(w, nw, f.pos * 8 + f.sub_bit[c], tr[f.track].end * 8);
     const uint32_t N = f.n;
     int32_t *out = planar + f.pcm_start + (uint64_t)c * N;
-    int32_t *row = rows + (uint64_t)blockIdx.x * nrows * 64 + threadIdx.x;
+    // [row/4][lane][4] scratch: this lane's 16-byte cells, every 64th int4
+    int4 *row = (int4 *)(rows + (uint64_t)blockIdx.x * nrows * 64) + threadIdx.x;
     JobMeta m;
     m.kind = 3;
     m.order = 0;
@@ -835,7 +853,8 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
             m.kind = 1;
             m.iters = N;
             for (uint32_t i = 0; i < N; ++i)
-                row[(uint64_t)i * 64] = (int32_t)((uint32_t)r.get_signed(bps) << ws);
+                ((int32_t *)(row + (uint64_t)(i >> 2) * 64))[i & 3] =
+                    (int32_t)((uint32_t)r.get_signed(bps) << ws);
         } else {
             m.kind = 2;
             m.order = (uint8_t)sh.order;
@@ -898,9 +917,10 @@ __global__ __launch_bounds__(256) void k_dec_unrow(const DecFrame *__restrict__ 
     if (t0 >= maxit)
         return;
     const int32_t *src = rows + ((uint64_t)slot * nrows + t0) * 64;
-    for (uint32_t k = tid; k < 64 * 64; k += 256) {
-        const uint32_t x = k >> 6, l = k & 63;
-        tile[x * 65 + l] = t0 + x < nrows ? src[(uint64_t)x * 64 + l] : 0;
+    for (uint32_t o = tid; o < 64 * 64; o += 256) {
+        // block element o = ((x / 4) * 64 + l) * 4 + x % 4
+        const uint32_t x = ((o >> 8) << 2) | (o & 3), l = (o >> 2) & 63;
+        tile[x * 65 + l] = src[o];
     }
     __syncthreads();
     for (uint32_t k = tid; k < 64 * 64; k += 256) {
@@ -1331,7 +1351,7 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     for (uint32_t t = 0; t < n; ++t)
         if (d->cnt[t].n_frames)
             max_bs = std::max(max_bs, d->tr[t].max_bs);
-    const uint32_t nrows = 2 * max_bs + 1;
+    const uint32_t nrows = (2 * max_bs + 1 + 63) & ~63u; // whole 64-row tiles
     const uint64_t nslots = (jb + 63) / 64;
     DHIP(d->rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
     DHIP(d->meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
