@@ -607,7 +607,12 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
     }
     const uint64_t endb = r.abspos() >> 3;
     rec.bytes = (uint32_t)(endb - pos);
+#if ATG_DEC_EXP == 3 // timing experiment only: no CRC-16
+    rec.status = FD_OK;
+    (void)T;
+#else
     rec.status = crc16_range(w, pos, endb, T) ? FD_FRAME_CRC : FD_OK;
+#endif
 }
 
 __device__ __forceinline__ void load_crc_lds(uint16_t (*T)[256])
