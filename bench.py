@@ -1,24 +1,36 @@
 #!/usr/bin/env python3
 """bench.py — FLAC-8 batch encode throughput on MI355X (BASELINE.json config 2).
 
-One step = one pass of the hot path over one batch: FLAC-8 encode of
-`--tracks` synthetic 44.1 kHz / 16-bit stereo tracks x `--frames` FLAC
-frames of 4096 PCM frames, PCM resident in HBM, complete .flac images
-(STREAMINFO with MD5, VORBIS_COMMENT, PADDING, frames) left in HBM.
+One step = one pass of the hot path over one batch: FLAC-8 encode of the
+rank's synthetic 44.1 kHz / 16-bit stereo tracks x `--frames` FLAC frames
+of 4096 PCM frames, PCM resident in HBM, complete .flac images (STREAMINFO
+with MD5, VORBIS_COMMENT, PADDING, frames) left in HBM.
 
-Multi-GPU: one process per GPU (torchrun); each rank encodes its own batch
-of `--tracks` tracks (tracks are independent, no collective on the data
-path) -> "scaling": "weak"; value = frames of all ranks / max-over-ranks time.
+Multi-GPU: one process per GPU.  Under torchrun the ranks come from the
+environment; `python bench.py --gpus N` without it spawns the N rank
+processes itself before anything touches a GPU.  Tracks are independent, so
+ranks share nothing on the data path:
+  --scaling weak   (default) every rank encodes `--tracks` tracks of its own;
+  --scaling strong the `--tracks` tracks are split over the ranks.
+value = frames of all ranks / max-over-ranks time of the K timed steps.
 
-Prints ONE JSON line on rank 0.  The roofline block is for the dominant
-kernel (timed with HIP events on the stream it runs on, inside libatgpu);
-cpu_baseline times the CPU oracle (oracle/flac_port.c) on a bounded sample
-of the same batch on this host's cores.
+Prints ONE JSON line on rank 0.  Parity: every GPU image of the batch is
+byte-compared with the CPU port (oracle/flac_port.c, pinned to the reference)
+and a sample with the reference encoder itself (oracle/_ref/flacenc, built
+from the reference's own C sources) when that build is present; the decode
+leg compares every decoded sample with the source PCM.  `roofline` is the
+HBM roofline of the longest kernel on the critical (main-stream) path,
+`roofline_valu` its integer-VALU roofline, `step_hbm` the whole step's
+algorithmic HBM fraction.  cpu_baseline = the reference encoder on this
+host's cores (one process per track, like track2track -j N).
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
+import tempfile
 import threading
 import time
 
@@ -32,9 +44,19 @@ METRIC = "FLAC-8 encode frames/s (4096-sample 44.1k stereo) at 1/2/4/8 GPUs; bit
 BLOCK = 4096
 PCM_BYTES_PER_FRAME = BLOCK * 2 * 2
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+# integer VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction
+# per 2 cycles per SIMD (MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz
+N_SIMD = 1024
+CLOCK_HZ = 2.4e9
+VALU_PEAK_WAVE_INSTS = N_SIMD * CLOCK_HZ / 2.0
 FLAC8 = dict(block_size=4096, max_lpc_order=12, min_residual_partition_order=0,
              max_residual_partition_order=6, mid_side=True,
              exhaustive_model_search=True)
+HEADER_BYTES = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + 4096
+# kernels on the encoder's main stream, in launch order (MD5 runs on its own
+# stream beside them, engine.hip)
+MAIN_STREAM = ("lpc_analyze", "subframe_search", "frame_decide", "track_scan",
+               "frame_pack", "stream_header")
 
 
 def parse_args(argv=None):
@@ -42,21 +64,32 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--tracks", type=int, default=1024)
+    ap.add_argument("--tracks", type=int, default=1024,
+                    help="tracks per GPU (weak) or in total (strong)")
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
-    ap.add_argument("--cpu-sample-tracks", type=int, default=1024)
+    ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--cpu-threads", type=int, default=0)
+    ap.add_argument("--cpu-ref-tracks", type=int, default=96,
+                    help="tracks the reference encoder baseline encodes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--no-decode", action="store_true",
-                    help="skip the decode leg (GPU FLAC decode of the encoded batch)")
+                    help="skip the decode / convert / ReplayGain legs")
+    ap.add_argument("--selftest", action="store_true",
+                    help="harness self-test on CPU (gloo, oracle as the step); "
+                         "prints a line that is not a measurement")
     return ap.parse_args(argv)
 
 
-def shard(n_total_ranks, rank, tracks_per_rank):
-    """global track ids owned by `rank` (weak scaling: a full batch per rank;
-    tracks are independent, so ranks share nothing on the data path)"""
-    return list(range(rank * tracks_per_rank, (rank + 1) * tracks_per_rank))
+def shard(n_total_ranks, rank, tracks, scaling="weak"):
+    """global track ids owned by `rank`.  weak: a full batch of `tracks` per
+    rank; strong: `tracks` split into contiguous near-equal slices.  Tracks
+    are independent, so ranks share nothing on the data path."""
+    if scaling == "weak":
+        return list(range(rank * tracks, (rank + 1) * tracks))
+    lo = rank * tracks // n_total_ranks
+    hi = (rank + 1) * tracks // n_total_ranks
+    return list(range(lo, hi))
 
 
 def reduce_max(torch, dist, value, device):
@@ -64,6 +97,38 @@ def reduce_max(torch, dist, value, device):
     t = torch.tensor([value], dtype=torch.float64, device=device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
+
+
+def reduce_sum(torch, dist, value, device):
+    t = torch.tensor([value], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def launch(args, argv):
+    """spawn one rank process per GPU (this process never touches a GPU);
+    returns the worst exit code"""
+    port = _free_port()
+    procs = []
+    for r in range(args.gpus):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(args.gpus),
+                   LOCAL_WORLD_SIZE=str(args.gpus), MASTER_ADDR="127.0.0.1",
+                   MASTER_PORT=str(port))
+        env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + argv,
+                                      env=env))
+    rc = 0
+    for p in procs:
+        rc = max(rc, abs(p.wait()))
+    return rc
 
 
 def synth_batch(torch, track_ids, n_samples, device):
@@ -80,7 +145,7 @@ def synth_batch(torch, track_ids, n_samples, device):
     a2 = torch.tensor([r.uniform(0.0, 0.3) for r in rs], dtype=torch.float64, device=device)
     kind = torch.tensor([(t * 2654435761) % 100 for t in track_ids], device=device)
     gen = torch.Generator(device=device)
-    gen.manual_seed(0x5EED + track_ids[0])
+    gen.manual_seed(0x5EED + (track_ids[0] if track_ids else 0))
     out = torch.empty((T, n_samples, 2), dtype=torch.int16, device=device)
     chunk = 64
     n = torch.arange(n_samples, dtype=torch.float64, device=device)
@@ -103,66 +168,103 @@ def synth_batch(torch, track_ids, n_samples, device):
     return out.reshape(-1)
 
 
-def cpu_baseline(pcm_host, n_tracks, samples_per_track, threads):
-    """oracle FLAC-8 encode of `n_tracks` tracks on `threads` host threads
-    (one track per thread at a time, like track2track -j N)"""
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _parallel(n_items, threads, fn):
+    """run fn(i) for i < n_items on `threads` host threads (the work is
+    ctypes / subprocess calls, which release the GIL); -> seconds"""
+    work = list(range(n_items - 1, -1, -1))
+    lock = threading.Lock()
+    err = []
+
+    def run():
+        while True:
+            with lock:
+                if not work or err:
+                    return
+                i = work.pop()
+            try:
+                fn(i)
+            except Exception as e:  # surfaced after join
+                with lock:
+                    err.append(e)
+
+    th = [threading.Thread(target=run) for _ in range(max(1, threads))]
+    t0 = time.perf_counter()
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    if err:
+        raise err[0]
+    return time.perf_counter() - t0
+
+
+def port_encode_all(pcm_host, n_tracks, samples_per_track, threads):
+    """the CPU port (oracle/flac_port.c) encodes every track of the batch on
+    `threads` host threads, one track per thread at a time like
+    track2track -j N; -> (images, seconds)"""
     import oracle_port
     oracle_port.load()
-    work = list(range(n_tracks))
-    lock = threading.Lock()
+    images = [None] * n_tracks
 
-    def run():
-        while True:
-            with lock:
-                if not work:
-                    return
-                t = work.pop()
-            p = pcm_host[t * samples_per_track * 2:(t + 1) * samples_per_track * 2]
-            oracle_port.encode(p.astype(np.int32), 2, 16, 44100, **FLAC8)
+    def one(t):
+        p = pcm_host[t * samples_per_track * 2:(t + 1) * samples_per_track * 2]
+        images[t], _ = oracle_port.encode(p.astype(np.int32), 2, 16, 44100, **FLAC8)
 
-    th = [threading.Thread(target=run) for _ in range(threads)]
-    t0 = time.perf_counter()
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
-    dt = time.perf_counter() - t0
-    frames = n_tracks * (samples_per_track // BLOCK)
-    return frames / dt, dt
+    return images, _parallel(n_tracks, threads, one)
 
 
-def cpu_decode_baseline(images, threads):
-    """oracle FLAC decode (oracle/flac_port.c, pinned to the reference
-    decoder) of `images` on `threads` host threads, one image per thread"""
+def ref_encode_sample(pcm_host, n_tracks, samples_per_track, procs):
+    """the reference encoder itself (oracle/_ref/flacenc = the reference's
+    src/encoders/flac.c built standalone from its own sources), one process
+    per track, `procs` at a time; -> (images, seconds) or None when the
+    build is absent"""
     import oracle_port
-    work = list(range(len(images)))
-    lock = threading.Lock()
-    nfr = [0]
+    exe = oracle_port.REF_FLACENC
+    if not os.path.exists(exe):
+        return None
+    args = [exe, "-c", "2", "-r", "44100", "-b", "16", "-B", "4096", "-l", "12", "-P", "0",
+            "-R", "6", "-m", "-e"]
+    images = [None] * n_tracks
+    raws = [pcm_host[t * samples_per_track * 2:(t + 1) * samples_per_track * 2]
+            .astype("<i2").tobytes() for t in range(n_tracks)]
+    with tempfile.TemporaryDirectory() as d:
+        def one(t):
+            fn = os.path.join(d, "%d.flac" % t)
+            subprocess.run(args + [fn], input=raws[t], stdout=subprocess.DEVNULL, check=True)
+            with open(fn, "rb") as f:
+                images[t] = f.read()
 
-    def run():
-        while True:
-            with lock:
-                if not work:
-                    return
-                t = work.pop()
-            r = oracle_port.decode_frames(images[t])
-            with lock:
-                nfr[0] += len(r["offsets"])
-
-    th = [threading.Thread(target=run) for _ in range(threads)]
-    t0 = time.perf_counter()
-    for x in th:
-        x.start()
-    for x in th:
-        x.join()
-    dt = time.perf_counter() - t0
-    return nfr[0] / dt, dt
+        dt = _parallel(n_tracks, procs, one)
+    return images, dt
 
 
-def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, barrier):
+def load_profile_json(name):
+    fn = os.path.join(ROOT, "profiles", name)
+    if os.path.exists(fn):
+        try:
+            with open(fn) as f:
+                return json.load(f)
+        except (OSError, ValueError):
+            return None
+    return None
+
+
+def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n_frames,
+               barrier):
     """GPU decode of the batch the encoder just left in HBM (the trackverify
-    path): every track is decoded, its PCM restored and
-    its STREAMINFO MD5 checked on the GPU.  Returns the JSON object."""
+    path): every track decoded, its STREAMINFO MD5
+    checked on the GPU, and every decoded sample compared with the source
+    PCM (lossless round trip).  Returns the JSON object."""
     from audiotools import _atgpu
     dec = _atgpu.Decoder(int(os.environ.get("LOCAL_RANK", "0")))
     tracks = []
@@ -172,7 +274,7 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
         si.sample_rate, si.channels, si.bits_per_sample = 44100, 2, 16
         si.max_block_size = BLOCK
         si.md5[:] = bytes(r.md5)
-        tracks.append(_atgpu.dec_track(r.out_offset + header, r.bytes - header, si))
+        tracks.append(_atgpu.dec_track(r.out_offset + HEADER_BYTES, r.bytes - HEADER_BYTES, si))
     nbytes = max(r.out_offset + r.bytes for r in res)
 
     def step():
@@ -193,8 +295,15 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
         elapsed = reduce_max(torch, dist, elapsed, device)
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     ok = all(r.status == 0 and r.pcm_frames == args.frames * BLOCK for r in dres)
-    comp = sum(int(r.bytes) - header for r in res)
-    pcm32 = args.tracks * args.frames * BLOCK * 2 * 4
+    # every decoded sample vs the source PCM (exact), outside the timed region
+    same = False
+    if ok and nsamp == pcm.numel():
+        got = np.empty(int(nsamp), dtype=np.int32)
+        eng.copy_to_host(got, d_pcm)
+        same = bool(np.array_equal(got, pcm_host))
+        del got
+    comp = sum(int(r.bytes) - HEADER_BYTES for r in res)
+    pcm32 = len(res) * args.frames * BLOCK * 2 * 4
     # algorithmic bytes per launch: the parsers read the compressed frames
     # once; the subframe decoder also writes its int32 row scratch, which
     # the row transposer reads and writes as planar samples; the
@@ -205,14 +314,9 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
     kernels = {k: v for k, v in kt.items() if k in alg}
     dom = max(kernels, key=kernels.get)
     achieved = alg[dom] / (kernels[dom] / 1e3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(dom)
-        except Exception:
-            traffic = None
+    traffic = (load_profile_json("pmc_traffic.json") or {}).get(dom)
     dec.close()
+    step_alg = comp + pcm32
     return {
         "metric": "FLAC-8 decode frames/s (GPU decode of the encoded batch, MD5-verified)",
         "value": round(n_frames * world * args.steps / elapsed, 1), "unit": "frames/s",
@@ -222,7 +326,11 @@ def decode_leg(args, torch, dist, world, device, out, res, header, n_frames, bar
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4)},
+        "step_hbm": {"alg_bytes_per_step": step_alg,
+                     "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)},
         "verified_md5_round_trip": ok,
+        "verified_pcm_vs_source": same,
+        "verified_tracks": len(dres) if (ok and same) else 0,
     }
 
 
@@ -256,12 +364,13 @@ def convert_leg(args, torch, device, pcm):
     ok = bool((((y ^ (x >> 8)) & ~1) == 0).all().item())
     alg = x.numel() * 8 + dither.numel()
     del x, y, dither
+    traffic = (load_profile_json("pmc_traffic.json") or {}).get("pcm_bps")
     return {"metric": "BPSConverter 16->8 dither, samples/s", "value": round(frames * 2 / dt, 1),
             "unit": "samples/s", "ms_per_step": round(dt * 1e3, 4),
             "roofline": {"bound": "hbm", "kernel": "k_pcm_bps",
                          "achieved": round(alg / dt / 1e9, 2), "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": round(alg / dt / 1e9 / HBM_PEAK_GBS, 4),
-                         "traffic": None, "alg_bytes_per_launch": alg,
+                         "traffic": traffic, "alg_bytes_per_launch": alg,
                          "launch_ms": round(dt * 1e3, 4)},
             "verified_dither_invariant": ok}
 
@@ -275,18 +384,18 @@ def album_reduce(dist, world, hist, peak):
         dist.all_reduce(peak, op=dist.ReduceOp.MAX)
 
 
-def replaygain_leg(args, torch, dist, world, rank, device, pcm, barrier):
+def replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks, barrier):
     """ReplayGain title analysis of every track of the batch (replaygain.hip,
     SURVEY 8(a) G1-G5) plus one album over ALL ranks' tracks: each rank sums
     its tracks' window histograms on the GPU, then the 12000-bin uint32
     histogram is all-reduced (SUM, exact) and the album peak (MAX) over RCCL
     -- the one real exchange step of the path.  Returns the
-    JSON object (rank 0) and per-track results for the CPU check."""
+    JSON object and per-track results for the CPU check."""
     from audiotools import _atgpu
     x = pcm.to(torch.int32)
     n_samples = args.frames * BLOCK
     tracks = [_atgpu.RgTrack(t * n_samples, n_samples, 2, 16, 44100, 0)
-              for t in range(args.tracks)]
+              for t in range(n_tracks)]
     hist = torch.zeros(12000, dtype=torch.int32, device=device)
 
     def step():
@@ -306,22 +415,94 @@ def replaygain_leg(args, torch, dist, world, rank, device, pcm, barrier):
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
-    host = pcm[:4 * n_samples * 2].cpu().numpy().astype(np.int32)
     del x
-    frames = args.tracks * args.frames * world * args.steps
+    frames = n_tracks * args.frames * args.steps
+    if world > 1:
+        frames = reduce_sum(torch, dist, frames, device)
     out = {"metric": "ReplayGain title analysis, FLAC-frame-equivalents/s (4096 PCM frames)",
            "value": round(frames / elapsed, 1), "unit": "frames/s",
            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
-           "album": {"tracks": args.tracks * world, "gain_db": album_gain,
+           "album": {"tracks": int(reduce_sum(torch, dist, n_tracks, device))
+                     if world > 1 else n_tracks, "gain_db": album_gain,
                      "peak": album_peak,
                      "collective": "all_reduce SUM uint32[12000] + MAX f64 (RCCL)"
                                    if world > 1 else "none (1 rank)"},
-           "bound": "serial fp64 IIR per channel (lane per track-channel, 32 waves)"}
-    return out, res, host
+           "bound": "serial fp64 IIR chain per track-channel (lane per track-channel)"}
+    return out, res
+
+
+def verify_replaygain(rg, rg_res, pcm_host, n_tracks, n_samples, threads):
+    """every track's title gain and peak vs the CPU oracle (exact)"""
+    import oracle_port
+    oracle_port.load()
+    bad = []
+
+    def one(t):
+        A, pk = oracle_port.rg_title(pcm_host[t * n_samples * 2:(t + 1) * n_samples * 2]
+                                     .astype(np.int32), 2, 16, 44100)
+        if not (oracle_port.rg_gain(A) == rg_res[t].title_gain and pk == rg_res[t].title_peak):
+            bad.append(t)
+
+    dt = _parallel(n_tracks, threads, one)
+    rg["verified_vs_oracle"] = not bad
+    rg["verified_tracks"] = n_tracks - len(bad)
+    rg["cpu_baseline"] = {"value": round(n_tracks * (n_samples // BLOCK) / dt, 2),
+                          "unit": "frames/s", "cores": threads, "kind": "port",
+                          "sample": "oracle title analysis of all %d tracks, %d threads, %.1f s"
+                                    % (n_tracks, threads, dt)}
+
+
+def selftest(args):
+    """the multi-rank harness on CPU (gloo): sharding, barrier + max-over-
+    ranks clock, whole-job frame count, rank-0 JSON line.  The "step" is the
+    CPU oracle encoding this rank's small tracks -- a harness check, not a
+    measurement (metric says so)."""
+    import torch
+    import torch.distributed as dist
+    import oracle_port
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    if world > 1:
+        dist.init_process_group("gloo")
+    dev = torch.device("cpu")
+    ids = shard(world, rank, args.tracks, args.scaling)
+    rng = np.random.RandomState(7)
+    pcms = {t: rng.randint(-3000, 3000, 2 * BLOCK * args.frames).astype(np.int32) for t in ids}
+    for _ in range(args.warmup):
+        for t in ids:
+            oracle_port.encode(pcms[t], 2, 16, 44100, **FLAC8)
+    if world > 1:
+        dist.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        for t in ids:
+            oracle_port.encode(pcms[t], 2, 16, 44100, **FLAC8)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    frames = len(ids) * args.frames * args.steps
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, dev)
+        frames = reduce_sum(torch, dist, frames, dev)
+    if rank == 0:
+        print(json.dumps({"metric": "bench harness self-test (CPU oracle step; not a measurement)",
+                          "value": round(frames / elapsed, 2), "unit": "frames/s",
+                          "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "scaling": args.scaling, "selftest": True,
+                          "tracks_total": int(frames // (args.frames * args.steps)),
+                          "parallelism": "dp%d" % world}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main(argv=None):
+    argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # spawn the ranks before anything initialises a GPU (never re-exec)
+        return launch(args, argv)
+    if args.selftest:
+        return selftest(args)
     import torch
     import torch.distributed as dist
 
@@ -339,9 +520,10 @@ def main(argv=None):
     opts = _atgpu.make_options(**FLAC8)
 
     n_samples = args.frames * BLOCK
-    ids = shard(world, rank, args.tracks)
+    ids = shard(world, rank, args.tracks, args.scaling)
+    n_tracks = len(ids)
     pcm = synth_batch(torch, ids, n_samples, device)
-    tracks = [(i * n_samples, n_samples) for i in range(args.tracks)]
+    tracks = [(i * n_samples, n_samples) for i in range(n_tracks)]
     n_frames, out_cap = eng.bounds(opts, tracks, 2, 16)
     table = _atgpu.TrackTable(tracks)
     out = torch.empty(out_cap, dtype=torch.uint8, device=device)
@@ -372,103 +554,120 @@ def main(argv=None):
         elapsed = reduce_max(torch, dist, elapsed, device)
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     out_bytes = sum(int(r.bytes) for r in res)
-    header = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + 4096
-    frame_bytes = out_bytes - header * len(res)
+    frame_bytes = out_bytes - HEADER_BYTES * len(res)
+    total_frames = n_frames * args.steps
+    if world > 1:
+        total_frames = reduce_sum(torch, dist, total_frames, device)
 
+    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    pcm_host = pcm.cpu().numpy()
+    host_out = out.cpu().numpy()
+    images = [host_out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res]
+    del host_out
+
+    # ---- parity: every image of the batch vs the CPU port (outside the
+    # timed region); the port's timing is the N-thread port baseline
     verified = None
+    port = None
     if not args.no_verify:
-        # parity spot check outside the timed region: a few tracks vs oracle
-        import oracle_port
-        host_out = out.cpu().numpy()
-        host_pcm = pcm[:4 * n_samples * 2].cpu().numpy()
-        verified = True
-        for t in range(min(4, args.tracks)):
-            r = res[t]
-            img = host_out[r.out_offset:r.out_offset + r.bytes].tobytes()
-            want, _ = oracle_port.encode(
-                host_pcm[t * n_samples * 2:(t + 1) * n_samples * 2].astype(np.int32),
-                2, 16, 44100, **FLAC8)
-            verified = verified and (img == want)
+        want, port_dt = port_encode_all(pcm_host, n_tracks, n_samples, threads)
+        bad = [t for t in range(n_tracks) if want[t] != images[t]]
+        verified = {"vs": "CPU port oracle/flac_port.c (pinned to the reference encoder)",
+                    "tracks": n_tracks, "mismatches": len(bad), "ok": not bad}
+        port = {"value": round(n_tracks * args.frames / port_dt, 2), "unit": "frames/s",
+                "cores": threads, "kind": "port",
+                "sample": "all %d tracks x %d frames, %d threads, %.1f s"
+                          % (n_tracks, args.frames, threads, port_dt)}
+        del want
 
-    decode = None
+    decode = convert = rg = rg_res = None
     if not args.no_decode:
-        decode = decode_leg(args, torch, dist, world, device, out, res, header, n_frames,
-                            barrier)
-
-    convert = None
-    if not args.no_decode and rank == 0:
-        convert = convert_leg(args, torch, device, pcm)
-    rg = rg_res = rg_host = None
-    if not args.no_decode:
-        rg, rg_res, rg_host = replaygain_leg(args, torch, dist, world, rank, device, pcm,
-                                             barrier)
+        decode = decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host,
+                            n_frames, barrier)
+        if rank == 0:
+            convert = convert_leg(args, torch, device, pcm)
+        rg, rg_res = replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks,
+                                    barrier)
 
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
-        return
+        return 0
 
-    total_frames = n_frames * world * args.steps
     value = total_frames / elapsed
-    # dominant kernel and its roofline.  Algorithmic bytes per launch
-    # (DESIGN.md section 4): every kernel that reads the batch reads its
-    # PCM once (16,384 B per 4096-sample stereo frame); the packer also
-    # writes the compressed frames.
-    pcm_bytes = args.tracks * n_samples * 2 * 2
+    # ---- rooflines.  Algorithmic bytes per launch:
+    # every kernel that reads the batch reads its PCM once (16,384 B per
+    # 4096-sample stereo frame); the packer also writes the compressed frames
+    pcm_bytes = n_tracks * n_samples * 2 * 2
     alg = {"lpc_analyze": pcm_bytes, "subframe_search": pcm_bytes,
            "frame_pack": pcm_bytes + frame_bytes, "track_md5": pcm_bytes,
            "frame_decide": 0, "track_scan": 0, "stream_header": out_bytes - frame_bytes}
-    kernels = {k: v for k, v in kt.items() if k != "total"}
-    dom = max(kernels, key=kernels.get)
-    dom_ms = kernels[dom]
+    main_k = {k: v for k, v in kt.items() if k in MAIN_STREAM}
+    dom = max(main_k, key=main_k.get)
+    dom_ms = main_k[dom]
     alg_bytes = alg.get(dom, pcm_bytes)
     achieved = alg_bytes / (dom_ms / 1e3) / 1e9
-    traffic = None
-    tf = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if os.path.exists(tf):
-        try:
-            traffic = json.load(open(tf)).get(dom)
-        except Exception:
-            traffic = None
+    traffic = (load_profile_json("pmc_traffic.json") or {}).get(dom)
+    # integer-VALU roofline of the subframe search: algorithmic
+    # MACs = sum over the 4 candidate subframes of the 12 LPC orders
+    # (1+..+12 = 78 taps x 4096 samples) + FIXED orders 1..4 (10 taps) --
+    # 2 MACs per v_dot2 lane-op, 64 lanes per wave instruction
+    sub_ms = kt.get("subframe_search", 0.0)
+    macs_per_frame = 4 * (78 + 10) * BLOCK
+    alg_wave_insts = n_frames * macs_per_frame / 2.0 / 64.0
+    pmc = (load_profile_json("pmc_valu.json") or {}).get("subframe_search") or {}
+    valu = {"kernel": "subframe_search", "bound": "valu", "unit": "wave-instructions/s",
+            "peak": VALU_PEAK_WAVE_INSTS,
+            "alg_mac_wave_insts_per_launch": alg_wave_insts,
+            "alg_mac_frac": round(alg_wave_insts / (sub_ms / 1e3) / VALU_PEAK_WAVE_INSTS, 4)
+            if sub_ms else None,
+            "launch_ms": round(sub_ms, 4)}
+    if pmc.get("SQ_INSTS_VALU") and sub_ms:
+        # PMC instruction count per launch (profiles/pmc_valu.json, same
+        # batch shape) over the live launch time
+        per_launch = pmc["SQ_INSTS_VALU"] * (n_frames / pmc.get("frames", n_frames))
+        valu["issued_wave_insts_per_launch"] = per_launch
+        valu["issue_frac"] = round(per_launch / (sub_ms / 1e3) / VALU_PEAK_WAVE_INSTS, 4)
+        valu["pmc_source"] = pmc.get("source")
+    step_alg = pcm_bytes + out_bytes
+    step_hbm = {"alg_bytes_per_step": step_alg,
+                "achieved": round(step_alg / (elapsed / args.steps) / 1e9, 2),
+                "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)}
 
+    # ---- CPU baselines on this host's cores
     cpu = None
     if not args.no_cpu_baseline:
-        threads = args.cpu_threads or min(16, os.cpu_count() or 1)
-        nt = min(args.cpu_sample_tracks, args.tracks)
-        sample_frames = args.frames
-        sps = sample_frames * BLOCK
-        host = pcm.reshape(args.tracks, n_samples * 2)[:nt, :sps * 2].cpu().numpy().reshape(-1)
-        fps, dt = cpu_baseline(host, nt, sps, threads)
-        cpu = {"value": round(fps, 2), "unit": "frames/s", "cores": threads, "kind": "port",
-               "sample": "%d tracks x %d FLAC-8 frames of the same synthetic batch, "
-                         "%d threads (one track per thread), %.1f s" % (nt, sample_frames,
-                                                                        threads, dt)}
+        import oracle_port
+        nref = min(args.cpu_ref_tracks, n_tracks)
+        ref = ref_encode_sample(pcm_host, nref, n_samples, threads)
+        t1 = min(2, n_tracks)
+        _, dt1 = port_encode_all(pcm_host, t1, n_samples, 1)
+        port1 = {"value": round(t1 * args.frames / dt1, 2), "unit": "frames/s", "cores": 1,
+                 "kind": "port", "sample": "%d tracks x %d frames, 1 thread, %.1f s"
+                                           % (t1, args.frames, dt1)}
+        if ref is not None:
+            ref_images, rdt = ref
+            ref_ok = all(ref_images[t] == images[t] for t in range(nref))
+            cpu = {"value": round(nref * args.frames / rdt, 2), "unit": "frames/s",
+                   "cores": threads, "kind": "reference",
+                   "sample": "reference encoder (oracle/_ref/flacenc, built from the "
+                             "reference's src/encoders/flac.c) on %d of the batch's tracks x "
+                             "%d frames, one process per track, %d at a time, %.1f s"
+                             % (nref, args.frames, threads, rdt),
+                   "gpu_images_identical": ref_ok}
+        else:
+            cpu = dict(port) if port else dict(port1)
+            cpu["note"] = "oracle/_ref absent: port timing"
+        cpu["cpu_model"] = cpu_model()
+        cpu["host_cpus"] = os.cpu_count()
+        cpu["port_1_thread"] = port1
+        if port:
+            cpu["port_n_threads"] = port
+        cal = load_profile_json("r02_cpu_calibration.json")
+        if cal:
+            cpu["calibration"] = cal.get("summary")
         if rg is not None:
-            # oracle on the first 4 tracks: exact title gains/peaks, timed
-            import oracle_port
-            t0 = time.perf_counter()
-            ok = True
-            for t in range(min(4, args.tracks)):
-                A, pk = oracle_port.rg_title(
-                    rg_host[t * n_samples * 2:(t + 1) * n_samples * 2], 2, 16, 44100)
-                ok = ok and oracle_port.rg_gain(A) == rg_res[t].title_gain and \
-                    pk == rg_res[t].title_peak
-            dt = time.perf_counter() - t0
-            rg["verified_vs_oracle"] = ok
-            rg["cpu_baseline"] = {"value": round(min(4, args.tracks) * args.frames / dt, 2),
-                                  "unit": "frames/s", "cores": 1, "kind": "port",
-                                  "sample": "oracle title analysis of 4 tracks, 1 thread, "
-                                            "%.1f s" % dt}
-        if decode is not None:
-            host_out = out.cpu().numpy()
-            imgs = [host_out[r.out_offset:r.out_offset + r.bytes].tobytes()
-                    for r in res[:nt]]
-            dfps, ddt = cpu_decode_baseline(imgs, threads)
-            decode["cpu_baseline"] = {
-                "value": round(dfps, 2), "unit": "frames/s", "cores": threads,
-                "kind": "port",
-                "sample": "oracle decode of %d of the encoded tracks, %d threads, %.1f s"
-                          % (nt, threads, ddt)}
+            verify_replaygain(rg, rg_res, pcm_host, n_tracks, n_samples, threads)
 
     line = {
         "metric": METRIC,
@@ -479,20 +678,24 @@ def main(argv=None):
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": args.scaling,
         "vs_baseline": None,
         "dtype": "int32 residuals / f64 LPC analysis (s16 PCM in)",
         "data": "synthetic (seeded sine+noise, 5% white noise, 2% silent tracks)",
         "config": {"workload": "FLAC-8 batch encode, %d tracks x %d frames x 4096 samples "
                                "per GPU, 44.1 kHz 16-bit stereo, PCM and .flac images in HBM"
-                               % (args.tracks, args.frames),
-                   "tracks_per_gpu": args.tracks, "frames_per_track": args.frames,
+                               % (n_tracks, args.frames),
+                   "tracks_per_gpu": n_tracks, "frames_per_track": args.frames,
                    "block_size": 4096, "preset": "FLAC-8 (-l 12 -m -e -R 6)",
-                   "parallelism": "dp%d (tracks sharded per GPU)" % world},
+                   "parallelism": "dp%d (tracks sharded per GPU, %s scaling)"
+                                  % (world, args.scaling)},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes, "launch_ms": round(dom_ms, 4)},
+                     "alg_bytes_per_launch": alg_bytes, "launch_ms": round(dom_ms, 4),
+                     "selection": "longest kernel on the main (critical-path) stream"},
+        "roofline_valu": valu,
+        "step_hbm": step_hbm,
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
         "compressed_bytes_per_frame": round(frame_bytes / n_frames, 1),
         "verified_vs_oracle": verified,
@@ -504,7 +707,8 @@ def main(argv=None):
     print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

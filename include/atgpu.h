@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ATG_ABI_VERSION 1
+#define ATG_ABI_VERSION 2
 
 typedef enum {
     ATG_OK = 0,
@@ -203,19 +203,26 @@ typedef struct {
     uint8_t md5[16];
 } atg_flac_dec_track;
 
-/* Per-track decode result.  The frames before `status` stopped the stream
-   decoded: pcm_frames PCM frames (interleaved int32, FrameList layout) at
-   PCM-frame index pcm_offset of the batch output, n_frames FLAC frames
-   starting at first_frame of the frame arrays.  md5 = MD5 of their
-   little-endian PCM bytes. */
+/* Per-track decode result.
+   read() view (src/decoders/flac.c:174-285): the stream hands out n_frames
+   FLAC frames = pcm_frames PCM frames (interleaved int32, FrameList layout,
+   at PCM-frame index pcm_offset of the batch output) and then raises
+   `status` (0 = end of stream with the MD5 verified); md5 = MD5 of those
+   frames' little-endian PCM bytes.
+   offsets() view (flac.c:365-443, which never checks CRC-16): walk_frames
+   frames are walked (frame arrays first_frame .. first_frame+walk_frames-1,
+   decoded PCM continuing after pcm_frames) before walk_status stops it.
+   The two differ only when a frame fails its CRC-16. */
 typedef struct {
     uint64_t pcm_offset;
     uint64_t pcm_frames;
     uint32_t first_frame;
     uint32_t n_frames;
     int32_t status;
-    uint32_t reserved;
+    uint32_t walk_frames;
     uint8_t md5[16];
+    int32_t walk_status;
+    uint32_t reserved;
 } atg_flac_dec_result;
 
 typedef struct atg_decoder atg_decoder;
@@ -294,6 +301,11 @@ typedef struct {
     uint64_t pcm_frames;
     uint32_t channels, bits_per_sample, sample_rate;
     uint32_t album;      /* album index (tracks grouped by album) */
+    /* host array: the frame counts pcmreader.read(4096) returned, one
+       ReplayGain_analyze_samples call each (replaygain.c:210-305); they
+       decide the fp64 summation order.  NULL = 4096-frame reads. */
+    const uint32_t *chunk_frames;
+    uint64_t n_chunks;
 } atg_rg_track;
 
 typedef struct {

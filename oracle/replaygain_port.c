@@ -11,8 +11,10 @@
  * section 4) and replaygain.c is a Python-2 extension module, so it is not
  * built here.  The filters are a continuous IIR from zero state per track;
  * the summation of squared outputs follows the reference's batches exactly
- * (4096-frame reads, the first 10 samples of each read as their own batch,
- * 50 ms window boundaries; singles for batch % 16, then 16-term groups).
+ * (one ReplayGain_analyze_samples call per pcmreader.read(4096) result --
+ * 4096-frame reads by default, or the chunk sizes the reader actually
+ * returned -- the first 10 samples of each read as their own batch, 50 ms
+ * window boundaries; singles for batch % 16, then 16-term groups).
  */
 #include <math.h>
 #include <stdint.h>
@@ -58,11 +60,14 @@ static double filter_one(chan_state *s, double x, const double *ky, const double
     return b;
 }
 
-/* title analysis of one track: pcm interleaved int32, channels 1 or 2.
+/* title analysis of one track: pcm interleaved int32, channels 1 or 2,
+   read in chunks of chunk[0..n_chunks) frames (NULL: 4096-frame reads).
    Writes the track's window histogram A[12000] and returns the title peak
-   (max |x| / 2^(bps-1)).  Returns -1 for unsupported rate / bps / channels. */
-double rgport_title(const int32_t *pcm, uint64_t frames, uint32_t channels, uint32_t bps,
-                    uint32_t rate, uint32_t *A)
+   (max |x| / 2^(bps-1)).  Returns -1 for unsupported rate / bps / channels
+   or chunk sizes that do not add up to frames. */
+double rgport_title_chunks(const int32_t *pcm, uint64_t frames, uint32_t channels,
+                           uint32_t bps, uint32_t rate, const uint32_t *chunk,
+                           uint64_t n_chunks, uint32_t *A)
 {
     const int fi = rgport_freqindex(rate);
     if (fi < 0 || (channels != 1 && channels != 2) || (bps != 8 && bps != 16 && bps != 24))
@@ -76,8 +81,17 @@ double rgport_title(const int32_t *pcm, uint64_t frames, uint32_t channels, uint
     memset(A, 0, sizeof(uint32_t) * RG_BINS);
     double lsum = 0, rsum = 0, peak = 0;
     long totsamp = 0;
-    for (uint64_t c0 = 0; c0 < frames; c0 += 4096) {
-        const long n = (long)(frames - c0 < 4096 ? frames - c0 : 4096);
+    if (chunk) {
+        uint64_t tot = 0;
+        for (uint64_t i = 0; i < n_chunks; i++)
+            tot += chunk[i];
+        if (tot != frames)
+            return -1.0;
+    }
+    uint64_t ci = 0;
+    for (uint64_t c0 = 0; c0 < frames;) {
+        const long n = chunk ? (long)chunk[ci++]
+                             : (long)(frames - c0 < 4096 ? frames - c0 : 4096);
         long pos = 0, batch = n;
         while (batch > 0) {
             long cur = batch > window - totsamp ? window - totsamp : batch;
@@ -132,8 +146,15 @@ double rgport_title(const int32_t *pcm, uint64_t frames, uint32_t channels, uint
                 totsamp = 0;
             }
         }
+        c0 += (uint64_t)n;
     }
     return peak;
+}
+
+double rgport_title(const int32_t *pcm, uint64_t frames, uint32_t channels, uint32_t bps,
+                    uint32_t rate, uint32_t *A)
+{
+    return rgport_title_chunks(pcm, frames, channels, bps, rate, NULL, 0, A);
 }
 
 /* analyzeResult (replaygain.c:754-776); NAN for "not enough samples" */

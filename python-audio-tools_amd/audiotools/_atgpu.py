@@ -95,8 +95,9 @@ class DecTrack(ctypes.Structure):
 class DecResult(ctypes.Structure):
     _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64),
                 ("first_frame", c_u32), ("n_frames", c_u32),
-                ("status", c_i32), ("reserved", c_u32),
-                ("md5", ctypes.c_uint8 * 16)]
+                ("status", c_i32), ("walk_frames", c_u32),
+                ("md5", ctypes.c_uint8 * 16), ("walk_status", c_i32),
+                ("reserved", c_u32)]
 
 
 # decode status codes (include/atgpu.h ATG_FD_*) and the reference's
@@ -119,7 +120,20 @@ FD_MESSAGES = {
 
 class RgTrack(ctypes.Structure):
     _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64), ("channels", c_u32),
-                ("bits_per_sample", c_u32), ("sample_rate", c_u32), ("album", c_u32)]
+                ("bits_per_sample", c_u32), ("sample_rate", c_u32), ("album", c_u32),
+                ("chunk_frames", ctypes.POINTER(c_u32)), ("n_chunks", c_u64)]
+
+    def set_chunks(self, chunks):
+        """attach the read() chunk sizes (kept alive on the object)"""
+        if chunks is None:
+            self._chunks = None
+            self.chunk_frames = None
+            self.n_chunks = 0
+        else:
+            self._chunks = np.ascontiguousarray(chunks, dtype=np.uint32)
+            self.chunk_frames = self._chunks.ctypes.data_as(ctypes.POINTER(c_u32))
+            self.n_chunks = len(self._chunks)
+        return self
 
 
 class RgResult(ctypes.Structure):
@@ -361,6 +375,13 @@ class Engine(object):
         k = self.lib.atg_engine_kernel_times(self.handle, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
+    def copy_to_host(self, dst, d_src):
+        """device bytes at d_src -> the numpy array dst (its full size)"""
+        _check(self.lib, self.lib.atg_copy_to_host(
+            self.handle, dst.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(d_src),
+            dst.nbytes))
+        return dst
+
 
 def read_metadata(data, sp_cap=4096):
     """flacdec_read_metadata over an in-memory image (host C in libatgpu).
@@ -565,6 +586,23 @@ def replaygain_host(pcm, tracks, n_albums=0, return_hist=False):
     if return_hist:
         return res, peaks, gains, hist[:n_albums]
     return res, peaks, gains
+
+
+def replaygain_hist_gain_host(hists):
+    """analyzeResult of host uint32[n][12000] histograms on the GPU
+    -> list of gains (NaN = not enough samples)"""
+    lib = load_library()
+    eng = engine()
+    h = np.ascontiguousarray(np.atleast_2d(hists), dtype=np.uint32)
+    n = h.shape[0]
+    d = ctypes.c_void_p()
+    _check(lib, lib.atg_device_alloc(eng.handle, max(4, h.nbytes), ctypes.byref(d)))
+    try:
+        _check(lib, lib.atg_copy_to_device(eng.handle, d, h.ctypes.data_as(ctypes.c_void_p),
+                                           h.nbytes))
+        return replaygain_hist_gain(d.value, n)
+    finally:
+        lib.atg_device_free(eng.handle, d)
 
 
 def apply_gain(pcm, channels, bits_per_sample, multiplier, chunk_frames, dither,

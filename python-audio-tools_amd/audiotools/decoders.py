@@ -12,7 +12,10 @@ audiotools.decoders.FlacDecoder (src/decoders/flac.c, methods :145-166):
                            the STREAMINFO MD5 check (flac.c:174-285, 479-493);
                            ValueError with the reference's message on a bad
                            frame, IOError "EOF reading frame" on truncation
-  .offsets()               [(byte offset from the first frame, block size)]
+  .seek(pcm_frame_offset)  last SEEKTABLE point at or before the offset
+                           (flac.c:287-356)
+  .offsets()               [(byte offset from the current position, block
+                           size)] of the frames left, CRC-16 unchecked
                            (flac.c:365-443)
   .close()                 further reads raise ValueError
 
@@ -32,12 +35,15 @@ from . import pcm
 
 
 def _read_all(file):
-    if isinstance(file, (str, bytes)) and not isinstance(file, bytes):
+    """-> (bytes, seekable): filenames and file objects can seek, raw bytes
+    cannot (the reference seeks only streams from file objects,
+    flac.c:298-307)"""
+    if isinstance(file, str):
         with open(file, "rb") as f:
-            return f.read()
+            return f.read(), True
     if isinstance(file, (bytes, bytearray, memoryview)):
-        return bytes(file)
-    return file.read()
+        return bytes(file), False
+    return file.read(), True
 
 
 def _metadata_error(rc):
@@ -46,11 +52,17 @@ def _metadata_error(rc):
     return IOError("EOF while reading metadata")
 
 
+def _status_error(status):
+    if status == _atgpu.FD_EOF:
+        return IOError(_atgpu.FD_MESSAGES[_atgpu.FD_EOF])
+    return ValueError(_atgpu.FD_MESSAGES.get(status, "Error"))
+
+
 class FlacDecoder(object):
     """reference src/decoders/flac.c FlacDecoder, decoded on the GPU"""
 
     def __init__(self, file):
-        data = _read_all(file)
+        data, self._seekable = _read_all(file)
         rc, si, points = _atgpu.read_metadata(data)
         if rc:
             raise _metadata_error(rc)
@@ -61,8 +73,17 @@ class FlacDecoder(object):
         self.bits_per_sample = si.bits_per_sample
         self.channels = si.channels
         self.channel_mask = si.channel_mask
-        self._decoded = False
         self._closed = False
+        # the bitstream position: byte offset from the first frame and
+        # remaining_samples there; MD5 validation only from sample 0
+        # (FlacDecoder_seek, flac.c:317-352)
+        self._start_byte = 0
+        self._remaining = si.total_samples
+        self._validate = True
+        self._reset()
+
+    def _reset(self):
+        self._decoded = False
         self._finalized = False
         self._next = 0
 
@@ -70,56 +91,93 @@ class FlacDecoder(object):
         if self._decoded:
             return
         start = self._si.frames_offset
-        track = _atgpu.dec_track(0, len(self._data) - start, self._si)
-        pcm_i32, res, offs, bss = _atgpu.decoder().decode(self._data[start:], [track])
+        body = self._data[start:]
+        track = _atgpu.dec_track(self._start_byte, len(body) - self._start_byte, self._si)
+        track.total_samples = self._remaining
+        if not self._validate:
+            track.md5[:] = bytes(16)  # a blank MD5 always verifies (flac.c:488)
+        pcm_i32, res, offs, bss = _atgpu.decoder().decode(body, [track])
         r = res[0]
-        n = r.pcm_frames * self.channels
-        self._pcm = pcm_i32[r.pcm_offset * self.channels:r.pcm_offset * self.channels + n]
-        self._offsets = offs[r.first_frame:r.first_frame + r.n_frames]
-        self._block_sizes = bss[r.first_frame:r.first_frame + r.n_frames]
-        # PCM frames of each decoded frame: MIN(block size, remaining)
-        lens, remaining = [], self._si.total_samples
+        ch = self.channels
+        self._offsets = offs[r.first_frame:r.first_frame + r.walk_frames]
+        self._block_sizes = bss[r.first_frame:r.first_frame + r.walk_frames]
+        # PCM frames of each walked frame: MIN(block size, remaining)
+        lens, remaining = [], self._remaining
         for bs in self._block_sizes:
             lens.append(min(int(bs), remaining))
             remaining = (remaining - int(bs)) % (1 << 64)
         self._lens = lens
         self._starts = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]) \
             if lens else np.zeros(1, dtype=np.int64)
-        self._status = r.status
+        total = int(self._starts[-1])
+        self._pcm = pcm_i32[r.pcm_offset * ch:(r.pcm_offset + total) * ch]
+        self._read_frames = r.n_frames    # frames read() hands out ...
+        self._status = r.status           # ... before raising this
+        self._walk_status = r.walk_status  # what stops offsets()
         self._decoded = True
 
     def read(self, pcm_frames):
+        """one FLAC frame per call (flac.c:174-285)"""
         if self._closed:
             raise ValueError("cannot read closed stream")
         if self._finalized:
             return pcm.empty_framelist(self.channels, self.bits_per_sample)
         self._decode()
-        if self._next < len(self._lens):
+        if self._next < self._read_frames:
             k = self._next
             self._next += 1
             a = int(self._starts[k]) * self.channels
             b = int(self._starts[k + 1]) * self.channels
             return pcm.FrameList._wrap(self._pcm[a:b].copy(), self.channels,
                                        self.bits_per_sample)
-        # every decoded frame handed out: the stream either reached
-        # remaining_samples == 0 (MD5 verdict) or stopped on an error
+        # every good frame handed out: the stream either reached
+        # remaining_samples == 0 (MD5 verdict) or stops on an error
         if self._status in (_atgpu.FD_OK, _atgpu.FD_MD5):
             self._finalized = True
             if self._status == _atgpu.FD_MD5:
                 raise ValueError(_atgpu.FD_MESSAGES[_atgpu.FD_MD5])
             return pcm.empty_framelist(self.channels, self.bits_per_sample)
-        if self._status == _atgpu.FD_EOF:
-            raise IOError(_atgpu.FD_MESSAGES[_atgpu.FD_EOF])
-        raise ValueError(_atgpu.FD_MESSAGES.get(self._status, "Error"))
+        raise _status_error(self._status)
+
+    def seek(self, pcm_frame_offset):
+        """position at the last SEEKTABLE point at or before
+        pcm_frame_offset (sample 0 without one) and return its sample
+        number (FlacDecoder_seek, flac.c:287-356); reads then continue from
+        that frame, with MD5 validation only when it is sample 0"""
+        if self._closed:
+            raise ValueError("cannot seek closed stream")
+        if not self._seekable:
+            raise TypeError("can only seek streams from file objects")
+        pcm_frame_offset = int(pcm_frame_offset)
+        if pcm_frame_offset < 0:
+            raise ValueError("cannot seek to negative value")
+        sample, byte = 0, 0
+        for (sample_number, byte_offset, _samples) in self._seekpoints:
+            if sample_number <= pcm_frame_offset:
+                sample, byte = sample_number, byte_offset
+            else:
+                break
+        self._start_byte = int(byte)
+        self._remaining = (self._si.total_samples - sample) % (1 << 64)
+        self._validate = sample == 0
+        self._reset()
+        return sample
 
     def offsets(self):
+        """[(byte offset from the current position, block size)] of every
+        frame from the current position to the end, CRC-16 unchecked; the
+        stream is then finished (flac.c:365-443)"""
         self._decode()
-        if self._status not in (_atgpu.FD_OK, _atgpu.FD_MD5):
-            if self._status == _atgpu.FD_EOF:
-                raise IOError(_atgpu.FD_MESSAGES[_atgpu.FD_EOF])
-            raise ValueError(_atgpu.FD_MESSAGES.get(self._status, "Error"))
+        if self._walk_status != _atgpu.FD_OK:
+            raise _status_error(self._walk_status)
         self._finalized = True
-        return [(int(o), int(b)) for o, b in zip(self._offsets, self._block_sizes)]
+        if self._next >= len(self._lens):  # remaining_samples already 0
+            return []
+        base = int(self._offsets[self._next])
+        out = [(int(o) - base, int(b)) for o, b in
+               zip(self._offsets[self._next:], self._block_sizes[self._next:])]
+        self._next = len(self._lens)
+        return out
 
     def close(self):
         self._closed = True

@@ -23,16 +23,23 @@ RATES = (48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000, 18900,
 
 
 class ReplayGain(object):
+    """ReplayGain(sample_rate) (replaygain.c:115-182).  Like the reference,
+    the object keeps only the album state between titles -- the summed
+    12000-bin window histogram B and the album peak -- never the samples."""
+
     def __init__(self, sample_rate):
         if sample_rate not in RATES:
             raise ValueError("unsupported sample rate")
         self.sample_rate = sample_rate
-        self._titles = []   # (samples, channels, bps) of every title so far
+        self._album_hist = np.zeros(12000, dtype=np.uint64)
+        self._album_peak = 0.0
 
     def title_gain(self, pcmreader):
+        """(title gain, title peak) of one reader; its histogram is added
+        to the album's (get_title_gain, replaygain.c:776-800)"""
         if pcmreader.sample_rate != self.sample_rate:
             raise ValueError("pcmreader's sample rate doesn't match")
-        parts = []
+        parts, sizes = [], []
         while True:
             fl = pcmreader.read(4096)
             if not isinstance(fl, pcm.FrameList):
@@ -42,35 +49,35 @@ class ReplayGain(object):
             if fl.channels not in (1, 2):
                 raise ValueError("FrameList must contain only 1 or 2 channels")
             parts.append(fl.samples)
+            sizes.append(fl.frames)
         bps, ch = pcmreader.bits_per_sample, pcmreader.channels
-        if bps not in (8, 16, 24):
+        if parts and bps not in (8, 16, 24):
             raise ValueError("unsupported bits per sample")
-        samples = np.concatenate(parts) if parts else np.zeros(0, np.int32)
-        self._titles.append((samples, ch, bps))
-        (res,), _, _ = self._run([(samples, ch, bps)], album=False)
+        if not parts:
+            return (0.0, 0.0)  # nothing read: no window, peak 0.0
+        samples = np.concatenate(parts)
+        frames = len(samples) // ch
+        track = _atgpu.RgTrack(0, frames, ch, bps, self.sample_rate, 0)
+        # each read() result is one analyze_samples call: its size decides
+        # the fp64 summation grouping (replaygain.c:210-305)
+        if any(n != 4096 for n in sizes[:-1]) or sizes[-1] > 4096:
+            track.set_chunks(sizes)
+        (res,), peaks, _, hist = _atgpu.replaygain_host(samples, [track], 1,
+                                                        return_hist=True)
+        self._album_hist += hist[0]
+        self._album_peak = max(self._album_peak, peaks[0])
         return (res.title_gain, res.title_peak)
 
-    def _run(self, titles, album):
-        # the reference analyses mono as a duplicated stereo pair
-        # (replaygain.c:228-229), so mono titles are widened and every title
-        # of the album goes in one 2-channel batch
-        bufs, tracks, off = [], [], 0
-        for s, ch, bps in titles:
-            st = np.repeat(s, 2) if ch == 1 else s
-            frames = len(st) // 2
-            tracks.append(_atgpu.RgTrack(off, frames, 2, bps, self.sample_rate, 0))
-            bufs.append(st)
-            off += frames
-        buf = np.concatenate(bufs) if bufs else np.zeros(0, np.int32)
-        return _atgpu.replaygain_host(buf, tracks, 1 if album else 0)
-
     def album_gain(self):
-        if not self._titles:
+        """(album gain, album peak) over every title so far
+        (get_album_gain, replaygain.c:803-807; ValueError when empty)"""
+        if not self._album_hist.any():
             raise ValueError("Not enough samples to perform calculation")
-        res, peaks, gains = self._run(self._titles, album=True)
-        if not gains or math.isnan(gains[0]):
+        (gain,) = _atgpu.replaygain_hist_gain_host(
+            (self._album_hist & 0xFFFFFFFF).astype(np.uint32))
+        if math.isnan(gain):
             raise ValueError("Not enough samples to perform calculation")
-        return (gains[0], peaks[0])
+        return (gain, self._album_peak)
 
 
 def batch_gains(pcm_i32, tracks, n_albums):

@@ -75,9 +75,12 @@ struct DecTrack {
 };
 
 struct DecCount {
-    uint64_t pcm_frames;
+    uint64_t pcm_frames; // walked (offsets() view: CRC-16 not checked)
     uint32_t n_frames;
-    int32_t status;
+    int32_t status;      // what stopped the walk
+    uint64_t crc_pcm;    // PCM frames before the first bad CRC-16 frame
+    uint32_t crc_frame;  // index of that frame, ~0u if none
+    uint32_t pad;
 };
 
 struct ParseRec {
@@ -639,7 +642,7 @@ __device__ __forceinline__ uint32_t find_track(const DecTrack *tr, uint32_t nt, 
 __global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w, uint64_t nw,
                                                   uint64_t len, const DecTrack *__restrict__ tr,
                                                   uint32_t nt, uint32_t *__restrict__ ncand,
-                                                  uint64_t *__restrict__ cand_pos,
+                                                  uint32_t cap, uint64_t *__restrict__ cand_pos,
                                                   uint32_t *__restrict__ cand_idx)
 {
     const uint64_t gw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -666,8 +669,10 @@ __global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w
         if (dec_header(r, T, h) != FD_OK)
             continue;
         const uint32_t i = atomicAdd(ncand, 1u);
-        cand_pos[i] = p;
-        cand_idx[p] = i;
+        if (i < cap) { // over capacity: the host re-scans with room for all
+            cand_pos[i] = p;
+            cand_idx[p] = i;
+        }
     }
 }
 
@@ -709,8 +714,8 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
         return;
     const DecTrack t = tr[ti];
     const uint32_t nc = *ncand;
-    uint64_t pos = t.start, remaining = t.total, pcm = 0;
-    uint32_t nf = 0;
+    uint64_t pos = t.start, remaining = t.total, pcm = 0, crc_pcm = 0;
+    uint32_t nf = 0, crc_frame = 0xFFFFFFFFu;
     int status = FD_OK;
     while (remaining != 0) {
         ParseRec rec;
@@ -724,7 +729,14 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
             rec = recs[ci];
         else // not a candidate (its header fails), or truncated by remaining
             parse_frame(w, nw, pos, t, remaining, T, rec);
-        if (rec.status) {
+        // a bad CRC-16 does not change the frame's length: read() raises at
+        // it (flac.c:251-255), offsets() never checks it (flac.c:413-415)
+        if (rec.status == FD_FRAME_CRC) {
+            if (crc_frame == 0xFFFFFFFFu) {
+                crc_frame = nf;
+                crc_pcm = pcm;
+            }
+        } else if (rec.status) {
             status = rec.status;
             break;
         }
@@ -757,6 +769,9 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
         dc.pcm_frames = pcm;
         dc.n_frames = nf;
         dc.status = status;
+        dc.crc_pcm = crc_pcm;
+        dc.crc_frame = crc_frame;
+        dc.pad = 0;
         counts[ti] = dc;
     }
 }
@@ -1299,22 +1314,31 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     DHIP(d->tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
     DHIP(d->counts.ensure(sizeof(DecCount) * std::max<uint32_t>(n, 1)));
     DHIP(d->ncand.ensure(sizeof(uint32_t)));
-    // a frame is at least 10 bytes (header 6 + subframe 1 + CRC 2 ...), so
-    // at most len/2 positions can start candidates; sized for the worst case
-    const uint64_t max_cand = len / 2 + 1;
-    DHIP(d->cand_pos.ensure(sizeof(uint64_t) * max_cand));
+    // candidate scratch: a real frame is >= 10 bytes, but the true count is
+    // close to the frame count, so start at one slot per 16 bytes and re-scan
+    // with the exact count in the rare batch that needs more
+    uint64_t cap = std::min<uint64_t>(len / 16 + 4096, 0xFFFFFFFFull);
     DHIP(d->cand_idx.ensure(sizeof(uint32_t) * (len + 4)));
-    DHIP(d->recs.ensure(sizeof(ParseRec) * max_cand));
     DHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
-    DHIP(hipMemsetAsync(d->ncand.p, 0, sizeof(uint32_t), s));
     const uint32_t *w = (const uint32_t *)d_data;
     DecTrack *dtr = (DecTrack *)d->tracks.p;
     DHIP(hipEventRecord(d->ev[0], s));
-    if (n && len)
-        hipLaunchKernelGGL(k_dec_scan, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w, nw,
-                           len, dtr, n, (uint32_t *)d->ncand.p, (uint64_t *)d->cand_pos.p,
-                           (uint32_t *)d->cand_idx.p);
-    DHIP(hipGetLastError());
+    uint32_t found = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+        DHIP(d->cand_pos.ensure(sizeof(uint64_t) * cap));
+        DHIP(hipMemsetAsync(d->ncand.p, 0, sizeof(uint32_t), s));
+        if (n && len)
+            hipLaunchKernelGGL(k_dec_scan, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w,
+                               nw, len, dtr, n, (uint32_t *)d->ncand.p, (uint32_t)cap,
+                               (uint64_t *)d->cand_pos.p, (uint32_t *)d->cand_idx.p);
+        DHIP(hipGetLastError());
+        DHIP(hipMemcpyAsync(&found, d->ncand.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        DHIP(hipStreamSynchronize(s));
+        if (found <= cap)
+            break;
+        cap = found; // every sync position of the buffer is now known
+    }
+    DHIP(d->recs.ensure(sizeof(ParseRec) * std::max<uint64_t>(found, 1)));
     DHIP(hipEventRecord(d->ev[1], s));
     hipLaunchKernelGGL(k_dec_parse, dim3(4096), dim3(64), 0, s, w, nw, dtr, n,
                        (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
@@ -1395,7 +1419,9 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     std::vector<uint64_t> md5_off(n), md5_len(n);
     for (uint32_t t = 0; t < n; ++t) {
         md5_off[t] = d->tr[t].md5_base;
-        md5_len[t] = d->cnt[t].pcm_frames * d->tr[t].channels * ((d->tr[t].bps + 7) / 8);
+        const uint64_t vis = d->cnt[t].crc_frame != 0xFFFFFFFFu ? d->cnt[t].crc_pcm
+                                                                 : d->cnt[t].pcm_frames;
+        md5_len[t] = vis * d->tr[t].channels * ((d->tr[t].bps + 7) / 8);
     }
     DBuf &mb_buf = d->md5meta;
     DHIP(mb_buf.ensure(sizeof(uint64_t) * 2 * std::max<uint32_t>(n, 1)));
@@ -1419,17 +1445,26 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     uint64_t fbase = 0;
     for (uint32_t t = 0; t < n; ++t) {
         atg_flac_dec_result &r = res[t];
+        const DecCount &c = d->cnt[t];
         r.pcm_offset = d->tr[t].pcm_base / d->tr[t].channels;
-        r.pcm_frames = d->cnt[t].pcm_frames;
         r.first_frame = (uint32_t)fbase;
-        r.n_frames = d->cnt[t].n_frames;
-        fbase += r.n_frames;
+        r.walk_frames = c.n_frames;
+        r.walk_status = c.status;
+        fbase += c.n_frames;
         std::memcpy(r.md5, &md5[16 * (size_t)t], 16);
-        r.status = d->cnt[t].status;
-        // FlacDecoder_verify_okay (flac.c:479-493) once remaining reaches 0
-        if (r.status == FD_OK && std::memcmp(tracks[t].md5, zero, 16) != 0 &&
-            std::memcmp(tracks[t].md5, r.md5, 16) != 0)
-            r.status = FD_MD5;
+        if (c.crc_frame != 0xFFFFFFFFu) { // read() stops at the bad frame
+            r.pcm_frames = c.crc_pcm;
+            r.n_frames = c.crc_frame;
+            r.status = FD_FRAME_CRC;
+        } else {
+            r.pcm_frames = c.pcm_frames;
+            r.n_frames = c.n_frames;
+            r.status = c.status;
+            // FlacDecoder_verify_okay (flac.c:479-493) once remaining reaches 0
+            if (r.status == FD_OK && std::memcmp(tracks[t].md5, zero, 16) != 0 &&
+                std::memcmp(tracks[t].md5, r.md5, 16) != 0)
+                r.status = FD_MD5;
+        }
         r.reserved = 0;
     }
     return ATG_OK;

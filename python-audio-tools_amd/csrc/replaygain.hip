@@ -21,6 +21,7 @@
 // atg_replaygain_device and atg_replaygain_hist_gain (bench.py).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
 #include <mutex>
 #include <string>
@@ -68,6 +69,7 @@ struct RgTrack {
     uint64_t off;    // first interleaved sample
     uint64_t frames;
     uint32_t ch, bps, fi, window;
+    uint64_t chunk_base; // first read() chunk size in the chunk array, ~0: 4096s
 };
 
 struct Chan {
@@ -105,6 +107,7 @@ __device__ __forceinline__ double filt(Chan &s, double x, const double *ky, cons
 __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm,
                                                  const RgTrack *__restrict__ tracks, uint32_t n,
                                                  const uint64_t *__restrict__ win_base,
+                                                 const uint32_t *__restrict__ chunks,
                                                  double *__restrict__ wsum,
                                                  double *__restrict__ peaks)
 {
@@ -130,8 +133,11 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
     const uint32_t stride = T.ch;
     int32_t nx = T.frames ? p[0] : 0;
     uint32_t pf = 0;
-    for (uint64_t c0 = 0; c0 < T.frames; c0 += 4096) {
-        const long n4 = (long)(T.frames - c0 < 4096 ? T.frames - c0 : 4096);
+    uint64_t ci = T.chunk_base;
+    for (uint64_t c0 = 0; c0 < T.frames;) {
+        // one analyze_samples call per read() result (replaygain.c:210-305)
+        const long n4 = T.chunk_base != ~0ull ? (long)chunks[ci++]
+                                              : (long)(T.frames - c0 < 4096 ? T.frames - c0 : 4096);
         long pos = 0, batch = n4;
         while (batch > 0) {
             long cur = batch > window - totsamp ? window - totsamp : batch;
@@ -177,6 +183,7 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
                 totsamp = 0;
             }
         }
+        c0 += (uint64_t)n4;
     }
     asm volatile("" ::"v"(pf)); // keep the prefetch loads
     const double peak = (double)amax / peak_shift;
@@ -271,14 +278,18 @@ __global__ __launch_bounds__(256) void k_rg_gain(const uint32_t *__restrict__ hi
     }
 }
 
+// device buffers of one device (kept across calls; a batch pipeline calls
+// this once per album batch)
 struct RgCtx {
     std::mutex mu;
-    int device = -1;
+    bool coeffs = false;
     void *tracks = nullptr, *hist = nullptr, *peaks = nullptr, *gains = nullptr, *alb = nullptr,
-         *meta = nullptr, *wsum = nullptr, *wbase = nullptr, *peak2 = nullptr;
-    size_t cap_tracks = 0, cap_albums = 0, cap_win = 0, cap_wbase = 0, cap_peak2 = 0;
+         *meta = nullptr, *wsum = nullptr, *wbase = nullptr, *peak2 = nullptr, *chunks = nullptr;
+    size_t cap_tracks = 0, cap_albums = 0, cap_win = 0, cap_wbase = 0, cap_peak2 = 0,
+           cap_chunks = 0;
 };
-RgCtx g_ctx;
+constexpr int kMaxDevices = 64;
+RgCtx g_ctxs[kMaxDevices];
 
 } // namespace
 
@@ -292,16 +303,20 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
 {
     if ((!tracks || !results) && n)
         return rfail(ATG_ERR_INVALID, "NULL argument");
-    std::lock_guard<std::mutex> lock(g_ctx.mu);
     hipStream_t s = (hipStream_t)stream;
     int dev = 0;
     RHIP(hipGetDevice(&dev));
-    if (g_ctx.device != dev) {
+    if (dev < 0 || dev >= kMaxDevices)
+        return rfail(ATG_ERR_UNSUPPORTED, "device index too large");
+    RgCtx &g_ctx = g_ctxs[dev];
+    std::lock_guard<std::mutex> lock(g_ctx.mu);
+    if (!g_ctx.coeffs) {
         RHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_yule), RG_YULE, sizeof(RG_YULE)));
         RHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_butter), RG_BUTTER, sizeof(RG_BUTTER)));
-        g_ctx.device = dev;
+        g_ctx.coeffs = true;
     }
     std::vector<RgTrack> tr(n);
+    std::vector<uint32_t> chunks;
     std::vector<uint64_t> wbase(n + 1, 0);
     std::vector<uint32_t> first(n_albums, 0), count(n_albums, 0);
     for (uint32_t t = 0; t < n; ++t) {
@@ -317,8 +332,21 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
             return rfail(ATG_ERR_INVALID, "album index out of range");
         if (n_albums && t && a.album < tracks[t - 1].album)
             return rfail(ATG_ERR_INVALID, "tracks must be grouped by album");
+        uint64_t cbase = ~0ull;
+        if (a.chunk_frames) {
+            uint64_t tot = 0;
+            for (uint64_t i = 0; i < a.n_chunks; ++i) {
+                if (!a.chunk_frames[i])
+                    return rfail(ATG_ERR_INVALID, "read() chunk sizes must be positive");
+                tot += a.chunk_frames[i];
+            }
+            if (tot != a.pcm_frames)
+                return rfail(ATG_ERR_INVALID, "read() chunk sizes must add up to pcm_frames");
+            cbase = chunks.size();
+            chunks.insert(chunks.end(), a.chunk_frames, a.chunk_frames + a.n_chunks);
+        }
         tr[t] = RgTrack{a.pcm_offset * a.channels, a.pcm_frames, a.channels, a.bits_per_sample,
-                        (uint32_t)fi, (uint32_t)std::ceil(a.sample_rate * 0.050)};
+                        (uint32_t)fi, (uint32_t)std::ceil(a.sample_rate * 0.050), cbase};
         wbase[t + 1] = wbase[t] + a.pcm_frames / tr[t].window;
         if (n_albums) {
             if (!count[a.album])
@@ -344,8 +372,27 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
         RHIP(hipMalloc(&g_ctx.gains, sizeof(double) * (g_ctx.cap_tracks + n_albums + 1)));
         g_ctx.cap_albums = n_albums;
     }
-    if (!n)
+    if (!n) { // empty albums: peak 0.0 (replaygain.c:180), empty histograms
+        if (album_peaks)
+            for (uint32_t a = 0; a < n_albums; ++a)
+                album_peaks[a] = 0.0;
+        if (n_albums) {
+            uint32_t *album = d_album_hist ? d_album_hist : (uint32_t *)g_ctx.alb;
+            RHIP(hipMemsetAsync(album, 0, sizeof(uint32_t) * kBins * (size_t)n_albums, s));
+            RHIP(hipStreamSynchronize(s));
+        }
         return ATG_OK;
+    }
+    if (chunks.size() > g_ctx.cap_chunks || !g_ctx.chunks) {
+        (void)hipFree(g_ctx.chunks);
+        g_ctx.chunks = nullptr;
+        const size_t want = std::max<size_t>(chunks.size(), 1);
+        RHIP(hipMalloc(&g_ctx.chunks, sizeof(uint32_t) * want));
+        g_ctx.cap_chunks = want;
+    }
+    if (!chunks.empty())
+        RHIP(hipMemcpyAsync(g_ctx.chunks, chunks.data(), sizeof(uint32_t) * chunks.size(),
+                            hipMemcpyHostToDevice, s));
     if (wbase[n] + 1 > g_ctx.cap_win) {
         (void)hipFree(g_ctx.wsum);
         (void)hipFree(g_ctx.wbase);
@@ -370,7 +417,8 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
     RHIP(hipMemsetAsync(g_ctx.hist, 0, sizeof(uint32_t) * kBins * (size_t)n, s));
     hipLaunchKernelGGL(k_rg_title, dim3((2 * n + 63) / 64), dim3(64), 0, s, d_pcm,
                        (const RgTrack *)g_ctx.tracks, n, (const uint64_t *)g_ctx.wbase,
-                       (double *)g_ctx.wsum, (double *)g_ctx.peak2);
+                       (const uint32_t *)g_ctx.chunks, (double *)g_ctx.wsum,
+                       (double *)g_ctx.peak2);
     RHIP(hipGetLastError());
     hipLaunchKernelGGL(k_rg_bin, dim3(4, n), dim3(256), 0, s, (const RgTrack *)g_ctx.tracks, n,
                        (const uint64_t *)g_ctx.wbase, (const double *)g_ctx.wsum,
@@ -414,7 +462,6 @@ atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *
 {
     if (!n)
         return ATG_OK;
-    std::lock_guard<std::mutex> lock(g_ctx.mu);
     hipStream_t s = (hipStream_t)stream;
     double *d_g = nullptr;
     RHIP(hipMalloc(&d_g, sizeof(double) * n));

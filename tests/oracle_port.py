@@ -316,16 +316,21 @@ def convert(kind, pcm, channels, in_bps, out_bps=None, mask=0, dither=b""):
 
 
 # --- ReplayGain (oracle/replaygain_port.c; parity unpinned, see header) ---
-def rg_title(pcm, channels, bps, rate):
-    """-> (histogram uint32[12000], title peak)"""
+def rg_title(pcm, channels, bps, rate, chunks=None):
+    """-> (histogram uint32[12000], title peak); chunks = the frame counts
+    the reader's read(4096) calls returned (None: 4096-frame reads)"""
     lib = load()
     a = np.ascontiguousarray(pcm, dtype=np.int32)
     A = np.zeros(12000, dtype=np.uint32)
     P = ctypes.c_void_p
-    lib.rgport_title.argtypes = [P, c_u64, c_u32, c_u32, c_u32, P]
-    lib.rgport_title.restype = ctypes.c_double
-    peak = lib.rgport_title(a.ctypes.data, len(a) // channels, channels, bps, rate,
-                            A.ctypes.data)
+    lib.rgport_title_chunks.argtypes = [P, c_u64, c_u32, c_u32, c_u32, P, c_u64, P]
+    lib.rgport_title_chunks.restype = ctypes.c_double
+    ch = None if chunks is None else np.ascontiguousarray(chunks, dtype=np.uint32)
+    peak = lib.rgport_title_chunks(a.ctypes.data, len(a) // channels, channels, bps, rate,
+                                   None if ch is None else ch.ctypes.data,
+                                   0 if ch is None else len(ch), A.ctypes.data)
+    if peak < 0:
+        raise ValueError("rgport_title_chunks rejected the track")
     return A, peak
 
 

@@ -120,3 +120,32 @@ def test_two_rank_album_reduce_matches_single_process():
         assert np.array_equal(hist, B.astype(np.uint32))
         assert pk == peak
         assert oracle_port.rg_gain(hist) == oracle_port.rg_gain(B.astype(np.uint32))
+
+
+@pytest.mark.parametrize("scaling,tracks,want_total", [("weak", 3, 6), ("strong", 5, 5)])
+def test_bench_spawns_ranks(scaling, tracks, want_total):
+    """`python bench.py --gpus 2` spawns its own ranks (no torchrun) and the
+    rank-0 line reports n_gpus, the scaling mode and the whole-job track
+    count; --selftest swaps the GPU step for the CPU oracle (gloo)"""
+    import json
+    import subprocess
+    import sys
+    env = dict(os.environ)
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    p = subprocess.run([sys.executable, bench.__file__, "--selftest", "--gpus", "2",
+                        "--tracks", str(tracks), "--frames", "1", "--steps", "1",
+                        "--warmup", "0", "--scaling", scaling],
+                       capture_output=True, text=True, env=env, timeout=300)
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [l for l in p.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1
+    d = json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["scaling"] == scaling and d["selftest"] is True
+    assert d["tracks_total"] == want_total
+
+
+def test_strong_shards_partition_the_batch():
+    for world in (1, 2, 3, 8):
+        ids = [t for r in range(world) for t in bench.shard(world, r, 1024, "strong")]
+        assert ids == list(range(1024))

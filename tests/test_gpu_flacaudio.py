@@ -57,4 +57,4 @@ def test_multichannel_mask_tag_and_round_trip(tmp_path):
             break
         got.append(fl.samples)
     assert np.array_equal(np.concatenate(got), pcm)
-    assert dec.offsets()[0][0] == 0
+    assert a.to_pcm().offsets()[0][0] == 0

@@ -130,3 +130,55 @@ def test_replaygain_class_mixed_mono_stereo():
     A2, p2 = op.rg_title(st, 2, 16, 48000)
     assert g1 == (op.rg_gain(A1), p1) and g2 == (op.rg_gain(A2), p2)
     assert rg.album_gain() == (op.rg_gain(A1 + A2), max(p1, p2))
+
+
+@pytest.mark.parametrize("chunk", [1152, 333, 7, 5000])
+def test_chunked_reads_match_oracle(chunk):
+    """title_gain over a reader whose read(4096) returns `chunk` frames:
+    every result is one analyze_samples call (replaygain.c:210-305), so the
+    grouping of the fp64 window sums follows the reader's chunks"""
+    import audiotools
+    from audiotools import replaygain
+
+    class ChunkReader(audiotools.FrameListReader):
+        def read(self, pcm_frames):
+            return audiotools.FrameListReader.read(self, chunk)
+
+    x = make(44100, 2, 16, 30000 + chunk, 5)
+    rg = replaygain.ReplayGain(44100)
+    got = rg.title_gain(ChunkReader(x, 44100, 2, 16))
+    n = len(x) // 2
+    sizes = [chunk] * (n // chunk) + ([n % chunk] if n % chunk else [])
+    A, pk = op.rg_title(x, 2, 16, 44100, chunks=sizes)
+    assert got == (op.rg_gain(A), pk)
+    assert rg.album_gain() == (op.rg_gain(A), pk)
+
+
+def test_title_gain_over_flac_decoder(tmp_path):
+    """ReplayGain of a FLAC preset-0 file read through FlacDecoder (one
+    1152-frame FLAC frame per read, flac.c:174)"""
+    import audiotools
+    from audiotools import flac, replaygain
+    x = make(44100, 2, 16, 44100 * 2 + 99, 0)
+    fn = str(tmp_path / "p0.flac")
+    a = flac.FlacAudio.from_pcm(fn, audiotools.FrameListReader(x, 44100, 2, 16, 3), "0",
+                                total_pcm_frames=len(x) // 2)
+    rg = replaygain.ReplayGain(44100)
+    got = rg.title_gain(a.to_pcm())
+    n = len(x) // 2
+    sizes = [1152] * (n // 1152) + ([n % 1152] if n % 1152 else [])
+    A, pk = op.rg_title(x, 2, 16, 44100, chunks=sizes)
+    assert got == (op.rg_gain(A), pk)
+
+
+def test_empty_title_and_empty_batch():
+    import audiotools
+    from audiotools import _atgpu, replaygain
+    rg = replaygain.ReplayGain(44100)
+    assert rg.title_gain(audiotools.FrameListReader(np.zeros(0, np.int32), 44100, 2, 16)) == \
+        (0.0, 0.0)
+    with pytest.raises(ValueError):
+        rg.album_gain()
+    res, peaks, gains, hist = _atgpu.replaygain_host(np.zeros(0, np.int32), [], 2,
+                                                     return_hist=True)
+    assert peaks == [0.0, 0.0] and not hist.any()

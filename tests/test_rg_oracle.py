@@ -4,6 +4,8 @@ input scaled by << 8, the 95th-percentile rule).  Parity unpinned: the
 reference has no ReplayGain fixtures and replaygain.c is a Python-2 module."""
 import math
 
+import pytest
+
 import numpy as np
 
 import oracle_port as op
@@ -57,3 +59,14 @@ def test_rg_reader_oracle_invariants():
     y = op.rg_apply(x, 2, 16, 2.0, 4096, d)
     base = np.clip(np.round(x.astype(np.float64) * 2.0), -32768, 32767).astype(np.int32)
     assert set(np.unique(y ^ base)) <= {0, 1}
+
+
+def test_chunked_oracle_equals_default_for_4096_chunks():
+    """the chunk-size form of the oracle reduces to the 4096-read form"""
+    x = np.random.default_rng(3).integers(-30000, 30000, 2 * 20000).astype(np.int32)
+    A0, p0 = op.rg_title(x, 2, 16, 44100)
+    sizes = [4096] * 4 + [20000 - 4 * 4096]
+    A1, p1 = op.rg_title(x, 2, 16, 44100, chunks=sizes)
+    assert np.array_equal(A0, A1) and p0 == p1
+    with pytest.raises(ValueError):
+        op.rg_title(x, 2, 16, 44100, chunks=[100])

@@ -8,6 +8,7 @@ OUT="$R/gpurun_out/pmc"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 ARGS="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify"
+# the converter leg (k_pcm_bps) runs inside the decode legs of the same process
 pass() {
     local name=$1; shift
     timeout -s KILL 90 rocprofv3 --pmc "$@" -d "$OUT/$name" -o run --output-format csv \

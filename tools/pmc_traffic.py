@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """profiles/pmc_traffic.json from a tools/gpu_pmc.sh run: HBM bytes per
 launch per kernel = FETCH_SIZE x 2 (gfx950 reports half of wide streaming
-reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both KiB -> bytes."""
+reads, MI355X_MICROARCH.md 'HBM') + WRITE_SIZE, both KiB -> bytes.
+Also profiles/pmc_valu.json: SQ_INSTS_VALU / SQ_INSTS_SALU / SQ_WAVES per
+launch (wave-instructions) per kernel, for bench.py's roofline_valu block.
+usage: pmc_traffic.py PMC_DIR TRAFFIC_JSON [VALU_JSON FRAMES_PER_LAUNCH SOURCE]"""
 import json
 import subprocess
 import sys
@@ -16,7 +19,8 @@ names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
          # decoder (flac_decode.hip, md5.hip)
          "k_dec_scan": "dec_scan", "k_dec_parse": "dec_parse", "k_dec_chain": "dec_chain",
          "k_dec_subframe": "dec_subframe", "k_dec_unrow": "dec_unrow",
-         "k_dec_interleave": "dec_interleave", "k_bytes_md5": "dec_md5"}
+         "k_dec_interleave": "dec_interleave", "k_bytes_md5": "dec_md5",
+         "k_pcm_bps": "pcm_bps"}
 out = {}
 for k, v in pmc.items():
     base = k.split("<")[0]
@@ -25,3 +29,14 @@ for k, v in pmc.items():
         out[names[base]] = int(v["HBM_read_bytes"] + v["HBM_write_bytes"])
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
 print(json.dumps(out, indent=1, sort_keys=True))
+if len(sys.argv) > 3:
+    valu = {}
+    for k, v in pmc.items():
+        base = k.split("<")[0]
+        if base in names and "SQ_INSTS_VALU" in v:
+            e = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES",
+                                   "SQ_INSTS_LDS", "SQ_INSTS_VMEM") if c in v}
+            e["frames"] = int(sys.argv[4])
+            e["source"] = sys.argv[5] if len(sys.argv) > 5 else src
+            valu[names[base]] = e
+    json.dump(valu, open(sys.argv[3], "w"), indent=1, sort_keys=True)
