@@ -69,7 +69,7 @@ def parse_args(argv=None):
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
     ap.add_argument("--scaling", choices=("weak", "strong"), default="weak")
     ap.add_argument("--cpu-threads", type=int, default=0)
-    ap.add_argument("--cpu-ref-tracks", type=int, default=96,
+    ap.add_argument("--cpu-ref-tracks", type=int, default=256,
                     help="tracks the reference encoder baseline encodes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")

@@ -1,9 +1,10 @@
 #!/bin/bash
-# GPU-box recipe: parity tests then one bench line (run via gpurun).
+# GPU-box recipe: parity tests, smoke, then one full bench line (run via gpurun).
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out"
 cd "$R"
-timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread \
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
     > gpurun_out/pytest_gpu.log 2>&1
-timeout -k 10 300 python -u bench.py --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/bench.log 2>&1
+timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+timeout -k 10 600 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.log 2>&1
