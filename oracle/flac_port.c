@@ -196,8 +196,11 @@ static void md5_pcm(md5_state *s, const int32_t *pcm, size_t nsamples,
     uint8_t tmp[4096];
     unsigned bytes = bps / 8;
     size_t fill = 0;
+    /* FrameList.to_bytes saturates out-of-range samples (src/pcm.c:1826-1948) */
+    const int32_t hi = bps >= 1 && bps <= 31 ? (int32_t)((1u << (bps - 1)) - 1u) : INT32_MAX;
+    const int32_t lo = -hi - 1;
     for (size_t i = 0; i < nsamples; i++) {
-        uint32_t v = (uint32_t)pcm[i];
+        uint32_t v = (uint32_t)(pcm[i] > hi ? hi : (pcm[i] < lo ? lo : pcm[i]));
         for (unsigned b = 0; b < bytes; b++)
             tmp[fill++] = (uint8_t)(v >> (8 * b));
         if (fill + 4 > sizeof(tmp)) {

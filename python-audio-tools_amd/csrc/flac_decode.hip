@@ -1020,14 +1020,20 @@ __global__ __launch_bounds__(256) void k_dec_interleave(const DecTrack *__restri
             for (uint32_t c = 0; c < ch && c < 8; ++c)
                 o[c] = src[(uint64_t)c * N + k];
         }
+        // FrameList.to_bytes saturates samples outside the bps range
+        // (src/pcm.c:1826-1948): only a corrupt stream can produce them
+        const int32_t hi = t.bps >= 1 && t.bps <= 31 ? (int32_t)((1u << (t.bps - 1)) - 1u)
+                                                      : 0x7FFFFFFF;
+        const int32_t lo = -hi - 1;
         for (uint32_t c = 0; c < ch && c < 8; ++c) {
             const uint64_t s = (uint64_t)k * ch + c;
             dst[s] = o[c];
+            const int32_t v = o[c] > hi ? hi : (o[c] < lo ? lo : o[c]);
             if (bb == 2) {
-                ((int16_t *)bdst)[s] = (int16_t)o[c];
+                ((int16_t *)bdst)[s] = (int16_t)v;
             } else {
                 for (uint32_t q = 0; q < bb; ++q)
-                    bdst[s * bb + q] = (uint8_t)((uint32_t)o[c] >> (8 * q));
+                    bdst[s * bb + q] = (uint8_t)((uint32_t)v >> (8 * q));
             }
         }
     }

@@ -1,0 +1,120 @@
+#!/usr/bin/env python3
+"""Generate tests/golden/alac_vectors.json with the REFERENCE ALAC encoder
+and decoder (oracle/_ref/alacenc, alacdec: src/encoders/alac.c and
+src/decoders/alac.c built standalone by `make -C oracle ref`, this
+container only).
+
+Encoder vectors: seeded inputs from tests/signals.py -> sha256 of the mdat
+atom the reference writes.  Decoder vectors: m4a files = the reference's
+mdat in the container audiotools.m4a writes (itself pinned to the
+reference's fixture test/alac-allframes.m4a), clean and with seeded bit
+flips / truncations, -> the reference decoder's exit status and the md5 /
+length of the PCM bytes it wrote (saturated little-endian, as
+FrameList.to_bytes).  The reference's own fixture alac-allframes.m4a is
+included.  The CPU tests then pin oracle/alac_port.c to these vectors on any
+machine, and the GPU tests pin the HIP kernels.
+"""
+import hashlib
+import json
+import os
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.dirname(HERE), os.path.join(os.path.dirname(os.path.dirname(HERE)),
+                                                    "python-audio-tools_amd")]
+import numpy as np  # noqa: E402
+
+import oracle_port  # noqa: E402
+import signals  # noqa: E402
+
+OUT = os.path.join(HERE, "alac_vectors.json")
+
+
+def enc_cases():
+    out = []
+    for ch in (1, 2, 3, 4, 5, 6, 7, 8):
+        for bps in (16, 24):
+            for kind in ("tone", "noise", "silence", "sine", "chirp", "wasted"):
+                if ch > 2 and kind in ("sine", "chirp"):
+                    continue
+                n = 4096 * 2 + 333 if ch <= 2 else 4096 + 77
+                out.append(("%s_c%d_b%d" % (kind, ch, bps), kind, n, ch, bps, 4096, ch * 31 + bps))
+    for bs in (1, 9, 10, 11, 20, 33, 1152, 4095):
+        for ch, bps in ((1, 16), (2, 16), (2, 24), (6, 24)):
+            n = 3 * bs + 5
+            out.append(("bs%d_c%d_b%d" % (bs, ch, bps), "tone", n, ch, bps, bs, bs + ch))
+    for n in (1, 5, 9, 10, 4096, 4097):
+        out.append(("len%d" % n, "noise", n, 2, 16, 4096, n))
+    return out
+
+
+def make_pcm(kind, n, ch, bps, seed):
+    return signals.make(kind, n, ch, bps, seed=seed)
+
+
+def main():
+    if not os.path.exists(oracle_port.REF_ALACENC):
+        sys.exit("oracle/_ref/alacenc missing: run `make -C oracle ref` where "
+                 "/root/reference exists")
+    from audiotools import m4a
+    enc, dec, bad = [], [], 0
+    for name, kind, n, ch, bps, bs, seed in enc_cases():
+        x = make_pcm(kind, n, ch, bps, seed)
+        ref = oracle_port.ref_alac_encode(x, ch, bps, block_size=bs)
+        mine, fs = oracle_port.alac_encode(x, ch, bps, block_size=bs)
+        bad += mine != ref
+        enc.append(dict(name=name, kind=kind, n=n, channels=ch, bps=bps, block_size=bs,
+                        seed=seed, bytes=len(ref), sha256=hashlib.sha256(ref).hexdigest(),
+                        framesets=len(fs)))
+    # decoder: containers around reference mdats, clean + corrupted
+    rng = np.random.default_rng(2024)
+    for name, kind, n, ch, bps, seed in (("d_tone_c2_b16", "tone", 4096 * 3 + 111, 2, 16, 1),
+                                         ("d_noise_c2_b24", "noise", 4096 * 2 + 7, 2, 24, 2),
+                                         ("d_tone_c6_b16", "tone", 4096 * 2 + 50, 6, 16, 3),
+                                         ("d_sil_c1_b16", "silence", 5000, 1, 16, 4),
+                                         ("d_tone_c8_b24", "tone", 4096 + 9, 8, 24, 5)):
+        x = make_pcm(kind, n, ch, bps, seed)
+        mdat = oracle_port.ref_alac_encode(x, ch, bps)
+        _, fs = oracle_port.alac_encode(x, ch, bps)
+        img = m4a.m4a_file(ch, bps, 44100, 4096, n, mdat, fs, create_date=0x7A11C0DE,
+                           version="2.22alpha1")
+        mstart = len(img) - len(mdat)
+        muts = [("clean", [], None)]
+        for t in range(24):
+            if t % 4 == 3:
+                muts.append(("cut%d" % t, [], int(rng.integers(mstart, len(img)))))
+            elif t % 4 == 2:
+                pos = int(rng.integers(0, mstart))
+                muts.append(("hdr%d" % t, [(pos, 1 << int(rng.integers(0, 8)))], None))
+            else:
+                pos = int(rng.integers(mstart + 8, len(img)))
+                muts.append(("flip%d" % t, [(pos, 1 << int(rng.integers(0, 8)))], None))
+        dec.append(dict(name=name, kind=kind, n=n, channels=ch, bps=bps, seed=seed,
+                        image_sha256=hashlib.sha256(img).hexdigest(), cases=[]))
+        for mname, xor, cut in muts:
+            b = bytearray(img)
+            for pos, v in xor:
+                b[pos] ^= v
+            if cut is not None:
+                b = b[:cut]
+            rc, out, err = oracle_port.ref_alac_decode(bytes(b))
+            dec[-1]["cases"].append(dict(name=mname, xor=xor, cut=cut, rc=rc,
+                                         pcm_bytes=len(out),
+                                         pcm_md5=hashlib.md5(out).hexdigest(),
+                                         stderr=err.strip()[:80]))
+    fx = os.path.join(HERE, "fixtures", "alac-allframes.m4a")
+    rc, out, err = oracle_port.ref_alac_decode(open(fx, "rb").read())
+    fixture = dict(file="alac-allframes.m4a", rc=rc, pcm_bytes=len(out),
+                   pcm_md5=hashlib.md5(out).hexdigest())
+    json.dump({"generator": "tests/golden/make_alac_golden.py",
+               "reference": "src/encoders/alac.c, src/decoders/alac.c standalone "
+                            "(oracle/_ref/alacenc, alacdec)",
+               "encoder": enc, "decoder": dec, "fixture": fixture},
+              open(OUT, "w"), indent=1)
+    print("%d encoder vectors (%d port mismatches), %d decoder streams -> %s"
+          % (len(enc), bad, len(dec), OUT))
+    sys.exit(1 if bad else 0)
+
+
+if __name__ == "__main__":
+    main()

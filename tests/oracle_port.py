@@ -272,8 +272,12 @@ def decode_frames(data, si=None, start=None, remaining=None, check_crc=True,
 
 
 def pcm_bytes(pcm, bps):
-    """FrameList.to_bytes(little_endian, signed) for 8/16/24-bit samples"""
+    """FrameList.to_bytes(little_endian, signed) for 8/16/24-bit samples;
+    out-of-range values saturate as the reference's int_to_char converters
+    do (src/pcm.c:1826-1948)"""
     a = np.asarray(pcm, dtype=np.int32)
+    lim = 1 << (bps - 1)
+    a = np.clip(a, -lim, lim - 1)
     if a.size == 0:
         return b""
     if bps == 8:
@@ -360,3 +364,149 @@ def rg_apply(pcm, channels, bps, multiplier, chunk_frames, dither):
     lib.pcmconvport_apply_gain(a.ctypes.data, out.ctypes.data, len(a) // channels, channels,
                                bps, multiplier, chunk_frames, d.ctypes.data)
     return out[:len(a)]
+
+
+# --- ALAC (oracle/alac_port.c; pinned to oracle/_ref/alacenc / alacdec) ---
+REF_ALACENC = os.path.join(ORACLE_DIR, "_ref", "alacenc")
+REF_ALACDEC = os.path.join(ORACLE_DIR, "_ref", "alacdec")
+ALAC_DEFAULTS = dict(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14)
+
+
+class AlacOptions(ctypes.Structure):
+    _fields_ = [("block_size", c_u32), ("initial_history", c_u32),
+                ("history_multiplier", c_u32), ("maximum_k", c_u32)]
+
+
+class AlacInfo(ctypes.Structure):
+    _fields_ = [("max_samples_per_frame", c_u32), ("bits_per_sample", c_u32),
+                ("history_multiplier", c_u32), ("initial_history", c_u32),
+                ("maximum_k", c_u32), ("channels", c_u32), ("sample_rate", c_u32),
+                ("total_frames", c_u32), ("mdat_offset", c_u64), ("n_seekpoints", c_u32),
+                ("reserved", c_u32)]
+
+
+class AlacSeekPoint(ctypes.Structure):
+    _fields_ = [("pcm_frames_offset", c_u64), ("file_offset", c_u64)]
+
+
+ALAC_OK, ALAC_IO_ERROR, ALAC_INVALID_UNUSED_BITS = 0, 1, 2
+ALAC_MESSAGES = {1: "I/O Errror", 2: "invalid unused bits", 3: "invalid alac atom",
+                 4: "invalid mdhd atom", 5: "mdia atom not found", 6: "stsd atom not found",
+                 7: "mdhd atom not found", 8: "invalid seektable entries",
+                 9: "Unable to locate 'mdat' atom in stream", 10: "channel length mismatch"}
+
+
+def _alac_lib():
+    lib = load()
+    if not hasattr(lib, "_alac_ready"):
+        P = ctypes.c_void_p
+        lib.alacport_encode.restype = ctypes.c_int
+        lib.alacport_encode.argtypes = [P, c_u64, c_u32, c_u32, ctypes.POINTER(AlacOptions), P,
+                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t), P,
+                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        lib.alacport_max_mdat_bytes.restype = ctypes.c_size_t
+        lib.alacport_max_mdat_bytes.argtypes = [c_u64, c_u32, c_u32, c_u32]
+        lib.alacport_read_info.restype = ctypes.c_int
+        lib.alacport_read_info.argtypes = [ctypes.c_char_p, ctypes.c_size_t,
+                                           ctypes.POINTER(AlacInfo), P, ctypes.c_size_t]
+        lib.alacport_decode.restype = ctypes.c_int
+        lib.alacport_decode.argtypes = [ctypes.c_char_p, ctypes.c_size_t,
+                                        ctypes.POINTER(AlacInfo), c_u64, c_u64, P,
+                                        ctypes.c_size_t, ctypes.POINTER(c_u64), P, P,
+                                        ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t)]
+        lib._alac_ready = True
+    return lib
+
+
+def alac_encode(pcm, channels, bps, **opts):
+    """-> (mdat atom bytes, [frameset byte sizes])"""
+    lib = _alac_lib()
+    o = dict(ALAC_DEFAULTS)
+    o.update(opts)
+    op = AlacOptions(o["block_size"], o["initial_history"], o["history_multiplier"],
+                     o["maximum_k"])
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames = len(a) // channels
+    cap = lib.alacport_max_mdat_bytes(frames, channels, bps, op.block_size)
+    out = np.zeros(cap, dtype=np.uint8)
+    olen = ctypes.c_size_t()
+    nfs_cap = frames // op.block_size + 2
+    fs = np.zeros(nfs_cap, dtype=np.uint32)
+    nfs = ctypes.c_size_t()
+    rc = lib.alacport_encode(a.ctypes.data_as(ctypes.c_void_p), frames, channels, bps,
+                             ctypes.byref(op), out.ctypes.data_as(ctypes.c_void_p), cap,
+                             ctypes.byref(olen), fs.ctypes.data_as(ctypes.c_void_p), nfs_cap,
+                             ctypes.byref(nfs))
+    if rc != 0:
+        raise ValueError("alacport_encode failed: %d" % rc)
+    return out[:olen.value].tobytes(), [int(x) for x in fs[:nfs.value]]
+
+
+def alac_read_info(data):
+    """-> (status, AlacInfo, [(pcm_frames_offset, file_offset)])"""
+    lib = _alac_lib()
+    info = AlacInfo()
+    sp = (AlacSeekPoint * 65536)()
+    rc = lib.alacport_read_info(bytes(data), len(data), ctypes.byref(info),
+                                ctypes.cast(sp, ctypes.c_void_p), 65536)
+    pts = [(sp[i].pcm_frames_offset, sp[i].file_offset)
+           for i in range(min(info.n_seekpoints, 65536))]
+    return rc, info, pts
+
+
+def alac_decode(data, info=None, start=None, remaining=None):
+    """the read() loop over an m4a image -> dict(code, pcm (wave order,
+    interleaved int32), framesets [(pcm frames, absolute byte offset)])"""
+    lib = _alac_lib()
+    data = bytes(data)
+    if info is None:
+        rc, info, _ = alac_read_info(data)
+        if rc:
+            return dict(code=100 + rc, pcm=np.zeros(0, np.int32), framesets=[])
+    if start is None:
+        start = info.mdat_offset
+    if remaining is None:
+        remaining = info.total_frames
+    ch = max(1, info.channels)
+    cap = (int(remaining) + 2 * max(1, info.max_samples_per_frame) + 64) * ch
+    while True:
+        pcm = np.zeros(cap, dtype=np.int32)
+        fsn = len(data) // 2 + 4
+        fsf = np.zeros(fsn, dtype=np.uint32)
+        fso = np.zeros(fsn, dtype=np.uint64)
+        got, nfs = c_u64(), ctypes.c_size_t()
+        code = lib.alacport_decode(data, len(data), ctypes.byref(info), start, remaining,
+                                   pcm.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(got),
+                                   fsf.ctypes.data_as(ctypes.c_void_p),
+                                   fso.ctypes.data_as(ctypes.c_void_p), fsn, ctypes.byref(nfs))
+        if code != -1:
+            break
+        cap *= 4
+    n = min(nfs.value, fsn)
+    return dict(code=code, pcm=pcm[:got.value * ch],
+                framesets=[(int(fsf[i]), int(fso[i])) for i in range(n)])
+
+
+def ref_alac_encode(pcm, channels, bps, **opts):
+    """the reference encoder (oracle/_ref/alacenc) -> mdat bytes"""
+    import tempfile
+    o = dict(ALAC_DEFAULTS)
+    o.update(opts)
+    args = [REF_ALACENC, "-c", str(channels), "-b", str(bps), "-B", str(o["block_size"]),
+            "-M", str(o["history_multiplier"]), "-K", str(o["maximum_k"])]
+    raw = pcm_bytes(pcm, bps)
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, "o.mdat")
+        subprocess.run(args + [fn], input=raw, stdout=subprocess.DEVNULL, check=True)
+        return open(fn, "rb").read()
+
+
+def ref_alac_decode(m4a_bytes):
+    """the reference decoder (oracle/_ref/alacdec) -> (exit code, PCM bytes,
+    stderr text)"""
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, "i.m4a")
+        open(fn, "wb").write(m4a_bytes)
+        p = subprocess.run([REF_ALACDEC, fn], capture_output=True)
+        return p.returncode, p.stdout, p.stderr.decode("latin-1")
