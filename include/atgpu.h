@@ -349,6 +349,63 @@ atg_status atg_pcm_apply_gain_host(int device, const int32_t *in, int32_t *out,
                                    uint32_t chunk_frames, const uint8_t *dither,
                                    uint64_t dither_bytes, uint64_t dither_bit0);
 
+/* ------------------------------------------------------------------ */
+/* ALAC encoder (E1-E7).  Replaces the body of the reference's          */
+/* audiotools.encoders.encode_alac (src/encoders/alac.c:30-206:         */
+/* ALACEncoder_encode_alac -> write_frameset / write_frame /            */
+/* compute_coefficients / calculate_residuals / encode_residuals) for a */
+/* batch of tracks; audiotools.m4a.ALACAudio.from_pcm wraps the mdat in */
+/* the M4A atoms on the host.  Leftweights 0..4, shift 2 (the           */
+/* reference's fixed minimum/maximum_interlacing_leftweight).           */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint32_t block_size;         /* PCM frames per frameset, 1..65535 */
+    uint32_t initial_history;    /* encode_alac keyword arguments     */
+    uint32_t history_multiplier;
+    uint32_t maximum_k;
+} atg_alac_options;
+
+/* Per-track result: the mdat atom (32-bit size, "mdat", framesets) is
+   `bytes` long at out + out_offset; frameset_bytes[first_frameset ..
+   first_frameset + n_framesets) is the frame-size log encode_alac returns
+   (alac.c:150-151, 1255-1290). */
+typedef struct {
+    uint64_t out_offset;
+    uint64_t bytes;
+    uint64_t pcm_frames;
+    uint32_t first_frameset;
+    uint32_t n_framesets;
+    int32_t status;
+    uint32_t reserved;
+} atg_alac_track_result;
+
+typedef struct atg_alac_encoder atg_alac_encoder;
+
+const char *atg_alac_last_error(void);
+atg_status atg_alac_encoder_create(int device, atg_alac_encoder **out);
+void atg_alac_encoder_destroy(atg_alac_encoder *enc);
+/* framesets and worst-case output bytes of a batch (tracks as for FLAC:
+   block_size frames + a short last one, or explicit frame_sizes) */
+atg_status atg_alac_batch_bounds(atg_alac_encoder *enc, const atg_alac_options *opts,
+                                 const atg_track *tracks, uint32_t n_tracks, uint32_t channels,
+                                 uint32_t bits_per_sample, uint64_t *total_framesets,
+                                 uint64_t *out_bytes);
+/* PCM and output in device memory (d_out 4-byte aligned, out_cap >= the
+   bound); frameset_bytes (host, total_framesets entries) may be NULL */
+atg_status atg_alac_encode_device(atg_alac_encoder *enc, const atg_alac_options *opts,
+                                  const void *d_pcm, atg_pcm_format format,
+                                  const atg_track *tracks, uint32_t n_tracks,
+                                  uint32_t channels, uint32_t bits_per_sample, void *d_out,
+                                  uint64_t out_cap, atg_alac_track_result *results,
+                                  uint32_t *frameset_bytes);
+/* the same for host buffers (staged through the device) */
+atg_status atg_alac_encode_host(atg_alac_encoder *enc, const atg_alac_options *opts,
+                                const void *pcm, atg_pcm_format format, const atg_track *tracks,
+                                uint32_t n_tracks, uint32_t channels, uint32_t bits_per_sample,
+                                uint8_t *out, uint64_t out_cap, atg_alac_track_result *results,
+                                uint32_t *frameset_bytes);
+int atg_alac_encoder_kernel_times(atg_alac_encoder *enc, const char **names, float *ms, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -38,6 +38,9 @@ EXPORTS = (
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
     "atg_replaygain_multiplier", "atg_pcm_apply_gain_device", "atg_pcm_apply_gain_host",
+    "atg_alac_last_error", "atg_alac_encoder_create", "atg_alac_encoder_destroy",
+    "atg_alac_batch_bounds", "atg_alac_encode_device", "atg_alac_encode_host",
+    "atg_alac_encoder_kernel_times",
 )
 
 CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
@@ -139,6 +142,17 @@ class RgTrack(ctypes.Structure):
 class RgResult(ctypes.Structure):
     _fields_ = [("title_gain", ctypes.c_double), ("title_peak", ctypes.c_double),
                 ("status", c_i32), ("reserved", c_u32)]
+
+
+class AlacOptions(ctypes.Structure):
+    _fields_ = [("block_size", c_u32), ("initial_history", c_u32),
+                ("history_multiplier", c_u32), ("maximum_k", c_u32)]
+
+
+class AlacTrackResult(ctypes.Structure):
+    _fields_ = [("out_offset", c_u64), ("bytes", c_u64), ("pcm_frames", c_u64),
+                ("first_frameset", c_u32), ("n_framesets", c_u32), ("status", c_i32),
+                ("reserved", c_u32)]
 
 
 class ATGError(RuntimeError):
@@ -244,6 +258,26 @@ def load_library():
         lib.atg_pcm_apply_gain_host.argtypes = [
             ctypes.c_int, P, P, c_u64, c_u32, c_u32, ctypes.c_double, c_u32, P, c_u64, c_u64]
         lib.atg_pcm_apply_gain_host.restype = ctypes.c_int
+        lib.atg_alac_last_error.restype = ctypes.c_char_p
+        lib.atg_alac_encoder_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        lib.atg_alac_encoder_create.restype = ctypes.c_int
+        lib.atg_alac_encoder_destroy.argtypes = [P]
+        lib.atg_alac_encoder_destroy.restype = None
+        lib.atg_alac_batch_bounds.argtypes = [
+            P, ctypes.POINTER(AlacOptions), ctypes.POINTER(Track), c_u32, c_u32, c_u32,
+            ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
+        lib.atg_alac_batch_bounds.restype = ctypes.c_int
+        lib.atg_alac_encode_device.argtypes = [
+            P, ctypes.POINTER(AlacOptions), P, ctypes.c_int, ctypes.POINTER(Track), c_u32,
+            c_u32, c_u32, P, c_u64, ctypes.POINTER(AlacTrackResult), P]
+        lib.atg_alac_encode_device.restype = ctypes.c_int
+        lib.atg_alac_encode_host.argtypes = [
+            P, ctypes.POINTER(AlacOptions), P, ctypes.c_int, ctypes.POINTER(Track), c_u32,
+            c_u32, c_u32, P, c_u64, ctypes.POINTER(AlacTrackResult), P]
+        lib.atg_alac_encode_host.restype = ctypes.c_int
+        lib.atg_alac_encoder_kernel_times.argtypes = [
+            P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        lib.atg_alac_encoder_kernel_times.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -480,9 +514,88 @@ class Decoder(object):
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
+class AlacEncoder(object):
+    """one libatgpu ALAC encoder (HIP stream + workspace) on one device"""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        self._check(self.lib.atg_alac_encoder_create(int(device), ctypes.byref(h)))
+        self.handle = h
+
+    def _check(self, status):
+        if status != ATG_OK:
+            raise ATGError(status, self.lib.atg_alac_last_error().decode("utf-8", "replace"))
+
+    def close(self):
+        if self.handle:
+            self.lib.atg_alac_encoder_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @staticmethod
+    def options(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14):
+        return AlacOptions(int(block_size), int(initial_history), int(history_multiplier),
+                           int(maximum_k))
+
+    def bounds(self, options, tracks, channels, bits_per_sample):
+        arr, n, _keep = _track_array(tracks)
+        nf, nb = c_u64(), c_u64()
+        self._check(self.lib.atg_alac_batch_bounds(self.handle, ctypes.byref(options), arr, n,
+                                                   channels, bits_per_sample, ctypes.byref(nf),
+                                                   ctypes.byref(nb)))
+        return nf.value, nb.value
+
+    def encode(self, options, pcm, tracks, channels, bits_per_sample):
+        """host PCM (int16 for 16-bit, int32 otherwise) -> (out bytes array,
+        [AlacTrackResult], frameset byte sizes uint32 array)"""
+        pcm = np.ascontiguousarray(pcm)
+        fmt = PCM_S16 if pcm.dtype == np.int16 else PCM_S32
+        if pcm.dtype not in (np.int16, np.int32):
+            raise TypeError("pcm must be int16 or int32")
+        tracks = list(tracks)
+        nf, nb = self.bounds(options, tracks, channels, bits_per_sample)
+        arr, n, keep = _track_array(tracks)
+        out = np.empty(max(1, nb), dtype=np.uint8)
+        res = (AlacTrackResult * max(1, n))()
+        fsb = np.zeros(max(1, nf), dtype=np.uint32)
+        self._check(self.lib.atg_alac_encode_host(
+            self.handle, ctypes.byref(options), pcm.ctypes.data_as(ctypes.c_void_p), fmt, arr,
+            n, channels, bits_per_sample, out.ctypes.data_as(ctypes.c_void_p), nb, res,
+            fsb.ctypes.data_as(ctypes.c_void_p)))
+        return out, [res[i] for i in range(n)], fsb[:nf]
+
+    def encode_device(self, options, d_pcm, fmt, tracks, channels, bits_per_sample, d_out,
+                      out_cap, frameset_bytes=None):
+        if isinstance(tracks, TrackTable):
+            arr, n = tracks.arr, tracks.n
+        else:
+            arr, n, keep = _track_array(tracks)
+        res = (AlacTrackResult * max(1, n))()
+        self._check(self.lib.atg_alac_encode_device(
+            self.handle, ctypes.byref(options), ctypes.c_void_p(d_pcm), fmt, arr, n, channels,
+            bits_per_sample, ctypes.c_void_p(d_out), out_cap, res,
+            frameset_bytes.ctypes.data_as(ctypes.c_void_p) if frameset_bytes is not None
+            else None))
+        return [res[i] for i in range(n)]
+
+    def kernel_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self.lib.atg_alac_encoder_kernel_times(self.handle, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
 _engine = None
 _engine_lock = threading.Lock()
 _decoder = None
+_alac_encoder = None
 
 
 def default_device():
@@ -508,6 +621,15 @@ def decoder():
         if _decoder is None:
             _decoder = Decoder(default_device())
         return _decoder
+
+
+def alac_encoder():
+    """process-wide ALAC encoder on ATG_DEVICE / LOCAL_RANK / device 0"""
+    global _alac_encoder
+    with _engine_lock:
+        if _alac_encoder is None:
+            _alac_encoder = AlacEncoder(default_device())
+        return _alac_encoder
 
 
 def pcm_convert(kind, pcm, channels, in_bps, out_bps=None, channel_mask=0,

@@ -23,6 +23,9 @@
 
 `encode_flac_batch` is the batch form the engine is built for: many tracks
 in one GPU pass (what track2track -j N achieves with N processes).
+
+`encode_alac` / `encode_alac_batch` do the same for ALAC (reference
+src/encoders/alac.c:30-189; GPU kernels alac_encode.hip).
 """
 
 import numpy as np
@@ -124,3 +127,62 @@ def encode_flac(filename, pcmreader, block_size, max_lpc_order,
         adaptive_mid_side, exhaustive_model_search, disable_verbatim_subframes,
         disable_constant_subframes, disable_fixed_subframes,
         disable_lpc_subframes, padding_size)[0]
+
+
+def encode_alac_batch(files, pcmreaders, block_size, initial_history, history_multiplier,
+                      maximum_k, minimum_interlacing_leftweight=0,
+                      maximum_interlacing_leftweight=4):
+    """several PCMReaders (same channels / bits) -> one mdat atom written to
+    each file object in one GPU batch; one (frame_byte_sizes,
+    total_pcm_frames) tuple per file"""
+    files = list(files)
+    pcmreaders = list(pcmreaders)
+    if len(files) != len(pcmreaders):
+        raise ValueError("files and pcmreaders differ in length")
+    if not pcmreaders:
+        return []
+    if (minimum_interlacing_leftweight, maximum_interlacing_leftweight) != (0, 4):
+        raise ValueError("interlacing leftweights other than 0..4 are not supported")
+    r0 = pcmreaders[0]
+    channels, bps = r0.channels, r0.bits_per_sample
+    if bps not in (16, 24):
+        raise ValueError("bits per sample must be 16 or 24")
+    for r in pcmreaders:
+        if (r.channels, r.bits_per_sample) != (channels, bps):
+            raise ValueError("all pcmreaders of a batch must share channels and "
+                             "bits-per-sample")
+    parts, tracks, start = [], [], 0
+    for r in pcmreaders:
+        samples, sizes = _collect(r, block_size)
+        frames = len(samples) // channels
+        tracks.append((start, frames, _frame_sizes_or_none(sizes, block_size)))
+        parts.append(samples)
+        start += frames
+    pcm = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
+    if bps <= 16:
+        pcm = pcm.astype(np.int16)
+    enc = _atgpu.alac_encoder()
+    opts = enc.options(block_size, initial_history, history_multiplier, maximum_k)
+    out, results, fsb = enc.encode(opts, pcm, tracks, channels, bps)
+    logs = []
+    for f, res in zip(files, results):
+        f.write(memoryview(out[res.out_offset:res.out_offset + res.bytes]))
+        lo = res.first_frameset
+        logs.append(([int(x) for x in fsb[lo:lo + res.n_framesets]], int(res.pcm_frames)))
+    for r in pcmreaders:
+        r.close()
+    return logs
+
+
+def encode_alac(file, pcmreader, block_size, initial_history, history_multiplier, maximum_k,
+                minimum_interlacing_leftweight=0, maximum_interlacing_leftweight=4):
+    """encode_alac(file, pcmreader, block_size, initial_history,
+    history_multiplier, maximum_k) -> ([frameset byte sizes], total PCM frames)
+
+    writes the mdat atom (size, "mdat", framesets) to the file object at
+    its position, as the reference does (src/encoders/alac.c:30-189)"""
+    if not hasattr(file, "write"):
+        raise TypeError("file must by a concrete file object")
+    return encode_alac_batch([file], [pcmreader], block_size, initial_history,
+                             history_multiplier, maximum_k, minimum_interlacing_leftweight,
+                             maximum_interlacing_leftweight)[0]
