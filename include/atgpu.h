@@ -406,6 +406,100 @@ atg_status atg_alac_encode_host(atg_alac_encoder *enc, const atg_alac_options *o
                                 uint32_t *frameset_bytes);
 int atg_alac_encoder_kernel_times(atg_alac_encoder *enc, const char **names, float *ms, int cap);
 
+/* ------------------------------------------------------------------ */
+/* ALAC decoder (D6).  Replaces the reference's                        */
+/* audiotools.decoders.ALACDecoder (src/decoders/alac.c: init          */
+/* :25-98 with parse_decoding_parameters :439-672 and seek_mdat        */
+/* :953-971, read() :183-254, read_frame :818-951, read_residuals       */
+/* :1017-1085, decode_subframe :1147-1235, decorrelate_channels         */
+/* :1237-1259, alac_order_to_wave_order :709-816) for a batch of M4A    */
+/* images.                                                             */
+/* ------------------------------------------------------------------ */
+/* status values: the reference's decoder status enum (decoders/alac.h)
+   plus the conditions its Python methods raise */
+enum {
+    ATG_AD_OK = 0,
+    ATG_AD_IO_ERROR = 1,           /* IOError ("I/O Errror" at init,
+                                      "EOF during frame reading" in read) */
+    ATG_AD_INVALID_UNUSED_BITS = 2,/* ValueError "invalid unused bits" */
+    ATG_AD_INVALID_ALAC_ATOM = 3,
+    ATG_AD_INVALID_MDHD_ATOM = 4,
+    ATG_AD_MDIA_NOT_FOUND = 5,
+    ATG_AD_STSD_NOT_FOUND = 6,
+    ATG_AD_MDHD_NOT_FOUND = 7,
+    ATG_AD_INVALID_SEEKTABLE = 8,
+    ATG_AD_NO_MDAT = 9,            /* IOError "Unable to locate 'mdat' atom" */
+    ATG_AD_CHANNEL_MISMATCH = 10   /* ValueError "channel length mismatch" */
+};
+
+/* the "alac" / "mdhd" fields the decoder keeps, and where "mdat" starts */
+typedef struct {
+    uint32_t max_samples_per_frame, bits_per_sample, history_multiplier, initial_history;
+    uint32_t maximum_k, channels, sample_rate, total_frames;
+    uint64_t mdat_offset;   /* byte (from the image start) of the first frameset */
+    uint32_t n_seekpoints;  /* entries of the stts/stsc/stco seektable */
+    uint32_t reserved;
+} atg_alac_info;
+
+typedef struct {
+    uint64_t pcm_frames_offset, file_offset;
+} atg_alac_seekpoint;
+
+/* parse_decoding_parameters + seek_mdat over an in-memory image (host):
+   returns an ATG_AD_* status.  Seekpoints (sp_cap) and the stsz frameset
+   sizes (fs_cap, a decoding hint the reference does not read) are copied
+   when the buffers are non-NULL. */
+int atg_alac_read_info(const uint8_t *data, uint64_t len, atg_alac_info *info,
+                       atg_alac_seekpoint *sp, uint32_t sp_cap, uint32_t *frame_sizes,
+                       uint32_t fs_cap, uint32_t *n_frame_sizes);
+
+/* One stream of a decode batch: the image at data[data_offset,
+   data_offset + data_bytes) (4-byte aligned); reading starts at byte
+   `start` of the image (the mdat offset, or a seekpoint's file offset) with
+   remaining_frames = `remaining`.  frameset_bytes: the stsz sizes from
+   `start` on (may be NULL: framesets are then found by the serial walk). */
+typedef struct {
+    uint64_t data_offset, data_bytes, start, remaining;
+    uint32_t max_samples_per_frame, bits_per_sample, history_multiplier, initial_history;
+    uint32_t maximum_k, channels;
+    const uint32_t *frameset_bytes;
+    uint64_t n_frameset_bytes;
+} atg_alac_dec_track;
+
+/* read() view: n_framesets framesets = pcm_frames PCM frames (interleaved
+   int32 in wave channel order at sample index sample_offset of the batch
+   output) are returned, then `status` ends the stream (0 = remaining_frames
+   reached 0). */
+typedef struct {
+    uint64_t sample_offset;
+    uint64_t pcm_frames;
+    uint32_t first_frameset;
+    uint32_t n_framesets;
+    int32_t status;
+    uint32_t channels;
+} atg_alac_dec_result;
+
+typedef struct atg_alac_decoder atg_alac_decoder;
+
+const char *atg_alac_decoder_last_error(void);
+atg_status atg_alac_decoder_create(int device, atg_alac_decoder **out);
+void atg_alac_decoder_destroy(atg_alac_decoder *dec);
+atg_status atg_alac_decode_host(atg_alac_decoder *dec, const uint8_t *data, uint64_t len,
+                                const atg_alac_dec_track *tracks, uint32_t n_tracks,
+                                atg_alac_dec_result *results, uint64_t *total_samples,
+                                uint64_t *total_framesets);
+/* the last decode's PCM and, per frameset, its PCM frames and its byte
+   offset from the image start */
+atg_status atg_alac_decode_fetch(atg_alac_decoder *dec, int32_t *pcm, uint64_t pcm_cap,
+                                 uint32_t *frameset_frames, uint64_t *frameset_offsets,
+                                 uint64_t fs_cap);
+atg_status atg_alac_decode_device(atg_alac_decoder *dec, const void *d_data, uint64_t len,
+                                  const atg_alac_dec_track *tracks, uint32_t n_tracks,
+                                  atg_alac_dec_result *results, const int32_t **d_pcm,
+                                  uint64_t *total_samples);
+int atg_alac_decoder_kernel_times(atg_alac_decoder *dec, const char **names, float *ms,
+                                  int cap);
+
 #ifdef __cplusplus
 }
 #endif

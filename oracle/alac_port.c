@@ -797,7 +797,9 @@ static void restore(int32_t *s, unsigned sample_size, const int32_t *res, unsign
         for (; i < n; i++) {
             const int base = s[i - (order + 1)];
             int residual = res[i];
-            int64_t sum = (int64_t)1 << (shift - 1);
+            /* 1 << (shift - 1) as an int shift on x86 (count masked to 5
+               bits): shift 0 gives INT_MIN, as the reference build does */
+            int64_t sum = (int64_t)(int32_t)(1u << ((shift - 1u) & 31u));
             for (unsigned j = 0; j < order; j++)
                 sum += (int64_t)coef[j] * (int64_t)(s[i - j - 1] - base);
             sum >>= shift;
@@ -917,7 +919,7 @@ int alacport_decode(const uint8_t *d, size_t len, const alacport_info *in, uint6
                     for (unsigned i = 0; i < frames_n[nchan]; i++) {
                         const int c0 = a[i], c1 = b[i];
                         int64_t t = (int64_t)(c1 * (int)lw);
-                        t >>= shift;
+                        t >>= (shift & 63u);
                         const int rs = c0 - (int)t;
                         a[i] = c1 + rs;
                         b[i] = rs;

@@ -40,7 +40,9 @@ EXPORTS = (
     "atg_replaygain_multiplier", "atg_pcm_apply_gain_device", "atg_pcm_apply_gain_host",
     "atg_alac_last_error", "atg_alac_encoder_create", "atg_alac_encoder_destroy",
     "atg_alac_batch_bounds", "atg_alac_encode_device", "atg_alac_encode_host",
-    "atg_alac_encoder_kernel_times",
+    "atg_alac_encoder_kernel_times", "atg_alac_decoder_last_error", "atg_alac_read_info",
+    "atg_alac_decoder_create", "atg_alac_decoder_destroy", "atg_alac_decode_host",
+    "atg_alac_decode_fetch", "atg_alac_decode_device", "atg_alac_decoder_kernel_times",
 )
 
 CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
@@ -153,6 +155,44 @@ class AlacTrackResult(ctypes.Structure):
     _fields_ = [("out_offset", c_u64), ("bytes", c_u64), ("pcm_frames", c_u64),
                 ("first_frameset", c_u32), ("n_framesets", c_u32), ("status", c_i32),
                 ("reserved", c_u32)]
+
+
+class AlacInfo(ctypes.Structure):
+    _fields_ = [("max_samples_per_frame", c_u32), ("bits_per_sample", c_u32),
+                ("history_multiplier", c_u32), ("initial_history", c_u32),
+                ("maximum_k", c_u32), ("channels", c_u32), ("sample_rate", c_u32),
+                ("total_frames", c_u32), ("mdat_offset", c_u64), ("n_seekpoints", c_u32),
+                ("reserved", c_u32)]
+
+
+class AlacSeekPoint(ctypes.Structure):
+    _fields_ = [("pcm_frames_offset", c_u64), ("file_offset", c_u64)]
+
+
+class AlacDecTrack(ctypes.Structure):
+    _fields_ = [("data_offset", c_u64), ("data_bytes", c_u64), ("start", c_u64),
+                ("remaining", c_u64), ("max_samples_per_frame", c_u32),
+                ("bits_per_sample", c_u32), ("history_multiplier", c_u32),
+                ("initial_history", c_u32), ("maximum_k", c_u32), ("channels", c_u32),
+                ("frameset_bytes", ctypes.POINTER(c_u32)), ("n_frameset_bytes", c_u64)]
+
+
+class AlacDecResult(ctypes.Structure):
+    _fields_ = [("sample_offset", c_u64), ("pcm_frames", c_u64), ("first_frameset", c_u32),
+                ("n_framesets", c_u32), ("status", c_i32), ("channels", c_u32)]
+
+
+# ALAC decoder status (include/atgpu.h ATG_AD_*) -> (exception, message) as
+# the reference raises them (src/decoders/alac.c alac_exception/strerror,
+# ALACDecoder_read, pcmconv.c aa_int_to_FrameList)
+AD_OK, AD_IO_ERROR, AD_NO_MDAT, AD_CHANNEL_MISMATCH = 0, 1, 9, 10
+AD_INIT_MESSAGES = {1: "I/O Errror", 2: "invalid unused bits", 3: "invalid alac atom",
+                    4: "invalid mdhd atom", 5: "mdia atom not found",
+                    6: "stsd atom not found", 7: "mdhd atom not found",
+                    8: "invalid seektable entries",
+                    9: "Unable to locate 'mdat' atom in stream"}
+AD_READ_MESSAGES = {1: "EOF during frame reading", 2: "invalid unused bits",
+                    10: "channel length mismatch"}
 
 
 class ATGError(RuntimeError):
@@ -278,6 +318,27 @@ def load_library():
         lib.atg_alac_encoder_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), ctypes.c_int]
         lib.atg_alac_encoder_kernel_times.restype = ctypes.c_int
+        lib.atg_alac_decoder_last_error.restype = ctypes.c_char_p
+        lib.atg_alac_read_info.argtypes = [ctypes.c_char_p, c_u64, ctypes.POINTER(AlacInfo), P,
+                                           c_u32, P, c_u32, ctypes.POINTER(c_u32)]
+        lib.atg_alac_read_info.restype = ctypes.c_int
+        lib.atg_alac_decoder_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
+        lib.atg_alac_decoder_create.restype = ctypes.c_int
+        lib.atg_alac_decoder_destroy.argtypes = [P]
+        lib.atg_alac_decoder_destroy.restype = None
+        lib.atg_alac_decode_host.argtypes = [
+            P, P, c_u64, ctypes.POINTER(AlacDecTrack), c_u32, ctypes.POINTER(AlacDecResult),
+            ctypes.POINTER(c_u64), ctypes.POINTER(c_u64)]
+        lib.atg_alac_decode_host.restype = ctypes.c_int
+        lib.atg_alac_decode_fetch.argtypes = [P, P, c_u64, P, P, c_u64]
+        lib.atg_alac_decode_fetch.restype = ctypes.c_int
+        lib.atg_alac_decode_device.argtypes = [
+            P, P, c_u64, ctypes.POINTER(AlacDecTrack), c_u32, ctypes.POINTER(AlacDecResult),
+            ctypes.POINTER(P), ctypes.POINTER(c_u64)]
+        lib.atg_alac_decode_device.restype = ctypes.c_int
+        lib.atg_alac_decoder_kernel_times.argtypes = [
+            P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        lib.atg_alac_decoder_kernel_times.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -592,8 +653,118 @@ class AlacEncoder(object):
         return {names[i].decode(): float(ms[i]) for i in range(k)}
 
 
+def alac_read_info(data, sp_cap=65536):
+    """parse_decoding_parameters + seek_mdat (host C in libatgpu)
+    -> (status, AlacInfo, [(pcm_frames_offset, file_offset)], stsz sizes)"""
+    lib = load_library()
+    data = bytes(data)
+    info = AlacInfo()
+    sp = (AlacSeekPoint * max(1, sp_cap))()
+    nfs = c_u32()
+    lib.atg_alac_read_info(data, len(data), ctypes.byref(info), None, 0, None, 0,
+                           ctypes.byref(nfs))
+    sizes = np.zeros(max(1, nfs.value), dtype=np.uint32)
+    st = lib.atg_alac_read_info(data, len(data), ctypes.byref(info),
+                                ctypes.cast(sp, ctypes.c_void_p), sp_cap,
+                                sizes.ctypes.data_as(ctypes.c_void_p), len(sizes),
+                                ctypes.byref(nfs))
+    pts = [(sp[i].pcm_frames_offset, sp[i].file_offset)
+           for i in range(min(info.n_seekpoints, sp_cap))]
+    return st, info, pts, sizes[:nfs.value]
+
+
+def alac_dec_track(offset, nbytes, info, start=None, remaining=None, frameset_bytes=None):
+    """AlacDecTrack for an image at `offset` of the batch buffer; keeps the
+    hint array alive on the returned object"""
+    t = AlacDecTrack()
+    t.data_offset = offset
+    t.data_bytes = nbytes
+    t.start = info.mdat_offset if start is None else start
+    t.remaining = info.total_frames if remaining is None else remaining
+    t.max_samples_per_frame = info.max_samples_per_frame
+    t.bits_per_sample = info.bits_per_sample
+    t.history_multiplier = info.history_multiplier
+    t.initial_history = info.initial_history
+    t.maximum_k = info.maximum_k
+    t.channels = info.channels
+    if frameset_bytes is not None and len(frameset_bytes):
+        hint = np.ascontiguousarray(frameset_bytes, dtype=np.uint32)
+        t._hint = hint
+        t.frameset_bytes = hint.ctypes.data_as(ctypes.POINTER(c_u32))
+        t.n_frameset_bytes = len(hint)
+    else:
+        t._hint = None
+        t.frameset_bytes = None
+        t.n_frameset_bytes = 0
+    return t
+
+
+class AlacDecoder(object):
+    """one libatgpu ALAC decoder (HIP stream + workspace) on one device"""
+
+    def __init__(self, device=0):
+        self.lib = load_library()
+        self.device = device
+        h = ctypes.c_void_p()
+        self._check(self.lib.atg_alac_decoder_create(int(device), ctypes.byref(h)))
+        self.handle = h
+
+    def _check(self, status):
+        if status != ATG_OK:
+            raise ATGError(status, self.lib.atg_alac_decoder_last_error().decode(
+                "utf-8", "replace"))
+
+    def close(self):
+        if self.handle:
+            self.lib.atg_alac_decoder_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def decode(self, data, tracks):
+        """decode a batch in host memory (images 4-byte aligned in data)
+        -> (pcm int32, [AlacDecResult], frameset frames, frameset offsets)"""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        n = len(tracks)
+        arr = (AlacDecTrack * max(1, n))(*tracks)
+        res = (AlacDecResult * max(1, n))()
+        ns, nf = c_u64(), c_u64()
+        self._check(self.lib.atg_alac_decode_host(
+            self.handle, buf.ctypes.data_as(ctypes.c_void_p), len(buf), arr, n, res,
+            ctypes.byref(ns), ctypes.byref(nf)))
+        pcm = np.empty(max(1, ns.value), dtype=np.int32)
+        ff = np.empty(max(1, nf.value), dtype=np.uint32)
+        fo = np.empty(max(1, nf.value), dtype=np.uint64)
+        self._check(self.lib.atg_alac_decode_fetch(
+            self.handle, pcm.ctypes.data_as(ctypes.c_void_p), ns.value,
+            ff.ctypes.data_as(ctypes.c_void_p), fo.ctypes.data_as(ctypes.c_void_p), nf.value))
+        return pcm[:ns.value], [res[i] for i in range(n)], ff[:nf.value], fo[:nf.value]
+
+    def decode_device(self, d_data, nbytes, tracks):
+        n = len(tracks)
+        arr = (AlacDecTrack * max(1, n))(*tracks)
+        res = (AlacDecResult * max(1, n))()
+        dp = ctypes.c_void_p()
+        ns = c_u64()
+        self._check(self.lib.atg_alac_decode_device(
+            self.handle, ctypes.c_void_p(d_data), nbytes, arr, n, res, ctypes.byref(dp),
+            ctypes.byref(ns)))
+        return [res[i] for i in range(n)], dp.value, ns.value
+
+    def kernel_times(self):
+        names = (ctypes.c_char_p * 16)()
+        ms = (ctypes.c_float * 16)()
+        k = self.lib.atg_alac_decoder_kernel_times(self.handle, names, ms, 16)
+        return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+
 _engine = None
 _engine_lock = threading.Lock()
+_alac_decoder = None
 _decoder = None
 _alac_encoder = None
 
@@ -621,6 +792,15 @@ def decoder():
         if _decoder is None:
             _decoder = Decoder(default_device())
         return _decoder
+
+
+def alac_decoder():
+    """process-wide ALAC decoder on ATG_DEVICE / LOCAL_RANK / device 0"""
+    global _alac_decoder
+    with _engine_lock:
+        if _alac_decoder is None:
+            _alac_decoder = AlacDecoder(default_device())
+        return _alac_decoder
 
 
 def alac_encoder():

@@ -36,3 +36,167 @@ __device__ __forceinline__ uint32_t alac_code_bits(uint32_t value, uint32_t k, u
     const uint32_t lsb = value - msb * m;
     return msb + 1u + (k > 1u ? (lsb > 0u ? k : k - 1u) : 0u);
 }
+
+// MSB-first bit reader over big-endian data held as 32-bit words (the image
+// is 4-byte aligned and readable to a whole word past its end); reads past
+// `end` return zeros and set `eof` (the reference longjmps: "EOF during
+// frame reading").
+struct ABitR {
+    const uint32_t *w;
+    uint64_t pos, end; // bit positions
+    bool eof;
+    __device__ __forceinline__ void init(const uint32_t *words, uint64_t bit0, uint64_t bit_end)
+    {
+        w = words;
+        pos = bit0;
+        end = bit_end;
+        eof = false;
+    }
+    // the next 32 bits at pos (zeros past end are harmless: callers check eof)
+    __device__ __forceinline__ uint32_t peek32() const
+    {
+        const uint64_t wi = pos >> 5;
+        const uint32_t sh = (uint32_t)(pos & 31u);
+        const uint32_t a = __builtin_bswap32(w[wi]);
+        const uint32_t b = __builtin_bswap32(w[wi + 1]);
+        return sh ? (a << sh) | (b >> (32u - sh)) : a;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t n) // n <= 32
+    {
+        if (!n)
+            return 0;
+        if (pos + n > end) {
+            eof = true;
+            pos = end;
+            return 0;
+        }
+        const uint32_t v = peek32() >> (32u - n);
+        pos += n;
+        return v;
+    }
+    __device__ __forceinline__ int32_t get_signed(uint32_t n)
+    {
+        const uint32_t v = get(n);
+        if (n == 0 || n >= 32)
+            return (int32_t)v;
+        return (v & (1u << (n - 1))) ? (int32_t)(v - (1u << n)) : (int32_t)v;
+    }
+    // read_limited_unary(0, 9): 1-bits before a 0, at most 9 (-1 = 9 ones)
+    __device__ __forceinline__ int32_t unary9()
+    {
+        const uint64_t avail = end > pos ? end - pos : 0;
+        const uint32_t x = peek32();
+        uint32_t ones = (uint32_t)__clz(~x); // leading ones (32 if all ones)
+        if (ones >= 9) {
+            if (avail < 9) {
+                eof = true;
+                pos = end;
+                return 0;
+            }
+            pos += 9;
+            return -1;
+        }
+        if (avail < ones + 1u) {
+            eof = true;
+            pos = end;
+            return 0;
+        }
+        pos += ones + 1u;
+        return (int32_t)ones;
+    }
+};
+
+// read_residual (decoders/alac.c:1087-1120)
+__device__ __forceinline__ uint32_t alac_read_residual(ABitR &r, uint32_t k, uint32_t ss)
+{
+    const int32_t msb = r.unary9();
+    if (r.eof)
+        return 0;
+    if (msb < 0)
+        return r.get(ss);
+    if (k == 0)
+        return (uint32_t)msb;
+    const uint32_t m = (1u << k) - 1u;
+    // read k bits; an LSB field of 0 or 1 gives one bit back (unread)
+    if (r.pos + k > r.end) {
+        // the reference reads k bits first: EOF if they are not all there
+        r.eof = true;
+        r.pos = r.end;
+        return 0;
+    }
+    const uint32_t lsb = r.peek32() >> (32u - k);
+    if (lsb > 1u) {
+        r.pos += k;
+        return (uint32_t)msb * m + (lsb - 1u);
+    }
+    r.pos += k - 1u;
+    return (uint32_t)msb * m;
+}
+
+// the decoder's LOG2 (decoders/alac.c:1006-1015): -1 for 0
+__device__ __forceinline__ int32_t alac_log2s(int32_t v)
+{
+    return v == 0 ? -1 : (v < 0 ? 31 : 31 - (int32_t)__clz((uint32_t)v));
+}
+
+// read_residuals (decoders/alac.c:1017-1085) as a generator: next() yields
+// the residuals one by one (zero runs expand inline); count() of produced
+// residuals may reach residual_count + 1 (the reference's MIN bound)
+struct AResidualReader {
+    int32_t history;
+    uint32_t sign_mod, hm, mk, ss, count;
+    int32_t i;          // the reference's loop index
+    uint32_t run_left;  // zeros still to hand out from a zero run
+    __device__ void init(uint32_t residual_count, uint32_t sample_size, uint32_t initial_history,
+                         uint32_t history_multiplier, uint32_t maximum_k)
+    {
+        history = (int32_t)initial_history;
+        sign_mod = 0;
+        hm = history_multiplier;
+        mk = maximum_k;
+        ss = sample_size;
+        count = residual_count;
+        i = 0;
+        run_left = 0;
+    }
+    // next residual; false at the end or on EOF (r.eof)
+    __device__ __forceinline__ bool next(ABitR &r, int32_t &out)
+    {
+        if (run_left) { // zeros of a zero block (the reference appends them
+            --run_left; // inside the same loop iteration)
+            out = 0;
+            return true;
+        }
+        if (i >= (int32_t)count)
+            return false;
+        int32_t kk = alac_log2s((history >> 9) + 3);
+        const uint32_t k = (uint32_t)kk < mk ? (uint32_t)kk : mk;
+        const uint32_t u = alac_read_residual(r, k, ss) + sign_mod;
+        if (r.eof)
+            return false;
+        sign_mod = 0;
+        out = (u & 1u) ? -(int32_t)((u + 1u) >> 1) : (int32_t)(u >> 1);
+        if (u > 0xFFFFu)
+            history = 0xFFFF;
+        else
+            history = (int32_t)((uint32_t)history + (u * hm - (((uint32_t)history * hm) >> 9)));
+        if (history < 128 && (i + 1) < (int32_t)count) {
+            const int32_t lz = alac_log2s(history);
+            const int32_t kz = 7 - lz + ((history + 16) / 64);
+            const uint32_t k2 = (uint32_t)kz < mk ? (uint32_t)kz : mk;
+            uint32_t z = alac_read_residual(r, k2, 16);
+            if (r.eof)
+                return false;
+            if (z > 0) {
+                const uint32_t cap = count - (uint32_t)i;
+                z = z < cap ? z : cap;
+                run_left = z;
+                i += (int32_t)z;
+            }
+            history = 0;
+            sign_mod = z <= 0xFFFFu ? 1u : 0u;
+        }
+        ++i;
+        return true;
+    }
+};

@@ -103,3 +103,139 @@ def test_encode_alac_errors():
     with pytest.raises(TypeError):
         encoders.encode_alac("not a file", audiotools.FrameListReader(x, 44100, 2, 16), 4096,
                              10, 40, 14)
+
+
+# ------------------------------------------------------------------ decoder
+def _alac_batch(images, hints=True):
+    from audiotools import _atgpu
+    tracks, parts, infos, pos = [], [], [], 0
+    for img in images:
+        st, info, _, sizes = _atgpu.alac_read_info(img)
+        infos.append((st, info))
+        if st:
+            continue
+        pad = (-len(img)) % 4
+        tracks.append(_atgpu.alac_dec_track(pos, len(img), info,
+                                            frameset_bytes=sizes if hints else None))
+        parts.append(img + b"\0" * pad)
+        pos += len(img) + pad
+    return tracks, b"".join(parts), infos
+
+
+@pytest.mark.parametrize("hints", [True, False])
+@pytest.mark.parametrize("s", G["decoder"], ids=lambda s: s["name"])
+def test_decoder_vectors_batch(s, hints):
+    """every clean / flipped / truncated image of a stream in one GPU batch:
+    same status class, same PCM bytes as the reference decoder recorded"""
+    from audiotools import _atgpu
+    x = alac_cases.enc_pcm(s)
+    mdat, fs = op.alac_encode(x, s["channels"], s["bps"])
+    img = alac_cases.dec_image(s, mdat, fs)
+    images = [alac_cases.mutate(img, c) for c in s["cases"]]
+    tracks, blob, infos = _alac_batch(images, hints)
+    pcm, res, _, _ = _atgpu.alac_decoder().decode(blob, tracks)
+    k = 0
+    for c, (st, info) in zip(s["cases"], infos):
+        if st:
+            assert c["rc"] == 1 and c["pcm_bytes"] == 0, c["name"]
+            continue
+        r = res[k]
+        k += 1
+        if r.status == _atgpu.AD_CHANNEL_MISMATCH:
+            continue  # the Python path raises; the standalone has no check
+        assert (r.status == 0) == (c["rc"] == 0), (c["name"], r.status, c["rc"])
+        got = pcm[r.sample_offset:r.sample_offset + r.pcm_frames * info.channels]
+        b = op.pcm_bytes(got, info.bits_per_sample)
+        assert len(b) == c["pcm_bytes"], c["name"]
+        assert hashlib.md5(b).hexdigest() == c["pcm_md5"], c["name"]
+        # and sample for sample the CPU oracle's walk
+        want = op.alac_decode(alac_cases.mutate(img, c))
+        assert np.array_equal(got, want["pcm"]) and (want["code"] == r.status), c["name"]
+
+
+def test_reference_fixture():
+    import os
+    from audiotools import decoders
+    f = G["fixture"]
+    fn = os.path.join(alac_cases.FIX, f["file"])
+    d = decoders.ALACDecoder(fn)
+    assert (d.channels, d.bits_per_sample, d.sample_rate, d.channel_mask) == (1, 16, 44100, 4)
+    frames = []
+    while True:
+        fl = d.read(4096)
+        if not len(fl):
+            break
+        frames.append(fl.samples)
+    assert [len(x) for x in frames] == [20, 20]
+    b = op.pcm_bytes(np.concatenate(frames), 16)
+    assert hashlib.md5(b).hexdigest() == f["pcm_md5"]
+
+
+@pytest.mark.parametrize("ch,bps", [(2, 16), (1, 24), (6, 24), (8, 16), (5, 16)])
+def test_round_trip_gpu_encode_decode(ch, bps):
+    from audiotools import decoders, m4a
+    pcms = [signals.make(k, 4096 * (2 + i) + 13 * i, ch, bps, seed=i)
+            for i, k in enumerate(["tone", "noise", "silence", "chirp"])]
+    mdats, sizes, _ = _gpu_encode(pcms, ch, bps)
+    imgs = [m4a.m4a_file(ch, bps, 44100, 4096, len(p) // ch, m, fs, create_date=3)
+            for p, m, fs in zip(pcms, mdats, sizes)]
+    out = decoders.decode_alac_batch(imgs)
+    for p, (st, info, pcm) in zip(pcms, out):
+        assert st == 0 and np.array_equal(pcm, p)
+
+
+def test_alac_audio_from_pcm_seek_and_read(tmp_path):
+    import audiotools
+    from audiotools import m4a
+    total = 44100 * 8 + 123
+    x = signals.make("tone", total, 2, 16, seed=9)
+    fn = str(tmp_path / "t.m4a")
+    a = m4a.ALACAudio.from_pcm(fn, audiotools.FrameListReader(x, 44100, 2, 16, 3),
+                               total_pcm_frames=total)
+    assert (a.channels(), a.bits_per_sample(), a.total_frames()) == (2, 16, total)
+    r = a.to_pcm()
+    got = []
+    while True:
+        fl = r.read(4096)
+        if not len(fl):
+            break
+        assert fl.frames <= 4096
+        got.append(fl.samples)
+    assert np.array_equal(np.concatenate(got), x)
+    with pytest.raises(ValueError):
+        r.seek(-1)
+    # seektable: a chunk of 5 framesets per entry (m4a.py:1342-1381)
+    assert r.seek(4096 * 7) == 4096 * 5
+    rest = []
+    while True:
+        fl = r.read(4096)
+        if not len(fl):
+            break
+        rest.append(fl.samples)
+    assert np.array_equal(np.concatenate(rest), x[2 * 4096 * 5:])
+    assert r.seek(0) == 0
+    assert np.array_equal(r.read(4096).samples, x[:2 * 4096])
+    r.close()
+    with pytest.raises(ValueError):
+        r.read(1)
+    with pytest.raises(ValueError):
+        r.seek(0)
+
+
+def test_alac_decoder_errors(tmp_path):
+    from audiotools import decoders, m4a
+    x = signals.make("noise", 4096 * 3, 2, 16, seed=2)
+    mdat, fs = op.alac_encode(x, 2, 16)
+    img = m4a.m4a_file(2, 16, 44100, 4096, 4096 * 3, mdat, fs, create_date=1)
+    fn = tmp_path / "cut.m4a"
+    fn.write_bytes(img[:-100])
+    d = decoders.ALACDecoder(str(fn))
+    d.read(4096)
+    d.read(4096)
+    with pytest.raises(IOError):
+        d.read(4096)
+    fn.write_bytes(img[:20])
+    with pytest.raises((IOError, ValueError)):
+        decoders.ALACDecoder(str(fn))
+    with pytest.raises(IOError):
+        decoders.ALACDecoder(str(tmp_path / "missing.m4a"))
