@@ -500,6 +500,57 @@ atg_status atg_alac_decode_device(atg_alac_decoder *dec, const void *d_data, uin
 int atg_alac_decoder_kernel_times(atg_alac_decoder *dec, const char **names, float *ms,
                                   int cap);
 
+/* ------------------------------------------------------------------ */
+/* Sinc resampler (R1-R3, track2track --sample-rate).  Replaces the     */
+/* reference's audiotools.pcmconverter.Resampler (src/pcmconverter.c    */
+/* :370-495: src_new(SRC_SINC_BEST_QUALITY) + src_process per 4096-frame */
+/* read, libsamplerate 0.1.8 src/samplerate/src_sinc.c) for whole       */
+/* tracks.  Coefficients: the MEDIUM table (BEST's table is absent from */
+/* the reference tree; parity is against oracle/resample_port.c).      */
+/* PCM is interleaved int32 (FrameList layout), 1..8 channels, 1..24    */
+/* bits, in and out (the output keeps bits_per_sample).                 */
+/* ------------------------------------------------------------------ */
+typedef struct {
+    uint64_t pcm_offset;  /* first frame of the track in the input buffer */
+    uint64_t pcm_frames;
+    uint32_t in_rate, out_rate;
+    /* frame counts the wrapped PCMReader's read(4096) calls returned (they
+       sum to pcm_frames; NULL = 4096-frame reads).  They can move the end
+       of the stream by one frame in rare ties (atg_resample_read_sizes). */
+    const uint32_t *reads;
+    uint64_t n_reads;
+} atg_rs_track;
+
+const char *atg_resample_last_error(void);
+/* output frames of one track read in 4096-frame reads (the converter's
+   termination rule) */
+uint64_t atg_resample_output_frames(uint64_t in_frames, uint32_t channels, uint32_t in_rate,
+                                    uint32_t out_rate);
+/* Device buffers.  Track t's output is written at frame out_offsets[t]
+   (host array, filled) of d_out, out_frames[t] frames; out_cap_samples
+   >= the sum of atg_resample_output_frames() x channels.  Returns after
+   the stream has drained. */
+atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t channels,
+                               uint32_t bits_per_sample, const int32_t *d_in, int32_t *d_out,
+                               uint64_t out_cap_samples, uint64_t *out_offsets,
+                               uint64_t *out_frames, void *stream);
+/* Host buffers (staged through the device). */
+atg_status atg_resample_host(int device, const atg_rs_track *tracks, uint32_t n,
+                             uint32_t channels, uint32_t bits_per_sample, const int32_t *in,
+                             uint64_t in_samples, int32_t *out, uint64_t out_cap_samples,
+                             uint64_t *out_offsets, uint64_t *out_frames);
+/* The frame counts successive Resampler.read() calls return (the last is
+   the 0 that ends the stream), given the frame counts the wrapped reader's
+   read(4096) calls returned (`reads`, its terminating 0 excluded).
+   Returns the number of counts (written up to cap), or -1. */
+int64_t atg_resample_read_sizes(uint64_t in_frames, uint32_t channels, uint32_t in_rate,
+                                uint32_t out_rate, const uint32_t *reads, uint64_t n_reads,
+                                uint32_t *sizes, uint64_t cap);
+/* durations (ms) of the last atg_resample_device call's kernels on the
+   calling thread's device: "rs_positions" (0 when every track had a closed
+   form) and "rs_filter" */
+int atg_resample_kernel_times(const char **names, float *ms, int cap);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,8 @@ EXPORTS = (
     "atg_alac_encoder_kernel_times", "atg_alac_decoder_last_error", "atg_alac_read_info",
     "atg_alac_decoder_create", "atg_alac_decoder_destroy", "atg_alac_decode_host",
     "atg_alac_decode_fetch", "atg_alac_decode_device", "atg_alac_decoder_kernel_times",
+    "atg_resample_last_error", "atg_resample_output_frames", "atg_resample_device",
+    "atg_resample_host", "atg_resample_read_sizes", "atg_resample_kernel_times",
 )
 
 CONV_BPS, CONV_DOWNMIX, CONV_AVERAGE = 0, 1, 2
@@ -180,6 +182,11 @@ class AlacDecTrack(ctypes.Structure):
 class AlacDecResult(ctypes.Structure):
     _fields_ = [("sample_offset", c_u64), ("pcm_frames", c_u64), ("first_frameset", c_u32),
                 ("n_framesets", c_u32), ("status", c_i32), ("channels", c_u32)]
+
+
+class RsTrack(ctypes.Structure):
+    _fields_ = [("pcm_offset", c_u64), ("pcm_frames", c_u64), ("in_rate", c_u32),
+                ("out_rate", c_u32), ("reads", ctypes.POINTER(c_u32)), ("n_reads", c_u64)]
 
 
 # ALAC decoder status (include/atgpu.h ATG_AD_*) -> (exception, message) as
@@ -339,6 +346,21 @@ def load_library():
         lib.atg_alac_decoder_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), ctypes.c_int]
         lib.atg_alac_decoder_kernel_times.restype = ctypes.c_int
+        lib.atg_resample_last_error.restype = ctypes.c_char_p
+        lib.atg_resample_output_frames.argtypes = [c_u64, c_u32, c_u32, c_u32]
+        lib.atg_resample_output_frames.restype = c_u64
+        lib.atg_resample_device.argtypes = [
+            ctypes.POINTER(RsTrack), c_u32, c_u32, c_u32, P, P, c_u64, P, P, P]
+        lib.atg_resample_device.restype = ctypes.c_int
+        lib.atg_resample_host.argtypes = [
+            ctypes.c_int, ctypes.POINTER(RsTrack), c_u32, c_u32, c_u32, P, c_u64, P, c_u64,
+            P, P]
+        lib.atg_resample_host.restype = ctypes.c_int
+        lib.atg_resample_read_sizes.argtypes = [c_u64, c_u32, c_u32, c_u32, P, c_u64, P, c_u64]
+        lib.atg_resample_read_sizes.restype = ctypes.c_int64
+        lib.atg_resample_kernel_times.argtypes = [
+            ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float), ctypes.c_int]
+        lib.atg_resample_kernel_times.restype = ctypes.c_int
         _lib = lib
         return lib
 
@@ -921,3 +943,97 @@ def apply_gain(pcm, channels, bits_per_sample, multiplier, chunk_frames, dither,
     if st != ATG_OK:
         raise ATGError(st, lib.atg_pcm_convert_last_error().decode("utf-8", "replace"))
     return out[:len(a)]
+
+
+# ------------------------------------------------------------------ resampler
+def _rs_check(lib, st):
+    if st != ATG_OK:
+        raise ATGError(st, lib.atg_resample_last_error().decode("utf-8", "replace"))
+
+
+def resample_output_frames(in_frames, channels, in_rate, out_rate):
+    return int(load_library().atg_resample_output_frames(in_frames, channels, in_rate, out_rate))
+
+
+def resample_tracks(tracks, channels):
+    """[(pcm_offset, pcm_frames, in_rate, out_rate[, reads])] -> RsTrack
+    array (reads: the upstream read() frame counts, None = 4096-frame
+    reads); the read arrays are kept alive on the returned object"""
+    arr = (RsTrack * max(1, len(tracks)))()
+    keep = []
+    for i, t in enumerate(tracks):
+        off, n, a, b = t[:4]
+        arr[i].pcm_offset, arr[i].pcm_frames = off, n
+        arr[i].in_rate, arr[i].out_rate = a, b
+        reads = t[4] if len(t) > 4 else None
+        if reads is not None:
+            r = np.ascontiguousarray(reads, dtype=np.uint32)
+            keep.append(r)
+            arr[i].reads = r.ctypes.data_as(ctypes.POINTER(c_u32))
+            arr[i].n_reads = len(r)
+    arr._keep = keep
+    return arr
+
+
+def resample_device(d_in, d_out, out_cap_samples, tracks, channels, bits_per_sample,
+                    stream=None):
+    """resample a batch whose int32 PCM is in device memory
+    -> (out frame offsets, out frame counts) numpy uint64"""
+    lib = load_library()
+    n = len(tracks)
+    arr = resample_tracks(tracks, channels)
+    offs = np.zeros(max(1, n), dtype=np.uint64)
+    cnt = np.zeros(max(1, n), dtype=np.uint64)
+    _rs_check(lib, lib.atg_resample_device(
+        arr, n, channels, bits_per_sample, ctypes.c_void_p(d_in), ctypes.c_void_p(d_out),
+        out_cap_samples, offs.ctypes.data_as(ctypes.c_void_p),
+        cnt.ctypes.data_as(ctypes.c_void_p), stream))
+    return offs[:n], cnt[:n]
+
+
+def resample_host(pcm, tracks, channels, bits_per_sample, device=None):
+    """resample int32 interleaved PCM held in host memory (atg_resample_host)
+    -> (int32 output, out frame offsets, out frame counts)"""
+    lib = load_library()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    n = len(tracks)
+    total = 0
+    for t in tracks:
+        if len(t) > 4 and t[4] is not None:
+            total += sum(resample_read_sizes(t[1], channels, t[2], t[3], t[4]))
+        else:
+            total += resample_output_frames(t[1], channels, t[2], t[3])
+    out = np.empty(max(1, total * channels), dtype=np.int32)
+    offs = np.zeros(max(1, n), dtype=np.uint64)
+    cnt = np.zeros(max(1, n), dtype=np.uint64)
+    _rs_check(lib, lib.atg_resample_host(
+        default_device() if device is None else device, resample_tracks(tracks, channels), n,
+        channels, bits_per_sample, a.ctypes.data_as(ctypes.c_void_p), len(a),
+        out.ctypes.data_as(ctypes.c_void_p), total * channels,
+        offs.ctypes.data_as(ctypes.c_void_p), cnt.ctypes.data_as(ctypes.c_void_p)))
+    return out[:total * channels], offs[:n], cnt[:n]
+
+
+def resample_read_sizes(in_frames, channels, in_rate, out_rate, reads):
+    """frame counts of successive Resampler.read() calls (the last is 0)"""
+    lib = load_library()
+    r = np.ascontiguousarray(reads, dtype=np.uint32)
+    cap = len(r) + 16
+    while True:
+        sizes = np.zeros(cap, dtype=np.uint32)
+        k = lib.atg_resample_read_sizes(in_frames, channels, in_rate, out_rate,
+                                        r.ctypes.data_as(ctypes.c_void_p), len(r),
+                                        sizes.ctypes.data_as(ctypes.c_void_p), cap)
+        if k < 0:
+            raise ValueError("invalid sample rate")
+        if k <= cap:
+            return [int(x) for x in sizes[:k]]
+        cap = int(k)
+
+
+def resample_kernel_times():
+    lib = load_library()
+    names = (ctypes.c_char_p * 4)()
+    ms = (ctypes.c_float * 4)()
+    k = lib.atg_resample_kernel_times(names, ms, 4)
+    return {names[i].decode(): float(ms[i]) for i in range(k)}

@@ -1,0 +1,752 @@
+// resample.hip — MI355X batch sinc resampler (SURVEY §8(a) rows R1–R3):
+// the reference's pcmconverter.Resampler (src/pcmconverter.c:370-495,
+// float buffers :533-629) over the vendored libsamplerate 0.1.8 sinc
+// converter (src/samplerate/src_sinc.c: sinc_*_vari_process :329-420,
+// 478-568, 1039-1128; calc_output_* :277-326, 423-475, 908-1036;
+// prepare_data :1135-1213), for a batch of tracks.
+//
+// Coefficients: the MEDIUM table the reference tree holds (src_coeffs.h,
+// tools/gen_src_coeffs.py); the reference's own choice, BEST, needs a table
+// the tree lacks, so parity is against the CPU restatement
+// oracle/resample_port.c, bit for bit, and unpinned to reference output.
+//
+// Output frame n of a track sits at input frame c_n + frac_n.  The
+// reference advances frac by 1/ratio in fp64 through fmod_one (:552-556), a
+// serial recurrence, but its arithmetic is exact in two common cases, where
+// every state is a multiple of 2^-53 and nothing rounds:
+//   * 1/ratio in [0.5, 1) with an even 53-bit numerator D (44.1k -> 48k):
+//     frac_n = (n D mod 2^53) 2^-53, c_n = floor(n D / 2^53);
+//   * an integer 1/ratio (192k -> 48k): frac_n = 0, c_n = n / ratio.
+// Those tracks need no serial pass at all; any other ratio replays the
+// fp64 recurrence in one lane per track (k_rs_positions) first.
+//
+//   k_rs_positions  lane per "serial" track: (c_n, start filter index) per
+//                   output, staged through LDS so the stores are coalesced.
+//   k_rs_filter     persistent blocks, the float table in LDS; a block takes
+//                   1024 consecutive outputs of one track, stages their
+//                   input window in LDS as float (x / 2^(bps-1)), and each
+//                   thread runs the left and right half filters of its
+//                   output (fp64 accumulation tap by tap in the reference's
+//                   order, contraction off), scale, float, then
+//                   (int)(f * 2^(bps-1)) clamped -- fb_export_frames.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/atgpu.h"
+#include "src_coeffs.h"
+
+#pragma clang fp contract(off)
+
+namespace {
+
+constexpr int kShift = 12;             // SHIFT_BITS (src_sinc.c:40)
+constexpr int kChunk = 1024;           // outputs per block iteration
+constexpr int kTable = SRC_MEDIUM_HALF_LEN + 2;
+
+enum { POS_CLOSED_FRAC = 0, POS_CLOSED_INT = 1, POS_TABLE = 2 };
+
+struct RsTrack {
+    uint64_t in_base;    // first input sample (interleaved index)
+    uint64_t in_frames;
+    uint64_t out_base;   // first output sample (interleaved index)
+    uint64_t out_frames;
+    uint64_t pos_base;   // POS_TABLE: first (c, sfi) entry
+    uint64_t D;          // POS_CLOSED_FRAC: 2^53 / ratio; POS_CLOSED_INT: 1/ratio
+    double float_increment, scale;
+    int32_t increment, mode;
+    uint64_t chunk_base; // first work chunk of the track
+};
+
+struct RsParams {
+    uint32_t ch, bps, n_tracks, n_chunks, chunk;
+    float inv_q, q;
+    int32_t lo, hi;
+};
+
+// (c_n, start_filter_index) of output n (see the file comment)
+__device__ __forceinline__ void position(const RsTrack &T, const int2 *__restrict__ pos,
+                                         uint64_t n, int64_t &c, int32_t &sfi)
+{
+    if (T.mode == POS_CLOSED_FRAC) {
+        const uint64_t lo = n * T.D, hi = __umul64hi(n, T.D);
+        c = (int64_t)((hi << 11) | (lo >> 53));
+        const uint64_t S = lo & ((1ull << 53) - 1ull);
+        const double frac = (double)S * 0x1p-53;
+        sfi = (int32_t)__double2int_rn((frac * T.float_increment) * (double)(1 << kShift));
+    } else if (T.mode == POS_CLOSED_INT) {
+        c = (int64_t)(n * T.D);
+        sfi = 0;
+    } else {
+        const int2 p = pos[T.pos_base + n];
+        c = (int64_t)(uint32_t)p.x;
+        sfi = p.y;
+    }
+}
+
+// the serial fp64 recurrence (src_sinc.c:522-556) for tracks without a
+// closed form: lane per track, 64 steps staged in LDS per flush
+__global__ __launch_bounds__(64) void k_rs_positions(const RsTrack *__restrict__ tr,
+                                                     const uint32_t *__restrict__ ids, uint32_t n,
+                                                     int2 *__restrict__ pos)
+{
+    __shared__ int2 buf[64][65];
+    const uint32_t lane = threadIdx.x;
+    const uint32_t g = blockIdx.x * 64 + lane;
+    const bool active = g < n;
+    RsTrack T;
+    if (active)
+        T = tr[ids[g]];
+    double input_index = 0.0, ratio_inv = 0.0;
+    uint64_t c = 0, total = active ? T.out_frames : 0;
+    if (active)
+        ratio_inv = __longlong_as_double((long long)T.D); // 1.0 / ratio (host double bits)
+    // every lane runs the block's longest track's steps; shorter ones idle
+    uint64_t steps = total;
+    for (int o = 32; o > 0; o >>= 1)
+        steps = max(steps, (uint64_t)__shfl_xor((unsigned long long)steps, o));
+    for (uint64_t n0 = 0; n0 < steps; n0 += 64) {
+        for (uint32_t k = 0; k < 64; ++k) {
+            const uint64_t nn = n0 + k;
+            int2 v = make_int2(0, 0);
+            if (active && nn < total) {
+                v.x = (int32_t)(uint32_t)c;
+                v.y = (int32_t)__double2int_rn((input_index * T.float_increment) *
+                                              (double)(1 << kShift));
+                input_index = input_index + ratio_inv;
+                // fmod_one (common.h:161-170) and the integer advance
+                double r = input_index - rint(input_index);
+                r = r < 0.0 ? r + 1.0 : r;
+                c += (uint64_t)(int64_t)rint(input_index - r);
+                input_index = r;
+            }
+            buf[lane][k] = v;
+        }
+        __syncthreads();
+        // flush: track j's 64 entries, one lane each -> coalesced
+        for (uint32_t j = 0; j < 64; ++j) {
+            const uint32_t gj = blockIdx.x * 64 + j;
+            if (gj >= n)
+                break;
+            const RsTrack Tj = tr[ids[gj]];
+            const uint64_t nn = n0 + lane;
+            if (nn < Tj.out_frames)
+                pos[Tj.pos_base + nn] = buf[j][lane];
+        }
+        __syncthreads();
+    }
+}
+
+template <int CH>
+__global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack *__restrict__ tr,
+                                                      const uint32_t *__restrict__ chunk_track,
+                                                      const int2 *__restrict__ pos,
+                                                      const uint32_t *__restrict__ table_bits,
+                                                      const int32_t *__restrict__ in,
+                                                      int32_t *__restrict__ out)
+{
+    extern __shared__ float lds[];
+    float *C = lds;                         // the coefficient table
+    float *X = lds + ((kTable + 3) & ~3);   // the chunk's input window
+    for (uint32_t i = threadIdx.x; i < (uint32_t)kTable; i += blockDim.x)
+        C[i] = __uint_as_float(table_bits[i]);
+    __syncthreads();
+    const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
+    for (uint32_t chunk = blockIdx.x; chunk < P.n_chunks; chunk += gridDim.x) {
+        const uint32_t t = chunk_track[chunk];
+        const RsTrack T = tr[t];
+        const uint64_t n0 = (uint64_t)(chunk - T.chunk_base) * P.chunk;
+        const uint64_t n_end = min(n0 + (uint64_t)P.chunk, T.out_frames);
+        const int32_t inc = T.increment;
+        // input window of the chunk: taps reach (max_fi / inc + 1) frames
+        // either side of the centres
+        const int64_t reach = (int64_t)(max_fi / inc) + 2;
+        int64_t c_first, c_last;
+        int32_t s_tmp;
+        position(T, pos, n0, c_first, s_tmp);
+        position(T, pos, n_end - 1, c_last, s_tmp);
+        const int64_t w0 = c_first - reach, w1 = c_last + reach + 1; // [w0, w1)
+        const uint32_t wn = (uint32_t)(w1 - w0);
+        for (uint32_t i = threadIdx.x; i < wn * CH; i += blockDim.x) {
+            const int64_t f = w0 + (int64_t)(i / CH);
+            float v = 0.0f;
+            if (f >= 0 && (uint64_t)f < T.in_frames)
+                v = (float)in[T.in_base + (uint64_t)f * CH + (i % CH)] * P.inv_q;
+            X[i] = v;
+        }
+        __syncthreads();
+        const uint64_t n = n0 + threadIdx.x;
+        if (n < n_end) {
+            int64_t c;
+            int32_t sfi;
+            position(T, pos, n, c, sfi);
+            double left[CH], right[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k)
+                left[k] = right[k] = 0.0;
+            // left half (calc_output_*: the farthest tap first)
+            int32_t fi = sfi;
+            int32_t cc = (max_fi - fi) / inc;
+            fi += cc * inc;
+            int32_t di = (int32_t)(c - cc - w0);
+            do {
+                const double fraction = (double)(fi & ((1 << kShift) - 1)) * (1.0 / 4096.0);
+                const int32_t ix = fi >> kShift;
+                const float c0 = C[ix], c1 = C[ix + 1];
+                const double icoeff = (double)c0 + fraction * (double)(c1 - c0);
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    left[k] = left[k] + icoeff * (double)X[di * CH + k];
+                fi -= inc;
+                di += 1;
+            } while (fi >= 0);
+            // right half
+            fi = inc - sfi;
+            cc = (max_fi - fi) / inc;
+            fi += cc * inc;
+            di = (int32_t)(c + 1 + cc - w0);
+            do {
+                const double fraction = (double)(fi & ((1 << kShift) - 1)) * (1.0 / 4096.0);
+                const int32_t ix = fi >> kShift;
+                const float c0 = C[ix], c1 = C[ix + 1];
+                const double icoeff = (double)c0 + fraction * (double)(c1 - c0);
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    right[k] = right[k] + icoeff * (double)X[di * CH + k];
+                fi -= inc;
+                di -= 1;
+            } while (fi > 0);
+            int32_t *o = out + T.out_base + n * CH;
+#pragma unroll
+            for (int k = 0; k < CH; ++k) {
+                const float f = (float)(T.scale * (left[k] + right[k]));
+                const float g = f * P.q;
+                // (int) of a float: truncation; x86 gives INT_MIN out of range
+                int32_t s = (g >= 2147483648.0f || g < -2147483648.0f || g != g)
+                                ? (int32_t)0x80000000
+                                : (int32_t)g;
+                o[k] = s > P.hi ? P.hi : (s < P.lo ? P.lo : s);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// ------------------------------------------------------------------ host
+thread_local std::string g_rs_err;
+
+atg_status rsfail(atg_status s, const std::string &m)
+{
+    g_rs_err = m;
+    return s;
+}
+
+#define RSHIP(expr)                                                                          \
+    do {                                                                                     \
+        hipError_t e_ = (expr);                                                              \
+        if (e_ != hipSuccess)                                                                \
+            return rsfail(ATG_ERR_DEVICE, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+double fmod_one(double x)
+{
+    double r = x - (double)std::lrint(x);
+    return r < 0.0 ? r + 1.0 : r;
+}
+
+// the per-track converter constants (sinc_set_converter + *_vari_process)
+struct Conv {
+    double ratio, float_increment, scale, terminate, inv;
+    int32_t increment;
+    int mode;
+    uint64_t D;
+    uint32_t half_frames; // half_filter_chan_len / channels
+};
+
+Conv make_conv(uint32_t in_rate, uint32_t out_rate)
+{
+    Conv v;
+    v.ratio = (double)out_rate / (double)in_rate;
+    const int index_inc = SRC_MEDIUM_INCREMENT;
+    v.float_increment = index_inc * 1.0;
+    if (v.ratio < 1.0)
+        v.float_increment = index_inc * v.ratio;
+    v.increment = (int32_t)std::lrint(v.float_increment * 4096.0);
+    v.scale = v.float_increment / index_inc;
+    v.terminate = 1.0 / v.ratio + 1e-20;
+    v.inv = 1.0 / v.ratio;
+    double count = (SRC_MEDIUM_HALF_LEN + 2.0) / index_inc;
+    if (v.ratio < 1.0)
+        count /= v.ratio;
+    v.half_frames = (uint32_t)(std::lrint(count) + 1);
+    // exact closed forms of the position recurrence (file comment)
+    const double d = v.inv;
+    v.mode = POS_TABLE;
+    v.D = 0;
+    if (d >= 0.5 && d < 1.0) {
+        const double scaled = std::ldexp(d, 53);
+        const uint64_t Di = (uint64_t)scaled;
+        if ((double)Di == scaled && (Di & 1u) == 0) {
+            v.mode = POS_CLOSED_FRAC;
+            v.D = Di;
+        }
+    } else if (d >= 1.0 && d == std::floor(d) && d < 4294967296.0) {
+        v.mode = POS_CLOSED_INT;
+        v.D = (uint64_t)d;
+    }
+    if (v.mode == POS_TABLE) {
+        uint64_t bits;
+        std::memcpy(&bits, &d, 8);
+        v.D = bits; // the serial kernel reads 1/ratio from here
+    }
+    return v;
+}
+
+// host replica of the position of output n for the closed forms
+void host_position(const Conv &v, uint64_t n, uint64_t &c, double &frac)
+{
+    if (v.mode == POS_CLOSED_FRAC) {
+        const unsigned __int128 p = (unsigned __int128)n * v.D;
+        c = (uint64_t)(p >> 53);
+        frac = std::ldexp((double)(uint64_t)(p & ((1ull << 53) - 1ull)), -53);
+    } else {
+        c = n * v.D;
+        frac = 0.0;
+    }
+}
+
+// The reference's control flow with the data left out: Resampler.read()
+// (pcmconverter.c:439-495) around src_process (samplerate.c:122-183),
+// sinc_*_vari_process (src_sinc.c:478-568) and prepare_data (:1135-1205),
+// tracking only buffer positions.  It gives the frame count of every read()
+// and the exact end of the stream: the termination test of :532-535 adds
+// the fractional position to the circular-buffer index b_current, so its
+// rounding depends on the buffer history, not just on the output index.
+struct SrcSim {
+    int64_t ch, b_len, half;
+    double inv, terminate;
+    int64_t b_current = 0, b_end = 0, b_real_end = -1;
+    double input_index = 0.0; // last_position
+
+    SrcSim(const Conv &v, uint32_t channels)
+    {
+        ch = channels;
+        const int64_t frames = std::max<int64_t>(
+            std::lrint(2.5 * SRC_MEDIUM_HALF_LEN / (SRC_MEDIUM_INCREMENT * 1.0) * 256.0), 4096);
+        b_len = frames * ch;
+        half = ch * (int64_t)v.half_frames;
+        inv = v.inv;
+        terminate = v.terminate;
+    }
+
+    // prepare_data; in_count/in_used in samples
+    void prepare(int64_t in_count, int64_t &in_used, bool eoi)
+    {
+        if (b_real_end >= 0)
+            return;
+        int64_t len;
+        if (b_current == 0) {
+            len = b_len - 2 * half;
+            b_current = b_end = half;
+        } else if (b_end + half + ch < b_len) {
+            len = std::max<int64_t>(b_len - b_current - half, 0);
+        } else {
+            len = b_end - b_current;
+            b_current = half;
+            b_end = b_current + len;
+            len = std::max<int64_t>(b_len - b_current - half, 0);
+        }
+        len = std::min(in_count - in_used, len);
+        len -= len % ch;
+        b_end += len;
+        in_used += len;
+        if (in_used == in_count && b_end - b_current < 2 * half && eoi) {
+            if (b_len - b_end < half + 5) {
+                len = b_end - b_current;
+                b_current = half;
+                b_end = b_current + len;
+            }
+            b_real_end = b_end;
+            len = half + 5;
+            if (b_end + len > b_len)
+                len = b_len - b_end;
+            b_end += len;
+        }
+    }
+
+    // one src_process call over in_frames pending frames with room for
+    // out_frames outputs -> (frames used, frames generated)
+    void process(uint64_t in_frames, uint64_t out_frames, bool eoi, uint64_t &used,
+                 uint64_t &gen)
+    {
+        const int64_t in_count = (int64_t)in_frames * ch, out_count = (int64_t)out_frames * ch;
+        int64_t in_used = 0, out_gen = 0;
+        while (out_gen < out_count) {
+            int64_t sih = (b_end - b_current + b_len) % b_len;
+            if (sih <= half) {
+                prepare(in_count, in_used, eoi);
+                sih = (b_end - b_current + b_len) % b_len;
+                if (sih <= half)
+                    break;
+            }
+            if (b_real_end >= 0 &&
+                (double)b_current + input_index + terminate >= (double)b_real_end)
+                break;
+            out_gen += ch;
+            input_index += inv;
+            const double rem = fmod_one(input_index);
+            b_current = (b_current + ch * (int64_t)std::lrint(input_index - rem)) % b_len;
+            input_index = rem;
+        }
+        used = (uint64_t)(in_used / ch);
+        gen = (uint64_t)(out_gen / ch);
+    }
+};
+
+// Resampler.read() frame counts for a source whose read(4096) calls return
+// reads[0..n_reads) (NULL: 4096-frame reads of `frames`); every count is
+// passed to `sink` (the final 0 included).  Returns the total.
+template <class Sink>
+uint64_t simulate_reads(const Conv &v, uint32_t ch, uint64_t frames, const uint32_t *reads,
+                        uint64_t n_reads, Sink sink)
+{
+    SrcSim sim(v, ch);
+    uint64_t max_frames = (uint64_t)(uint32_t)std::ceil(4096 * v.ratio);
+    uint64_t pending = 0, r = 0, fed = 0, total = 0;
+    for (;;) {
+        uint64_t out = 0;
+        bool eoi;
+        do {
+            uint64_t got;
+            if (reads)
+                got = r < n_reads ? reads[r++] : 0;
+            else
+                got = std::min<uint64_t>(4096, frames - fed);
+            fed += got;
+            pending += got;
+            eoi = pending == 0;
+            uint64_t used, gen;
+            sim.process(pending, max_frames, eoi, used, gen);
+            pending -= used;
+            if (pending > 0)
+                max_frames += max_frames;
+            out += gen;
+        } while (out == 0 && !eoi);
+        sink(out);
+        total += out;
+        if (out == 0)
+            return total;
+    }
+}
+
+// the closed-form position of output n (POS_CLOSED_*), exactly
+void host_position(const Conv &v, uint64_t n, uint64_t &c, uint64_t &S)
+{
+    if (v.mode == POS_CLOSED_FRAC) {
+        const unsigned __int128 p = (unsigned __int128)n * v.D;
+        c = (uint64_t)(p >> 53);
+        S = (uint64_t)(p & ((1ull << 53) - 1ull));
+    } else {
+        c = n * v.D;
+        S = 0;
+    }
+}
+
+// output frame count.  Closed forms: the first n with
+// ch*c_n + frac_n + 1/ratio >= ch*frames (the sequence increases), found by
+// bisection in exact integer arithmetic; when that comparison is within
+// rounding distance of a tie (the reference evaluates it in doubles on a
+// buffer-relative index), and for ratios without a closed form, the count
+// comes from the control-flow simulation.
+uint64_t output_frames(const Conv &v, uint32_t ch, uint64_t frames, const uint32_t *reads,
+                       uint64_t n_reads)
+{
+    if (v.mode == POS_TABLE)
+        return simulate_reads(v, ch, frames, reads, n_reads, [](uint64_t) {});
+    // margin(n) = ch*(frames - c_n) - (frac_n + d) in units of 2^-53 (FRAC)
+    // or of 1 (INT): terminated iff margin <= 0
+    auto margin = [&](uint64_t n) -> __int128 {
+        uint64_t c, S;
+        host_position(v, n, c, S);
+        const __int128 k = (__int128)ch * ((__int128)frames - (__int128)c);
+        if (v.mode == POS_CLOSED_FRAC)
+            return (k << 53) - (__int128)S - (__int128)v.D;
+        return k - (__int128)v.D;
+    };
+    uint64_t lo = 0, hi = (uint64_t)((double)frames * v.ratio) + 64;
+    while (margin(hi) > 0)
+        hi *= 2;
+    while (lo < hi) {
+        const uint64_t mid = lo + (hi - lo) / 2;
+        if (margin(mid) <= 0)
+            hi = mid;
+        else
+            lo = mid + 1;
+    }
+    if (v.mode == POS_CLOSED_FRAC) {
+        // the reference's sum b_current + frac + 1/ratio (b_current < b_len
+        // < 2^20) rounds by at most 2^-33: a margin within 2^-29 of zero
+        // is settled by the simulation
+        const __int128 tol = (__int128)1 << 24;
+        const __int128 m0 = margin(lo), m1 = lo ? margin(lo - 1) : tol + 1;
+        if ((m0 > -tol && m0 <= tol) || (m1 > -tol && m1 <= tol))
+            return simulate_reads(v, ch, frames, reads, n_reads, [](uint64_t) {});
+    }
+    return lo;
+}
+
+struct RsCtx {
+    void *tracks = nullptr, *chunk_track = nullptr, *pos = nullptr, *table = nullptr,
+         *ids = nullptr;
+    size_t cap_tracks = 0, cap_chunks = 0, cap_pos = 0, cap_ids = 0;
+    bool table_up = false;
+    hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
+    float ms[2] = {0.0f, 0.0f};
+};
+constexpr int kMaxDev = 64;
+RsCtx g_rs[kMaxDev];
+
+hipError_t grow(void *&p, size_t &cap, size_t bytes)
+{
+    if (p && bytes <= cap)
+        return hipSuccess;
+    if (p)
+        (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(bytes, 256);
+    hipError_t e = hipMalloc(&p, want);
+    if (e == hipSuccess)
+        cap = want;
+    return e;
+}
+
+} // namespace
+
+extern "C" {
+
+const char *atg_resample_last_error(void) { return g_rs_err.c_str(); }
+
+uint64_t atg_resample_output_frames(uint64_t in_frames, uint32_t channels, uint32_t in_rate,
+                                    uint32_t out_rate)
+{
+    if (!in_rate || !out_rate || !channels)
+        return 0;
+    return output_frames(make_conv(in_rate, out_rate), channels, in_frames, nullptr, 0);
+}
+
+atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t channels,
+                               uint32_t bits_per_sample, const int32_t *d_in, int32_t *d_out,
+                               uint64_t out_cap_samples, uint64_t *out_offsets,
+                               uint64_t *out_frames, void *stream)
+{
+    if ((!tracks && n) || !out_offsets || !out_frames)
+        return rsfail(ATG_ERR_INVALID, "NULL argument");
+    if (channels < 1 || channels > 8)
+        return rsfail(ATG_ERR_UNSUPPORTED, "channels must be 1..8");
+    if (bits_per_sample < 1 || bits_per_sample > 24)
+        return rsfail(ATG_ERR_UNSUPPORTED, "bits per sample must be 1..24");
+    hipStream_t s = (hipStream_t)stream;
+    int dev = 0;
+    RSHIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= kMaxDev)
+        return rsfail(ATG_ERR_UNSUPPORTED, "device index too large");
+    RsCtx &X = g_rs[dev];
+    std::vector<RsTrack> tr(n);
+    std::vector<uint32_t> chunk_track, serial;
+    // outputs per block iteration: the LDS holds the table plus the input
+    // window of one chunk (chunk / ratio frames plus the taps either side)
+    double min_ratio = 1e300;
+    int32_t min_inc = 1 << 30;
+    std::vector<Conv> conv(n);
+    for (uint32_t t = 0; t < n; ++t) {
+        const atg_rs_track &a = tracks[t];
+        if (!a.in_rate || !a.out_rate)
+            return rsfail(ATG_ERR_INVALID, "sample rates must be positive");
+        conv[t] = make_conv(a.in_rate, a.out_rate);
+        if (conv[t].ratio > 256.0 || conv[t].ratio < 1.0 / 256.0) // is_bad_src_ratio
+            return rsfail(ATG_ERR_INVALID, "SRC ratio outside [1/256, 256]");
+        min_ratio = std::min(min_ratio, conv[t].ratio);
+        min_inc = std::min(min_inc, conv[t].increment);
+    }
+    uint32_t chunk = kChunk;
+    size_t lds = 0;
+    for (;; chunk /= 2) {
+        const uint64_t reach = (uint64_t)((SRC_MEDIUM_HALF_LEN << kShift) / min_inc) + 2;
+        const uint64_t wn = (uint64_t)std::ceil(chunk / min_ratio) + 2 * reach + 4;
+        lds = sizeof(float) * (((kTable + 3) & ~3) + wn * channels);
+        if (lds <= 160 * 1024)
+            break;
+        if (chunk <= 64)
+            return rsfail(ATG_ERR_UNSUPPORTED, "resampling ratio too low for the LDS window");
+    }
+    uint64_t out = 0, posn = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        const atg_rs_track &a = tracks[t];
+        const Conv &v = conv[t];
+        RsTrack &T = tr[t];
+        T.in_base = a.pcm_offset * channels;
+        T.in_frames = a.pcm_frames;
+        T.out_frames = output_frames(v, channels, a.pcm_frames, a.reads, a.n_reads);
+        T.out_base = out * channels;
+        T.float_increment = v.float_increment;
+        T.scale = v.scale;
+        T.increment = v.increment;
+        T.mode = v.mode;
+        T.D = v.D;
+        T.pos_base = 0;
+        if (v.mode == POS_TABLE) {
+            T.pos_base = posn;
+            posn += T.out_frames;
+            serial.push_back(t);
+        }
+        T.chunk_base = chunk_track.size();
+        for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
+            chunk_track.push_back(t);
+        out_offsets[t] = out;
+        out_frames[t] = T.out_frames;
+        out += T.out_frames;
+    }
+    if (out * channels > out_cap_samples)
+        return rsfail(ATG_ERR_CAPACITY, "output buffer too small (atg_resample_output_frames)");
+    if (!X.table_up) {
+        RSHIP(hipMalloc(&X.table, sizeof(SRC_MEDIUM_BITS)));
+        RSHIP(hipMemcpy(X.table, SRC_MEDIUM_BITS, sizeof(SRC_MEDIUM_BITS), hipMemcpyHostToDevice));
+        for (int k = 0; k < 3; ++k)
+            RSHIP(hipEventCreate(&X.ev[k]));
+#define RS_ATTR(K)                                                                            \
+    RSHIP(hipFuncSetAttribute((const void *)k_rs_filter<K>,                                  \
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+        RS_ATTR(1) RS_ATTR(2) RS_ATTR(3) RS_ATTR(4) RS_ATTR(5) RS_ATTR(6) RS_ATTR(7) RS_ATTR(8)
+#undef RS_ATTR
+        X.table_up = true;
+    }
+    RSHIP(grow(X.tracks, X.cap_tracks, sizeof(RsTrack) * std::max<uint32_t>(n, 1)));
+    RSHIP(grow(X.chunk_track, X.cap_chunks, sizeof(uint32_t) * std::max<size_t>(chunk_track.size(), 1)));
+    RSHIP(grow(X.pos, X.cap_pos, sizeof(int2) * std::max<uint64_t>(posn, 1)));
+    RSHIP(grow(X.ids, X.cap_ids, sizeof(uint32_t) * std::max<size_t>(serial.size(), 1)));
+    if (n)
+        RSHIP(hipMemcpyAsync(X.tracks, tr.data(), sizeof(RsTrack) * n, hipMemcpyHostToDevice, s));
+    if (!chunk_track.empty())
+        RSHIP(hipMemcpyAsync(X.chunk_track, chunk_track.data(),
+                             sizeof(uint32_t) * chunk_track.size(), hipMemcpyHostToDevice, s));
+    RSHIP(hipEventRecord(X.ev[0], s));
+    if (!serial.empty()) {
+        RSHIP(hipMemcpyAsync(X.ids, serial.data(), sizeof(uint32_t) * serial.size(),
+                             hipMemcpyHostToDevice, s));
+        hipLaunchKernelGGL(k_rs_positions, dim3((unsigned)((serial.size() + 63) / 64)),
+                           dim3(64), 0, s, (const RsTrack *)X.tracks,
+                           (const uint32_t *)X.ids, (uint32_t)serial.size(), (int2 *)X.pos);
+        RSHIP(hipGetLastError());
+    }
+    RsParams P;
+    P.ch = channels;
+    P.bps = bits_per_sample;
+    P.n_tracks = n;
+    P.n_chunks = (uint32_t)chunk_track.size();
+    P.q = (float)(1u << (bits_per_sample - 1));
+    P.inv_q = 1.0f / P.q;
+    P.lo = -(int32_t)(1u << (bits_per_sample - 1));
+    P.hi = (int32_t)(1u << (bits_per_sample - 1)) - 1;
+    P.chunk = chunk;
+    RSHIP(hipEventRecord(X.ev[1], s));
+    if (P.n_chunks) {
+        const unsigned grid = std::min<uint32_t>(P.n_chunks, 256u);
+        switch (channels) {
+#define RS_CASE(K)                                                                            \
+    case K:                                                                                   \
+        hipLaunchKernelGGL(k_rs_filter<K>, dim3(grid), dim3(chunk), lds, s, P,                \
+                           (const RsTrack *)X.tracks, (const uint32_t *)X.chunk_track,        \
+                           (const int2 *)X.pos, (const uint32_t *)X.table, d_in, d_out);      \
+        break;
+            RS_CASE(1) RS_CASE(2) RS_CASE(3) RS_CASE(4) RS_CASE(5) RS_CASE(6) RS_CASE(7)
+            RS_CASE(8)
+#undef RS_CASE
+        }
+        RSHIP(hipGetLastError());
+    }
+    RSHIP(hipEventRecord(X.ev[2], s));
+    RSHIP(hipStreamSynchronize(s));
+    X.ms[0] = X.ms[1] = 0.0f;
+    (void)hipEventElapsedTime(&X.ms[0], X.ev[0], X.ev[1]);
+    (void)hipEventElapsedTime(&X.ms[1], X.ev[1], X.ev[2]);
+    return ATG_OK;
+}
+
+int atg_resample_kernel_times(const char **names, float *ms, int cap)
+{
+    static const char *kNames[2] = {"rs_positions", "rs_filter"};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDev)
+        return 0;
+    for (int k = 0; k < 2 && k < cap; ++k) {
+        if (names)
+            names[k] = kNames[k];
+        if (ms)
+            ms[k] = g_rs[dev].ms[k];
+    }
+    return 2;
+}
+
+atg_status atg_resample_host(int device, const atg_rs_track *tracks, uint32_t n,
+                             uint32_t channels, uint32_t bits_per_sample, const int32_t *in,
+                             uint64_t in_samples, int32_t *out, uint64_t out_cap_samples,
+                             uint64_t *out_offsets, uint64_t *out_frames)
+{
+    RSHIP(hipSetDevice(device));
+    if (channels < 1 || channels > 8)
+        return rsfail(ATG_ERR_UNSUPPORTED, "channels must be 1..8");
+    uint64_t total = 0;
+    for (uint32_t t = 0; t < n; ++t) {
+        if (!tracks[t].in_rate || !tracks[t].out_rate)
+            return rsfail(ATG_ERR_INVALID, "sample rates must be positive");
+        total += output_frames(make_conv(tracks[t].in_rate, tracks[t].out_rate), channels,
+                               tracks[t].pcm_frames, tracks[t].reads, tracks[t].n_reads);
+    }
+    if (total * channels > out_cap_samples)
+        return rsfail(ATG_ERR_CAPACITY, "output buffer too small (atg_resample_output_frames)");
+    int32_t *d_in = nullptr, *d_out = nullptr;
+    RSHIP(hipMalloc(&d_in, std::max<uint64_t>(in_samples, 1) * 4));
+    hipError_t e = hipMalloc(&d_out, std::max<uint64_t>(total * channels, 1) * 4);
+    if (e != hipSuccess) {
+        (void)hipFree(d_in);
+        return rsfail(ATG_ERR_NOMEM, hipGetErrorString(e));
+    }
+    atg_status st = ATG_OK;
+    if (in_samples && hipMemcpy(d_in, in, in_samples * 4, hipMemcpyHostToDevice) != hipSuccess)
+        st = rsfail(ATG_ERR_DEVICE, "hipMemcpy input");
+    if (st == ATG_OK)
+        st = atg_resample_device(tracks, n, channels, bits_per_sample, d_in, d_out,
+                                 total * channels, out_offsets, out_frames, nullptr);
+    if (st == ATG_OK && total &&
+        hipMemcpy(out, d_out, total * channels * 4, hipMemcpyDeviceToHost) != hipSuccess)
+        st = rsfail(ATG_ERR_DEVICE, "hipMemcpy output");
+    (void)hipFree(d_in);
+    (void)hipFree(d_out);
+    return st;
+}
+
+// the frame counts Resampler.read() returns, one per call (pcmconverter.c
+// :439-495 over src_process): `reads` are the frame counts the wrapped
+// reader's read(4096) calls returned
+int64_t atg_resample_read_sizes(uint64_t in_frames, uint32_t channels, uint32_t in_rate,
+                                uint32_t out_rate, const uint32_t *reads, uint64_t n_reads,
+                                uint32_t *sizes, uint64_t cap)
+{
+    if (!in_rate || !out_rate || !channels || channels > 8)
+        return -1;
+    const Conv v = make_conv(in_rate, out_rate);
+    int64_t k = 0;
+    simulate_reads(v, channels, in_frames, reads, n_reads, [&](uint64_t n) {
+        if (sizes && (uint64_t)k < cap)
+            sizes[k] = (uint32_t)n;
+        ++k;
+    });
+    return k;
+}
+
+} // extern "C"

@@ -510,3 +510,44 @@ def ref_alac_decode(m4a_bytes):
         open(fn, "wb").write(m4a_bytes)
         p = subprocess.run([REF_ALACDEC, fn], capture_output=True)
         return p.returncode, p.stdout, p.stderr.decode("latin-1")
+
+
+# --- Resampler (oracle/resample_port.c; parity unpinned, see its header) ---
+def resample(pcm, channels, bps, ratio, reads=None, return_sizes=False):
+    """Resampler(reader, rate) read to the end, libsamplerate sinc (MEDIUM
+    table) over int32 interleaved PCM; reads = the wrapped reader's read()
+    frame counts (None: 4096-frame reads) -> int32 interleaved output
+    [, frame count of every read() including the final 0]"""
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    frames = len(a) // channels
+    P, L = ctypes.c_void_p, ctypes.c_long
+    lib.rsport_resample.argtypes = [P, L, ctypes.c_int, ctypes.c_int, ctypes.c_double, P, L,
+                                    P, L, P, L, ctypes.POINTER(L)]
+    lib.rsport_resample.restype = L
+    cap = int(frames * ratio) + 64
+    out = np.zeros(max(1, cap * channels), dtype=np.int32)
+    r = None if reads is None else np.ascontiguousarray(reads, dtype=np.uint32)
+    scap = (len(r) if r is not None else frames // 4096 + 1) + 64
+    sizes = np.zeros(scap, dtype=np.uint32)
+    ns = L()
+    n = lib.rsport_resample(a.ctypes.data, frames, channels, bps, ratio,
+                            None if r is None else r.ctypes.data, 0 if r is None else len(r),
+                            out.ctypes.data, cap, sizes.ctypes.data, scap, ctypes.byref(ns))
+    assert 0 <= n <= cap and ns.value <= scap
+    if return_sizes:
+        return out[:n * channels], [int(x) for x in sizes[:ns.value]]
+    return out[:n * channels]
+
+
+def resample_positions(n_out, ratio):
+    """-> (center frames uint32, start filter indices int32) of the first
+    n_out outputs (the fp64 position recurrence)"""
+    lib = load()
+    P = ctypes.c_void_p
+    lib.rsport_positions.argtypes = [c_u64, ctypes.c_double, P, P]
+    lib.rsport_positions.restype = c_u64
+    c = np.zeros(max(1, n_out), dtype=np.uint32)
+    s = np.zeros(max(1, n_out), dtype=np.int32)
+    lib.rsport_positions(n_out, ratio, c.ctypes.data, s.ctypes.data)
+    return c[:n_out], s[:n_out]
