@@ -44,6 +44,8 @@ METRIC = "FLAC-8 encode frames/s (4096-sample 44.1k stereo) at 1/2/4/8 GPUs; bit
 BLOCK = 4096
 PCM_BYTES_PER_FRAME = BLOCK * 2 * 2
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s (spec)
+F64_PEAK_TFLOPS = 78.6         # MI355X FP64 vector, AMD spec (= half the 157.3 TF FP32 vector
+                               # peak of MI355X_MICROARCH.md; the guide lists no f64 row)
 # integer VALU issue peak: 256 CUs x 4 SIMDs, one wave64 VALU instruction
 # per 2 cycles per SIMD (MI355X_MICROARCH.md "Wave scheduling"), 2.4 GHz
 N_SIMD = 1024
@@ -73,6 +75,10 @@ def parse_args(argv=None):
                     help="tracks the reference encoder baseline encodes")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--chain-tracks", type=int, default=64,
+                    help="config-5 chain leg: 192 kHz 5.1 tracks per GPU")
+    ap.add_argument("--chain-seconds", type=int, default=10)
+    ap.add_argument("--no-chain", action="store_true")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -375,6 +381,267 @@ def convert_leg(args, torch, device, pcm):
             "verified_dither_invariant": ok}
 
 
+def resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier, threads, verify):
+    """BASELINE config 3: 44.1 kHz -> 48 kHz sinc resample (resample.hip,
+    SURVEY 8(a) R1-R3) + 24 -> 16-bit dither (pcm_convert.hip R4) of every
+    track of the batch, 24-bit stereo in HBM.  Every resampled sample of
+    every track is compared with the CPU restatement oracle/resample_port.c
+    (parity unpinned to reference output: BEST table absent), outside the
+    timed region.  Returns the JSON object."""
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    n_in = args.frames * BLOCK
+    x16 = pcm.to(torch.int32)
+    x = x16 * 256 + ((x16 * 73 + 41) & 255)  # 24-bit: the signal plus low bits
+    del x16
+    tracks = [(t * n_in, n_in, 44100, 48000) for t in range(n_tracks)]
+    n_out = _atgpu.resample_output_frames(n_in, 2, 44100, 48000)
+    total = n_out * n_tracks
+    y = torch.empty(total * 2, dtype=torch.int32, device=device)
+    z = torch.empty_like(y)
+    dither = torch.randint(0, 256, ((total * 2 + 7) // 8,), dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+
+    def step():
+        _atgpu.resample_device(x.data_ptr(), y.data_ptr(), total * 2, tracks, 2, 24, stream)
+        st = lib.atg_pcm_convert_device(_atgpu.CONV_BPS, y.data_ptr(), z.data_ptr(), total, 2,
+                                        0, 24, 16, dither.data_ptr(), 0, stream)
+        if st != _atgpu.ATG_OK:
+            raise RuntimeError(lib.atg_pcm_convert_last_error())
+
+    for _ in range(args.warmup):
+        step()
+    kt_sum = {}
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        for k, v in _atgpu.resample_kernel_times().items():
+            kt_sum[k] = kt_sum.get(k, 0.0) + v
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, device)
+    kt = {k: v / args.steps for k, v in kt_sum.items()}
+    dither_ok = bool((((z ^ (y >> 8)) & ~1) == 0).all().item())
+    # fp64 roofline of the filter: the reference's arithmetic per output
+    # frame is (taps) x (2 flops to interpolate the coefficient + 2 per
+    # channel to accumulate); taps = 2 x half_len x 4096 / increment on
+    # average (45.70 per side at 44.1k -> 48k)
+    taps = 2.0 * 22437 * 4096 / (491 * 4096)
+    flops = total * taps * (2 + 2 * 2)
+    f_ms = kt.get("rs_filter", 0.0)
+    achieved = flops / (f_ms / 1e3) / 1e12 if f_ms else None
+    hbm = (n_tracks * n_in + total) * 2 * 4
+    out = {"metric": "44.1k->48k sinc resample + 24->16 dither, output frames/s (config 3)",
+           "value": round(total * world * args.steps / elapsed, 1), "unit": "frames/s",
+           "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "realtime_x": round(n_tracks * world * n_in / 44100.0 / (elapsed / args.steps), 1),
+           "config": {"tracks_per_gpu": n_tracks, "input_frames_per_track": n_in,
+                      "output_frames_per_track": n_out, "channels": 2, "bits": "24 -> 16",
+                      "coefficients": "libsamplerate MEDIUM (BEST table absent from the "
+                                      "reference tree)"},
+           "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+           "roofline": {"bound": "f64-valu", "kernel": "rs_filter",
+                        "achieved": round(achieved, 3) if achieved else None,
+                        "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                        "frac": round(achieved / F64_PEAK_TFLOPS, 4) if achieved else None,
+                        "alg_flops_per_launch": flops, "launch_ms": round(f_ms, 4),
+                        "hbm_alg_bytes": hbm,
+                        "hbm_frac": round(hbm / (f_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
+                        if f_ms else None},
+           "verified_dither_invariant": dither_ok}
+    if verify:
+        import oracle_port
+        oracle_port.load()
+        yh = y.cpu().numpy()
+        xh = x.cpu().numpy()
+        bad = []
+
+        def one(t):
+            want = oracle_port.resample(xh[t * n_in * 2:(t + 1) * n_in * 2], 2, 24,
+                                        48000 / 44100.0)
+            if not np.array_equal(want, yh[t * n_out * 2:(t + 1) * n_out * 2]):
+                bad.append(t)
+
+        dt = _parallel(n_tracks, threads, one)
+        out["verified_vs_oracle"] = not bad
+        out["verified_tracks"] = n_tracks - len(bad)
+        t1 = min(2, n_tracks)
+        dt1 = _parallel(t1, 1, one)
+        out["cpu_baseline"] = {
+            "value": round(t1 * n_out / dt1, 1), "unit": "frames/s", "cores": 1,
+            "kind": "port", "sample": "oracle/resample_port.c on %d tracks, 1 thread, %.1f s"
+                                      % (t1, dt1),
+            "n_threads": {"value": round(n_tracks * n_out / dt, 1), "cores": threads,
+                          "sample": "all %d tracks, %d threads, %.1f s"
+                                    % (n_tracks, threads, dt)}}
+        del yh, xh
+    del x, y, z, dither
+    return out
+
+
+def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
+    """BASELINE config 5, the track2track chain: ALAC (192 kHz / 24-bit /
+    5.1) decode -> 48 kHz sinc resample -> FLAC-8 encode, all three on the
+    GPU with the data left in HBM between stages (alac_decode.hip ->
+    resample.hip -> the FLAC encoder).  The ALAC input is made once, untimed,
+    by the GPU ALAC encoder from synthetic PCM.  Checks outside the timed
+    region: every decoded sample equals the source (lossless); the first
+    tracks' resampled PCM vs oracle/resample_port.c and FLAC images vs the
+    FLAC port, bit for bit."""
+    from audiotools import _atgpu
+    ch, rin, rout, bps = 6, 192000, 48000, 24
+    n_tracks, n_in = args.chain_tracks, args.chain_seconds * rin
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    g = torch.Generator(device=device)
+    g.manual_seed(11 + int(os.environ.get("RANK", "0")))
+    t = torch.arange(n_in, device=device, dtype=torch.float64)
+    src = torch.empty((n_tracks, n_in, ch), dtype=torch.int32, device=device)
+    for k in range(n_tracks):
+        f = (110.0 + 37.0 * k + 55.0 * torch.arange(ch, device=device, dtype=torch.float64))
+        tone = torch.sin(2 * np.pi * t[:, None] * f[None, :] / rin) * (3e6 + 1e5 * k)
+        noise = torch.randint(-4096, 4096, (n_in, ch), device=device, generator=g,
+                              dtype=torch.int32)
+        src[k] = tone.to(torch.int32) + noise
+    del t
+    src = src.reshape(-1)
+    # ALAC input (untimed): one mdat atom per track, framesets from the encoder
+    aenc = _atgpu.AlacEncoder(local)
+    aopts = aenc.options()
+    atracks = [(k * n_in, n_in) for k in range(n_tracks)]
+    n_fs, acap = aenc.bounds(aopts, atracks, ch, bps)
+    alac = torch.zeros(acap, dtype=torch.uint8, device=device)
+    fsb = np.zeros(max(1, n_fs), dtype=np.uint32)
+    ares = aenc.encode_device(aopts, src.data_ptr(), _atgpu.PCM_S32, atracks, ch, bps,
+                              alac.data_ptr(), acap, fsb)
+    aenc.close()
+    info = _atgpu.AlacInfo()
+    info.max_samples_per_frame, info.bits_per_sample = 4096, bps
+    info.history_multiplier, info.initial_history, info.maximum_k = 40, 10, 14
+    info.channels, info.sample_rate, info.total_frames = ch, rin, n_in
+    dtracks = []
+    for r in ares:
+        dtracks.append(_atgpu.alac_dec_track(
+            r.out_offset, r.bytes, info, start=8, remaining=n_in,
+            frameset_bytes=fsb[r.first_frameset:r.first_frameset + r.n_framesets]))
+    alac_bytes = sum(int(r.bytes) for r in ares)
+    nbytes = max(int(r.out_offset + r.bytes) for r in ares)
+    adec = _atgpu.AlacDecoder(local)
+    rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
+    n_out = _atgpu.resample_output_frames(n_in, ch, rin, rout)
+    y = torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device)
+    eng = _atgpu.Engine(local)
+    fopts = _atgpu.make_options(**FLAC8)
+    ftracks = [(k * n_out, n_out) for k in range(n_tracks)]
+    n_flac, fcap = eng.bounds(fopts, ftracks, ch, bps)
+    ftable = _atgpu.TrackTable(ftracks)
+    flac = torch.empty(fcap, dtype=torch.uint8, device=device)
+    stream = torch.cuda.current_stream(device).cuda_stream
+    state = {}
+
+    def step():
+        dres, d_pcm, nsamp = adec.decode_device(alac.data_ptr(), nbytes, dtracks)
+        _atgpu.resample_device(d_pcm, y.data_ptr(), y.numel(), rtracks, ch, bps, stream)
+        fres = eng.encode_device(fopts, y.data_ptr(), _atgpu.PCM_S32, ftable, ch, bps, rout,
+                                 flac.data_ptr(), fcap)
+        state.update(dres=dres, d_pcm=d_pcm, nsamp=nsamp, fres=fres)
+
+    for _ in range(args.warmup):
+        step()
+    kt = {}
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        for pre, d in (("alac_", {k: v for k, v in adec.kernel_times().items()}),
+                       ("", _atgpu.resample_kernel_times()), ("flac_", eng.kernel_times())):
+            for k, v in d.items():
+                key = k if k.startswith(pre) else pre + k
+                kt[key] = kt.get(key, 0.0) + v / args.steps
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, device)
+    dres, fres = state["dres"], state["fres"]
+    dec_ok = all(r.status == 0 and r.pcm_frames == n_in for r in dres) and \
+        state["nsamp"] == src.numel()
+    lossless = dec_ok and _device_equal(torch, state["d_pcm"], src)
+    flac_bytes = sum(int(r.bytes) for r in fres)
+    out = {"metric": "config 5 track2track chain: ALAC 192k/24-bit 5.1 decode -> 48k resample "
+                     "-> FLAC-8, output frames/s (48 kHz PCM frames)",
+           "value": round(n_out * n_tracks * world * args.steps / elapsed, 1),
+           "unit": "frames/s", "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "flac_frames_per_s": round(n_flac * world * args.steps / elapsed, 1),
+           "realtime_x": round(n_tracks * world * args.chain_seconds / (elapsed / args.steps), 1),
+           "config": {"tracks_per_gpu": n_tracks, "seconds_per_track": args.chain_seconds,
+                      "channels": ch, "bits": bps, "rates": "%d -> %d" % (rin, rout),
+                      "alac_bytes": alac_bytes, "flac_bytes": flac_bytes,
+                      "flac_frames": n_flac},
+           "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
+           "verified_alac_lossless": bool(dec_ok and lossless)}
+    if verify:
+        import oracle_port
+        oracle_port.load()
+        yh = y[:2 * n_out * ch].cpu().numpy()
+        sh = src[:2 * n_in * ch].cpu().numpy()
+        fh = flac.cpu().numpy()
+        rs_ok = fl_ok = True
+        t_rs = t_fl = 0.0
+        for k in range(min(2, n_tracks)):
+            t1 = time.perf_counter()
+            want = oracle_port.resample(sh[k * n_in * ch:(k + 1) * n_in * ch], ch, bps, rout / rin)
+            t_rs += time.perf_counter() - t1
+            rs_ok = rs_ok and np.array_equal(want, yh[k * n_out * ch:(k + 1) * n_out * ch])
+            t1 = time.perf_counter()
+            img, _ = oracle_port.encode(want, ch, bps, rout, **FLAC8)
+            t_fl += time.perf_counter() - t1
+            r = fres[k]
+            fl_ok = fl_ok and img == fh[r.out_offset:r.out_offset + r.bytes].tobytes()
+        k = min(2, n_tracks)
+        alac_h = alac.cpu().numpy()
+        ainfo = oracle_port.AlacInfo()
+        for f in ("max_samples_per_frame", "bits_per_sample", "history_multiplier",
+                  "initial_history", "maximum_k", "channels", "sample_rate", "total_frames"):
+            setattr(ainfo, f, getattr(info, f))
+        al_ok = True
+        t1 = time.perf_counter()
+        for j in range(k):
+            r = ares[j]
+            d = oracle_port.alac_decode(alac_h[r.out_offset:r.out_offset + r.bytes].tobytes(),
+                                        info=ainfo, start=8, remaining=n_in)
+            al_ok = al_ok and d["code"] == 0 and np.array_equal(
+                d["pcm"], sh[j * n_in * ch:(j + 1) * n_in * ch])
+        t_al = time.perf_counter() - t1
+        out["verified_alac_port_decode"] = al_ok
+        out["verified_resample_vs_oracle"] = rs_ok
+        out["verified_flac_vs_port"] = fl_ok
+        out["verified_tracks"] = k
+        out["cpu_baseline"] = {
+            "value": round(k * n_out / (t_rs + t_fl + t_al), 1), "unit": "frames/s",
+            "cores": 1, "kind": "port",
+            "sample": "%d tracks through the CPU restatements, 1 thread: resample %.1f s + "
+                      "FLAC-8 %.1f s + ALAC decode %.1f s" % (k, t_rs, t_fl, t_al)}
+        del yh, sh, fh, alac_h
+    adec.close()
+    eng.close()
+    del src, alac, y, flac
+    return out
+
+
+def _device_equal(torch, d_ptr, ref):
+    """compare n int32 at device address d_ptr with the tensor ref (on its
+    device) without a host copy"""
+    import ctypes
+    got = torch.empty_like(ref)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if hip.hipMemcpy(ctypes.c_void_p(got.data_ptr()), ctypes.c_void_p(d_ptr),
+                     ref.numel() * 4, 3) != 0:
+        return False
+    return bool(torch.equal(got, ref))
+
+
 def album_reduce(dist, world, hist, peak):
     """an album spread over ranks: SUM of the uint32 window histograms (held
     as int32; two's-complement sums are the same bits) and MAX of the peak,
@@ -580,12 +847,18 @@ def main(argv=None):
                           % (n_tracks, args.frames, threads, port_dt)}
         del want
 
-    decode = convert = rg = rg_res = None
+    decode = convert = rg = rg_res = resample = None
     if not args.no_decode:
         decode = decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host,
                             n_frames, barrier)
         if rank == 0:
             convert = convert_leg(args, torch, device, pcm)
+        resample = resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier,
+                                threads, rank == 0 and not args.no_verify)
+    chain = None
+    if not args.no_chain:
+        chain = chain_leg(args, torch, dist, world, device, barrier, threads,
+                          rank == 0 and not args.no_verify)
         rg, rg_res = replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks,
                                     barrier)
 
@@ -703,6 +976,8 @@ def main(argv=None):
         "decode": decode,
         "convert": convert,
         "replaygain": rg,
+        "resample": resample,
+        "chain": chain,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -32,6 +32,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <numeric>
 #include <cmath>
 #include <cstring>
 #include <string>
@@ -59,7 +60,10 @@ struct RsTrack {
     uint64_t D;          // POS_CLOSED_FRAC: 2^53 / ratio; POS_CLOSED_INT: 1/ratio
     double float_increment, scale;
     int32_t increment, mode;
-    uint64_t chunk_base; // first work chunk of the track
+    uint64_t chunk_base; // first work chunk of the track (k_rs_filter)
+    uint64_t span;       // k_rs_phase: outputs per task (64 x period x rows)
+    uint32_t period;     // k_rs_phase: outputs per phase cycle (out_rate / gcd)
+    uint32_t pad;
 };
 
 struct RsParams {
@@ -141,7 +145,38 @@ __global__ __launch_bounds__(64) void k_rs_positions(const RsTrack *__restrict__
     }
 }
 
-template <int CH>
+// one half filter of calc_output_* (src_sinc.c:423-475): taps from the
+// farthest in, while fi >= 0 (left) or fi > 0 (right), data index di
+// stepping by +1 (left) or -1 (right) frames; the tap count is known up
+// front, so the loop is counted and unrolled for ILP.  HOIST: the increment
+// is a multiple of 4096 (ratio >= 1), so every tap of the half shares one
+// interpolation fraction.  The coefficient c0 + fraction * (c1 - c0) is a
+// fused multiply-add: fraction (12 bits) times the float difference (24
+// bits) is exact in fp64, so the FMA rounds once exactly where the
+// reference's separate multiply and add do.
+template <int CH, bool LEFT, bool HOIST, typename XT>
+__device__ __forceinline__ void half_filter(const float *__restrict__ C, const XT *__restrict__ X,
+                                            int32_t fi, int32_t inc, int32_t di,
+                                            double (&acc)[CH])
+{
+    constexpr int32_t kMask = (1 << kShift) - 1;
+    const double hfrac = (double)(fi & kMask) * (1.0 / 4096.0);
+    const int32_t taps = LEFT ? fi / inc + 1 : (fi - 1) / inc + 1;
+#pragma unroll 4
+    for (int32_t j = 0; j < taps; ++j) {
+        const double fraction = HOIST ? hfrac : (double)(fi & kMask) * (1.0 / 4096.0);
+        const int32_t ix = fi >> kShift;
+        const float c0 = C[ix], c1 = C[ix + 1];
+        const double icoeff = __builtin_fma(fraction, (double)(c1 - c0), (double)c0);
+#pragma unroll
+        for (int k = 0; k < CH; ++k)
+            acc[k] = acc[k] + icoeff * (double)X[di * CH + k];
+        fi -= inc;
+        di += LEFT ? 1 : -1;
+    }
+}
+
+template <int CH, bool HOIST, typename XT>
 __global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack *__restrict__ tr,
                                                       const uint32_t *__restrict__ chunk_track,
                                                       const int2 *__restrict__ pos,
@@ -149,9 +184,9 @@ __global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack 
                                                       const int32_t *__restrict__ in,
                                                       int32_t *__restrict__ out)
 {
-    extern __shared__ float lds[];
-    float *C = lds;                         // the coefficient table
-    float *X = lds + ((kTable + 3) & ~3);   // the chunk's input window
+    extern __shared__ double lds_d[];
+    float *C = reinterpret_cast<float *>(lds_d);                    // the coefficient table
+    XT *X = reinterpret_cast<XT *>(lds_d + (((kTable + 3) & ~3) / 2)); // the chunk's input window
     for (uint32_t i = threadIdx.x; i < (uint32_t)kTable; i += blockDim.x)
         C[i] = __uint_as_float(table_bits[i]);
     __syncthreads();
@@ -176,7 +211,7 @@ __global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack 
             float v = 0.0f;
             if (f >= 0 && (uint64_t)f < T.in_frames)
                 v = (float)in[T.in_base + (uint64_t)f * CH + (i % CH)] * P.inv_q;
-            X[i] = v;
+            X[i] = (XT)v;
         }
         __syncthreads();
         const uint64_t n = n0 + threadIdx.x;
@@ -188,38 +223,12 @@ __global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack 
 #pragma unroll
             for (int k = 0; k < CH; ++k)
                 left[k] = right[k] = 0.0;
-            // left half (calc_output_*: the farthest tap first)
-            int32_t fi = sfi;
-            int32_t cc = (max_fi - fi) / inc;
-            fi += cc * inc;
-            int32_t di = (int32_t)(c - cc - w0);
-            do {
-                const double fraction = (double)(fi & ((1 << kShift) - 1)) * (1.0 / 4096.0);
-                const int32_t ix = fi >> kShift;
-                const float c0 = C[ix], c1 = C[ix + 1];
-                const double icoeff = (double)c0 + fraction * (double)(c1 - c0);
-#pragma unroll
-                for (int k = 0; k < CH; ++k)
-                    left[k] = left[k] + icoeff * (double)X[di * CH + k];
-                fi -= inc;
-                di += 1;
-            } while (fi >= 0);
-            // right half
-            fi = inc - sfi;
-            cc = (max_fi - fi) / inc;
-            fi += cc * inc;
-            di = (int32_t)(c + 1 + cc - w0);
-            do {
-                const double fraction = (double)(fi & ((1 << kShift) - 1)) * (1.0 / 4096.0);
-                const int32_t ix = fi >> kShift;
-                const float c0 = C[ix], c1 = C[ix + 1];
-                const double icoeff = (double)c0 + fraction * (double)(c1 - c0);
-#pragma unroll
-                for (int k = 0; k < CH; ++k)
-                    right[k] = right[k] + icoeff * (double)X[di * CH + k];
-                fi -= inc;
-                di -= 1;
-            } while (fi > 0);
+            int32_t cc = (max_fi - sfi) / inc;
+            half_filter<CH, true, HOIST>(C, X, sfi + cc * inc, inc, (int32_t)(c - cc - w0), left);
+            const int32_t fr = inc - sfi;
+            cc = (max_fi - fr) / inc;
+            half_filter<CH, false, HOIST>(C, X, fr + cc * inc, inc, (int32_t)(c + 1 + cc - w0),
+                                          right);
             int32_t *o = out + T.out_base + n * CH;
 #pragma unroll
             for (int k = 0; k < CH; ++k) {
@@ -230,6 +239,143 @@ __global__ __launch_bounds__(kChunk) void k_rs_filter(RsParams P, const RsTrack 
                                 ? (int32_t)0x80000000
                                 : (int32_t)g;
                 o[k] = s > P.hi ? P.hi : (s < P.lo ? P.lo : s);
+            }
+        }
+        __syncthreads();
+    }
+}
+
+// c0 + fraction * (c1 - c0) of filter index fi from the float table
+__device__ __forceinline__ double interp_coeff(const float *__restrict__ C, int32_t fi)
+{
+    const double fraction = (double)(fi & ((1 << kShift) - 1)) * (1.0 / 4096.0);
+    const int32_t ix = fi >> kShift;
+    const float c0 = C[ix], c1 = C[ix + 1];
+    return __builtin_fma(fraction, (double)(c1 - c0), (double)c0);
+}
+
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// The phase-sharing filter.  The output positions of a rational ratio
+// repeat their fractional part every `period` = out_rate / gcd outputs, so
+// outputs n, n + period, n + 2 period, ... have the same start filter index
+// and the same interpolated coefficients.  A wave takes 64 such outputs (one
+// per lane, input frames `period / ratio` apart): the lanes compute the
+// row's coefficients once, tap j in lane j % 64, into a per-wave LDS list,
+// and every tap then costs a broadcast LDS read of the coefficient, a read
+// of the lane's input sample and one multiply + add per channel.  A task is
+// 64 x period x rows consecutive outputs of one track, whose input window is
+// staged in LDS as float x / 2^(bps-1).  Each lane still computes its own
+// exact position; a row whose lanes disagree on the start index (the fp64
+// recurrence drifting across a rounding boundary) takes the per-lane path
+// with the coefficients read from the global table.
+template <int CH>
+__global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__restrict__ tr,
+                                                   const uint2 *__restrict__ tasks,
+                                                   uint32_t n_tasks, const int2 *__restrict__ pos,
+                                                   const uint32_t *__restrict__ table_bits,
+                                                   const int32_t *__restrict__ in,
+                                                   int32_t *__restrict__ out, uint32_t tmax)
+{
+    extern __shared__ double lds_d[];
+    const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
+    double *coefL = lds_d + (size_t)wave * 2 * tmax;
+    double *coefR = coefL + tmax;
+    float *X = reinterpret_cast<float *>(lds_d + (size_t)nwaves * 2 * tmax);
+    const float *Cg = reinterpret_cast<const float *>(table_bits);
+    const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
+    for (uint32_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
+        const uint2 tk = tasks[task];
+        const RsTrack T = tr[tk.x];
+        const uint64_t B0 = (uint64_t)tk.y * T.span;
+        const uint64_t Bend = min(B0 + T.span, T.out_frames);
+        const int32_t inc = T.increment;
+        const int64_t reach = (int64_t)(max_fi / inc) + 2;
+        int64_t c_first, c_last;
+        int32_t s_tmp;
+        position(T, pos, B0, c_first, s_tmp);
+        position(T, pos, Bend - 1, c_last, s_tmp);
+        const int64_t w0 = c_first - reach;
+        const uint32_t wn = (uint32_t)(c_last + reach + 1 - w0);
+        for (uint32_t i = threadIdx.x; i < wn * CH; i += blockDim.x) {
+            const int64_t f = w0 + (int64_t)(i / CH);
+            float v = 0.0f;
+            if (f >= 0 && (uint64_t)f < T.in_frames)
+                v = (float)in[T.in_base + (uint64_t)f * CH + (i % CH)] * P.inv_q;
+            X[i] = v;
+        }
+        __syncthreads();
+        const uint32_t per = T.period;
+        const uint64_t row_len = 64ull * per;
+        const uint32_t rows = (uint32_t)((Bend - B0 + row_len - 1) / row_len);
+        for (uint32_t tr_i = wave; tr_i < rows * per; tr_i += nwaves) {
+            const uint64_t base = B0 + (uint64_t)(tr_i / per) * row_len + (tr_i % per);
+            if (base >= Bend)
+                continue; // wave-uniform
+            const uint64_t n = base + (uint64_t)per * lane;
+            const bool active = n < Bend;
+            int64_t c;
+            int32_t sfi;
+            position(T, pos, active ? n : base, c, sfi);
+            const int32_t sfi0 = __builtin_amdgcn_readfirstlane(sfi); // lane 0: n = base
+            double left[CH], right[CH];
+#pragma unroll
+            for (int k = 0; k < CH; ++k)
+                left[k] = right[k] = 0.0;
+            const int32_t ccL = (max_fi - sfi0) / inc;
+            const int32_t fiL = sfi0 + ccL * inc;
+            const int32_t frR = inc - sfi0;
+            const int32_t ccR = (max_fi - frR) / inc;
+            const int32_t fiR = frR + ccR * inc;
+            if (__all(sfi == sfi0)) {
+                const int32_t nL = fiL / inc + 1, nR = (fiR - 1) / inc + 1;
+                for (int32_t j = (int32_t)lane; j < nL; j += 64)
+                    coefL[j] = interp_coeff(Cg, fiL - j * inc);
+                for (int32_t j = (int32_t)lane; j < nR; j += 64)
+                    coefR[j] = interp_coeff(Cg, fiR - j * inc);
+                wave_lds_sync();
+                const float *xl = X + (int64_t)(c - ccL - w0) * CH;
+#pragma unroll 4
+                for (int32_t j = 0; j < nL; ++j) {
+                    const double ic = coefL[j];
+#pragma unroll
+                    for (int k = 0; k < CH; ++k)
+                        left[k] = left[k] + ic * (double)xl[j * CH + k];
+                }
+                const float *xr = X + (int64_t)(c + 1 + ccR - w0) * CH;
+#pragma unroll 4
+                for (int32_t j = 0; j < nR; ++j) {
+                    const double ic = coefR[j];
+#pragma unroll
+                    for (int k = 0; k < CH; ++k)
+                        right[k] = right[k] + ic * (double)xr[-j * CH + k];
+                }
+                wave_lds_sync(); // the list is rewritten by the next row
+            } else {
+                const int32_t ccl = (max_fi - sfi) / inc;
+                half_filter<CH, true, false>(Cg, X, sfi + ccl * inc, inc,
+                                             (int32_t)(c - ccl - w0), left);
+                const int32_t fr = inc - sfi;
+                const int32_t ccr = (max_fi - fr) / inc;
+                half_filter<CH, false, false>(Cg, X, fr + ccr * inc, inc,
+                                              (int32_t)(c + 1 + ccr - w0), right);
+            }
+            if (active) {
+                int32_t *o = out + T.out_base + n * CH;
+#pragma unroll
+                for (int k = 0; k < CH; ++k) {
+                    const float f = (float)(T.scale * (left[k] + right[k]));
+                    const float g = f * P.q;
+                    int32_t s = (g >= 2147483648.0f || g < -2147483648.0f || g != g)
+                                    ? (int32_t)0x80000000
+                                    : (int32_t)g;
+                    o[k] = s > P.hi ? P.hi : (s < P.lo ? P.lo : s);
+                }
             }
         }
         __syncthreads();
@@ -499,10 +645,62 @@ uint64_t output_frames(const Conv &v, uint32_t ch, uint64_t frames, const uint32
     return lo;
 }
 
+struct FilterArgs {
+    RsParams P;
+    const RsTrack *tr;
+    const uint32_t *chunk_track;
+    const int2 *pos;
+    const uint32_t *table;
+    const int32_t *in;
+    int32_t *out;
+};
+
+template <int CH>
+void launch_filter(const FilterArgs &A, bool hoist, bool xd, unsigned grid, unsigned block,
+                   size_t lds, hipStream_t s)
+{
+#define RS_GO(H, XT)                                                                           \
+    hipLaunchKernelGGL((k_rs_filter<CH, H, XT>), dim3(grid), dim3(block), lds, s, A.P, A.tr,   \
+                       A.chunk_track, A.pos, A.table, A.in, A.out)
+    if (hoist && xd)
+        RS_GO(true, double);
+    else if (hoist)
+        RS_GO(true, float);
+    else if (xd)
+        RS_GO(false, double);
+    else
+        RS_GO(false, float);
+#undef RS_GO
+}
+
+template <int CH>
+void launch_phase(const FilterArgs &A, const uint2 *tasks, uint32_t n_tasks, uint32_t tmax,
+                  unsigned grid, size_t lds, hipStream_t s)
+{
+    hipLaunchKernelGGL((k_rs_phase<CH>), dim3(grid), dim3(1024), lds, s, A.P, A.tr, tasks, n_tasks,
+                       A.pos, A.table, A.in, A.out, tmax);
+}
+
+template <int CH>
+hipError_t set_lds_attr()
+{
+    const hipFuncAttribute a = hipFuncAttributeMaxDynamicSharedMemorySize;
+    hipError_t e = hipFuncSetAttribute((const void *)k_rs_phase<CH>, a, 160 * 1024);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_rs_filter<CH, true, double>, a, 160 * 1024);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_rs_filter<CH, true, float>, a, 160 * 1024);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_rs_filter<CH, false, double>, a, 160 * 1024);
+    if (e == hipSuccess)
+        e = hipFuncSetAttribute((const void *)k_rs_filter<CH, false, float>, a, 160 * 1024);
+    return e;
+}
+
 struct RsCtx {
     void *tracks = nullptr, *chunk_track = nullptr, *pos = nullptr, *table = nullptr,
-         *ids = nullptr;
-    size_t cap_tracks = 0, cap_chunks = 0, cap_pos = 0, cap_ids = 0;
+         *ids = nullptr, *ptasks = nullptr;
+    size_t cap_tracks = 0, cap_chunks = 0, cap_pos = 0, cap_ids = 0, cap_ptasks = 0;
     bool table_up = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float ms[2] = {0.0f, 0.0f};
@@ -560,8 +758,6 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
     std::vector<uint32_t> chunk_track, serial;
     // outputs per block iteration: the LDS holds the table plus the input
     // window of one chunk (chunk / ratio frames plus the taps either side)
-    double min_ratio = 1e300;
-    int32_t min_inc = 1 << 30;
     std::vector<Conv> conv(n);
     for (uint32_t t = 0; t < n; ++t) {
         const atg_rs_track &a = tracks[t];
@@ -570,20 +766,85 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         conv[t] = make_conv(a.in_rate, a.out_rate);
         if (conv[t].ratio > 256.0 || conv[t].ratio < 1.0 / 256.0) // is_bad_src_ratio
             return rsfail(ATG_ERR_INVALID, "SRC ratio outside [1/256, 256]");
+    }
+    // Phase-sharing plan (k_rs_phase): a track whose rational ratio repeats
+    // its phases every `period` outputs goes there when a task of 64 x period
+    // outputs fits the LDS with its input window and the per-wave
+    // coefficient lists; the rest go to the per-output kernel k_rs_filter.
+    const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
+    const size_t kLds = 160 * 1024;
+    std::vector<uint32_t> per(n, 0), rows(n, 0);
+    std::vector<char> phase(n, 0);
+    uint32_t tmax = 0;
+    for (int it = 0; it < 2; ++it) {
+        uint32_t tm = 0;
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint64_t g = std::gcd((uint64_t)tracks[t].in_rate, (uint64_t)tracks[t].out_rate);
+            const uint64_t p_out = tracks[t].out_rate / g, q_in = tracks[t].in_rate / g;
+            const uint64_t reach = (uint64_t)(max_fi / conv[t].increment) + 2;
+            const uint32_t tm_t = std::max<uint32_t>(tmax, (uint32_t)reach);
+            const size_t coef = (size_t)16 * 2 * tm_t * sizeof(double);
+            phase[t] = 0;
+            if (p_out > 65536)
+                continue;
+            uint64_t r = 0;
+            for (uint64_t R = 1; R <= 64; R *= 2) {
+                const size_t win = (size_t)(64 * q_in * R + 2 * reach + 8) * channels * 4;
+                if (coef + win > kLds)
+                    break;
+                r = R;
+                if (64 * p_out * R >= std::max<uint64_t>(tracks[t].pcm_frames, 1) * 2)
+                    break; // one task already covers the track
+            }
+            if (!r)
+                continue;
+            phase[t] = 1;
+            per[t] = (uint32_t)p_out;
+            rows[t] = (uint32_t)r;
+            tm = std::max<uint32_t>(tm, (uint32_t)reach);
+        }
+        if (tm <= tmax)
+            break;
+        tmax = tm;
+    }
+    // k_rs_filter: the window as doubles when a chunk of >= 512 outputs fits
+    // (no conversion per tap), else as floats with the largest chunk that fits
+    double min_ratio = 1e300;
+    int32_t min_inc = 1 << 30;
+    bool hoist = true;
+    for (uint32_t t = 0; t < n; ++t) {
+        if (phase[t])
+            continue;
         min_ratio = std::min(min_ratio, conv[t].ratio);
         min_inc = std::min(min_inc, conv[t].increment);
+        hoist = hoist && (conv[t].increment & ((1 << kShift) - 1)) == 0;
     }
-    uint32_t chunk = kChunk;
+    uint32_t chunk = 0;
     size_t lds = 0;
-    for (;; chunk /= 2) {
-        const uint64_t reach = (uint64_t)((SRC_MEDIUM_HALF_LEN << kShift) / min_inc) + 2;
-        const uint64_t wn = (uint64_t)std::ceil(chunk / min_ratio) + 2 * reach + 4;
-        lds = sizeof(float) * (((kTable + 3) & ~3) + wn * channels);
-        if (lds <= 160 * 1024)
-            break;
-        if (chunk <= 64)
-            return rsfail(ATG_ERR_UNSUPPORTED, "resampling ratio too low for the LDS window");
+    bool xd = false;
+    if (min_inc == (1 << 30)) { // every track goes to k_rs_phase
+        chunk = kChunk;
+        min_inc = 1 << 20;
+        min_ratio = 1.0;
     }
+    for (int pass = 0; pass < 2 && !chunk; ++pass) {
+        const size_t xsz = pass == 0 ? sizeof(double) : sizeof(float);
+        for (uint32_t ck = kChunk; ck >= (pass == 0 ? 512u : 64u); ck /= 2) {
+            const uint64_t reach = (uint64_t)((SRC_MEDIUM_HALF_LEN << kShift) / min_inc) + 2;
+            const uint64_t wn = (uint64_t)std::ceil(ck / min_ratio) + 2 * reach + 4;
+            const size_t need = sizeof(float) * ((kTable + 3) & ~3) + xsz * wn * channels;
+            if (need <= kLds) {
+                chunk = ck;
+                lds = need;
+                xd = pass == 0;
+                break;
+            }
+        }
+    }
+    if (!chunk)
+        return rsfail(ATG_ERR_UNSUPPORTED, "resampling ratio too low for the LDS window");
+    std::vector<uint2> ptasks;
+    size_t lds_phase = 0;
     uint64_t out = 0, posn = 0;
     for (uint32_t t = 0; t < n; ++t) {
         const atg_rs_track &a = tracks[t];
@@ -599,14 +860,28 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         T.mode = v.mode;
         T.D = v.D;
         T.pos_base = 0;
+        T.span = 0;
+        T.period = per[t];
+        T.pad = 0;
         if (v.mode == POS_TABLE) {
             T.pos_base = posn;
             posn += T.out_frames;
             serial.push_back(t);
         }
         T.chunk_base = chunk_track.size();
-        for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
-            chunk_track.push_back(t);
+        if (phase[t]) {
+            T.span = 64ull * per[t] * rows[t];
+            for (uint64_t k = 0; k * T.span < T.out_frames; ++k)
+                ptasks.push_back(make_uint2(t, (uint32_t)k));
+            const uint64_t g = std::gcd((uint64_t)a.in_rate, (uint64_t)a.out_rate);
+            const uint64_t reach = (uint64_t)(max_fi / v.increment) + 2;
+            lds_phase = std::max(lds_phase, (size_t)16 * 2 * tmax * sizeof(double) +
+                                                (size_t)(64 * (a.in_rate / g) * rows[t] +
+                                                         2 * reach + 8) * channels * 4);
+        } else {
+            for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
+                chunk_track.push_back(t);
+        }
         out_offsets[t] = out;
         out_frames[t] = T.out_frames;
         out += T.out_frames;
@@ -618,17 +893,24 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         RSHIP(hipMemcpy(X.table, SRC_MEDIUM_BITS, sizeof(SRC_MEDIUM_BITS), hipMemcpyHostToDevice));
         for (int k = 0; k < 3; ++k)
             RSHIP(hipEventCreate(&X.ev[k]));
-#define RS_ATTR(K)                                                                            \
-    RSHIP(hipFuncSetAttribute((const void *)k_rs_filter<K>,                                  \
-                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-        RS_ATTR(1) RS_ATTR(2) RS_ATTR(3) RS_ATTR(4) RS_ATTR(5) RS_ATTR(6) RS_ATTR(7) RS_ATTR(8)
-#undef RS_ATTR
+        RSHIP(set_lds_attr<1>());
+        RSHIP(set_lds_attr<2>());
+        RSHIP(set_lds_attr<3>());
+        RSHIP(set_lds_attr<4>());
+        RSHIP(set_lds_attr<5>());
+        RSHIP(set_lds_attr<6>());
+        RSHIP(set_lds_attr<7>());
+        RSHIP(set_lds_attr<8>());
         X.table_up = true;
     }
     RSHIP(grow(X.tracks, X.cap_tracks, sizeof(RsTrack) * std::max<uint32_t>(n, 1)));
     RSHIP(grow(X.chunk_track, X.cap_chunks, sizeof(uint32_t) * std::max<size_t>(chunk_track.size(), 1)));
     RSHIP(grow(X.pos, X.cap_pos, sizeof(int2) * std::max<uint64_t>(posn, 1)));
     RSHIP(grow(X.ids, X.cap_ids, sizeof(uint32_t) * std::max<size_t>(serial.size(), 1)));
+    RSHIP(grow(X.ptasks, X.cap_ptasks, sizeof(uint2) * std::max<size_t>(ptasks.size(), 1)));
+    if (!ptasks.empty())
+        RSHIP(hipMemcpyAsync(X.ptasks, ptasks.data(), sizeof(uint2) * ptasks.size(),
+                             hipMemcpyHostToDevice, s));
     if (n)
         RSHIP(hipMemcpyAsync(X.tracks, tr.data(), sizeof(RsTrack) * n, hipMemcpyHostToDevice, s));
     if (!chunk_track.empty())
@@ -656,16 +938,36 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
     RSHIP(hipEventRecord(X.ev[1], s));
     if (P.n_chunks) {
         const unsigned grid = std::min<uint32_t>(P.n_chunks, 256u);
+        const FilterArgs A{P, (const RsTrack *)X.tracks, (const uint32_t *)X.chunk_track,
+                           (const int2 *)X.pos, (const uint32_t *)X.table, d_in, d_out};
         switch (channels) {
-#define RS_CASE(K)                                                                            \
-    case K:                                                                                   \
-        hipLaunchKernelGGL(k_rs_filter<K>, dim3(grid), dim3(chunk), lds, s, P,                \
-                           (const RsTrack *)X.tracks, (const uint32_t *)X.chunk_track,        \
-                           (const int2 *)X.pos, (const uint32_t *)X.table, d_in, d_out);      \
-        break;
-            RS_CASE(1) RS_CASE(2) RS_CASE(3) RS_CASE(4) RS_CASE(5) RS_CASE(6) RS_CASE(7)
-            RS_CASE(8)
-#undef RS_CASE
+        case 1: launch_filter<1>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 2: launch_filter<2>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 3: launch_filter<3>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 4: launch_filter<4>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 5: launch_filter<5>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 6: launch_filter<6>(A, hoist, xd, grid, chunk, lds, s); break;
+        case 7: launch_filter<7>(A, hoist, xd, grid, chunk, lds, s); break;
+        default: launch_filter<8>(A, hoist, xd, grid, chunk, lds, s); break;
+        }
+        RSHIP(hipGetLastError());
+    }
+    if (!ptasks.empty()) {
+        const FilterArgs A{P, (const RsTrack *)X.tracks, (const uint32_t *)X.chunk_track,
+                           (const int2 *)X.pos, (const uint32_t *)X.table, d_in, d_out};
+        const unsigned per_cu = lds_phase <= kLds / 2 ? 2u : 1u;
+        const unsigned grid = (unsigned)std::min<size_t>(ptasks.size(), 256u * per_cu);
+        const uint2 *tk = (const uint2 *)X.ptasks;
+        const uint32_t nt = (uint32_t)ptasks.size();
+        switch (channels) {
+        case 1: launch_phase<1>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 2: launch_phase<2>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 3: launch_phase<3>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 4: launch_phase<4>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 5: launch_phase<5>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 6: launch_phase<6>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 7: launch_phase<7>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        default: launch_phase<8>(A, tk, nt, tmax, grid, lds_phase, s); break;
         }
         RSHIP(hipGetLastError());
     }
