@@ -79,6 +79,7 @@ def parse_args(argv=None):
                     help="config-5 chain leg: 192 kHz 5.1 tracks per GPU")
     ap.add_argument("--chain-seconds", type=int, default=10)
     ap.add_argument("--no-chain", action="store_true")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-to-host leg")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -381,6 +382,37 @@ def convert_leg(args, torch, device, pcm):
             "verified_dither_invariant": ok}
 
 
+def host_leg(args, torch, dist, world, device, eng, opts, pcm_host, tracks, n_frames, images,
+             barrier):
+    """SURVEY 8(d)'s host-to-host timer: host PCM (pageable numpy int16) in,
+    .flac images back in host memory, through atg_flac_encode_host -- chunks
+    of ~256 MB of PCM staged through pinned buffers, chunk c's upload, chunk
+    c's encode and chunk c-1's download overlapping.  Every image is compared
+    with the device-path image of the same track."""
+    steps = max(1, min(args.steps, 3))
+    out = None
+    out, res, _, _ = eng.encode(opts, pcm_host, tracks, 2, 16, 44100)  # warm-up
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out, res, _, _ = eng.encode(opts, pcm_host, tracks, 2, 16, 44100)
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, device)
+    same = all(bytes(out[r.out_offset:r.out_offset + r.bytes]) == images[t]
+               for t, r in enumerate(res))
+    in_b = pcm_host.nbytes
+    out_b = sum(int(r.bytes) for r in res)
+    return {"metric": "FLAC-8 encode frames/s, host PCM in -> .flac images in host memory",
+            "value": round(n_frames * world * steps / elapsed, 1), "unit": "frames/s",
+            "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
+            "bytes_in": in_b, "bytes_out": out_b,
+            "host_gbps": round((in_b + out_b) / (elapsed / steps) / 1e9, 2),
+            "chunk_mb": int(os.environ.get("ATG_HOST_CHUNK_MB", "256")),
+            "images_identical_to_device_path": same}
+
+
 def resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier, threads, verify):
     """BASELINE config 3: 44.1 kHz -> 48 kHz sinc resample (resample.hip,
     SURVEY 8(a) R1-R3) + 24 -> 16-bit dither (pcm_convert.hip R4) of every
@@ -566,7 +598,8 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     dres, fres = state["dres"], state["fres"]
     dec_ok = all(r.status == 0 and r.pcm_frames == n_in for r in dres) and \
         state["nsamp"] == src.numel()
-    lossless = dec_ok and _device_equal(torch, state["d_pcm"], src)
+    lossless, bad_track = _device_equal(torch, eng, state["d_pcm"], src, n_tracks) if dec_ok \
+        else (False, -3)
     flac_bytes = sum(int(r.bytes) for r in fres)
     out = {"metric": "config 5 track2track chain: ALAC 192k/24-bit 5.1 decode -> 48k resample "
                      "-> FLAC-8, output frames/s (48 kHz PCM frames)",
@@ -579,7 +612,11 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
                       "alac_bytes": alac_bytes, "flac_bytes": flac_bytes,
                       "flac_frames": n_flac},
            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
-           "verified_alac_lossless": bool(dec_ok and lossless)}
+           "verified_alac_lossless": bool(dec_ok and lossless),
+           "alac_decode_status": sorted({int(r.status) for r in dres}),
+           "alac_decode_frames_ok": all(int(r.pcm_frames) == n_in for r in dres),
+           "alac_decode_samples": int(state["nsamp"]),
+           "alac_first_bad_track": bad_track}
     if verify:
         import oracle_port
         oracle_port.load()
@@ -629,17 +666,19 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     return out
 
 
-def _device_equal(torch, d_ptr, ref):
-    """compare n int32 at device address d_ptr with the tensor ref (on its
-    device) without a host copy"""
-    import ctypes
+def _device_equal(torch, eng, d_ptr, ref, n_tracks=1):
+    """compare int32 at device address d_ptr with the tensor ref (on its
+    device), copying through the engine (the process's one HIP runtime)
+    -> (equal, first mismatching track or -1)"""
     got = torch.empty_like(ref)
-    hip = ctypes.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
-    if hip.hipMemcpy(ctypes.c_void_p(got.data_ptr()), ctypes.c_void_p(d_ptr),
-                     ref.numel() * 4, 3) != 0:
-        return False
-    return bool(torch.equal(got, ref))
+    eng.copy_device(got.data_ptr(), d_ptr, ref.numel() * 4)
+    if torch.equal(got, ref):
+        return True, -1
+    per = ref.numel() // max(1, n_tracks)
+    for t in range(n_tracks):
+        if not torch.equal(got[t * per:(t + 1) * per], ref[t * per:(t + 1) * per]):
+            return False, t
+    return False, n_tracks
 
 
 def album_reduce(dist, world, hist, peak):
@@ -793,15 +832,27 @@ def main(argv=None):
     tracks = [(i * n_samples, n_samples) for i in range(n_tracks)]
     n_frames, out_cap = eng.bounds(opts, tracks, 2, 16)
     table = _atgpu.TrackTable(tracks)
-    out = torch.empty(out_cap, dtype=torch.uint8, device=device)
+    # two output buffers: batch k+1 is enqueued before batch k is waited
+    # (atg_flac_encode_device_async), so batch k's MD5 chains and headers run
+    # under batch k+1's search; every batch is complete inside the clock
+    outs = [torch.empty(out_cap, dtype=torch.uint8, device=device) for _ in range(2)]
     torch.cuda.synchronize()
+    pending = []
 
-    def step():
-        return eng.encode_device(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16,
-                                 44100, out.data_ptr(), out_cap)
+    def step(k):
+        t = eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16, 44100,
+                                    outs[k % 2].data_ptr(), out_cap)
+        r = eng.wait(pending.pop()) if pending else None
+        pending.append(t)
+        return r
 
-    for _ in range(args.warmup):
-        res = step()
+    def drain():
+        return eng.wait(pending.pop())
+
+    for k in range(args.warmup):
+        step(k)
+    if args.warmup:
+        drain()
 
     def barrier():
         if world > 1:
@@ -811,14 +862,20 @@ def main(argv=None):
     kt_sum = {}
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        res = step()
-        for k, v in eng.kernel_times().items():
-            kt_sum[k] = kt_sum.get(k, 0.0) + v
+    for k in range(args.steps):
+        step(k)
+        if k:
+            for name, v in eng.kernel_times().items():
+                kt_sum[name] = kt_sum.get(name, 0.0) + v
+    res = drain()
+    for name, v in eng.kernel_times().items():
+        kt_sum[name] = kt_sum.get(name, 0.0) + v
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
+    out = outs[(args.steps - 1) % 2]
+    del outs
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     out_bytes = sum(int(r.bytes) for r in res)
     frame_bytes = out_bytes - HEADER_BYTES * len(res)
@@ -847,7 +904,10 @@ def main(argv=None):
                           % (n_tracks, args.frames, threads, port_dt)}
         del want
 
-    decode = convert = rg = rg_res = resample = None
+    decode = convert = rg = rg_res = resample = host = None
+    if not args.no_host:
+        host = host_leg(args, torch, dist, world, device, eng, opts, pcm_host, tracks, n_frames,
+                        images, barrier)
     if not args.no_decode:
         decode = decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host,
                             n_frames, barrier)
@@ -976,6 +1036,7 @@ def main(argv=None):
         "decode": decode,
         "convert": convert,
         "replaygain": rg,
+        "host_to_host": host,
         "resample": resample,
         "chain": chain,
     }

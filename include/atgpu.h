@@ -135,6 +135,22 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
                                   uint32_t sample_rate, void *d_out,
                                   uint64_t out_cap, atg_track_result *results);
 
+/* The same batch encode, enqueued: returns once the work is queued, with a
+   ticket for atg_flac_encode_wait.  The engine keeps two batches in flight
+   (each its own device workspace): batch k's MD5 chains and stream headers
+   run on their own stream while batch k+1's analysis runs, so a caller that
+   waits for ticket k after enqueueing k+1 overlaps them.  d_pcm and d_out
+   must stay untouched until the ticket is waited; enqueueing a third batch
+   drains the oldest (its results stay readable until its slot is reused). */
+atg_status atg_flac_encode_device_async(atg_engine *eng, const atg_flac_options *opts,
+                                        const void *d_pcm, atg_pcm_format format,
+                                        const atg_track *tracks, uint32_t n_tracks,
+                                        uint32_t channels, uint32_t bits_per_sample,
+                                        uint32_t sample_rate, void *d_out, uint64_t out_cap,
+                                        uint64_t *ticket);
+/* wait for the batch of `ticket`; results as atg_flac_encode_device's */
+atg_status atg_flac_encode_wait(atg_engine *eng, uint64_t ticket, atg_track_result *results);
+
 /* Per-kernel device time of the engine's most recent encode, measured with
    HIP events recorded on the stream each kernel ran on.  names/ms arrays of
    capacity `cap`; returns the number of entries written. */
@@ -145,6 +161,7 @@ atg_status atg_device_alloc(atg_engine *eng, uint64_t bytes, void **d_ptr);
 atg_status atg_device_free(atg_engine *eng, void *d_ptr);
 atg_status atg_copy_to_device(atg_engine *eng, void *d_dst, const void *src,
                               uint64_t bytes);
+atg_status atg_copy_device(atg_engine *eng, void *d_dst, const void *d_src, uint64_t bytes);
 atg_status atg_copy_to_host(atg_engine *eng, void *dst, const void *d_src,
                             uint64_t bytes);
 

@@ -29,8 +29,9 @@ PCM_S32 = 1
 EXPORTS = (
     "atg_abi_version", "atg_last_error", "atg_engine_create",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
-    "atg_flac_encode_device", "atg_engine_kernel_times", "atg_device_alloc",
-    "atg_device_free", "atg_copy_to_device", "atg_copy_to_host",
+    "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
+    "atg_engine_kernel_times", "atg_device_alloc",
+    "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
     "atg_flac_decode_device", "atg_decoder_kernel_times",
@@ -246,6 +247,12 @@ def load_library():
             P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
             c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult)]
         lib.atg_flac_encode_device.restype = ctypes.c_int
+        lib.atg_flac_encode_device_async.argtypes = [
+            P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
+            c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(c_u64)]
+        lib.atg_flac_encode_device_async.restype = ctypes.c_int
+        lib.atg_flac_encode_wait.argtypes = [P, c_u64, ctypes.POINTER(TrackResult)]
+        lib.atg_flac_encode_wait.restype = ctypes.c_int
         lib.atg_engine_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -256,6 +263,8 @@ def load_library():
         lib.atg_device_free.restype = ctypes.c_int
         lib.atg_copy_to_device.argtypes = [P, P, P, c_u64]
         lib.atg_copy_to_device.restype = ctypes.c_int
+        lib.atg_copy_device.argtypes = [P, P, P, c_u64]
+        lib.atg_copy_device.restype = ctypes.c_int
         lib.atg_copy_to_host.argtypes = [P, P, P, c_u64]
         lib.atg_copy_to_host.restype = ctypes.c_int
         lib.atg_flac_read_metadata.argtypes = [
@@ -486,11 +495,37 @@ class Engine(object):
             out_cap, res))
         return [res[i] for i in range(n)]
 
+    def encode_device_async(self, options, d_pcm, fmt, tracks, channels, bits_per_sample,
+                            sample_rate, d_out, out_cap):
+        """enqueue a device-memory batch; -> (ticket, n_tracks) for wait()"""
+        if isinstance(tracks, TrackTable):
+            arr, n = tracks.arr, tracks.n
+        else:
+            arr, n, keep = _track_array(tracks)
+        t = c_u64()
+        _check(self.lib, self.lib.atg_flac_encode_device_async(
+            self.handle, ctypes.byref(options), ctypes.c_void_p(d_pcm), fmt, arr, n,
+            channels, bits_per_sample, sample_rate, ctypes.c_void_p(d_out), out_cap,
+            ctypes.byref(t)))
+        return (t.value, n)
+
+    def wait(self, ticket):
+        """TrackResults of an enqueued batch (waits for it)"""
+        t, n = ticket
+        res = (TrackResult * max(1, n))()
+        _check(self.lib, self.lib.atg_flac_encode_wait(self.handle, t, res))
+        return [res[i] for i in range(n)]
+
     def kernel_times(self):
         names = (ctypes.c_char_p * 16)()
         ms = (ctypes.c_float * 16)()
         k = self.lib.atg_engine_kernel_times(self.handle, names, ms, 16)
         return {names[i].decode(): float(ms[i]) for i in range(k)}
+
+    def copy_device(self, d_dst, d_src, nbytes):
+        """device-to-device copy on this engine's device"""
+        _check(self.lib, self.lib.atg_copy_device(self.handle, ctypes.c_void_p(d_dst),
+                                                  ctypes.c_void_p(d_src), nbytes))
 
     def copy_to_host(self, dst, d_src):
         """device bytes at d_src -> the numpy array dst (its full size)"""

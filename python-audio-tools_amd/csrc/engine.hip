@@ -13,7 +13,9 @@
 #include <cstdlib>
 #include <cstring>
 #include <map>
+#include <memory>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/atgpu.h"
@@ -111,22 +113,59 @@ void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16])
 
 } // namespace
 
+namespace {
+struct Plan;
+}
+
+// One batch in flight: its device workspace, its MD5/header stream and the
+// pinned host copies of its results.  Two slots let batch k's MD5 chains and
+// stream headers (on the slot's aux stream) run under batch k+1's search.
+struct EncSlot {
+    DevBuf frames, tracks, order, coef, shift, est, sub, fdesc, tout, err;
+    hipStream_t s_aux = nullptr;
+    hipEvent_t ev[2 * kNumTimed] = {};
+    hipEvent_t ev_tables = nullptr, ev_pack = nullptr, ev_done = nullptr;
+    std::shared_ptr<Plan> plan;      // the batch's plan (kept alive while in flight)
+    const Plan *uploaded = nullptr;  // plan whose tables this slot's device holds
+    TrackOut *tout_h = nullptr;      // pinned
+    size_t tout_cap = 0;
+    FrameDesc *fdesc_h = nullptr;    // pinned
+    size_t fdesc_cap = 0;
+    uint32_t *err_h = nullptr;       // pinned
+    size_t err_cap = 0;
+    bool want_fdesc = false;
+    bool busy = false;               // enqueued, not yet waited
+    bool done = false;               // waited: results below are valid
+    uint64_t ticket = 0;
+    atg_status status = ATG_OK;
+    std::string error;
+    float times[kNumTimed] = {};
+};
+
 struct atg_engine {
     int device = 0;
-    hipStream_t s_main = nullptr, s_aux = nullptr;
-    hipEvent_t ev[2 * kNumTimed] = {};
-    hipEvent_t ev_tables = nullptr, ev_md5 = nullptr;
-    DevBuf frames, tracks, order, windows, coef, shift, est, sub, fdesc, tout, err;
-    DevBuf h_pcm, h_out; // staging for the host-memory API
+    hipStream_t s_main = nullptr;
+    EncSlot slot[2];
+    DevBuf windows;
+    // host-memory API: per slot, device PCM/image buffers and pinned host
+    // staging, plus copy streams, so chunk c's upload, chunk c-1's download
+    // and chunk c's encode overlap (atg_flac_encode_host)
+    DevBuf d_pcm[2], d_img[2];
+    uint8_t *p_in[2] = {nullptr, nullptr}, *p_out[2] = {nullptr, nullptr};
+    size_t p_in_cap[2] = {0, 0}, p_out_cap[2] = {0, 0};
+    hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_d2h[2] = {nullptr, nullptr};
+    uint64_t chunk_bytes = 256ull << 20; // PCM bytes per chunk
     std::map<uint32_t, uint32_t> win_off;
     std::vector<double> win_host;
     size_t win_uploaded = 0;
     float times[kNumTimed] = {};
     bool have_times = false;
+    uint64_t next_ticket = 1;
     // plan cache: a batch with the same geometry as the previous call reuses
-    // the plan and the frame/track tables already on the device
-    std::vector<uint8_t> plan_key, plan_key_pending;
-    void *plan_cached = nullptr; // Plan*
+    // the plan (and a slot's frame/track tables when it last ran that plan)
+    std::vector<uint8_t> plan_key;
+    std::shared_ptr<Plan> plan_cached;
 };
 
 namespace {
@@ -341,10 +380,55 @@ atg_status prepare_windows(atg_engine *e, Plan &pl)
     return ATG_OK;
 }
 
-atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, int fmt,
-                     uint8_t *d_out, uint64_t out_cap, std::vector<TrackOut> &tout_h,
-                     std::vector<FrameDesc> *fdesc_h)
+// memcpy split over host threads (pageable <-> pinned staging of large
+// chunks runs at several times one core's copy bandwidth)
+void par_memcpy(void *dst, const void *src, size_t n)
 {
+    const size_t kMin = 8u << 20;
+    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    if (n < kMin || nt < 2) {
+        std::memcpy(dst, src, n);
+        return;
+    }
+    nt = (unsigned)std::min<size_t>(nt, n / (kMin / 4));
+    std::vector<std::thread> th;
+    const size_t part = (n / nt + 4095) & ~(size_t)4095;
+    for (unsigned i = 0; i < nt; ++i) {
+        const size_t a = (size_t)i * part;
+        if (a >= n)
+            break;
+        const size_t len = std::min(part, n - a);
+        th.emplace_back([=] { std::memcpy((uint8_t *)dst + a, (const uint8_t *)src + a, len); });
+    }
+    for (auto &t : th)
+        t.join();
+}
+
+template <class T>
+hipError_t ensure_pinned(T *&p, size_t &cap, size_t n)
+{
+    if (p && n <= cap)
+        return hipSuccess;
+    if (p)
+        (void)hipHostFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = std::max<size_t>(n, 16);
+    hipError_t e = hipHostMalloc((void **)&p, want * sizeof(T), hipHostMallocDefault);
+    if (e == hipSuccess)
+        cap = want;
+    return e;
+}
+
+// Enqueue one batch on slot `sl`: the search chain on the engine's main
+// stream, the MD5 chains from the start of the batch and the stream headers
+// on the slot's aux stream, then the results back to pinned host memory.
+// Returns without waiting.
+atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan> &plp,
+                         const void *d_pcm, int fmt, uint8_t *d_out, uint64_t out_cap,
+                         bool want_fdesc, hipEvent_t wait_before = nullptr)
+{
+    Plan &pl = *plp;
     FlacParams &p = pl.p;
     if (pl.out_bytes > out_cap)
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
@@ -354,102 +438,114 @@ atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, in
     if (st != ATG_OK)
         return st;
     const size_t nf = pl.frames.size(), nt = pl.tracks.size();
+    bool upload = sl.uploaded != &pl;
     {
-        void *f0 = e->frames.p, *t0 = e->tracks.p, *o0 = e->order.p;
-        HIP_TRY(e->frames.ensure(nf * sizeof(FrameInfo)));
-        HIP_TRY(e->tracks.ensure(nt * sizeof(TrackInfo)));
-        HIP_TRY(e->order.ensure(nf * sizeof(uint32_t)));
-        if (f0 != e->frames.p || t0 != e->tracks.p || o0 != e->order.p)
+        void *f0 = sl.frames.p, *t0 = sl.tracks.p, *o0 = sl.order.p;
+        HIP_TRY(sl.frames.ensure(nf * sizeof(FrameInfo)));
+        HIP_TRY(sl.tracks.ensure(nt * sizeof(TrackInfo)));
+        HIP_TRY(sl.order.ensure(nf * sizeof(uint32_t)));
+        if (f0 != sl.frames.p || t0 != sl.tracks.p || o0 != sl.order.p)
             upload = true;
     }
-    HIP_TRY(e->coef.ensure(nf * p.n_cand * p.coef_stride * sizeof(int16_t)));
-    HIP_TRY(e->shift.ensure(nf * p.n_cand * std::max<uint32_t>(1, p.max_lpc_order)));
-    HIP_TRY(e->est.ensure(nf * p.n_cand));
-    HIP_TRY(e->sub.ensure(nf * p.n_cand * sizeof(SubDesc)));
-    HIP_TRY(e->fdesc.ensure(nf * sizeof(FrameDesc)));
-    HIP_TRY(e->tout.ensure(nt * sizeof(TrackOut)));
-    HIP_TRY(e->err.ensure(sizeof(uint32_t)));
+    HIP_TRY(sl.coef.ensure(nf * p.n_cand * p.coef_stride * sizeof(int16_t)));
+    HIP_TRY(sl.shift.ensure(nf * p.n_cand * std::max<uint32_t>(1, p.max_lpc_order)));
+    HIP_TRY(sl.est.ensure(nf * p.n_cand));
+    HIP_TRY(sl.sub.ensure(nf * p.n_cand * sizeof(SubDesc)));
+    HIP_TRY(sl.fdesc.ensure(nf * sizeof(FrameDesc)));
+    HIP_TRY(sl.tout.ensure(nt * sizeof(TrackOut)));
+    HIP_TRY(sl.err.ensure(sizeof(uint32_t)));
+    HIP_TRY(ensure_pinned(sl.tout_h, sl.tout_cap, nt));
+    HIP_TRY(ensure_pinned(sl.err_h, sl.err_cap, 1));
+    if (want_fdesc)
+        HIP_TRY(ensure_pinned(sl.fdesc_h, sl.fdesc_cap, nf));
+    sl.uploaded = nullptr;
+    if (wait_before)
+        HIP_TRY(hipStreamWaitEvent(e->s_main, wait_before, 0));
     if (upload && nf)
-        HIP_TRY(hipMemcpyAsync(e->frames.p, pl.frames.data(), nf * sizeof(FrameInfo),
+        HIP_TRY(hipMemcpyAsync(sl.frames.p, pl.frames.data(), nf * sizeof(FrameInfo),
                                hipMemcpyHostToDevice, e->s_main));
     if (upload && nt)
-        HIP_TRY(hipMemcpyAsync(e->tracks.p, pl.tracks.data(), nt * sizeof(TrackInfo),
+        HIP_TRY(hipMemcpyAsync(sl.tracks.p, pl.tracks.data(), nt * sizeof(TrackInfo),
                                hipMemcpyHostToDevice, e->s_main));
     if (upload && nf)
-        HIP_TRY(hipMemcpyAsync(e->order.p, pl.order.data(), nf * sizeof(uint32_t),
+        HIP_TRY(hipMemcpyAsync(sl.order.p, pl.order.data(), nf * sizeof(uint32_t),
                                hipMemcpyHostToDevice, e->s_main));
-    HIP_TRY(hipMemsetAsync(e->err.p, 0, sizeof(uint32_t), e->s_main));
-    HIP_TRY(hipEventRecord(e->ev_tables, e->s_main));
+    HIP_TRY(hipMemsetAsync(sl.err.p, 0, sizeof(uint32_t), e->s_main));
+    HIP_TRY(hipEventRecord(sl.ev_tables, e->s_main));
 
-    const FrameInfo *dfr = (const FrameInfo *)e->frames.p;
-    const TrackInfo *dtr = (const TrackInfo *)e->tracks.p;
-    TrackOut *dto = (TrackOut *)e->tout.p;
-    uint32_t *derr = (uint32_t *)e->err.p;
+    const FrameInfo *dfr = (const FrameInfo *)sl.frames.p;
+    const TrackInfo *dtr = (const TrackInfo *)sl.tracks.p;
+    TrackOut *dto = (TrackOut *)sl.tout.p;
+    uint32_t *derr = (uint32_t *)sl.err.p;
+    hipEvent_t *ev = sl.ev;
 
-    HIP_TRY(hipEventRecord(e->ev[14], e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[0], e->s_main));
+    HIP_TRY(hipEventRecord(ev[14], e->s_main));
+    HIP_TRY(hipEventRecord(ev[0], e->s_main));
     HIP_TRY(launch_lpc_analyze(p, d_pcm, fmt, dfr, (const double *)e->windows.p,
-                               (int16_t *)e->coef.p, (int8_t *)e->shift.p,
-                               (uint8_t *)e->est.p, e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[1], e->s_main));
-    // MD5 chains on the aux stream, concurrent with the search and pack
-    // kernels.  They start after the LPC kernel: its grid is only ~1.3
-    // waves per SIMD deep, so a SIMD shared with a (high-priority) chain
-    // would leave straggler waves; the search/pack grids are >60 deep and
-    // absorb it.
-#if ATG_EXP == 10
-    hipStream_t s_md5 = e->s_main; // timing experiment: MD5 alone, serialized
-#else
-    hipStream_t s_md5 = e->s_aux;
-#endif
-    HIP_TRY(hipStreamWaitEvent(s_md5, e->ev[1], 0));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5], s_md5));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, s_md5));
-    HIP_TRY(hipEventRecord(e->ev[2 * 5 + 1], s_md5));
-    HIP_TRY(hipEventRecord(e->ev_md5, s_md5));
-    HIP_TRY(hipEventRecord(e->ev[2], e->s_main));
-    HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)e->coef.p,
-                                   (const int8_t *)e->shift.p, (const uint8_t *)e->est.p,
-                                   (SubDesc *)e->sub.p, derr, e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[3], e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[4], e->s_main));
-    HIP_TRY(launch_frame_decide(p, dfr, (const SubDesc *)e->sub.p, (FrameDesc *)e->fdesc.p,
-                                e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[5], e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[6], e->s_main));
-    HIP_TRY(launch_track_scan(p, dtr, (const uint32_t *)e->order.p, (FrameDesc *)e->fdesc.p,
-                              dto, e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[7], e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[8], e->s_main));
-    HIP_TRY(launch_frame_pack(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)e->sub.p,
-                              (const FrameDesc *)e->fdesc.p, d_out, derr, e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[9], e->s_main));
-    HIP_TRY(hipStreamWaitEvent(e->s_main, e->ev_md5, 0));
-    HIP_TRY(hipEventRecord(e->ev[12], e->s_main));
-    HIP_TRY(launch_stream_header(p, dtr, dto, d_out, e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[13], e->s_main));
-    HIP_TRY(hipEventRecord(e->ev[15], e->s_main));
-
-    tout_h.resize(nt);
-    uint32_t err_h = 0;
-    if (nt)
-        HIP_TRY(hipMemcpyAsync(tout_h.data(), dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost,
+                               (int16_t *)sl.coef.p, (int8_t *)sl.shift.p, (uint8_t *)sl.est.p,
                                e->s_main));
-    if (fdesc_h) {
-        fdesc_h->resize(nf);
-        if (nf)
-            HIP_TRY(hipMemcpyAsync(fdesc_h->data(), e->fdesc.p, nf * sizeof(FrameDesc),
-                                   hipMemcpyDeviceToHost, e->s_main));
-    }
-    HIP_TRY(hipMemcpyAsync(&err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, e->s_main));
-    HIP_TRY(hipStreamSynchronize(e->s_main));
+    HIP_TRY(hipEventRecord(ev[1], e->s_main));
+    // MD5 chains (a serial hash per track, high-priority waves) on the slot's
+    // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
+    // so a SIMD shared with a chain would leave straggler waves; the search
+    // and pack grids are deep enough to absorb them
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
+    HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[2], e->s_main));
+    HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                   (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
+                                   (SubDesc *)sl.sub.p, derr, e->s_main));
+    HIP_TRY(hipEventRecord(ev[3], e->s_main));
+    HIP_TRY(hipEventRecord(ev[4], e->s_main));
+    HIP_TRY(launch_frame_decide(p, dfr, (const SubDesc *)sl.sub.p, (FrameDesc *)sl.fdesc.p,
+                                e->s_main));
+    HIP_TRY(hipEventRecord(ev[5], e->s_main));
+    HIP_TRY(hipEventRecord(ev[6], e->s_main));
+    HIP_TRY(launch_track_scan(p, dtr, (const uint32_t *)sl.order.p, (FrameDesc *)sl.fdesc.p, dto,
+                              e->s_main));
+    HIP_TRY(hipEventRecord(ev[7], e->s_main));
+    HIP_TRY(hipEventRecord(ev[8], e->s_main));
+    HIP_TRY(launch_frame_pack(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
+                              (const FrameDesc *)sl.fdesc.p, d_out, derr, e->s_main));
+    HIP_TRY(hipEventRecord(ev[9], e->s_main));
+    HIP_TRY(hipEventRecord(sl.ev_pack, e->s_main));
+    // headers once both the pack and the MD5 chains are done, on the aux
+    // stream: the main stream goes on with the next batch meanwhile
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
+    HIP_TRY(hipEventRecord(ev[12], sl.s_aux));
+    HIP_TRY(launch_stream_header(p, dtr, dto, d_out, sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[13], sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[15], sl.s_aux));
+    if (nt)
+        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost,
+                               sl.s_aux));
+    if (want_fdesc && nf)
+        HIP_TRY(hipMemcpyAsync(sl.fdesc_h, sl.fdesc.p, nf * sizeof(FrameDesc),
+                               hipMemcpyDeviceToHost, sl.s_aux));
+    HIP_TRY(hipMemcpyAsync(sl.err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.s_aux));
+    HIP_TRY(hipEventRecord(sl.ev_done, sl.s_aux));
+    sl.uploaded = &pl;
+    sl.plan = plp;
+    sl.want_fdesc = want_fdesc;
+    return ATG_OK;
+}
+
+// wait for the slot's batch; records its kernel times and error status
+atg_status finish_batch(atg_engine *e, EncSlot &sl)
+{
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipEventSynchronize(sl.ev_done));
     for (int k = 0; k < kNumTimed; ++k) {
         float ms = 0.f;
-        if (hipEventElapsedTime(&ms, e->ev[2 * k], e->ev[2 * k + 1]) != hipSuccess)
+        if (hipEventElapsedTime(&ms, sl.ev[2 * k], sl.ev[2 * k + 1]) != hipSuccess)
             ms = 0.f;
+        sl.times[k] = ms;
         e->times[k] = ms;
     }
     e->have_times = true;
+    uint32_t err_h = *sl.err_h;
     if (err_h & 1u)
         return fail(ATG_ERR_UNSUPPORTED, "frame longer than the GPU block limit");
 #if ATG_EXP != 0
@@ -461,9 +557,8 @@ atg_status run_batch(atg_engine *e, Plan &pl, bool upload, const void *d_pcm, in
     return ATG_OK;
 }
 
-void fill_results(const Plan &pl, const std::vector<TrackOut> &to, atg_track_result *res,
-                  const std::vector<FrameDesc> *fd, uint64_t *frame_offsets,
-                  uint32_t *frame_pcm)
+void fill_results(const Plan &pl, const TrackOut *to, atg_track_result *res,
+                  const FrameDesc *fd, uint64_t *frame_offsets, uint32_t *frame_pcm)
 {
     for (size_t t = 0; t < pl.tracks.size(); ++t) {
         const TrackInfo &ti = pl.tracks[t];
@@ -481,7 +576,7 @@ void fill_results(const Plan &pl, const std::vector<TrackOut> &to, atg_track_res
             for (uint32_t i = 0; i < ti.n_frames; ++i) {
                 const uint32_t f = pl.order[ti.first_pos + i];
                 if (frame_offsets)
-                    frame_offsets[r.first_frame + i] = (*fd)[f].out_off;
+                    frame_offsets[r.first_frame + i] = fd[f].out_off;
                 if (frame_pcm)
                     frame_pcm[r.first_frame + i] = pl.frames[f].n;
             }
@@ -512,37 +607,61 @@ std::vector<uint8_t> plan_key(const atg_flac_options *o, const atg_track *tracks
     return k;
 }
 
-// plan for this call: the cached one when the geometry repeats (fresh=false:
-// device tables are current), else a new plan that replaces the cache
+// plan for this call: the cached one when the geometry repeats, else a new
+// plan that replaces the cache (slots that ran the old one keep it alive)
 atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *tracks,
                     uint32_t n_tracks, uint32_t channels, uint32_t bps, uint32_t rate,
-                    Plan *&pl, bool &fresh)
+                    std::shared_ptr<Plan> &pl)
 {
     std::vector<uint8_t> key = plan_key(o, tracks, n_tracks, channels, bps, rate);
     if (e->plan_cached && key == e->plan_key) {
-        pl = (Plan *)e->plan_cached;
-        fresh = false;
+        pl = e->plan_cached;
         return ATG_OK;
     }
-    Plan *np = new Plan();
+    auto np = std::make_shared<Plan>();
     atg_status st = make_plan(o, tracks, n_tracks, channels, bps, rate, *np);
-    if (st != ATG_OK) {
-        delete np;
+    if (st != ATG_OK)
         return st;
-    }
-    delete (Plan *)e->plan_cached;
     e->plan_cached = np;
-    e->plan_key.clear();            // valid only once its tables are uploaded
-    e->plan_key_pending.swap(key);  // committed by commit_plan()
+    e->plan_key.swap(key);
     pl = np;
-    fresh = true;
     return ATG_OK;
 }
 
-void commit_plan(atg_engine *e, bool fresh)
+// the slot for a new batch: the one after the last ticket's; a slot still
+// holding an unwaited batch is drained first (its results stay readable)
+atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 {
-    if (fresh)
-        e->plan_key.swap(e->plan_key_pending);
+    ticket = e->next_ticket++;
+    EncSlot &sl = e->slot[ticket & 1u];
+    if (sl.busy) {
+        sl.status = finish_batch(e, sl);
+        sl.error = g_err;
+        sl.busy = false;
+        sl.done = true;
+    }
+    sl.ticket = ticket;
+    sl.done = false;
+    out = &sl;
+    return ATG_OK;
+}
+
+// results of ticket t (waits if still running)
+atg_status wait_ticket(atg_engine *e, uint64_t t, EncSlot *&out)
+{
+    EncSlot &sl = e->slot[t & 1u];
+    if (sl.ticket != t || (!sl.busy && !sl.done))
+        return fail(ATG_ERR_INVALID, "unknown or expired encode ticket");
+    if (sl.busy) {
+        sl.status = finish_batch(e, sl);
+        sl.error = g_err;
+        sl.busy = false;
+        sl.done = true;
+    }
+    out = &sl;
+    if (sl.status != ATG_OK)
+        return fail(sl.status, sl.error);
+    return ATG_OK;
 }
 
 } // namespace
@@ -567,11 +686,20 @@ atg_status atg_engine_create(int device, atg_engine **out)
     atg_engine *e = new atg_engine();
     e->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&e->s_aux, hipStreamNonBlocking));
-    for (auto &ev : e->ev)
-        HIP_TRY(hipEventCreate(&ev));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_tables, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&e->ev_md5, hipEventDisableTiming));
+    for (EncSlot &sl : e->slot) {
+        HIP_TRY(hipStreamCreateWithFlags(&sl.s_aux, hipStreamNonBlocking));
+        for (auto &ev : sl.ev)
+            HIP_TRY(hipEventCreate(&ev));
+        HIP_TRY(hipEventCreateWithFlags(&sl.ev_tables, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&sl.ev_pack, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+    }
+    HIP_TRY(hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking));
+    HIP_TRY(hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking));
+    for (int k = 0; k < 2; ++k) {
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_h2d[k], hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&e->ev_d2h[k], hipEventDisableTiming));
+    }
     static uint32_t t16[4][256], t8[256];
     static uint16_t adv[24][16];
     build_crc_tables(t16, t8, adv);
@@ -586,17 +714,40 @@ void atg_engine_destroy(atg_engine *e)
         return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->s_main);
-    (void)hipStreamSynchronize(e->s_aux);
-    for (DevBuf *b : {&e->frames, &e->tracks, &e->order, &e->windows, &e->coef, &e->shift, &e->est,
-                      &e->sub, &e->fdesc, &e->tout, &e->err, &e->h_pcm, &e->h_out})
-        b->release();
-    for (auto &ev : e->ev)
-        (void)hipEventDestroy(ev);
-    (void)hipEventDestroy(e->ev_tables);
-    (void)hipEventDestroy(e->ev_md5);
-    delete (Plan *)e->plan_cached;
+    for (EncSlot &sl : e->slot) {
+        (void)hipStreamSynchronize(sl.s_aux);
+        for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
+                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err})
+            b->release();
+        for (auto &ev : sl.ev)
+            (void)hipEventDestroy(ev);
+        (void)hipEventDestroy(sl.ev_tables);
+        (void)hipEventDestroy(sl.ev_pack);
+        (void)hipEventDestroy(sl.ev_done);
+        if (sl.tout_h)
+            (void)hipHostFree(sl.tout_h);
+        if (sl.fdesc_h)
+            (void)hipHostFree(sl.fdesc_h);
+        if (sl.err_h)
+            (void)hipHostFree(sl.err_h);
+        (void)hipStreamDestroy(sl.s_aux);
+    }
+    (void)hipStreamSynchronize(e->s_h2d);
+    (void)hipStreamSynchronize(e->s_d2h);
+    for (int k = 0; k < 2; ++k) {
+        e->d_pcm[k].release();
+        e->d_img[k].release();
+        if (e->p_in[k])
+            (void)hipHostFree(e->p_in[k]);
+        if (e->p_out[k])
+            (void)hipHostFree(e->p_out[k]);
+        (void)hipEventDestroy(e->ev_h2d[k]);
+        (void)hipEventDestroy(e->ev_d2h[k]);
+    }
+    (void)hipStreamDestroy(e->s_h2d);
+    (void)hipStreamDestroy(e->s_d2h);
+    e->windows.release();
     (void)hipStreamDestroy(e->s_main);
-    (void)hipStreamDestroy(e->s_aux);
     delete e;
 }
 
@@ -615,6 +766,52 @@ atg_status atg_flac_batch_bounds(const atg_flac_options *opts, const atg_track *
     return ATG_OK;
 }
 
+atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *opts,
+                                        const void *d_pcm, atg_pcm_format format,
+                                        const atg_track *tracks, uint32_t n_tracks,
+                                        uint32_t channels, uint32_t bps, uint32_t rate,
+                                        void *d_out, uint64_t out_cap, uint64_t *ticket)
+{
+    if (!e || (!tracks && n_tracks) || !ticket)
+        return fail(ATG_ERR_INVALID, "NULL argument");
+    if (format == ATG_PCM_S16 && bps > 16)
+        return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
+    std::shared_ptr<Plan> pl;
+    atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, pl);
+    if (st != ATG_OK)
+        return st;
+    EncSlot *sl = nullptr;
+    uint64_t t = 0;
+    st = take_slot(e, sl, t);
+    if (st != ATG_OK)
+        return st;
+    st = enqueue_batch(e, *sl, pl, d_pcm, (int)format, (uint8_t *)d_out, out_cap, false);
+    if (st != ATG_OK) {
+        // nothing of this batch may be relied on: drain what was queued
+        (void)hipStreamSynchronize(e->s_main);
+        (void)hipStreamSynchronize(sl->s_aux);
+        sl->uploaded = nullptr;
+        sl->ticket = 0;
+        return st;
+    }
+    sl->busy = true;
+    *ticket = t;
+    return ATG_OK;
+}
+
+atg_status atg_flac_encode_wait(atg_engine *e, uint64_t ticket, atg_track_result *results)
+{
+    if (!e)
+        return fail(ATG_ERR_INVALID, "NULL engine");
+    EncSlot *sl = nullptr;
+    atg_status st = wait_ticket(e, ticket, sl);
+    if (st != ATG_OK)
+        return st;
+    if (results)
+        fill_results(*sl->plan, sl->tout_h, results, nullptr, nullptr, nullptr);
+    return ATG_OK;
+}
+
 atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
                                   const void *d_pcm, atg_pcm_format format,
                                   const atg_track *tracks, uint32_t n_tracks,
@@ -623,22 +820,12 @@ atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
 {
     if (!e || (!tracks && n_tracks) || (!results && n_tracks))
         return fail(ATG_ERR_INVALID, "NULL argument");
-    if (format == ATG_PCM_S16 && bps > 16)
-        return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    Plan *pl = nullptr;
-    bool fresh = true;
-    atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, pl, fresh);
+    uint64_t t = 0;
+    atg_status st = atg_flac_encode_device_async(e, opts, d_pcm, format, tracks, n_tracks,
+                                                 channels, bps, rate, d_out, out_cap, &t);
     if (st != ATG_OK)
         return st;
-    std::vector<TrackOut> to;
-    st = run_batch(e, *pl, fresh, d_pcm, (int)format, (uint8_t *)d_out, out_cap, to, nullptr);
-    if (st != ATG_OK) {
-        e->plan_key.clear(); // tables may not be on the device
-        return st;
-    }
-    commit_plan(e, fresh);
-    fill_results(*pl, to, results, nullptr, nullptr, nullptr);
-    return ATG_OK;
+    return atg_flac_encode_wait(e, t, results);
 }
 
 atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, const void *pcm,
@@ -652,43 +839,174 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    Plan *plp = nullptr;
-    bool fresh = true;
-    atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, plp, fresh);
+    // the whole batch's layout (what atg_flac_batch_bounds sized)
+    Plan whole;
+    atg_status st = make_plan(opts, tracks, n_tracks, channels, bps, rate, whole);
     if (st != ATG_OK)
         return st;
-    Plan &pl = *plp;
-    if (pl.out_bytes > out_cap) {
-        e->plan_key.clear();
+    if (whole.out_bytes > out_cap)
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
-    }
-    uint64_t samples = 0;
-    for (uint32_t t = 0; t < n_tracks; ++t)
-        samples = std::max<uint64_t>(samples, (tracks[t].pcm_offset + tracks[t].pcm_frames) *
-                                                  channels);
     const size_t elem = format == ATG_PCM_S16 ? 2 : 4;
     HIP_TRY(hipSetDevice(e->device));
-    HIP_TRY(e->h_pcm.ensure(samples * elem + 16));
-    HIP_TRY(e->h_out.ensure(pl.out_bytes + 16));
-    if (samples)
-        HIP_TRY(hipMemcpyAsync(e->h_pcm.p, pcm, samples * elem, hipMemcpyHostToDevice,
-                               e->s_main));
-    std::vector<TrackOut> to;
-    std::vector<FrameDesc> fd;
-    st = run_batch(e, pl, fresh, e->h_pcm.p, (int)format, (uint8_t *)e->h_out.p, e->h_out.cap,
-                   to, &fd);
-    if (st != ATG_OK) {
-        e->plan_key.clear(); // tables may not be on the device
-        return st;
+    // the slots' device state is reused below: drain any batch in flight
+    for (EncSlot &s2 : e->slot)
+        if (s2.busy) {
+            s2.status = finish_batch(e, s2);
+            s2.error = g_err;
+            s2.busy = false;
+            s2.done = true;
+        }
+
+    // chunks of consecutive tracks, ~chunk_bytes of PCM each (ATG_HOST_CHUNK_MB
+    // overrides the size, for tests)
+    if (const char *cb = std::getenv("ATG_HOST_CHUNK_MB"))
+        e->chunk_bytes = std::max<uint64_t>(1, std::strtoull(cb, nullptr, 10)) << 20;
+    struct Chunk {
+        uint32_t t0, t1;          // tracks [t0, t1)
+        uint64_t pcm0, samples;   // first sample and samples of the chunk's PCM span
+        uint64_t frame0;          // first frame (global numbering)
+        std::vector<atg_track> tr;
+        std::shared_ptr<Plan> plan;
+        uint64_t ticket = 0;
+        uint64_t img_bytes = 0;   // image span downloaded
+    };
+    std::vector<Chunk> chunks;
+    {
+        uint32_t t = 0;
+        uint64_t frame0 = 0;
+        while (t < n_tracks) {
+            Chunk c;
+            c.t0 = t;
+            uint64_t lo = UINT64_MAX, hi = 0;
+            do {
+                lo = std::min<uint64_t>(lo, tracks[t].pcm_offset * channels);
+                hi = std::max<uint64_t>(hi, (tracks[t].pcm_offset + tracks[t].pcm_frames) *
+                                                channels);
+                ++t;
+            } while (t < n_tracks && (hi - std::min<uint64_t>(lo, tracks[t].pcm_offset * channels) +
+                                      tracks[t].pcm_frames * channels) * elem <= e->chunk_bytes);
+            c.t1 = t;
+            c.pcm0 = lo == UINT64_MAX ? 0 : lo;
+            c.samples = hi > c.pcm0 ? hi - c.pcm0 : 0;
+            c.frame0 = frame0;
+            for (uint32_t k = c.t0; k < c.t1; ++k) {
+                atg_track a = tracks[k];
+                a.pcm_offset -= c.pcm0 / channels;
+                c.tr.push_back(a);
+                frame0 += whole.tracks[k].n_frames;
+            }
+            c.plan = std::make_shared<Plan>();
+            st = make_plan(opts, c.tr.data(), (uint32_t)c.tr.size(), channels, bps, rate, *c.plan);
+            if (st != ATG_OK)
+                return st;
+            chunks.push_back(std::move(c));
+        }
     }
-    for (size_t t = 0; t < pl.tracks.size(); ++t)
-        if (to[t].bytes)
-            HIP_TRY(hipMemcpyAsync(out + pl.tracks[t].out_base,
-                                   (uint8_t *)e->h_out.p + pl.tracks[t].out_base, to[t].bytes,
-                                   hipMemcpyDeviceToHost, e->s_main));
-    HIP_TRY(hipStreamSynchronize(e->s_main));
-    commit_plan(e, fresh);
-    fill_results(pl, to, results, &fd, frame_offsets, frame_pcm_frames);
+
+    // finish chunk ci (slot ci & 1): wait, download its images, copy them and
+    // its results into the caller's arrays
+    auto collect = [&](size_t ci) -> atg_status {
+        Chunk &c = chunks[ci];
+        const int k = (int)(ci & 1u);
+        EncSlot *sl = nullptr;
+        atg_status s2 = wait_ticket(e, c.ticket, sl);
+        if (s2 != ATG_OK)
+            return s2;
+        const Plan &cp = *c.plan;
+        uint64_t span = 0;
+        for (size_t j = 0; j < cp.tracks.size(); ++j)
+            span = std::max<uint64_t>(span, cp.tracks[j].out_base + sl->tout_h[j].bytes);
+        c.img_bytes = span;
+        if (span)
+            HIP_TRY(hipMemcpyAsync(e->p_out[k], e->d_img[k].p, span, hipMemcpyDeviceToHost,
+                                   e->s_d2h));
+        HIP_TRY(hipEventRecord(e->ev_d2h[k], e->s_d2h));
+        HIP_TRY(hipEventSynchronize(e->ev_d2h[k]));
+        {
+            // the chunk's images to the caller's layout, in parallel
+            std::vector<std::thread> th;
+            const unsigned nt = std::min<unsigned>(
+                16, std::max(1u, std::thread::hardware_concurrency()));
+            const size_t nj = cp.tracks.size();
+            for (unsigned w = 0; w < nt && w < nj; ++w)
+                th.emplace_back([&, w] {
+                    for (size_t j = w; j < nj; j += nt)
+                        std::memcpy(out + whole.tracks[c.t0 + j].out_base,
+                                    e->p_out[k] + cp.tracks[j].out_base, sl->tout_h[j].bytes);
+                });
+            for (auto &t : th)
+                t.join();
+        }
+        for (size_t j = 0; j < cp.tracks.size(); ++j) {
+            const uint32_t t = c.t0 + (uint32_t)j;
+            const TrackOut &to = sl->tout_h[j];
+            atg_track_result &r = results[t];
+            r.out_offset = whole.tracks[t].out_base;
+            r.bytes = to.bytes;
+            r.first_frame = whole.track_frame_pos[t];
+            r.n_frames = whole.tracks[t].n_frames;
+            r.min_frame_bytes = to.min_fs;
+            r.max_frame_bytes = to.max_fs;
+            std::memcpy(r.md5, to.md5, 16);
+            r.status = 0;
+            r.reserved = 0;
+            const TrackInfo &ti = cp.tracks[j];
+            for (uint32_t i = 0; i < ti.n_frames; ++i) {
+                const uint32_t f = cp.order[ti.first_pos + i];
+                if (frame_offsets)
+                    frame_offsets[r.first_frame + i] = sl->fdesc_h[f].out_off;
+                if (frame_pcm_frames)
+                    frame_pcm_frames[r.first_frame + i] = cp.frames[f].n;
+            }
+        }
+        return ATG_OK;
+    };
+
+    for (size_t ci = 0; ci < chunks.size(); ++ci) {
+        Chunk &c = chunks[ci];
+        const int k = (int)(ci & 1u);
+        const uint64_t in_bytes = c.samples * elem;
+        HIP_TRY(e->d_pcm[k].ensure(in_bytes + 16));
+        HIP_TRY(e->d_img[k].ensure(c.plan->out_bytes + 16));
+        HIP_TRY(ensure_pinned(e->p_in[k], e->p_in_cap[k], in_bytes + 16));
+        HIP_TRY(ensure_pinned(e->p_out[k], e->p_out_cap[k], c.plan->out_bytes + 16));
+        // stage through pinned memory (the caller's buffer is pageable)
+        if (in_bytes)
+            par_memcpy(e->p_in[k], (const uint8_t *)pcm + c.pcm0 * elem, in_bytes);
+        if (in_bytes)
+            HIP_TRY(hipMemcpyAsync(e->d_pcm[k].p, e->p_in[k], in_bytes, hipMemcpyHostToDevice,
+                                   e->s_h2d));
+        HIP_TRY(hipEventRecord(e->ev_h2d[k], e->s_h2d));
+        EncSlot *sl = nullptr;
+        uint64_t ticket = 0;
+        st = take_slot(e, sl, ticket);
+        if (st == ATG_OK)
+            st = enqueue_batch(e, *sl, c.plan, e->d_pcm[k].p, (int)format,
+                               (uint8_t *)e->d_img[k].p, e->d_img[k].cap, true, e->ev_h2d[k]);
+        if (st != ATG_OK) {
+            (void)hipDeviceSynchronize();
+            if (sl) {
+                sl->uploaded = nullptr;
+                sl->ticket = 0;
+            }
+            return st;
+        }
+        sl->busy = true;
+        c.ticket = ticket;
+        // chunk ci-1's results come back while chunk ci encodes
+        if (ci >= 1) {
+            st = collect(ci - 1);
+            if (st != ATG_OK) {
+                (void)hipDeviceSynchronize();
+                return st;
+            }
+        }
+    }
+    if (!chunks.empty()) {
+        st = collect(chunks.size() - 1);
+        if (st != ATG_OK)
+            return st;
+    }
     return ATG_OK;
 }
 
@@ -731,6 +1049,15 @@ atg_status atg_copy_to_device(atg_engine *e, void *d_dst, const void *src, uint6
         return fail(ATG_ERR_INVALID, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));
     HIP_TRY(hipMemcpy(d_dst, src, bytes, hipMemcpyHostToDevice));
+    return ATG_OK;
+}
+
+atg_status atg_copy_device(atg_engine *e, void *d_dst, const void *d_src, uint64_t bytes)
+{
+    if (!e)
+        return fail(ATG_ERR_INVALID, "NULL engine");
+    HIP_TRY(hipSetDevice(e->device));
+    HIP_TRY(hipMemcpy(d_dst, d_src, bytes, hipMemcpyDeviceToDevice));
     return ATG_OK;
 }
 

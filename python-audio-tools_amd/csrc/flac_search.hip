@@ -35,6 +35,14 @@
 #ifndef ATG_EXP
 #define ATG_EXP 0
 #endif
+// partition-order search: DPP butterflies (1) or lane shuffles (0)
+#ifndef ATG_K2_SEL_DPP
+#define ATG_K2_SEL_DPP 0
+#endif
+// waves per SIMD the register allocation targets
+#ifndef ATG_K2_WPE
+#define ATG_K2_WPE 2
+#endif
 
 // Rice parameter of one partition: the reference's loop
 //   while ((uint64_t)(plength << Rice) < sum) if (Rice < max) Rice++; else break;
@@ -81,25 +89,6 @@ struct PartSel {
     uint32_t hdr_bits;
 };
 
-// wave primitives on 32- or 64-bit values
-__device__ __forceinline__ uint32_t wshfl_up(uint32_t v, int d)
-{
-    return (uint32_t)__shfl_up((int)v, d, 64);
-}
-__device__ __forceinline__ uint64_t wshfl_up(uint64_t v, int d) { return shfl_up_u64(v, d); }
-__device__ __forceinline__ uint32_t wshfl(uint32_t v, int src)
-{
-    return (uint32_t)__shfl((int)v, src, 64);
-}
-__device__ __forceinline__ uint64_t wshfl(uint64_t v, int src) { return shfl_u64(v, src); }
-__device__ __forceinline__ uint32_t wshfl_xor(uint32_t v, int m) { return shfl_xor_u32(v, m); }
-__device__ __forceinline__ uint64_t wshfl_xor(uint64_t v, int m) { return shfl_xor_u64(v, m); }
-__device__ __forceinline__ uint32_t wreadlane(uint32_t v, int l)
-{
-    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
-}
-__device__ __forceinline__ uint64_t wreadlane(uint64_t v, int l) { return readlane_u64(v, l); }
-
 // Estimated bits of one partition (flac.c:1437-1505).  S = uint64_t is the
 // reference's accumulator; S = uint32_t gives the same values whenever the
 // subframe's sum |r| < 2^31 (then no term or total reaches 2^32).
@@ -123,6 +112,111 @@ __device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, S Sj, S total
     k = rice_param(plen, (uint64_t)sum, c.max_rice);
     e = part_estimate<S>(plen, sum, k);
 }
+
+#if ATG_K2_SEL_DPP
+// flacenc_encode_residuals' partition-order search (flac.c:1362-1402) from
+// per-lane |r| sums; the level-lv partition of lane l is l >> (6 - lv).
+// Partition sums of every level come from DPP butterflies (no LDS round
+// trips): after s steps every lane holds the sum of its aligned 2^s-lane
+// group, i.e. its level-(6-s) partition; the four 16-lane row sums are
+// read into SGPRs for levels 1 and 0.  Levels 0..2 (1, 2, 4 partitions)
+// are estimated on those scalars, levels 3..6 in the lanes, one estimate
+// per partition taken from its first lane.  The level with the smallest
+// total wins, the lowest level on ties (strict <), as in the reference.
+template <typename S>
+__device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t order,
+                                                       const RunCtx &c)
+{
+    const int lane = c.lane;
+    const S g6 = lane_sum;
+    const S g5 = dpp_group_sum<1>(g6);
+    const S g4 = g5 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_QUAD_SWAP2>((uint64_t)g5)
+                                      : (S)dpp_u32<DPP_QUAD_SWAP2>((uint32_t)g5));
+    const S g3 = g4 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_ROW_HALF_MIRROR>((uint64_t)g4)
+                                      : (S)dpp_u32<DPP_ROW_HALF_MIRROR>((uint32_t)g4));
+    const S g2 = g3 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_ROW_MIRROR>((uint64_t)g3)
+                                      : (S)dpp_u32<DPP_ROW_MIRROR>((uint32_t)g3));
+    const S r0 = rd_lane(g2, 0), r1 = rd_lane(g2, 16), r2 = rd_lane(g2, 32), r3 = rd_lane(g2, 48);
+    const S h0 = r0 + r1, h1 = r2 + r3;
+    const S total = h0 + h1;
+
+    // levels 0..2 on scalars
+    uint32_t k0, k1a, k1b, k2[4];
+    S e0, e1a, e1b, e2[4];
+    part_eval<S>(0, 0, total, total, order, c, k0, e0);
+    part_eval<S>(1, 0, h0, total, order, c, k1a, e1a);
+    part_eval<S>(1, 1, h1, total, order, c, k1b, e1b);
+    part_eval<S>(2, 0, r0, total, order, c, k2[0], e2[0]);
+    part_eval<S>(2, 1, r1, total, order, c, k2[1], e2[1]);
+    part_eval<S>(2, 2, r2, total, order, c, k2[2], e2[2]);
+    part_eval<S>(2, 3, r3, total, order, c, k2[3], e2[3]);
+    S T[7];
+    T[0] = e0;
+    T[1] = e1a + e1b;
+    T[2] = (e2[0] + e2[1]) + (e2[2] + e2[3]);
+    // levels 3..6 in the lanes
+    uint32_t k3, k4, k5, k6;
+    S e3, e4, e5, e6;
+    part_eval<S>(3, (uint32_t)lane >> 3, g3, total, order, c, k3, e3);
+    part_eval<S>(4, (uint32_t)lane >> 2, g4, total, order, c, k4, e4);
+    part_eval<S>(5, (uint32_t)lane >> 1, g5, total, order, c, k5, e5);
+    part_eval<S>(6, (uint32_t)lane, g6, total, order, c, k6, e6);
+    T[3] = dpp_wave_sum<S>((lane & 7) == 0 ? e3 : (S)0);
+    T[4] = dpp_wave_sum<S>((lane & 3) == 0 ? e4 : (S)0);
+    T[5] = dpp_wave_sum<S>((lane & 1) == 0 ? e5 : (S)0);
+    T[6] = dpp_wave_sum<S>(e6);
+
+    S best_tot = (S)~(S)0;
+    uint32_t best_p = 0;
+#pragma unroll
+    for (int lv = 0; lv <= 6; ++lv) {
+        if (lv <= c.P && T[lv] < best_tot) {
+            best_tot = T[lv];
+            best_p = (uint32_t)lv;
+        }
+    }
+    PartSel r;
+    r.porder = best_p;
+    uint32_t ko;
+    switch (best_p) {
+    case 0: ko = k0; break;
+    case 1: ko = lane < 32 ? k1a : k1b; break;
+    case 2: ko = lane < 16 ? k2[0] : lane < 32 ? k2[1] : lane < 48 ? k2[2] : k2[3]; break;
+    case 3: ko = k3; break;
+    case 4: ko = k4; break;
+    case 5: ko = k5; break;
+    default: ko = k6; break;
+    }
+    r.k_own = ko;
+    const bool degen_best = (c.N >> best_p) < order;
+    const uint32_t kfirst = (uint32_t)__builtin_amdgcn_readfirstlane((int)ko);
+    r.k_lane = degen_best ? kfirst : ko;
+    r.method = 0;
+    if (c.max_rice > 14u)
+        r.method = dpp_wave_max_u32(ko) > 14u ? 1u : 0u;
+    r.hdr_bits = 6u + (1u << best_p) * (r.method ? 5u : 4u);
+    return r;
+}
+
+#else
+// wave primitives on 32- or 64-bit values
+__device__ __forceinline__ uint32_t wshfl_up(uint32_t v, int d)
+{
+    return (uint32_t)__shfl_up((int)v, d, 64);
+}
+__device__ __forceinline__ uint64_t wshfl_up(uint64_t v, int d) { return shfl_up_u64(v, d); }
+__device__ __forceinline__ uint32_t wshfl(uint32_t v, int src)
+{
+    return (uint32_t)__shfl((int)v, src, 64);
+}
+__device__ __forceinline__ uint64_t wshfl(uint64_t v, int src) { return shfl_u64(v, src); }
+__device__ __forceinline__ uint32_t wshfl_xor(uint32_t v, int m) { return shfl_xor_u32(v, m); }
+__device__ __forceinline__ uint64_t wshfl_xor(uint64_t v, int m) { return shfl_xor_u64(v, m); }
+__device__ __forceinline__ uint32_t wreadlane(uint32_t v, int l)
+{
+    return (uint32_t)__builtin_amdgcn_readlane((int)v, l);
+}
+__device__ __forceinline__ uint64_t wreadlane(uint64_t v, int l) { return readlane_u64(v, l); }
 
 // flacenc_encode_residuals' partition-order search (flac.c:1362-1402) from
 // per-lane |r| sums; level lv partition of lane l is l >> (6 - lv).
@@ -199,6 +293,8 @@ __device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t orde
     r.hdr_bits = 6u + (1u << best_p) * (r.method ? 5u : 4u);
     return r;
 }
+
+#endif
 
 // `small`: the subframe's sum |r| is known to be < 2^31 (32-bit search)
 __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order,
@@ -365,7 +461,7 @@ __device__ __forceinline__ Eval eval_generic(const int32_t *__restrict__ sl, con
         const int r = (int)((uint32_t)sl[saddr(i)] - (uint32_t)(int32_t)(acc >> shift));
         lb += (zigzag(r) >> k) + 1u + k;
     }
-    ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
+    ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
     return ev;
 }
 
@@ -425,7 +521,7 @@ __device__ __forceinline__ Eval eval_fast_any(const int32_t *sl, const RunCtx &c
         for (int t = 0; t < ATG_RUN; t += 2)
             lb = lb + (u[t] >> k) + (u[t + 1] >> k); // v_add3_u32
     }
-    ev.bits = wave_sum_u32(lb) + ev.sel.hdr_bits;
+    ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
     return ev;
 }
 
@@ -444,7 +540,7 @@ __device__ __forceinline__ int fixed_tap(uint32_t o, int j)
 __device__ __forceinline__ uint32_t wasted_field(uint32_t w) { return w ? w + 1u : 1u; }
 
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_subframe_search(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2_WPE))) void k_subframe_search(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
@@ -484,7 +580,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                             amax = max(amax, iabs_u(s));
                             same = same && (s == first);
                         });
-    orv = wave_or_u32(orv);
+    orv = dpp_wave_or_u32(orv);
     same = wave_all(same);
     __syncthreads();
 
@@ -504,7 +600,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
     }
     const uint32_t w = orv ? (uint32_t)__builtin_ctz(orv) : 0u;
     // every sample is a multiple of 2^w, so max|s >> w| = max|s| >> w
-    const uint32_t maxabs = wave_max_u32(amax) >> w;
+    const uint32_t maxabs = dpp_wave_max_u32(amax) >> w;
     if (w) {
         for (uint32_t i = lane; i < N; i += 64)
             sl[saddr((int)i)] >>= w;
@@ -608,7 +704,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         }
 #pragma unroll
         for (int k = 0; k < 5; ++k)
-            s5[k] = wave_sum_u64(s5[k]);
+            s5[k] = dpp_wave_sum<uint64_t>(s5[k]);
         uint64_t best = s5[0];
         if (N > 4) {
 #pragma unroll

@@ -113,6 +113,64 @@ __device__ __forceinline__ uint32_t pcm_byte(const T *s, uint64_t j, uint32_t bb
     return ((uint32_t)(int32_t)s[k] >> (8u * r)) & 0xFFu;
 }
 
+// The little-endian byte stream of G int32 samples of BB bytes each, as
+// MD5 words (v_perm_b32 picks the bytes): BB = 3 -> 64 samples, 48 words
+// (3 blocks); BB = 2 -> 32 samples, 16 words; BB = 1 -> 64 samples, 16 words.
+template <int BB>
+struct S32Pack {
+    static constexpr int G = BB == 2 ? 32 : 64;   // samples per group
+    static constexpr int W = G * BB / 4;          // words per group
+    static constexpr int Q = G / 4;               // uint4 loads per group
+    __device__ static __forceinline__ void pack(const uint4 (&v)[Q], uint32_t (&w)[W])
+    {
+#pragma unroll
+        for (int q = 0; q < Q; ++q) {
+            const uint32_t s0 = v[q].x, s1 = v[q].y, s2 = v[q].z, s3 = v[q].w;
+            if constexpr (BB == 3) {
+                w[3 * q] = __builtin_amdgcn_perm(s1, s0, 0x04020100u);
+                w[3 * q + 1] = __builtin_amdgcn_perm(s2, s1, 0x05040201u);
+                w[3 * q + 2] = __builtin_amdgcn_perm(s3, s2, 0x06050402u);
+            } else if constexpr (BB == 2) {
+                w[2 * q] = __builtin_amdgcn_perm(s1, s0, 0x05040100u);
+                w[2 * q + 1] = __builtin_amdgcn_perm(s3, s2, 0x05040100u);
+            } else {
+                const uint32_t lo = __builtin_amdgcn_perm(s1, s0, 0x0C0C0400u);
+                const uint32_t hi = __builtin_amdgcn_perm(s3, s2, 0x04000C0Cu);
+                w[q] = lo | hi;
+            }
+        }
+    }
+};
+
+// hash `groups` whole groups of int32 samples from q (16-byte aligned), one
+// group's loads in flight while the previous group is hashed
+template <int BB>
+__device__ __forceinline__ void md5_s32_groups(uint32_t h[4], const uint4 *__restrict__ q,
+                                               uint64_t groups)
+{
+    using P = S32Pack<BB>;
+    if (!groups)
+        return;
+    uint4 cur[P::Q], nxt[P::Q];
+#pragma unroll
+    for (int i = 0; i < P::Q; ++i)
+        cur[i] = q[i];
+    for (uint64_t g = 0; g < groups; ++g) {
+        const uint64_t ng = min(g + 1u, groups - 1u);
+#pragma unroll
+        for (int i = 0; i < P::Q; ++i)
+            nxt[i] = q[ng * P::Q + i];
+        uint32_t w[P::W];
+        P::pack(cur, w);
+#pragma unroll
+        for (int b = 0; b < P::W / 16; ++b)
+            md5_compress(h, &w[16 * b]);
+#pragma unroll
+        for (int i = 0; i < P::Q; ++i)
+            cur[i] = nxt[i];
+    }
+}
+
 template <typename T>
 __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restrict__ pcm,
                                                   const TrackInfo *__restrict__ tracks,
@@ -171,7 +229,27 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
             }
         }
     } else if (!raw) {
-        for (uint64_t blk = 0; blk < full; ++blk) {
+        // int32 container, 16-byte aligned: whole sample groups by v_perm
+        // packing; the bytes after the last whole group go the generic way
+        uint64_t blk = 0;
+        if (sizeof(T) == 4 && (((uintptr_t)s) & 15u) == 0 && bb >= 1 && bb <= 3) {
+            const uint64_t samples = ti.pcm_frames * p.channels;
+            const uint4 *q = (const uint4 *)s;
+            if (bb == 3) {
+                const uint64_t g = samples / S32Pack<3>::G;
+                md5_s32_groups<3>(h, q, g);
+                blk = g * 3u;
+            } else if (bb == 2) {
+                const uint64_t g = samples / S32Pack<2>::G;
+                md5_s32_groups<2>(h, q, g);
+                blk = g;
+            } else {
+                const uint64_t g = samples / S32Pack<1>::G;
+                md5_s32_groups<1>(h, q, g);
+                blk = g;
+            }
+        }
+        for (; blk < full; ++blk) {
             for (int i = 0; i < 16; ++i) {
                 const uint64_t j = blk * 64u + 4u * (uint32_t)i;
                 X[i] = pcm_byte(s, j, bb) | (pcm_byte(s, j + 1, bb) << 8) |

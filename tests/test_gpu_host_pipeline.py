@@ -1,0 +1,94 @@
+"""GPU: the chunked, overlapped host-memory encode (atg_flac_encode_host):
+tracks are cut into chunks of ~ATG_HOST_CHUNK_MB of PCM, staged through
+pinned buffers, and chunk c's upload / encode / chunk c-1's download
+overlap.  Every image and frame offset must equal the CPU port's, whatever
+the chunking, track order in memory or explicit frame sizes."""
+import os
+
+import numpy as np
+import pytest
+
+import oracle_port
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine():
+    from audiotools import _atgpu
+    return _atgpu.engine(), _atgpu
+
+
+def _tracks(rng, n, lo, hi):
+    lens = [int(rng.integers(lo, hi)) for _ in range(n)]
+    parts = []
+    for k, m in enumerate(lens):
+        t = np.arange(m)
+        x = (6000 * np.sin(2 * np.pi * (180 + 40 * k) * t / 44100)).astype(np.int64)
+        x = np.stack([x, (x * 3) // 4 + rng.integers(-300, 300, m)], 1)
+        parts.append(np.clip(x, -32768, 32767).astype(np.int16).reshape(-1))
+    return lens, parts
+
+
+@pytest.mark.parametrize("chunk_mb", ["1", "3", "4096"])
+def test_chunked_host_encode_matches_port(chunk_mb, monkeypatch):
+    eng, A = _engine()
+    monkeypatch.setenv("ATG_HOST_CHUNK_MB", chunk_mb)
+    rng = np.random.default_rng(int(chunk_mb))
+    lens, parts = _tracks(rng, 19, 20000, 160000)
+    # tracks stored out of order, with gaps between them
+    order = rng.permutation(len(parts))
+    buf, where, pos = [], {}, 0
+    for k in order:
+        buf.append(np.zeros(2 * int(rng.integers(0, 50)), np.int16))
+        pos += len(buf[-1]) // 2
+        where[int(k)] = pos
+        buf.append(parts[k])
+        pos += lens[k]
+    pcm = np.concatenate(buf)
+    tracks = [(where[k], lens[k]) for k in range(len(parts))]
+    opts = A.make_options(**oracle_port.PRESETS["8"])
+    out, res, offs, fpcm = eng.encode(opts, pcm, tracks, 2, 16, 44100)
+    for k in range(len(parts)):
+        want, woffs = oracle_port.encode(parts[k].astype(np.int32), 2, 16, 44100,
+                                         **oracle_port.PRESETS["8"])
+        r = res[k]
+        assert bytes(out[r.out_offset:r.out_offset + r.bytes]) == want, k
+        got = [(int(offs[r.first_frame + i]), int(fpcm[r.first_frame + i]))
+               for i in range(r.n_frames)]
+        assert got == woffs, k
+
+
+def test_chunked_host_encode_explicit_frame_sizes(monkeypatch):
+    eng, A = _engine()
+    monkeypatch.setenv("ATG_HOST_CHUNK_MB", "1")
+    rng = np.random.default_rng(5)
+    lens, parts = _tracks(rng, 6, 150000, 200000)
+    pcm = np.concatenate(parts)
+    tracks, base = [], 0
+    for k, m in enumerate(lens):
+        sizes = []
+        left = m
+        while left:
+            s = min(left, int(rng.choice([1152, 4096, 777])))
+            sizes.append(s)
+            left -= s
+        tracks.append((base, m, sizes) if k % 2 else (base, m))
+        base += m
+    opts = A.make_options(**oracle_port.PRESETS["8"])
+    out, res, offs, fpcm = eng.encode(opts, pcm, tracks, 2, 16, 44100)
+    monkeypatch.setenv("ATG_HOST_CHUNK_MB", "4096")
+    out1, res1, offs1, fpcm1 = eng.encode(opts, pcm, tracks, 2, 16, 44100)
+    assert np.array_equal(offs, offs1) and np.array_equal(fpcm, fpcm1)
+    for k in range(len(parts)):
+        r, r1 = res[k], res1[k]
+        img = bytes(out[r.out_offset:r.out_offset + r.bytes])
+        # chunked == one chunk, byte for byte
+        assert img == bytes(out1[r1.out_offset:r1.out_offset + r1.bytes]), k
+        got = [int(fpcm[r.first_frame + i]) for i in range(r.n_frames)]
+        if k % 2:
+            assert got == tracks[k][2]
+        else:
+            assert sum(got) == lens[k] and max(got) == 4096
+            # default framing: the image decodes back to the source exactly
+            pcm_dec = oracle_port.decode(img)[0]
+            assert np.array_equal(pcm_dec, parts[k].astype(np.int32))

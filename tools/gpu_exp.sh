@@ -1,11 +1,13 @@
 #!/bin/bash
 # GPU-box recipe: time experiment builds (exp/libatgpu_e*.so, not byte-exact)
+# next to the product library; encoder leg only.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p "$R/gpurun_out/exp"
 cd "$R"
-for lib in exp/libatgpu_e*.so; do
+ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-decode --no-chain --no-host"
+timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/exp/base.log 2>&1
+for lib in exp/libatgpu_*.so; do
     n=$(basename $lib .so)
-    ATGPU_LIB=$R/$lib timeout -k 10 120 python -u bench.py --steps 3 --warmup 1 --no-cpu-baseline --no-verify \
-        > gpurun_out/exp/$n.log 2>&1
+    ATGPU_LIB=$R/$lib timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/exp/$n.log 2>&1
 done
