@@ -531,8 +531,10 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     t = torch.arange(n_in, device=device, dtype=torch.float64)
     src = torch.empty((n_tracks, n_in, ch), dtype=torch.int32, device=device)
     for k in range(n_tracks):
+        # tone + noise, peaks below 2^23 (a 24-bit source must fit 24 bits to
+        # round-trip losslessly)
         f = (110.0 + 37.0 * k + 55.0 * torch.arange(ch, device=device, dtype=torch.float64))
-        tone = torch.sin(2 * np.pi * t[:, None] * f[None, :] / rin) * (3e6 + 1e5 * k)
+        tone = torch.sin(2 * np.pi * t[:, None] * f[None, :] / rin) * (3e6 + 1e5 * (k % 40))
         noise = torch.randint(-4096, 4096, (n_in, ch), device=device, generator=g,
                               dtype=torch.int32)
         src[k] = tone.to(torch.int32) + noise
