@@ -433,6 +433,7 @@ def resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier, threa
     z = torch.empty_like(y)
     dither = torch.randint(0, 256, ((total * 2 + 7) // 8,), dtype=torch.uint8, device=device)
     stream = torch.cuda.current_stream(device).cuda_stream
+    torch.cuda.synchronize()
 
     def step():
         _atgpu.resample_device(x.data_ptr(), y.data_ptr(), total * 2, tracks, 2, 24, stream)
@@ -540,6 +541,9 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
         src[k] = tone.to(torch.int32) + noise
     del t
     src = src.reshape(-1)
+    # the library's kernels run on their own non-blocking streams: the torch
+    # work that produced their inputs must be finished first
+    torch.cuda.synchronize()
     # ALAC input (untimed): one mdat atom per track, framesets from the encoder
     aenc = _atgpu.AlacEncoder(local)
     aopts = aenc.options()
@@ -547,9 +551,12 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     n_fs, acap = aenc.bounds(aopts, atracks, ch, bps)
     alac = torch.zeros(acap, dtype=torch.uint8, device=device)
     fsb = np.zeros(max(1, n_fs), dtype=np.uint32)
+    torch.cuda.synchronize()
     ares = aenc.encode_device(aopts, src.data_ptr(), _atgpu.PCM_S32, atracks, ch, bps,
                               alac.data_ptr(), acap, fsb)
     aenc.close()
+    if any(r.status for r in ares):
+        raise RuntimeError("ALAC encode failed: %s" % sorted({int(r.status) for r in ares}))
     info = _atgpu.AlacInfo()
     info.max_samples_per_frame, info.bits_per_sample = 4096, bps
     info.history_multiplier, info.initial_history, info.maximum_k = 40, 10, 14
@@ -564,39 +571,65 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     adec = _atgpu.AlacDecoder(local)
     rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
     n_out = _atgpu.resample_output_frames(n_in, ch, rin, rout)
-    y = torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device)
+    # double-buffered resampled PCM and FLAC images: batch k's MD5 chains
+    # and headers (serial per track, ~9 MB per 5.1 track) run under batch
+    # k+1's decode/resample/search (atg_flac_encode_device_async)
+    ys = [torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device) for _ in range(2)]
     eng = _atgpu.Engine(local)
     fopts = _atgpu.make_options(**FLAC8)
     ftracks = [(k * n_out, n_out) for k in range(n_tracks)]
     n_flac, fcap = eng.bounds(fopts, ftracks, ch, bps)
     ftable = _atgpu.TrackTable(ftracks)
-    flac = torch.empty(fcap, dtype=torch.uint8, device=device)
+    flacs = [torch.empty(fcap, dtype=torch.uint8, device=device) for _ in range(2)]
     stream = torch.cuda.current_stream(device).cuda_stream
     state = {}
+    pending = []
 
-    def step():
+    torch.cuda.synchronize()
+
+    def step(k):
         dres, d_pcm, nsamp = adec.decode_device(alac.data_ptr(), nbytes, dtracks)
+        # the resampler reads n_in frames per track at fixed offsets: only a
+        # complete decode may feed it
+        if nsamp != src.numel() or any(r.status or r.pcm_frames != n_in for r in dres):
+            raise RuntimeError("ALAC decode incomplete: %d samples, statuses %s"
+                               % (nsamp, sorted({int(r.status) for r in dres})))
+        y = ys[k % 2]
         _atgpu.resample_device(d_pcm, y.data_ptr(), y.numel(), rtracks, ch, bps, stream)
-        fres = eng.encode_device(fopts, y.data_ptr(), _atgpu.PCM_S32, ftable, ch, bps, rout,
-                                 flac.data_ptr(), fcap)
-        state.update(dres=dres, d_pcm=d_pcm, nsamp=nsamp, fres=fres)
+        t = eng.encode_device_async(fopts, y.data_ptr(), _atgpu.PCM_S32, ftable, ch, bps, rout,
+                                    flacs[k % 2].data_ptr(), fcap)
+        if pending:
+            state["fres"] = eng.wait(pending.pop())
+        pending.append(t)
+        state.update(dres=dres, d_pcm=d_pcm, nsamp=nsamp, last=k)
 
-    for _ in range(args.warmup):
-        step()
+    def drain():
+        state["fres"] = eng.wait(pending.pop())
+
+    for k in range(args.warmup):
+        step(k)
+    if pending:
+        drain()
     kt = {}
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        for pre, d in (("alac_", {k: v for k, v in adec.kernel_times().items()}),
-                       ("", _atgpu.resample_kernel_times()), ("flac_", eng.kernel_times())):
-            for k, v in d.items():
-                key = k if k.startswith(pre) else pre + k
+    for k in range(args.steps):
+        step(k)
+        for pre, d in (("alac_", adec.kernel_times()), ("", _atgpu.resample_kernel_times()),
+                       ("flac_", eng.kernel_times() if k else {})):
+            for name, v in d.items():
+                key = name if name.startswith(pre) else pre + name
                 kt[key] = kt.get(key, 0.0) + v / args.steps
+    drain()
+    for name, v in eng.kernel_times().items():
+        key = name if name.startswith("flac_") else "flac_" + name
+        kt[key] = kt.get(key, 0.0) + v / args.steps
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
+    y = ys[(args.steps - 1) % 2]
+    flac = flacs[(args.steps - 1) % 2]
     dres, fres = state["dres"], state["fres"]
     dec_ok = all(r.status == 0 and r.pcm_frames == n_in for r in dres) and \
         state["nsamp"] == src.numel()
@@ -664,7 +697,7 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
         del yh, sh, fh, alac_h
     adec.close()
     eng.close()
-    del src, alac, y, flac
+    del src, alac, y, flac, ys, flacs
     return out
 
 
@@ -701,6 +734,7 @@ def replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks, barrie
     JSON object and per-track results for the CPU check."""
     from audiotools import _atgpu
     x = pcm.to(torch.int32)
+    torch.cuda.synchronize()  # the library's streams read x
     n_samples = args.frames * BLOCK
     tracks = [_atgpu.RgTrack(t * n_samples, n_samples, 2, 16, 44100, 0)
               for t in range(n_tracks)]

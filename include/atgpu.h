@@ -124,6 +124,10 @@ atg_status atg_flac_encode_host(atg_engine *eng, const atg_flac_options *opts,
                                 uint64_t *frame_offsets,
                                 uint32_t *frame_pcm_frames);
 
+/* Device-memory entry points run on the library's own non-blocking HIP
+   streams: device inputs must be complete (e.g. the producing stream
+   synchronized) when the call is made. */
+
 /* Encode a batch whose PCM already lives in device memory (HBM) and leave
    the .flac images in device memory at d_out (out_cap bytes).  Results are
    copied back to host `results` (small).  Runs on the engine's streams and

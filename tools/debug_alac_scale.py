@@ -35,6 +35,7 @@ def main():
             src[k] = tone.to(torch.int32) + noise
         del t
         src = src.reshape(-1)
+    torch.cuda.synchronize()
     aenc = _atgpu.AlacEncoder(0)
     aopts = aenc.options()
     atracks = [(k * n_in, n_in) for k in range(n_tracks)]
