@@ -122,6 +122,7 @@ struct Plan;
 // stream headers (on the slot's aux stream) run under batch k+1's search.
 struct EncSlot {
     DevBuf frames, tracks, order, coef, shift, est, sub, fdesc, tout, err;
+    DevBuf rice_big, scratch; // large-frame path (flac_big.hip)
     hipStream_t s_aux = nullptr;
     hipEvent_t ev[2 * kNumTimed] = {};
     hipEvent_t ev_tables = nullptr, ev_pack = nullptr, ev_done = nullptr;
@@ -179,7 +180,23 @@ struct Plan {
     uint64_t frame_bound = 0;               // worst-case frame bytes
     uint64_t out_bytes = 0;
     uint32_t n_reg_prefix = 0; // leading frame ids of 4096 samples at 4-frame-aligned starts
+    // large-frame path (flac_big.hip): a frame longer than 4096 samples or a
+    // partition order above 6 anywhere in the batch
+    bool big = false;
+    uint32_t big_nmax = 0;       // longest frame
+    uint32_t big_porder = 0;     // deepest usable partition order
 };
+
+// persistent grid of the large-frame kernels and their per-workgroup
+// scratch: the candidate's samples, then the partition-sum pyramid
+const uint32_t kBigGrid = 1024;
+
+uint64_t big_row_bytes(const Plan &pl) { return ((uint64_t)pl.big_nmax * 4u + 255u) & ~255ull; }
+
+uint64_t big_slot_bytes(const Plan &pl)
+{
+    return big_row_bytes(pl) + (16ull << pl.big_porder);
+}
 
 uint32_t qlp_precision_for(uint32_t n)
 {
@@ -198,12 +215,12 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
         return fail(ATG_ERR_UNSUPPORTED, "bits_per_sample must be 4..24 on the GPU path");
     if (o->block_size == 0)
         return fail(ATG_ERR_INVALID, "block_size must be > 0");
-    if (o->block_size > ATG_MAX_BLOCK)
-        return fail(ATG_ERR_UNSUPPORTED, "block_size > 4096 not supported on the GPU path");
+    if (o->block_size > ATG_BIG_MAX_BLOCK)
+        return fail(ATG_ERR_UNSUPPORTED, "block_size > 65535 cannot be framed");
     if (o->max_lpc_order > ATG_MAX_LPC)
         return fail(ATG_ERR_INVALID, "max_lpc_order must be <= 32");
-    if (o->max_residual_partition_order > ATG_MAX_PORDER)
-        return fail(ATG_ERR_UNSUPPORTED, "max_residual_partition_order > 6 not supported");
+    if (o->max_residual_partition_order > ATG_BIG_MAX_PORDER)
+        return fail(ATG_ERR_INVALID, "max_residual_partition_order must be <= 15");
     if (o->padding_size > 0xFFFFFFu)
         return fail(ATG_ERR_INVALID, "padding_size must fit in 24 bits");
     if (rate == 0)
@@ -233,17 +250,8 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
     p.padding_size = o->padding_size;
     p.header_bytes = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + o->padding_size;
 
-    // worst-case frame: verbatim subframes (+1 bit side channel) + headers;
-    // without VERBATIM a predictor may exceed that, so bound by LDS instead
     const uint64_t B = o->block_size;
     const uint64_t nsub = channels;
-    uint64_t fb = 16 + nsub * ((8 + 32 + B * (bps + 1) + 7) / 8) + 2;
-    if (!p.try_verbatim)
-        fb = std::max<uint64_t>(fb, 120 * 1024);
-    pl.frame_bound = fb;
-    p.frame_lds_words = (uint32_t)((fb + 3) / 4 + 2);
-    if (p.frame_lds_words * 4ull > 128 * 1024)
-        return fail(ATG_ERR_UNSUPPORTED, "frame image exceeds the pack kernel's LDS budget");
 
     // frame table: every frame's length, in track order
     pl.tracks.resize(n_tracks);
@@ -259,9 +267,9 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
             uint64_t sum = 0;
             for (uint64_t k = 0; k < tr.n_frame_sizes; ++k) {
                 const uint32_t n = tr.frame_sizes[k];
-                if (n == 0 || n > ATG_MAX_BLOCK)
+                if (n == 0 || n > ATG_BIG_MAX_BLOCK)
                     return fail(n ? ATG_ERR_UNSUPPORTED : ATG_ERR_INVALID,
-                                "explicit frame sizes must be 1..4096");
+                                "explicit frame sizes must be 1..65535");
                 sum += n;
                 lens.push_back(n);
                 owner.push_back(t);
@@ -302,18 +310,30 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
         f.win_off = 0;
         start[t] += lens[i];
     }
-    // frames longer than block_size (explicit sizes) widen the bound
+    // worst-case frame: verbatim subframes (+1 bit side channel) + headers.
+    // Without VERBATIM a predictor may exceed that: the 4096-sample packer is
+    // bounded by its LDS image, the large-frame packer checks the track's
+    // slot on the device (error bit 4)
     uint32_t maxn = 0;
     for (size_t i = 0; i < nfr; ++i)
         maxn = std::max(maxn, lens[i]);
-    if (maxn > B) {
-        fb = 16 + nsub * ((8 + 32 + (uint64_t)maxn * (bps + 1) + 7) / 8) + 2;
-        if (!p.try_verbatim)
-            fb = std::max<uint64_t>(fb, 120 * 1024);
-        pl.frame_bound = fb;
-        p.frame_lds_words = (uint32_t)((fb + 3) / 4 + 2);
-        if (p.frame_lds_words * 4ull > 128 * 1024)
-            return fail(ATG_ERR_UNSUPPORTED, "frame image exceeds the pack kernel's LDS budget");
+    const uint64_t nb = std::max<uint64_t>(B, maxn);
+    uint64_t fb = 16 + nsub * ((8 + 32 + nb * (bps + 1) + 7) / 8) + 2;
+    pl.big = nb > ATG_MAX_BLOCK || p.max_porder > ATG_MAX_PORDER;
+    if (!p.try_verbatim)
+        fb = pl.big ? 2 * fb + 120 * 1024 : std::max<uint64_t>(fb, 120 * 1024);
+    pl.frame_bound = fb;
+    p.frame_bound = (uint32_t)fb;
+    p.frame_lds_words = (uint32_t)((fb + 3) / 4 + 2);
+    if (!pl.big && p.frame_lds_words * 4ull > 128 * 1024)
+        return fail(ATG_ERR_UNSUPPORTED, "frame image exceeds the pack kernel's LDS budget");
+    if (pl.big) {
+        pl.big_nmax = maxn;
+        pl.big_porder = 0;
+        for (size_t i = 0; i < nfr; ++i) {
+            const uint32_t tz = (uint32_t)__builtin_ctz(lens[i]);
+            pl.big_porder = std::max(pl.big_porder, std::min<uint32_t>(p.max_porder, tz));
+        }
     }
     uint64_t out = 0;
     for (uint32_t t = 0; t < n_tracks; ++t) {
@@ -328,7 +348,7 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
     // register-staged packer (K5): 16-bit stereo mid/side, 4096-sample
     // frames whose first pair is 16-byte aligned (with an aligned base)
     pl.n_reg_prefix = 0;
-    if (channels == 2 && p.n_cand == 4 && bps <= 16 && B == ATG_MAX_BLOCK)
+    if (channels == 2 && p.n_cand == 4 && bps <= 16 && B == ATG_MAX_BLOCK && !pl.big)
         while (pl.n_reg_prefix < p.n_frames && pl.frames[pl.n_reg_prefix].n == ATG_MAX_BLOCK &&
                (pl.frames[pl.n_reg_prefix].pcm_start & 3u) == 0)
             pl.n_reg_prefix++;
@@ -454,6 +474,13 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     HIP_TRY(sl.fdesc.ensure(nf * sizeof(FrameDesc)));
     HIP_TRY(sl.tout.ensure(nt * sizeof(TrackOut)));
     HIP_TRY(sl.err.ensure(sizeof(uint32_t)));
+    const uint32_t big_grid =
+        pl.big ? (uint32_t)std::min<uint64_t>(kBigGrid, std::max<uint64_t>(nf, 1) * p.n_cand) : 0u;
+    const uint32_t rice_stride = 1u << pl.big_porder;
+    if (pl.big) {
+        HIP_TRY(sl.rice_big.ensure(nf * p.n_cand * (size_t)rice_stride));
+        HIP_TRY(sl.scratch.ensure(big_grid * big_slot_bytes(pl)));
+    }
     HIP_TRY(ensure_pinned(sl.tout_h, sl.tout_cap, nt));
     HIP_TRY(ensure_pinned(sl.err_h, sl.err_cap, 1));
     if (want_fdesc)
@@ -494,9 +521,17 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
     HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
-    HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
-                                   (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
-                                   (SubDesc *)sl.sub.p, derr, e->s_main));
+    if (pl.big)
+        HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                           (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
+                                           (SubDesc *)sl.sub.p, (uint8_t *)sl.rice_big.p,
+                                           rice_stride, (uint8_t *)sl.scratch.p,
+                                           big_slot_bytes(pl), big_row_bytes(pl), big_grid,
+                                           e->s_main));
+    else
+        HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                       (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
+                                       (SubDesc *)sl.sub.p, derr, e->s_main));
     HIP_TRY(hipEventRecord(ev[3], e->s_main));
     HIP_TRY(hipEventRecord(ev[4], e->s_main));
     HIP_TRY(launch_frame_decide(p, dfr, (const SubDesc *)sl.sub.p, (FrameDesc *)sl.fdesc.p,
@@ -507,8 +542,18 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                               e->s_main));
     HIP_TRY(hipEventRecord(ev[7], e->s_main));
     HIP_TRY(hipEventRecord(ev[8], e->s_main));
-    HIP_TRY(launch_frame_pack(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
-                              (const FrameDesc *)sl.fdesc.p, d_out, derr, e->s_main));
+    if (pl.big) {
+        // the large-frame packer ORs bits into a zeroed image
+        HIP_TRY(hipMemsetAsync(d_out, 0, pl.out_bytes, e->s_main));
+        HIP_TRY(launch_frame_pack_big(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
+                                      (const uint8_t *)sl.rice_big.p, rice_stride,
+                                      (const FrameDesc *)sl.fdesc.p, d_out, derr,
+                                      (uint8_t *)sl.scratch.p, big_slot_bytes(pl),
+                                      (uint32_t)std::min<uint64_t>(kBigGrid, nf), e->s_main));
+    } else {
+        HIP_TRY(launch_frame_pack(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
+                                  (const FrameDesc *)sl.fdesc.p, d_out, derr, e->s_main));
+    }
     HIP_TRY(hipEventRecord(ev[9], e->s_main));
     HIP_TRY(hipEventRecord(sl.ev_pack, e->s_main));
     // headers once both the pack and the MD5 chains are done, on the aux
@@ -548,6 +593,8 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
     uint32_t err_h = *sl.err_h;
     if (err_h & 1u)
         return fail(ATG_ERR_UNSUPPORTED, "frame longer than the GPU block limit");
+    if (err_h & 4u)
+        return fail(ATG_ERR_CAPACITY, "a frame exceeds its track's output slot");
 #if ATG_EXP != 0
     err_h = 0; // timing experiments do not produce valid streams
 #endif
@@ -717,7 +764,7 @@ void atg_engine_destroy(atg_engine *e)
     for (EncSlot &sl : e->slot) {
         (void)hipStreamSynchronize(sl.s_aux);
         for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
-                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err})
+                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch})
             b->release();
         for (auto &ev : sl.ev)
             (void)hipEventDestroy(ev);

@@ -19,6 +19,8 @@
 #define ATG_MAX_PORDER 6      // partition orders the GPU search handles
 #define ATG_MAX_BLOCK 4096    // block lengths the GPU search handles
 #define ATG_RUN 64            // samples per lane (4096 / 64 lanes)
+#define ATG_BIG_MAX_BLOCK 65535 // large-frame path (flac_big.hip): FLAC's 16-bit block field
+#define ATG_BIG_MAX_PORDER 15   // large-frame path: the format's 4-bit partition order
 
 enum { SF_CONSTANT = 0, SF_VERBATIM = 1, SF_FIXED = 2, SF_LPC = 3 };
 
@@ -47,6 +49,7 @@ struct FlacParams {
     uint32_t padding_size;
     uint32_t header_bytes;   // bytes before the first frame of every track
     uint32_t frame_lds_words;// pack kernel frame buffer (32-bit words)
+    uint32_t frame_bound;    // worst-case bytes of one frame (output slot = n_frames x this)
 };
 
 struct FrameInfo {

@@ -17,6 +17,19 @@ hipError_t launch_subframe_search(const FlacParams &p, const void *pcm, int fmt,
                                   const int8_t *shift_tab,
                                   const uint8_t *est_tab, SubDesc *sub,
                                   uint32_t *err, hipStream_t s);
+// flac_big.hip: frames longer than 4096 samples / partition orders > 6
+hipError_t launch_subframe_search_big(const FlacParams &p, const void *pcm, int fmt,
+                                      const FrameInfo *frames, const int16_t *coef_tab,
+                                      const int8_t *shift_tab, const uint8_t *est_tab,
+                                      SubDesc *sub, uint8_t *rice_big, uint32_t rice_stride,
+                                      uint8_t *scratch, uint64_t slot_bytes, uint64_t row_bytes,
+                                      uint32_t grid, hipStream_t s);
+hipError_t launch_frame_pack_big(const FlacParams &p, const void *pcm, int fmt,
+                                 const FrameInfo *frames, const TrackInfo *tracks,
+                                 const SubDesc *sub, const uint8_t *rice_big,
+                                 uint32_t rice_stride, const FrameDesc *fd, uint8_t *out,
+                                 uint32_t *err, uint8_t *scratch, uint64_t slot_bytes,
+                                 uint32_t grid, hipStream_t s);
 // flac_frame.hip
 hipError_t launch_frame_decide(const FlacParams &p, const FrameInfo *frames,
                                const SubDesc *sub, FrameDesc *fd, hipStream_t s);

@@ -96,8 +96,8 @@ def test_explicit_frame_sizes_checked():
 
 
 @pytest.mark.parametrize("kw,ch,bps,status", [
-    (dict(block_size=8192), 2, 16, _atgpu.ATG_ERR_UNSUPPORTED),
-    (dict(max_residual_partition_order=8), 2, 16, _atgpu.ATG_ERR_UNSUPPORTED),
+    (dict(block_size=65536), 2, 16, _atgpu.ATG_ERR_UNSUPPORTED),
+    (dict(max_residual_partition_order=16), 2, 16, _atgpu.ATG_ERR_INVALID),
     (dict(block_size=0), 2, 16, _atgpu.ATG_ERR_INVALID),
     (dict(max_lpc_order=33), 2, 16, _atgpu.ATG_ERR_INVALID),
     (dict(), 9, 16, _atgpu.ATG_ERR_INVALID),
@@ -107,6 +107,15 @@ def test_option_validation(kw, ch, bps, status):
     st, _, _ = bounds(flac8(**kw), [(0, 10000)], ch, bps)
     assert st == status
     assert _atgpu.load_library().atg_last_error()
+
+
+@pytest.mark.parametrize("kw", [dict(block_size=8192), dict(block_size=65535),
+                                dict(max_residual_partition_order=15)])
+def test_large_frame_options_accepted(kw):
+    """block sizes up to 65535 and partition orders up to 15 take the
+    large-frame path (flac_big.hip), as the reference encoder accepts them"""
+    st, nf, nb = bounds(flac8(**kw), [(0, 100000)])
+    assert st == _atgpu.ATG_OK and nf >= 2 and nb > 0
 
 
 def test_null_arguments_rejected():

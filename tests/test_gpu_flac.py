@@ -145,11 +145,11 @@ def test_explicit_frame_sizes(gpu_engine):
 
 def test_unsupported_options_raise(gpu_engine):
     from audiotools import _atgpu
-    o = _atgpu.make_options(block_size=8192, max_lpc_order=8,
+    o = _atgpu.make_options(block_size=65536, max_lpc_order=8,
                             min_residual_partition_order=0, max_residual_partition_order=6)
-    pcm = np.zeros(20000, np.int16)
+    pcm = np.zeros(200000, np.int16)
     with pytest.raises(_atgpu.ATGError) as e:
-        gpu_engine.encode(o, pcm, [(0, 10000)], 2, 16, 44100)
+        gpu_engine.encode(o, pcm, [(0, 100000)], 2, 16, 44100)
     assert e.value.status == _atgpu.ATG_ERR_UNSUPPORTED
 
 

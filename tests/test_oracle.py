@@ -44,6 +44,18 @@ def test_golden_vectors(preset):
         assert hashlib.sha256(data).hexdigest() == v["sha256"], v["name"]
 
 
+def test_golden_vectors_big_blocks():
+    """reference-encoder sha256 for block sizes 4608..65535 and partition
+    orders up to 15 (tests/golden/make_golden_big.py)"""
+    vecs = json.load(open(os.path.join(GOLDEN, "flac_vectors_big.json")))["vectors"]
+    assert len(vecs) == 90
+    for v in vecs:
+        pcm = signals.make(v["kind"], v["n"], v["channels"], v["bps"], seed=v["seed"])
+        data, _ = oracle_port.encode(pcm, v["channels"], v["bps"], 44100, **v["opts"])
+        assert len(data) == v["bytes"], v["name"]
+        assert hashlib.sha256(data).hexdigest() == v["sha256"], v["name"]
+
+
 def test_golden_vectors_round_trip():
     for v in VECTORS[::7]:
         pcm = make_pcm(v)
