@@ -1541,7 +1541,9 @@ int flacport_decode(const uint8_t *flac, size_t len, uint32_t *channels,
         return 0;
     if (pcm_cap < si.total_samples * si.channels)
         return -2;
-    size_t cap = (size_t)(si.total_samples / (si.min_block_size ? si.min_block_size : 1)) + 2;
+    /* frames cut at the writer's read sizes may be shorter than the
+       STREAMINFO minimum block: every frame holds >= 1 sample */
+    size_t cap = (size_t)si.total_samples + 2;
     uint64_t *offs = malloc(sizeof(uint64_t) * cap);
     uint32_t *bss = malloc(sizeof(uint32_t) * cap);
     size_t nf;

@@ -108,6 +108,10 @@ def encode(pcm, channels, bps, rate, **opts):
     frames = len(a) // channels
     cap = lib.flacport_max_stream_bytes(frames, channels, bps, o.block_size,
                                         o.padding_size)
+    if opts.get("disable_verbatim_subframes"):
+        # without VERBATIM a predictor may exceed the verbatim bound (24-bit
+        # noise): leave room for twice that
+        cap = 2 * cap + (1 << 20)
     out = np.empty(cap, dtype=np.uint8)
     olen = ctypes.c_size_t()
     nfmax = frames // max(1, o.block_size) + 2

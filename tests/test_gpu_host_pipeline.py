@@ -89,6 +89,6 @@ def test_chunked_host_encode_explicit_frame_sizes(monkeypatch):
             assert got == tracks[k][2]
         else:
             assert sum(got) == lens[k] and max(got) == 4096
-            # default framing: the image decodes back to the source exactly
-            pcm_dec = oracle_port.decode(img)[0]
-            assert np.array_equal(pcm_dec, parts[k].astype(np.int32))
+        # the image decodes back to the source exactly
+        pcm_dec = oracle_port.decode(img)[0]
+        assert np.array_equal(pcm_dec, parts[k].astype(np.int32))
