@@ -284,18 +284,32 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
         tracks.append(_atgpu.dec_track(r.out_offset + HEADER_BYTES, r.bytes - HEADER_BYTES, si))
     nbytes = max(r.out_offset + r.bytes for r in res)
 
-    def step():
-        return dec.decode_device(out.data_ptr(), nbytes, tracks)
-
-    for _ in range(args.warmup):
-        dres, _, _ = step()
     kt_sum = {}
+
+    def run(k_steps, timed):
+        # two batches in flight (atg_flac_decode_device_async): batch k's
+        # per-track MD5 runs on its own stream under batch k+1's parse and
+        # restore; the last batch's drain is inside the timed region
+        pending, last = None, None
+        for _ in range(k_steps):
+            t = dec.decode_device_async(out.data_ptr(), nbytes, tracks)
+            if pending is not None:
+                last = dec.decode_wait(pending)
+                if timed:
+                    for k, v in dec.kernel_times().items():
+                        kt_sum[k] = kt_sum.get(k, 0.0) + v
+            pending = t
+        last = dec.decode_wait(pending)
+        if timed:
+            for k, v in dec.kernel_times().items():
+                kt_sum[k] = kt_sum.get(k, 0.0) + v
+        return last
+
+    if args.warmup:
+        run(args.warmup, False)
     barrier()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        dres, d_pcm, nsamp = step()
-        for k, v in dec.kernel_times().items():
-            kt_sum[k] = kt_sum.get(k, 0.0) + v
+    dres, d_pcm, nsamp = run(args.steps, True)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
@@ -318,7 +332,9 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     alg = {"dec_scan": comp, "dec_parse": comp, "dec_chain": 0,
            "dec_subframe": comp + pcm32, "dec_unrow": 2 * pcm32,
            "dec_interleave": pcm32 * 2 + pcm32 // 2, "dec_md5": pcm32 // 2}
-    kernels = {k: v for k, v in kt.items() if k in alg}
+    # the dominant kernel on the critical path: the MD5 chains run beside the
+    # next batch on their own stream
+    kernels = {k: v for k, v in kt.items() if k in alg and k != "dec_md5"}
     dom = max(kernels, key=kernels.get)
     achieved = alg[dom] / (kernels[dom] / 1e3) / 1e9
     traffic = (load_profile_json("pmc_traffic.json") or {}).get(dom)
@@ -332,7 +348,9 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4)},
+                     "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4),
+                     "selection": "longest kernel on the decoder (critical-path) stream"},
+        "pipelining": "two batches in flight: MD5 of batch k beside the restore of batch k+1",
         "step_hbm": {"alg_bytes_per_step": step_alg,
                      "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)},
         "verified_md5_round_trip": ok,

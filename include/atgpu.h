@@ -269,13 +269,26 @@ atg_status atg_flac_decode_fetch(atg_decoder *dec, int32_t *pcm, uint64_t pcm_ca
 
 /* Decode a batch already in device memory (4-byte aligned, readable up to
    len rounded up to 4).  *d_pcm receives the decoder-owned device PCM
-   (valid until the next call). */
+   (valid until the call after next). */
 atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t len,
                                   const atg_flac_dec_track *tracks, uint32_t n_tracks,
                                   atg_flac_dec_result *results, const int32_t **d_pcm,
                                   uint64_t *total_samples);
 
-/* Per-kernel device time of the decoder's most recent batch (HIP events). */
+/* Asynchronous form of atg_flac_decode_device (two batches in flight):
+   returns once batch k's restore is queued, with its per-track MD5 on a
+   second stream, so batch k's MD5 runs under batch k+1's parse and restore.
+   d_data must stay valid until the wait; the PCM pointer the wait returns
+   stays valid until the batch after next is enqueued.  A third enqueue
+   before a wait fails with ATG_ERR_INVALID. */
+atg_status atg_flac_decode_device_async(atg_decoder *dec, const void *d_data, uint64_t len,
+                                        const atg_flac_dec_track *tracks, uint32_t n_tracks,
+                                        uint64_t *ticket);
+atg_status atg_flac_decode_wait(atg_decoder *dec, uint64_t ticket,
+                                atg_flac_dec_result *results, const int32_t **d_pcm,
+                                uint64_t *total_samples);
+
+/* Per-kernel device time of the decoder's most recently waited batch. */
 int atg_decoder_kernel_times(atg_decoder *dec, const char **names, float *ms, int cap);
 
 /* ------------------------------------------------------------------ */

@@ -34,7 +34,8 @@ EXPORTS = (
     "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
-    "atg_flac_decode_device", "atg_decoder_kernel_times",
+    "atg_flac_decode_device", "atg_flac_decode_device_async", "atg_flac_decode_wait",
+    "atg_decoder_kernel_times",
     "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
@@ -285,6 +286,12 @@ def load_library():
             P, P, c_u64, ctypes.POINTER(DecTrack), c_u32, ctypes.POINTER(DecResult),
             ctypes.POINTER(P), ctypes.POINTER(c_u64)]
         lib.atg_flac_decode_device.restype = ctypes.c_int
+        lib.atg_flac_decode_device_async.argtypes = [
+            P, P, c_u64, ctypes.POINTER(DecTrack), c_u32, ctypes.POINTER(c_u64)]
+        lib.atg_flac_decode_device_async.restype = ctypes.c_int
+        lib.atg_flac_decode_wait.argtypes = [
+            P, c_u64, ctypes.POINTER(DecResult), ctypes.POINTER(P), ctypes.POINTER(c_u64)]
+        lib.atg_flac_decode_wait.restype = ctypes.c_int
         lib.atg_decoder_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -572,6 +579,7 @@ class Decoder(object):
         h = ctypes.c_void_p()
         self._check(self.lib.atg_decoder_create(int(device), ctypes.byref(h)))
         self.handle = h
+        self._pending = {}
 
     def _check(self, status):
         if status != ATG_OK:
@@ -623,6 +631,27 @@ class Decoder(object):
         self._check(self.lib.atg_flac_decode_device(
             self.handle, ctypes.c_void_p(d_data), nbytes, arr, n, res, ctypes.byref(dp),
             ctypes.byref(ns)))
+        return [res[i] for i in range(n)], dp.value, ns.value
+
+    def decode_device_async(self, d_data, nbytes, tracks):
+        """enqueue a device-resident batch (two may be in flight) -> ticket;
+        d_data must stay valid until decode_wait(ticket)"""
+        n = len(tracks)
+        arr = (DecTrack * max(1, n))(*tracks)
+        ticket = c_u64()
+        self._check(self.lib.atg_flac_decode_device_async(
+            self.handle, ctypes.c_void_p(d_data), nbytes, arr, n, ctypes.byref(ticket)))
+        self._pending[ticket.value] = n
+        return ticket.value
+
+    def decode_wait(self, ticket):
+        """-> ([DecResult], device pointer of the int32 PCM, interleaved samples)"""
+        n = self._pending.pop(ticket, 0)
+        res = (DecResult * max(1, n))()
+        dp = ctypes.c_void_p()
+        ns = c_u64()
+        self._check(self.lib.atg_flac_decode_wait(self.handle, ticket, res, ctypes.byref(dp),
+                                                  ctypes.byref(ns)))
         return [res[i] for i in range(n)], dp.value, ns.value
 
     def kernel_times(self):

@@ -1086,18 +1086,37 @@ struct DBuf {
     }
 };
 
+// One batch in flight: its PCM / MD5 byte buffers, the MD5 stream, and the
+// host copies its results are computed from.  Two slots let batch k's
+// per-track MD5 chains run under batch k+1's parse and restore.
+struct DecSlot {
+    DBuf pcm, bytes, md5, md5meta;
+    hipStream_t s_md5 = nullptr;
+    hipEvent_t ev[kDecTimed + 1] = {}; // phase events (interleave end = ev[6])
+    hipEvent_t ev_done = nullptr;
+    uint8_t *md5_h = nullptr;          // pinned
+    size_t md5_cap = 0;
+    std::vector<DecTrack> tr;
+    std::vector<DecCount> cnt;
+    std::vector<uint64_t> md5_meta;    // offsets then lengths (upload source)
+    std::vector<atg_flac_dec_track> want; // the caller's tracks (STREAMINFO MD5)
+    uint64_t total_samples = 0, total_frames = 0;
+    uint64_t ticket = 0;
+    bool busy = false;
+};
+
 struct atg_decoder {
     int device = 0;
     hipStream_t s = nullptr;
-    hipEvent_t ev[kDecTimed + 1] = {};
     float times[kDecTimed] = {};
     bool have_times = false;
-    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, planar, pcm,
-        bytes, md5, md5meta, rows, meta;
-    // results of the last decode
+    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, planar, rows, meta;
+    DecSlot slot[2];
+    uint64_t next_ticket = 1;
+    int last = -1; // slot of the last waited batch (decode_fetch)
+    // frame table of the most recent batch (decode_fetch)
     std::vector<DecTrack> tr;
-    std::vector<DecCount> cnt;
-    uint64_t total_samples = 0, total_frames = 0;
+    uint64_t total_frames = 0;
 };
 
 static void build_dec_tables(uint8_t *t8, uint16_t t16[4][256])
@@ -1269,8 +1288,12 @@ atg_status atg_decoder_create(int device, atg_decoder **out)
     atg_decoder *d = new atg_decoder();
     d->device = device;
     DHIP(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
-    for (auto &e : d->ev)
-        DHIP(hipEventCreate(&e));
+    for (DecSlot &sl : d->slot) {
+        DHIP(hipStreamCreateWithFlags(&sl.s_md5, hipStreamNonBlocking));
+        for (auto &e : sl.ev)
+            DHIP(hipEventCreate(&e));
+        DHIP(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
+    }
     *out = d;
     return ATG_OK;
 }
@@ -1282,26 +1305,38 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->pcm, &d->bytes, &d->md5, &d->md5meta, &d->rows, &d->meta})
+                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->rows, &d->meta})
         b->release();
-    for (auto &e : d->ev)
-        (void)hipEventDestroy(e);
+    for (DecSlot &sl : d->slot) {
+        (void)hipStreamSynchronize(sl.s_md5);
+        for (DBuf *b : {&sl.pcm, &sl.bytes, &sl.md5, &sl.md5meta})
+            b->release();
+        for (auto &e : sl.ev)
+            (void)hipEventDestroy(e);
+        (void)hipEventDestroy(sl.ev_done);
+        if (sl.md5_h)
+            (void)hipHostFree(sl.md5_h);
+        (void)hipStreamDestroy(sl.s_md5);
+    }
     (void)hipStreamDestroy(d->s);
     delete d;
 }
 
 } // extern "C"
 
-// the device-resident decode of a batch already in d->data (or caller HBM)
-static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len,
-                             const atg_flac_dec_track *tracks, uint32_t n,
-                             atg_flac_dec_result *res)
+// Enqueue the device-resident decode of a batch on slot `sl`: scan ->
+// parse -> chain (two host round trips for the counts) -> restore ->
+// interleave on the decoder stream, then the per-track MD5 on the slot's
+// stream.  Returns once the restore is queued; finish_decode waits.
+static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_data,
+                                 uint64_t len, const atg_flac_dec_track *tracks, uint32_t n)
 {
     hipStream_t s = d->s;
-    d->tr.assign(n, DecTrack());
+    std::vector<DecTrack> &tr = sl.tr;
+    tr.assign(n, DecTrack());
     for (uint32_t t = 0; t < n; ++t) {
         const atg_flac_dec_track &a = tracks[t];
-        DecTrack &b = d->tr[t];
+        DecTrack &b = tr[t];
         if (a.data_offset > len || a.data_bytes > len - a.data_offset)
             return dfail(ATG_ERR_INVALID, "track data range outside the buffer");
         if (t && a.data_offset < tracks[t - 1].data_offset)
@@ -1316,6 +1351,7 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
         b.bps = a.bits_per_sample;
         b.max_bs = a.max_block_size;
     }
+    sl.want.assign(tracks, tracks + n);
     const uint64_t nw = std::max<uint64_t>(1, (len + 3) / 4);
     DHIP(d->tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
     DHIP(d->counts.ensure(sizeof(DecCount) * std::max<uint32_t>(n, 1)));
@@ -1325,10 +1361,11 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
     // with the exact count in the rare batch that needs more
     uint64_t cap = std::min<uint64_t>(len / 16 + 4096, 0xFFFFFFFFull);
     DHIP(d->cand_idx.ensure(sizeof(uint32_t) * (len + 4)));
-    DHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
+    DHIP(hipMemcpyAsync(d->tracks.p, tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
     const uint32_t *w = (const uint32_t *)d_data;
     DecTrack *dtr = (DecTrack *)d->tracks.p;
-    DHIP(hipEventRecord(d->ev[0], s));
+    hipEvent_t *ev = sl.ev;
+    DHIP(hipEventRecord(ev[0], s));
     uint32_t found = 0;
     for (int pass = 0; pass < 2; ++pass) {
         DHIP(d->cand_pos.ensure(sizeof(uint64_t) * cap));
@@ -1345,12 +1382,12 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
         cap = found; // every sync position of the buffer is now known
     }
     DHIP(d->recs.ensure(sizeof(ParseRec) * std::max<uint64_t>(found, 1)));
-    DHIP(hipEventRecord(d->ev[1], s));
+    DHIP(hipEventRecord(ev[1], s));
     hipLaunchKernelGGL(k_dec_parse, dim3(4096), dim3(64), 0, s, w, nw, dtr, n,
                        (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
                        (ParseRec *)d->recs.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[2], s));
+    DHIP(hipEventRecord(ev[2], s));
     const dim3 tg((n + 63) / 64);
     if (n)
         hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, dtr, n,
@@ -1358,42 +1395,42 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
                            (const uint32_t *)d->cand_idx.p, (const ParseRec *)d->recs.p,
                            (DecCount *)d->counts.p, 1, (DecFrame *)nullptr, (uint2 *)nullptr);
     DHIP(hipGetLastError());
-    d->cnt.assign(n, DecCount());
-    DHIP(hipMemcpyAsync(d->cnt.data(), d->counts.p, sizeof(DecCount) * n, hipMemcpyDeviceToHost,
+    sl.cnt.assign(n, DecCount());
+    DHIP(hipMemcpyAsync(sl.cnt.data(), d->counts.p, sizeof(DecCount) * n, hipMemcpyDeviceToHost,
                         s));
     DHIP(hipStreamSynchronize(s));
     // host prefix over tracks: frame slots, PCM placement, MD5 byte streams
     uint64_t fb = 0, pb = 0, mb = 0, jb = 0;
     for (uint32_t t = 0; t < n; ++t) {
-        DecTrack &b = d->tr[t];
+        DecTrack &b = tr[t];
         b.frame_base = fb;
         b.pcm_base = pb;
         b.md5_base = mb;
         b.job_base = jb;
-        fb += d->cnt[t].n_frames;
-        jb += (uint64_t)d->cnt[t].n_frames * b.channels;
-        const uint64_t ns = d->cnt[t].pcm_frames * b.channels;
+        fb += sl.cnt[t].n_frames;
+        jb += (uint64_t)sl.cnt[t].n_frames * b.channels;
+        const uint64_t ns = sl.cnt[t].pcm_frames * b.channels;
         pb += ns;
         mb += (ns * ((b.bps + 7) / 8) + 63) & ~63ull;
     }
-    d->total_samples = pb;
-    d->total_frames = fb;
+    sl.total_samples = pb;
+    sl.total_frames = fb;
     DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
     DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
     DHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
     // row scratch: a residual loop runs at most N + 2^porder <= 2N iterations
     uint32_t max_bs = 1;
     for (uint32_t t = 0; t < n; ++t)
-        if (d->cnt[t].n_frames)
-            max_bs = std::max(max_bs, d->tr[t].max_bs);
+        if (sl.cnt[t].n_frames)
+            max_bs = std::max(max_bs, tr[t].max_bs);
     const uint32_t nrows = (2 * max_bs + 1 + 63) & ~63u; // whole 64-row tiles
     const uint64_t nslots = (jb + 63) / 64;
     DHIP(d->rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
     DHIP(d->meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
-    DHIP(d->pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
-    DHIP(d->bytes.ensure(std::max<uint64_t>(mb, 64)));
-    DHIP(d->md5.ensure(16 * std::max<uint32_t>(n, 1)));
-    DHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
+    DHIP(sl.pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    DHIP(sl.bytes.ensure(std::max<uint64_t>(mb, 64)));
+    DHIP(sl.md5.ensure(16 * std::max<uint32_t>(n, 1)));
+    DHIP(hipMemcpyAsync(d->tracks.p, tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
     if (n)
         hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, dtr, n,
                            (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
@@ -1401,63 +1438,87 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
                            (DecCount *)d->counts.p, 2, (DecFrame *)d->frames.p,
                            (uint2 *)d->jobs.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[3], s));
+    DHIP(hipEventRecord(ev[3], s));
     if (jb)
         hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
                            nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
                            (int32_t *)d->planar.p, (int32_t *)d->rows.p, nrows,
                            (JobMeta *)d->meta.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[4], s));
+    DHIP(hipEventRecord(ev[4], s));
     if (jb)
         hipLaunchKernelGGL(k_dec_unrow, dim3((unsigned)nslots, (nrows + 63) / 64), dim3(256), 0,
                            s, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
                            (const JobMeta *)d->meta.p, (const int32_t *)d->rows.p, nrows,
                            (int32_t *)d->planar.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[5], s));
+    DHIP(hipEventRecord(ev[5], s));
     if (fb)
         hipLaunchKernelGGL(k_dec_interleave, dim3((unsigned)fb), dim3(256), 0, s, dtr,
                            (const DecFrame *)d->frames.p, (const int32_t *)d->planar.p,
-                           (int32_t *)d->pcm.p, (uint8_t *)d->bytes.p);
+                           (int32_t *)sl.pcm.p, (uint8_t *)sl.bytes.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(d->ev[6], s));
-    std::vector<uint64_t> md5_off(n), md5_len(n);
+    DHIP(hipEventRecord(ev[6], s));
+    // MD5 of the decoded bytes on the slot's stream: the next batch's scan,
+    // parse and restore run on the decoder stream meanwhile
+    sl.md5_meta.assign(2 * (size_t)n, 0);
     for (uint32_t t = 0; t < n; ++t) {
-        md5_off[t] = d->tr[t].md5_base;
-        const uint64_t vis = d->cnt[t].crc_frame != 0xFFFFFFFFu ? d->cnt[t].crc_pcm
-                                                                 : d->cnt[t].pcm_frames;
-        md5_len[t] = vis * d->tr[t].channels * ((d->tr[t].bps + 7) / 8);
+        sl.md5_meta[t] = tr[t].md5_base;
+        const uint64_t vis = sl.cnt[t].crc_frame != 0xFFFFFFFFu ? sl.cnt[t].crc_pcm
+                                                                : sl.cnt[t].pcm_frames;
+        sl.md5_meta[n + t] = vis * tr[t].channels * ((tr[t].bps + 7) / 8);
     }
-    DBuf &mb_buf = d->md5meta;
-    DHIP(mb_buf.ensure(sizeof(uint64_t) * 2 * std::max<uint32_t>(n, 1)));
-    DHIP(hipMemcpyAsync(mb_buf.p, md5_off.data(), sizeof(uint64_t) * n, hipMemcpyHostToDevice, s));
-    DHIP(hipMemcpyAsync((uint64_t *)mb_buf.p + n, md5_len.data(), sizeof(uint64_t) * n,
-                        hipMemcpyHostToDevice, s));
-    DHIP(launch_bytes_md5((const uint8_t *)d->bytes.p, (const uint64_t *)mb_buf.p,
-                          (const uint64_t *)mb_buf.p + n, n, (uint8_t *)d->md5.p, s));
-    DHIP(hipEventRecord(d->ev[7], s));
-    std::vector<uint8_t> md5(16 * (size_t)n);
+    DHIP(sl.md5meta.ensure(sizeof(uint64_t) * 2 * std::max<uint32_t>(n, 1)));
+    if (sl.md5_cap < 16 * (size_t)std::max<uint32_t>(n, 1)) {
+        if (sl.md5_h)
+            (void)hipHostFree(sl.md5_h);
+        sl.md5_h = nullptr;
+        sl.md5_cap = 0;
+        DHIP(hipHostMalloc((void **)&sl.md5_h, 16 * (size_t)std::max<uint32_t>(n, 1),
+                           hipHostMallocDefault));
+        sl.md5_cap = 16 * (size_t)std::max<uint32_t>(n, 1);
+    }
+    DHIP(hipStreamWaitEvent(sl.s_md5, ev[6], 0));
     if (n)
-        DHIP(hipMemcpyAsync(md5.data(), d->md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost, s));
-    DHIP(hipStreamSynchronize(s));
+        DHIP(hipMemcpyAsync(sl.md5meta.p, sl.md5_meta.data(), sizeof(uint64_t) * 2 * n,
+                            hipMemcpyHostToDevice, sl.s_md5));
+    DHIP(hipEventRecord(ev[7], sl.s_md5));
+    DHIP(launch_bytes_md5((const uint8_t *)sl.bytes.p, (const uint64_t *)sl.md5meta.p,
+                          (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p, sl.s_md5));
+    DHIP(hipEventRecord(ev[8], sl.s_md5));
+    if (n)
+        DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
+                            sl.s_md5));
+    DHIP(hipEventRecord(sl.ev_done, sl.s_md5));
+    // the frame table belongs to the newest batch (decode_fetch)
+    d->tr = tr;
+    d->total_frames = fb;
+    return ATG_OK;
+}
+
+// wait for slot `sl`'s batch and fill its results
+static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result *res)
+{
+    DHIP(hipEventSynchronize(sl.ev_done));
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
-    // interleave, md5, total
-    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {6, 7}, {0, 7}};
+    // unrow, interleave, md5, total (scan start -> md5 end)
+    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {0, 8}};
     for (int k = 0; k < kDecTimed; ++k)
-        (void)hipEventElapsedTime(&d->times[k], d->ev[map[k][0]], d->ev[map[k][1]]);
+        if (hipEventElapsedTime(&d->times[k], sl.ev[map[k][0]], sl.ev[map[k][1]]) != hipSuccess)
+            d->times[k] = 0.f;
     d->have_times = true;
     static const uint8_t zero[16] = {0};
     uint64_t fbase = 0;
+    const uint32_t n = (uint32_t)sl.tr.size();
     for (uint32_t t = 0; t < n; ++t) {
         atg_flac_dec_result &r = res[t];
-        const DecCount &c = d->cnt[t];
-        r.pcm_offset = d->tr[t].pcm_base / d->tr[t].channels;
+        const DecCount &c = sl.cnt[t];
+        r.pcm_offset = sl.tr[t].pcm_base / sl.tr[t].channels;
         r.first_frame = (uint32_t)fbase;
         r.walk_frames = c.n_frames;
         r.walk_status = c.status;
         fbase += c.n_frames;
-        std::memcpy(r.md5, &md5[16 * (size_t)t], 16);
+        std::memcpy(r.md5, &sl.md5_h[16 * (size_t)t], 16);
         if (c.crc_frame != 0xFFFFFFFFu) { // read() stops at the bad frame
             r.pcm_frames = c.crc_pcm;
             r.n_frames = c.crc_frame;
@@ -1467,16 +1528,81 @@ static atg_status run_decode(atg_decoder *d, const uint8_t *d_data, uint64_t len
             r.n_frames = c.n_frames;
             r.status = c.status;
             // FlacDecoder_verify_okay (flac.c:479-493) once remaining reaches 0
-            if (r.status == FD_OK && std::memcmp(tracks[t].md5, zero, 16) != 0 &&
-                std::memcmp(tracks[t].md5, r.md5, 16) != 0)
+            if (r.status == FD_OK && std::memcmp(sl.want[t].md5, zero, 16) != 0 &&
+                std::memcmp(sl.want[t].md5, r.md5, 16) != 0)
                 r.status = FD_MD5;
         }
         r.reserved = 0;
     }
+    sl.busy = false;
+    d->last = (int)(&sl - d->slot);
     return ATG_OK;
 }
 
+// the slot for a new batch: the older of the two, waited for if still busy
+static atg_status take_dec_slot(atg_decoder *d, DecSlot **out)
+{
+    DecSlot *sl = &d->slot[0];
+    if (d->slot[1].ticket < sl->ticket)
+        sl = &d->slot[1];
+    if (sl->busy)
+        return dfail(ATG_ERR_INVALID, "two decode batches already in flight: wait for one");
+    sl->ticket = d->next_ticket++;
+    *out = sl;
+    return ATG_OK;
+}
+
+static DecSlot *find_dec_ticket(atg_decoder *d, uint64_t ticket)
+{
+    for (DecSlot &sl : d->slot)
+        if (sl.ticket == ticket && sl.busy)
+            return &sl;
+    return nullptr;
+}
+
 extern "C" {
+
+atg_status atg_flac_decode_device_async(atg_decoder *d, const void *d_data, uint64_t len,
+                                        const atg_flac_dec_track *tracks, uint32_t n,
+                                        uint64_t *ticket)
+{
+    if (!d || (!tracks && n) || !ticket || (!d_data && len))
+        return dfail(ATG_ERR_INVALID, "NULL argument");
+    if (((uintptr_t)d_data) & 3)
+        return dfail(ATG_ERR_INVALID, "d_data must be 4-byte aligned");
+    DHIP(hipSetDevice(d->device));
+    DecSlot *sl = nullptr;
+    atg_status st = take_dec_slot(d, &sl);
+    if (st != ATG_OK)
+        return st;
+    st = enqueue_decode(d, *sl, (const uint8_t *)d_data, len, tracks, n);
+    if (st != ATG_OK)
+        return st;
+    sl->busy = true;
+    *ticket = sl->ticket;
+    return ATG_OK;
+}
+
+atg_status atg_flac_decode_wait(atg_decoder *d, uint64_t ticket, atg_flac_dec_result *results,
+                                const int32_t **d_pcm, uint64_t *total_samples)
+{
+    if (!d)
+        return dfail(ATG_ERR_INVALID, "NULL decoder");
+    DecSlot *sl = find_dec_ticket(d, ticket);
+    if (!sl)
+        return dfail(ATG_ERR_INVALID, "unknown or already waited decode ticket");
+    if (!results && !sl->tr.empty())
+        return dfail(ATG_ERR_INVALID, "NULL results");
+    DHIP(hipSetDevice(d->device));
+    atg_status st = finish_decode(d, *sl, results);
+    if (st != ATG_OK)
+        return st;
+    if (d_pcm)
+        *d_pcm = (const int32_t *)sl->pcm.p;
+    if (total_samples)
+        *total_samples = sl->total_samples;
+    return ATG_OK;
+}
 
 atg_status atg_flac_decode_device(atg_decoder *d, const void *d_data, uint64_t len,
                                   const atg_flac_dec_track *tracks, uint32_t n,
@@ -1485,17 +1611,11 @@ atg_status atg_flac_decode_device(atg_decoder *d, const void *d_data, uint64_t l
 {
     if (!d || (!tracks && n) || (!results && n) || (!d_data && len))
         return dfail(ATG_ERR_INVALID, "NULL argument");
-    if (((uintptr_t)d_data) & 3)
-        return dfail(ATG_ERR_INVALID, "d_data must be 4-byte aligned");
-    DHIP(hipSetDevice(d->device));
-    atg_status st = run_decode(d, (const uint8_t *)d_data, len, tracks, n, results);
+    uint64_t ticket = 0;
+    atg_status st = atg_flac_decode_device_async(d, d_data, len, tracks, n, &ticket);
     if (st != ATG_OK)
         return st;
-    if (d_pcm)
-        *d_pcm = (const int32_t *)d->pcm.p;
-    if (total_samples)
-        *total_samples = d->total_samples;
-    return ATG_OK;
+    return atg_flac_decode_wait(d, ticket, results, d_pcm, total_samples);
 }
 
 atg_status atg_flac_decode_host(atg_decoder *d, const uint8_t *data, uint64_t len,
@@ -1506,15 +1626,24 @@ atg_status atg_flac_decode_host(atg_decoder *d, const uint8_t *data, uint64_t le
     if (!d || (!tracks && n) || (!results && n) || (!data && len))
         return dfail(ATG_ERR_INVALID, "NULL argument");
     DHIP(hipSetDevice(d->device));
+    // the staging buffer is read by the decoder stream: no batch in flight
+    for (DecSlot &sl : d->slot)
+        if (sl.busy)
+            return dfail(ATG_ERR_INVALID, "a device decode is in flight: wait for it first");
     DHIP(d->data.ensure(len + 64));
     DHIP(hipMemsetAsync((uint8_t *)d->data.p + (len & ~3ull), 0, 64, d->s));
     if (len)
         DHIP(hipMemcpyAsync(d->data.p, data, len, hipMemcpyHostToDevice, d->s));
-    atg_status st = run_decode(d, (const uint8_t *)d->data.p, len, tracks, n, results);
+    uint64_t ticket = 0;
+    atg_status st = atg_flac_decode_device_async(d, d->data.p, len, tracks, n, &ticket);
+    if (st != ATG_OK)
+        return st;
+    uint64_t ts = 0;
+    st = atg_flac_decode_wait(d, ticket, results, nullptr, &ts);
     if (st != ATG_OK)
         return st;
     if (total_samples)
-        *total_samples = d->total_samples;
+        *total_samples = ts;
     if (total_frames)
         *total_frames = d->total_frames;
     return ATG_OK;
@@ -1526,12 +1655,15 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
 {
     if (!d)
         return dfail(ATG_ERR_INVALID, "NULL decoder");
-    if ((pcm && pcm_cap < d->total_samples) ||
+    if (d->last < 0)
+        return dfail(ATG_ERR_INVALID, "no decoded batch");
+    DecSlot &sl = d->slot[d->last];
+    if ((pcm && pcm_cap < sl.total_samples) ||
         ((frame_offsets || frame_block_sizes) && frame_cap < d->total_frames))
         return dfail(ATG_ERR_CAPACITY, "output buffer too small for the decoded batch");
     DHIP(hipSetDevice(d->device));
-    if (pcm && d->total_samples)
-        DHIP(hipMemcpyAsync(pcm, d->pcm.p, sizeof(int32_t) * d->total_samples,
+    if (pcm && sl.total_samples)
+        DHIP(hipMemcpyAsync(pcm, sl.pcm.p, sizeof(int32_t) * sl.total_samples,
                             hipMemcpyDeviceToHost, d->s));
     std::vector<DecFrame> fr;
     if ((frame_offsets || frame_block_sizes) && d->total_frames) {

@@ -165,3 +165,42 @@ def test_truncated_stream_raises_ioerror():
     with pytest.raises(IOError):
         while len(dec.read(4096)):
             pass
+
+
+def test_async_decode_two_in_flight(gpu_engine):
+    """atg_flac_decode_device_async: two batches in flight (batch k's MD5
+    under batch k+1's restore) give the synchronous decode's results and
+    PCM; a third enqueue before a wait is refused"""
+    import torch
+    from audiotools import _atgpu
+    opts = dict(oracle_port.PRESETS["8"])
+    pcms = [signals.make(k, 4096 * 5 + 311 * i, 2, 16, seed=40 + i)
+            for i, k in enumerate(["tone", "noise", "chirp", "silence", "sine"])]
+    o = _atgpu.make_options(**opts)
+    tracks, start = [], 0
+    for p in pcms:
+        tracks.append((start, len(p) // 2))
+        start += len(p) // 2
+    allpcm = np.concatenate(pcms).astype(np.int16)
+    out, res, _, _ = gpu_engine.encode(o, allpcm, tracks, 2, 16, 44100)
+    images = [out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res]
+    dtracks, blob, _ = _batch(images)
+    d_blob = torch.frombuffer(bytearray(blob + b"\0" * 64), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    dec = _atgpu.Decoder(0)
+    want, _, wn = dec.decode_device(d_blob.data_ptr(), len(blob), dtracks)
+    want = [(r.status, r.pcm_frames, bytes(r.md5)) for r in want]
+    t1 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    t2 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    with pytest.raises(_atgpu.ATGError):
+        dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    for t in (t1, t2):
+        got, d_pcm, n = dec.decode_wait(t)
+        assert [(r.status, r.pcm_frames, bytes(r.md5)) for r in got] == want
+        assert n == wn == len(allpcm)
+        host = np.empty(n, dtype=np.int32)
+        gpu_engine.copy_to_host(host, d_pcm)
+        assert np.array_equal(host, allpcm.astype(np.int32))
+    with pytest.raises(_atgpu.ATGError):
+        dec.decode_wait(t1)
+    dec.close()
