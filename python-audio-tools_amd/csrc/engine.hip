@@ -123,6 +123,7 @@ struct Plan;
 struct EncSlot {
     DevBuf frames, tracks, order, coef, shift, est, sub, fdesc, tout, err;
     DevBuf rice_big, scratch; // large-frame path (flac_big.hip)
+    DevBuf slow;              // [count, pad x3][list]: candidates the 16-bit search hands over
     hipStream_t s_aux = nullptr;
     hipEvent_t ev[2 * kNumTimed] = {};
     hipEvent_t ev_tables = nullptr, ev_pack = nullptr, ev_done = nullptr;
@@ -474,6 +475,12 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     HIP_TRY(sl.fdesc.ensure(nf * sizeof(FrameDesc)));
     HIP_TRY(sl.tout.ensure(nt * sizeof(TrackOut)));
     HIP_TRY(sl.err.ensure(sizeof(uint32_t)));
+    // 16-bit search (flac_search16.hip) for full 4096-sample frames; what it
+    // cannot take goes through the general kernel as a list
+    const bool fast16 = !pl.big && p.block_size == ATG_MAX_BLOCK &&
+                        p.max_lpc_order <= ATG_FAST_ORDER && p.bps <= 16u;
+    if (fast16)
+        HIP_TRY(sl.slow.ensure((4 + nf * p.n_cand) * sizeof(uint32_t)));
     const uint32_t big_grid =
         pl.big ? (uint32_t)std::min<uint64_t>(kBigGrid, std::max<uint64_t>(nf, 1) * p.n_cand) : 0u;
     const uint32_t rice_stride = 1u << pl.big_porder;
@@ -528,7 +535,19 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                                            rice_stride, (uint8_t *)sl.scratch.p,
                                            big_slot_bytes(pl), big_row_bytes(pl), big_grid,
                                            e->s_main));
-    else
+    else if (fast16) {
+        uint32_t *cnt = (uint32_t *)sl.slow.p, *list = cnt + 4;
+        HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(uint32_t), e->s_main));
+        HIP_TRY(launch_subframe_search16(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                         (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
+                                         (SubDesc *)sl.sub.p, list, cnt, e->s_main));
+        const uint32_t units = (uint32_t)(nf * p.n_cand);
+        HIP_TRY(launch_subframe_search_list(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                            (const int8_t *)sl.shift.p,
+                                            (const uint8_t *)sl.est.p, (SubDesc *)sl.sub.p,
+                                            derr, list, cnt, std::min<uint32_t>(units, 4096u),
+                                            e->s_main));
+    } else
         HIP_TRY(launch_subframe_search(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
                                        (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
                                        (SubDesc *)sl.sub.p, derr, e->s_main));

@@ -1,0 +1,955 @@
+// flac_search16.hip — K2 fast path: the subframe search for full 4096-sample
+// frames of sources whose samples fit int16.  Same decisions and the same
+// uint32 bit counts as k_subframe_search (flac_search.hip; reference
+// flacenc_write_subframe, src/encoders/flac.c:673-1016, 1326-1505,
+// 1578-1631); any candidate it cannot take is handed to that kernel through
+// a list.
+//
+// Two kernels:
+//   k_frame_search_ms   stereo with mid/side (the FLAC-8 case): one
+//                       256-thread workgroup per frame, wave c searches
+//                       candidate c.  The frame's PCM is read once and LDS
+//                       holds L, R and M = (L + R) >> 1 as packed int16
+//                       pairs plus the raw (L, R) words (45 KB per frame);
+//                       the side channel S = L - R (17 bits) is never
+//                       stored: its predictor takes one v_dot2 per tap on
+//                       (L, R) words with taps (c, -c) (exact, linear).
+//   k_subframe_search16 any other layout: one wave per candidate with its
+//                       own packed array (candidates outside int16 are
+//                       handed over).
+//
+// Residual arithmetic (lane l owns samples [64l, 64l + 64)).  With
+// O_t = (s[t-1], s[t]) as an int16 pair (an LDS word for odd t, one
+// v_alignbit of two words for even t, shared by every tap pair), tap pairs
+// (c0, -2^sh), (c2, c1), (c4, c3), ... and an accumulator that starts at
+// -2^(sh + w) (w = wasted bits, samples unshifted):
+//     acc >> (sh + w) = floor(pred') - s' - 1 = ~r       (s' = s >> w)
+// exactly -- the reference's r = s' - (sum c s' >> sh), flac.c:1060-1126 --
+// whenever the true sum fits int32 (checked per predictor, wave-uniform;
+// otherwise a 64-bit loop runs).  v = n ^ (n >> 31) is the same for n and
+// ~n, so the loop has no subtraction and no sample unpacking: floor(order /
+// 2) + 1 v_dot2 + 4 VALU per residual, wasted bits included for free.
+// v = |r| - [r < 0] is kept per sample (u >> k = v >> (k - 1) for the
+// zig-zag code u = 2v + [r < 0], k >= 1); #neg = 64 + sum (n >> 31).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "flac_dev.h"
+#include "launch.h"
+#include "partsel.h"
+#include "pcm_read.h"
+#include "residual.h"
+#include "rice.h"
+#include "wave.h"
+
+// timing experiments only (tools/gpu_exp.sh), 0 in every product build:
+// 1 FIXED predictor only, 2 no pass 2, 3 trivial partition choice, 4 no FIXED sums
+#ifndef ATG_K2F_EXP
+#define ATG_K2F_EXP 0
+#endif
+// waves per SIMD the register allocation targets
+#ifndef ATG_K2F_WPE
+#define ATG_K2F_WPE 3
+#endif
+
+#define PK_PRE 16
+#define PK_WORDS (PK_PRE + ATG_MAX_BLOCK / 2 + 4 * (ATG_MAX_BLOCK / 64) + 16)
+
+// word m of a packed candidate; 4 pad words after every 32 words, so lane
+// runs (32 words apart) start 36 words apart: 16-byte aligned and
+// conflict-free for ds_read_b128 (36 l mod 64 hits every 4-bank group of a
+// 16-lane access group once).  Words -8..-1 (lane 0's history) are zeros.
+__device__ __forceinline__ int paddr(int m) { return PK_PRE + m + 4 * (m >> 5); }
+
+// low / high sample of a packed word
+__device__ __forceinline__ int lo16(uint32_t w) { return (int32_t)(int16_t)(w & 0xFFFFu); }
+__device__ __forceinline__ int hi16(uint32_t w) { return (int32_t)w >> 16; }
+
+// sample i of a packed image (i >= -16), sign-extended
+__device__ __forceinline__ int32_t pk_sample(const uint32_t *__restrict__ pk, int i)
+{
+    const uint32_t w = pk[paddr(i >> 1)];
+    return (i & 1) ? hi16(w) : lo16(w);
+}
+
+// raw (L, R) word image of a stereo frame: one word per sample, 4 pad words
+// after every 64 (lane runs 68 words apart: 16-byte aligned, conflict-free
+// for ds_read_b128); words -24..-1 are zeros (lane 0's history)
+#define LR_PRE 24
+#define LR_WORDS (LR_PRE + ATG_MAX_BLOCK + 4 * (ATG_MAX_BLOCK / 64) + 8)
+__device__ __forceinline__ int laddr(int i) { return LR_PRE + i + 4 * (i >> 6); }
+
+// candidate sample i: a packed image (TWO = false) or L - R of an (L, R)
+// word image (TWO = true, the side channel)
+template <bool TWO>
+__device__ __forceinline__ int32_t cand_pk(const uint32_t *__restrict__ img, int i)
+{
+    if (TWO) {
+        const uint32_t w = img[laddr(i)];
+        return lo16(w) - hi16(w);
+    }
+    return pk_sample(img, i);
+}
+
+__device__ __forceinline__ uint32_t align16(uint32_t hi_word, uint32_t lo_word)
+{
+    return __builtin_amdgcn_alignbit(hi_word, lo_word, 16);
+}
+
+__device__ __forceinline__ int dot2(uint32_t a, int b_uniform, int c)
+{
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a),
+                                  __builtin_bit_cast(short2_t, b_uniform), c, false);
+}
+
+// First tap of a residual: VOP3 v_dot2 with the tap pair in a VGPR and the
+// accumulator start in an SGPR (one SGPR operand per VALU instruction on
+// gfx950), so no v_mov seeds an accumulator per sample.
+__device__ __forceinline__ int dot2_first(uint32_t a, int tap_v, int acc_s)
+{
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(tap_v), "s"(acc_s));
+    return d;
+}
+
+// A lane's window over one packed image: words -8..15 of the current
+// 16-sample chunk (W) and their v_alignbit pairs (E).
+struct Win {
+    uint32_t W[16], E[16];
+};
+
+__device__ __forceinline__ void win_init(const uint32_t *__restrict__ run, Win &x)
+{
+    const uint4 h0 = *(const uint4 *)(run - 12);
+    const uint4 h1 = *(const uint4 *)(run - 8);
+    x.W[8] = h0.x; x.W[9] = h0.y; x.W[10] = h0.z; x.W[11] = h0.w;
+    x.W[12] = h1.x; x.W[13] = h1.y; x.W[14] = h1.z; x.W[15] = h1.w;
+#pragma unroll
+    for (int k = 9; k < 16; ++k)
+        x.E[k] = align16(x.W[k], x.W[k - 1]);
+    x.E[8] = 0;
+}
+
+// slide by one chunk: words 8c .. 8c + 7 of the run
+__device__ __forceinline__ void win_next(const uint32_t *__restrict__ run, int c, Win &x)
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        x.W[k] = x.W[8 + k];
+        x.E[k] = x.E[8 + k];
+    }
+    const uint4 a0 = *(const uint4 *)(run + 8 * c);
+    const uint4 a1 = *(const uint4 *)(run + 8 * c + 4);
+    x.W[8] = a0.x; x.W[9] = a0.y; x.W[10] = a0.z; x.W[11] = a0.w;
+    x.W[12] = a1.x; x.W[13] = a1.y; x.W[14] = a1.z; x.W[15] = a1.w;
+#pragma unroll
+    for (int k = 8; k < 16; ++k)
+        x.E[k] = align16(x.W[k], x.W[k - 1]);
+}
+
+// O_{t - 2j} for sample ii of the chunk
+__device__ __forceinline__ uint32_t win_pair(const Win &x, int ii, int j)
+{
+    return (ii & 1) ? x.W[8 + (ii - 1) / 2 - j] : x.E[8 + ii / 2 - j];
+}
+
+// Pass 1 of one predictor over the lane's 64 samples, D tap pairs cp on a
+// packed image.  Keeps v per sample in u[] and returns the run's sum |r| =
+// sum (v + [r < 0]) = 64 + sum (v + (n >> 31)) (n >= 0 <=> r < 0); lane 0's
+// warm-up samples (i < warm) are forced to n = -1 (v = 0, |r| = 0).  shv: the total shift sh + w, in a VGPR (a
+// shift by an SGPR operand issues at half the rate on gfx950,
+// tools/int_rate.hip).
+template <int D>
+__device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const int (&cp)[14],
+                                      int c0acc, int shv, int warm, uint32_t (&u)[ATG_RUN],
+                                      uint32_t &sabs)
+{
+    int tap0 = cp[0];
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap pair in a VGPR
+    Win A;
+    win_init(run, A);
+    uint32_t sa = 0;
+#pragma unroll
+    for (int c = 0; c < ATG_RUN / 16; ++c) {
+        // keep each chunk's loads inside the chunk (bounds live registers)
+        asm volatile("" ::: "memory");
+        win_next(run, c, A);
+#pragma unroll
+        for (int ii = 0; ii < 16; ++ii) {
+            const int i = 16 * c + ii;
+            int acc = dot2_first(win_pair(A, ii, 0), tap0, c0acc);
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+                acc = dot2(win_pair(A, ii, j), cp[j], acc);
+            int n = acc >> shv;
+            if (i < ATG_FAST_ORDER)
+                n = i < warm ? -1 : n;
+            const uint32_t s31 = (uint32_t)(n >> 31);
+            const uint32_t v = (uint32_t)n ^ s31;
+            u[i] = v;
+            sa = sa + v + s31; // v_add3_u32
+        }
+    }
+    sabs = sa + (uint32_t)ATG_RUN;
+}
+
+// The same for the side channel on an (L, R) word image: tap k of sample t
+// is v_dot2((L, R)[t - k], (c_(k-1), -c_(k-1))), tap 0 the fold
+// (-2^sh, 2^sh); TAPS = min(2D, 13) covers order <= 2D - 1.
+template <int D>
+__device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const int (&cl)[14],
+                                         int c0acc, int shv, int warm, uint32_t (&u)[ATG_RUN],
+                                         uint32_t &sabs)
+{
+    constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
+    int tap0 = cl[0];
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap in a VGPR
+    uint32_t W[28]; // words t0 - 12 .. t0 + 15 of the current chunk
+    {
+        const uint4 h0 = *(const uint4 *)(run - 16);
+        const uint4 h1 = *(const uint4 *)(run - 12);
+        const uint4 h2 = *(const uint4 *)(run - 8);
+        W[16] = h0.x; W[17] = h0.y; W[18] = h0.z; W[19] = h0.w;
+        W[20] = h1.x; W[21] = h1.y; W[22] = h1.z; W[23] = h1.w;
+        W[24] = h2.x; W[25] = h2.y; W[26] = h2.z; W[27] = h2.w;
+    }
+    uint32_t sa = 0;
+#pragma unroll
+    for (int c = 0; c < ATG_RUN / 16; ++c) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+            W[k] = W[16 + k];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const uint4 a = *(const uint4 *)(run + 16 * c + 4 * q);
+            W[12 + 4 * q] = a.x;
+            W[13 + 4 * q] = a.y;
+            W[14 + 4 * q] = a.z;
+            W[15 + 4 * q] = a.w;
+        }
+#pragma unroll
+        for (int ii = 0; ii < 16; ++ii) {
+            const int i = 16 * c + ii;
+            int acc = dot2_first(W[12 + ii], tap0, c0acc);
+#pragma unroll
+            for (int k = 1; k < TAPS; ++k)
+                acc = dot2(W[12 + ii - k], cl[k], acc);
+            int n = acc >> shv;
+            if (i < ATG_FAST_ORDER)
+                n = i < warm ? -1 : n;
+            const uint32_t s31 = (uint32_t)(n >> 31);
+            const uint32_t v = (uint32_t)n ^ s31;
+            u[i] = v;
+            sa = sa + v + s31; // v_add3_u32
+        }
+    }
+    sabs = sa + (uint32_t)ATG_RUN;
+}
+
+struct Eval16 {
+    uint32_t bits; // residual section bits
+    PartSel sel;
+};
+
+// One predictor with the folded 32-bit arithmetic (caller checked the
+// bounds): pass 1, partition search, exact bits.  run: the lane's run in a
+// packed image, or in the (L, R) word image (TWO).
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
+                                            const int (&cf)[ATG_FAST_ORDER], int order, int sh,
+                                            uint32_t w)
+{
+    int cq[14];
+    if (TWO) {
+        // (L, R) taps: (-2^sh, 2^sh), then (c_k, -c_k)
+        cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
+#pragma unroll
+        for (int k = 1; k < 14; ++k) {
+            const int ck = k - 1 < ATG_FAST_ORDER ? cf[k - 1] : 0;
+            cq[k] = (int)(((uint32_t)ck & 0xFFFFu) | ((uint32_t)(-ck) << 16));
+        }
+    } else {
+        // pairs (c0, -2^sh), (c2, c1), (c4, c3), ...
+        cq[0] = (int)(((uint32_t)cf[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
+#pragma unroll
+        for (int j = 1; j < 7; ++j) {
+            const int lo = 2 * j < ATG_FAST_ORDER ? cf[2 * j] : 0;
+            cq[j] = (int)(((uint32_t)lo & 0xFFFFu) | ((uint32_t)cf[2 * j - 1] << 16));
+        }
+#pragma unroll
+        for (int j = 7; j < 14; ++j)
+            cq[j] = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 14; ++j)
+        cq[j] = uniform_i32(cq[j]);
+    const int c0acc = uniform_i32(-(1 << (sh + (int)w)));
+    int shv = sh + (int)w;
+    asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
+    const int warm = c.lane == 0 ? order : 0;
+    uint32_t u[ATG_RUN];
+    uint32_t lane_sum; // sum |r| of the run
+    if (TWO) {
+        switch (order / 2 + 1) {
+        case 1: pass1_lr<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 2: pass1_lr<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 3: pass1_lr<3>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 4: pass1_lr<4>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 5: pass1_lr<5>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 6: pass1_lr<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        default: pass1_lr<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        }
+    } else {
+        switch (order / 2 + 1) {
+        case 1: pass1<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 2: pass1<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 3: pass1<3>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 4: pass1<4>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 5: pass1<5>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 6: pass1<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        default: pass1<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        }
+    }
+    Eval16 ev;
+#if ATG_K2F_EXP == 3
+    ev.sel.porder = 6; ev.sel.method = 0; ev.sel.k_own = ev.sel.k_lane = (lane_sum >> 6) & 7u;
+    ev.sel.hdr_bits = 262;
+    if (0)
+#endif
+    if (wave_all(lane_sum < (1u << 25)))
+        ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
+    else
+        ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
+    const uint32_t k = ev.sel.k_lane;
+    const uint32_t cnt = (uint32_t)(ATG_RUN - warm);
+    const uint32_t kv = k ? k - 1u : 0u;
+    uint32_t sh2 = 0;
+#if ATG_K2F_EXP == 2
+    sh2 = u[kv & 63];
+#else
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; t += 2)
+        sh2 = sh2 + (u[t] >> kv) + (u[t + 1] >> kv); // v_add3_u32
+#endif
+    // k = 0: sum u = 2 sum v + #neg = sum v + sum |r| (sh2 = sum v)
+    const uint32_t lb = cnt * (1u + k) + (k ? sh2 : sh2 + lane_sum);
+    ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
+    return ev;
+}
+
+// Any predictor (order <= 12): 64-bit accumulation on the shifted samples,
+// residuals recomputed for the exact bits.
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_wide(const uint32_t *__restrict__ img, const RunCtx &c,
+                                            const int *cf, int order, int shift, uint32_t w)
+{
+    uint64_t sum = 0;
+    const int start = max(c.a, order);
+    const int end = c.a + c.len;
+    for (int i = start; i < end; ++i) {
+        int64_t acc = 0;
+        for (int k = 0; k < order; ++k)
+            acc += (int64_t)cf[k] * (int64_t)(cand_pk<TWO>(img, i - 1 - k) >> w);
+        const int r = (int)((uint32_t)(cand_pk<TWO>(img, i) >> w) -
+                            (uint32_t)(int32_t)(acc >> shift));
+        sum += iabs_u(r);
+    }
+    Eval16 ev;
+    ev.sel = select_partitions(sum, (uint32_t)order, c);
+    const uint32_t k = ev.sel.k_lane;
+    uint32_t lb = 0;
+    for (int i = start; i < end; ++i) {
+        int64_t acc = 0;
+        for (int k2 = 0; k2 < order; ++k2)
+            acc += (int64_t)cf[k2] * (int64_t)(cand_pk<TWO>(img, i - 1 - k2) >> w);
+        const int r = (int)((uint32_t)(cand_pk<TWO>(img, i) >> w) -
+                            (uint32_t)(int32_t)(acc >> shift));
+        lb += (zigzag(r) >> k) + 1u + k;
+    }
+    ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
+    return ev;
+}
+
+// FIXED predictor of order o as taps (flac.c:918-1016)
+__device__ __forceinline__ int fixed_tap16(uint32_t o, int j)
+{
+    switch (o) {
+    case 1: return j == 0 ? 1 : 0;
+    case 2: return j == 0 ? 2 : j == 1 ? -1 : 0;
+    case 3: return j == 0 ? 3 : j == 1 ? -3 : j == 2 ? 1 : 0;
+    case 4: return j == 0 ? 4 : j == 1 ? -6 : j == 2 ? 4 : j == 3 ? -1 : 0;
+    default: return 0;
+    }
+}
+
+// Sums of |x|, |d1| .. |d4| over the lane's run, unshifted samples (every
+// term is a multiple of 2^w, so their order and ties are those of the
+// shifted sums the reference compares, flac.c:856-916); samples 0..3 are
+// outside the sums.  |d_k| < 2^(17 + k): 64 terms per lane < 2^28, the
+// frame's sums < 2^31.  run: packed image, or (L, R) words (TWO).
+template <bool TWO>
+__device__ __forceinline__ uint32_t fixed_order_of(const uint32_t *__restrict__ run, int lane)
+{
+    uint32_t a5[5] = {0, 0, 0, 0, 0};
+    int x1, x2, x3, x4;
+    {
+        const uint4 h = *(const uint4 *)(run - 8); // packed: a-8 .. a-1; (L, R): a-4 .. a-1
+        if (TWO) {
+            x1 = lo16(h.w) - hi16(h.w);
+            x2 = lo16(h.z) - hi16(h.z);
+            x3 = lo16(h.y) - hi16(h.y);
+            x4 = lo16(h.x) - hi16(h.x);
+        } else {
+            x1 = hi16(h.w);
+            x2 = lo16(h.w);
+            x3 = hi16(h.z);
+            x4 = lo16(h.z);
+        }
+    }
+    int d1p = x1 - x2, d2p = d1p - (x2 - x3);
+    int d3p = d2p - ((x2 - x3) - (x3 - x4));
+    // chunks rolled: nothing here needs static indexing across chunks, and
+    // an unrolled schedule computes all 64 difference chains at once
+#pragma unroll 1
+    for (int chn = 0; chn < ATG_RUN / 16; ++chn) {
+        int x[16];
+        if (TWO) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const uint4 a = *(const uint4 *)(run + 16 * chn + 4 * q);
+                x[4 * q] = lo16(a.x) - hi16(a.x);
+                x[4 * q + 1] = lo16(a.y) - hi16(a.y);
+                x[4 * q + 2] = lo16(a.z) - hi16(a.z);
+                x[4 * q + 3] = lo16(a.w) - hi16(a.w);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < 2; ++q) {
+                const uint4 a = *(const uint4 *)(run + 8 * chn + 4 * q);
+                x[8 * q] = lo16(a.x);
+                x[8 * q + 1] = hi16(a.x);
+                x[8 * q + 2] = lo16(a.y);
+                x[8 * q + 3] = hi16(a.y);
+                x[8 * q + 4] = lo16(a.z);
+                x[8 * q + 5] = hi16(a.z);
+                x[8 * q + 6] = lo16(a.w);
+                x[8 * q + 7] = hi16(a.w);
+            }
+        }
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+            const int x0 = x[tt];
+            const int d1 = x0 - x1, d2 = d1 - d1p, d3 = d2 - d2p, d4 = d3 - d3p;
+            x1 = x0;
+            d1p = d1;
+            d2p = d2;
+            d3p = d3;
+            const bool v = chn > 0 || tt >= 4 || lane > 0;
+            a5[0] += v ? iabs_u(x0) : 0u;
+            a5[1] += v ? iabs_u(d1) : 0u;
+            a5[2] += v ? iabs_u(d2) : 0u;
+            a5[3] += v ? iabs_u(d3) : 0u;
+            a5[4] += v ? iabs_u(d4) : 0u;
+        }
+    }
+    uint32_t s5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        s5[k] = dpp_wave_sum<uint32_t>(a5[k]);
+    uint32_t best = s5[0], order = 0;
+#pragma unroll
+    for (int k = 1; k < 5; ++k)
+        if (s5[k] < best) {
+            best = s5[k];
+            order = (uint32_t)k;
+        }
+    return uniform_u32(order);
+}
+
+// Candidate extrema over the frame (unshifted), wave-uniform
+struct CandStats {
+    int32_t mn, mx;
+    uint32_t orv;
+};
+
+// The search of one candidate (one wave): samples in a packed image, or
+// L - R of an (L, R) word image (TWO), statistics from staging.  Writes its
+// SubDesc.
+template <bool TWO>
+__device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uint32_t unit,
+                                            uint32_t sbps, const uint32_t *__restrict__ img,
+                                            CandStats cs,
+                                            int lane, const int16_t *__restrict__ coef_tab,
+                                            const int8_t *__restrict__ shift_tab,
+                                            const uint8_t *__restrict__ est_tab,
+                                            SubDesc *__restrict__ d)
+{
+    if (p.try_constant && cs.mn == cs.mx) {
+        if (lane == 0) {
+            d->bits = 8u + sbps;
+            d->type = SF_CONSTANT;
+            d->order = 0;
+            d->wasted = 0;
+            d->porder = 0;
+            d->method = 0;
+            d->precision = 0;
+            d->shift = 0;
+            d->sbps = (uint8_t)sbps;
+        }
+        return;
+    }
+    const uint32_t w = cs.orv ? (uint32_t)__builtin_ctz(cs.orv) : 0u;
+    const uint32_t amax = max(iabs_u(cs.mn), iabs_u(cs.mx)); // unshifted
+    // every sample is a multiple of 2^w, so max|s >> w| = max|s| >> w
+    const uint32_t maxabs = amax >> w;
+    const uint32_t *__restrict__ run =
+        TWO ? img + LR_PRE + (ATG_RUN + 4) * lane : img + PK_PRE + 36 * lane;
+
+    RunCtx c;
+    c.lane = lane;
+    c.a = ATG_RUN * lane;
+    c.len = ATG_RUN;
+    c.N = N;
+    c.max_rice = p.max_rice;
+    c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
+    const uint32_t wf = w ? w + 1u : 1u;
+    const uint32_t rb = sbps - w; // bits per warm-up / verbatim sample
+
+    // ---- FIXED order by |residual| sums over samples [4,N) (flac.c:856-916)
+#if ATG_K2F_EXP == 4
+    const uint32_t fixed_order = 2u;
+#else
+    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run, lane) : 0u;
+#endif
+
+    // ---- LPC candidate orders (flac.c:1034-1126); N = 4096 > M + 1 always
+    const int16_t *__restrict__ qtab = coef_tab + (size_t)unit * p.coef_stride;
+    const int8_t *__restrict__ stab = shift_tab + (size_t)unit * p.max_lpc_order;
+    const uint32_t M = p.max_lpc_order;
+    uint32_t lo = 1, hi = 0;
+    if (p.try_lpc) {
+        if (p.exhaustive) {
+            lo = 1;
+            hi = M;
+        } else {
+            lo = hi = est_tab[unit];
+        }
+    }
+
+    // ---- evaluate every predictor: [FIXED], LPC lo..hi
+    uint32_t fixed_bits = 0;
+    PartSel fixed_sel = {};
+    uint32_t lpc_bits = 0xFFFFFFFFu, lpc_order = 0, lpc_prec = 0;
+    int lpc_shift = 0;
+    PartSel lpc_sel = {};
+#if ATG_K2F_EXP == 1
+    const uint32_t n_pred = p.try_fixed ? 1u : 0u;
+#else
+    const uint32_t n_pred = (p.try_fixed ? 1u : 0u) + (p.try_lpc ? hi - lo + 1u : 0u);
+#endif
+    for (uint32_t pi = 0; pi < n_pred; ++pi) {
+        const bool is_fixed = p.try_fixed && pi == 0;
+        const uint32_t o = is_fixed ? fixed_order : lo + pi - (p.try_fixed ? 1u : 0u);
+        int shift = 0;
+        uint32_t prec = 0;
+        const int16_t *__restrict__ row = qtab + (size_t)(o ? o - 1u : 0u) * p.coef_row;
+        if (!is_fixed) {
+            shift = uniform_i32(stab[o - 1u]);
+            prec = p.qlp_precision;
+        }
+        int cfu[ATG_FAST_ORDER];
+        uint64_t csum = 0;
+#pragma unroll
+        for (int j = 0; j < ATG_FAST_ORDER; ++j) {
+            const int cj = is_fixed ? fixed_tap16(o, j) : ((uint32_t)j < o ? (int)row[j] : 0);
+            cfu[j] = cj;
+            csum += (uint64_t)(cj < 0 ? -cj : cj);
+        }
+        // folded int32 sum exact: |sum c s| + 2^sh |s| + 2^(sh + w) < 2^31
+        // on unshifted samples (TWO: the tap (-2^sh, 2^sh) needs
+        // 2^sh <= 32767); 32-bit run sums: codes < 2^26
+        const uint64_t mu = amax, ms = maxabs;
+        const bool fold_ok = csum * mu + (mu << shift) + (1ull << (shift + (int)w)) < (1ull << 31) &&
+                             (!TWO || shift <= 14);
+        const uint64_t rbound = ms + ((csum * ms) >> shift) + 1u;
+        Eval16 ev;
+        if (fold_ok && 2u * rbound + 1u < (1ull << 26))
+            ev = eval_fold<TWO>(run, c, cfu, (int)o, shift, w);
+        else
+            ev = eval_wide<TWO>(img, c, cfu, (int)o, shift, w);
+        if (is_fixed) {
+            fixed_bits = 7u + wf + o * rb + ev.bits;
+            fixed_sel = ev.sel;
+        } else {
+            const uint32_t bits = 7u + wf + o * rb + 4u + 5u + o * prec + ev.bits;
+            if (bits < lpc_bits) {
+                lpc_bits = bits;
+                lpc_order = o;
+                lpc_shift = shift;
+                lpc_prec = prec;
+                lpc_sel = ev.sel;
+            }
+        }
+    }
+
+    // ---- subframe choice (flac.c:727-809)
+    const uint32_t verbatim_cmp = p.try_verbatim ? rb * N : 0x7FFFFFFFu;
+    int pick;
+    const bool F = p.try_fixed, L = p.try_lpc, V = p.try_verbatim;
+    if (F && L && V) {
+        const uint32_t m = lpc_bits < verbatim_cmp ? lpc_bits : verbatim_cmp;
+        pick = fixed_bits < m ? SF_FIXED : (lpc_bits < verbatim_cmp ? SF_LPC : SF_VERBATIM);
+    } else if (!F && !L) {
+        pick = SF_VERBATIM;
+    } else if (F && !L && !V) {
+        pick = SF_FIXED;
+    } else if (!F && L && !V) {
+        pick = SF_LPC;
+    } else if (F && L && !V) {
+        pick = fixed_bits < lpc_bits ? SF_FIXED : SF_LPC;
+    } else if (F && !L && V) {
+        pick = fixed_bits < verbatim_cmp ? SF_FIXED : SF_VERBATIM;
+    } else {
+        pick = lpc_bits < verbatim_cmp ? SF_LPC : SF_VERBATIM;
+    }
+
+    const PartSel &sel = pick == SF_FIXED ? fixed_sel : lpc_sel;
+    if (pick != SF_VERBATIM) {
+        // rice parameter of partition j is held by its first lane
+        const uint32_t po = sel.porder;
+        const uint32_t mask = (64u >> po) - 1u;
+        if (((uint32_t)lane & mask) == 0u)
+            d->rice[(uint32_t)lane >> (6u - po)] = (uint8_t)sel.k_own;
+    }
+    if (pick == SF_LPC) {
+        if (lane < (int)lpc_order)
+            d->coef[lane] = qtab[(lpc_order - 1u) * p.coef_row + lane];
+    }
+    if (lane == 0) {
+        d->type = (uint8_t)pick;
+        d->wasted = (uint8_t)w;
+        d->sbps = (uint8_t)sbps;
+        d->method = (uint8_t)sel.method;
+        d->porder = (uint8_t)sel.porder;
+        if (pick == SF_FIXED) {
+            d->bits = fixed_bits;
+            d->order = (uint8_t)fixed_order;
+            d->precision = 0;
+            d->shift = 0;
+        } else if (pick == SF_LPC) {
+            d->bits = lpc_bits;
+            d->order = (uint8_t)lpc_order;
+            d->precision = (uint8_t)lpc_prec;
+            d->shift = (int8_t)lpc_shift;
+        } else {
+            d->bits = 7u + wf + rb * N;
+            d->order = 0;
+            d->precision = 0;
+            d->shift = 0;
+            d->method = 0;
+            d->porder = 0;
+        }
+    }
+}
+
+// wave-uniform min / max / OR of per-lane values
+__device__ __forceinline__ CandStats wave_stats(int32_t mn, int32_t mx, uint32_t orv)
+{
+    CandStats s;
+    s.orv = dpp_wave_or_u32(orv);
+    // through the biased unsigned order
+    s.mx = (int32_t)(dpp_wave_max_u32((uint32_t)mx ^ 0x80000000u) ^ 0x80000000u);
+    s.mn = (int32_t)(~dpp_wave_max_u32(~((uint32_t)mn ^ 0x80000000u)) ^ 0x80000000u);
+    return s;
+}
+
+__device__ __forceinline__ void stats_add(const int32_t (&s)[4], int32_t &mn, int32_t &mx,
+                                          uint32_t &orv)
+{
+    mn = min(mn, min(min(s[0], s[1]), min(s[2], s[3])));
+    mx = max(mx, max(max(s[0], s[1]), max(s[2], s[3])));
+    orv |= (uint32_t)s[0] | (uint32_t)s[1] | (uint32_t)s[2] | (uint32_t)s[3];
+}
+
+__device__ __forceinline__ uint2 pack4(const int32_t (&s)[4])
+{
+    uint2 w;
+    w.x = __builtin_amdgcn_perm((uint32_t)s[1], (uint32_t)s[0], 0x05040100u);
+    w.y = __builtin_amdgcn_perm((uint32_t)s[3], (uint32_t)s[2], 0x05040100u);
+    return w;
+}
+
+// ---------------------------------------------------------------------------
+// stereo with mid/side: one workgroup (4 waves) per frame
+
+// 4 stereo PCM frames starting at j0: left / right samples
+template <bool A16, typename T>
+__device__ __forceinline__ void load_lr4(const T *__restrict__ src, uint32_t j0, int32_t (&l)[4],
+                                         int32_t (&r)[4])
+{
+    if constexpr (sizeof(T) == 2 && A16) {
+        const uint4 v = *(const uint4 *)((const uint32_t *)src + j0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            l[q] = lo16(w[q]);
+            r[q] = hi16(w[q]);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            l[q] = (int32_t)src[2u * (j0 + q)];
+            r[q] = (int32_t)src[2u * (j0 + q) + 1u];
+        }
+    }
+}
+
+template <bool A16, typename T>
+__device__ __forceinline__ void stage_ms(const T *__restrict__ src, int tid, uint32_t *__restrict__ img,
+                                         uint32_t *__restrict__ lr, int32_t (&mn)[4],
+                                         int32_t (&mx)[4], uint32_t (&orv)[4])
+{
+#pragma unroll
+    for (int m = 0; m < ATG_MAX_BLOCK / 1024; ++m) {
+        const uint32_t q0 = (uint32_t)(tid + 256 * m); // 4-frame group
+        int32_t s[4][4];
+        load_lr4<A16>(src, 4u * q0, s[0], s[1]);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            s[2][q] = (int32_t)((uint32_t)s[0][q] + (uint32_t)s[1][q]) >> 1;
+            s[3][q] = (int32_t)((uint32_t)s[0][q] - (uint32_t)s[1][q]);
+        }
+#pragma unroll
+        for (int cnd = 0; cnd < 4; ++cnd)
+            stats_add(s[cnd], mn[cnd], mx[cnd], orv[cnd]);
+#pragma unroll
+        for (int cnd = 0; cnd < 3; ++cnd)
+            *(uint2 *)&img[cnd * PK_WORDS + paddr(2 * (int)q0)] = pack4(s[cnd]);
+        uint4 w;
+        w.x = __builtin_amdgcn_perm((uint32_t)s[1][0], (uint32_t)s[0][0], 0x05040100u);
+        w.y = __builtin_amdgcn_perm((uint32_t)s[1][1], (uint32_t)s[0][1], 0x05040100u);
+        w.z = __builtin_amdgcn_perm((uint32_t)s[1][2], (uint32_t)s[0][2], 0x05040100u);
+        w.w = __builtin_amdgcn_perm((uint32_t)s[1][3], (uint32_t)s[0][3], 0x05040100u);
+        *(uint4 *)&lr[laddr(4 * (int)q0)] = w;
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE))) void k_frame_search_ms(
+    FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
+    const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
+    const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
+    uint32_t *__restrict__ slow_list, uint32_t *__restrict__ slow_count)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t img[3 * PK_WORDS]; // L, R, M packed
+    __shared__ __attribute__((aligned(16))) uint32_t lr[LR_WORDS];       // (L, R) words
+    __shared__ int32_t red[4][4][3];                                      // [wave][cand][mn,mx,or]
+
+    const uint32_t f = blockIdx.x;
+    if (f >= p.n_frames)
+        return;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const FrameInfo fi = frames[f];
+    const uint32_t N = fi.n;
+    if (N != ATG_MAX_BLOCK) {
+        if (tid < 4) {
+            const uint32_t slot = atomicAdd(slow_count, 1u);
+            slow_list[slot] = f * 4u + (uint32_t)tid;
+        }
+        return;
+    }
+    if (tid < 3 * PK_PRE)
+        img[(tid / PK_PRE) * PK_WORDS + (tid % PK_PRE)] = 0u;
+    else if (tid < 3 * PK_PRE + LR_PRE)
+        lr[tid - 3 * PK_PRE] = 0u;
+    int32_t mn[4], mx[4];
+    uint32_t orv[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        mn[k] = INT32_MAX;
+        mx[k] = INT32_MIN;
+        orv[k] = 0;
+    }
+    {
+        const T *__restrict__ src = pcm + fi.pcm_start * 2u;
+        if ((((uintptr_t)src) & 15u) == 0u)
+            stage_ms<true>(src, tid, img, lr, mn, mx, orv);
+        else
+            stage_ms<false>(src, tid, img, lr, mn, mx, orv);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const CandStats s = wave_stats(mn[k], mx[k], orv[k]);
+        if (lane == 0) {
+            red[wave][k][0] = s.mn;
+            red[wave][k][1] = s.mx;
+            red[wave][k][2] = (int32_t)s.orv;
+        }
+    }
+    __syncthreads();
+    const uint32_t cand = (uint32_t)wave;
+    CandStats cs;
+    cs.mn = min(min(red[0][cand][0], red[1][cand][0]), min(red[2][cand][0], red[3][cand][0]));
+    cs.mx = max(max(red[0][cand][1], red[1][cand][1]), max(red[2][cand][1], red[3][cand][1]));
+    cs.orv = (uint32_t)(red[0][cand][2] | red[1][cand][2] | red[2][cand][2] | red[3][cand][2]);
+    cs.mn = uniform_i32(cs.mn);
+    cs.mx = uniform_i32(cs.mx);
+    cs.orv = uniform_u32(cs.orv);
+    const uint32_t unit = f * 4u + cand;
+    const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
+    // L, R and M fit int16 for any source of <= 16 bits; S is L - R
+    bool fits = true;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const int32_t a = min(min(red[0][k][0], red[1][k][0]), min(red[2][k][0], red[3][k][0]));
+        const int32_t b = max(max(red[0][k][1], red[1][k][1]), max(red[2][k][1], red[3][k][1]));
+        fits = fits && a >= -32768 && b <= 32767;
+    }
+    if (!fits) {
+        if (lane == 0) {
+            const uint32_t slot = atomicAdd(slow_count, 1u);
+            slow_list[slot] = unit;
+        }
+        return;
+    }
+    if (cand == 3u)
+        search_cand<true>(p, N, unit, sbps, lr, cs, lane, coef_tab, shift_tab, est_tab,
+                          out + unit);
+    else
+        search_cand<false>(p, N, unit, sbps, img + cand * PK_WORDS, cs, lane, coef_tab,
+                           shift_tab, est_tab, out + unit);
+}
+
+// ---------------------------------------------------------------------------
+// any other layout: one wave per candidate
+
+// 4 consecutive candidate samples starting at PCM frame j0
+enum { CS_L = 0, CS_R = 1, CS_AVG = 2, CS_DIF = 3, CS_CH = 4 };
+template <int CS, typename T>
+__device__ __forceinline__ void load4(const T *__restrict__ src, uint32_t j0, uint32_t ch,
+                                      uint32_t cand, int32_t (&s)[4])
+{
+    if constexpr (CS == CS_CH) {
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+            s[q] = (int32_t)src[(size_t)(j0 + q) * ch + cand];
+    } else {
+        int32_t l[4], r[4];
+        load_lr4<false>(src, j0, l, r);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            if (CS == CS_L) s[q] = l[q];
+            else if (CS == CS_R) s[q] = r[q];
+            else if (CS == CS_AVG) s[q] = (int32_t)((uint32_t)l[q] + (uint32_t)r[q]) >> 1;
+            else s[q] = (int32_t)((uint32_t)l[q] - (uint32_t)r[q]);
+        }
+    }
+}
+
+template <int CS, typename T>
+__device__ __forceinline__ void stage16(const T *__restrict__ src, uint32_t ch, uint32_t cand,
+                                        int lane, uint32_t *__restrict__ pk, int32_t &mn,
+                                        int32_t &mx, uint32_t &orv)
+{
+#pragma unroll 4
+    for (int m = 0; m < ATG_MAX_BLOCK / 256; ++m) {
+        const uint32_t q0 = (uint32_t)(lane + 64 * m); // 4-sample group
+        int32_t s[4];
+        load4<CS>(src, 4u * q0, ch, cand, s);
+        stats_add(s, mn, mx, orv);
+        *(uint2 *)&pk[paddr(2 * (int)q0)] = pack4(s);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE))) void k_subframe_search16(
+    FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
+    const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
+    const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
+    uint32_t *__restrict__ slow_list, uint32_t *__restrict__ slow_count)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t pk[PK_WORDS];
+
+    uint32_t f, cand;
+    xcd_unit_map(blockIdx.x, p.n_cand, &f, &cand);
+    if (f >= p.n_frames)
+        return;
+    const int lane = threadIdx.x;
+    const FrameInfo fi = frames[f];
+    const uint32_t N = fi.n;
+    const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
+    const uint32_t sbps = p.bps + ((ms && cand == 3u) ? 1u : 0u);
+    const uint32_t unit = f * p.n_cand + cand;
+
+    auto hand_over = [&]() {
+        if (lane == 0) {
+            const uint32_t slot = atomicAdd(slow_count, 1u);
+            slow_list[slot] = unit;
+        }
+    };
+    if (N != ATG_MAX_BLOCK) {
+        hand_over();
+        return;
+    }
+    if (lane < PK_PRE)
+        pk[lane] = 0u;
+    int32_t mn = INT32_MAX, mx = INT32_MIN;
+    uint32_t orv = 0;
+    {
+        const T *__restrict__ src = pcm + fi.pcm_start * p.channels;
+        if (!ms) {
+            stage16<CS_CH>(src, p.channels, cand, lane, pk, mn, mx, orv);
+        } else {
+            switch (cand) {
+            case 0: stage16<CS_L>(src, 2u, cand, lane, pk, mn, mx, orv); break;
+            case 1: stage16<CS_R>(src, 2u, cand, lane, pk, mn, mx, orv); break;
+            case 2: stage16<CS_AVG>(src, 2u, cand, lane, pk, mn, mx, orv); break;
+            default: stage16<CS_DIF>(src, 2u, cand, lane, pk, mn, mx, orv); break;
+            }
+        }
+    }
+    const CandStats cs = wave_stats(mn, mx, orv);
+    const bool constant = p.try_constant && cs.mn == cs.mx;
+    if (!constant && (cs.mn < -32768 || cs.mx > 32767)) {
+        hand_over();
+        return;
+    }
+    __syncthreads();
+    search_cand<false>(p, N, unit, sbps, pk, cs, lane, coef_tab, shift_tab, est_tab, out + unit);
+}
+
+hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fmt,
+                                    const FrameInfo *frames, const int16_t *coef_tab,
+                                    const int8_t *shift_tab, const uint8_t *est_tab,
+                                    SubDesc *sub, uint32_t *slow_list, uint32_t *slow_count,
+                                    hipStream_t s)
+{
+    if (p.n_frames == 0)
+        return hipSuccess;
+    const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
+    if (ms) {
+        dim3 grid(p.n_frames);
+        if (fmt == 0)
+            hipLaunchKernelGGL((k_frame_search_ms<int16_t>), grid, dim3(256), 0, s, p,
+                               (const int16_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                               slow_list, slow_count);
+        else
+            hipLaunchKernelGGL((k_frame_search_ms<int32_t>), grid, dim3(256), 0, s, p,
+                               (const int32_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                               slow_list, slow_count);
+        return hipGetLastError();
+    }
+    const uint32_t f8 = (p.n_frames + 7u) / 8u * 8u;
+    dim3 grid(f8 * p.n_cand);
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_subframe_search16<int16_t>), grid, dim3(64), 0, s, p,
+                           (const int16_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                           slow_list, slow_count);
+    else
+        hipLaunchKernelGGL((k_subframe_search16<int32_t>), grid, dim3(64), 0, s, p,
+                           (const int32_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                           slow_list, slow_count);
+    return hipGetLastError();
+}

@@ -17,6 +17,20 @@ hipError_t launch_subframe_search(const FlacParams &p, const void *pcm, int fmt,
                                   const int8_t *shift_tab,
                                   const uint8_t *est_tab, SubDesc *sub,
                                   uint32_t *err, hipStream_t s);
+// the candidates flac_search16.hip handed over (list[0 .. *count))
+hipError_t launch_subframe_search_list(const FlacParams &p, const void *pcm, int fmt,
+                                       const FrameInfo *frames, const int16_t *coef_tab,
+                                       const int8_t *shift_tab, const uint8_t *est_tab,
+                                       SubDesc *sub, uint32_t *err, const uint32_t *list,
+                                       const uint32_t *count, uint32_t grid, hipStream_t s);
+// flac_search16.hip: full 4096-sample frames whose candidates fit int16;
+// appends every other candidate to slow_list (count in *slow_count, zeroed
+// by the caller)
+hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fmt,
+                                    const FrameInfo *frames, const int16_t *coef_tab,
+                                    const int8_t *shift_tab, const uint8_t *est_tab,
+                                    SubDesc *sub, uint32_t *slow_list, uint32_t *slow_count,
+                                    hipStream_t s);
 // flac_big.hip: frames longer than 4096 samples / partition orders > 6
 hipError_t launch_subframe_search_big(const FlacParams &p, const void *pcm, int fmt,
                                       const FrameInfo *frames, const int16_t *coef_tab,

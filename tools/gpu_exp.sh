@@ -9,5 +9,5 @@ ARGS="--steps 3 --warmup 1 --no-cpu-baseline --no-verify --no-decode --no-chain 
 timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/exp/base.log 2>&1
 for lib in exp/libatgpu_*.so; do
     n=$(basename $lib .so)
-    ATGPU_LIB=$R/$lib timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/exp/$n.log 2>&1
+    ATGPU_LIB=$R/$lib timeout -k 10 120 python -u bench.py $ARGS > gpurun_out/exp/$n.log 2>&1 || echo "$n failed" >> gpurun_out/exp/failed.txt
 done
