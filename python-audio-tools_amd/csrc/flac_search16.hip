@@ -105,11 +105,18 @@ __device__ __forceinline__ int dot2(uint32_t a, int b_uniform, int c)
 // First tap of a residual: VOP3 v_dot2 with the tap pair in a VGPR and the
 // accumulator start in an SGPR (one SGPR operand per VALU instruction on
 // gfx950), so no v_mov seeds an accumulator per sample.
+#ifndef ATG_K2F_DOT2FIRST
+#define ATG_K2F_DOT2FIRST 1
+#endif
 __device__ __forceinline__ int dot2_first(uint32_t a, int tap_v, int acc_s)
 {
+#if ATG_K2F_DOT2FIRST
     int d;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(tap_v), "s"(acc_s));
     return d;
+#else
+    return dot2(a, tap_v, acc_s);
+#endif
 }
 
 // A lane's window over one packed image: words -8..15 of the current
@@ -473,17 +480,46 @@ struct CandStats {
     uint32_t orv;
 };
 
-// The search of one candidate (one wave): samples in a packed image, or
-// L - R of an (L, R) word image (TWO), statistics from staging.  Writes its
-// SubDesc.
+// Per-candidate state a workgroup's waves share (LDS)
+struct CandInfo {
+    uint32_t active;      // not CONSTANT: its predictors are evaluated
+    uint32_t w;           // wasted bits
+    uint32_t amax;        // max |s|, unshifted
+    uint32_t fixed_order; // FIXED order chosen from the difference sums
+    uint32_t lo, hi;      // LPC orders evaluated
+    uint32_t sbps;
+};
+
+#define K2F_MAXPRED (1 + ATG_FAST_ORDER)
+// Per-(candidate, predictor) results (LDS): residual-section bits
+// (partition header included), partition order, coding method and every
+// lane's Rice parameter
+struct PredRes {
+    uint32_t bits[K2F_MAXPRED];
+    uint8_t porder[K2F_MAXPRED];
+    uint8_t method[K2F_MAXPRED];
+    uint8_t k[K2F_MAXPRED][64];
+};
+
+__device__ __forceinline__ uint32_t n_pred_of(const FlacParams &p, const CandInfo &ci)
+{
+    return (p.try_fixed ? 1u : 0u) + (p.try_lpc ? ci.hi - ci.lo + 1u : 0u);
+}
+
+__device__ __forceinline__ const uint32_t *run_of(const uint32_t *__restrict__ img, bool two,
+                                                  int lane)
+{
+    return two ? img + LR_PRE + (ATG_RUN + 4) * lane : img + PK_PRE + 36 * lane;
+}
+
+// Phase 1 of a candidate (one wave): CONSTANT (written here), wasted bits,
+// the FIXED order (flac.c:856-916, 1578-1620) and the LPC orders to try
+// (flac.c:1034-1126).  img: packed image, or (L, R) words (TWO).
 template <bool TWO>
-__device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uint32_t unit,
-                                            uint32_t sbps, const uint32_t *__restrict__ img,
-                                            CandStats cs,
-                                            int lane, const int16_t *__restrict__ coef_tab,
-                                            const int8_t *__restrict__ shift_tab,
-                                            const uint8_t *__restrict__ est_tab,
-                                            SubDesc *__restrict__ d)
+__device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit, uint32_t sbps,
+                                             const uint32_t *__restrict__ img, CandStats cs,
+                                             int lane, const uint8_t *__restrict__ est_tab,
+                                             SubDesc *__restrict__ d, CandInfo *__restrict__ ci)
 {
     if (p.try_constant && cs.mn == cs.mx) {
         if (lane == 0) {
@@ -496,16 +532,67 @@ __device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uin
             d->precision = 0;
             d->shift = 0;
             d->sbps = (uint8_t)sbps;
+            ci->active = 0;
         }
         return;
     }
     const uint32_t w = cs.orv ? (uint32_t)__builtin_ctz(cs.orv) : 0u;
-    const uint32_t amax = max(iabs_u(cs.mn), iabs_u(cs.mx)); // unshifted
-    // every sample is a multiple of 2^w, so max|s >> w| = max|s| >> w
-    const uint32_t maxabs = amax >> w;
-    const uint32_t *__restrict__ run =
-        TWO ? img + LR_PRE + (ATG_RUN + 4) * lane : img + PK_PRE + 36 * lane;
+#if ATG_K2F_EXP == 4
+    const uint32_t fixed_order = 2u;
+#else
+    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run_of(img, TWO, lane), lane) : 0u;
+#endif
+    uint32_t lo = 1, hi = 0;
+    if (p.try_lpc) {
+        if (p.exhaustive) {
+            lo = 1;
+            hi = p.max_lpc_order;
+        } else {
+            lo = hi = est_tab[unit];
+        }
+    }
+#if ATG_K2F_EXP == 1
+    lo = 1;
+    hi = 0;
+#endif
+    if (lane == 0) {
+        ci->active = 1;
+        ci->w = w;
+        ci->amax = max(iabs_u(cs.mn), iabs_u(cs.mx));
+        ci->fixed_order = fixed_order;
+        ci->lo = lo;
+        ci->hi = hi;
+        ci->sbps = sbps;
+    }
+}
 
+// One predictor of one candidate (one wave, any wave of the workgroup):
+// residual-section bits and partition choice into res[pi].  pi = 0 is
+// FIXED when FIXED is tried, then LPC orders lo, lo + 1, ...
+template <bool TWO>
+__device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N, uint32_t unit,
+                                         const uint32_t *__restrict__ img, const CandInfo &ci,
+                                         uint32_t pi, int lane,
+                                         const int16_t *__restrict__ coef_tab,
+                                         const int8_t *__restrict__ shift_tab,
+                                         PredRes *__restrict__ res)
+{
+    const bool is_fixed = p.try_fixed && pi == 0;
+    const uint32_t o = is_fixed ? ci.fixed_order : ci.lo + pi - (p.try_fixed ? 1u : 0u);
+    const int16_t *__restrict__ qtab = coef_tab + (size_t)unit * p.coef_stride;
+    const int8_t *__restrict__ stab = shift_tab + (size_t)unit * p.max_lpc_order;
+    int shift = 0;
+    const int16_t *__restrict__ row = qtab + (size_t)(o ? o - 1u : 0u) * p.coef_row;
+    if (!is_fixed)
+        shift = uniform_i32(stab[o - 1u]);
+    int cfu[ATG_FAST_ORDER];
+    uint64_t csum = 0;
+#pragma unroll
+    for (int j = 0; j < ATG_FAST_ORDER; ++j) {
+        const int cj = is_fixed ? fixed_tap16(o, j) : ((uint32_t)j < o ? (int)row[j] : 0);
+        cfu[j] = cj;
+        csum += (uint64_t)(cj < 0 ? -cj : cj);
+    }
     RunCtx c;
     c.lane = lane;
     c.a = ATG_RUN * lane;
@@ -513,87 +600,58 @@ __device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uin
     c.N = N;
     c.max_rice = p.max_rice;
     c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
+    // folded int32 sum exact: |sum c s| + 2^sh |s| + 2^(sh + w) < 2^31 on
+    // unshifted samples (TWO: the tap (-2^sh, 2^sh) needs 2^sh <= 32767);
+    // 32-bit run sums: codes < 2^26
+    const uint64_t mu = ci.amax, ms = ci.amax >> ci.w;
+    const bool fold_ok = csum * mu + (mu << shift) + (1ull << (shift + (int)ci.w)) < (1ull << 31) &&
+                         (!TWO || shift <= 14);
+    const uint64_t rbound = ms + ((csum * ms) >> shift) + 1u;
+    Eval16 ev;
+    if (fold_ok && 2u * rbound + 1u < (1ull << 26))
+        ev = eval_fold<TWO>(run_of(img, TWO, lane), c, cfu, (int)o, shift, ci.w);
+    else
+        ev = eval_wide<TWO>(img, c, cfu, (int)o, shift, ci.w);
+    res->k[pi][lane] = (uint8_t)ev.sel.k_own;
+    if (lane == 0) {
+        res->bits[pi] = ev.bits;
+        res->porder[pi] = (uint8_t)ev.sel.porder;
+        res->method[pi] = (uint8_t)ev.sel.method;
+    }
+}
+
+// Phase 3 of a candidate (one wave): the subframe choice (flac.c:727-809)
+// from the predictor results, its SubDesc.
+__device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, uint32_t unit,
+                                            const CandInfo &ci, const PredRes *__restrict__ res,
+                                            int lane, const int16_t *__restrict__ coef_tab,
+                                            const int8_t *__restrict__ shift_tab,
+                                            SubDesc *__restrict__ d)
+{
+    if (!ci.active)
+        return;
+    const uint32_t w = ci.w;
     const uint32_t wf = w ? w + 1u : 1u;
-    const uint32_t rb = sbps - w; // bits per warm-up / verbatim sample
-
-    // ---- FIXED order by |residual| sums over samples [4,N) (flac.c:856-916)
-#if ATG_K2F_EXP == 4
-    const uint32_t fixed_order = 2u;
-#else
-    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run, lane) : 0u;
-#endif
-
-    // ---- LPC candidate orders (flac.c:1034-1126); N = 4096 > M + 1 always
+    const uint32_t rb = ci.sbps - w; // bits per warm-up / verbatim sample
     const int16_t *__restrict__ qtab = coef_tab + (size_t)unit * p.coef_stride;
     const int8_t *__restrict__ stab = shift_tab + (size_t)unit * p.max_lpc_order;
-    const uint32_t M = p.max_lpc_order;
-    uint32_t lo = 1, hi = 0;
-    if (p.try_lpc) {
-        if (p.exhaustive) {
-            lo = 1;
-            hi = M;
-        } else {
-            lo = hi = est_tab[unit];
-        }
-    }
-
-    // ---- evaluate every predictor: [FIXED], LPC lo..hi
+    const uint32_t n_pred = n_pred_of(p, ci);
     uint32_t fixed_bits = 0;
-    PartSel fixed_sel = {};
-    uint32_t lpc_bits = 0xFFFFFFFFu, lpc_order = 0, lpc_prec = 0;
+    if (p.try_fixed)
+        fixed_bits = 7u + wf + ci.fixed_order * rb + res->bits[0];
+    uint32_t lpc_bits = 0xFFFFFFFFu, lpc_order = 0, lpc_pi = 0;
     int lpc_shift = 0;
-    PartSel lpc_sel = {};
-#if ATG_K2F_EXP == 1
-    const uint32_t n_pred = p.try_fixed ? 1u : 0u;
-#else
-    const uint32_t n_pred = (p.try_fixed ? 1u : 0u) + (p.try_lpc ? hi - lo + 1u : 0u);
-#endif
-    for (uint32_t pi = 0; pi < n_pred; ++pi) {
-        const bool is_fixed = p.try_fixed && pi == 0;
-        const uint32_t o = is_fixed ? fixed_order : lo + pi - (p.try_fixed ? 1u : 0u);
-        int shift = 0;
-        uint32_t prec = 0;
-        const int16_t *__restrict__ row = qtab + (size_t)(o ? o - 1u : 0u) * p.coef_row;
-        if (!is_fixed) {
-            shift = uniform_i32(stab[o - 1u]);
-            prec = p.qlp_precision;
-        }
-        int cfu[ATG_FAST_ORDER];
-        uint64_t csum = 0;
-#pragma unroll
-        for (int j = 0; j < ATG_FAST_ORDER; ++j) {
-            const int cj = is_fixed ? fixed_tap16(o, j) : ((uint32_t)j < o ? (int)row[j] : 0);
-            cfu[j] = cj;
-            csum += (uint64_t)(cj < 0 ? -cj : cj);
-        }
-        // folded int32 sum exact: |sum c s| + 2^sh |s| + 2^(sh + w) < 2^31
-        // on unshifted samples (TWO: the tap (-2^sh, 2^sh) needs
-        // 2^sh <= 32767); 32-bit run sums: codes < 2^26
-        const uint64_t mu = amax, ms = maxabs;
-        const bool fold_ok = csum * mu + (mu << shift) + (1ull << (shift + (int)w)) < (1ull << 31) &&
-                             (!TWO || shift <= 14);
-        const uint64_t rbound = ms + ((csum * ms) >> shift) + 1u;
-        Eval16 ev;
-        if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-            ev = eval_fold<TWO>(run, c, cfu, (int)o, shift, w);
-        else
-            ev = eval_wide<TWO>(img, c, cfu, (int)o, shift, w);
-        if (is_fixed) {
-            fixed_bits = 7u + wf + o * rb + ev.bits;
-            fixed_sel = ev.sel;
-        } else {
-            const uint32_t bits = 7u + wf + o * rb + 4u + 5u + o * prec + ev.bits;
-            if (bits < lpc_bits) {
-                lpc_bits = bits;
-                lpc_order = o;
-                lpc_shift = shift;
-                lpc_prec = prec;
-                lpc_sel = ev.sel;
-            }
+    for (uint32_t pi = p.try_fixed ? 1u : 0u; pi < n_pred; ++pi) {
+        const uint32_t o = ci.lo + pi - (p.try_fixed ? 1u : 0u);
+        const uint32_t bits = 7u + wf + o * rb + 4u + 5u + o * p.qlp_precision + res->bits[pi];
+        if (bits < lpc_bits) {
+            lpc_bits = bits;
+            lpc_order = o;
+            lpc_pi = pi;
         }
     }
-
-    // ---- subframe choice (flac.c:727-809)
+    if (lpc_order)
+        lpc_shift = stab[lpc_order - 1u];
     const uint32_t verbatim_cmp = p.try_verbatim ? rb * N : 0x7FFFFFFFu;
     int pick;
     const bool F = p.try_fixed, L = p.try_lpc, V = p.try_verbatim;
@@ -613,14 +671,13 @@ __device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uin
     } else {
         pick = lpc_bits < verbatim_cmp ? SF_LPC : SF_VERBATIM;
     }
-
-    const PartSel &sel = pick == SF_FIXED ? fixed_sel : lpc_sel;
+    const uint32_t spi = pick == SF_FIXED ? 0u : lpc_pi;
+    const uint32_t po = res->porder[spi];
     if (pick != SF_VERBATIM) {
         // rice parameter of partition j is held by its first lane
-        const uint32_t po = sel.porder;
         const uint32_t mask = (64u >> po) - 1u;
         if (((uint32_t)lane & mask) == 0u)
-            d->rice[(uint32_t)lane >> (6u - po)] = (uint8_t)sel.k_own;
+            d->rice[(uint32_t)lane >> (6u - po)] = res->k[spi][lane];
     }
     if (pick == SF_LPC) {
         if (lane < (int)lpc_order)
@@ -629,18 +686,18 @@ __device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uin
     if (lane == 0) {
         d->type = (uint8_t)pick;
         d->wasted = (uint8_t)w;
-        d->sbps = (uint8_t)sbps;
-        d->method = (uint8_t)sel.method;
-        d->porder = (uint8_t)sel.porder;
+        d->sbps = (uint8_t)ci.sbps;
+        d->method = res->method[spi];
+        d->porder = (uint8_t)po;
         if (pick == SF_FIXED) {
             d->bits = fixed_bits;
-            d->order = (uint8_t)fixed_order;
+            d->order = (uint8_t)ci.fixed_order;
             d->precision = 0;
             d->shift = 0;
         } else if (pick == SF_LPC) {
             d->bits = lpc_bits;
             d->order = (uint8_t)lpc_order;
-            d->precision = (uint8_t)lpc_prec;
+            d->precision = (uint8_t)p.qlp_precision;
             d->shift = (int8_t)lpc_shift;
         } else {
             d->bits = 7u + wf + rb * N;
@@ -651,6 +708,19 @@ __device__ __forceinline__ void search_cand(const FlacParams &p, uint32_t N, uin
             d->porder = 0;
         }
     }
+}
+
+__device__ __forceinline__ CandInfo load_info(const CandInfo *ci)
+{
+    CandInfo r;
+    r.active = uniform_u32(ci->active);
+    r.w = uniform_u32(ci->w);
+    r.amax = uniform_u32(ci->amax);
+    r.fixed_order = uniform_u32(ci->fixed_order);
+    r.lo = uniform_u32(ci->lo);
+    r.hi = uniform_u32(ci->hi);
+    r.sbps = uniform_u32(ci->sbps);
+    return r;
 }
 
 // wave-uniform min / max / OR of per-lane values
@@ -745,6 +815,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
     __shared__ __attribute__((aligned(16))) uint32_t img[3 * PK_WORDS]; // L, R, M packed
     __shared__ __attribute__((aligned(16))) uint32_t lr[LR_WORDS];       // (L, R) words
     __shared__ int32_t red[4][4][3];                                      // [wave][cand][mn,mx,or]
+    __shared__ CandInfo info[4];
+    __shared__ PredRes res[4];
+    __shared__ uint32_t qnext;
 
     const uint32_t f = blockIdx.x;
     if (f >= p.n_frames)
@@ -764,6 +837,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         img[(tid / PK_PRE) * PK_WORDS + (tid % PK_PRE)] = 0u;
     else if (tid < 3 * PK_PRE + LR_PRE)
         lr[tid - 3 * PK_PRE] = 0u;
+    else if (tid == 255)
+        qnext = 0u;
     int32_t mn[4], mx[4];
     uint32_t orv[4];
 #pragma unroll
@@ -789,16 +864,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         }
     }
     __syncthreads();
-    const uint32_t cand = (uint32_t)wave;
-    CandStats cs;
-    cs.mn = min(min(red[0][cand][0], red[1][cand][0]), min(red[2][cand][0], red[3][cand][0]));
-    cs.mx = max(max(red[0][cand][1], red[1][cand][1]), max(red[2][cand][1], red[3][cand][1]));
-    cs.orv = (uint32_t)(red[0][cand][2] | red[1][cand][2] | red[2][cand][2] | red[3][cand][2]);
-    cs.mn = uniform_i32(cs.mn);
-    cs.mx = uniform_i32(cs.mx);
-    cs.orv = uniform_u32(cs.orv);
-    const uint32_t unit = f * 4u + cand;
-    const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
     // L, R and M fit int16 for any source of <= 16 bits; S is L - R
     bool fits = true;
 #pragma unroll
@@ -808,18 +873,64 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         fits = fits && a >= -32768 && b <= 32767;
     }
     if (!fits) {
-        if (lane == 0) {
+        if (tid < 4) {
             const uint32_t slot = atomicAdd(slow_count, 1u);
-            slow_list[slot] = unit;
+            slow_list[slot] = f * 4u + (uint32_t)tid;
         }
         return;
     }
-    if (cand == 3u)
-        search_cand<true>(p, N, unit, sbps, lr, cs, lane, coef_tab, shift_tab, est_tab,
-                          out + unit);
-    else
-        search_cand<false>(p, N, unit, sbps, img + cand * PK_WORDS, cs, lane, coef_tab,
-                           shift_tab, est_tab, out + unit);
+
+    // phase 1: wave c prepares candidate c
+    const uint32_t cand = (uint32_t)wave;
+    const uint32_t unit = f * 4u + cand;
+    {
+        CandStats cs;
+        cs.mn = min(min(red[0][cand][0], red[1][cand][0]), min(red[2][cand][0], red[3][cand][0]));
+        cs.mx = max(max(red[0][cand][1], red[1][cand][1]), max(red[2][cand][1], red[3][cand][1]));
+        cs.orv = (uint32_t)(red[0][cand][2] | red[1][cand][2] | red[2][cand][2] | red[3][cand][2]);
+        cs.mn = uniform_i32(cs.mn);
+        cs.mx = uniform_i32(cs.mx);
+        cs.orv = uniform_u32(cs.orv);
+        const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
+        if (cand == 3u)
+            cand_prepare<true>(p, unit, sbps, lr, cs, lane, est_tab, out + unit, &info[3]);
+        else
+            cand_prepare<false>(p, unit, sbps, img + cand * PK_WORDS, cs, lane, est_tab,
+                                out + unit, &info[cand]);
+    }
+    __syncthreads();
+
+    // phase 2: the (candidate, predictor) jobs, dynamically shared by the 4
+    // waves, the costliest first (highest orders, side channel first): the
+    // waves finish together although a side-channel residual costs up to
+    // twice a packed one
+    const uint32_t jmax = (p.try_fixed ? 1u : 0u) +
+                          (p.try_lpc ? (p.exhaustive ? p.max_lpc_order : 1u) : 0u);
+    const uint32_t njobs = 4u * jmax;
+    for (;;) {
+        // every lane adds 1, so each fetch advances the counter by exactly
+        // 64 and any lane's old value >> 6 is the job index (a fetch under
+        // `if (lane == 0)` made the loop exit divergent to the compiler, and
+        // the structurized loop re-entered with a stale index: a hang)
+        const uint32_t j = uniform_u32(atomicAdd(&qnext, 1u)) >> 6;
+        if (j >= njobs)
+            break;
+        const uint32_t jc = (j + 3u) & 3u; // 3, 0, 1, 2
+        const uint32_t pi = jmax - 1u - (j >> 2);
+        const CandInfo ci = load_info(&info[jc]);
+        if (!ci.active || pi >= n_pred_of(p, ci))
+            continue;
+        if (jc == 3u)
+            pred_job<true>(p, N, f * 4u + 3u, lr, ci, pi, lane, coef_tab, shift_tab, &res[3]);
+        else
+            pred_job<false>(p, N, f * 4u + jc, img + jc * PK_WORDS, ci, pi, lane, coef_tab,
+                            shift_tab, &res[jc]);
+    }
+    __syncthreads();
+
+    // phase 3: wave c writes candidate c
+    cand_finish(p, N, unit, load_info(&info[cand]), &res[cand], lane, coef_tab, shift_tab,
+                out + unit);
 }
 
 // ---------------------------------------------------------------------------
@@ -871,6 +982,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
     uint32_t *__restrict__ slow_list, uint32_t *__restrict__ slow_count)
 {
     __shared__ __attribute__((aligned(16))) uint32_t pk[PK_WORDS];
+    __shared__ CandInfo info;
+    __shared__ PredRes res;
 
     uint32_t f, cand;
     xcd_unit_map(blockIdx.x, p.n_cand, &f, &cand);
@@ -917,7 +1030,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
         return;
     }
     __syncthreads();
-    search_cand<false>(p, N, unit, sbps, pk, cs, lane, coef_tab, shift_tab, est_tab, out + unit);
+    cand_prepare<false>(p, unit, sbps, pk, cs, lane, est_tab, out + unit, &info);
+    __syncthreads();
+    const CandInfo ci = load_info(&info);
+    if (!ci.active)
+        return;
+    const uint32_t n_pred = n_pred_of(p, ci);
+    for (uint32_t pi = 0; pi < n_pred; ++pi)
+        pred_job<false>(p, N, unit, pk, ci, pi, lane, coef_tab, shift_tab, &res);
+    __syncthreads();
+    cand_finish(p, N, unit, ci, &res, lane, coef_tab, shift_tab, out + unit);
 }
 
 hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fmt,
