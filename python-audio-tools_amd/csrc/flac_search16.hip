@@ -47,6 +47,10 @@
 #ifndef ATG_K2F_EXP
 #define ATG_K2F_EXP 0
 #endif
+// 1: three residual-loop variants instead of seven (smaller code image)
+#ifndef ATG_K2F_FEW
+#define ATG_K2F_FEW 0
+#endif
 // waves per SIMD the register allocation targets
 #ifndef ATG_K2F_WPE
 #define ATG_K2F_WPE 3
@@ -119,6 +123,13 @@ __device__ __forceinline__ int dot2_first(uint32_t a, int tap_v, int acc_s)
 #endif
 }
 
+// sa += v + s31 as one v_add3_u32 the compiler cannot re-associate (it
+// otherwise defers the sums and keeps every s31 live: register pressure)
+__device__ __forceinline__ void add3_acc(uint32_t &sa, uint32_t v, uint32_t s31)
+{
+    asm("v_add3_u32 %0, %0, %1, %2" : "+v"(sa) : "v"(v), "v"(s31));
+}
+
 // A lane's window over one packed image: words -8..15 of the current
 // 16-sample chunk (W) and their v_alignbit pairs (E).
 struct Win {
@@ -137,16 +148,14 @@ __device__ __forceinline__ void win_init(const uint32_t *__restrict__ run, Win &
     x.E[8] = 0;
 }
 
-// slide by one chunk: words 8c .. 8c + 7 of the run
-__device__ __forceinline__ void win_next(const uint32_t *__restrict__ run, int c, Win &x)
+// slide by one chunk: a0, a1 = words 8c .. 8c + 7 of the run
+__device__ __forceinline__ void win_next(const uint4 &a0, const uint4 &a1, Win &x)
 {
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
         x.W[k] = x.W[8 + k];
         x.E[k] = x.E[8 + k];
     }
-    const uint4 a0 = *(const uint4 *)(run + 8 * c);
-    const uint4 a1 = *(const uint4 *)(run + 8 * c + 4);
     x.W[8] = a0.x; x.W[9] = a0.y; x.W[10] = a0.z; x.W[11] = a0.w;
     x.W[12] = a1.x; x.W[13] = a1.y; x.W[14] = a1.z; x.W[15] = a1.w;
 #pragma unroll
@@ -175,26 +184,43 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap pair in a VGPR
     Win A;
     win_init(run, A);
+    // chunk c + 1's words are read while chunk c is computed
+    uint4 n0 = *(const uint4 *)run, n1 = *(const uint4 *)(run + 4);
     uint32_t sa = 0;
 #pragma unroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
         // keep each chunk's loads inside the chunk (bounds live registers)
         asm volatile("" ::: "memory");
-        win_next(run, c, A);
+        const uint4 a0 = n0, a1 = n1;
+        if (c + 1 < ATG_RUN / 16) {
+            n0 = *(const uint4 *)(run + 8 * (c + 1));
+            n1 = *(const uint4 *)(run + 8 * (c + 1) + 4);
+        }
+        win_next(a0, a1, A);
+        // two samples' tap chains interleaved: no dependent-issue bubble
+        // after each chain
 #pragma unroll
-        for (int ii = 0; ii < 16; ++ii) {
-            const int i = 16 * c + ii;
-            int acc = dot2_first(win_pair(A, ii, 0), tap0, c0acc);
+        for (int ii = 0; ii < 16; ii += 2) {
+            int acc[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                acc[h] = dot2_first(win_pair(A, ii + h, 0), tap0, c0acc);
 #pragma unroll
             for (int j = 1; j < D; ++j)
-                acc = dot2(win_pair(A, ii, j), cp[j], acc);
-            int n = acc >> shv;
-            if (i < ATG_FAST_ORDER)
-                n = i < warm ? -1 : n;
-            const uint32_t s31 = (uint32_t)(n >> 31);
-            const uint32_t v = (uint32_t)n ^ s31;
-            u[i] = v;
-            sa = sa + v + s31; // v_add3_u32
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    acc[h] = dot2(win_pair(A, ii + h, j), cp[j], acc[h]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 16 * c + ii + h;
+                int n = acc[h] >> shv;
+                if (i < ATG_FAST_ORDER)
+                    n = i < warm ? -1 : n;
+                const uint32_t s31 = (uint32_t)(n >> 31);
+                const uint32_t v = (uint32_t)n ^ s31;
+                u[i] = v;
+                add3_acc(sa, v, s31);
+            }
         }
     }
     sabs = sa + (uint32_t)ATG_RUN;
@@ -220,6 +246,11 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
         W[20] = h1.x; W[21] = h1.y; W[22] = h1.z; W[23] = h1.w;
         W[24] = h2.x; W[25] = h2.y; W[26] = h2.z; W[27] = h2.w;
     }
+    // chunk c + 1's words are read while chunk c is computed
+    uint4 nx[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+        nx[q] = *(const uint4 *)(run + 4 * q);
     uint32_t sa = 0;
 #pragma unroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
@@ -229,26 +260,38 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
             W[k] = W[16 + k];
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
-            const uint4 a = *(const uint4 *)(run + 16 * c + 4 * q);
-            W[12 + 4 * q] = a.x;
-            W[13 + 4 * q] = a.y;
-            W[14 + 4 * q] = a.z;
-            W[15 + 4 * q] = a.w;
+            W[12 + 4 * q] = nx[q].x;
+            W[13 + 4 * q] = nx[q].y;
+            W[14 + 4 * q] = nx[q].z;
+            W[15 + 4 * q] = nx[q].w;
+        }
+        if (c + 1 < ATG_RUN / 16) {
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+                nx[q] = *(const uint4 *)(run + 16 * (c + 1) + 4 * q);
         }
 #pragma unroll
-        for (int ii = 0; ii < 16; ++ii) {
-            const int i = 16 * c + ii;
-            int acc = dot2_first(W[12 + ii], tap0, c0acc);
+        for (int ii = 0; ii < 16; ii += 2) {
+            int accs[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+                accs[h] = dot2_first(W[12 + ii + h], tap0, c0acc);
 #pragma unroll
             for (int k = 1; k < TAPS; ++k)
-                acc = dot2(W[12 + ii - k], cl[k], acc);
-            int n = acc >> shv;
-            if (i < ATG_FAST_ORDER)
-                n = i < warm ? -1 : n;
-            const uint32_t s31 = (uint32_t)(n >> 31);
-            const uint32_t v = (uint32_t)n ^ s31;
-            u[i] = v;
-            sa = sa + v + s31; // v_add3_u32
+#pragma unroll
+                for (int h = 0; h < 2; ++h)
+                    accs[h] = dot2(W[12 + ii + h - k], cl[k], accs[h]);
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 16 * c + ii + h;
+                int n = accs[h] >> shv;
+                if (i < ATG_FAST_ORDER)
+                    n = i < warm ? -1 : n;
+                const uint32_t s31 = (uint32_t)(n >> 31);
+                const uint32_t v = (uint32_t)n ^ s31;
+                u[i] = v;
+                add3_acc(sa, v, s31);
+            }
         }
     }
     sabs = sa + (uint32_t)ATG_RUN;
@@ -262,9 +305,11 @@ struct Eval16 {
 // One predictor with the folded 32-bit arithmetic (caller checked the
 // bounds): pass 1, partition search, exact bits.  run: the lane's run in a
 // packed image, or in the (L, R) word image (TWO).
+// cw: the predictor's taps as the LPC table stores them, int16 pairs
+// (c_2m, c_2m+1) per dword, zero past the order (cw[6] = 0); wave-uniform.
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
-                                            const int (&cf)[ATG_FAST_ORDER], int order, int sh,
+                                            const uint32_t (&cw)[7], int order, int sh,
                                             uint32_t w)
 {
     int cq[14];
@@ -273,31 +318,38 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
 #pragma unroll
         for (int k = 1; k < 14; ++k) {
-            const int ck = k - 1 < ATG_FAST_ORDER ? cf[k - 1] : 0;
+            const uint32_t d = cw[(k - 1) >> 1];
+            const int ck = ((k - 1) & 1) ? hi16(d) : lo16(d);
             cq[k] = (int)(((uint32_t)ck & 0xFFFFu) | ((uint32_t)(-ck) << 16));
         }
     } else {
-        // pairs (c0, -2^sh), (c2, c1), (c4, c3), ...
-        cq[0] = (int)(((uint32_t)cf[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
+        // pairs (c0, -2^sh), (c2, c1), (c4, c3), ...: halves of adjacent
+        // table dwords (s_pack_lh)
+        cq[0] = (int)((cw[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
 #pragma unroll
-        for (int j = 1; j < 7; ++j) {
-            const int lo = 2 * j < ATG_FAST_ORDER ? cf[2 * j] : 0;
-            cq[j] = (int)(((uint32_t)lo & 0xFFFFu) | ((uint32_t)cf[2 * j - 1] << 16));
-        }
+        for (int j = 1; j < 7; ++j)
+            cq[j] = (int)((cw[j] & 0xFFFFu) | (cw[j - 1] & 0xFFFF0000u));
 #pragma unroll
         for (int j = 7; j < 14; ++j)
             cq[j] = 0;
     }
-#pragma unroll
-    for (int j = 0; j < 14; ++j)
-        cq[j] = uniform_i32(cq[j]);
-    const int c0acc = uniform_i32(-(1 << (sh + (int)w)));
+    const int c0acc = -(1 << (sh + (int)w));
     int shv = sh + (int)w;
     asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
     const int warm = c.lane == 0 ? order : 0;
     uint32_t u[ATG_RUN];
     uint32_t lane_sum; // sum |r| of the run
     if (TWO) {
+#if ATG_K2F_FEW
+        // three tap counts only (zero taps past the order): a code image that
+        // fits the instruction cache
+        if (order < 4)
+            pass1_lr<2>(run, cq, c0acc, shv, warm, u, lane_sum);
+        else if (order < 8)
+            pass1_lr<4>(run, cq, c0acc, shv, warm, u, lane_sum);
+        else
+            pass1_lr<7>(run, cq, c0acc, shv, warm, u, lane_sum);
+#else
         switch (order / 2 + 1) {
         case 1: pass1_lr<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         case 2: pass1_lr<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
@@ -307,7 +359,16 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         case 6: pass1_lr<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         default: pass1_lr<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         }
+#endif
     } else {
+#if ATG_K2F_FEW
+        if (order < 4)
+            pass1<2>(run, cq, c0acc, shv, warm, u, lane_sum);
+        else if (order < 8)
+            pass1<4>(run, cq, c0acc, shv, warm, u, lane_sum);
+        else
+            pass1<7>(run, cq, c0acc, shv, warm, u, lane_sum);
+#else
         switch (order / 2 + 1) {
         case 1: pass1<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         case 2: pass1<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
@@ -317,6 +378,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         case 6: pass1<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         default: pass1<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
         }
+#endif
     }
     Eval16 ev;
 #if ATG_K2F_EXP == 3
@@ -349,8 +411,13 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
 // residuals recomputed for the exact bits.
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_wide(const uint32_t *__restrict__ img, const RunCtx &c,
-                                            const int *cf, int order, int shift, uint32_t w)
+                                            const uint32_t (&cw)[7], int order, int shift,
+                                            uint32_t w)
 {
+    int cf[ATG_FAST_ORDER];
+#pragma unroll
+    for (int k = 0; k < ATG_FAST_ORDER; ++k)
+        cf[k] = (k & 1) ? hi16(cw[k >> 1]) : lo16(cw[k >> 1]);
     uint64_t sum = 0;
     const int start = max(c.a, order);
     const int end = c.a + c.len;
@@ -376,18 +443,6 @@ __device__ __forceinline__ Eval16 eval_wide(const uint32_t *__restrict__ img, co
     }
     ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
     return ev;
-}
-
-// FIXED predictor of order o as taps (flac.c:918-1016)
-__device__ __forceinline__ int fixed_tap16(uint32_t o, int j)
-{
-    switch (o) {
-    case 1: return j == 0 ? 1 : 0;
-    case 2: return j == 0 ? 2 : j == 1 ? -1 : 0;
-    case 3: return j == 0 ? 3 : j == 1 ? -3 : j == 2 ? 1 : 0;
-    case 4: return j == 0 ? 4 : j == 1 ? -6 : j == 2 ? 4 : j == 3 ? -1 : 0;
-    default: return 0;
-    }
 }
 
 // Sums of |x|, |d1| .. |d4| over the lane's run, unshifted samples (every
@@ -569,29 +624,43 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
 // One predictor of one candidate (one wave, any wave of the workgroup):
 // residual-section bits and partition choice into res[pi].  pi = 0 is
 // FIXED when FIXED is tried, then LPC orders lo, lo + 1, ...
+// lq / ls: the candidate's LPC table rows and shifts, staged in LDS.
 template <bool TWO>
-__device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N, uint32_t unit,
+__device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
                                          const uint32_t *__restrict__ img, const CandInfo &ci,
-                                         uint32_t pi, int lane,
-                                         const int16_t *__restrict__ coef_tab,
-                                         const int8_t *__restrict__ shift_tab,
+                                         uint32_t pi, int lane, const int16_t *__restrict__ lq,
+                                         const int8_t *__restrict__ ls,
                                          PredRes *__restrict__ res)
 {
     const bool is_fixed = p.try_fixed && pi == 0;
     const uint32_t o = is_fixed ? ci.fixed_order : ci.lo + pi - (p.try_fixed ? 1u : 0u);
-    const int16_t *__restrict__ qtab = coef_tab + (size_t)unit * p.coef_stride;
-    const int8_t *__restrict__ stab = shift_tab + (size_t)unit * p.max_lpc_order;
     int shift = 0;
-    const int16_t *__restrict__ row = qtab + (size_t)(o ? o - 1u : 0u) * p.coef_row;
-    if (!is_fixed)
-        shift = uniform_i32(stab[o - 1u]);
-    int cfu[ATG_FAST_ORDER];
-    uint64_t csum = 0;
+    uint32_t cw[7];
+    if (is_fixed) {
+        // FIXED predictor of order o as taps (flac.c:918-1016)
+        switch (o) {
+        case 1: cw[0] = 1u; cw[1] = 0u; break;
+        case 2: cw[0] = 2u | 0xFFFF0000u; cw[1] = 0u; break;                  // 2, -1
+        case 3: cw[0] = 3u | 0xFFFD0000u; cw[1] = 1u; break;                  // 3, -3, 1
+        case 4: cw[0] = 4u | 0xFFFA0000u; cw[1] = 4u | 0xFFFF0000u; break;    // 4, -6, 4, -1
+        default: cw[0] = 0u; cw[1] = 0u; break;
+        }
 #pragma unroll
-    for (int j = 0; j < ATG_FAST_ORDER; ++j) {
-        const int cj = is_fixed ? fixed_tap16(o, j) : ((uint32_t)j < o ? (int)row[j] : 0);
-        cfu[j] = cj;
-        csum += (uint64_t)(cj < 0 ? -cj : cj);
+        for (int m = 2; m < 7; ++m)
+            cw[m] = 0u;
+    } else {
+        shift = uniform_i32(ls[o - 1u]);
+        const uint32_t *__restrict__ rw = (const uint32_t *)(lq + (o - 1u) * p.coef_row);
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+            cw[m] = 2u * (uint32_t)m < p.coef_row ? uniform_u32(rw[m]) : 0u;
+        cw[6] = 0u;
+    }
+    uint32_t csum = 0; // sum |c| < 12 * 2^14
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const int a = lo16(cw[m]), b = hi16(cw[m]);
+        csum += (uint32_t)(a < 0 ? -a : a) + (uint32_t)(b < 0 ? -b : b);
     }
     RunCtx c;
     c.lane = lane;
@@ -604,14 +673,15 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N, uint32
     // unshifted samples (TWO: the tap (-2^sh, 2^sh) needs 2^sh <= 32767);
     // 32-bit run sums: codes < 2^26
     const uint64_t mu = ci.amax, ms = ci.amax >> ci.w;
-    const bool fold_ok = csum * mu + (mu << shift) + (1ull << (shift + (int)ci.w)) < (1ull << 31) &&
+    const bool fold_ok = (uint64_t)csum * mu + (mu << shift) + (1ull << (shift + (int)ci.w)) <
+                             (1ull << 31) &&
                          (!TWO || shift <= 14);
-    const uint64_t rbound = ms + ((csum * ms) >> shift) + 1u;
+    const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
     Eval16 ev;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-        ev = eval_fold<TWO>(run_of(img, TWO, lane), c, cfu, (int)o, shift, ci.w);
+        ev = eval_fold<TWO>(run_of(img, TWO, lane), c, cw, (int)o, shift, ci.w);
     else
-        ev = eval_wide<TWO>(img, c, cfu, (int)o, shift, ci.w);
+        ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
     res->k[pi][lane] = (uint8_t)ev.sel.k_own;
     if (lane == 0) {
         res->bits[pi] = ev.bits;
@@ -622,19 +692,16 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N, uint32
 
 // Phase 3 of a candidate (one wave): the subframe choice (flac.c:727-809)
 // from the predictor results, its SubDesc.
-__device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, uint32_t unit,
-                                            const CandInfo &ci, const PredRes *__restrict__ res,
-                                            int lane, const int16_t *__restrict__ coef_tab,
-                                            const int8_t *__restrict__ shift_tab,
-                                            SubDesc *__restrict__ d)
+__device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, const CandInfo &ci,
+                                            const PredRes *__restrict__ res, int lane,
+                                            const int16_t *__restrict__ lq,
+                                            const int8_t *__restrict__ ls, SubDesc *__restrict__ d)
 {
     if (!ci.active)
         return;
     const uint32_t w = ci.w;
     const uint32_t wf = w ? w + 1u : 1u;
     const uint32_t rb = ci.sbps - w; // bits per warm-up / verbatim sample
-    const int16_t *__restrict__ qtab = coef_tab + (size_t)unit * p.coef_stride;
-    const int8_t *__restrict__ stab = shift_tab + (size_t)unit * p.max_lpc_order;
     const uint32_t n_pred = n_pred_of(p, ci);
     uint32_t fixed_bits = 0;
     if (p.try_fixed)
@@ -651,7 +718,7 @@ __device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, uin
         }
     }
     if (lpc_order)
-        lpc_shift = stab[lpc_order - 1u];
+        lpc_shift = ls[lpc_order - 1u];
     const uint32_t verbatim_cmp = p.try_verbatim ? rb * N : 0x7FFFFFFFu;
     int pick;
     const bool F = p.try_fixed, L = p.try_lpc, V = p.try_verbatim;
@@ -681,7 +748,7 @@ __device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, uin
     }
     if (pick == SF_LPC) {
         if (lane < (int)lpc_order)
-            d->coef[lane] = qtab[(lpc_order - 1u) * p.coef_row + lane];
+            d->coef[lane] = lq[(lpc_order - 1u) * p.coef_row + lane];
     }
     if (lane == 0) {
         d->type = (uint8_t)pick;
@@ -818,6 +885,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
     __shared__ CandInfo info[4];
     __shared__ PredRes res[4];
     __shared__ uint32_t qnext;
+    // the frame's LPC tables (4 candidates x M rows) and shifts
+    __shared__ __attribute__((aligned(16))) uint32_t lq32[4 * ATG_FAST_ORDER * ATG_FAST_ORDER / 2];
+    __shared__ uint32_t ls32[ATG_FAST_ORDER];
 
     const uint32_t f = blockIdx.x;
     if (f >= p.n_frames)
@@ -839,6 +909,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         lr[tid - 3 * PK_PRE] = 0u;
     else if (tid == 255)
         qnext = 0u;
+    {
+        // the 4 candidates' tables are contiguous (unit = 4 f + cand)
+        const uint32_t nq = 2u * p.coef_stride, ns = p.max_lpc_order;
+        const uint32_t *__restrict__ gq = (const uint32_t *)(coef_tab + (size_t)f * 4u * p.coef_stride);
+        const uint32_t *__restrict__ gs = (const uint32_t *)(shift_tab + (size_t)f * 4u * p.max_lpc_order);
+        for (uint32_t i = (uint32_t)tid; i < nq; i += 256u)
+            lq32[i] = gq[i];
+        if ((uint32_t)tid < ns)
+            ls32[tid] = gs[tid];
+    }
     int32_t mn[4], mx[4];
     uint32_t orv[4];
 #pragma unroll
@@ -920,17 +1000,19 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         const CandInfo ci = load_info(&info[jc]);
         if (!ci.active || pi >= n_pred_of(p, ci))
             continue;
+        const int16_t *lq = (const int16_t *)lq32 + jc * p.coef_stride;
+        const int8_t *ls = (const int8_t *)ls32 + jc * p.max_lpc_order;
         if (jc == 3u)
-            pred_job<true>(p, N, f * 4u + 3u, lr, ci, pi, lane, coef_tab, shift_tab, &res[3]);
+            pred_job<true>(p, N, lr, ci, pi, lane, lq, ls, &res[3]);
         else
-            pred_job<false>(p, N, f * 4u + jc, img + jc * PK_WORDS, ci, pi, lane, coef_tab,
-                            shift_tab, &res[jc]);
+            pred_job<false>(p, N, img + jc * PK_WORDS, ci, pi, lane, lq, ls, &res[jc]);
     }
     __syncthreads();
 
     // phase 3: wave c writes candidate c
-    cand_finish(p, N, unit, load_info(&info[cand]), &res[cand], lane, coef_tab, shift_tab,
-                out + unit);
+    cand_finish(p, N, load_info(&info[cand]), &res[cand], lane,
+                (const int16_t *)lq32 + cand * p.coef_stride,
+                (const int8_t *)ls32 + cand * p.max_lpc_order, out + unit);
 }
 
 // ---------------------------------------------------------------------------
@@ -984,6 +1066,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
     __shared__ __attribute__((aligned(16))) uint32_t pk[PK_WORDS];
     __shared__ CandInfo info;
     __shared__ PredRes res;
+    __shared__ __attribute__((aligned(16))) uint32_t lq32[ATG_FAST_ORDER * ATG_FAST_ORDER / 2];
+    __shared__ uint32_t ls32[ATG_FAST_ORDER / 4];
 
     uint32_t f, cand;
     xcd_unit_map(blockIdx.x, p.n_cand, &f, &cand);
@@ -1008,6 +1092,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
     }
     if (lane < PK_PRE)
         pk[lane] = 0u;
+    {
+        // this candidate's table rows and shifts (alignment: coef_stride is
+        // even, M shifts per unit are read bytewise)
+        const uint32_t *__restrict__ gq = (const uint32_t *)(coef_tab + (size_t)unit * p.coef_stride);
+        for (uint32_t i = (uint32_t)lane; i < p.coef_stride / 2u; i += 64u)
+            lq32[i] = gq[i];
+        if ((uint32_t)lane < p.max_lpc_order)
+            ((int8_t *)ls32)[lane] = shift_tab[(size_t)unit * p.max_lpc_order + lane];
+    }
     int32_t mn = INT32_MAX, mx = INT32_MIN;
     uint32_t orv = 0;
     {
@@ -1037,9 +1130,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
         return;
     const uint32_t n_pred = n_pred_of(p, ci);
     for (uint32_t pi = 0; pi < n_pred; ++pi)
-        pred_job<false>(p, N, unit, pk, ci, pi, lane, coef_tab, shift_tab, &res);
+        pred_job<false>(p, N, pk, ci, pi, lane, (const int16_t *)lq32, (const int8_t *)ls32, &res);
     __syncthreads();
-    cand_finish(p, N, unit, ci, &res, lane, coef_tab, shift_tab, out + unit);
+    cand_finish(p, N, ci, &res, lane, (const int16_t *)lq32, (const int8_t *)ls32, out + unit);
 }
 
 hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fmt,
