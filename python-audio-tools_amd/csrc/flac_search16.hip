@@ -10,10 +10,11 @@
 //                       256-thread workgroup per frame, wave c searches
 //                       candidate c.  The frame's PCM is read once and LDS
 //                       holds L, R and M = (L + R) >> 1 as packed int16
-//                       pairs plus the raw (L, R) words (45 KB per frame);
-//                       the side channel S = L - R (17 bits) is never
-//                       stored: its predictor takes one v_dot2 per tap on
-//                       (L, R) words with taps (c, -c) (exact, linear).
+//                       pairs (28 KB per frame: 4 frames per CU); the side
+//                       channel S = L - R (17 bits) is never stored: its
+//                       predictor takes one v_dot2 per tap on (L, R) words
+//                       (one v_perm of the L and R images per sample) with
+//                       taps (c, -c) (exact, linear).
 //   k_subframe_search16 any other layout: one wave per candidate with its
 //                       own packed array (candidates outside int16 are
 //                       handed over).
@@ -53,7 +54,7 @@
 #endif
 // waves per SIMD the register allocation targets
 #ifndef ATG_K2F_WPE
-#define ATG_K2F_WPE 3
+#define ATG_K2F_WPE 4
 #endif
 
 #define PK_PRE 16
@@ -76,23 +77,12 @@ __device__ __forceinline__ int32_t pk_sample(const uint32_t *__restrict__ pk, in
     return (i & 1) ? hi16(w) : lo16(w);
 }
 
-// raw (L, R) word image of a stereo frame: one word per sample, 4 pad words
-// after every 64 (lane runs 68 words apart: 16-byte aligned, conflict-free
-// for ds_read_b128); words -24..-1 are zeros (lane 0's history)
-#define LR_PRE 24
-#define LR_WORDS (LR_PRE + ATG_MAX_BLOCK + 4 * (ATG_MAX_BLOCK / 64) + 8)
-__device__ __forceinline__ int laddr(int i) { return LR_PRE + i + 4 * (i >> 6); }
-
-// candidate sample i: a packed image (TWO = false) or L - R of an (L, R)
-// word image (TWO = true, the side channel)
+// candidate sample i: a packed image (TWO = false), or L - R with the L
+// image at img and the R image right after it (TWO = true, the side channel)
 template <bool TWO>
 __device__ __forceinline__ int32_t cand_pk(const uint32_t *__restrict__ img, int i)
 {
-    if (TWO) {
-        const uint32_t w = img[laddr(i)];
-        return lo16(w) - hi16(w);
-    }
-    return pk_sample(img, i);
+    return TWO ? pk_sample(img, i) - pk_sample(img + PK_WORDS, i) : pk_sample(img, i);
 }
 
 __device__ __forceinline__ uint32_t align16(uint32_t hi_word, uint32_t lo_word)
@@ -226,52 +216,56 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
     sabs = sa + (uint32_t)ATG_RUN;
 }
 
-// The same for the side channel on an (L, R) word image: tap k of sample t
-// is v_dot2((L, R)[t - k], (c_(k-1), -c_(k-1))), tap 0 the fold
-// (-2^sh, 2^sh); TAPS = min(2D, 13) covers order <= 2D - 1.
+// The same for the side channel S = L - R (17 bits): tap k of sample t is
+// v_dot2((L, R)[t - k], (c_(k-1), -c_(k-1))), tap 0 the fold (-2^sh, 2^sh),
+// on (L, R) words built with one v_perm per sample from the packed L and
+// R images (runL, runL + PK_WORDS); TAPS = min(2D, 13) covers order
+// <= 2D - 1.  Chunks of 8 samples (window: 12 history + 8 words).
+__device__ __forceinline__ void lr_words(const uint4 &l, const uint4 &r, uint32_t *w)
+{
+    const uint32_t lw[4] = {l.x, l.y, l.z, l.w}, rw[4] = {r.x, r.y, r.z, r.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        w[2 * q] = __builtin_amdgcn_perm(rw[q], lw[q], 0x05040100u);     // (L[2m], R[2m])
+        w[2 * q + 1] = __builtin_amdgcn_perm(rw[q], lw[q], 0x07060302u); // (L[2m+1], R[2m+1])
+    }
+}
+
 template <int D>
 __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const int (&cl)[14],
                                          int c0acc, int shv, int warm, uint32_t (&u)[ATG_RUN],
                                          uint32_t &sabs)
 {
     constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
+    const uint32_t *__restrict__ runR = run + PK_WORDS;
     int tap0 = cl[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap in a VGPR
-    uint32_t W[28]; // words t0 - 12 .. t0 + 15 of the current chunk
+    uint32_t W[20]; // (L, R) words of samples t0 - 12 .. t0 + 7 of the current chunk
     {
-        const uint4 h0 = *(const uint4 *)(run - 16);
-        const uint4 h1 = *(const uint4 *)(run - 12);
-        const uint4 h2 = *(const uint4 *)(run - 8);
-        W[16] = h0.x; W[17] = h0.y; W[18] = h0.z; W[19] = h0.w;
-        W[20] = h1.x; W[21] = h1.y; W[22] = h1.z; W[23] = h1.w;
-        W[24] = h2.x; W[25] = h2.y; W[26] = h2.z; W[27] = h2.w;
+        // packed words -8..-1 = samples a-16 .. a-1; keep a-12 .. a-1
+        uint32_t h[16];
+        lr_words(*(const uint4 *)(run - 12), *(const uint4 *)(runR - 12), h);
+        lr_words(*(const uint4 *)(run - 8), *(const uint4 *)(runR - 8), h + 8);
+#pragma unroll
+        for (int k = 0; k < 12; ++k)
+            W[8 + k] = h[4 + k];
     }
     // chunk c + 1's words are read while chunk c is computed
-    uint4 nx[4];
-#pragma unroll
-    for (int q = 0; q < 4; ++q)
-        nx[q] = *(const uint4 *)(run + 4 * q);
+    uint4 nl = *(const uint4 *)run, nr = *(const uint4 *)runR;
     uint32_t sa = 0;
 #pragma unroll
-    for (int c = 0; c < ATG_RUN / 16; ++c) {
+    for (int c = 0; c < ATG_RUN / 8; ++c) {
         asm volatile("" ::: "memory");
 #pragma unroll
         for (int k = 0; k < 12; ++k)
-            W[k] = W[16 + k];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-            W[12 + 4 * q] = nx[q].x;
-            W[13 + 4 * q] = nx[q].y;
-            W[14 + 4 * q] = nx[q].z;
-            W[15 + 4 * q] = nx[q].w;
-        }
-        if (c + 1 < ATG_RUN / 16) {
-#pragma unroll
-            for (int q = 0; q < 4; ++q)
-                nx[q] = *(const uint4 *)(run + 16 * (c + 1) + 4 * q);
+            W[k] = W[8 + k];
+        lr_words(nl, nr, W + 12);
+        if (c + 1 < ATG_RUN / 8) {
+            nl = *(const uint4 *)(run + 4 * (c + 1));
+            nr = *(const uint4 *)(runR + 4 * (c + 1));
         }
 #pragma unroll
-        for (int ii = 0; ii < 16; ii += 2) {
+        for (int ii = 0; ii < 8; ii += 2) {
             int accs[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h)
@@ -283,7 +277,7 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
                     accs[h] = dot2(W[12 + ii + h - k], cl[k], accs[h]);
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
-                const int i = 16 * c + ii + h;
+                const int i = 8 * c + ii + h;
                 int n = accs[h] >> shv;
                 if (i < ATG_FAST_ORDER)
                     n = i < warm ? -1 : n;
@@ -456,12 +450,13 @@ __device__ __forceinline__ uint32_t fixed_order_of(const uint32_t *__restrict__ 
     uint32_t a5[5] = {0, 0, 0, 0, 0};
     int x1, x2, x3, x4;
     {
-        const uint4 h = *(const uint4 *)(run - 8); // packed: a-8 .. a-1; (L, R): a-4 .. a-1
+        uint4 h = *(const uint4 *)(run - 8); // packed words -4..-1: samples a-8 .. a-1
         if (TWO) {
-            x1 = lo16(h.w) - hi16(h.w);
-            x2 = lo16(h.z) - hi16(h.z);
-            x3 = lo16(h.y) - hi16(h.y);
-            x4 = lo16(h.x) - hi16(h.x);
+            const uint4 g = *(const uint4 *)(run + PK_WORDS - 8);
+            x1 = hi16(h.w) - hi16(g.w);
+            x2 = lo16(h.w) - lo16(g.w);
+            x3 = hi16(h.z) - hi16(g.z);
+            x4 = lo16(h.z) - lo16(g.z);
         } else {
             x1 = hi16(h.w);
             x2 = lo16(h.w);
@@ -476,27 +471,19 @@ __device__ __forceinline__ uint32_t fixed_order_of(const uint32_t *__restrict__ 
 #pragma unroll 1
     for (int chn = 0; chn < ATG_RUN / 16; ++chn) {
         int x[16];
-        if (TWO) {
 #pragma unroll
-            for (int q = 0; q < 4; ++q) {
-                const uint4 a = *(const uint4 *)(run + 16 * chn + 4 * q);
-                x[4 * q] = lo16(a.x) - hi16(a.x);
-                x[4 * q + 1] = lo16(a.y) - hi16(a.y);
-                x[4 * q + 2] = lo16(a.z) - hi16(a.z);
-                x[4 * q + 3] = lo16(a.w) - hi16(a.w);
+        for (int q = 0; q < 2; ++q) {
+            const uint4 a = *(const uint4 *)(run + 8 * chn + 4 * q);
+            const uint32_t wa[4] = {a.x, a.y, a.z, a.w};
+            uint32_t wb[4] = {0, 0, 0, 0};
+            if (TWO) {
+                const uint4 b = *(const uint4 *)(run + PK_WORDS + 8 * chn + 4 * q);
+                wb[0] = b.x; wb[1] = b.y; wb[2] = b.z; wb[3] = b.w;
             }
-        } else {
 #pragma unroll
-            for (int q = 0; q < 2; ++q) {
-                const uint4 a = *(const uint4 *)(run + 8 * chn + 4 * q);
-                x[8 * q] = lo16(a.x);
-                x[8 * q + 1] = hi16(a.x);
-                x[8 * q + 2] = lo16(a.y);
-                x[8 * q + 3] = hi16(a.y);
-                x[8 * q + 4] = lo16(a.z);
-                x[8 * q + 5] = hi16(a.z);
-                x[8 * q + 6] = lo16(a.w);
-                x[8 * q + 7] = hi16(a.w);
+            for (int k = 0; k < 4; ++k) {
+                x[8 * q + 2 * k] = lo16(wa[k]) - (TWO ? lo16(wb[k]) : 0);
+                x[8 * q + 2 * k + 1] = hi16(wa[k]) - (TWO ? hi16(wb[k]) : 0);
             }
         }
 #pragma unroll
@@ -561,10 +548,9 @@ __device__ __forceinline__ uint32_t n_pred_of(const FlacParams &p, const CandInf
     return (p.try_fixed ? 1u : 0u) + (p.try_lpc ? ci.hi - ci.lo + 1u : 0u);
 }
 
-__device__ __forceinline__ const uint32_t *run_of(const uint32_t *__restrict__ img, bool two,
-                                                  int lane)
+__device__ __forceinline__ const uint32_t *run_of(const uint32_t *__restrict__ img, int lane)
 {
-    return two ? img + LR_PRE + (ATG_RUN + 4) * lane : img + PK_PRE + 36 * lane;
+    return img + PK_PRE + 36 * lane;
 }
 
 // Phase 1 of a candidate (one wave): CONSTANT (written here), wasted bits,
@@ -595,7 +581,7 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
 #if ATG_K2F_EXP == 4
     const uint32_t fixed_order = 2u;
 #else
-    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run_of(img, TWO, lane), lane) : 0u;
+    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run_of(img, lane), lane) : 0u;
 #endif
     uint32_t lo = 1, hi = 0;
     if (p.try_lpc) {
@@ -679,7 +665,7 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
     Eval16 ev;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-        ev = eval_fold<TWO>(run_of(img, TWO, lane), c, cw, (int)o, shift, ci.w);
+        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w);
     else
         ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
     res->k[pi][lane] = (uint8_t)ev.sel.k_own;
@@ -844,8 +830,7 @@ __device__ __forceinline__ void load_lr4(const T *__restrict__ src, uint32_t j0,
 
 template <bool A16, typename T>
 __device__ __forceinline__ void stage_ms(const T *__restrict__ src, int tid, uint32_t *__restrict__ img,
-                                         uint32_t *__restrict__ lr, int32_t (&mn)[4],
-                                         int32_t (&mx)[4], uint32_t (&orv)[4])
+                                         int32_t (&mn)[4], int32_t (&mx)[4], uint32_t (&orv)[4])
 {
 #pragma unroll
     for (int m = 0; m < ATG_MAX_BLOCK / 1024; ++m) {
@@ -863,12 +848,7 @@ __device__ __forceinline__ void stage_ms(const T *__restrict__ src, int tid, uin
 #pragma unroll
         for (int cnd = 0; cnd < 3; ++cnd)
             *(uint2 *)&img[cnd * PK_WORDS + paddr(2 * (int)q0)] = pack4(s[cnd]);
-        uint4 w;
-        w.x = __builtin_amdgcn_perm((uint32_t)s[1][0], (uint32_t)s[0][0], 0x05040100u);
-        w.y = __builtin_amdgcn_perm((uint32_t)s[1][1], (uint32_t)s[0][1], 0x05040100u);
-        w.z = __builtin_amdgcn_perm((uint32_t)s[1][2], (uint32_t)s[0][2], 0x05040100u);
-        w.w = __builtin_amdgcn_perm((uint32_t)s[1][3], (uint32_t)s[0][3], 0x05040100u);
-        *(uint4 *)&lr[laddr(4 * (int)q0)] = w;
+
     }
 }
 
@@ -880,7 +860,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
     uint32_t *__restrict__ slow_list, uint32_t *__restrict__ slow_count)
 {
     __shared__ __attribute__((aligned(16))) uint32_t img[3 * PK_WORDS]; // L, R, M packed
-    __shared__ __attribute__((aligned(16))) uint32_t lr[LR_WORDS];       // (L, R) words
     __shared__ int32_t red[4][4][3];                                      // [wave][cand][mn,mx,or]
     __shared__ CandInfo info[4];
     __shared__ PredRes res[4];
@@ -905,8 +884,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
     }
     if (tid < 3 * PK_PRE)
         img[(tid / PK_PRE) * PK_WORDS + (tid % PK_PRE)] = 0u;
-    else if (tid < 3 * PK_PRE + LR_PRE)
-        lr[tid - 3 * PK_PRE] = 0u;
     else if (tid == 255)
         qnext = 0u;
     {
@@ -930,9 +907,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
     {
         const T *__restrict__ src = pcm + fi.pcm_start * 2u;
         if ((((uintptr_t)src) & 15u) == 0u)
-            stage_ms<true>(src, tid, img, lr, mn, mx, orv);
+            stage_ms<true>(src, tid, img, mn, mx, orv);
         else
-            stage_ms<false>(src, tid, img, lr, mn, mx, orv);
+            stage_ms<false>(src, tid, img, mn, mx, orv);
     }
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -973,7 +950,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         cs.orv = uniform_u32(cs.orv);
         const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
         if (cand == 3u)
-            cand_prepare<true>(p, unit, sbps, lr, cs, lane, est_tab, out + unit, &info[3]);
+            cand_prepare<true>(p, unit, sbps, img, cs, lane, est_tab, out + unit, &info[3]);
         else
             cand_prepare<false>(p, unit, sbps, img + cand * PK_WORDS, cs, lane, est_tab,
                                 out + unit, &info[cand]);
@@ -1003,7 +980,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         const int16_t *lq = (const int16_t *)lq32 + jc * p.coef_stride;
         const int8_t *ls = (const int8_t *)ls32 + jc * p.max_lpc_order;
         if (jc == 3u)
-            pred_job<true>(p, N, lr, ci, pi, lane, lq, ls, &res[3]);
+            pred_job<true>(p, N, img, ci, pi, lane, lq, ls, &res[3]);
         else
             pred_job<false>(p, N, img + jc * PK_WORDS, ci, pi, lane, lq, ls, &res[jc]);
     }
