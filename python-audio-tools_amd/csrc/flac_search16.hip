@@ -162,12 +162,12 @@ __device__ __forceinline__ uint32_t win_pair(const Win &x, int ii, int j)
 // Pass 1 of one predictor over the lane's 64 samples, D tap pairs cp on a
 // packed image.  Keeps v per sample in u[] and returns the run's sum |r| =
 // sum (v + [r < 0]) = 64 + sum (v + (n >> 31)) (n >= 0 <=> r < 0); lane 0's
-// warm-up samples (i < warm) are forced to n = -1 (v = 0, |r| = 0).  shv: the total shift sh + w, in a VGPR (a
-// shift by an SGPR operand issues at half the rate on gfx950,
-// tools/int_rate.hip).
+// warm-up samples (lane0 && i < order) are forced to n = -1 (v = 0,
+// |r| = 0).  shv: the total shift sh + w, in a VGPR (a shift by an SGPR
+// operand issues at half the rate on gfx950, tools/int_rate.hip).
 template <int D>
 __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const int (&cp)[14],
-                                      int c0acc, int shv, int warm, uint32_t (&u)[ATG_RUN],
+                                      int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
                                       uint32_t &sabs)
 {
     int tap0 = cp[0];
@@ -205,7 +205,7 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
                 const int i = 16 * c + ii + h;
                 int n = acc[h] >> shv;
                 if (i < ATG_FAST_ORDER)
-                    n = i < warm ? -1 : n;
+                    n = (lane0 && i < order) ? -1 : n;
                 const uint32_t s31 = (uint32_t)(n >> 31);
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
@@ -233,7 +233,7 @@ __device__ __forceinline__ void lr_words(const uint4 &l, const uint4 &r, uint32_
 
 template <int D>
 __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const int (&cl)[14],
-                                         int c0acc, int shv, int warm, uint32_t (&u)[ATG_RUN],
+                                         int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
                                          uint32_t &sabs)
 {
     constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
@@ -280,7 +280,7 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
                 const int i = 8 * c + ii + h;
                 int n = accs[h] >> shv;
                 if (i < ATG_FAST_ORDER)
-                    n = i < warm ? -1 : n;
+                    n = (lane0 && i < order) ? -1 : n;
                 const uint32_t s31 = (uint32_t)(n >> 31);
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
@@ -330,7 +330,10 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     const int c0acc = -(1 << (sh + (int)w));
     int shv = sh + (int)w;
     asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
-    const int warm = c.lane == 0 ? order : 0;
+    // lane 0's first `order` samples are warm-up: (lane0 && i < order) is a
+    // lane mask and a scalar compare, so one v_cndmask per masked sample
+    const bool lane0 = c.lane == 0;
+    const int warm = lane0 ? order : 0;
     uint32_t u[ATG_RUN];
     uint32_t lane_sum; // sum |r| of the run
     if (TWO) {
@@ -338,39 +341,39 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         // three tap counts only (zero taps past the order): a code image that
         // fits the instruction cache
         if (order < 4)
-            pass1_lr<2>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
         else if (order < 8)
-            pass1_lr<4>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1_lr<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
         else
-            pass1_lr<7>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
 #else
         switch (order / 2 + 1) {
-        case 1: pass1_lr<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 2: pass1_lr<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 3: pass1_lr<3>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 4: pass1_lr<4>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 5: pass1_lr<5>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 6: pass1_lr<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        default: pass1_lr<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 1: pass1_lr<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 2: pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 3: pass1_lr<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 4: pass1_lr<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 5: pass1_lr<5>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 6: pass1_lr<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        default: pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         }
 #endif
     } else {
 #if ATG_K2F_FEW
         if (order < 4)
-            pass1<2>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
         else if (order < 8)
-            pass1<4>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
         else
-            pass1<7>(run, cq, c0acc, shv, warm, u, lane_sum);
+            pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
 #else
         switch (order / 2 + 1) {
-        case 1: pass1<1>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 2: pass1<2>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 3: pass1<3>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 4: pass1<4>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 5: pass1<5>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        case 6: pass1<6>(run, cq, c0acc, shv, warm, u, lane_sum); break;
-        default: pass1<7>(run, cq, c0acc, shv, warm, u, lane_sum); break;
+        case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 3: pass1<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 4: pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 5: pass1<5>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 6: pass1<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        default: pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         }
 #endif
     }
