@@ -13,6 +13,10 @@ src = sys.argv[1] if len(sys.argv) > 1 else "gpurun_out/pmc"
 dst = sys.argv[2] if len(sys.argv) > 2 else "profiles/pmc_traffic.json"
 pmc = json.loads(subprocess.check_output([sys.executable, "tools/pmc_summary.py", src]))
 names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
+         # the 16-bit search and the general kernel's hand-over list run in
+         # the same step slot: their per-launch figures add up
+         "k_frame_search_ms": "subframe_search", "k_subframe_search16": "subframe_search",
+         "k_subframe_search_list": "subframe_search",
          "k_frame_decide": "frame_decide", "k_track_scan": "track_scan",
          "k_frame_pack": "frame_pack", "k_track_md5": "track_md5",
          "k_stream_header": "stream_header",
@@ -28,7 +32,7 @@ for k, v in pmc.items():
     base = k.split("<")[0]
     if base in names and "HBM_read_bytes" in v and "HBM_write_bytes" in v:
         # k_dec_chain runs twice per step (count + write passes): per step
-        out[names[base]] = int(v["HBM_read_bytes"] + v["HBM_write_bytes"])
+        out[names[base]] = out.get(names[base], 0) + int(v["HBM_read_bytes"] + v["HBM_write_bytes"])
 json.dump(out, open(dst, "w"), indent=1, sort_keys=True)
 print(json.dumps(out, indent=1, sort_keys=True))
 if len(sys.argv) > 3:
@@ -36,9 +40,11 @@ if len(sys.argv) > 3:
     for k, v in pmc.items():
         base = k.split("<")[0]
         if base in names and "SQ_INSTS_VALU" in v:
-            e = {c: v[c] for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES",
-                                   "SQ_INSTS_LDS", "SQ_INSTS_VMEM") if c in v}
+            e = valu.setdefault(names[base], {})
+            for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_WAVES", "SQ_INSTS_LDS",
+                      "SQ_INSTS_VMEM"):
+                if c in v:
+                    e[c] = e.get(c, 0) + v[c]
             e["frames"] = int(sys.argv[4])
             e["source"] = sys.argv[5] if len(sys.argv) > 5 else src
-            valu[names[base]] = e
     json.dump(valu, open(sys.argv[3], "w"), indent=1, sort_keys=True)
