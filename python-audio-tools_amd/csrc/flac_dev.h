@@ -80,6 +80,7 @@ struct SubDesc {
     uint8_t precision;
     int8_t shift;
     uint8_t sbps;        // subframe bits per sample before wasted shift
+    uint32_t amax;       // max |s >> wasted| of the candidate (FIXED/LPC/VERBATIM)
     int16_t coef[ATG_MAX_LPC];
     uint8_t rice[1 << ATG_MAX_PORDER];
 };

@@ -251,11 +251,15 @@ __device__ __forceinline__ void put_bits(uint32_t *fb, uint32_t pos, uint32_t n,
         atomicOr(&fb[w + 1], lo);
 }
 
-// per-lane MSB-first bit stream into the zeroed LDS image
+// per-lane MSB-first bit stream into the zeroed LDS image.  A lane's bit
+// range [begin, end) shares at most its first and last words with the
+// neighbouring lanes: those two are OR-ed in by end() (the first is held
+// in a register until then), every word in between is a plain store, so
+// the word-crossing branch holds no atomics and no nested conditions.
 struct LaneWriter {
     uint32_t *fb;
     uint64_t acc; // bits of words cw (high half) and cw + 1 (low half)
-    uint32_t cw, w0, bp;
+    uint32_t cw, w0, bp, first;
 
     __device__ __forceinline__ void begin(uint32_t *f, uint32_t pos)
     {
@@ -264,15 +268,7 @@ struct LaneWriter {
         cw = pos >> 5;
         w0 = cw;
         bp = pos;
-    }
-    __device__ __forceinline__ void emit(uint32_t w, uint32_t v)
-    {
-        if (v) {
-            if (w == w0)
-                atomicOr(&fb[w], v); // may be shared with the previous run
-            else
-                fb[w] = v;           // wholly this lane's
-        }
+        first = 0;
     }
     // `zeros` 0-bits, then the low n (1..32) bits of v (v < 2^n)
     __device__ __forceinline__ void put(uint32_t zeros, uint32_t n, uint32_t v)
@@ -280,13 +276,15 @@ struct LaneWriter {
         bp += zeros;
         const uint32_t nw = bp >> 5;
         if (nw != cw) {
-            emit(cw, (uint32_t)(acc >> 32));
-            if (nw == cw + 1u) {
-                acc <<= 32;
-            } else {
-                emit(cw + 1u, (uint32_t)acc);
-                acc = 0;
-            }
+            const uint32_t hi = (uint32_t)(acc >> 32), lo = (uint32_t)acc;
+            if (cw == w0)
+                first = hi;
+            else
+                fb[cw] = hi;
+            const bool adj = nw == cw + 1u;
+            if (!adj)
+                fb[cw + 1u] = lo; // wholly this lane's: the run goes on past it
+            acc = adj ? (uint64_t)lo << 32 : 0ull;
             cw = nw;
         }
         acc |= (uint64_t)v << (64u - (bp & 31u) - n);
@@ -295,6 +293,8 @@ struct LaneWriter {
     __device__ __forceinline__ void end()
     {
         const uint32_t hi = (uint32_t)(acc >> 32), lo = (uint32_t)acc;
+        if (first)
+            atomicOr(&fb[w0], first);
         if (hi)
             atomicOr(&fb[cw], hi);
         if (lo)
@@ -405,7 +405,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
         const SubDesc &d = sub[(size_t)f * p.n_cand + cand];
         const uint32_t type = d.type, order = d.order, w = d.wasted, sbps = d.sbps;
         const uint32_t start = pos;
-        uint32_t maxabs = 0;
+        // max |sample| of the candidate, from the search (picks the residual kernel)
+        const uint32_t maxabs = d.amax;
         // REG: candidate sample (ra - 16 + i) from the staged pairs, computed
         // where used (one v_dot2 + one shift) instead of held in 80 VGPRs
         const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
@@ -415,19 +416,9 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
             return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr[i]),
                                           __builtin_bit_cast(short2_t, wts), 0, false) >> xsh;
         };
-        if (REG) {
-#pragma unroll
-            for (int i = 16; i < 80; ++i)
-                maxabs = max(maxabs, iabs_u(xs(i)));
-        } else {
+        if (!REG)
             stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
-                                [&](uint32_t i, int32_t s) {
-                                    s >>= w;
-                                    sl[saddr((int)i)] = s;
-                                    maxabs = max(maxabs, iabs_u(s));
-                                });
-        }
-        maxabs = wave_max_u32(maxabs);
+                                [&](uint32_t i, int32_t s) { sl[saddr((int)i)] = s >> w; });
         // sample i of this subframe (generic paths; REG reads PCM directly)
         auto sample = [&](int i) -> int32_t {
             if (REG)

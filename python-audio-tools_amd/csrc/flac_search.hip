@@ -564,6 +564,7 @@ __device__ __forceinline__ void search_unit(const FlacParams &p, const T *__rest
         d->type = (uint8_t)pick;
         d->wasted = (uint8_t)w;
         d->sbps = (uint8_t)sbps;
+        d->amax = maxabs;
         d->method = (uint8_t)sel.method;
         d->porder = (uint8_t)sel.porder;
         if (pick == SF_FIXED) {

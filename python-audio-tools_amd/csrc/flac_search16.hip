@@ -743,6 +743,7 @@ __device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, con
         d->type = (uint8_t)pick;
         d->wasted = (uint8_t)w;
         d->sbps = (uint8_t)ci.sbps;
+        d->amax = ci.amax >> w; // exact: the low w bits of every sample are 0
         d->method = res->method[spi];
         d->porder = (uint8_t)po;
         if (pick == SF_FIXED) {
