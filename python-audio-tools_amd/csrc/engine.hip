@@ -514,6 +514,15 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     hipEvent_t *ev = sl.ev;
 
     HIP_TRY(hipEventRecord(ev[14], e->s_main));
+    // development switch: ATG_MD5_AT=1 starts the MD5 chains with the batch
+    // (before the LPC kernel) instead of after it
+    static const bool md5_first = getenv("ATG_MD5_AT") && atoi(getenv("ATG_MD5_AT")) == 1;
+    if (md5_first) {
+        HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_tables, 0));
+        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
+        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    }
     HIP_TRY(hipEventRecord(ev[0], e->s_main));
     HIP_TRY(launch_lpc_analyze(p, d_pcm, fmt, dfr, (const double *)e->windows.p,
                                (int16_t *)sl.coef.p, (int8_t *)sl.shift.p, (uint8_t *)sl.est.p,
@@ -523,10 +532,12 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
     // so a SIMD shared with a chain would leave straggler waves; the search
     // and pack grids are deep enough to absorb them
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
-    HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
-    HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    if (!md5_first) {
+        HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
+        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
+        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    }
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
     if (pl.big)
         HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,

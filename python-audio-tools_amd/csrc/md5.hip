@@ -2,15 +2,24 @@
 // little-endian signed sample bytes fed by the PCM reader callback,
 // src/encoders/flac.c:187-188, 1570-1576; src/pcmconv.c:266-291).
 //
-// MD5 is one serial chain per track, so the kernel runs one lane per track
-// and is launched on its own stream, concurrently with the encoder kernels
-// (it occupies a handful of SIMDs).  Round functions use v_bfi/v_xor3 forms
-// and v_alignbit rotates; message words are fetched 16 per block.
+// MD5 is one serial chain per track, so a lane hashes one track and the
+// time of a batch is one lane's chain.  A lone wave issues one VALU op per
+// ~2.2 ns (tools/md5_rate.hip, profiles/r02_int_rate.txt), so the chain is
+// bound by its instruction count, not by dependent latency: a round is
+// F (v_bitop3), a + F + (X[g] + T) (v_add3), the rotate (v_alignbit) and
+// + b (v_add) once the message-plus-constant word X[g] + T is given.
+// Whole 64-byte blocks therefore run on a wave PAIR per 64 streams: the
+// helper wave loads the blocks, forms the 64 words X[g(i)] + T[i] in round
+// order and stores them to an LDS ring; the hasher wave reads them with
+// 16 ds_read_b128 and runs 4 VALU ops per round.  One s_barrier per block
+// hands a ring slot over.  The encoder launches it on its own stream,
+// concurrently with the encoder kernels (it occupies a handful of SIMDs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "flac_dev.h"
 #include "launch.h"
+#include "wave.h"
 
 #define MD5_D 4
 
@@ -21,12 +30,10 @@ __device__ __forceinline__ uint32_t rotl(uint32_t x, int s) { return __builtin_a
 #define F1(x, y, z) (z ^ (x & (y ^ z)))
 #define F2(x, y, z) (y ^ (z & (x ^ y)))
 // x ^ y ^ z as one v_bitop3_b32 (truth table 0x96); the compiler emits two
-// v_xor_b32 otherwise
+// v_xor_b32 otherwise (the builtin, unlike inline asm, needs no hazard nop)
 __device__ __forceinline__ uint32_t xor3(uint32_t x, uint32_t y, uint32_t z)
 {
-    uint32_t r;
-    asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(x), "v"(y), "v"(z));
-    return r;
+    return __builtin_amdgcn_bitop3_b32(x, y, z, 0x96);
 }
 #define F3(x, y, z) xor3(x, y, z)
 #define F4(x, y, z) (y ^ (x | ~z))
@@ -104,6 +111,228 @@ __device__ __forceinline__ void md5_compress(uint32_t h[4], const uint32_t X[16]
     h[3] += d;
 }
 
+// RFC 1321 round i: message word g(i), constant T[i], rotate s(i)
+#define MD5_ROUNDS_LO(S) \
+    S(0, 0, 0xd76aa478, 7) S(1, 1, 0xe8c7b756, 12) S(2, 2, 0x242070db, 17) \
+    S(3, 3, 0xc1bdceee, 22) S(4, 4, 0xf57c0faf, 7) S(5, 5, 0x4787c62a, 12) \
+    S(6, 6, 0xa8304613, 17) S(7, 7, 0xfd469501, 22) S(8, 8, 0x698098d8, 7) \
+    S(9, 9, 0x8b44f7af, 12) S(10, 10, 0xffff5bb1, 17) S(11, 11, 0x895cd7be, 22) \
+    S(12, 12, 0x6b901122, 7) S(13, 13, 0xfd987193, 12) S(14, 14, 0xa679438e, 17) \
+    S(15, 15, 0x49b40821, 22) S(16, 1, 0xf61e2562, 5) S(17, 6, 0xc040b340, 9) \
+    S(18, 11, 0x265e5a51, 14) S(19, 0, 0xe9b6c7aa, 20) S(20, 5, 0xd62f105d, 5) \
+    S(21, 10, 0x02441453, 9) S(22, 15, 0xd8a1e681, 14) S(23, 4, 0xe7d3fbc8, 20) \
+    S(24, 9, 0x21e1cde6, 5) S(25, 14, 0xc33707d6, 9) S(26, 3, 0xf4d50d87, 14) \
+    S(27, 8, 0x455a14ed, 20) S(28, 13, 0xa9e3e905, 5) S(29, 2, 0xfcefa3f8, 9) \
+    S(30, 7, 0x676f02d9, 14) S(31, 12, 0x8d2a4c8a, 20)
+#define MD5_ROUNDS_HI(S) \
+    S(32, 5, 0xfffa3942, 4) S(33, 8, 0x8771f681, 11) S(34, 11, 0x6d9d6122, 16) \
+    S(35, 14, 0xfde5380c, 23) S(36, 1, 0xa4beea44, 4) S(37, 4, 0x4bdecfa9, 11) \
+    S(38, 7, 0xf6bb4b60, 16) S(39, 10, 0xbebfbc70, 23) S(40, 13, 0x289b7ec6, 4) \
+    S(41, 0, 0xeaa127fa, 11) S(42, 3, 0xd4ef3085, 16) S(43, 6, 0x04881d05, 23) \
+    S(44, 9, 0xd9d4d039, 4) S(45, 12, 0xe6db99e5, 11) S(46, 15, 0x1fa27cf8, 16) \
+    S(47, 2, 0xc4ac5665, 23) S(48, 0, 0xf4292244, 6) S(49, 7, 0x432aff97, 10) \
+    S(50, 14, 0xab9423a7, 15) S(51, 5, 0xfc93a039, 21) S(52, 12, 0x655b59c3, 6) \
+    S(53, 3, 0x8f0ccc92, 10) S(54, 10, 0xffeff47d, 15) S(55, 1, 0x85845dd1, 21) \
+    S(56, 8, 0x6fa87e4f, 6) S(57, 15, 0xfe2ce6e0, 10) S(58, 6, 0xa3014314, 15) \
+    S(59, 13, 0x4e0811a1, 21) S(60, 4, 0xf7537e82, 6) S(61, 11, 0xbd3af235, 10) \
+    S(62, 2, 0x2ad7d2bb, 15) S(63, 9, 0xeb86d391, 21)
+#define MD5_ROUNDS(S) MD5_ROUNDS_LO(S) MD5_ROUNDS_HI(S)
+
+__device__ __forceinline__ uint32_t u4_at(const uint4 &v, int c)
+{
+    return c == 0 ? v.x : c == 1 ? v.y : c == 2 ? v.z : v.w;
+}
+
+// helper: the round-ordered words X[g(i)] + T[i] of half HALF of a block
+template <int HALF>
+__device__ __forceinline__ void md5_xt_half(const uint4 (&blk)[4], uint4 (&xt)[8])
+{
+    uint32_t w[32];
+#define MD5_XT(i, g, t, s) w[(i) & 31] = u4_at(blk[(g) >> 2], (g) & 3) + (t);
+    if constexpr (HALF == 0) {
+        MD5_ROUNDS_LO(MD5_XT)
+    } else {
+        MD5_ROUNDS_HI(MD5_XT)
+    }
+#undef MD5_XT
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+        xt[q] = make_uint4(w[4 * q], w[4 * q + 1], w[4 * q + 2], w[4 * q + 3]);
+}
+
+// hasher: rounds 32 * HALF .. 32 * HALF + 31 of a block on the state v =
+// (a, b, c, d) from that half's X[g] + T words (F1 .. F4 by round)
+template <int HALF>
+__device__ __forceinline__ void md5_half_xt(uint32_t (&v)[4], const uint4 (&xt)[8])
+{
+#define MD5_F(i, x, y, z) ((i) < 16 ? F1(x, y, z) : (i) < 32 ? F2(x, y, z) : (i) < 48 ? F3(x, y, z) : F4(x, y, z))
+#define MD5_HS(i, g, t, s)                                                                      \
+    {                                                                                           \
+        uint32_t &a = v[(64 - (i)) & 3];                                                        \
+        const uint32_t b = v[(65 - (i)) & 3], c = v[(66 - (i)) & 3], d = v[(67 - (i)) & 3];   \
+        a = b + rotl(a + MD5_F(i, b, c, d) + u4_at(xt[((i) >> 2) & 7], (i) & 3), s);            \
+    }
+    if constexpr (HALF == 0) {
+        MD5_ROUNDS_LO(MD5_HS)
+    } else {
+        MD5_ROUNDS_HI(MD5_HS)
+    }
+#undef MD5_HS
+#undef MD5_F
+}
+
+// LDS ring of the wave pair: 3 half-block slots x 8 round-quads x 64
+// lanes = 24 KB (it fits beside four K2 frame workgroups on a CU), and the
+// two progress counters.  Units are half blocks, u = 2 * block + half, in
+// slot u % 3.  prod = units the helper has stored; cons = units whose ring
+// reads the hasher has completed.  A wave's LDS instructions execute in
+// issue order, so a counter store issued after the data stores (helper) or
+// after the data loads (hasher) is seen only once those have executed; a
+// hasher load issued after a counter load that showed unit u is ready sees
+// unit u's data.  No s_barrier in the loop (one costs the pair ~130 ns).
+struct Md5Pair {
+    uint4 ring[3][8][64];
+    uint32_t prod, cons;
+};
+
+#define MD5_SPIN_MAX (1u << 22) // bounded waits: a lost wake-up cannot hang the GPU
+
+__device__ __forceinline__ uint32_t md5_ctr(const uint32_t *c)
+{
+    return __builtin_amdgcn_readfirstlane(__atomic_load_n(c, __ATOMIC_RELAXED));
+}
+
+__device__ __forceinline__ void md5_wait(const uint32_t *c, uint32_t need)
+{
+    for (uint32_t i = 0; i < MD5_SPIN_MAX && md5_ctr(c) < need; ++i)
+        __builtin_amdgcn_s_sleep(1);
+    asm volatile("" ::: "memory");
+}
+
+__device__ __forceinline__ void md5_publish(uint32_t *c, uint32_t v)
+{
+    asm volatile("" ::: "memory");
+    if ((threadIdx.x & 63u) == 0u)
+        __atomic_store_n(c, v, __ATOMIC_RELAXED);
+}
+
+__device__ __forceinline__ void md5_load_unit(const Md5Pair &pr, uint32_t slot, int lane, uint4 (&x)[8])
+{
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+        x[k] = pr.ring[slot][k][lane];
+}
+
+// Whole blocks [0, full) of the lane's 16-byte aligned stream q, on the
+// wave pair (threadIdx.x >> 6: 0 hasher, 1 helper; both call this with the
+// same lane -> stream mapping and the same wave-uniform nbmax = max full,
+// after pr's counters were zeroed and the pair met once).  The hasher's h
+// advances over the lane's `full` blocks.  The hasher loads unit u + 1
+// speculatively, with the prod counter, while it hashes unit u, and checks
+// the counter after; the helper runs up to 2 units ahead.
+__device__ __forceinline__ void md5_pair_blocks(const uint4 *__restrict__ q, uint32_t full,
+                                                uint32_t nbmax, uint32_t h[4], Md5Pair &pr)
+{
+    const int lane = threadIdx.x & 63;
+    const bool helper = (threadIdx.x >> 6) != 0;
+    const uint32_t last = full ? full - 1u : 0u;
+    if (helper) {
+        uint4 buf[MD5_D][4]; // block k in buf[k % MD5_D]
+        if (full) {
+#pragma unroll
+            for (int j = 0; j < MD5_D; ++j)
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+                    buf[j][i] = q[(size_t)min((uint32_t)j, last) * 4u + i];
+        }
+        uint32_t slot = 0; // slot of unit 2b
+        for (uint32_t b0 = 0; b0 < nbmax; b0 += MD5_D) {
+#pragma unroll
+            for (int j = 0; j < MD5_D; ++j) {
+                const uint32_t b = b0 + (uint32_t)j;
+                if (b < nbmax) {
+#pragma unroll
+                    for (int hf = 0; hf < 2; ++hf) {
+                        const uint32_t u = 2u * b + (uint32_t)hf;
+                        uint4 xt[8];
+                        if (hf == 0)
+                            md5_xt_half<0>(buf[j], xt);
+                        else
+                            md5_xt_half<1>(buf[j], xt);
+                        if (hf == 1 && full) {
+#pragma unroll
+                            for (int i = 0; i < 4; ++i)
+                                buf[j][i] = q[(size_t)min(b + MD5_D, last) * 4u + i];
+                        }
+                        if (u >= 3u)
+                            md5_wait(&pr.cons, u - 2u); // unit u - 3 left the slot
+#pragma unroll
+                        for (int k = 0; k < 8; ++k)
+                            pr.ring[slot][k][lane] = xt[k];
+                        md5_publish(&pr.prod, u + 1u);
+                        slot = slot == 2u ? 0u : slot + 1u;
+                    }
+                }
+            }
+        }
+    } else {
+        uint4 cur[8], nxt[8];
+        md5_wait(&pr.prod, 1u);
+        md5_load_unit(pr, 0u, lane, cur);
+        uint32_t slot = 0; // slot of unit 2b
+        for (uint32_t b = 0; b < nbmax; ++b) {
+            const bool on = b < full;
+            const uint32_t u = 2u * b;
+            const uint32_t s1 = slot == 2u ? 0u : slot + 1u, s2 = s1 == 2u ? 0u : s1 + 1u;
+            uint32_t v[4] = {h[0], h[1], h[2], h[3]};
+            // half 0 (unit u from cur); unit u + 1 loaded meanwhile
+            uint32_t p = md5_ctr(&pr.prod);
+            asm volatile("" ::: "memory");
+            md5_load_unit(pr, s1, lane, nxt);
+            if (on)
+                md5_half_xt<0>(v, cur);
+            if (p < u + 2u) {
+                md5_wait(&pr.prod, u + 2u);
+                md5_load_unit(pr, s1, lane, nxt);
+            }
+            md5_publish(&pr.cons, u + 2u); // units <= u + 1 read
+            // half 1 (unit u + 1 from nxt); unit u + 2 loaded meanwhile
+            const bool more = b + 1u < nbmax;
+            if (more) {
+                p = md5_ctr(&pr.prod);
+                asm volatile("" ::: "memory");
+                md5_load_unit(pr, s2, lane, cur);
+            }
+            if (on) {
+                md5_half_xt<1>(v, nxt);
+                h[0] += v[0];
+                h[1] += v[1];
+                h[2] += v[2];
+                h[3] += v[3];
+            }
+            if (more) {
+                if (p < u + 3u) {
+                    md5_wait(&pr.prod, u + 3u);
+                    md5_load_unit(pr, s2, lane, cur);
+                }
+            }
+            if (more)
+                md5_publish(&pr.cons, u + 3u);
+            slot = s2;
+        }
+    }
+}
+
+// zero the pair's counters, then meet once
+__device__ __forceinline__ void md5_pair_init(Md5Pair &pr)
+{
+    if (threadIdx.x == 0) {
+        pr.prod = 0;
+        pr.cons = 0;
+    }
+    __syncthreads();
+}
+
 // byte j of the track's little-endian PCM byte stream (generic formats)
 template <typename T>
 __device__ __forceinline__ uint32_t pcm_byte(const T *s, uint64_t j, uint32_t bb)
@@ -171,98 +400,33 @@ __device__ __forceinline__ void md5_s32_groups(uint32_t h[4], const uint4 *__res
     }
 }
 
-template <typename T>
-__global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restrict__ pcm,
-                                                  const TrackInfo *__restrict__ tracks,
-                                                  TrackOut *__restrict__ tout)
+// the MD5 state as digest-order bytes: the hand-over from the pair kernel
+// to the finishing kernel (and, after the padding block, the digest itself)
+__device__ __forceinline__ void md5_put(uint8_t *d, const uint32_t h[4])
 {
-    // the hash chains are the longest serial path of a batch: let their
-    // waves issue ahead of the encoder kernels sharing the SIMD
-    __builtin_amdgcn_s_setprio(3);
-    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
-    if (t >= p.n_tracks)
-        return;
-    const TrackInfo ti = tracks[t];
-    const uint32_t bb = p.bps / 8u;
-    const T *s = pcm + ti.pcm_start * p.channels;
-    const uint64_t nbytes = ti.pcm_frames * p.channels * bb;
-    // fast path: the sample container IS the byte stream (S16 at 16 bits)
-    const bool raw = sizeof(T) == 2 && bb == 2 && (((uintptr_t)s) & 15u) == 0;
-    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    uint32_t X[16];
+    for (int i = 0; i < 4; ++i)
+        for (int j = 0; j < 4; ++j)
+            d[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
+__device__ __forceinline__ void md5_get(const uint8_t *d, uint32_t h[4])
+{
+    for (int i = 0; i < 4; ++i)
+        h[i] = d[4 * i] | ((uint32_t)d[4 * i + 1] << 8) | ((uint32_t)d[4 * i + 2] << 16) |
+               ((uint32_t)d[4 * i + 3] << 24);
+}
+
+// the last partial block + padding (0x80, zeros, 64-bit little-endian bit
+// length) of an nbytes stream whose whole blocks are in h; byte(j) = byte j
+template <typename B>
+__device__ __forceinline__ void md5_pad(uint32_t h[4], uint64_t nbytes, B &&byte)
+{
     const uint64_t full = nbytes / 64u;
-    if (raw && full > 0) {
-        // MD5_D blocks in flight per lane: the loads of block b + MD5_D are
-        // issued before block b is hashed, so HBM latency hides behind
-        // ~MD5_D x 320 dependent VALU ops (one chain per lane, 4 cyc each)
-        const uint4 *q = (const uint4 *)s;
-        uint4 buf[MD5_D][4];
-#pragma unroll
-        for (int j = 0; j < MD5_D; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                buf[j][i] = q[(uint64_t)min((uint64_t)j, full - 1u) * 4u + i];
-        uint64_t blk = 0;
-        for (; blk + MD5_D <= full; blk += MD5_D) {
-#pragma unroll
-            for (int j = 0; j < MD5_D; ++j) {
-                // hash straight from the load registers, then refill them
-                // (block blk + j + MD5_D, clamped) -- no message copies
-                md5_compress(h, (const uint32_t *)&buf[j][0]);
-                const uint64_t nb = min(blk + (uint64_t)(j + MD5_D), full - 1u);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    buf[j][i] = q[nb * 4u + i];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < MD5_D; ++j) {
-            if (blk + (uint64_t)j < full) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) {
-                    X[4 * i] = buf[j][i].x;
-                    X[4 * i + 1] = buf[j][i].y;
-                    X[4 * i + 2] = buf[j][i].z;
-                    X[4 * i + 3] = buf[j][i].w;
-                }
-                md5_compress(h, X);
-            }
-        }
-    } else if (!raw) {
-        // int32 container, 16-byte aligned: whole sample groups by v_perm
-        // packing; the bytes after the last whole group go the generic way
-        uint64_t blk = 0;
-        if (sizeof(T) == 4 && (((uintptr_t)s) & 15u) == 0 && bb >= 1 && bb <= 3) {
-            const uint64_t samples = ti.pcm_frames * p.channels;
-            const uint4 *q = (const uint4 *)s;
-            if (bb == 3) {
-                const uint64_t g = samples / S32Pack<3>::G;
-                md5_s32_groups<3>(h, q, g);
-                blk = g * 3u;
-            } else if (bb == 2) {
-                const uint64_t g = samples / S32Pack<2>::G;
-                md5_s32_groups<2>(h, q, g);
-                blk = g;
-            } else {
-                const uint64_t g = samples / S32Pack<1>::G;
-                md5_s32_groups<1>(h, q, g);
-                blk = g;
-            }
-        }
-        for (; blk < full; ++blk) {
-            for (int i = 0; i < 16; ++i) {
-                const uint64_t j = blk * 64u + 4u * (uint32_t)i;
-                X[i] = pcm_byte(s, j, bb) | (pcm_byte(s, j + 1, bb) << 8) |
-                       (pcm_byte(s, j + 2, bb) << 16) | (pcm_byte(s, j + 3, bb) << 24);
-            }
-            md5_compress(h, X);
-        }
-    }
-    // tail + padding (0x80, zeros, 64-bit little-endian bit length)
+    uint32_t X[16];
     uint8_t tail[128];
     const uint32_t rem = (uint32_t)(nbytes - full * 64u);
     for (uint32_t i = 0; i < rem; ++i)
-        tail[i] = (uint8_t)pcm_byte(s, full * 64u + i, bb);
+        tail[i] = (uint8_t)byte(full * 64u + i);
     tail[rem] = 0x80;
     const uint32_t tl = rem < 56u ? 64u : 128u;
     for (uint32_t i = rem + 1; i < tl - 8u; ++i)
@@ -276,13 +440,127 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
                    ((uint32_t)tail[o + 4 * i + 2] << 16) | ((uint32_t)tail[o + 4 * i + 3] << 24);
         md5_compress(h, X);
     }
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j)
-            tout[t].md5[4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+}
+
+// S16 PCM at 16 bits, 16-byte aligned: the sample container IS the byte
+// stream, hashed block by block on the wave pair
+__device__ __forceinline__ bool md5_track_raw(const FlacParams &p, const TrackInfo &ti,
+                                              const int16_t *pcm, uint64_t &full)
+{
+    const uint64_t nbytes = ti.pcm_frames * p.channels * 2u;
+    full = nbytes / 64u;
+    const int16_t *s = pcm + ti.pcm_start * p.channels;
+    return p.bps == 16u && (((uintptr_t)s) & 15u) == 0 && full < (1ull << 32);
+}
+
+// whole blocks of the raw tracks (a hasher + helper wave pair per 64
+// tracks); the state goes to tout[t].md5 for k_track_md5
+__global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int16_t *__restrict__ pcm,
+                                                        const TrackInfo *__restrict__ tracks,
+                                                        TrackOut *__restrict__ tout)
+{
+    // the hash chains are the longest serial path of a batch: let their
+    // waves issue ahead of the encoder kernels sharing the SIMD
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ Md5Pair pair_lds;
+    const uint32_t t = blockIdx.x * 64u + (threadIdx.x & 63u);
+    const bool valid = t < p.n_tracks;
+    const TrackInfo ti = tracks[valid ? t : 0u];
+    uint64_t full = 0;
+    const bool raw = valid && md5_track_raw(p, ti, pcm, full);
+    const uint32_t nbmax = wave_max_u32(raw ? (uint32_t)full : 0u);
+    if (!nbmax)
+        return;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    md5_pair_init(pair_lds);
+    md5_pair_blocks((const uint4 *)(pcm + ti.pcm_start * p.channels), raw ? (uint32_t)full : 0u,
+                    nbmax, h, pair_lds);
+    if (threadIdx.x < 64u && raw)
+        md5_put(tout[t].md5, h);
+}
+
+// lane per track: the tracks the pair kernel did not take (int32
+// containers, other widths, unaligned starts) from the start, then every
+// track's last partial block + padding, and the digest
+template <typename T>
+__global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restrict__ pcm,
+                                                  const TrackInfo *__restrict__ tracks,
+                                                  TrackOut *__restrict__ tout, int paired)
+{
+    __builtin_amdgcn_s_setprio(3);
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= p.n_tracks)
+        return;
+    const TrackInfo ti = tracks[t];
+    const uint32_t bb = p.bps / 8u;
+    const T *s = pcm + ti.pcm_start * p.channels;
+    const uint64_t nbytes = ti.pcm_frames * p.channels * bb;
+    uint64_t full = nbytes / 64u;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    uint64_t blk = 0;
+    if (paired && sizeof(T) == 2 && md5_track_raw(p, ti, (const int16_t *)pcm, full)) {
+        if (full) // (no whole block: the pair kernel left this lane alone)
+            md5_get(tout[t].md5, h);
+        blk = full;
+    } else if (sizeof(T) == 4 && (((uintptr_t)s) & 15u) == 0 && bb >= 1 && bb <= 3) {
+        // int32 container, 16-byte aligned: whole sample groups by v_perm
+        // packing; the bytes after the last whole group go the generic way
+        const uint64_t samples = ti.pcm_frames * p.channels;
+        const uint4 *q = (const uint4 *)s;
+        if (bb == 3) {
+            const uint64_t g = samples / S32Pack<3>::G;
+            md5_s32_groups<3>(h, q, g);
+            blk = g * 3u;
+        } else if (bb == 2) {
+            const uint64_t g = samples / S32Pack<2>::G;
+            md5_s32_groups<2>(h, q, g);
+            blk = g;
+        } else {
+            const uint64_t g = samples / S32Pack<1>::G;
+            md5_s32_groups<1>(h, q, g);
+            blk = g;
+        }
+    }
+    uint32_t X[16];
+    for (; blk < full; ++blk) {
+        for (int i = 0; i < 16; ++i) {
+            const uint64_t j = blk * 64u + 4u * (uint32_t)i;
+            X[i] = pcm_byte(s, j, bb) | (pcm_byte(s, j + 1, bb) << 8) |
+                   (pcm_byte(s, j + 2, bb) << 16) | (pcm_byte(s, j + 3, bb) << 24);
+        }
+        md5_compress(h, X);
+    }
+    md5_pad(h, nbytes, [&](uint64_t j) { return pcm_byte(s, j, bb); });
+    md5_put(tout[t].md5, h);
 }
 
 // MD5 of a plain byte stream per lane (the decoder hashes the little-endian
-// PCM bytes K5 of flac_decode.hip wrote; streams start 64-byte aligned)
+// PCM bytes K5 of flac_decode.hip wrote; streams start 64-byte aligned):
+// whole blocks on the wave pair, state to md5[16 t]
+__global__ __launch_bounds__(128) void k_bytes_md5_pair(const uint8_t *__restrict__ base,
+                                                        const uint64_t *__restrict__ off,
+                                                        const uint64_t *__restrict__ len, uint32_t n,
+                                                        uint8_t *__restrict__ md5)
+{
+    __builtin_amdgcn_s_setprio(3);
+    __shared__ Md5Pair pair_lds;
+    const uint32_t t = blockIdx.x * 64u + (threadIdx.x & 63u);
+    const bool valid = t < n;
+    const uint64_t full = valid ? len[t] / 64u : 0u;
+    const bool pair = full < (1ull << 32);
+    const uint32_t nbmax = wave_max_u32(pair ? (uint32_t)full : 0u);
+    if (!nbmax)
+        return;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    md5_pair_init(pair_lds);
+    md5_pair_blocks((const uint4 *)(base + off[valid ? t : 0u]), pair ? (uint32_t)full : 0u, nbmax,
+                    h, pair_lds);
+    if (threadIdx.x < 64u && valid)
+        md5_put(md5 + 16u * t, h);
+}
+
+// lane per stream: the blocks the pair kernel did not take, the padding,
+// the digest
 __global__ __launch_bounds__(64) void k_bytes_md5(const uint8_t *__restrict__ base,
                                                   const uint64_t *__restrict__ off,
                                                   const uint64_t *__restrict__ len, uint32_t n,
@@ -296,51 +574,22 @@ __global__ __launch_bounds__(64) void k_bytes_md5(const uint8_t *__restrict__ ba
     const uint64_t nbytes = len[t];
     const uint64_t full = nbytes / 64u;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    uint32_t X[16];
-    if (full > 0) {
-        const uint4 *q = (const uint4 *)s;
-        uint4 buf[MD5_D][4];
-#pragma unroll
-        for (int j = 0; j < MD5_D; ++j)
-#pragma unroll
-            for (int i = 0; i < 4; ++i)
-                buf[j][i] = q[(uint64_t)min((uint64_t)j, full - 1u) * 4u + i];
-        uint64_t blk = 0;
-        for (; blk + MD5_D <= full; blk += MD5_D) {
-#pragma unroll
-            for (int j = 0; j < MD5_D; ++j) {
-                md5_compress(h, (const uint32_t *)&buf[j][0]);
-                const uint64_t nb = min(blk + (uint64_t)(j + MD5_D), full - 1u);
-#pragma unroll
-                for (int i = 0; i < 4; ++i)
-                    buf[j][i] = q[nb * 4u + i];
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < MD5_D; ++j)
-            if (blk + (uint64_t)j < full)
-                md5_compress(h, (const uint32_t *)&buf[j][0]);
+    uint64_t blk = 0;
+    if (full < (1ull << 32)) {
+        if (full)
+            md5_get(md5 + 16u * t, h);
+        blk = full;
     }
-    uint8_t tail[128];
-    const uint32_t rem = (uint32_t)(nbytes - full * 64u);
-    for (uint32_t i = 0; i < rem; ++i)
-        tail[i] = s[full * 64u + i];
-    tail[rem] = 0x80;
-    const uint32_t tl = rem < 56u ? 64u : 128u;
-    for (uint32_t i = rem + 1; i < tl - 8u; ++i)
-        tail[i] = 0;
-    const uint64_t bits = nbytes * 8u;
-    for (int i = 0; i < 8; ++i)
-        tail[tl - 8u + i] = (uint8_t)(bits >> (8 * i));
-    for (uint32_t o = 0; o < tl; o += 64) {
+    uint32_t X[16];
+    for (; blk < full; ++blk) {
         for (int i = 0; i < 16; ++i)
-            X[i] = tail[o + 4 * i] | ((uint32_t)tail[o + 4 * i + 1] << 8) |
-                   ((uint32_t)tail[o + 4 * i + 2] << 16) | ((uint32_t)tail[o + 4 * i + 3] << 24);
+            X[i] = s[blk * 64u + 4 * i] | ((uint32_t)s[blk * 64u + 4 * i + 1] << 8) |
+                   ((uint32_t)s[blk * 64u + 4 * i + 2] << 16) |
+                   ((uint32_t)s[blk * 64u + 4 * i + 3] << 24);
         md5_compress(h, X);
     }
-    for (int i = 0; i < 4; ++i)
-        for (int j = 0; j < 4; ++j)
-            md5[16 * t + 4 * i + j] = (uint8_t)(h[i] >> (8 * j));
+    md5_pad(h, nbytes, [&](uint64_t j) { return (uint32_t)s[j]; });
+    md5_put(md5 + 16u * t, h);
 }
 
 hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint64_t *len,
@@ -348,8 +597,9 @@ hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint
 {
     if (!n)
         return hipSuccess;
-    hipLaunchKernelGGL(k_bytes_md5, dim3((n + 63u) / 64u), dim3(64), 0, s, base, off, len, n,
-                       md5);
+    const dim3 grid((n + 63u) / 64u);
+    hipLaunchKernelGGL(k_bytes_md5_pair, grid, dim3(128), 0, s, base, off, len, n, md5);
+    hipLaunchKernelGGL(k_bytes_md5, grid, dim3(64), 0, s, base, off, len, n, md5);
     return hipGetLastError();
 }
 
@@ -358,12 +608,16 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
 {
     if (!p.n_tracks)
         return hipSuccess;
-    dim3 grid((p.n_tracks + 63u) / 64u);
+    const dim3 grid((p.n_tracks + 63u) / 64u);
+    const int paired = fmt == 0 && p.bps == 16u;
+    if (paired)
+        hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
+                           tout);
     if (fmt == 0)
         hipLaunchKernelGGL((k_track_md5<int16_t>), grid, dim3(64), 0, s, p,
-                           (const int16_t *)pcm, tracks, tout);
+                           (const int16_t *)pcm, tracks, tout, paired);
     else
         hipLaunchKernelGGL((k_track_md5<int32_t>), grid, dim3(64), 0, s, p,
-                           (const int32_t *)pcm, tracks, tout);
+                           (const int32_t *)pcm, tracks, tout, 0);
     return hipGetLastError();
 }

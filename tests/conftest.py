@@ -16,5 +16,10 @@ def pytest_configure(config):
 
 @pytest.fixture(scope="session")
 def gpu_engine():
+    # torch's HIP runtime comes up first: tests hand torch device buffers to
+    # the engine, and torch cannot initialise once libatgpu's runtime has
+    import torch
+    if torch.cuda.is_available():
+        torch.cuda.init()
     from audiotools import _atgpu
     return _atgpu.engine()

@@ -195,6 +195,33 @@ __global__ __launch_bounds__(64) void k_md5(const uint4 *__restrict__ data, uint
             out[(t * TR + r) * 4 + i] = h[r][i];
 }
 
+typedef short bg_short2 __attribute__((ext_vector_type(2)));
+// background load shaped like K2: 256-thread workgroups with 33 KB of LDS,
+// a v_dot2 chain per ds_read_b128 (VALU-bound, LDS ~40% busy), `iters` long
+__global__ __launch_bounds__(256) void k_busy(uint32_t *out, uint32_t iters, int lds_reads)
+{
+    __shared__ uint4 lds[33 * 1024 / 16];
+    const int tid = threadIdx.x;
+    for (int i = tid; i < 33 * 1024 / 16; i += 256)
+        lds[i] = make_uint4(i, i + 1, i + 2, i + 3);
+    __syncthreads();
+    int acc[8] = {tid, tid + 1, tid + 2, tid + 3, tid + 4, tid + 5, tid + 6, tid + 7};
+    for (uint32_t it = 0; it < iters; ++it) {
+        uint4 w = lds_reads ? lds[(tid + it * 64) & (33 * 1024 / 16 - 1)] : make_uint4(it, it, it, it);
+#pragma unroll
+        for (int r = 0; r < 9; ++r)
+#pragma unroll
+            for (int k = 0; k < 8; ++k)
+                acc[k] = __builtin_amdgcn_sdot2(__builtin_bit_cast(bg_short2, w.x ^ (uint32_t)k),
+                                                __builtin_bit_cast(bg_short2, w.y + (uint32_t)r), acc[k], false);
+    }
+    int s = 0;
+    for (int k = 0; k < 8; ++k)
+        s += acc[k];
+    if (s == 0x7fffffff)
+        out[0] = s;
+}
+
 template <int V, bool ONE>
 static float run(const uint4 *d, uint32_t ntr, uint32_t nb, uint32_t *out)
 {
@@ -208,6 +235,29 @@ static float run(const uint4 *d, uint32_t ntr, uint32_t nb, uint32_t *out)
     hipLaunchKernelGGL((k_md5<V, ONE>), grid, dim3(64), 0, 0, d, ntr, nb, out);
     hipEventRecord(e1);
     hipEventSynchronize(e1);
+    float ms = 0;
+    hipEventElapsedTime(&ms, e0, e1);
+    return ms;
+}
+
+static hipStream_t g_bg = nullptr, g_fg = nullptr;
+static uint32_t *g_sink = nullptr;
+
+// MD5 variant V timed on its own stream while k_busy fills the GPU
+template <int V>
+static float run_loaded(const uint4 *d, uint32_t ntr, uint32_t nb, uint32_t *out, int lds_reads)
+{
+    const uint32_t tr = V == 3 ? ntr / 2 : ntr;
+    dim3 grid((tr + 63) / 64);
+    hipEvent_t e0, e1;
+    hipEventCreate(&e0);
+    hipEventCreate(&e1);
+    hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 1200u, lds_reads);
+    hipEventRecord(e0, g_fg);
+    hipLaunchKernelGGL((k_md5<V, false>), grid, dim3(64), 0, g_fg, d, ntr, nb, out);
+    hipEventRecord(e1, g_fg);
+    hipEventSynchronize(e1);
+    hipDeviceSynchronize();
     float ms = 0;
     hipEventElapsedTime(&ms, e0, e1);
     return ms;
@@ -238,6 +288,74 @@ int main(int argc, char **argv)
         {"v2 fast rotate, 64 lanes", run<2, false>}, {"v3 2 tracks/lane", run<3, false>},
         {"v0 shipped, 1 lane/wave", run<0, true>},   {"v1 add3 off-chain, 1 lane/wave", run<1, true>},
     };
+    {
+        // the shipped wave-pair kernel (md5.hip k_bytes_md5: whole blocks on a
+        // hasher + helper pair, then the padding block)
+        std::vector<uint64_t> off(ntr), len(ntr);
+        for (uint32_t t = 0; t < ntr; ++t) {
+            off[t] = (uint64_t)t * nb * 64u;
+            len[t] = (uint64_t)nb * 64u;
+        }
+        uint64_t *doff, *dlen;
+        uint8_t *dmd5;
+        hipMalloc(&doff, ntr * 8);
+        hipMalloc(&dlen, ntr * 8);
+        hipMalloc(&dmd5, ntr * 16);
+        hipMemcpy(doff, off.data(), ntr * 8, hipMemcpyHostToDevice);
+        hipMemcpy(dlen, len.data(), ntr * 8, hipMemcpyHostToDevice);
+        launch_bytes_md5((const uint8_t *)d, doff, dlen, ntr, dmd5, 0);
+        hipEvent_t e0, e1;
+        hipEventCreate(&e0);
+        hipEventCreate(&e1);
+        hipEventRecord(e0);
+        launch_bytes_md5((const uint8_t *)d, doff, dlen, ntr, dmd5, 0);
+        hipEventRecord(e1);
+        hipEventSynchronize(e1);
+        float ms = 0;
+        hipEventElapsedTime(&ms, e0, e1);
+        printf("%-34s %8.3f ms  %7.1f ns/block\n", "k_bytes_md5 wave pair (shipped)", ms, ms * 1e6 / nb);
+    }
+    hipStreamCreateWithFlags(&g_bg, hipStreamNonBlocking);
+    hipStreamCreateWithFlags(&g_fg, hipStreamNonBlocking);
+    hipMalloc(&g_sink, 64);
+    {
+        // under a K2-shaped background load (launched first on its own stream)
+        std::vector<uint64_t> off(ntr), len(ntr);
+        for (uint32_t t = 0; t < ntr; ++t) {
+            off[t] = (uint64_t)t * nb * 64u;
+            len[t] = (uint64_t)nb * 64u;
+        }
+        uint64_t *doff, *dlen;
+        uint8_t *dmd5;
+        hipMalloc(&doff, ntr * 8);
+        hipMalloc(&dlen, ntr * 8);
+        hipMalloc(&dmd5, ntr * 16);
+        hipMemcpy(doff, off.data(), ntr * 8, hipMemcpyHostToDevice);
+        hipMemcpy(dlen, len.data(), ntr * 8, hipMemcpyHostToDevice);
+        for (int lr = 0; lr < 2; ++lr) {
+            hipEvent_t e0, e1;
+            hipEventCreate(&e0);
+            hipEventCreate(&e1);
+            hipEvent_t b0, b1;
+            hipEventCreate(&b0);
+            hipEventCreate(&b1);
+            hipEventRecord(b0, g_bg);
+            hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 1200u, lr);
+            hipEventRecord(b1, g_bg);
+            hipEventRecord(e0, g_fg);
+            launch_bytes_md5((const uint8_t *)d, doff, dlen, ntr, dmd5, g_fg);
+            hipEventRecord(e1, g_fg);
+            hipDeviceSynchronize();
+            float ms = 0, bms = 0;
+            hipEventElapsedTime(&ms, e0, e1);
+            hipEventElapsedTime(&bms, b0, b1);
+            printf("loaded(lds=%d, busy %.1f ms) %-20s %8.3f ms  %7.1f ns/block\n", lr, bms,
+                   "wave pair (shipped)", ms, ms * 1e6 / nb);
+            const float m0 = run_loaded<0>(d, ntr, nb, out, lr);
+            printf("loaded(lds=%d) %-35s %8.3f ms  %7.1f ns/block\n", lr, "v0 single wave", m0,
+                   m0 * 1e6 / nb);
+        }
+    }
     for (size_t i = 0; i < sizeof(runs) / sizeof(runs[0]); ++i) {
         hipMemset(out, 0, ntr * 16);
         const float ms = runs[i].fn(d, ntr, nb, out);
