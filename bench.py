@@ -66,6 +66,8 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--inflight", type=int, default=3, choices=(2, 3),
+                    help="encode batches in flight (the engine keeps three slots)")
     ap.add_argument("--tracks", type=int, default=1024,
                     help="tracks per GPU (weak) or in total (strong)")
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
@@ -886,22 +888,26 @@ def main(argv=None):
     tracks = [(i * n_samples, n_samples) for i in range(n_tracks)]
     n_frames, out_cap = eng.bounds(opts, tracks, 2, 16)
     table = _atgpu.TrackTable(tracks)
-    # two output buffers: batch k+1 is enqueued before batch k is waited
-    # (atg_flac_encode_device_async), so batch k's MD5 chains and headers run
-    # under batch k+1's search; every batch is complete inside the clock
-    outs = [torch.empty(out_cap, dtype=torch.uint8, device=device) for _ in range(2)]
+    # `depth` output buffers: batch k is waited once batch k + depth - 1 is
+    # enqueued (atg_flac_encode_device_async), so batch k's MD5 chains and
+    # headers run under the next batches' search chains; every batch is
+    # complete inside the clock
+    depth = args.inflight
+    outs = [torch.empty(out_cap, dtype=torch.uint8, device=device) for _ in range(depth)]
     torch.cuda.synchronize()
     pending = []
 
     def step(k):
         t = eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16, 44100,
-                                    outs[k % 2].data_ptr(), out_cap)
-        r = eng.wait(pending.pop()) if pending else None
+                                    outs[k % depth].data_ptr(), out_cap)
         pending.append(t)
-        return r
+        return eng.wait(pending.pop(0)) if len(pending) >= depth else None
 
     def drain():
-        return eng.wait(pending.pop())
+        r = None
+        while pending:
+            r = eng.wait(pending.pop(0))
+        return r
 
     for k in range(args.warmup):
         step(k)
@@ -928,7 +934,7 @@ def main(argv=None):
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
-    out = outs[(args.steps - 1) % 2]
+    out = outs[(args.steps - 1) % depth]
     del outs
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     out_bytes = sum(int(r.bytes) for r in res)

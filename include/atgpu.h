@@ -140,12 +140,13 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
                                   uint64_t out_cap, atg_track_result *results);
 
 /* The same batch encode, enqueued: returns once the work is queued, with a
-   ticket for atg_flac_encode_wait.  The engine keeps two batches in flight
+   ticket for atg_flac_encode_wait.  The engine keeps three batches in flight
    (each its own device workspace): batch k's MD5 chains and stream headers
-   run on their own stream while batch k+1's analysis runs, so a caller that
-   waits for ticket k after enqueueing k+1 overlaps them.  d_pcm and d_out
-   must stay untouched until the ticket is waited; enqueueing a third batch
-   drains the oldest (its results stay readable until its slot is reused). */
+   run on their own stream while batches k+1 and k+2 are analysed, so a
+   caller that waits for ticket k after enqueueing k+2 (or k+1) overlaps
+   them.  d_pcm and d_out must stay untouched until the ticket is waited;
+   enqueueing a fourth batch drains the oldest (its results stay readable
+   until its slot is reused). */
 atg_status atg_flac_encode_device_async(atg_engine *eng, const atg_flac_options *opts,
                                         const void *d_pcm, atg_pcm_format format,
                                         const atg_track *tracks, uint32_t n_tracks,

@@ -144,10 +144,15 @@ struct EncSlot {
     float times[kNumTimed] = {};
 };
 
+// batches in flight on an engine (each its own device workspace): the MD5
+// chains of a batch run ~12 ms, longer than a batch's search chain, so a
+// third slot keeps them off the critical path at normal wave priority
+constexpr uint64_t kEncSlots = 3;
+
 struct atg_engine {
     int device = 0;
     hipStream_t s_main = nullptr;
-    EncSlot slot[2];
+    EncSlot slot[kEncSlots];
     DevBuf windows;
     // host-memory API: per slot, device PCM/image buffers and pinned host
     // staging, plus copy streams, so chunk c's upload, chunk c-1's download
@@ -516,7 +521,9 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     HIP_TRY(hipEventRecord(ev[14], e->s_main));
     // development switch: ATG_MD5_AT=1 starts the MD5 chains with the batch
     // (before the LPC kernel) instead of after it
-    static const bool md5_first = getenv("ATG_MD5_AT") && atoi(getenv("ATG_MD5_AT")) == 1;
+    // (ATG_MD5_AT=2 skips them: timing experiments only, the digests are not set)
+    static const int md5_at = getenv("ATG_MD5_AT") ? atoi(getenv("ATG_MD5_AT")) : 0;
+    static const bool md5_first = md5_at == 1;
     if (md5_first) {
         HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_tables, 0));
         HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
@@ -532,7 +539,11 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
     // so a SIMD shared with a chain would leave straggler waves; the search
     // and pack grids are deep enough to absorb them
-    if (!md5_first) {
+    if (md5_at == 2) {
+        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    }
+    if (md5_at == 0) {
         HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
         HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
         HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
@@ -710,7 +721,7 @@ atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *t
 atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 {
     ticket = e->next_ticket++;
-    EncSlot &sl = e->slot[ticket & 1u];
+    EncSlot &sl = e->slot[ticket % kEncSlots];
     if (sl.busy) {
         sl.status = finish_batch(e, sl);
         sl.error = g_err;
@@ -726,7 +737,7 @@ atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 // results of ticket t (waits if still running)
 atg_status wait_ticket(atg_engine *e, uint64_t t, EncSlot *&out)
 {
-    EncSlot &sl = e->slot[t & 1u];
+    EncSlot &sl = e->slot[t % kEncSlots];
     if (sl.ticket != t || (!sl.busy && !sl.done))
         return fail(ATG_ERR_INVALID, "unknown or expired encode ticket");
     if (sl.busy) {

@@ -16,6 +16,7 @@
 // concurrently with the encoder kernels (it occupies a handful of SIMDs).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "flac_dev.h"
 #include "launch.h"
@@ -223,6 +224,64 @@ __device__ __forceinline__ void md5_load_unit(const Md5Pair &pr, uint32_t slot, 
         x[k] = pr.ring[slot][k][lane];
 }
 
+// one block b = u / 2 of the hasher: half 0 from cur while unit u + 1 is
+// loaded into nxt, half 1 from nxt while unit u + 2 (MORE) is loaded into
+// cur; the prod counter is read before each speculative load and checked
+// after the half it overlaps
+template <bool ON_ALL, bool MORE>
+__device__ __forceinline__ void md5_hasher_block(uint32_t b, uint32_t full, uint32_t h[4],
+                                                 Md5Pair &pr, int lane, uint32_t &slot,
+                                                 uint4 (&cur)[8], uint4 (&nxt)[8])
+{
+    const bool on = ON_ALL || b < full;
+    const uint32_t u = 2u * b;
+    const uint32_t s1 = slot == 2u ? 0u : slot + 1u, s2 = s1 == 2u ? 0u : s1 + 1u;
+    uint32_t v[4] = {h[0], h[1], h[2], h[3]};
+    uint32_t p = md5_ctr(&pr.prod);
+    asm volatile("" ::: "memory");
+    md5_load_unit(pr, s1, lane, nxt);
+    if (on)
+        md5_half_xt<0>(v, cur);
+    if (p < u + 2u) {
+        md5_wait(&pr.prod, u + 2u);
+        md5_load_unit(pr, s1, lane, nxt);
+    }
+    md5_publish(&pr.cons, u + 2u); // units <= u + 1 read
+    if (MORE) {
+        p = md5_ctr(&pr.prod);
+        asm volatile("" ::: "memory");
+        md5_load_unit(pr, s2, lane, cur);
+    }
+    if (on) {
+        md5_half_xt<1>(v, nxt);
+        h[0] += v[0];
+        h[1] += v[1];
+        h[2] += v[2];
+        h[3] += v[3];
+    }
+    if (MORE) {
+        if (p < u + 3u) {
+            md5_wait(&pr.prod, u + 3u);
+            md5_load_unit(pr, s2, lane, cur);
+        }
+        md5_publish(&pr.cons, u + 3u);
+    }
+    slot = s2;
+}
+
+template <bool ON_ALL>
+__device__ __forceinline__ void md5_hasher(uint32_t full, uint32_t nbmax, uint32_t h[4],
+                                           Md5Pair &pr, int lane)
+{
+    uint4 cur[8], nxt[8];
+    md5_wait(&pr.prod, 1u);
+    md5_load_unit(pr, 0u, lane, cur);
+    uint32_t slot = 0; // slot of unit 2b
+    for (uint32_t b = 0; b + 1u < nbmax; ++b)
+        md5_hasher_block<ON_ALL, true>(b, full, h, pr, lane, slot, cur, nxt);
+    md5_hasher_block<ON_ALL, false>(nbmax - 1u, full, h, pr, lane, slot, cur, nxt);
+}
+
 // Whole blocks [0, full) of the lane's 16-byte aligned stream q, on the
 // wave pair (threadIdx.x >> 6: 0 hasher, 1 helper; both call this with the
 // same lane -> stream mapping and the same wave-uniform nbmax = max full,
@@ -275,52 +334,23 @@ __device__ __forceinline__ void md5_pair_blocks(const uint4 *__restrict__ q, uin
                 }
             }
         }
+    } else if (wave_all(full == nbmax)) {
+        md5_hasher<true>(full, nbmax, h, pr, lane); // every lane hashes every block
     } else {
-        uint4 cur[8], nxt[8];
-        md5_wait(&pr.prod, 1u);
-        md5_load_unit(pr, 0u, lane, cur);
-        uint32_t slot = 0; // slot of unit 2b
-        for (uint32_t b = 0; b < nbmax; ++b) {
-            const bool on = b < full;
-            const uint32_t u = 2u * b;
-            const uint32_t s1 = slot == 2u ? 0u : slot + 1u, s2 = s1 == 2u ? 0u : s1 + 1u;
-            uint32_t v[4] = {h[0], h[1], h[2], h[3]};
-            // half 0 (unit u from cur); unit u + 1 loaded meanwhile
-            uint32_t p = md5_ctr(&pr.prod);
-            asm volatile("" ::: "memory");
-            md5_load_unit(pr, s1, lane, nxt);
-            if (on)
-                md5_half_xt<0>(v, cur);
-            if (p < u + 2u) {
-                md5_wait(&pr.prod, u + 2u);
-                md5_load_unit(pr, s1, lane, nxt);
-            }
-            md5_publish(&pr.cons, u + 2u); // units <= u + 1 read
-            // half 1 (unit u + 1 from nxt); unit u + 2 loaded meanwhile
-            const bool more = b + 1u < nbmax;
-            if (more) {
-                p = md5_ctr(&pr.prod);
-                asm volatile("" ::: "memory");
-                md5_load_unit(pr, s2, lane, cur);
-            }
-            if (on) {
-                md5_half_xt<1>(v, nxt);
-                h[0] += v[0];
-                h[1] += v[1];
-                h[2] += v[2];
-                h[3] += v[3];
-            }
-            if (more) {
-                if (p < u + 3u) {
-                    md5_wait(&pr.prod, u + 3u);
-                    md5_load_unit(pr, s2, lane, cur);
-                }
-            }
-            if (more)
-                md5_publish(&pr.cons, u + 3u);
-            slot = s2;
-        }
+        md5_hasher<false>(full, nbmax, h, pr, lane);
     }
+}
+
+// The pair's waves allocate 192 VGPRs.  A lone hash chain issues about as
+// often as half a SIMD, so the waves beside it split the other half: at 192
+// VGPRs at most one LPC wave (184), two search waves (120) or one pack wave
+// (256) fit beside a chain -- each then gets the issue share it has on a
+// SIMD of its own kernel, and none straggles.  At 128 VGPRs two LPC waves
+// shared a chain's SIMD at a quarter of the issue each and the LPC kernel
+// ran 2.2 ms instead of 1.3 ms beside the chains.
+__device__ __forceinline__ void md5_vgpr_192()
+{
+    asm volatile("" ::: "v191");
 }
 
 // zero the pair's counters, then meet once
@@ -457,11 +487,11 @@ __device__ __forceinline__ bool md5_track_raw(const FlacParams &p, const TrackIn
 // tracks); the state goes to tout[t].md5 for k_track_md5
 __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int16_t *__restrict__ pcm,
                                                         const TrackInfo *__restrict__ tracks,
-                                                        TrackOut *__restrict__ tout)
+                                                        TrackOut *__restrict__ tout, int prio)
 {
-    // the hash chains are the longest serial path of a batch: let their
-    // waves issue ahead of the encoder kernels sharing the SIMD
-    __builtin_amdgcn_s_setprio(3);
+    // prio: the chains' waves issue ahead of the kernels sharing their SIMDs
+    if (prio)
+        __builtin_amdgcn_s_setprio(3);
     __shared__ Md5Pair pair_lds;
     const uint32_t t = blockIdx.x * 64u + (threadIdx.x & 63u);
     const bool valid = t < p.n_tracks;
@@ -472,6 +502,7 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
     if (!nbmax)
         return;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    md5_vgpr_192();
     md5_pair_init(pair_lds);
     md5_pair_blocks((const uint4 *)(pcm + ti.pcm_start * p.channels), raw ? (uint32_t)full : 0u,
                     nbmax, h, pair_lds);
@@ -552,6 +583,7 @@ __global__ __launch_bounds__(128) void k_bytes_md5_pair(const uint8_t *__restric
     if (!nbmax)
         return;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    md5_vgpr_192();
     md5_pair_init(pair_lds);
     md5_pair_blocks((const uint4 *)(base + off[valid ? t : 0u]), pair ? (uint32_t)full : 0u, nbmax,
                     h, pair_lds);
@@ -610,9 +642,13 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
         return hipSuccess;
     const dim3 grid((p.n_tracks + 63u) / 64u);
     const int paired = fmt == 0 && p.bps == 16u;
+    // ATG_MD5_PRIO=1: the chains at raised wave priority (a development
+    // switch; the engine keeps three batches in flight so the chains run at
+    // normal priority without reaching the critical path)
+    static const int prio = getenv("ATG_MD5_PRIO") ? atoi(getenv("ATG_MD5_PRIO")) : 0;
     if (paired)
         hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
-                           tout);
+                           tout, prio);
     if (fmt == 0)
         hipLaunchKernelGGL((k_track_md5<int16_t>), grid, dim3(64), 0, s, p,
                            (const int16_t *)pcm, tracks, tout, paired);

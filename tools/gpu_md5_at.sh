@@ -1,11 +1,13 @@
 #!/bin/bash
-# MD5 placement experiment: encoder-only bench with the MD5 chains after the
-# LPC kernel (default) and at the start of the batch (ATG_MD5_AT=1).
+# MD5 placement experiment (encoder leg): ATG_MD5_AT = 0 after the LPC
+# kernel (product), 1 at the start of the batch, 2 skipped (timing only).
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p "$R/gpurun_out"
+mkdir -p "$R/gpurun_out/at"
 cd "$R"
-timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-decode --no-chain --no-host --no-cpu-baseline \
-    > gpurun_out/bench_at0.log 2>&1
-ATG_MD5_AT=1 timeout -k 10 300 python -u bench.py --steps 10 --warmup 3 --no-decode --no-chain --no-host \
-    --no-cpu-baseline > gpurun_out/bench_at1.log 2>&1
+ARGS="--steps 30 --warmup 3 --no-cpu-baseline --no-verify --no-decode --no-chain --no-host"
+for k in 1 2; do
+    for a in ${AT_LIST:-0 1 2}; do
+        ATG_MD5_AT=$a timeout -k 10 200 python -u bench.py $ARGS > gpurun_out/at/at${a}_$k.log 2>&1
+    done
+done

@@ -240,7 +240,33 @@ static float run(const uint4 *d, uint32_t ntr, uint32_t nb, uint32_t *out)
     return ms;
 }
 
+// shader clock (s_memtime ticks per s_memrealtime 100 MHz tick) while the
+// rest of the GPU is idle or busy: one wave spinning ~2 ms
+__global__ void k_clock(unsigned long long *out)
+{
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime(), r0 = __builtin_amdgcn_s_memrealtime();
+    unsigned long long r = r0;
+    while (r - r0 < 200000ull)
+        r = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    if (threadIdx.x == 0) {
+        out[0] = t1 - t0;
+        out[1] = r - r0;
+    }
+}
+
 static hipStream_t g_bg = nullptr, g_fg = nullptr;
+
+static void clock_probe(const char *what)
+{
+    unsigned long long *d, h[2];
+    hipMalloc(&d, 16);
+    hipLaunchKernelGGL(k_clock, dim3(1), dim3(64), 0, g_fg, d);
+    hipStreamSynchronize(g_fg);
+    hipMemcpy(h, d, 16, hipMemcpyDeviceToHost);
+    printf("shader clock %-28s %.0f MHz\n", what, 100.0 * (double)h[0] / (double)h[1]);
+    hipFree(d);
+}
 static uint32_t *g_sink = nullptr;
 
 // MD5 variant V timed on its own stream while k_busy fills the GPU
@@ -252,7 +278,7 @@ static float run_loaded(const uint4 *d, uint32_t ntr, uint32_t nb, uint32_t *out
     hipEvent_t e0, e1;
     hipEventCreate(&e0);
     hipEventCreate(&e1);
-    hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 1200u, lds_reads);
+    hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 4000u, lds_reads);
     hipEventRecord(e0, g_fg);
     hipLaunchKernelGGL((k_md5<V, false>), grid, dim3(64), 0, g_fg, d, ntr, nb, out);
     hipEventRecord(e1, g_fg);
@@ -332,6 +358,10 @@ int main(int argc, char **argv)
         hipMalloc(&dmd5, ntr * 16);
         hipMemcpy(doff, off.data(), ntr * 8, hipMemcpyHostToDevice);
         hipMemcpy(dlen, len.data(), ntr * 8, hipMemcpyHostToDevice);
+        clock_probe("(GPU idle)");
+        hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 4000u, 1);
+        clock_probe("(K2-shaped load)");
+        hipDeviceSynchronize();
         for (int lr = 0; lr < 2; ++lr) {
             hipEvent_t e0, e1;
             hipEventCreate(&e0);
@@ -340,7 +370,7 @@ int main(int argc, char **argv)
             hipEventCreate(&b0);
             hipEventCreate(&b1);
             hipEventRecord(b0, g_bg);
-            hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 1200u, lr);
+            hipLaunchKernelGGL(k_busy, dim3(256 * 8 * 4), dim3(256), 0, g_bg, g_sink, 4000u, lr);
             hipEventRecord(b1, g_bg);
             hipEventRecord(e0, g_fg);
             launch_bytes_md5((const uint8_t *)d, doff, dlen, ntr, dmd5, g_fg);
