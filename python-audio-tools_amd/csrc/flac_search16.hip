@@ -291,6 +291,28 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
     sabs = sa + (uint32_t)ATG_RUN;
 }
 
+// A lower bound on the Rice-coded bits of the wave's residuals under any
+// partitioning: a lane's cnt codes with parameter k cost cnt (1 + k) +
+// sum floor(u / 2^k) >= cnt k + (U + cnt) / 2^k (U = sum u), whose minimum
+// over real k is cnt log2((U + cnt) ln2 / cnt) + cnt / ln2 (k = 0 when that
+// log is negative: U + cnt); a coarser partition shares one k between lanes
+// and costs at least the lanes' minima.  U >= 2 sum|r| - cnt (u = 2|r| or
+// 2|r| - 1).  fp32 with a 4-bit margin per lane (sum|r| < 2^25 rounds by at
+// most 2 in U).  Jobs are compared on exact bits; this only skips the
+// partition search of a predictor that cannot win (flac.c:1326-1505 picks
+// the smallest exact total, so one whose bound exceeds a finished total
+// cannot be chosen).
+#define K2F_PRUNED 0x3FFFFFFFu
+__device__ __forceinline__ uint32_t residual_lb(uint32_t lane_sum, uint32_t cnt)
+{
+    const float cf = (float)cnt;
+    const float U = fmaxf(2.0f * (float)lane_sum - cf, 0.0f);
+    const float x = (U + cf) * 0.69314718f / cf;
+    const float lb = x >= 1.0f ? cf * __log2f(x) + cf * 1.44269504f : U + cf;
+    const uint32_t lbi = (uint32_t)fmaxf(lb - 4.0f, 0.0f);
+    return dpp_wave_sum<uint32_t>(lbi);
+}
+
 struct Eval16 {
     uint32_t bits; // residual section bits
     PartSel sel;
@@ -304,7 +326,7 @@ struct Eval16 {
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
                                             const uint32_t (&cw)[7], int order, int sh,
-                                            uint32_t w)
+                                            uint32_t w, uint32_t thr)
 {
     int cq[14];
     if (TWO) {
@@ -378,6 +400,16 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
 #endif
     }
     Eval16 ev;
+    if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
+        // cannot beat a finished LPC job: no partition search, no exact bits
+        ev.bits = K2F_PRUNED;
+        ev.sel.porder = 0;
+        ev.sel.method = 0;
+        ev.sel.k_lane = 0;
+        ev.sel.k_own = 0;
+        ev.sel.hdr_bits = 0;
+        return ev;
+    }
 #if ATG_K2F_EXP == 3
     ev.sel.porder = 6; ev.sel.method = 0; ev.sel.k_own = ev.sel.k_lane = (lane_sum >> 6) & 7u;
     ev.sel.hdr_bits = 262;
@@ -540,6 +572,7 @@ struct CandInfo {
 // (partition header included), partition order, coding method and every
 // lane's Rice parameter
 struct PredRes {
+    uint32_t best_lpc; // smallest LPC subframe total of the finished jobs
     uint32_t bits[K2F_MAXPRED];
     uint8_t porder[K2F_MAXPRED];
     uint8_t method[K2F_MAXPRED];
@@ -666,11 +699,23 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
                              (1ull << 31) &&
                          (!TWO || shift <= 14);
     const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
+    // LPC jobs: the subframe total is hdr + the residual section; a job
+    // whose residual bound exceeds (best finished total - hdr) is skipped
+    const uint32_t wf = ci.w ? ci.w + 1u : 1u;
+    const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
+    uint32_t thr = 0xFFFFFFFFu;
+    if (!is_fixed) {
+        const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+        if (best != 0xFFFFFFFFu)
+            thr = best > hdr ? best - hdr : 0u;
+    }
     Eval16 ev;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w);
+        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr);
     else
         ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
+    if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)
+        atomicMin(&res->best_lpc, hdr + ev.bits);
     res->k[pi][lane] = (uint8_t)ev.sel.k_own;
     if (lane == 0) {
         res->bits[pi] = ev.bits;
@@ -958,6 +1003,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
         else
             cand_prepare<false>(p, unit, sbps, img + cand * PK_WORDS, cs, lane, est_tab,
                                 out + unit, &info[cand]);
+        if (lane == 0)
+            res[cand].best_lpc = 0xFFFFFFFFu;
     }
     __syncthreads();
 
@@ -1105,12 +1152,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
     }
     __syncthreads();
     cand_prepare<false>(p, unit, sbps, pk, cs, lane, est_tab, out + unit, &info);
+    if (lane == 0)
+        res.best_lpc = 0xFFFFFFFFu;
     __syncthreads();
     const CandInfo ci = load_info(&info);
     if (!ci.active)
         return;
     const uint32_t n_pred = n_pred_of(p, ci);
-    for (uint32_t pi = 0; pi < n_pred; ++pi)
+    // highest orders first: their totals prune the lower orders
+    for (uint32_t pi = n_pred; pi-- > 0;)
         pred_job<false>(p, N, pk, ci, pi, lane, (const int16_t *)lq32, (const int8_t *)ls32, &res);
     __syncthreads();
     cand_finish(p, N, ci, &res, lane, (const int16_t *)lq32, (const int8_t *)ls32, out + unit);
