@@ -634,7 +634,7 @@ class Decoder(object):
         return [res[i] for i in range(n)], dp.value, ns.value
 
     def decode_device_async(self, d_data, nbytes, tracks):
-        """enqueue a device-resident batch (two may be in flight) -> ticket;
+        """enqueue a device-resident batch (three may be in flight) -> ticket;
         d_data must stay valid until decode_wait(ticket)"""
         n = len(tracks)
         arr = (DecTrack * max(1, n))(*tracks)
