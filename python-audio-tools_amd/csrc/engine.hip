@@ -136,6 +136,13 @@ struct EncSlot {
     uint32_t *err_h = nullptr;       // pinned
     size_t err_cap = 0;
     bool want_fdesc = false;
+    // the batch's second MD5 part, stream headers and result copies are
+    // enqueued one batch later (after the next batch's LPC kernel), or when
+    // the batch is waited: batch_end()
+    bool end_pending = false;
+    const void *pend_pcm = nullptr;
+    int pend_fmt = 0;
+    uint8_t *pend_out = nullptr;
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
     uint64_t ticket = 0;
@@ -446,6 +453,41 @@ hipError_t ensure_pinned(T *&p, size_t &cap, size_t n)
     return e;
 }
 
+// The tail of a batch on its slot's stream: MD5 part 1 (+ the lane-per-
+// track finishing kernel), then, once the pack is done, the stream headers
+// and the results to pinned host memory.  `after`: an event the MD5 part
+// waits for (the next batch's LPC kernel), or none.
+atg_status batch_end(atg_engine *e, EncSlot &sl, hipEvent_t after)
+{
+    const Plan &pl = *sl.plan;
+    const FlacParams &p = pl.p;
+    const size_t nf = pl.frames.size(), nt = pl.tracks.size();
+    const TrackInfo *dtr = (const TrackInfo *)sl.tracks.p;
+    TrackOut *dto = (TrackOut *)sl.tout.p;
+    uint32_t *derr = (uint32_t *)sl.err.p;
+    hipEvent_t *ev = sl.ev;
+    sl.end_pending = false;
+    if (after)
+        HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
+    HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    // headers once both the pack and the MD5 chains are done
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
+    HIP_TRY(hipEventRecord(ev[12], sl.s_aux));
+    HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[13], sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[15], sl.s_aux));
+    if (nt)
+        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost,
+                               sl.s_aux));
+    if (sl.want_fdesc && nf)
+        HIP_TRY(hipMemcpyAsync(sl.fdesc_h, sl.fdesc.p, nf * sizeof(FrameDesc),
+                               hipMemcpyDeviceToHost, sl.s_aux));
+    HIP_TRY(hipMemcpyAsync(sl.err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.s_aux));
+    HIP_TRY(hipEventRecord(sl.ev_done, sl.s_aux));
+    return ATG_OK;
+}
+
 // Enqueue one batch on slot `sl`: the search chain on the engine's main
 // stream, the MD5 chains from the start of the batch and the stream headers
 // on the slot's aux stream, then the results back to pinned host memory.
@@ -519,17 +561,6 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     hipEvent_t *ev = sl.ev;
 
     HIP_TRY(hipEventRecord(ev[14], e->s_main));
-    // development switch: ATG_MD5_AT=1 starts the MD5 chains with the batch
-    // (before the LPC kernel) instead of after it
-    // (ATG_MD5_AT=2 skips them: timing experiments only, the digests are not set)
-    static const int md5_at = getenv("ATG_MD5_AT") ? atoi(getenv("ATG_MD5_AT")) : 0;
-    static const bool md5_first = md5_at == 1;
-    if (md5_first) {
-        HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_tables, 0));
-        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
-        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
-    }
     HIP_TRY(hipEventRecord(ev[0], e->s_main));
     HIP_TRY(launch_lpc_analyze(p, d_pcm, fmt, dfr, (const double *)e->windows.p,
                                (int16_t *)sl.coef.p, (int8_t *)sl.shift.p, (uint8_t *)sl.est.p,
@@ -539,16 +570,13 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
     // so a SIMD shared with a chain would leave straggler waves; the search
     // and pack grids are deep enough to absorb them
-    if (md5_at == 2) {
-        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
-    }
-    if (md5_at == 0) {
-        HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
-        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, sl.s_aux));
-        HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
-    }
+    // MD5 chains, part 0 (the first half of every track's blocks) on the
+    // slot's stream once the LPC kernel is done; part 1 follows after the
+    // next batch's LPC kernel (batch_end), so no chain runs beside an LPC
+    // grid
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
+    HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, 0, sl.s_aux));
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
     if (pl.big)
         HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
@@ -597,24 +625,21 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     }
     HIP_TRY(hipEventRecord(ev[9], e->s_main));
     HIP_TRY(hipEventRecord(sl.ev_pack, e->s_main));
-    // headers once both the pack and the MD5 chains are done, on the aux
-    // stream: the main stream goes on with the next batch meanwhile
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
-    HIP_TRY(hipEventRecord(ev[12], sl.s_aux));
-    HIP_TRY(launch_stream_header(p, dtr, dto, d_out, sl.s_aux));
-    HIP_TRY(hipEventRecord(ev[13], sl.s_aux));
-    HIP_TRY(hipEventRecord(ev[15], sl.s_aux));
-    if (nt)
-        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost,
-                               sl.s_aux));
-    if (want_fdesc && nf)
-        HIP_TRY(hipMemcpyAsync(sl.fdesc_h, sl.fdesc.p, nf * sizeof(FrameDesc),
-                               hipMemcpyDeviceToHost, sl.s_aux));
-    HIP_TRY(hipMemcpyAsync(sl.err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.s_aux));
-    HIP_TRY(hipEventRecord(sl.ev_done, sl.s_aux));
     sl.uploaded = &pl;
     sl.plan = plp;
     sl.want_fdesc = want_fdesc;
+    sl.end_pending = true;
+    sl.pend_pcm = d_pcm;
+    sl.pend_fmt = fmt;
+    sl.pend_out = d_out;
+    // the previous batches' second MD5 parts start now that this batch's
+    // LPC kernel is done
+    for (EncSlot &o : e->slot)
+        if (&o != &sl && o.end_pending) {
+            atg_status st2 = batch_end(e, o, ev[1]);
+            if (st2 != ATG_OK)
+                return st2;
+        }
     return ATG_OK;
 }
 
@@ -622,6 +647,11 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
 atg_status finish_batch(atg_engine *e, EncSlot &sl)
 {
     HIP_TRY(hipSetDevice(e->device));
+    if (sl.end_pending) {
+        atg_status st = batch_end(e, sl, nullptr);
+        if (st != ATG_OK)
+            return st;
+    }
     HIP_TRY(hipEventSynchronize(sl.ev_done));
     for (int k = 0; k < kNumTimed; ++k) {
         float ms = 0.f;

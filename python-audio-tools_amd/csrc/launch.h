@@ -62,8 +62,7 @@ hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
                              const uint32_t *crc8_tab /*[256]*/);
 // md5.hip
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
-                            const TrackInfo *tracks, TrackOut *tout,
-                            hipStream_t s);
+                            const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s);
 // MD5 of n byte streams base[off[t] .. off[t] + len[t]) (off 64-aligned),
 // digests to md5[16 t] (the decoder's STREAMINFO check)
 hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint64_t *len,

@@ -484,10 +484,15 @@ __device__ __forceinline__ bool md5_track_raw(const FlacParams &p, const TrackIn
 }
 
 // whole blocks of the raw tracks (a hasher + helper wave pair per 64
-// tracks); the state goes to tout[t].md5 for k_track_md5
+// tracks), in two parts: part 0 blocks [0, full / 2) from the initial
+// state, part 1 the rest from part 0's state; the state goes to tout[t].md5
+// (for part 1, then k_track_md5).  The engine runs the parts one batch
+// apart, beside the search and pack kernels of two batches, so no chain
+// runs beside the LPC kernel (whose two-waves-per-SIMD grid straggles when
+// a chain takes SIMD slots).
 __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int16_t *__restrict__ pcm,
                                                         const TrackInfo *__restrict__ tracks,
-                                                        TrackOut *__restrict__ tout, int prio)
+                                                        TrackOut *__restrict__ tout, int prio, int part)
 {
     // prio: the chains' waves issue ahead of the kernels sharing their SIMDs
     if (prio)
@@ -498,15 +503,19 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
     const TrackInfo ti = tracks[valid ? t : 0u];
     uint64_t full = 0;
     const bool raw = valid && md5_track_raw(p, ti, pcm, full);
-    const uint32_t nbmax = wave_max_u32(raw ? (uint32_t)full : 0u);
+    const uint32_t split = (uint32_t)(full / 2u);
+    const uint32_t b0 = part ? split : 0u, n = raw ? (part ? (uint32_t)full - split : split) : 0u;
+    const uint32_t nbmax = wave_max_u32(n);
     if (!nbmax)
         return;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (part && split && raw && threadIdx.x < 64u)
+        md5_get(tout[t].md5, h); // part 0's state (written for every lane with split > 0)
     md5_vgpr_192();
     md5_pair_init(pair_lds);
-    md5_pair_blocks((const uint4 *)(pcm + ti.pcm_start * p.channels), raw ? (uint32_t)full : 0u,
-                    nbmax, h, pair_lds);
-    if (threadIdx.x < 64u && raw)
+    md5_pair_blocks((const uint4 *)(pcm + ti.pcm_start * p.channels) + (size_t)b0 * 4u, n, nbmax,
+                    h, pair_lds);
+    if (threadIdx.x < 64u && n)
         md5_put(tout[t].md5, h);
 }
 
@@ -636,7 +645,7 @@ hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint
 }
 
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
-                            const TrackInfo *tracks, TrackOut *tout, hipStream_t s)
+                            const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s)
 {
     if (!p.n_tracks)
         return hipSuccess;
@@ -648,7 +657,9 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
     static const int prio = getenv("ATG_MD5_PRIO") ? atoi(getenv("ATG_MD5_PRIO")) : 0;
     if (paired)
         hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
-                           tout, prio);
+                           tout, prio, part);
+    if (part == 0)
+        return hipGetLastError();
     if (fmt == 0)
         hipLaunchKernelGGL((k_track_md5<int16_t>), grid, dim3(64), 0, s, p,
                            (const int16_t *)pcm, tracks, tout, paired);
