@@ -484,12 +484,13 @@ __device__ __forceinline__ bool md5_track_raw(const FlacParams &p, const TrackIn
 }
 
 // whole blocks of the raw tracks (a hasher + helper wave pair per 64
-// tracks), in two parts: part 0 blocks [0, full / 2) from the initial
+// tracks), in two parts: part 0 blocks [0, 3 full / 5) from the initial
 // state, part 1 the rest from part 0's state; the state goes to tout[t].md5
 // (for part 1, then k_track_md5).  The engine runs the parts one batch
 // apart, beside the search and pack kernels of two batches, so no chain
 // runs beside the LPC kernel (whose two-waves-per-SIMD grid straggles when
-// a chain takes SIMD slots).
+// a chain takes SIMD slots).  Part 0 (~7.3 ms) fits under a batch's search
+// and pack (~9 ms) with room; part 1 is what a last batch adds when waited.
 __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int16_t *__restrict__ pcm,
                                                         const TrackInfo *__restrict__ tracks,
                                                         TrackOut *__restrict__ tout, int prio, int part)
@@ -503,7 +504,7 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
     const TrackInfo ti = tracks[valid ? t : 0u];
     uint64_t full = 0;
     const bool raw = valid && md5_track_raw(p, ti, pcm, full);
-    const uint32_t split = (uint32_t)(full / 2u);
+    const uint32_t split = (uint32_t)(full * 3u / 5u);
     const uint32_t b0 = part ? split : 0u, n = raw ? (part ? (uint32_t)full - split : split) : 0u;
     const uint32_t nbmax = wave_max_u32(n);
     if (!nbmax)
