@@ -143,6 +143,7 @@ struct EncSlot {
     const void *pend_pcm = nullptr;
     int pend_fmt = 0;
     uint8_t *pend_out = nullptr;
+    bool pend_split = false;         // part 1 of a split MD5 chain still to run
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
     uint64_t ticket = 0;
@@ -158,6 +159,7 @@ constexpr uint64_t kEncSlots = 3;
 
 struct atg_engine {
     int device = 0;
+    bool sync_call = false; // inside atg_flac_encode_device (enqueue + wait)
     hipStream_t s_main = nullptr;
     EncSlot slot[kEncSlots];
     DevBuf windows;
@@ -467,9 +469,11 @@ atg_status batch_end(atg_engine *e, EncSlot &sl, hipEvent_t after)
     uint32_t *derr = (uint32_t *)sl.err.p;
     hipEvent_t *ev = sl.ev;
     sl.end_pending = false;
-    if (after)
-        HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
-    HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, sl.s_aux));
+    if (sl.pend_split) {
+        if (after)
+            HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
+        HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, sl.s_aux));
+    }
     HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
     // headers once both the pack and the MD5 chains are done
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
@@ -494,7 +498,7 @@ atg_status batch_end(atg_engine *e, EncSlot &sl, hipEvent_t after)
 // Returns without waiting.
 atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan> &plp,
                          const void *d_pcm, int fmt, uint8_t *d_out, uint64_t out_cap,
-                         bool want_fdesc, hipEvent_t wait_before = nullptr)
+                         bool want_fdesc, hipEvent_t wait_before = nullptr, bool pipelined = false)
 {
     Plan &pl = *plp;
     FlacParams &p = pl.p;
@@ -570,13 +574,15 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
     // so a SIMD shared with a chain would leave straggler waves; the search
     // and pack grids are deep enough to absorb them
-    // MD5 chains, part 0 (the first half of every track's blocks) on the
-    // slot's stream once the LPC kernel is done; part 1 follows after the
-    // next batch's LPC kernel (batch_end), so no chain runs beside an LPC
-    // grid
+    // MD5 chains on the slot's stream once the LPC kernel is done.  Split
+    // (pipelined device batches of 16-bit PCM): part 0 = 60 % of every
+    // track's blocks now, part 1 after the next batch's LPC kernel
+    // (batch_end), so no chain runs beside an LPC grid; otherwise the whole
+    // chain now (a caller waiting on each batch gains nothing from a split)
+    const bool split_md5 = pipelined && fmt == ATG_PCM_S16 && p.bps == 16u;
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, 0, sl.s_aux));
+    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
     if (pl.big)
         HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
@@ -632,6 +638,12 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     sl.pend_pcm = d_pcm;
     sl.pend_fmt = fmt;
     sl.pend_out = d_out;
+    sl.pend_split = split_md5;
+    if (!split_md5) {
+        atg_status st2 = batch_end(e, sl, nullptr);
+        if (st2 != ATG_OK)
+            return st2;
+    }
     // the previous batches' second MD5 parts start now that this batch's
     // LPC kernel is done
     for (EncSlot &o : e->slot)
@@ -903,7 +915,8 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
     st = take_slot(e, sl, t);
     if (st != ATG_OK)
         return st;
-    st = enqueue_batch(e, *sl, pl, d_pcm, (int)format, (uint8_t *)d_out, out_cap, false);
+    st = enqueue_batch(e, *sl, pl, d_pcm, (int)format, (uint8_t *)d_out, out_cap, false, nullptr,
+                       !e->sync_call);
     if (st != ATG_OK) {
         // nothing of this batch may be relied on: drain what was queued
         (void)hipStreamSynchronize(e->s_main);
@@ -939,8 +952,10 @@ atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
     if (!e || (!tracks && n_tracks) || (!results && n_tracks))
         return fail(ATG_ERR_INVALID, "NULL argument");
     uint64_t t = 0;
+    e->sync_call = true; // waited at once: no split MD5 chain
     atg_status st = atg_flac_encode_device_async(e, opts, d_pcm, format, tracks, n_tracks,
                                                  channels, bps, rate, d_out, out_cap, &t);
+    e->sync_call = false;
     if (st != ATG_OK)
         return st;
     return atg_flac_encode_wait(e, t, results);

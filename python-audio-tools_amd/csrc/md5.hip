@@ -504,13 +504,15 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
     const TrackInfo ti = tracks[valid ? t : 0u];
     uint64_t full = 0;
     const bool raw = valid && md5_track_raw(p, ti, pcm, full);
-    const uint32_t split = (uint32_t)(full * 3u / 5u);
-    const uint32_t b0 = part ? split : 0u, n = raw ? (part ? (uint32_t)full - split : split) : 0u;
+    // part 2: every block (an unsplit chain)
+    const uint32_t split = part == 2 ? 0u : (uint32_t)(full * 3u / 5u);
+    const uint32_t b0 = part == 1 ? split : 0u;
+    const uint32_t n = raw ? (part == 0 ? split : (uint32_t)full - split) : 0u;
     const uint32_t nbmax = wave_max_u32(n);
     if (!nbmax)
         return;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    if (part && split && raw && threadIdx.x < 64u)
+    if (part == 1 && split && raw && threadIdx.x < 64u)
         md5_get(tout[t].md5, h); // part 0's state (written for every lane with split > 0)
     md5_vgpr_192();
     md5_pair_init(pair_lds);
@@ -645,6 +647,8 @@ hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint
     return hipGetLastError();
 }
 
+// part 0 / 1: the two halves of a split chain (part 1 adds the finishing
+// kernel); part 2: the whole chain and the finishing kernel
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                             const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s)
 {
