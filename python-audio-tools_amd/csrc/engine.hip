@@ -923,6 +923,7 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
         (void)hipStreamSynchronize(sl->s_aux);
         sl->uploaded = nullptr;
         sl->ticket = 0;
+        sl->end_pending = false;
         return st;
     }
     sl->busy = true;
@@ -1121,6 +1122,7 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
             if (sl) {
                 sl->uploaded = nullptr;
                 sl->ticket = 0;
+                sl->end_pending = false;
             }
             return st;
         }
