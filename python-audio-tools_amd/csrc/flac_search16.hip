@@ -120,16 +120,35 @@ __device__ __forceinline__ void add3_acc(uint32_t &sa, uint32_t v, uint32_t s31)
     asm("v_add3_u32 %0, %0, %1, %2" : "+v"(sa) : "v"(v), "v"(s31));
 }
 
+// packed int16 L - R per half word (v_pk_sub_u16): the side channel's
+// packed words, exact when every |L - R| fits int16
+__device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, a) - __builtin_bit_cast(short2_t, b));
+}
+__device__ __forceinline__ uint4 load_run4(const uint32_t *__restrict__ p, bool subr)
+{
+    uint4 a = *(const uint4 *)p;
+    if (subr) {
+        const uint4 b = *(const uint4 *)(p + PK_WORDS);
+        a.x = pk_sub16(a.x, b.x);
+        a.y = pk_sub16(a.y, b.y);
+        a.z = pk_sub16(a.z, b.z);
+        a.w = pk_sub16(a.w, b.w);
+    }
+    return a;
+}
+
 // A lane's window over one packed image: words -8..15 of the current
 // 16-sample chunk (W) and their v_alignbit pairs (E).
 struct Win {
     uint32_t W[16], E[16];
 };
 
-__device__ __forceinline__ void win_init(const uint32_t *__restrict__ run, Win &x)
+__device__ __forceinline__ void win_init(const uint32_t *__restrict__ run, Win &x, bool subr)
 {
-    const uint4 h0 = *(const uint4 *)(run - 12);
-    const uint4 h1 = *(const uint4 *)(run - 8);
+    const uint4 h0 = load_run4(run - 12, subr);
+    const uint4 h1 = load_run4(run - 8, subr);
     x.W[8] = h0.x; x.W[9] = h0.y; x.W[10] = h0.z; x.W[11] = h0.w;
     x.W[12] = h1.x; x.W[13] = h1.y; x.W[14] = h1.z; x.W[15] = h1.w;
 #pragma unroll
@@ -165,17 +184,19 @@ __device__ __forceinline__ uint32_t win_pair(const Win &x, int ii, int j)
 // warm-up samples (lane0 && i < order) are forced to n = -1 (v = 0,
 // |r| = 0).  shv: the total shift sh + w, in a VGPR (a shift by an SGPR
 // operand issues at half the rate on gfx950, tools/int_rate.hip).
+// subr: run is the L image and the samples are L - R (the side channel
+// of a frame whose |S| fits int16), packed on the fly from the R image
 template <int D>
 __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const int (&cp)[14],
                                       int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
-                                      uint32_t &sabs)
+                                      uint32_t &sabs, bool subr)
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap pair in a VGPR
     Win A;
-    win_init(run, A);
+    win_init(run, A, subr);
     // chunk c + 1's words are read while chunk c is computed
-    uint4 n0 = *(const uint4 *)run, n1 = *(const uint4 *)(run + 4);
+    uint4 n0 = load_run4(run, subr), n1 = load_run4(run + 4, subr);
     uint32_t sa = 0;
 #pragma unroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
@@ -183,8 +204,8 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
         asm volatile("" ::: "memory");
         const uint4 a0 = n0, a1 = n1;
         if (c + 1 < ATG_RUN / 16) {
-            n0 = *(const uint4 *)(run + 8 * (c + 1));
-            n1 = *(const uint4 *)(run + 8 * (c + 1) + 4);
+            n0 = load_run4(run + 8 * (c + 1), subr);
+            n1 = load_run4(run + 8 * (c + 1) + 4, subr);
         }
         win_next(a0, a1, A);
         // two samples' tap chains interleaved: no dependent-issue bubble
@@ -326,10 +347,13 @@ struct Eval16 {
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
                                             const uint32_t (&cw)[7], int order, int sh,
-                                            uint32_t w, uint32_t thr)
+                                            uint32_t w, uint32_t thr, bool s16)
 {
+    // s16 (side channel, every |S| <= 32767): the packed path on L - R
+    // words formed on the fly -- 2 taps per v_dot2 instead of 1
+    const bool lr = TWO && !s16;
     int cq[14];
-    if (TWO) {
+    if (lr) {
         // (L, R) taps: (-2^sh, 2^sh), then (c_k, -c_k)
         cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
 #pragma unroll
@@ -358,7 +382,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     const int warm = lane0 ? order : 0;
     uint32_t u[ATG_RUN];
     uint32_t lane_sum; // sum |r| of the run
-    if (TWO) {
+    if (lr) {
 #if ATG_K2F_FEW
         // three tap counts only (zero taps past the order): a code image that
         // fits the instruction cache
@@ -382,20 +406,20 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     } else {
 #if ATG_K2F_FEW
         if (order < 4)
-            pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
+            pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
         else if (order < 8)
-            pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
+            pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
         else
-            pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
+            pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
 #else
         switch (order / 2 + 1) {
-        case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 3: pass1<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 4: pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 5: pass1<5>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 6: pass1<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        default: pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        case 3: pass1<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        case 4: pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        case 5: pass1<5>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        case 6: pass1<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
+        default: pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         }
 #endif
     }
@@ -711,7 +735,8 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     }
     Eval16 ev;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr);
+        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
+                            TWO && ci.amax <= 32767u);
     else
         ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
     if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)
