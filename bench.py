@@ -64,7 +64,7 @@ MAIN_STREAM = ("lpc_analyze", "subframe_search", "frame_decide", "track_scan",
 def parse_args(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--inflight", type=int, default=3, choices=(2, 3),
                     help="encode batches in flight (the engine keeps three slots)")
