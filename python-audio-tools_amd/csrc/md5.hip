@@ -583,9 +583,10 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
 __global__ __launch_bounds__(128) void k_bytes_md5_pair(const uint8_t *__restrict__ base,
                                                         const uint64_t *__restrict__ off,
                                                         const uint64_t *__restrict__ len, uint32_t n,
-                                                        uint8_t *__restrict__ md5)
+                                                        uint8_t *__restrict__ md5, int prio)
 {
-    __builtin_amdgcn_s_setprio(3);
+    if (prio)
+        __builtin_amdgcn_s_setprio(3);
     __shared__ Md5Pair pair_lds;
     const uint32_t t = blockIdx.x * 64u + (threadIdx.x & 63u);
     const bool valid = t < n;
@@ -642,7 +643,10 @@ hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint
     if (!n)
         return hipSuccess;
     const dim3 grid((n + 63u) / 64u);
-    hipLaunchKernelGGL(k_bytes_md5_pair, grid, dim3(128), 0, s, base, off, len, n, md5);
+    // ATG_DEC_MD5_PRIO=0: the decoder's chains at normal wave priority (a
+    // development switch)
+    static const int prio = getenv("ATG_DEC_MD5_PRIO") ? atoi(getenv("ATG_DEC_MD5_PRIO")) : 1;
+    hipLaunchKernelGGL(k_bytes_md5_pair, grid, dim3(128), 0, s, base, off, len, n, md5, prio);
     hipLaunchKernelGGL(k_bytes_md5, grid, dim3(64), 0, s, base, off, len, n, md5);
     return hipGetLastError();
 }
