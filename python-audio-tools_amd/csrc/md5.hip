@@ -596,7 +596,10 @@ __global__ __launch_bounds__(128) void k_bytes_md5_pair(const uint8_t *__restric
     if (!nbmax)
         return;
     uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
-    md5_vgpr_192();
+    // the decoder's kernels run few, long waves (a lane parses a whole frame):
+    // a chain wave takes a SIMD to itself (256 VGPRs + 256 AGPRs) so none
+    // of them shares its issue with a chain
+    asm volatile("" ::: "v255", "a255");
     md5_pair_init(pair_lds);
     md5_pair_blocks((const uint4 *)(base + off[valid ? t : 0u]), pair ? (uint32_t)full : 0u, nbmax,
                     h, pair_lds);
