@@ -18,6 +18,8 @@
 #include <stdint.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "flac_dev.h"
 #include "launch.h"
 #include "wave.h"
@@ -493,7 +495,8 @@ __device__ __forceinline__ bool md5_track_raw(const FlacParams &p, const TrackIn
 // and pack (~9 ms) with room; part 1 is what a last batch adds when waited.
 __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int16_t *__restrict__ pcm,
                                                         const TrackInfo *__restrict__ tracks,
-                                                        TrackOut *__restrict__ tout, int prio, int part)
+                                                        TrackOut *__restrict__ tout, int prio, int part,
+                                                        uint32_t split_pct)
 {
     // prio: the chains' waves issue ahead of the kernels sharing their SIMDs
     if (prio)
@@ -505,7 +508,7 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
     uint64_t full = 0;
     const bool raw = valid && md5_track_raw(p, ti, pcm, full);
     // part 2: every block (an unsplit chain)
-    const uint32_t split = part == 2 ? 0u : (uint32_t)(full * 3u / 5u);
+    const uint32_t split = part == 2 ? 0u : (uint32_t)(full * split_pct / 100u);
     const uint32_t b0 = part == 1 ? split : 0u;
     const uint32_t n = raw ? (part == 0 ? split : (uint32_t)full - split) : 0u;
     const uint32_t nbmax = wave_max_u32(n);
@@ -667,9 +670,12 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
     // switch; the engine keeps three batches in flight so the chains run at
     // normal priority without reaching the critical path)
     static const int prio = getenv("ATG_MD5_PRIO") ? atoi(getenv("ATG_MD5_PRIO")) : 0;
+    // share of the blocks in part 0 (ATG_MD5_SPLIT_PCT, development switch)
+    static const uint32_t split_pct =
+        getenv("ATG_MD5_SPLIT_PCT") ? (uint32_t)std::min(100, std::max(0, atoi(getenv("ATG_MD5_SPLIT_PCT")))) : 60u;
     if (paired)
         hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
-                           tout, prio, part);
+                           tout, prio, part, split_pct);
     if (part == 0)
         return hipGetLastError();
     if (fmt == 0)
