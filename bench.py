@@ -187,6 +187,33 @@ def cpu_model():
     return "unknown"
 
 
+def cpu_share():
+    """host CPUs this process may use: the affinity mask, the cgroup CPU
+    quota and the harness's stated share (OMP_NUM_THREADS is set to the
+    box's per-GPU CPU share) -> (threads to use, details)"""
+    info = {"os_cpu_count": os.cpu_count()}
+    n = os.cpu_count() or 1
+    try:
+        info["affinity"] = len(os.sched_getaffinity(0))
+        n = min(n, info["affinity"])
+    except (AttributeError, OSError):
+        pass
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            info["cgroup_quota_cpus"] = round(int(q) / int(per), 2)
+            n = min(n, max(1, int(int(q) // int(per))))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    if omp and omp.isdigit():
+        info["omp_num_threads"] = int(omp)
+        n = min(n, int(omp))
+    info["used"] = n
+    return n, info
+
+
 def _parallel(n_items, threads, fn):
     """run fn(i) for i < n_items on `threads` host threads (the work is
     ctypes / subprocess calls, which release the GIL); -> seconds"""
@@ -673,51 +700,107 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
            "alac_decode_samples": int(state["nsamp"]),
            "alac_first_bad_track": bad_track}
     if verify:
-        import oracle_port
-        oracle_port.load()
-        yh = y[:2 * n_out * ch].cpu().numpy()
-        sh = src[:2 * n_in * ch].cpu().numpy()
-        fh = flac.cpu().numpy()
-        rs_ok = fl_ok = True
-        t_rs = t_fl = 0.0
-        for k in range(min(2, n_tracks)):
-            t1 = time.perf_counter()
-            want = oracle_port.resample(sh[k * n_in * ch:(k + 1) * n_in * ch], ch, bps, rout / rin)
-            t_rs += time.perf_counter() - t1
-            rs_ok = rs_ok and np.array_equal(want, yh[k * n_out * ch:(k + 1) * n_out * ch])
-            t1 = time.perf_counter()
-            img, _ = oracle_port.encode(want, ch, bps, rout, **FLAC8)
-            t_fl += time.perf_counter() - t1
-            r = fres[k]
-            fl_ok = fl_ok and img == fh[r.out_offset:r.out_offset + r.bytes].tobytes()
-        k = min(2, n_tracks)
-        alac_h = alac.cpu().numpy()
-        ainfo = oracle_port.AlacInfo()
-        for f in ("max_samples_per_frame", "bits_per_sample", "history_multiplier",
-                  "initial_history", "maximum_k", "channels", "sample_rate", "total_frames"):
-            setattr(ainfo, f, getattr(info, f))
-        al_ok = True
-        t1 = time.perf_counter()
-        for j in range(k):
-            r = ares[j]
-            d = oracle_port.alac_decode(alac_h[r.out_offset:r.out_offset + r.bytes].tobytes(),
-                                        info=ainfo, start=8, remaining=n_in)
-            al_ok = al_ok and d["code"] == 0 and np.array_equal(
-                d["pcm"], sh[j * n_in * ch:(j + 1) * n_in * ch])
-        t_al = time.perf_counter() - t1
-        out["verified_alac_port_decode"] = al_ok
-        out["verified_resample_vs_oracle"] = rs_ok
-        out["verified_flac_vs_port"] = fl_ok
-        out["verified_tracks"] = k
-        out["cpu_baseline"] = {
-            "value": round(k * n_out / (t_rs + t_fl + t_al), 1), "unit": "frames/s",
-            "cores": 1, "kind": "port",
-            "sample": "%d tracks through the CPU restatements, 1 thread: resample %.1f s + "
-                      "FLAC-8 %.1f s + ALAC decode %.1f s" % (k, t_rs, t_fl, t_al)}
-        del yh, sh, fh, alac_h
+        out.update(chain_verify(args, threads, ch, bps, rin, rout, n_tracks, n_in, n_out, info,
+                                ares, fsb, fres, alac, src, y, flac))
     adec.close()
     eng.close()
     del src, alac, y, flac, ys, flacs
+    return out
+
+
+def chain_verify(args, threads, ch, bps, rin, rout, n_tracks, n_in, n_out, info, ares, fsb,
+                 fres, alac, src, y, flac):
+    """config-5 parity outside the timed region, EVERY track: the port
+    decodes each GPU-written ALAC track back to the source, resamples it
+    (oracle/resample_port.c) and FLAC-8 encodes that (oracle/flac_port.c);
+    the GPU's resampled PCM and FLAC image must equal the port's bit for
+    bit.  Then the CPU baseline: the reference's own ALAC decoder and FLAC
+    encoder (oracle/_ref/alacdec, flacenc) as processes around the resample
+    port (the reference's resampler is unbuildable: BEST table absent), one
+    track per worker like track2track -j N."""
+    import oracle_port
+    from audiotools import m4a
+    oracle_port.load()
+    yh = y.cpu().numpy()
+    sh = src.cpu().numpy()
+    fh = flac.cpu().numpy()
+    alac_h = alac.cpu().numpy()
+    ainfo = oracle_port.AlacInfo()
+    for f in ("max_samples_per_frame", "bits_per_sample", "history_multiplier",
+              "initial_history", "maximum_k", "channels", "sample_rate", "total_frames"):
+        setattr(ainfo, f, getattr(info, f))
+    bad = {"alac": [], "resample": [], "flac": []}
+
+    def one(k):
+        r = ares[k]
+        mdat = alac_h[r.out_offset:r.out_offset + r.bytes].tobytes()
+        d = oracle_port.alac_decode(mdat, info=ainfo, start=8, remaining=n_in)
+        x = sh[k * n_in * ch:(k + 1) * n_in * ch]
+        if d["code"] != 0 or not np.array_equal(d["pcm"], x):
+            bad["alac"].append(k)
+        want = oracle_port.resample(x, ch, bps, rout / rin)
+        if not np.array_equal(want, yh[k * n_out * ch:(k + 1) * n_out * ch]):
+            bad["resample"].append(k)
+        img, _ = oracle_port.encode(want, ch, bps, rout, **FLAC8)
+        fr = fres[k]
+        if img != fh[fr.out_offset:fr.out_offset + fr.bytes].tobytes():
+            bad["flac"].append(k)
+
+    dt = _parallel(n_tracks, threads, one)
+    out = {"verified_alac_port_decode": not bad["alac"],
+           "verified_resample_vs_oracle": not bad["resample"],
+           "verified_flac_vs_port": not bad["flac"],
+           "verified_tracks": n_tracks - len(set(sum(bad.values(), []))),
+           "verify_seconds": round(dt, 1)}
+    # CPU baseline: reference binaries where they exist
+    ref_ok = os.path.exists(oracle_port.REF_ALACDEC) and os.path.exists(oracle_port.REF_FLACENC)
+    nb = min(n_tracks, max(1, threads))
+    fargs = [oracle_port.REF_FLACENC, "-c", str(ch), "-r", str(rout), "-b", str(bps), "-B",
+             "4096", "-l", "12", "-P", "0", "-R", "6", "-m", "-e"]
+    imgs = []
+    if ref_ok:
+        for k in range(nb):
+            r = ares[k]
+            mdat = alac_h[r.out_offset:r.out_offset + r.bytes].tobytes()
+            sizes = [int(v) for v in fsb[r.first_frameset:r.first_frameset + r.n_framesets]]
+            imgs.append(m4a.m4a_file(ch, bps, rin, 4096, n_in, mdat, sizes, create_date=1))
+    same = []
+
+    def base(k):
+        if ref_ok:
+            with tempfile.TemporaryDirectory() as d:
+                fa = os.path.join(d, "a.m4a")
+                with open(fa, "wb") as f:
+                    f.write(imgs[k])
+                p = subprocess.run([oracle_port.REF_ALACDEC, fa], capture_output=True, check=True)
+                x = np.frombuffer(p.stdout, dtype=np.uint8).reshape(-1, 3)
+                x = (x[:, 0].astype(np.int32) | (x[:, 1].astype(np.int32) << 8) |
+                     (x[:, 2].astype(np.int8).astype(np.int32) << 16))
+                rs = oracle_port.resample(x, ch, bps, rout / rin)
+                raw = oracle_port.pcm_bytes(rs, bps)
+                fo = os.path.join(d, "o.flac")
+                subprocess.run(fargs + [fo], input=raw, stdout=subprocess.DEVNULL, check=True)
+                with open(fo, "rb") as f:
+                    img = f.read()
+        else:
+            x = sh[k * n_in * ch:(k + 1) * n_in * ch]
+            rs = oracle_port.resample(x, ch, bps, rout / rin)
+            img, _ = oracle_port.encode(rs, ch, bps, rout, **FLAC8)
+        fr = fres[k]
+        same.append(img == fh[fr.out_offset:fr.out_offset + fr.bytes].tobytes())
+
+    bdt = _parallel(nb, threads, base)
+    out["cpu_baseline"] = {
+        "value": round(nb * n_out / bdt, 1), "unit": "frames/s", "cores": threads,
+        "kind": "reference" if ref_ok else "port",
+        "sample": "%d tracks x %d s, one track per worker, %d workers, %.1f s: %s"
+                  % (nb, args.chain_seconds, threads, bdt,
+                     "reference alacdec + flacenc processes (built from the reference's "
+                     "src/decoders/alac.c, src/encoders/flac.c) around the resample port "
+                     "(the reference's BEST-table resampler is unbuildable)" if ref_ok else
+                     "CPU restatements (oracle/_ref absent)"),
+        "gpu_images_identical": all(same)}
+    del yh, sh, fh, alac_h
     return out
 
 
@@ -943,7 +1026,8 @@ def main(argv=None):
     if world > 1:
         total_frames = reduce_sum(torch, dist, total_frames, device)
 
-    threads = args.cpu_threads or min(16, os.cpu_count() or 1)
+    share, share_info = cpu_share()
+    threads = args.cpu_threads or share
     pcm_host = pcm.cpu().numpy()
     host_out = out.cpu().numpy()
     images = [host_out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res]
@@ -1053,6 +1137,7 @@ def main(argv=None):
             cpu["note"] = "oracle/_ref absent: port timing"
         cpu["cpu_model"] = cpu_model()
         cpu["host_cpus"] = os.cpu_count()
+        cpu["cpu_share"] = share_info
         cpu["port_1_thread"] = port1
         if port:
             cpu["port_n_threads"] = port

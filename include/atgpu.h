@@ -70,7 +70,7 @@ typedef enum {
    track is cut exactly as listed instead (the reference encodes whatever
    each pcmreader.read(block_size) call returns as one frame,
    src/encoders/flac.c:244-274); sizes must sum to pcm_frames and each be
-   1..4096. */
+   1..65535 (frames above 4096 samples take the large-frame kernels). */
 typedef struct {
     uint64_t pcm_offset; /* index of the track's first PCM frame */
     uint64_t pcm_frames; /* number of PCM frames (samples per channel) */
@@ -124,6 +124,11 @@ atg_status atg_flac_encode_host(atg_engine *eng, const atg_flac_options *opts,
                                 uint64_t *frame_offsets,
                                 uint32_t *frame_pcm_frames);
 
+/* PCM bytes per chunk of atg_flac_encode_host's pipeline (default 256 MiB):
+   consecutive tracks are grouped into chunks of about this much PCM, and
+   chunk c+1's upload, chunk c's encode and chunk c-1's download overlap. */
+atg_status atg_engine_set_host_chunk_bytes(atg_engine *eng, uint64_t bytes);
+
 /* Device-memory entry points run on the library's own non-blocking HIP
    streams: device inputs must be complete (e.g. the producing stream
    synchronized) when the call is made. */
@@ -144,9 +149,12 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
    (each its own device workspace): batch k's MD5 chains and stream headers
    run on their own stream while batches k+1 and k+2 are analysed, so a
    caller that waits for ticket k after enqueueing k+2 (or k+1) overlaps
-   them.  d_pcm and d_out must stay untouched until the ticket is waited;
-   enqueueing a fourth batch drains the oldest (its results stay readable
-   until its slot is reused). */
+   them.  d_pcm and d_out must stay untouched until the ticket is waited.
+   A fourth enqueue while three tickets are unwaited fails with
+   ATG_ERR_INVALID (wait the oldest first); atg_flac_encode_device takes a
+   slot too and fails the same way, and atg_flac_encode_host fails while any
+   ticket is unwaited.  A waited ticket's
+   results stay readable until its slot is reused three enqueues later. */
 atg_status atg_flac_encode_device_async(atg_engine *eng, const atg_flac_options *opts,
                                         const void *d_pcm, atg_pcm_format format,
                                         const atg_track *tracks, uint32_t n_tracks,

@@ -30,7 +30,7 @@ EXPORTS = (
     "atg_abi_version", "atg_last_error", "atg_engine_create",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
-    "atg_engine_kernel_times", "atg_device_alloc",
+    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_device_alloc",
     "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
@@ -254,6 +254,8 @@ def load_library():
         lib.atg_flac_encode_device_async.restype = ctypes.c_int
         lib.atg_flac_encode_wait.argtypes = [P, c_u64, ctypes.POINTER(TrackResult)]
         lib.atg_flac_encode_wait.restype = ctypes.c_int
+        lib.atg_engine_set_host_chunk_bytes.argtypes = [P, c_u64]
+        lib.atg_engine_set_host_chunk_bytes.restype = ctypes.c_int
         lib.atg_engine_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -522,6 +524,10 @@ class Engine(object):
         res = (TrackResult * max(1, n))()
         _check(self.lib, self.lib.atg_flac_encode_wait(self.handle, t, res))
         return [res[i] for i in range(n)]
+
+    def set_host_chunk_bytes(self, nbytes):
+        """PCM bytes per chunk of the host-memory pipeline (encode())"""
+        _check(self.lib, self.lib.atg_engine_set_host_chunk_bytes(self.handle, int(nbytes)))
 
     def kernel_times(self):
         names = (ctypes.c_char_p * 16)()

@@ -144,6 +144,8 @@ struct EncSlot {
     int pend_fmt = 0;
     uint8_t *pend_out = nullptr;
     bool pend_split = false;         // part 1 of a split MD5 chain still to run
+    atg_status end_status = ATG_OK;  // the batch end failed to queue: its wait reports this
+    std::string end_error;
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
     uint64_t ticket = 0;
@@ -459,7 +461,22 @@ hipError_t ensure_pinned(T *&p, size_t &cap, size_t n)
 // track finishing kernel), then, once the pack is done, the stream headers
 // and the results to pinned host memory.  `after`: an event the MD5 part
 // waits for (the next batch's LPC kernel), or none.
+atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after);
+
+// batch_end_queue, and if any of its HIP calls fails the slot's batch is
+// marked failed (its ev_done was never recorded, so a wait must not trust it)
 atg_status batch_end(atg_engine *e, EncSlot &sl, hipEvent_t after)
+{
+    sl.end_pending = false;
+    const atg_status st = batch_end_queue(e, sl, after);
+    if (st != ATG_OK) {
+        sl.end_status = st;
+        sl.end_error = g_err;
+    }
+    return st;
+}
+
+atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
 {
     const Plan &pl = *sl.plan;
     const FlacParams &p = pl.p;
@@ -468,7 +485,6 @@ atg_status batch_end(atg_engine *e, EncSlot &sl, hipEvent_t after)
     TrackOut *dto = (TrackOut *)sl.tout.p;
     uint32_t *derr = (uint32_t *)sl.err.p;
     hipEvent_t *ev = sl.ev;
-    sl.end_pending = false;
     if (sl.pend_split) {
         if (after)
             HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
@@ -633,6 +649,8 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     HIP_TRY(hipEventRecord(sl.ev_pack, e->s_main));
     sl.uploaded = &pl;
     sl.plan = plp;
+    sl.end_status = ATG_OK;
+    sl.end_error.clear();
     sl.want_fdesc = want_fdesc;
     sl.end_pending = true;
     sl.pend_pcm = d_pcm;
@@ -663,6 +681,12 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
         atg_status st = batch_end(e, sl, nullptr);
         if (st != ATG_OK)
             return st;
+    }
+    if (sl.end_status != ATG_OK) {
+        // ev_done was never recorded: drain the slot's streams, report the error
+        (void)hipStreamSynchronize(e->s_main);
+        (void)hipStreamSynchronize(sl.s_aux);
+        return fail(sl.end_status, sl.end_error);
     }
     HIP_TRY(hipEventSynchronize(sl.ev_done));
     for (int k = 0; k < kNumTimed; ++k) {
@@ -758,18 +782,15 @@ atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *t
     return ATG_OK;
 }
 
-// the slot for a new batch: the one after the last ticket's; a slot still
-// holding an unwaited batch is drained first (its results stay readable)
+// the slot for a new batch: the one after the last ticket's.  A slot still
+// holding an unwaited batch is never reused (its results would be lost):
+// the caller must wait the oldest ticket first, as with the decoder
 atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 {
+    EncSlot &sl = e->slot[e->next_ticket % kEncSlots];
+    if (sl.busy)
+        return fail(ATG_ERR_INVALID, "three encode batches already in flight: wait for the oldest");
     ticket = e->next_ticket++;
-    EncSlot &sl = e->slot[ticket % kEncSlots];
-    if (sl.busy) {
-        sl.status = finish_batch(e, sl);
-        sl.error = g_err;
-        sl.busy = false;
-        sl.done = true;
-    }
     sl.ticket = ticket;
     sl.done = false;
     out = &sl;
@@ -982,19 +1003,14 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
     const size_t elem = format == ATG_PCM_S16 ? 2 : 4;
     HIP_TRY(hipSetDevice(e->device));
-    // the slots' device state is reused below: drain any batch in flight
+    // the slots' device state is reused below: an unwaited async batch
+    // would lose its results
     for (EncSlot &s2 : e->slot)
-        if (s2.busy) {
-            s2.status = finish_batch(e, s2);
-            s2.error = g_err;
-            s2.busy = false;
-            s2.done = true;
-        }
+        if (s2.busy)
+            return fail(ATG_ERR_INVALID, "an async encode batch is in flight: wait for it first");
 
-    // chunks of consecutive tracks, ~chunk_bytes of PCM each (ATG_HOST_CHUNK_MB
-    // overrides the size, for tests)
-    if (const char *cb = std::getenv("ATG_HOST_CHUNK_MB"))
-        e->chunk_bytes = std::max<uint64_t>(1, std::strtoull(cb, nullptr, 10)) << 20;
+    // chunks of consecutive tracks, ~chunk_bytes of PCM each
+    // (atg_engine_set_host_chunk_bytes)
     struct Chunk {
         uint32_t t0, t1;          // tracks [t0, t1)
         uint64_t pcm0, samples;   // first sample and samples of the chunk's PCM span
@@ -1142,6 +1158,14 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
         if (st != ATG_OK)
             return st;
     }
+    return ATG_OK;
+}
+
+atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)
+{
+    if (!e || !bytes)
+        return fail(ATG_ERR_INVALID, "NULL engine or zero chunk size");
+    e->chunk_bytes = bytes;
     return ATG_OK;
 }
 

@@ -1114,9 +1114,9 @@ struct atg_decoder {
     DecSlot slot[2];
     uint64_t next_ticket = 1;
     int last = -1; // slot of the last waited batch (decode_fetch)
-    // frame table of the most recent batch (decode_fetch)
-    std::vector<DecTrack> tr;
-    uint64_t total_frames = 0;
+    // ticket of the newest enqueued batch: the shared device frame table
+    // (frames) belongs to it
+    uint64_t frames_ticket = 0;
 };
 
 static void build_dec_tables(uint8_t *t8, uint16_t t16[4][256])
@@ -1490,9 +1490,8 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
         DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
                             sl.s_md5));
     DHIP(hipEventRecord(sl.ev_done, sl.s_md5));
-    // the frame table belongs to the newest batch (decode_fetch)
-    d->tr = tr;
-    d->total_frames = fb;
+    // the device frame table now belongs to this batch (decode_fetch)
+    d->frames_ticket = sl.ticket;
     return ATG_OK;
 }
 
@@ -1645,7 +1644,7 @@ atg_status atg_flac_decode_host(atg_decoder *d, const uint8_t *data, uint64_t le
     if (total_samples)
         *total_samples = ts;
     if (total_frames)
-        *total_frames = d->total_frames;
+        *total_frames = d->slot[d->last].total_frames;
     return ATG_OK;
 }
 
@@ -1658,22 +1657,27 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
     if (d->last < 0)
         return dfail(ATG_ERR_INVALID, "no decoded batch");
     DecSlot &sl = d->slot[d->last];
-    if ((pcm && pcm_cap < sl.total_samples) ||
-        ((frame_offsets || frame_block_sizes) && frame_cap < d->total_frames))
+    const bool want_frames = frame_offsets || frame_block_sizes;
+    // the frame table lives in one device buffer shared by the slots: only
+    // the newest batch's is there
+    if (want_frames && sl.ticket != d->frames_ticket)
+        return dfail(ATG_ERR_INVALID, "frame table of the last waited batch was replaced by a "
+                                      "newer batch: fetch it before enqueueing another");
+    if ((pcm && pcm_cap < sl.total_samples) || (want_frames && frame_cap < sl.total_frames))
         return dfail(ATG_ERR_CAPACITY, "output buffer too small for the decoded batch");
     DHIP(hipSetDevice(d->device));
     if (pcm && sl.total_samples)
         DHIP(hipMemcpyAsync(pcm, sl.pcm.p, sizeof(int32_t) * sl.total_samples,
                             hipMemcpyDeviceToHost, d->s));
     std::vector<DecFrame> fr;
-    if ((frame_offsets || frame_block_sizes) && d->total_frames) {
-        fr.resize(d->total_frames);
-        DHIP(hipMemcpyAsync(fr.data(), d->frames.p, sizeof(DecFrame) * d->total_frames,
+    if (want_frames && sl.total_frames) {
+        fr.resize(sl.total_frames);
+        DHIP(hipMemcpyAsync(fr.data(), d->frames.p, sizeof(DecFrame) * sl.total_frames,
                             hipMemcpyDeviceToHost, d->s));
     }
     DHIP(hipStreamSynchronize(d->s));
     for (uint64_t i = 0; i < fr.size(); ++i) {
-        const DecTrack &t = d->tr[fr[i].track];
+        const DecTrack &t = sl.tr[fr[i].track];
         if (frame_offsets)
             frame_offsets[i] = fr[i].pos - t.start;
         if (frame_block_sizes)

@@ -360,7 +360,8 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
         RHIP(hipMalloc(&g_ctx.tracks, sizeof(RgTrack) * n));
         RHIP(hipMalloc(&g_ctx.hist, sizeof(uint32_t) * kBins * (size_t)n));
         RHIP(hipMalloc(&g_ctx.peaks, sizeof(double) * n));
-        RHIP(hipMalloc(&g_ctx.gains, sizeof(double) * (n + n_albums + 1)));
+        RHIP(hipMalloc(&g_ctx.gains,
+                       sizeof(double) * (n + std::max<size_t>(n_albums, g_ctx.cap_albums) + 1)));
         g_ctx.cap_tracks = n;
     }
     if (n_albums > g_ctx.cap_albums) {

@@ -1,0 +1,122 @@
+"""GPU: the pipelined device API (atg_flac_encode_device_async / _wait).
+
+Batches enqueued with encode_device_async keep their MD5 chains split in two
+parts one batch apart (md5.hip launch_track_md5 part 0 / part 1, engine.hip
+batch_end), so a batch's STREAMINFO MD5 is only complete once a later batch
+was enqueued or the batch was waited.  These tests keep several batches with
+different PCM buffers and mixed track shapes in flight -- tracks shorter than
+two MD5 blocks, odd PCM offsets (the unaligned finishing path), uneven
+lengths, a synchronous encode in between -- and require every waited image
+to equal the CPU port's byte for byte.  They also pin the slot contract of
+include/atgpu.h: a fourth unwaited enqueue fails, results survive until
+waited."""
+import numpy as np
+import pytest
+
+import oracle_port
+import signals
+
+pytestmark = pytest.mark.gpu
+
+FLAC8 = oracle_port.PRESETS["8"]
+
+
+def _batch(seed, shapes):
+    """shapes: list of (leading gap frames, track frames) -> (pcm int16,
+    tracks, per-track int32 pcm)"""
+    rng = np.random.default_rng(seed)
+    parts, tracks, per, pos = [], [], [], 0
+    for gap, n in shapes:
+        if gap:
+            parts.append(rng.integers(-99, 99, 2 * gap).astype(np.int16))
+            pos += gap
+        kind = ["tone", "noise", "chirp", "sine"][len(per) % 4]
+        p = signals.make(kind, n, 2, 16, seed=int(rng.integers(1 << 30))) if n else \
+            np.zeros(0, np.int32)
+        parts.append(p.astype(np.int16))
+        tracks.append((pos, n))
+        per.append(p.astype(np.int32))
+        pos += n
+    return np.concatenate(parts), tracks, per
+
+
+SHAPES = [
+    [(0, 4096 * 3 + 5), (1, 7), (0, 31), (3, 4096 * 2), (0, 1), (5, 9000), (0, 0), (2, 300)],
+    [(1, 4096 * 4), (0, 4096 * 4), (1, 100), (0, 15), (1, 16), (0, 17), (7, 12345)],
+    [(0, 64), (0, 4096), (1, 4097), (0, 4096 * 5 + 4095)],
+]
+
+
+def _dev(torch, arr):
+    return torch.from_numpy(arr.copy()).to("cuda")
+
+
+def _check(eng, torch, d_out, res, per, label):
+    host = d_out.cpu().numpy()
+    for t, (r, p) in enumerate(zip(res, per)):
+        want, _ = oracle_port.encode(p, 2, 16, 44100, **FLAC8)
+        got = host[r.out_offset:r.out_offset + r.bytes].tobytes()
+        assert got == want, "%s track %d (%d frames): GPU %d B vs port %d B" % (
+            label, t, len(p) // 2, len(got), len(want))
+
+
+def test_async_batches_split_md5_match_port(gpu_engine):
+    import torch
+    from audiotools import _atgpu
+    eng = gpu_engine
+    opts = _atgpu.make_options(**FLAC8)
+    batches = [_batch(100 + i, s) for i, s in enumerate(SHAPES)]
+    dev = []
+    for pcm, tracks, per in batches:
+        d_pcm = _dev(torch, pcm)
+        _, cap = eng.bounds(opts, tracks, 2, 16)
+        dev.append((d_pcm, torch.empty(cap, dtype=torch.uint8, device="cuda"), cap))
+    torch.cuda.synchronize()
+    # three batches in flight, waited oldest first
+    tickets = []
+    for (d_pcm, d_out, cap), (_, tracks, _) in zip(dev, batches):
+        tickets.append(eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, tracks,
+                                               2, 16, 44100, d_out.data_ptr(), cap))
+    for i, t in enumerate(tickets):
+        res = eng.wait(t)
+        _check(eng, torch, dev[i][1], res, batches[i][2], "pipelined batch %d" % i)
+    # waited in reverse order, with a synchronous encode in between
+    t0 = eng.encode_device_async(opts, dev[0][0].data_ptr(), _atgpu.PCM_S16, batches[0][1],
+                                 2, 16, 44100, dev[0][1].data_ptr(), dev[0][2])
+    t1 = eng.encode_device_async(opts, dev[1][0].data_ptr(), _atgpu.PCM_S16, batches[1][1],
+                                 2, 16, 44100, dev[1][1].data_ptr(), dev[1][2])
+    res2 = eng.encode_device(opts, dev[2][0].data_ptr(), _atgpu.PCM_S16, batches[2][1],
+                             2, 16, 44100, dev[2][1].data_ptr(), dev[2][2])
+    _check(eng, torch, dev[2][1], res2, batches[2][2], "sync between async")
+    res1 = eng.wait(t1)
+    res0 = eng.wait(t0)
+    _check(eng, torch, dev[1][1], res1, batches[1][2], "async waited first")
+    _check(eng, torch, dev[0][1], res0, batches[0][2], "async waited last")
+
+
+def test_fourth_enqueue_refused_results_survive(gpu_engine):
+    import torch
+    from audiotools import _atgpu
+    eng = gpu_engine
+    opts = _atgpu.make_options(**FLAC8)
+    pcm, tracks, per = _batch(7, [(0, 4096 * 2 + 11), (1, 333)])
+    d_pcm = _dev(torch, pcm)
+    _, cap = eng.bounds(opts, tracks, 2, 16)
+    outs = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(4)]
+    torch.cuda.synchronize()
+    ts = [eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16,
+                                  44100, outs[k].data_ptr(), cap) for k in range(3)]
+    with pytest.raises(_atgpu.ATGError) as e:
+        eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16, 44100,
+                                outs[3].data_ptr(), cap)
+    assert e.value.status == _atgpu.ATG_ERR_INVALID
+    with pytest.raises(_atgpu.ATGError):   # the host pipeline refuses too
+        eng.encode(opts, pcm, tracks, 2, 16, 44100)
+    # the first ticket's results were not lost
+    _check(eng, torch, outs[0], eng.wait(ts[0]), per, "ticket 0")
+    t3 = eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16, 44100,
+                                 outs[3].data_ptr(), cap)
+    for k, t in ((1, ts[1]), (2, ts[2]), (3, t3)):
+        _check(eng, torch, outs[k], eng.wait(t), per, "ticket %d" % k)
+    with pytest.raises(_atgpu.ATGError):   # waited twice after its slot was reused
+        eng.wait(ts[0])

@@ -54,7 +54,7 @@ def check_batch(engine, pcms, channels, bps, opts, rate=44100):
 
 
 @pytest.mark.parametrize("preset", ["8", "0", "1", "2", "3", "4", "5", "6", "7"])
-@pytest.mark.parametrize("channels,bps", [(2, 16), (1, 16), (2, 24), (6, 16), (1, 8)])
+@pytest.mark.parametrize("channels,bps", [(2, 16), (1, 16), (2, 24), (6, 16), (6, 24), (1, 8)])
 def test_presets_vs_oracle(gpu_engine, preset, channels, bps):
     opts = dict(oracle_port.PRESETS[preset])
     B = opts["block_size"]

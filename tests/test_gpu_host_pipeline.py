@@ -1,5 +1,6 @@
 """GPU: the chunked, overlapped host-memory encode (atg_flac_encode_host):
-tracks are cut into chunks of ~ATG_HOST_CHUNK_MB of PCM, staged through
+tracks are cut into chunks of ~chunk_bytes of PCM
+(atg_engine_set_host_chunk_bytes), staged through
 pinned buffers, and chunk c's upload / encode / chunk c-1's download
 overlap.  Every image and frame offset must equal the CPU port's, whatever
 the chunking, track order in memory or explicit frame sizes."""
@@ -13,9 +14,16 @@ import oracle_port
 pytestmark = pytest.mark.gpu
 
 
-def _engine():
+DEFAULT_CHUNK = 256 << 20
+
+
+@pytest.fixture
+def chunked():
+    """the session engine; its chunk size is restored afterwards"""
     from audiotools import _atgpu
-    return _atgpu.engine(), _atgpu
+    eng = _atgpu.engine()
+    yield eng, _atgpu
+    eng.set_host_chunk_bytes(DEFAULT_CHUNK)
 
 
 def _tracks(rng, n, lo, hi):
@@ -30,9 +38,9 @@ def _tracks(rng, n, lo, hi):
 
 
 @pytest.mark.parametrize("chunk_mb", ["1", "3", "4096"])
-def test_chunked_host_encode_matches_port(chunk_mb, monkeypatch):
-    eng, A = _engine()
-    monkeypatch.setenv("ATG_HOST_CHUNK_MB", chunk_mb)
+def test_chunked_host_encode_matches_port(chunk_mb, chunked):
+    eng, A = chunked
+    eng.set_host_chunk_bytes(int(chunk_mb) << 20)
     rng = np.random.default_rng(int(chunk_mb))
     lens, parts = _tracks(rng, 19, 20000, 160000)
     # tracks stored out of order, with gaps between them
@@ -58,9 +66,9 @@ def test_chunked_host_encode_matches_port(chunk_mb, monkeypatch):
         assert got == woffs, k
 
 
-def test_chunked_host_encode_explicit_frame_sizes(monkeypatch):
-    eng, A = _engine()
-    monkeypatch.setenv("ATG_HOST_CHUNK_MB", "1")
+def test_chunked_host_encode_explicit_frame_sizes(chunked):
+    eng, A = chunked
+    eng.set_host_chunk_bytes(1 << 20)
     rng = np.random.default_rng(5)
     lens, parts = _tracks(rng, 6, 150000, 200000)
     pcm = np.concatenate(parts)
@@ -76,7 +84,7 @@ def test_chunked_host_encode_explicit_frame_sizes(monkeypatch):
         base += m
     opts = A.make_options(**oracle_port.PRESETS["8"])
     out, res, offs, fpcm = eng.encode(opts, pcm, tracks, 2, 16, 44100)
-    monkeypatch.setenv("ATG_HOST_CHUNK_MB", "4096")
+    eng.set_host_chunk_bytes(4096 << 20)
     out1, res1, offs1, fpcm1 = eng.encode(opts, pcm, tracks, 2, 16, 44100)
     assert np.array_equal(offs, offs1) and np.array_equal(fpcm, fpcm1)
     for k in range(len(parts)):
