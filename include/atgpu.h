@@ -112,9 +112,15 @@ atg_status atg_flac_batch_bounds(const atg_flac_options *opts,
                                  uint64_t *total_frames, uint64_t *out_bytes);
 
 /* Encode a batch whose PCM and output live in host memory.
-   pcm: interleaved samples in `format`; out: out_cap bytes; results:
-   n_tracks entries; frame_offsets / frame_pcm_frames: total_frames entries
-   each (may be NULL).  Each track's image starts at results[t].out_offset. */
+   pcm: interleaved samples in `format`; out: out_cap bytes (>= the
+   atg_flac_batch_bounds size); results: n_tracks entries; frame_offsets /
+   frame_pcm_frames: total_frames entries each (may be NULL).  Each track's
+   image starts at results[t].out_offset; the images are packed back to back
+   (16-byte aligned) from out on.  The batch runs as a pipeline of chunks of
+   consecutive tracks (atg_engine_set_host_chunk_bytes), three in flight:
+   chunk c+1's upload, chunk c's encode and chunk c-1's download overlap.
+   Page-locked buffers (atg_host_alloc, hipHostMalloc, hipHostRegister) are
+   copied by DMA directly; pageable ones through pinned staging. */
 atg_status atg_flac_encode_host(atg_engine *eng, const atg_flac_options *opts,
                                 const void *pcm, atg_pcm_format format,
                                 const atg_track *tracks, uint32_t n_tracks,
@@ -168,6 +174,11 @@ atg_status atg_flac_encode_wait(atg_engine *eng, uint64_t ticket, atg_track_resu
    HIP events recorded on the stream each kernel ran on.  names/ms arrays of
    capacity `cap`; returns the number of entries written. */
 int atg_engine_kernel_times(atg_engine *eng, const char **names, float *ms, int cap);
+
+/* Page-locked host memory: PCM and output buffers the host pipeline moves
+   by DMA without staging (SURVEY 8(d)'s timer starts from pinned PCM). */
+atg_status atg_host_alloc(uint64_t bytes, void **ptr);
+void atg_host_free(void *ptr);
 
 /* Device-memory helpers so callers without a GPU framework can stage data. */
 atg_status atg_device_alloc(atg_engine *eng, uint64_t bytes, void **d_ptr);

@@ -9,6 +9,7 @@ CPU fallback on the product path.
 import ctypes
 import os
 import threading
+import weakref
 
 import numpy as np
 
@@ -30,7 +31,8 @@ EXPORTS = (
     "atg_abi_version", "atg_last_error", "atg_engine_create",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
-    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_device_alloc",
+    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_host_alloc",
+    "atg_host_free", "atg_device_alloc",
     "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
@@ -254,6 +256,10 @@ def load_library():
         lib.atg_flac_encode_device_async.restype = ctypes.c_int
         lib.atg_flac_encode_wait.argtypes = [P, c_u64, ctypes.POINTER(TrackResult)]
         lib.atg_flac_encode_wait.restype = ctypes.c_int
+        lib.atg_host_alloc.argtypes = [c_u64, ctypes.POINTER(P)]
+        lib.atg_host_alloc.restype = ctypes.c_int
+        lib.atg_host_free.argtypes = [P]
+        lib.atg_host_free.restype = None
         lib.atg_engine_set_host_chunk_bytes.argtypes = [P, c_u64]
         lib.atg_engine_set_host_chunk_bytes.restype = ctypes.c_int
         lib.atg_engine_kernel_times.argtypes = [
@@ -461,10 +467,13 @@ class Engine(object):
         return nf.value, nb.value
 
     def encode(self, options, pcm, tracks, channels, bits_per_sample,
-               sample_rate):
+               sample_rate, out=None):
         """encode a batch held in host memory.
 
-        pcm: numpy int16 (bits <= 16) or int32 interleaved samples.
+        pcm: numpy int16 (bits <= 16) or int32 interleaved samples; out: an
+        optional uint8 array of at least bounds() bytes (e.g. pinned_empty)
+        the images are written to.  Page-locked pcm / out are moved by DMA
+        without staging.
         Returns (out: uint8 array, results: list of TrackResult,
                  frame_offsets: uint64 array, frame_pcm: uint32 array)."""
         pcm = np.ascontiguousarray(pcm)
@@ -477,7 +486,10 @@ class Engine(object):
         tracks = list(tracks)
         nf, nb = self.bounds(options, tracks, channels, bits_per_sample)
         arr, n, keep = _track_array(tracks)
-        out = np.empty(max(1, nb), dtype=np.uint8)
+        if out is None:
+            out = np.empty(max(1, nb), dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.nbytes < nb:
+            raise ValueError("out must be a contiguous uint8 array of >= %d bytes" % nb)
         res = (TrackResult * max(1, n))()
         offs = np.zeros(max(1, nf), dtype=np.uint64)
         fpcm = np.zeros(max(1, nf), dtype=np.uint32)
@@ -546,6 +558,20 @@ class Engine(object):
             self.handle, dst.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(d_src),
             dst.nbytes))
         return dst
+
+
+def pinned_empty(shape, dtype=np.uint8):
+    """a numpy array in page-locked host memory (atg_host_alloc), freed
+    when the array is collected"""
+    lib = load_library()
+    dtype = np.dtype(dtype)
+    count = int(np.prod(shape)) if np.ndim(shape) else int(shape)
+    nbytes = max(1, count * dtype.itemsize)
+    p = ctypes.c_void_p()
+    _check(lib, lib.atg_host_alloc(nbytes, ctypes.byref(p)))
+    buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
+    weakref.finalize(buf, lib.atg_host_free, p.value)
+    return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
 
 
 def read_metadata(data, sp_cap=4096):

@@ -159,20 +159,30 @@ struct EncSlot {
 // third slot keeps them off the critical path at normal wave priority
 constexpr uint64_t kEncSlots = 3;
 
+// one stage of the host pipeline (chunk c uses stage c % kEncSlots)
+struct HostStage {
+    DevBuf d_pcm, d_img, d_pack, d_off;
+    uint8_t *p_in = nullptr, *p_out = nullptr; // pinned staging (pageable callers)
+    size_t p_in_cap = 0, p_out_cap = 0;
+    uint64_t *p_off = nullptr;                 // pinned: packed offsets to upload
+    size_t p_off_cap = 0;
+    hipEvent_t ev_h2d = nullptr;    // chunk PCM on the device
+    hipEvent_t ev_packed = nullptr; // images moved out of d_img
+    hipEvent_t ev_d2h = nullptr;    // packed images in host memory
+};
+
 struct atg_engine {
     int device = 0;
     bool sync_call = false; // inside atg_flac_encode_device (enqueue + wait)
     hipStream_t s_main = nullptr;
     EncSlot slot[kEncSlots];
     DevBuf windows;
-    // host-memory API: per slot, device PCM/image buffers and pinned host
-    // staging, plus copy streams, so chunk c's upload, chunk c-1's download
-    // and chunk c's encode overlap (atg_flac_encode_host)
-    DevBuf d_pcm[2], d_img[2];
-    uint8_t *p_in[2] = {nullptr, nullptr}, *p_out[2] = {nullptr, nullptr};
-    size_t p_in_cap[2] = {0, 0}, p_out_cap[2] = {0, 0};
+    // host-memory API (atg_flac_encode_host): per pipeline stage, device
+    // PCM / image / packed-image buffers and pinned host staging (used only
+    // for pageable caller buffers), plus copy streams, so chunk c+1's upload,
+    // chunk c's encode and chunk c-1's download overlap
+    HostStage hs[kEncSlots];
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
-    hipEvent_t ev_h2d[2] = {nullptr, nullptr}, ev_d2h[2] = {nullptr, nullptr};
     uint64_t chunk_bytes = 256ull << 20; // PCM bytes per chunk
     std::map<uint32_t, uint32_t> win_off;
     std::vector<double> win_host;
@@ -419,10 +429,9 @@ atg_status prepare_windows(atg_engine *e, Plan &pl)
 
 // memcpy split over host threads (pageable <-> pinned staging of large
 // chunks runs at several times one core's copy bandwidth)
-void par_memcpy(void *dst, const void *src, size_t n)
+void par_memcpy(void *dst, const void *src, size_t n, unsigned nt)
 {
     const size_t kMin = 8u << 20;
-    unsigned nt = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
     if (n < kMin || nt < 2) {
         std::memcpy(dst, src, n);
         return;
@@ -439,6 +448,19 @@ void par_memcpy(void *dst, const void *src, size_t n)
     }
     for (auto &t : th)
         t.join();
+}
+
+// page-locked host memory (hipHostMalloc / hipHostRegister): DMA-able as is
+bool is_pinned(const void *p)
+{
+    if (!p)
+        return false;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError(); // pageable memory: not an error for the caller
+        return false;
+    }
+    return a.type == hipMemoryTypeHost;
 }
 
 template <class T>
@@ -847,9 +869,10 @@ atg_status atg_engine_create(int device, atg_engine **out)
     }
     HIP_TRY(hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking));
     HIP_TRY(hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking));
-    for (int k = 0; k < 2; ++k) {
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_h2d[k], hipEventDisableTiming));
-        HIP_TRY(hipEventCreateWithFlags(&e->ev_d2h[k], hipEventDisableTiming));
+    for (HostStage &h : e->hs) {
+        HIP_TRY(hipEventCreateWithFlags(&h.ev_h2d, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h.ev_packed, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&h.ev_d2h, hipEventDisableTiming));
     }
     static uint32_t t16[4][256], t8[256];
     static uint16_t adv[24][16];
@@ -885,15 +908,15 @@ void atg_engine_destroy(atg_engine *e)
     }
     (void)hipStreamSynchronize(e->s_h2d);
     (void)hipStreamSynchronize(e->s_d2h);
-    for (int k = 0; k < 2; ++k) {
-        e->d_pcm[k].release();
-        e->d_img[k].release();
-        if (e->p_in[k])
-            (void)hipHostFree(e->p_in[k]);
-        if (e->p_out[k])
-            (void)hipHostFree(e->p_out[k]);
-        (void)hipEventDestroy(e->ev_h2d[k]);
-        (void)hipEventDestroy(e->ev_d2h[k]);
+    for (HostStage &h : e->hs) {
+        for (DevBuf *b : {&h.d_pcm, &h.d_img, &h.d_pack, &h.d_off})
+            b->release();
+        for (void *q : {(void *)h.p_in, (void *)h.p_out, (void *)h.p_off})
+            if (q)
+                (void)hipHostFree(q);
+        (void)hipEventDestroy(h.ev_h2d);
+        (void)hipEventDestroy(h.ev_packed);
+        (void)hipEventDestroy(h.ev_d2h);
     }
     (void)hipStreamDestroy(e->s_h2d);
     (void)hipStreamDestroy(e->s_d2h);
@@ -1014,16 +1037,15 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
     struct Chunk {
         uint32_t t0, t1;          // tracks [t0, t1)
         uint64_t pcm0, samples;   // first sample and samples of the chunk's PCM span
-        uint64_t frame0;          // first frame (global numbering)
         std::vector<atg_track> tr;
         std::shared_ptr<Plan> plan;
         uint64_t ticket = 0;
-        uint64_t img_bytes = 0;   // image span downloaded
+        uint64_t out0 = 0, out_bytes = 0; // packed span in `out`
+        bool staged_out = false;          // D2H went to pinned staging
     };
     std::vector<Chunk> chunks;
     {
         uint32_t t = 0;
-        uint64_t frame0 = 0;
         while (t < n_tracks) {
             Chunk c;
             c.t0 = t;
@@ -1038,12 +1060,10 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
             c.t1 = t;
             c.pcm0 = lo == UINT64_MAX ? 0 : lo;
             c.samples = hi > c.pcm0 ? hi - c.pcm0 : 0;
-            c.frame0 = frame0;
             for (uint32_t k = c.t0; k < c.t1; ++k) {
                 atg_track a = tracks[k];
                 a.pcm_offset -= c.pcm0 / channels;
                 c.tr.push_back(a);
-                frame0 += whole.tracks[k].n_frames;
             }
             c.plan = std::make_shared<Plan>();
             st = make_plan(opts, c.tr.data(), (uint32_t)c.tr.size(), channels, bps, rate, *c.plan);
@@ -1052,46 +1072,72 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
             chunks.push_back(std::move(c));
         }
     }
+    // page-locked caller buffers are copied by DMA directly; pageable ones
+    // go through pinned staging (copied on host threads)
+    const bool pin_in = is_pinned(pcm), pin_out = is_pinned(out);
+    const unsigned host_threads = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+    auto par_copy = [&](void *dst, const void *src, size_t n) {
+        if (n)
+            par_memcpy(dst, src, n, host_threads);
+    };
+    // chunk c's images are packed back to back (16-byte aligned) at
+    // out + c.out0: the caller reads each at results[t].out_offset
+    uint64_t out_pos = 0;
+    // a staged chunk whose D2H is queued but not yet copied to `out`
+    int pending_copy = -1;
 
-    // finish chunk ci (slot ci & 1): wait, download its images, copy them and
-    // its results into the caller's arrays
+    auto finish_copy = [&](int ci) -> atg_status {
+        Chunk &c = chunks[(size_t)ci];
+        HostStage &h = e->hs[(size_t)ci % kEncSlots];
+        HIP_TRY(hipEventSynchronize(h.ev_d2h));
+        if (c.staged_out)
+            par_copy(out + c.out0, h.p_out, c.out_bytes);
+        return ATG_OK;
+    };
+
+    // finish chunk ci: wait for its batch, pack its images on the device,
+    // queue their copy to host memory, fill its results
     auto collect = [&](size_t ci) -> atg_status {
         Chunk &c = chunks[ci];
-        const int k = (int)(ci & 1u);
+        HostStage &h = e->hs[ci % kEncSlots];
         EncSlot *sl = nullptr;
         atg_status s2 = wait_ticket(e, c.ticket, sl);
         if (s2 != ATG_OK)
             return s2;
         const Plan &cp = *c.plan;
-        uint64_t span = 0;
-        for (size_t j = 0; j < cp.tracks.size(); ++j)
-            span = std::max<uint64_t>(span, cp.tracks[j].out_base + sl->tout_h[j].bytes);
-        c.img_bytes = span;
-        if (span)
-            HIP_TRY(hipMemcpyAsync(e->p_out[k], e->d_img[k].p, span, hipMemcpyDeviceToHost,
-                                   e->s_d2h));
-        HIP_TRY(hipEventRecord(e->ev_d2h[k], e->s_d2h));
-        HIP_TRY(hipEventSynchronize(e->ev_d2h[k]));
-        {
-            // the chunk's images to the caller's layout, in parallel
-            std::vector<std::thread> th;
-            const unsigned nt = std::min<unsigned>(
-                16, std::max(1u, std::thread::hardware_concurrency()));
-            const size_t nj = cp.tracks.size();
-            for (unsigned w = 0; w < nt && w < nj; ++w)
-                th.emplace_back([&, w] {
-                    for (size_t j = w; j < nj; j += nt)
-                        std::memcpy(out + whole.tracks[c.t0 + j].out_base,
-                                    e->p_out[k] + cp.tracks[j].out_base, sl->tout_h[j].bytes);
-                });
-            for (auto &t : th)
-                t.join();
+        const size_t nt = cp.tracks.size();
+        HIP_TRY(ensure_pinned(h.p_off, h.p_off_cap, std::max<size_t>(nt, 1)));
+        uint64_t pos = 0;
+        for (size_t j = 0; j < nt; ++j) {
+            h.p_off[j] = pos;
+            pos += (sl->tout_h[j].bytes + 15u) & ~15ull;
         }
-        for (size_t j = 0; j < cp.tracks.size(); ++j) {
+        c.out0 = out_pos;
+        c.out_bytes = pos;
+        out_pos += pos;
+        HIP_TRY(h.d_off.ensure(std::max<size_t>(nt, 1) * sizeof(uint64_t)));
+        HIP_TRY(h.d_pack.ensure(std::max<uint64_t>(pos, 16)));
+        if (nt)
+            HIP_TRY(hipMemcpyAsync(h.d_off.p, h.p_off, nt * sizeof(uint64_t),
+                                   hipMemcpyHostToDevice, e->s_d2h));
+        HIP_TRY(launch_pack_images((const uint8_t *)h.d_img.p, (const TrackInfo *)sl->tracks.p,
+                                   (const TrackOut *)sl->tout.p, (const uint64_t *)h.d_off.p,
+                                   (uint32_t)nt, (uint8_t *)h.d_pack.p, e->s_d2h));
+        HIP_TRY(hipEventRecord(h.ev_packed, e->s_d2h));
+        c.staged_out = !pin_out;
+        uint8_t *dst = out + c.out0;
+        if (c.staged_out) {
+            HIP_TRY(ensure_pinned(h.p_out, h.p_out_cap, std::max<uint64_t>(pos, 16)));
+            dst = h.p_out;
+        }
+        if (pos)
+            HIP_TRY(hipMemcpyAsync(dst, h.d_pack.p, pos, hipMemcpyDeviceToHost, e->s_d2h));
+        HIP_TRY(hipEventRecord(h.ev_d2h, e->s_d2h));
+        for (size_t j = 0; j < nt; ++j) {
             const uint32_t t = c.t0 + (uint32_t)j;
             const TrackOut &to = sl->tout_h[j];
             atg_track_result &r = results[t];
-            r.out_offset = whole.tracks[t].out_base;
+            r.out_offset = c.out0 + h.p_off[j];
             r.bytes = to.bytes;
             r.first_frame = whole.track_frame_pos[t];
             r.n_frames = whole.tracks[t].n_frames;
@@ -1109,54 +1155,82 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
                     frame_pcm_frames[r.first_frame + i] = cp.frames[f].n;
             }
         }
+        // the previous staged chunk's bytes are in host memory by now
+        if (pending_copy >= 0) {
+            s2 = finish_copy(pending_copy);
+            if (s2 != ATG_OK)
+                return s2;
+        }
+        pending_copy = (int)ci;
         return ATG_OK;
+    };
+
+    auto drain = [&](atg_status err) {
+        (void)hipDeviceSynchronize();
+        for (EncSlot &s2 : e->slot)
+            if (s2.busy) {
+                s2.busy = false;
+                s2.done = false;
+                s2.ticket = 0;
+                s2.end_pending = false;
+            }
+        return err;
     };
 
     for (size_t ci = 0; ci < chunks.size(); ++ci) {
         Chunk &c = chunks[ci];
-        const int k = (int)(ci & 1u);
+        HostStage &h = e->hs[ci % kEncSlots];
         const uint64_t in_bytes = c.samples * elem;
-        HIP_TRY(e->d_pcm[k].ensure(in_bytes + 16));
-        HIP_TRY(e->d_img[k].ensure(c.plan->out_bytes + 16));
-        HIP_TRY(ensure_pinned(e->p_in[k], e->p_in_cap[k], in_bytes + 16));
-        HIP_TRY(ensure_pinned(e->p_out[k], e->p_out_cap[k], c.plan->out_bytes + 16));
-        // stage through pinned memory (the caller's buffer is pageable)
+        // stage ci % 3 last held chunk ci - 3, collected (waited, packed)
+        // two iterations ago; its device buffers are reused in stream order
+        HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
+        HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
+        const uint8_t *src = (const uint8_t *)pcm + c.pcm0 * elem;
+        if (in_bytes && !pin_in) {
+            HIP_TRY(ensure_pinned(h.p_in, h.p_in_cap, in_bytes + 16));
+            HIP_TRY(hipEventSynchronize(h.ev_h2d)); // its previous upload has finished
+            par_copy(h.p_in, src, in_bytes);
+            src = h.p_in;
+        }
+        // the encode overwrites d_img: the previous occupant's images must
+        // have been packed first
+        HIP_TRY(hipStreamWaitEvent(e->s_h2d, h.ev_packed, 0));
         if (in_bytes)
-            par_memcpy(e->p_in[k], (const uint8_t *)pcm + c.pcm0 * elem, in_bytes);
-        if (in_bytes)
-            HIP_TRY(hipMemcpyAsync(e->d_pcm[k].p, e->p_in[k], in_bytes, hipMemcpyHostToDevice,
-                                   e->s_h2d));
-        HIP_TRY(hipEventRecord(e->ev_h2d[k], e->s_h2d));
+            HIP_TRY(hipMemcpyAsync(h.d_pcm.p, src, in_bytes, hipMemcpyHostToDevice, e->s_h2d));
+        HIP_TRY(hipEventRecord(h.ev_h2d, e->s_h2d));
         EncSlot *sl = nullptr;
         uint64_t ticket = 0;
         st = take_slot(e, sl, ticket);
         if (st == ATG_OK)
-            st = enqueue_batch(e, *sl, c.plan, e->d_pcm[k].p, (int)format,
-                               (uint8_t *)e->d_img[k].p, e->d_img[k].cap, true, e->ev_h2d[k]);
+            st = enqueue_batch(e, *sl, c.plan, h.d_pcm.p, (int)format, (uint8_t *)h.d_img.p,
+                               h.d_img.cap, true, h.ev_h2d, true);
         if (st != ATG_OK) {
-            (void)hipDeviceSynchronize();
             if (sl) {
                 sl->uploaded = nullptr;
                 sl->ticket = 0;
                 sl->end_pending = false;
             }
-            return st;
+            return drain(st);
         }
         sl->busy = true;
         c.ticket = ticket;
-        // chunk ci-1's results come back while chunk ci encodes
-        if (ci >= 1) {
-            st = collect(ci - 1);
-            if (st != ATG_OK) {
-                (void)hipDeviceSynchronize();
-                return st;
-            }
+        // keep kEncSlots chunks in flight: chunk ci - 2 finishes now
+        if (ci + 1 >= kEncSlots) {
+            st = collect(ci + 1 - kEncSlots);
+            if (st != ATG_OK)
+                return drain(st);
         }
     }
-    if (!chunks.empty()) {
-        st = collect(chunks.size() - 1);
+    for (size_t ci = chunks.size() >= kEncSlots ? chunks.size() + 1 - kEncSlots : 0;
+         ci < chunks.size(); ++ci) {
+        st = collect(ci);
         if (st != ATG_OK)
-            return st;
+            return drain(st);
+    }
+    if (pending_copy >= 0) {
+        st = finish_copy(pending_copy);
+        if (st != ATG_OK)
+            return drain(st);
     }
     return ATG_OK;
 }
@@ -1200,6 +1274,24 @@ atg_status atg_device_free(atg_engine *e, void *d_ptr)
     if (d_ptr)
         HIP_TRY(hipFree(d_ptr));
     return ATG_OK;
+}
+
+atg_status atg_host_alloc(uint64_t bytes, void **ptr)
+{
+    if (!ptr)
+        return fail(ATG_ERR_INVALID, "NULL argument");
+    *ptr = nullptr;
+    if (hipHostMalloc(ptr, bytes ? bytes : 1, hipHostMallocDefault) != hipSuccess) {
+        *ptr = nullptr;
+        return fail(ATG_ERR_NOMEM, "hipHostMalloc failed");
+    }
+    return ATG_OK;
+}
+
+void atg_host_free(void *ptr)
+{
+    if (ptr)
+        (void)hipHostFree(ptr);
 }
 
 atg_status atg_copy_to_device(atg_engine *e, void *d_dst, const void *src, uint64_t bytes)

@@ -772,3 +772,34 @@ hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
     hipLaunchKernelGGL(k_stream_header, dim3(p.n_tracks), dim3(64), 0, s, p, tracks, tout, out);
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------- images
+// The host pipeline's compaction: each track's finished image moves from
+// its worst-case slot (tracks[t].out_base) to dst + dst_off[t] (16-byte
+// aligned, tracks back to back), so one contiguous copy brings a chunk's
+// images to host memory.  One workgroup per track, 16-byte moves; the
+// rounded-up tail stays inside both 16-byte-aligned slots.
+__global__ __launch_bounds__(256) void k_pack_images(const uint8_t *__restrict__ img,
+                                                     const TrackInfo *__restrict__ tracks,
+                                                     const TrackOut *__restrict__ tout,
+                                                     const uint64_t *__restrict__ dst_off,
+                                                     uint32_t n, uint8_t *__restrict__ dst)
+{
+    for (uint32_t t = blockIdx.x; t < n; t += gridDim.x) {
+        const uint4 *__restrict__ s = (const uint4 *)(img + tracks[t].out_base);
+        uint4 *__restrict__ d = (uint4 *)(dst + dst_off[t]);
+        const uint64_t n16 = (tout[t].bytes + 15u) / 16u;
+        for (uint64_t i = threadIdx.x; i < n16; i += blockDim.x)
+            d[i] = s[i];
+    }
+}
+
+hipError_t launch_pack_images(const uint8_t *img, const TrackInfo *tracks, const TrackOut *tout,
+                              const uint64_t *dst_off, uint32_t n, uint8_t *dst, hipStream_t s)
+{
+    if (!n)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_pack_images, dim3(n < 4096u ? n : 4096u), dim3(256), 0, s, img, tracks,
+                       tout, dst_off, n, dst);
+    return hipGetLastError();
+}

@@ -57,6 +57,9 @@ hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
 hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
                                 const TrackOut *tout, uint8_t *out,
                                 hipStream_t s);
+// host pipeline: track images from their slots to dst + dst_off[t]
+hipError_t launch_pack_images(const uint8_t *img, const TrackInfo *tracks, const TrackOut *tout,
+                              const uint64_t *dst_off, uint32_t n, uint8_t *dst, hipStream_t s);
 hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
                              const uint32_t *crc16_tab /*[4][256] slicing tables*/,
                              const uint32_t *crc8_tab /*[256]*/);

@@ -100,3 +100,36 @@ def test_chunked_host_encode_explicit_frame_sizes(chunked):
         # the image decodes back to the source exactly
         pcm_dec = oracle_port.decode(img)[0]
         assert np.array_equal(pcm_dec, parts[k].astype(np.int32))
+
+
+@pytest.mark.parametrize("pin_in,pin_out", [(True, True), (True, False), (False, True)])
+def test_pinned_buffers_direct_dma(pin_in, pin_out, chunked):
+    """page-locked PCM / output (atg_host_alloc) move by DMA without the
+    staging copies; images are packed back to back in `out` and equal the
+    port's, whatever the chunking (1 MB chunks: the three-stage ring wraps)"""
+    eng, A = chunked
+    eng.set_host_chunk_bytes(1 << 20)
+    rng = np.random.default_rng(11 + 2 * pin_in + pin_out)
+    lens, parts = _tracks(rng, 23, 1000, 120000)
+    host = np.concatenate(parts)
+    pcm = A.pinned_empty(host.shape, np.int16) if pin_in else host
+    pcm[:] = host
+    tracks, pos = [], 0
+    for m in lens:
+        tracks.append((pos, m))
+        pos += m
+    opts = A.make_options(**oracle_port.PRESETS["8"])
+    _, nb = eng.bounds(opts, tracks, 2, 16)
+    out = A.pinned_empty(nb, np.uint8) if pin_out else None
+    out, res, offs, fpcm = eng.encode(opts, pcm, tracks, 2, 16, 44100, out=out)
+    end = 0
+    for k in range(len(parts)):
+        r = res[k]
+        assert r.out_offset == (end + 15) // 16 * 16      # packed, 16-byte aligned
+        end = r.out_offset + r.bytes
+        want, woffs = oracle_port.encode(parts[k].astype(np.int32), 2, 16, 44100,
+                                         **oracle_port.PRESETS["8"])
+        assert bytes(out[r.out_offset:r.out_offset + r.bytes]) == want, k
+        got = [(int(offs[r.first_frame + i]), int(fpcm[r.first_frame + i]))
+               for i in range(r.n_frames)]
+        assert got == woffs, k
