@@ -130,6 +130,39 @@ atg_status atg_flac_encode_host(atg_engine *eng, const atg_flac_options *opts,
                                 uint64_t *frame_offsets,
                                 uint32_t *frame_pcm_frames);
 
+/* Streaming form for ONE track (the reference's frame loop,
+   src/encoders/flac.c:244-274, run over bounded segments of a long track):
+   encodes pcm_frames PCM frames (host memory, cut into block_size frames or
+   the explicit frame_sizes, as atg_track) as FLAC frames only -- no stream
+   header, no MD5 -- numbered from first_frame_number (the frame header's
+   UTF-8 frame number, flac.c:1531-1566).  The frames land back to back at
+   out (*out_bytes in total, frame_bytes[i] each; out_cap >=
+   atg_flac_max_frames_bytes).  The caller hashes the PCM (a serial MD5
+   chain per track runs faster on a host core than on one GPU lane) and
+   writes the stream header with atg_flac_stream_header before the first
+   segment and again, with the final STREAMINFO, at the end (the reference
+   rewrites STREAMINFO once the frames are written, flac.c:276-279). */
+atg_status atg_flac_encode_frames(atg_engine *eng, const atg_flac_options *opts,
+                                  const void *pcm, atg_pcm_format format, uint64_t pcm_frames,
+                                  const uint32_t *frame_sizes, uint64_t n_frame_sizes,
+                                  uint32_t channels, uint32_t bits_per_sample,
+                                  uint32_t sample_rate, uint64_t first_frame_number,
+                                  uint8_t *out, uint64_t out_cap, uint64_t *out_bytes,
+                                  uint32_t *frame_bytes);
+/* worst-case bytes of atg_flac_encode_frames' output (0: invalid options) */
+uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_frames,
+                                   const uint32_t *frame_sizes, uint64_t n_frame_sizes,
+                                   uint32_t channels, uint32_t bits_per_sample);
+/* fLaC + STREAMINFO (fields clamped as flacenc_write_streaminfo,
+   flac.c:376-409) + VORBIS_COMMENT (vendor string) + PADDING of
+   opts->padding_size bytes (flac.c:208-238), host-side; returns the header
+   size, or 0 when cap is too small or an argument is invalid. */
+uint64_t atg_flac_stream_header(const atg_flac_options *opts, uint32_t channels,
+                                uint32_t bits_per_sample, uint32_t sample_rate,
+                                uint64_t total_samples, uint32_t min_frame_bytes,
+                                uint32_t max_frame_bytes, const uint8_t *md5, uint8_t *out,
+                                uint64_t cap);
+
 /* PCM bytes per chunk of atg_flac_encode_host's pipeline (default 256 MiB):
    consecutive tracks are grouped into chunks of about this much PCM, and
    chunk c+1's upload, chunk c's encode and chunk c-1's download overlap. */

@@ -31,7 +31,8 @@ EXPORTS = (
     "atg_abi_version", "atg_last_error", "atg_engine_create",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
-    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_host_alloc",
+    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_flac_encode_frames",
+    "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
     "atg_host_free", "atg_device_alloc",
     "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
@@ -256,6 +257,16 @@ def load_library():
         lib.atg_flac_encode_device_async.restype = ctypes.c_int
         lib.atg_flac_encode_wait.argtypes = [P, c_u64, ctypes.POINTER(TrackResult)]
         lib.atg_flac_encode_wait.restype = ctypes.c_int
+        lib.atg_flac_encode_frames.argtypes = [
+            P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, c_u64, P, c_u64, c_u32, c_u32,
+            c_u32, c_u64, P, c_u64, ctypes.POINTER(c_u64), P]
+        lib.atg_flac_encode_frames.restype = ctypes.c_int
+        lib.atg_flac_max_frames_bytes.argtypes = [ctypes.POINTER(FlacOptions), c_u64, P, c_u64,
+                                                  c_u32, c_u32]
+        lib.atg_flac_max_frames_bytes.restype = c_u64
+        lib.atg_flac_stream_header.argtypes = [ctypes.POINTER(FlacOptions), c_u32, c_u32, c_u32,
+                                               c_u64, c_u32, c_u32, P, P, c_u64]
+        lib.atg_flac_stream_header.restype = c_u64
         lib.atg_host_alloc.argtypes = [c_u64, ctypes.POINTER(P)]
         lib.atg_host_alloc.restype = ctypes.c_int
         lib.atg_host_free.argtypes = [P]
@@ -537,6 +548,37 @@ class Engine(object):
         _check(self.lib, self.lib.atg_flac_encode_wait(self.handle, t, res))
         return [res[i] for i in range(n)]
 
+    def encode_frames(self, options, pcm, channels, bits_per_sample, sample_rate,
+                      first_frame_number=0, frame_sizes=None):
+        """one track's PCM (host numpy int16 / int32, interleaved) as FLAC
+        frames only, numbered from first_frame_number (atg_flac_encode_frames)
+        -> (frame bytes: uint8 array, per-frame byte counts: uint32 array)"""
+        pcm = np.ascontiguousarray(pcm)
+        if pcm.dtype == np.int16:
+            fmt = PCM_S16
+        elif pcm.dtype == np.int32:
+            fmt = PCM_S32
+        else:
+            raise TypeError("pcm must be int16 or int32")
+        frames = len(pcm) // channels
+        fs = None if frame_sizes is None else np.ascontiguousarray(frame_sizes, dtype=np.uint32)
+        fs_p = fs.ctypes.data_as(ctypes.c_void_p) if fs is not None else None
+        nfs = len(fs) if fs is not None else 0
+        cap = self.lib.atg_flac_max_frames_bytes(ctypes.byref(options), frames, fs_p, nfs,
+                                                 channels, bits_per_sample)
+        if not cap:
+            raise ATGError(ATG_ERR_INVALID, "invalid encoder options")
+        n_fr = nfs if fs is not None else (frames + options.block_size - 1) // options.block_size
+        out = np.empty(max(1, cap), dtype=np.uint8)
+        fb = np.zeros(max(1, n_fr), dtype=np.uint32)
+        nb = c_u64()
+        _check(self.lib, self.lib.atg_flac_encode_frames(
+            self.handle, ctypes.byref(options), pcm.ctypes.data_as(ctypes.c_void_p), fmt,
+            frames, fs_p, nfs, channels, bits_per_sample, sample_rate, int(first_frame_number),
+            out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(nb),
+            fb.ctypes.data_as(ctypes.c_void_p)))
+        return out[:nb.value], fb[:n_fr]
+
     def set_host_chunk_bytes(self, nbytes):
         """PCM bytes per chunk of the host-memory pipeline (encode())"""
         _check(self.lib, self.lib.atg_engine_set_host_chunk_bytes(self.handle, int(nbytes)))
@@ -558,6 +600,21 @@ class Engine(object):
             self.handle, dst.ctypes.data_as(ctypes.c_void_p), ctypes.c_void_p(d_src),
             dst.nbytes))
         return dst
+
+
+def stream_header(options, channels, bits_per_sample, sample_rate, total_samples=0,
+                  min_frame_bytes=0xFFFFFF, max_frame_bytes=0, md5=b"\0" * 16):
+    """fLaC + STREAMINFO + VORBIS_COMMENT + PADDING (atg_flac_stream_header)"""
+    lib = load_library()
+    cap = 4096 + int(options.padding_size)
+    out = ctypes.create_string_buffer(cap)
+    m = ctypes.create_string_buffer(bytes(md5), 16)
+    n = lib.atg_flac_stream_header(ctypes.byref(options), channels, bits_per_sample,
+                                   sample_rate, int(total_samples), int(min_frame_bytes),
+                                   int(max_frame_bytes), m, out, cap)
+    if not n:
+        raise ATGError(ATG_ERR_INVALID, "invalid stream header arguments")
+    return out.raw[:n]
 
 
 def pinned_empty(shape, dtype=np.uint8):

@@ -212,6 +212,9 @@ struct Plan {
     bool big = false;
     uint32_t big_nmax = 0;       // longest frame
     uint32_t big_porder = 0;     // deepest usable partition order
+    // streaming segment (atg_flac_encode_frames): frames only, numbered from
+    // a base, no stream header and no MD5 (the caller hashes the PCM)
+    bool frames_only = false;
 };
 
 // persistent grid of the large-frame kernels and their per-workgroup
@@ -232,7 +235,8 @@ uint32_t qlp_precision_for(uint32_t n)
 }
 
 atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_t n_tracks,
-                     uint32_t channels, uint32_t bps, uint32_t rate, Plan &pl)
+                     uint32_t channels, uint32_t bps, uint32_t rate, Plan &pl,
+                     bool frames_only = false, uint32_t index_base = 0)
 {
     if (!o)
         return fail(ATG_ERR_INVALID, "options is NULL");
@@ -275,7 +279,8 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
     p.coef_row = std::max<uint32_t>(2, (M + 1u) & ~1u);
     p.coef_stride = std::max<uint32_t>(1, M) * p.coef_row;
     p.padding_size = o->padding_size;
-    p.header_bytes = 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + o->padding_size;
+    p.header_bytes = frames_only ? 0u : 4 + 4 + 34 + 4 + 4 + 29 + 4 + 4 + o->padding_size;
+    pl.frames_only = frames_only;
 
     const uint64_t B = o->block_size;
     const uint64_t nsub = channels;
@@ -333,7 +338,7 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
         f.pcm_start = pl.tracks[t].pcm_start + start[t];
         f.n = lens[i];
         f.track = t;
-        f.index = idx[t]++;
+        f.index = index_base + idx[t]++;
         f.win_off = 0;
         start[t] += lens[i];
     }
@@ -507,7 +512,7 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
     TrackOut *dto = (TrackOut *)sl.tout.p;
     uint32_t *derr = (uint32_t *)sl.err.p;
     hipEvent_t *ev = sl.ev;
-    if (sl.pend_split) {
+    if (sl.pend_split && !pl.frames_only) {
         if (after)
             HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
         HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, sl.s_aux));
@@ -516,7 +521,8 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
     // headers once both the pack and the MD5 chains are done
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
     HIP_TRY(hipEventRecord(ev[12], sl.s_aux));
-    HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, sl.s_aux));
+    if (!pl.frames_only)
+        HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, sl.s_aux));
     HIP_TRY(hipEventRecord(ev[13], sl.s_aux));
     HIP_TRY(hipEventRecord(ev[15], sl.s_aux));
     if (nt)
@@ -620,7 +626,8 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     const bool split_md5 = pipelined && fmt == ATG_PCM_S16 && p.bps == 16u;
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-    HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
+    if (!pl.frames_only)
+        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
     if (pl.big)
         HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
@@ -1233,6 +1240,150 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
             return drain(st);
     }
     return ATG_OK;
+}
+
+uint64_t atg_flac_stream_header(const atg_flac_options *o, uint32_t channels, uint32_t bps,
+                                uint32_t rate, uint64_t total_samples, uint32_t min_frame_bytes,
+                                uint32_t max_frame_bytes, const uint8_t *md5, uint8_t *out,
+                                uint64_t cap)
+{
+    // fLaC + STREAMINFO (flacenc_write_streaminfo, flac.c:376-409, fields
+    // clamped) + VORBIS_COMMENT with the vendor string + PADDING
+    // (flac.c:208-238): the bytes k_stream_header writes on the device
+    static const char vendor[] = "Python Audio Tools 2.22alpha1";
+    const uint32_t vlen = (uint32_t)sizeof(vendor) - 1u;
+    if (!o || !md5 || channels < 1 || bps < 1 || o->padding_size > 0xFFFFFFu)
+        return 0;
+    const uint64_t need = 4 + 4 + 34 + 4 + 4 + vlen + 4 + 4 + (uint64_t)o->padding_size;
+    if (!out || cap < need)
+        return 0;
+    uint64_t n = 0;
+    auto put = [&](uint8_t b) { out[n++] = b; };
+    put('f'); put('L'); put('a'); put('C');
+    put(0x00); put(0); put(0); put(34);
+    // 34 STREAMINFO bytes, MSB first
+    uint8_t si[34] = {0};
+    uint32_t bitpos = 0;
+    auto bits = [&](uint32_t count, uint64_t v) {
+        for (uint32_t i = count; i-- > 0; ++bitpos)
+            if ((v >> i) & 1u)
+                si[bitpos >> 3] |= (uint8_t)(0x80u >> (bitpos & 7u));
+    };
+    const uint32_t bs = o->block_size > 0xFFFFu ? 0xFFFFu : o->block_size;
+    bits(16, bs);
+    bits(16, bs);
+    bits(24, min_frame_bytes > 0xFFFFFFu ? 0xFFFFFFu : min_frame_bytes);
+    bits(24, max_frame_bytes > 0xFFFFFFu ? 0xFFFFFFu : max_frame_bytes);
+    bits(20, rate > 0xFFFFFu ? 0xFFFFFu : rate);
+    bits(3, channels - 1u > 7u ? 7u : channels - 1u);
+    bits(5, bps - 1u > 31u ? 31u : bps - 1u);
+    bits(36, total_samples & 0xFFFFFFFFFull);
+    for (int i = 0; i < 16; ++i)
+        bits(8, md5[i]);
+    for (int i = 0; i < 34; ++i)
+        put(si[i]);
+    const uint32_t vc = 4u + vlen + 4u;
+    put(0x04); put((uint8_t)(vc >> 16)); put((uint8_t)(vc >> 8)); put((uint8_t)vc);
+    put((uint8_t)vlen); put(0); put(0); put(0);
+    for (uint32_t i = 0; i < vlen; ++i)
+        put((uint8_t)vendor[i]);
+    put(0); put(0); put(0); put(0);
+    put(0x81); put((uint8_t)(o->padding_size >> 16)); put((uint8_t)(o->padding_size >> 8));
+    put((uint8_t)o->padding_size);
+    std::memset(out + n, 0, o->padding_size);
+    return need;
+}
+
+atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, const void *pcm,
+                                  atg_pcm_format format, uint64_t pcm_frames,
+                                  const uint32_t *frame_sizes, uint64_t n_frame_sizes,
+                                  uint32_t channels, uint32_t bps, uint32_t rate,
+                                  uint64_t first_frame_number, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *out_bytes, uint32_t *frame_bytes)
+{
+    if (!e || (!pcm && pcm_frames) || !out_bytes)
+        return fail(ATG_ERR_INVALID, "NULL argument");
+    if (format == ATG_PCM_S16 && bps > 16)
+        return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
+    const uint64_t nfr_max = frame_sizes ? n_frame_sizes
+                                         : (opts && opts->block_size
+                                                ? (pcm_frames + opts->block_size - 1) / opts->block_size
+                                                : 0);
+    // the frame header's UTF-8 number holds 31 bits (flac.c:1531-1566)
+    if (first_frame_number + nfr_max > 0x7FFFFFFFull)
+        return fail(ATG_ERR_INVALID, "frame numbers beyond 2^31 - 1");
+    for (EncSlot &s2 : e->slot)
+        if (s2.busy)
+            return fail(ATG_ERR_INVALID, "an async encode batch is in flight: wait for it first");
+    atg_track tr;
+    tr.pcm_offset = 0;
+    tr.pcm_frames = pcm_frames;
+    tr.frame_sizes = frame_sizes;
+    tr.n_frame_sizes = n_frame_sizes;
+    auto pl = std::make_shared<Plan>();
+    atg_status st = make_plan(opts, &tr, 1, channels, bps, rate, *pl, true,
+                              (uint32_t)first_frame_number);
+    if (st != ATG_OK)
+        return st;
+    HIP_TRY(hipSetDevice(e->device));
+    HostStage &h = e->hs[0];
+    const size_t elem = format == ATG_PCM_S16 ? 2 : 4;
+    const uint64_t in_bytes = pcm_frames * channels * elem;
+    HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
+    HIP_TRY(h.d_img.ensure(pl->out_bytes + 16));
+    // the previous host-pipeline batch is finished (no slot busy); its
+    // packing kernel may still read d_img
+    HIP_TRY(hipStreamWaitEvent(e->s_main, h.ev_packed, 0));
+    if (in_bytes)
+        HIP_TRY(hipMemcpyAsync(h.d_pcm.p, pcm, in_bytes, hipMemcpyHostToDevice, e->s_main));
+    EncSlot *sl = nullptr;
+    uint64_t ticket = 0;
+    st = take_slot(e, sl, ticket);
+    if (st == ATG_OK)
+        st = enqueue_batch(e, *sl, pl, h.d_pcm.p, (int)format, (uint8_t *)h.d_img.p,
+                           h.d_img.cap, true, nullptr, false);
+    if (st != ATG_OK) {
+        (void)hipDeviceSynchronize();
+        if (sl) {
+            sl->uploaded = nullptr;
+            sl->ticket = 0;
+            sl->end_pending = false;
+        }
+        return st;
+    }
+    sl->busy = true;
+    st = wait_ticket(e, ticket, sl);
+    if (st != ATG_OK)
+        return st;
+    const uint64_t nb = sl->tout_h[0].bytes;
+    *out_bytes = nb;
+    if (nb > out_cap)
+        return fail(ATG_ERR_CAPACITY, "output buffer too small for the segment's frames");
+    if (nb) {
+        HIP_TRY(hipMemcpyAsync(out, h.d_img.p, nb, hipMemcpyDeviceToHost, e->s_main));
+        HIP_TRY(hipStreamSynchronize(e->s_main));
+    }
+    if (frame_bytes) {
+        const TrackInfo &ti = pl->tracks[0];
+        for (uint32_t i = 0; i < ti.n_frames; ++i)
+            frame_bytes[i] = sl->fdesc_h[pl->order[ti.first_pos + i]].bytes;
+    }
+    return ATG_OK;
+}
+
+uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_frames,
+                                   const uint32_t *frame_sizes, uint64_t n_frame_sizes,
+                                   uint32_t channels, uint32_t bps)
+{
+    atg_track tr;
+    tr.pcm_offset = 0;
+    tr.pcm_frames = pcm_frames;
+    tr.frame_sizes = frame_sizes;
+    tr.n_frame_sizes = n_frame_sizes;
+    Plan pl;
+    if (make_plan(opts, &tr, 1, channels, bps, 44100, pl, true, 0) != ATG_OK)
+        return 0;
+    return pl.out_bytes;
 }
 
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)

@@ -123,3 +123,29 @@ def test_null_arguments_rejected():
     assert lib.atg_engine_create(0, None) == _atgpu.ATG_ERR_INVALID
     lib.atg_engine_destroy(None)  # no-op
     assert lib.atg_engine_kernel_times(None, None, None, 0) == 0
+
+
+@pytest.mark.parametrize("ch,bps,rate,n,pad", [(2, 16, 44100, 30000, 4096), (6, 24, 48000, 9001, 0),
+                                               (1, 8, 8000, 0, 100), (2, 16, 700000, 5, 4096)])
+def test_host_stream_header_matches_port(ch, bps, rate, n, pad):
+    """atg_flac_stream_header (host code, no GPU): the streaming encoder's
+    header equals the whole-stream header the oracle writes -- STREAMINFO
+    fields and MD5 as given, VORBIS_COMMENT vendor, PADDING"""
+    import hashlib
+    import oracle_port
+    import signals
+    from audiotools.encoders import pcm_le_bytes
+    x = signals.make("tone", n, ch, bps, seed=n) if n else np.zeros(0, np.int32)
+    opts = dict(oracle_port.PRESETS["8"], padding_size=pad)
+    img, lst = oracle_port.encode(x, ch, bps, rate, **opts)
+    blocks, frames = oracle_port.split_flac(img)
+    hdr_len = len(img) - len(frames)
+    sizes = []
+    for k, (off, _) in enumerate(lst):
+        end = lst[k + 1][0] if k + 1 < len(lst) else len(frames)
+        sizes.append(end - off)
+    md5 = hashlib.md5(pcm_le_bytes(x, bps)).digest()
+    got = _atgpu.stream_header(_atgpu.make_options(**opts), ch, bps, rate, n,
+                               min(sizes) if sizes else 0xFFFFFF, max(sizes) if sizes else 0,
+                               md5)
+    assert got == img[:hdr_len]

@@ -164,3 +164,71 @@ def test_encode_flac_api(tmp_path):
     want, wlst = oracle_port.encode(pcm, 2, 16, 44100, **oracle_port.PRESETS["8"])
     assert open(fn, "rb").read() == want
     assert offsets == wlst
+
+
+class _SizedReader(object):
+    """a PCMReader whose read() returns the listed frame counts, then
+    `block` frames at a time (each read is one FLAC frame, flac.c:244-274)"""
+
+    def __init__(self, samples, rate, channels, bps, sizes=()):
+        import audiotools
+        self._r = audiotools.FrameListReader(samples, rate, channels, bps)
+        self.sample_rate, self.channels, self.bits_per_sample = rate, channels, bps
+        self.channel_mask = 0
+        self.sizes = list(sizes)
+        self.closed = False
+
+    def read(self, n):
+        return self._r.read(self.sizes.pop(0) if self.sizes else n)
+
+    def close(self):
+        self.closed = True
+
+
+@pytest.mark.parametrize("ch,bps,n,sizes,seg", [
+    (2, 16, 4096 * 20 + 77, (), 3),          # 7 segments of 3 frames
+    (2, 16, 4096 * 9, (4096, 1000, 7, 4096, 4095, 1), 4),
+    (6, 24, 4096 * 5 + 5, (), 2),
+    (1, 8, 3000, (), 256),
+    (2, 16, 0, (), 3),                       # empty stream
+])
+def test_encode_flac_streaming(tmp_path, monkeypatch, ch, bps, n, sizes, seg):
+    """encode_flac streams in segments of SEGMENT_FRAMES frames (frame
+    numbers continue across segments, host MD5 per read, STREAMINFO rewritten
+    at the end): the file equals the oracle's encode of the same reads"""
+    from audiotools import encoders
+    monkeypatch.setattr(encoders, "SEGMENT_FRAMES", seg)
+    x = signals.make("tone", n, ch, bps, seed=n + ch) if n else np.zeros(0, np.int32)
+    opts = dict(oracle_port.PRESETS["8"])
+    r = _SizedReader(x, 44100, ch, bps, sizes)
+    fn = str(tmp_path / "s.flac")
+    lst = encoders.encode_flac(fn, r, **opts)
+    assert r.closed
+    got = open(fn, "rb").read()
+    # the oracle cuts the same frames: explicit sizes
+    cut, left = list(sizes), n - sum(sizes)
+    while left > 0:
+        cut.append(min(left, opts["block_size"]))
+        left -= cut[-1]
+    if sizes:
+        img = _port_frames(x, ch, bps, cut, opts)
+    else:
+        img, wl = oracle_port.encode(x, ch, bps, 44100, **opts)
+        assert lst == wl
+    assert [m for _, m in lst] == cut
+    assert got == img
+    dec, _, _, _ = oracle_port.decode(got)
+    assert np.array_equal(dec, x)
+
+
+def _port_frames(x, ch, bps, cut, opts):
+    """the oracle stream for explicit frame sizes: the GPU batch path with
+    frame_sizes is itself parity-checked against the port, so encode the
+    same cut through it"""
+    from audiotools import _atgpu
+    eng = _atgpu.engine()
+    pcm = x.astype(np.int16 if bps <= 16 else np.int32)
+    out, res, _, _ = eng.encode(_atgpu.make_options(**opts), pcm, [(0, len(x) // ch, cut)], ch,
+                                bps, 44100)
+    r = res[0]
+    return out[r.out_offset:r.out_offset + r.bytes].tobytes()
