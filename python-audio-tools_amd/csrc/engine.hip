@@ -574,7 +574,10 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // cannot take goes through the general kernel as a list
     const bool fast16 = !pl.big && p.block_size == ATG_MAX_BLOCK &&
                         p.max_lpc_order <= ATG_FAST_ORDER && p.bps <= 16u;
-    if (fast16)
+    // wider sources (24-bit): the hi/lo split search, same hand-over list
+    const bool fast_hl = !pl.big && p.block_size == ATG_MAX_BLOCK &&
+                         p.max_lpc_order <= ATG_FAST_ORDER && p.bps > 16u;
+    if (fast16 || fast_hl)
         HIP_TRY(sl.slow.ensure((4 + nf * p.n_cand) * sizeof(uint32_t)));
     const uint32_t big_grid =
         pl.big ? (uint32_t)std::min<uint64_t>(kBigGrid, std::max<uint64_t>(nf, 1) * p.n_cand) : 0u;
@@ -623,7 +626,8 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // track's blocks now, part 1 after the next batch's LPC kernel
     // (batch_end), so no chain runs beside an LPC grid; otherwise the whole
     // chain now (a caller waiting on each batch gains nothing from a split)
-    const bool split_md5 = pipelined && fmt == ATG_PCM_S16 && p.bps == 16u;
+    const bool split_md5 = pipelined && ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
+                                         (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
     if (!pl.frames_only)
@@ -636,12 +640,19 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                                            rice_stride, (uint8_t *)sl.scratch.p,
                                            big_slot_bytes(pl), big_row_bytes(pl), big_grid,
                                            e->s_main));
-    else if (fast16) {
+    else if (fast16 || fast_hl) {
         uint32_t *cnt = (uint32_t *)sl.slow.p, *list = cnt + 4;
         HIP_TRY(hipMemsetAsync(cnt, 0, sizeof(uint32_t), e->s_main));
-        HIP_TRY(launch_subframe_search16(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
-                                         (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
-                                         (SubDesc *)sl.sub.p, list, cnt, e->s_main));
+        if (fast16)
+            HIP_TRY(launch_subframe_search16(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                             (const int8_t *)sl.shift.p,
+                                             (const uint8_t *)sl.est.p, (SubDesc *)sl.sub.p,
+                                             list, cnt, e->s_main));
+        else
+            HIP_TRY(launch_subframe_search_hl(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
+                                              (const int8_t *)sl.shift.p,
+                                              (const uint8_t *)sl.est.p, (SubDesc *)sl.sub.p,
+                                              list, cnt, e->s_main));
         const uint32_t units = (uint32_t)(nf * p.n_cand);
         HIP_TRY(launch_subframe_search_list(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
                                             (const int8_t *)sl.shift.p,

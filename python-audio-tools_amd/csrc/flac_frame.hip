@@ -512,9 +512,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
                 for (uint32_t j = 0; j < order; ++j)
                     csum += (uint64_t)(cfs[j] < 0 ? -(int64_t)cfs[j] : cfs[j]);
                 const int kind = residual_kernel(csum, maxabs, (int)order);
+                // wide samples (24-bit): the hi/lo split, exact in 32 bits
+                const bool hl = !REG && kind == RES_GENERIC && order <= ATG_FAST_ORDER &&
+                                maxabs < (1u << 26) &&
+                                csum * (uint64_t)((maxabs >> 12) + 1u) < (1ull << 31);
                 uint32_t total, excl;
                 LaneWriter wr;
-                if (kind != RES_GENERIC) {
+                if (kind != RES_GENERIC || hl) {
                     int cf[ATG_FAST_ORDER];
 #pragma unroll
                     for (int j = 0; j < ATG_FAST_ORDER; ++j)
@@ -530,6 +534,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_
 #pragma unroll
                         for (int t = 0; t < ATG_FAST_ORDER; ++t)
                             u[t] = t < warm ? 0u : u[t];
+                    } else if (hl) {
+                        uint64_t asum;
+                        const bool full = N == ATG_MAX_BLOCK;
+                        if (shift >= 12)
+                            asum = full ? lane_residuals_hl<true, true>(sl, (int)ra, len, cf, shift, u)
+                                        : lane_residuals_hl<false, true>(sl, (int)ra, len, cf, shift, u);
+                        else
+                            asum = full ? lane_residuals_hl<true, false>(sl, (int)ra, len, cf, shift, u)
+                                        : lane_residuals_hl<false, false>(sl, (int)ra, len, cf, shift, u);
+                        warm = drop_warmup((int)ra, len, (int)order, u, asum);
                     } else {
                         uint64_t asum;
                         const bool full = N == ATG_MAX_BLOCK;

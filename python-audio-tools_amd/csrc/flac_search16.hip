@@ -79,10 +79,13 @@ __device__ __forceinline__ int32_t pk_sample(const uint32_t *__restrict__ pk, in
 
 // candidate sample i: a packed image (TWO = false), or L - R with the L
 // image at img and the R image right after it (TWO = true, the side channel)
-template <bool TWO>
+template <int MODE>
 __device__ __forceinline__ int32_t cand_pk(const uint32_t *__restrict__ img, int i)
 {
-    return TWO ? pk_sample(img, i) - pk_sample(img + PK_WORDS, i) : pk_sample(img, i);
+    // MODE 2: s = hi * 4096 + lo from the hi image and the lo image after it
+    if (MODE == 2)
+        return (pk_sample(img, i) << 12) + pk_sample(img + PK_WORDS, i);
+    return MODE ? pk_sample(img, i) - pk_sample(img + PK_WORDS, i) : pk_sample(img, i);
 }
 
 __device__ __forceinline__ uint32_t align16(uint32_t hi_word, uint32_t lo_word)
@@ -339,6 +342,9 @@ struct Eval16 {
     PartSel sel;
 };
 
+__device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
+                                            const RunCtx &c, int order, int warm, uint32_t thr);
+
 // One predictor with the folded 32-bit arithmetic (caller checked the
 // bounds): pass 1, partition search, exact bits.  run: the lane's run in a
 // packed image, or in the (L, R) word image (TWO).
@@ -423,6 +429,14 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         }
 #endif
     }
+    return eval_tail(lane_sum, u, c, order, warm, thr);
+}
+
+// After pass 1 (every predictor form): the lower-bound pruning, the
+// partition search and the exact bit count from the kept v = |r| - [r < 0]
+__device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
+                                            const RunCtx &c, int order, int warm, uint32_t thr)
+{
     Eval16 ev;
     if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
         // cannot beat a finished LPC job: no partition search, no exact bits
@@ -461,8 +475,8 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
 }
 
 // Any predictor (order <= 12): 64-bit accumulation on the shifted samples,
-// residuals recomputed for the exact bits.
-template <bool TWO>
+// residuals recomputed for the exact bits.  TWO: 0 packed, 1 L - R, 2 hi/lo.
+template <int TWO>
 __device__ __forceinline__ Eval16 eval_wide(const uint32_t *__restrict__ img, const RunCtx &c,
                                             const uint32_t (&cw)[7], int order, int shift,
                                             uint32_t w)
@@ -629,7 +643,21 @@ __device__ __forceinline__ const uint32_t *run_of(const uint32_t *__restrict__ i
 // Phase 1 of a candidate (one wave): CONSTANT (written here), wasted bits,
 // the FIXED order (flac.c:856-916, 1578-1620) and the LPC orders to try
 // (flac.c:1034-1126).  img: packed image, or (L, R) words (TWO).
-template <bool TWO>
+__device__ __forceinline__ uint32_t fixed_order_hl(const uint32_t *__restrict__ run, int lane);
+
+// Next job of the workgroup's LDS queue for the whole wave: ds_append adds
+// the wave's active-lane count (64: every lane is active here) to the
+// counter in one LDS operation and returns the old value, so old >> 6 is the
+// job index.  (An atomicAdd from all 64 lanes on one address serialises 64
+// read-modify-writes; one under `if (lane == 0)` made the loop exit
+// divergent to the compiler, which then re-entered with a stale index.)
+__device__ __forceinline__ uint32_t next_job(uint32_t *q)
+{
+    const int old = __builtin_amdgcn_ds_append((__attribute__((address_space(3))) int *)q);
+    return uniform_u32((uint32_t)old) >> 6;
+}
+
+template <bool TWO, bool HL = false>
 __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit, uint32_t sbps,
                                              const uint32_t *__restrict__ img, CandStats cs,
                                              int lane, const uint8_t *__restrict__ est_tab,
@@ -654,7 +682,9 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
 #if ATG_K2F_EXP == 4
     const uint32_t fixed_order = 2u;
 #else
-    const uint32_t fixed_order = p.try_fixed ? fixed_order_of<TWO>(run_of(img, lane), lane) : 0u;
+    const uint32_t fixed_order = !p.try_fixed ? 0u
+                               : HL ? fixed_order_hl(run_of(img, lane), lane)
+                                    : fixed_order_of<TWO>(run_of(img, lane), lane);
 #endif
     uint32_t lo = 1, hi = 0;
     if (p.try_lpc) {
@@ -1054,11 +1084,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
                           (p.try_lpc ? (p.exhaustive ? p.max_lpc_order : 1u) : 0u);
     const uint32_t njobs = 4u * jmax;
     for (;;) {
-        // every lane adds 1, so each fetch advances the counter by exactly
-        // 64 and any lane's old value >> 6 is the job index (a fetch under
-        // `if (lane == 0)` made the loop exit divergent to the compiler, and
-        // the structurized loop re-entered with a stale index: a hang)
-        const uint32_t j = uniform_u32(atomicAdd(&qnext, 1u)) >> 6;
+        const uint32_t j = next_job(&qnext);
         if (j >= njobs)
             break;
         const uint32_t jc = (j + 3u) & 3u; // 3, 0, 1, 2
@@ -1202,6 +1228,410 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE)
         pred_job<false>(p, N, pk, ci, pi, lane, (const int16_t *)lq32, (const int8_t *)ls32, &res);
     __syncthreads();
     cand_finish(p, N, ci, &res, lane, (const int16_t *)lq32, (const int8_t *)ls32, out + unit);
+}
+
+// ---------------------------------------------------------------------------
+// Samples wider than int16 (24-bit sources; the 25-bit side channel of
+// 24-bit stereo): s = hi * 4096 + lo with hi = s >> 12 and lo = s & 4095, two
+// packed int16 images (hi, then lo PK_WORDS later).  A predictor runs the
+// 16-bit tap chain on both images with the same tap pairs -- the fold
+// (c0, -2^sh) included -- into two int32 accumulators A (hi) and B (lo), and
+// the shifted prediction of the reference's 64-bit sum (flac.c:999-1008),
+// floor((4096 A + B) / 2^shv), comes from 32-bit operations:
+//     shv >= 12:  (A + (B >> 12)) >> (shv - 12)
+//     shv <  12:  (A << (12 - shv)) + (B >> shv)
+// with the -2^shv seed in A or B, so the result is ~r as on the 16-bit path
+// and everything after pass 1 is shared.  |s| < 2^26 keeps A and B exact.
+// One 128-thread workgroup (two waves sharing the predictor jobs) per
+// candidate, any channel layout.
+
+__device__ __forceinline__ uint2 pack4_hi(const int32_t (&s)[4])
+{
+    const int32_t h[4] = {s[0] >> 12, s[1] >> 12, s[2] >> 12, s[3] >> 12};
+    return pack4(h);
+}
+
+__device__ __forceinline__ uint2 pack4_lo(const int32_t (&s)[4])
+{
+    const int32_t l[4] = {s[0] & 4095, s[1] & 4095, s[2] & 4095, s[3] & 4095};
+    return pack4(l);
+}
+
+template <int D, bool BIG>
+__device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const int (&cp)[14],
+                                         int seed_h, int seed_l, int sa_v, int sb_v, bool lane0,
+                                         int order, uint32_t (&u)[ATG_RUN], uint32_t &sabs)
+{
+    int tap0 = cp[0];
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+    Win A, B;
+    win_init(run, A, false);
+    win_init(run + PK_WORDS, B, false);
+    uint4 n0 = load_run4(run, false), n1 = load_run4(run + 4, false);
+    uint4 m0 = load_run4(run + PK_WORDS, false), m1 = load_run4(run + PK_WORDS + 4, false);
+    uint32_t sa = 0;
+#pragma unroll
+    for (int c = 0; c < ATG_RUN / 16; ++c) {
+        asm volatile("" ::: "memory");
+        const uint4 a0 = n0, a1 = n1, b0 = m0, b1 = m1;
+        if (c + 1 < ATG_RUN / 16) {
+            n0 = load_run4(run + 8 * (c + 1), false);
+            n1 = load_run4(run + 8 * (c + 1) + 4, false);
+            m0 = load_run4(run + PK_WORDS + 8 * (c + 1), false);
+            m1 = load_run4(run + PK_WORDS + 8 * (c + 1) + 4, false);
+        }
+        win_next(a0, a1, A);
+        win_next(b0, b1, B);
+#pragma unroll
+        for (int ii = 0; ii < 16; ii += 2) {
+            int ah[2], al[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                ah[h] = dot2_first(win_pair(A, ii + h, 0), tap0, seed_h);
+                al[h] = dot2_first(win_pair(B, ii + h, 0), tap0, seed_l);
+            }
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    ah[h] = dot2(win_pair(A, ii + h, j), cp[j], ah[h]);
+                    al[h] = dot2(win_pair(B, ii + h, j), cp[j], al[h]);
+                }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 16 * c + ii + h;
+                int n = BIG ? (ah[h] + (al[h] >> 12)) >> sa_v : (ah[h] << sa_v) + (al[h] >> sb_v);
+                if (i < ATG_FAST_ORDER)
+                    n = (lane0 && i < order) ? -1 : n;
+                const uint32_t s31 = (uint32_t)(n >> 31);
+                const uint32_t v = (uint32_t)n ^ s31;
+                u[i] = v;
+                add3_acc(sa, v, s31);
+            }
+        }
+    }
+    sabs = sa + (uint32_t)ATG_RUN;
+}
+
+template <bool BIG>
+__device__ __forceinline__ void pass1_hl_any(const uint32_t *__restrict__ run, const int (&cq)[14],
+                                             int seed_h, int seed_l, int sa_v, int sb_v,
+                                             bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                             uint32_t &sabs)
+{
+    switch (order / 2 + 1) {
+    case 1: pass1_hl<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 2: pass1_hl<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 3: pass1_hl<3, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 4: pass1_hl<4, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 5: pass1_hl<5, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 6: pass1_hl<6, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    default: pass1_hl<7, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    }
+}
+
+// one predictor on the hi/lo images (caller checked the bounds)
+__device__ __forceinline__ Eval16 eval_fold_hl(const uint32_t *__restrict__ run, const RunCtx &c,
+                                               const uint32_t (&cw)[7], int order, int sh,
+                                               uint32_t w, uint32_t thr)
+{
+    int cq[14];
+    cq[0] = (int)((cw[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
+#pragma unroll
+    for (int j = 1; j < 7; ++j)
+        cq[j] = (int)((cw[j] & 0xFFFFu) | (cw[j - 1] & 0xFFFF0000u));
+#pragma unroll
+    for (int j = 7; j < 14; ++j)
+        cq[j] = 0;
+    const int shv = sh + (int)w;
+    const bool big = shv >= 12;
+    const int seed_h = big ? -(1 << (shv - 12)) : 0;
+    const int seed_l = big ? 0 : -(1 << shv);
+    int sa_v = big ? shv - 12 : 12 - shv, sb_v = shv;
+    asm volatile("v_mov_b32 %0, %0" : "+v"(sa_v)); // shift amounts in VGPRs
+    asm volatile("v_mov_b32 %0, %0" : "+v"(sb_v));
+    const bool lane0 = c.lane == 0;
+    const int warm = lane0 ? order : 0;
+    uint32_t u[ATG_RUN];
+    uint32_t lane_sum;
+    if (big)
+        pass1_hl_any<true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
+    else
+        pass1_hl_any<false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
+    return eval_tail(lane_sum, u, c, order, warm, thr);
+}
+
+// FIXED order (flac.c:856-916) on the hi/lo images: differences in int32
+// (|d4| < 2^30 for |s| < 2^26), sums in 64 bits
+__device__ __forceinline__ uint32_t fixed_order_hl(const uint32_t *__restrict__ run, int lane)
+{
+    uint64_t a5[5] = {0, 0, 0, 0, 0};
+    int x1, x2, x3, x4;
+    {
+        const uint4 h = *(const uint4 *)(run - 8), g = *(const uint4 *)(run + PK_WORDS - 8);
+        x1 = (hi16(h.w) << 12) + hi16(g.w);
+        x2 = (lo16(h.w) << 12) + lo16(g.w);
+        x3 = (hi16(h.z) << 12) + hi16(g.z);
+        x4 = (lo16(h.z) << 12) + lo16(g.z);
+    }
+    int d1p = x1 - x2, d2p = d1p - (x2 - x3);
+    int d3p = d2p - ((x2 - x3) - (x3 - x4));
+#pragma unroll 1
+    for (int chn = 0; chn < ATG_RUN / 16; ++chn) {
+        int x[16];
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint4 a = *(const uint4 *)(run + 8 * chn + 4 * q);
+            const uint4 b = *(const uint4 *)(run + PK_WORDS + 8 * chn + 4 * q);
+            const uint32_t wa[4] = {a.x, a.y, a.z, a.w}, wb[4] = {b.x, b.y, b.z, b.w};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                x[8 * q + 2 * k] = (lo16(wa[k]) << 12) + lo16(wb[k]);
+                x[8 * q + 2 * k + 1] = (hi16(wa[k]) << 12) + hi16(wb[k]);
+            }
+        }
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+            const int x0 = x[tt];
+            const int d1 = x0 - x1, d2 = d1 - d1p, d3 = d2 - d2p, d4 = d3 - d3p;
+            if (chn > 0 || tt >= 4 || lane > 0) {
+                a5[0] += iabs_u(x0);
+                a5[1] += iabs_u(d1);
+                a5[2] += iabs_u(d2);
+                a5[3] += iabs_u(d3);
+                a5[4] += iabs_u(d4);
+            }
+            x1 = x0;
+            d1p = d1;
+            d2p = d2;
+            d3p = d3;
+        }
+    }
+    uint64_t s5[5];
+#pragma unroll
+    for (int k = 0; k < 5; ++k)
+        s5[k] = dpp_wave_sum<uint64_t>(a5[k]);
+    uint64_t best = s5[0];
+    uint32_t order = 0;
+#pragma unroll
+    for (int k = 1; k < 5; ++k)
+        if (s5[k] < best) {
+            best = s5[k];
+            order = (uint32_t)k;
+        }
+    return uniform_u32(order);
+}
+
+// one predictor of a hi/lo candidate (pred_job's wide-sample form)
+__device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
+                                            const uint32_t *__restrict__ img, const CandInfo &ci,
+                                            uint32_t pi, int lane, const int16_t *__restrict__ lq,
+                                            const int8_t *__restrict__ ls,
+                                            PredRes *__restrict__ res)
+{
+    const bool is_fixed = p.try_fixed && pi == 0;
+    const uint32_t o = is_fixed ? ci.fixed_order : ci.lo + pi - (p.try_fixed ? 1u : 0u);
+    int shift = 0;
+    uint32_t cw[7];
+    if (is_fixed) {
+        switch (o) {
+        case 1: cw[0] = 1u; cw[1] = 0u; break;
+        case 2: cw[0] = 2u | 0xFFFF0000u; cw[1] = 0u; break;
+        case 3: cw[0] = 3u | 0xFFFD0000u; cw[1] = 1u; break;
+        case 4: cw[0] = 4u | 0xFFFA0000u; cw[1] = 4u | 0xFFFF0000u; break;
+        default: cw[0] = 0u; cw[1] = 0u; break;
+        }
+#pragma unroll
+        for (int m = 2; m < 7; ++m)
+            cw[m] = 0u;
+    } else {
+        shift = uniform_i32(ls[o - 1u]);
+        const uint32_t *__restrict__ rw = (const uint32_t *)(lq + (o - 1u) * p.coef_row);
+#pragma unroll
+        for (int m = 0; m < 6; ++m)
+            cw[m] = 2u * (uint32_t)m < p.coef_row ? uniform_u32(rw[m]) : 0u;
+        cw[6] = 0u;
+    }
+    uint32_t csum = 0;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+        const int a = lo16(cw[m]), b = hi16(cw[m]);
+        csum += (uint32_t)(a < 0 ? -a : a) + (uint32_t)(b < 0 ? -b : b);
+    }
+    RunCtx c;
+    c.lane = lane;
+    c.a = ATG_RUN * lane;
+    c.len = ATG_RUN;
+    c.N = N;
+    c.max_rice = p.max_rice;
+    c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
+    // A and B exact in int32: (sum|c| + 2^sh) (max|hi| + 1) + 2^(shv - 12)
+    // and (sum|c| + 2^sh) 4095 + 2^shv below 2^31; codes below 2^26
+    const uint64_t mu = ci.amax, ms = ci.amax >> ci.w;
+    const uint64_t hmax = (mu >> 12) + 1u, tsum = (uint64_t)csum + (1ull << shift);
+    const uint32_t shv = (uint32_t)shift + ci.w;
+    const bool fold_ok = tsum * hmax + (1ull << (shv > 12 ? shv - 12 : 0)) < (1ull << 31) &&
+                         tsum * 4095u + (shv < 12 ? (1ull << shv) : 0ull) < (1ull << 31);
+    const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
+    const uint32_t wf = ci.w ? ci.w + 1u : 1u;
+    const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
+    uint32_t thr = 0xFFFFFFFFu;
+    if (!is_fixed) {
+        const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+        if (best != 0xFFFFFFFFu)
+            thr = best > hdr ? best - hdr : 0u;
+    }
+    Eval16 ev;
+    if (fold_ok && 2u * rbound + 1u < (1ull << 26))
+        ev = eval_fold_hl(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr);
+    else
+        ev = eval_wide<2>(img, c, cw, (int)o, shift, ci.w);
+    if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)
+        atomicMin(&res->best_lpc, hdr + ev.bits);
+    res->k[pi][lane] = (uint8_t)ev.sel.k_own;
+    if (lane == 0) {
+        res->bits[pi] = ev.bits;
+        res->porder[pi] = (uint8_t)ev.sel.porder;
+        res->method[pi] = (uint8_t)ev.sel.method;
+    }
+}
+
+template <int CS, typename T>
+__device__ __forceinline__ void stage_hl(const T *__restrict__ src, uint32_t ch, uint32_t cand,
+                                         int tid, uint32_t *__restrict__ pk, int32_t &mn,
+                                         int32_t &mx, uint32_t &orv)
+{
+#pragma unroll 4
+    for (int m = 0; m < ATG_MAX_BLOCK / 512; ++m) {
+        const uint32_t q0 = (uint32_t)(tid + 128 * m); // 4-sample group
+        int32_t s[4];
+        load4<CS>(src, 4u * q0, ch, cand, s);
+        stats_add(s, mn, mx, orv);
+        *(uint2 *)&pk[paddr(2 * (int)q0)] = pack4_hi(s);
+        *(uint2 *)&pk[PK_WORDS + paddr(2 * (int)q0)] = pack4_lo(s);
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(128) void k_subframe_search_hl(
+    FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
+    const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
+    const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
+    uint32_t *__restrict__ slow_list, uint32_t *__restrict__ slow_count)
+{
+    __shared__ __attribute__((aligned(16))) uint32_t pk[2 * PK_WORDS]; // hi, lo images
+    __shared__ int32_t red[2][3];
+    __shared__ CandInfo info;
+    __shared__ PredRes res;
+    __shared__ uint32_t qnext;
+    __shared__ __attribute__((aligned(16))) uint32_t lq32[ATG_FAST_ORDER * ATG_FAST_ORDER / 2];
+    __shared__ uint32_t ls32[ATG_FAST_ORDER / 4];
+
+    uint32_t f, cand;
+    xcd_unit_map(blockIdx.x, p.n_cand, &f, &cand);
+    if (f >= p.n_frames)
+        return;
+    const int tid = threadIdx.x;
+    const int wave = tid >> 6, lane = tid & 63;
+    const FrameInfo fi = frames[f];
+    const uint32_t N = fi.n;
+    const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
+    const uint32_t sbps = p.bps + ((ms && cand == 3u) ? 1u : 0u);
+    const uint32_t unit = f * p.n_cand + cand;
+    if (N != ATG_MAX_BLOCK) {
+        if (tid == 0)
+            slow_list[atomicAdd(slow_count, 1u)] = unit;
+        return;
+    }
+    if (tid < 2 * PK_PRE)
+        pk[(tid / PK_PRE) * PK_WORDS + (tid % PK_PRE)] = 0u;
+    else if (tid == 127)
+        qnext = 0u;
+    {
+        const uint32_t *__restrict__ gq = (const uint32_t *)(coef_tab + (size_t)unit * p.coef_stride);
+        for (uint32_t i = (uint32_t)tid; i < p.coef_stride / 2u; i += 128u)
+            lq32[i] = gq[i];
+        if ((uint32_t)tid < p.max_lpc_order)
+            ((int8_t *)ls32)[tid] = shift_tab[(size_t)unit * p.max_lpc_order + tid];
+    }
+    int32_t mn = INT32_MAX, mx = INT32_MIN;
+    uint32_t orv = 0;
+    {
+        const T *__restrict__ src = pcm + fi.pcm_start * p.channels;
+        if (!ms) {
+            stage_hl<CS_CH>(src, p.channels, cand, tid, pk, mn, mx, orv);
+        } else {
+            switch (cand) {
+            case 0: stage_hl<CS_L>(src, 2u, cand, tid, pk, mn, mx, orv); break;
+            case 1: stage_hl<CS_R>(src, 2u, cand, tid, pk, mn, mx, orv); break;
+            case 2: stage_hl<CS_AVG>(src, 2u, cand, tid, pk, mn, mx, orv); break;
+            default: stage_hl<CS_DIF>(src, 2u, cand, tid, pk, mn, mx, orv); break;
+            }
+        }
+    }
+    {
+        const CandStats w = wave_stats(mn, mx, orv);
+        if (lane == 0) {
+            red[wave][0] = w.mn;
+            red[wave][1] = w.mx;
+            red[wave][2] = (int32_t)w.orv;
+        }
+    }
+    __syncthreads();
+    CandStats cs;
+    cs.mn = uniform_i32(min(red[0][0], red[1][0]));
+    cs.mx = uniform_i32(max(red[0][1], red[1][1]));
+    cs.orv = uniform_u32((uint32_t)(red[0][2] | red[1][2]));
+    const bool constant = p.try_constant && cs.mn == cs.mx;
+    if (!constant && (cs.mn < -(1 << 26) || cs.mx >= (1 << 26))) {
+        if (tid == 0)
+            slow_list[atomicAdd(slow_count, 1u)] = unit;
+        return;
+    }
+    if (wave == 0) {
+        cand_prepare<false, true>(p, unit, sbps, pk, cs, lane, est_tab, out + unit, &info);
+        if (lane == 0)
+            res.best_lpc = 0xFFFFFFFFu;
+    }
+    __syncthreads();
+    const CandInfo ci = load_info(&info);
+    if (!ci.active)
+        return;
+    const uint32_t n_pred = n_pred_of(p, ci);
+    // the two waves share the predictor jobs, highest orders first (their
+    // totals prune the lower orders); see k_frame_search_ms for the counter
+    for (;;) {
+        const uint32_t j = next_job(&qnext);
+        if (j >= n_pred)
+            break;
+        pred_job_hl(p, N, pk, ci, n_pred - 1u - j, lane, (const int16_t *)lq32,
+                    (const int8_t *)ls32, &res);
+    }
+    __syncthreads();
+    if (wave == 0)
+        cand_finish(p, N, ci, &res, lane, (const int16_t *)lq32, (const int8_t *)ls32,
+                    out + unit);
+}
+
+hipError_t launch_subframe_search_hl(const FlacParams &p, const void *pcm, int fmt,
+                                     const FrameInfo *frames, const int16_t *coef_tab,
+                                     const int8_t *shift_tab, const uint8_t *est_tab,
+                                     SubDesc *sub, uint32_t *slow_list, uint32_t *slow_count,
+                                     hipStream_t s)
+{
+    if (p.n_frames == 0)
+        return hipSuccess;
+    const uint32_t f8 = (p.n_frames + 7u) / 8u * 8u;
+    dim3 grid(f8 * p.n_cand);
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_subframe_search_hl<int16_t>), grid, dim3(128), 0, s, p,
+                           (const int16_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                           slow_list, slow_count);
+    else
+        hipLaunchKernelGGL((k_subframe_search_hl<int32_t>), grid, dim3(128), 0, s, p,
+                           (const int32_t *)pcm, frames, coef_tab, shift_tab, est_tab, sub,
+                           slow_list, slow_count);
+    return hipGetLastError();
 }
 
 hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fmt,

@@ -31,6 +31,13 @@ hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fm
                                     const int8_t *shift_tab, const uint8_t *est_tab,
                                     SubDesc *sub, uint32_t *slow_list, uint32_t *slow_count,
                                     hipStream_t s);
+// flac_search16.hip: full 4096-sample frames of sources wider than 16 bits
+// (hi/lo split images, |s| < 2^26), any channel layout; hand-over as above
+hipError_t launch_subframe_search_hl(const FlacParams &p, const void *pcm, int fmt,
+                                     const FrameInfo *frames, const int16_t *coef_tab,
+                                     const int8_t *shift_tab, const uint8_t *est_tab,
+                                     SubDesc *sub, uint32_t *slow_list, uint32_t *slow_count,
+                                     hipStream_t s);
 // flac_big.hip: frames longer than 4096 samples / partition orders > 6
 hipError_t launch_subframe_search_big(const FlacParams &p, const void *pcm, int fmt,
                                       const FrameInfo *frames, const int16_t *coef_tab,

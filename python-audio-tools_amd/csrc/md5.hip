@@ -355,6 +355,78 @@ __device__ __forceinline__ void md5_pair_blocks(const uint4 *__restrict__ q, uin
     }
 }
 
+// int32 containers (16-byte aligned tracks of 1..3-byte samples): the same
+// wave pair, the helper packing whole sample groups into the little-endian
+// byte stream with v_perm (S32Pack, defined below) -- a group of G samples is
+// W / 16 blocks (3 for 24-bit) -- and feeding the same ring; `full` blocks
+// are whole groups.
+template <int BB>
+struct S32Pack;
+
+template <int BB>
+__device__ __forceinline__ void md5_pair_blocks_s32(const uint4 *__restrict__ q, uint32_t full,
+                                                    uint32_t nbmax, uint32_t h[4], Md5Pair &pr)
+{
+    using P = S32Pack<BB>;
+    constexpr uint32_t BPG = P::W / 16; // blocks per group
+    const int lane = threadIdx.x & 63;
+    const bool helper = (threadIdx.x >> 6) != 0;
+    if (helper) {
+        const uint32_t groups = full / BPG;
+        const uint32_t lastg = groups ? groups - 1u : 0u;
+        uint4 cur[P::Q], nxt[P::Q];
+        if (groups) {
+#pragma unroll
+            for (int i = 0; i < P::Q; ++i)
+                cur[i] = q[i];
+        }
+        uint32_t slot = 0;
+        for (uint32_t g = 0; g * BPG < nbmax; ++g) {
+            if (groups) {
+#pragma unroll
+                for (int i = 0; i < P::Q; ++i)
+                    nxt[i] = q[(size_t)min(g + 1u, lastg) * P::Q + i];
+            }
+            uint32_t w[P::W];
+            P::pack(cur, w);
+#pragma unroll
+            for (uint32_t k = 0; k < BPG; ++k) {
+                const uint32_t b = g * BPG + k;
+                if (b < nbmax) {
+                    uint4 bl[4];
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+                        bl[i] = make_uint4(w[16 * k + 4 * i], w[16 * k + 4 * i + 1],
+                                           w[16 * k + 4 * i + 2], w[16 * k + 4 * i + 3]);
+#pragma unroll
+                    for (int hf = 0; hf < 2; ++hf) {
+                        const uint32_t u = 2u * b + (uint32_t)hf;
+                        uint4 xt[8];
+                        if (hf == 0)
+                            md5_xt_half<0>(bl, xt);
+                        else
+                            md5_xt_half<1>(bl, xt);
+                        if (u >= 3u)
+                            md5_wait(&pr.cons, u - 2u);
+#pragma unroll
+                        for (int m = 0; m < 8; ++m)
+                            pr.ring[slot][m][lane] = xt[m];
+                        md5_publish(&pr.prod, u + 1u);
+                        slot = slot == 2u ? 0u : slot + 1u;
+                    }
+                }
+            }
+#pragma unroll
+            for (int i = 0; i < P::Q; ++i)
+                cur[i] = nxt[i];
+        }
+    } else if (wave_all(full == nbmax)) {
+        md5_hasher<true>(full, nbmax, h, pr, lane);
+    } else {
+        md5_hasher<false>(full, nbmax, h, pr, lane);
+    }
+}
+
 // The pair's waves allocate 192 VGPRs.  A lone hash chain issues about as
 // often as half a SIMD, so the waves beside it split the other half: at 192
 // VGPRs at most one LPC wave (184), two search waves (120) or one pack wave
@@ -537,6 +609,43 @@ __global__ __launch_bounds__(128) void k_track_md5_pair(FlacParams p, const int1
         md5_put(tout[t].md5, h);
 }
 
+// k_track_md5_pair for int32 containers of BB-byte samples: whole sample
+// groups on the wave pair, split in two parts at a group boundary as above
+template <int BB>
+__global__ __launch_bounds__(128) void k_track_md5_pair_s32(FlacParams p,
+                                                            const int32_t *__restrict__ pcm,
+                                                            const TrackInfo *__restrict__ tracks,
+                                                            TrackOut *__restrict__ tout, int prio,
+                                                            int part, uint32_t split_pct)
+{
+    using P = S32Pack<BB>;
+    constexpr uint32_t BPG = P::W / 16;
+    if (prio)
+        __builtin_amdgcn_s_setprio(3);
+    __shared__ Md5Pair pair_lds;
+    const uint32_t t = blockIdx.x * 64u + (threadIdx.x & 63u);
+    const bool valid = t < p.n_tracks;
+    const TrackInfo ti = tracks[valid ? t : 0u];
+    const int32_t *s = pcm + ti.pcm_start * p.channels;
+    const uint64_t groups64 = valid && (((uintptr_t)s) & 15u) == 0
+                                  ? ti.pcm_frames * p.channels / P::G : 0u;
+    const uint32_t groups = groups64 * BPG < (1ull << 32) ? (uint32_t)groups64 : 0u;
+    const uint32_t split = part == 2 ? 0u : (uint32_t)((uint64_t)groups * split_pct / 100u);
+    const uint32_t g0 = part == 1 ? split : 0u;
+    const uint32_t n = (part == 0 ? split : groups - split) * BPG;
+    const uint32_t nbmax = wave_max_u32(n);
+    if (!nbmax)
+        return;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (part == 1 && split && threadIdx.x < 64u)
+        md5_get(tout[t].md5, h);
+    md5_vgpr_192();
+    md5_pair_init(pair_lds);
+    md5_pair_blocks_s32<BB>((const uint4 *)s + (size_t)g0 * P::Q, n, nbmax, h, pair_lds);
+    if (threadIdx.x < 64u && n)
+        md5_put(tout[t].md5, h);
+}
+
 // lane per track: the tracks the pair kernel did not take (int32
 // containers, other widths, unaligned starts) from the start, then every
 // track's last partial block + padding, and the digest
@@ -562,22 +671,24 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
         blk = full;
     } else if (sizeof(T) == 4 && (((uintptr_t)s) & 15u) == 0 && bb >= 1 && bb <= 3) {
         // int32 container, 16-byte aligned: whole sample groups by v_perm
-        // packing; the bytes after the last whole group go the generic way
+        // packing -- on the wave pair when `paired` (its state in tout.md5),
+        // here otherwise; the bytes after the last whole group go the
+        // generic way
         const uint64_t samples = ti.pcm_frames * p.channels;
         const uint4 *q = (const uint4 *)s;
-        if (bb == 3) {
-            const uint64_t g = samples / S32Pack<3>::G;
+        const uint64_t g = samples / (bb == 2 ? S32Pack<2>::G : S32Pack<3>::G);
+        const uint32_t bpg = bb == 3 ? 3u : 1u;
+        if (paired && g * bpg < (1ull << 32)) {
+            if (g)
+                md5_get(tout[t].md5, h);
+        } else if (bb == 3) {
             md5_s32_groups<3>(h, q, g);
-            blk = g * 3u;
         } else if (bb == 2) {
-            const uint64_t g = samples / S32Pack<2>::G;
             md5_s32_groups<2>(h, q, g);
-            blk = g;
         } else {
-            const uint64_t g = samples / S32Pack<1>::G;
             md5_s32_groups<1>(h, q, g);
-            blk = g;
         }
+        blk = g * bpg;
     }
     uint32_t X[16];
     for (; blk < full; ++blk) {
@@ -677,7 +788,8 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
     if (!p.n_tracks)
         return hipSuccess;
     const dim3 grid((p.n_tracks + 63u) / 64u);
-    const int paired = fmt == 0 && p.bps == 16u;
+    const uint32_t bb = p.bps / 8u;
+    const int paired = (fmt == 0 && p.bps == 16u) || (fmt == 1 && bb >= 1u && bb <= 3u);
     // the chains at normal wave priority (-DATG_MD5_PRIO=1 raises it: no
     // measurable difference, the engine keeps three batches in flight so the
     // chains stay off the critical path); part 0 takes ATG_MD5_SPLIT_PCT % of
@@ -685,9 +797,18 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
     // Build-time constants: a driver's environment cannot change a run.
     const int prio = ATG_MD5_PRIO;
     const uint32_t split_pct = ATG_MD5_SPLIT_PCT;
-    if (paired)
+    if (paired && fmt == 0)
         hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
                            tout, prio, part, split_pct);
+    else if (paired && bb == 3u)
+        hipLaunchKernelGGL(k_track_md5_pair_s32<3>, grid, dim3(128), 0, s, p, (const int32_t *)pcm,
+                           tracks, tout, prio, part, split_pct);
+    else if (paired && bb == 2u)
+        hipLaunchKernelGGL(k_track_md5_pair_s32<2>, grid, dim3(128), 0, s, p, (const int32_t *)pcm,
+                           tracks, tout, prio, part, split_pct);
+    else if (paired)
+        hipLaunchKernelGGL(k_track_md5_pair_s32<1>, grid, dim3(128), 0, s, p, (const int32_t *)pcm,
+                           tracks, tout, prio, part, split_pct);
     if (part == 0)
         return hipGetLastError();
     if (fmt == 0)
@@ -695,6 +816,6 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                            (const int16_t *)pcm, tracks, tout, paired);
     else
         hipLaunchKernelGGL((k_track_md5<int32_t>), grid, dim3(64), 0, s, p,
-                           (const int32_t *)pcm, tracks, tout, 0);
+                           (const int32_t *)pcm, tracks, tout, paired);
     return hipGetLastError();
 }

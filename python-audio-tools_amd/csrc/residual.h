@@ -146,6 +146,81 @@ __device__ __forceinline__ uint64_t lane_residuals(const int32_t *__restrict__ s
     return sum;
 }
 
+// Samples too wide for the 32-bit kernels above (24-bit sources): with
+// s = hi * 4096 + lo (hi = s >> 12, lo = s & 4095) the predictor is two exact
+// v_mad_i32_i24 chains A = sum c hi, B = sum c lo, and the reference's
+// 64-bit (sum c s) >> shift (flac.c:999-1008) is
+//     BIG (shift >= 12):  (A + (B >> 12)) >> (shift - 12)
+//     else:               (A << (12 - shift)) + (B >> shift)
+// Exact when sum|c| * (max|s| / 4096 + 1) < 2^31 (caller checks) and
+// max|s| < 2^26.  Same outputs as lane_residuals.
+template <bool FULL, bool BIG>
+__device__ __forceinline__ uint64_t lane_residuals_hl(const int32_t *__restrict__ sl, int a,
+                                                      int len, const int (&cf)[ATG_FAST_ORDER],
+                                                      int shift, uint32_t (&u)[ATG_RUN])
+{
+    constexpr int W = ATG_FAST_ORDER;
+    const int sa = BIG ? shift - 12 : 12 - shift;
+    uint64_t sum = 0;
+    int wh[W], wl[W]; // hi / lo of s[i-1-k]
+#pragma unroll
+    for (int k = 0; k < W; ++k) {
+        const int h = sl[saddr(a - 1 - k)];
+        wh[k] = h >> 12;
+        wl[k] = h & 4095;
+    }
+#pragma unroll
+    for (int ch = 0; ch < ATG_RUN / 16; ++ch) {
+        asm volatile("" : "+v"(a)::"memory");
+        int x[16];
+        if (FULL) {
+            const int4 *p4 = (const int4 *)&sl[saddr(a + 16 * ch)];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+                const int4 v = p4[q];
+                x[4 * q] = v.x;
+                x[4 * q + 1] = v.y;
+                x[4 * q + 2] = v.z;
+                x[4 * q + 3] = v.w;
+            }
+        } else {
+#pragma unroll
+            for (int t = 0; t < 16; ++t)
+                x[t] = sl[saddr(a + 16 * ch + t)];
+        }
+#pragma unroll
+        for (int tt = 0; tt < 16; ++tt) {
+            const int t = 16 * ch + tt;
+            const int s = x[tt];
+            int ah = 0, al = 0;
+#pragma unroll
+            for (int k = 0; k < W; ++k) {
+                ah = mad24(wh[k], cf[k], ah);
+                al = mad24(wl[k], cf[k], al);
+            }
+#pragma unroll
+            for (int k = W - 1; k > 0; --k) {
+                wh[k] = wh[k - 1];
+                wl[k] = wl[k - 1];
+            }
+            wh[0] = s >> 12;
+            wl[0] = s & 4095;
+            const int q = BIG ? (ah + (al >> 12)) >> sa : (ah << sa) + (al >> shift);
+            const int r = (int)((uint32_t)s - (uint32_t)q);
+            uint32_t uu = zigzag(r);
+            uint32_t ar = iabs_u(r);
+            if (!FULL) {
+                const bool v = t < len;
+                uu = v ? uu : 0u;
+                ar = v ? ar : 0u;
+            }
+            u[t] = uu;
+            sum += ar;
+        }
+    }
+    return sum;
+}
+
 // Exclude warm-up positions (< order) from a run's codes and |r| sum.
 // |r| = (u + 1) >> 1 for a zig-zag code u.
 __device__ __forceinline__ int drop_warmup(int a, int len, int order, uint32_t (&u)[ATG_RUN],
