@@ -100,6 +100,19 @@ def _frames(d):
         out.append(np.asarray(fl.samples).copy())
 
 
+def _outcome(d):
+    """(frames read, the exception type and message that ended the stream)"""
+    out = []
+    try:
+        while True:
+            fl = d.read(4096)
+            if not len(fl):
+                return out, None
+            out.append(np.asarray(fl.samples).copy())
+    except (ValueError, IOError) as e:
+        return out, (type(e), str(e))
+
+
 def test_flac_decoder_extension_tone():
     from audiotools import _decoders_c, decoders
     fn = os.path.join(HERE, "golden", "tone.flac")
@@ -121,10 +134,13 @@ def test_flac_decoder_extension_tone():
 def test_flac_decoder_extension_seek_and_errors(tmp_path):
     from audiotools import _decoders_c, decoders
     fn = os.path.join(FIX, "flac-seektable.flac")
-    for target in (0, 1, 44100, 44100 * 3 + 5, 10 ** 9):
+    # the fixture's first seekpoint is (sample 0, byte 1): a seek lands one
+    # byte into the first frame and read() fails there, in both decoders
+    for target in (0, 1, 44100, 438272, 44100 * 30 + 5, 10 ** 9):
         c, p = _decoders_c.FlacDecoder(fn), decoders.FlacDecoder(fn)
         assert c.seek(target) == p.seek(target)
-        fc, fp = _frames(c), _frames(p)
+        (fc, ec), (fp, ep) = _outcome(c), _outcome(p)
+        assert ec == ep
         assert len(fc) == len(fp) and all(np.array_equal(a, b) for a, b in zip(fc, fp))
     # a flipped byte inside a frame: the same error at the same frame
     data = bytearray(open(os.path.join(HERE, "golden", "tone.flac"), "rb").read())
