@@ -44,7 +44,8 @@
 #include "wave.h"
 
 // timing experiments only (tools/gpu_exp.sh), 0 in every product build:
-// 1 FIXED predictor only, 2 no pass 2, 3 trivial partition choice, 4 no FIXED sums
+// 1 FIXED predictor only, 2 no pass 2, 3 trivial partition choice, 4 no FIXED sums,
+// 5 no lower-bound pruning, 6 one tap pair per residual (prediction cost)
 #ifndef ATG_K2F_EXP
 #define ATG_K2F_EXP 0
 #endif
@@ -399,7 +400,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         else
             pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
 #else
-        switch (order / 2 + 1) {
+        switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
         case 1: pass1_lr<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         case 2: pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         case 3: pass1_lr<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
@@ -418,7 +419,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         else
             pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
 #else
-        switch (order / 2 + 1) {
+        switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
         case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         case 3: pass1<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
@@ -771,7 +772,7 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
     uint32_t thr = 0xFFFFFFFFu;
-    if (!is_fixed) {
+    if (!is_fixed && ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
         if (best != 0xFFFFFFFFu)
             thr = best > hdr ? best - hdr : 0u;
@@ -1476,7 +1477,7 @@ __device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
     uint32_t thr = 0xFFFFFFFFu;
-    if (!is_fixed) {
+    if (!is_fixed && ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
         if (best != 0xFFFFFFFFu)
             thr = best > hdr ? best - hdr : 0u;

@@ -1,0 +1,13 @@
+#!/bin/bash
+# Experiment builds of libatgpu.so (exp/libatgpu_<name>.so, NOT byte-exact):
+# the product objects with one source recompiled under extra -D flags.
+#   tools/build_exp.sh <name> <source.hip> <flags...>
+set -e
+R=$(cd "$(dirname "$0")/.." && pwd)
+name=$1; src=$2; shift 2
+C=$R/python-audio-tools_amd/csrc
+make -s -C "$C" -j8 ../audiotools/libatgpu.so
+mkdir -p "$C/obj_$name" "$R/exp"
+cp -p "$C"/obj/*.o "$C/obj_$name/"
+rm -f "$C/obj_$name/${src%.hip}.o"
+make -s -C "$C" OBJDIR="obj_$name" OUT="$R/exp/libatgpu_$name.so" EXTRA="$*" "$R/exp/libatgpu_$name.so"
