@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ATG_ABI_VERSION 2
+#define ATG_ABI_VERSION 3
 
 typedef enum {
     ATG_OK = 0,
@@ -129,6 +129,25 @@ atg_status atg_flac_encode_host(atg_engine *eng, const atg_flac_options *opts,
                                 uint64_t out_cap, atg_track_result *results,
                                 uint64_t *frame_offsets,
                                 uint32_t *frame_pcm_frames);
+
+/* Asynchronous form of atg_flac_encode_host: plans the job, queues its
+   chunks on the pipeline (collecting older chunks, of this or earlier jobs,
+   as stages free up) and returns a ticket; pcm, out, results and the frame
+   arrays must stay valid until atg_flac_encode_host_wait(ticket).  Jobs
+   share the pipeline in submission order, so job k+1's uploads overlap job
+   k's last chunks: back to back, the PCIe link stays busy.  Fails with
+   ATG_ERR_INVALID while an atg_flac_encode_device_async batch is unwaited
+   (and that call fails while a host job is in flight). */
+atg_status atg_flac_encode_host_async(atg_engine *eng, const atg_flac_options *opts,
+                                      const void *pcm, atg_pcm_format format,
+                                      const atg_track *tracks, uint32_t n_tracks,
+                                      uint32_t channels, uint32_t bits_per_sample,
+                                      uint32_t sample_rate, uint8_t *out, uint64_t out_cap,
+                                      atg_track_result *results, uint64_t *frame_offsets,
+                                      uint32_t *frame_pcm_frames, uint64_t *ticket);
+/* Wait for host job `ticket` (and the jobs before it); its results and
+   images are then complete.  A job's ticket can be waited once. */
+atg_status atg_flac_encode_host_wait(atg_engine *eng, uint64_t ticket);
 
 /* Streaming form for ONE track (the reference's frame loop,
    src/encoders/flac.c:244-274, run over bounded segments of a long track):
@@ -442,14 +461,17 @@ atg_status atg_pcm_apply_gain_host(int device, const int32_t *in, int32_t *out,
 /* ALACEncoder_encode_alac -> write_frameset / write_frame /            */
 /* compute_coefficients / calculate_residuals / encode_residuals) for a */
 /* batch of tracks; audiotools.m4a.ALACAudio.from_pcm wraps the mdat in */
-/* the M4A atoms on the host.  Leftweights 0..4, shift 2 (the           */
-/* reference's fixed minimum/maximum_interlacing_leftweight).           */
+/* the M4A atoms on the host.  Interlacing shift 2; leftweights        */
+/* minimum..maximum_interlacing_leftweight (0..4 by default,            */
+/* alac.c:57-72; 0 <= min <= max <= 255, others ATG_ERR_INVALID).       */
 /* ------------------------------------------------------------------ */
 typedef struct {
     uint32_t block_size;         /* PCM frames per frameset, 1..65535 */
     uint32_t initial_history;    /* encode_alac keyword arguments     */
     uint32_t history_multiplier;
     uint32_t maximum_k;
+    uint32_t minimum_interlacing_leftweight;
+    uint32_t maximum_interlacing_leftweight;
 } atg_alac_options;
 
 /* Per-track result: the mdat atom (32-bit size, "mdat", framesets) is

@@ -342,7 +342,8 @@ static void write_frame(bw *w, const alacport_options *o, uint32_t bps, const in
             bw best = {NULL, 0, 0};
             uint64_t best_bits = UINT32_MAX; /* unsigned best_interlaced_frame_bits */
             int overflow = 0;
-            for (unsigned lw = 0; lw <= 4 && !overflow; lw++) {
+            /* write_compressed_frame's leftweight loop (alac.c:459-481) */
+            for (unsigned lw = o->min_leftweight; lw <= o->max_leftweight && !overflow; lw++) {
                 for (unsigned i = 0; i < N; i++) {
                     if (lw) {
                         int64_t t = msb[0][i] - msb[1][i];

@@ -18,6 +18,9 @@ extern "C" {
    interlacing leftweights are the reference's 0..4 */
 typedef struct {
     uint32_t block_size, initial_history, history_multiplier, maximum_k;
+    /* interlacing leftweights tried, min..max inclusive (alac.c:57-58,
+       459-481: 0 and 4 unless the caller passes others) */
+    uint32_t min_leftweight, max_leftweight;
 } alacport_options;
 
 /* the mdat atom (8-byte header + framesets) of a whole stream, as the

@@ -30,6 +30,7 @@ PCM_S32 = 1
 EXPORTS = (
     "atg_abi_version", "atg_last_error", "atg_engine_create",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
+    "atg_flac_encode_host_async", "atg_flac_encode_host_wait",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
     "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
@@ -155,7 +156,9 @@ class RgResult(ctypes.Structure):
 
 class AlacOptions(ctypes.Structure):
     _fields_ = [("block_size", c_u32), ("initial_history", c_u32),
-                ("history_multiplier", c_u32), ("maximum_k", c_u32)]
+                ("history_multiplier", c_u32), ("maximum_k", c_u32),
+                ("minimum_interlacing_leftweight", c_u32),
+                ("maximum_interlacing_leftweight", c_u32)]
 
 
 class AlacTrackResult(ctypes.Structure):
@@ -247,6 +250,13 @@ def load_library():
             c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult),
             P, P]
         lib.atg_flac_encode_host.restype = ctypes.c_int
+        lib.atg_flac_encode_host_async.argtypes = [
+            P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
+            c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult),
+            P, P, ctypes.POINTER(c_u64)]
+        lib.atg_flac_encode_host_async.restype = ctypes.c_int
+        lib.atg_flac_encode_host_wait.argtypes = [P, c_u64]
+        lib.atg_flac_encode_host_wait.restype = ctypes.c_int
         lib.atg_flac_encode_device.argtypes = [
             P, ctypes.POINTER(FlacOptions), P, ctypes.c_int, ctypes.POINTER(Track),
             c_u32, c_u32, c_u32, c_u32, P, c_u64, ctypes.POINTER(TrackResult)]
@@ -448,6 +458,23 @@ class TrackTable(object):
         self.arr, self.n, self._keep = _track_array(tracks)
 
 
+class HostJob:
+    """a queued host-memory encode (Engine.encode_async)"""
+
+    def __init__(self, engine, ticket, keep, n, nf):
+        self.engine, self.ticket, self._keep, self.n, self.nf = engine, ticket, keep, n, nf
+        self._done = None
+
+    def wait(self):
+        if self._done is None:
+            _check(self.engine.lib, self.engine.lib.atg_flac_encode_host_wait(
+                self.engine.handle, self.ticket))
+            _pcm, out, res, offs, fpcm, _arr, _k = self._keep
+            self._done = (out, [res[i] for i in range(self.n)], offs[:self.nf], fpcm[:self.nf])
+            self._keep = (out, res, offs, fpcm)
+        return self._done
+
+
 class Engine(object):
     """one libatgpu engine (two HIP streams + workspace) on one device"""
 
@@ -510,6 +537,38 @@ class Engine(object):
             out.ctypes.data_as(ctypes.c_void_p), nb, res,
             offs.ctypes.data_as(ctypes.c_void_p), fpcm.ctypes.data_as(ctypes.c_void_p)))
         return out, [res[i] for i in range(n)], offs[:nf], fpcm[:nf]
+
+    def encode_async(self, options, pcm, tracks, channels, bits_per_sample,
+                     sample_rate, out=None):
+        """queue a host-memory batch (atg_flac_encode_host_async); returns a
+        HostJob whose wait() gives encode()'s (out, results, frame_offsets,
+        frame_pcm).  The job keeps pcm, out and the result arrays alive
+        until it is waited; jobs overlap in submission order."""
+        pcm = np.ascontiguousarray(pcm)
+        if pcm.dtype == np.int16:
+            fmt = PCM_S16
+        elif pcm.dtype == np.int32:
+            fmt = PCM_S32
+        else:
+            raise TypeError("pcm must be int16 or int32")
+        tracks = list(tracks)
+        nf, nb = self.bounds(options, tracks, channels, bits_per_sample)
+        arr, n, keep = _track_array(tracks)
+        if out is None:
+            out = np.empty(max(1, nb), dtype=np.uint8)
+        elif out.dtype != np.uint8 or not out.flags.c_contiguous or out.nbytes < nb:
+            raise ValueError("out must be a contiguous uint8 array of >= %d bytes" % nb)
+        res = (TrackResult * max(1, n))()
+        offs = np.zeros(max(1, nf), dtype=np.uint64)
+        fpcm = np.zeros(max(1, nf), dtype=np.uint32)
+        t = c_u64()
+        _check(self.lib, self.lib.atg_flac_encode_host_async(
+            self.handle, ctypes.byref(options), pcm.ctypes.data_as(ctypes.c_void_p),
+            fmt, arr, n, channels, bits_per_sample, sample_rate,
+            out.ctypes.data_as(ctypes.c_void_p), nb, res,
+            offs.ctypes.data_as(ctypes.c_void_p), fpcm.ctypes.data_as(ctypes.c_void_p),
+            ctypes.byref(t)))
+        return HostJob(self, t.value, (pcm, out, res, offs, fpcm, arr, keep), n, nf)
 
     def encode_device(self, options, d_pcm, fmt, tracks, channels,
                       bits_per_sample, sample_rate, d_out, out_cap):
@@ -776,9 +835,11 @@ class AlacEncoder(object):
             pass
 
     @staticmethod
-    def options(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14):
+    def options(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14,
+                minimum_interlacing_leftweight=0, maximum_interlacing_leftweight=4):
         return AlacOptions(int(block_size), int(initial_history), int(history_multiplier),
-                           int(maximum_k))
+                           int(maximum_k), int(minimum_interlacing_leftweight),
+                           int(maximum_interlacing_leftweight))
 
     def bounds(self, options, tracks, channels, bits_per_sample):
         arr, n, _keep = _track_array(tracks)

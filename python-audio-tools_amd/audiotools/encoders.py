@@ -224,8 +224,11 @@ def encode_alac_batch(files, pcmreaders, block_size, initial_history, history_mu
         raise ValueError("files and pcmreaders differ in length")
     if not pcmreaders:
         return []
-    if (minimum_interlacing_leftweight, maximum_interlacing_leftweight) != (0, 4):
-        raise ValueError("interlacing leftweights other than 0..4 are not supported")
+    # the leftweights tried per stereo frame (alac.c:57-72, 459-481); the
+    # reference writes them in 8 bits and, with min > max, emits a stale
+    # frame: both refused here
+    if not (0 <= minimum_interlacing_leftweight <= maximum_interlacing_leftweight <= 255):
+        raise ValueError("interlacing leftweights must satisfy 0 <= minimum <= maximum <= 255")
     r0 = pcmreaders[0]
     channels, bps = r0.channels, r0.bits_per_sample
     if bps not in (16, 24):
@@ -245,7 +248,8 @@ def encode_alac_batch(files, pcmreaders, block_size, initial_history, history_mu
     if bps <= 16:
         pcm = pcm.astype(np.int16)
     enc = _atgpu.alac_encoder()
-    opts = enc.options(block_size, initial_history, history_multiplier, maximum_k)
+    opts = enc.options(block_size, initial_history, history_multiplier, maximum_k,
+                       minimum_interlacing_leftweight, maximum_interlacing_leftweight)
     out, results, fsb = enc.encode(opts, pcm, tracks, channels, bps)
     logs = []
     for f, res in zip(files, results):

@@ -10,10 +10,12 @@
 // runs side by side:
 //
 //   K1 k_alac_lpc      lane per (element, signal): the distinct signals a
-//                      stereo element's five leftweights need -- ch0, ch1
+//                      stereo element's leftweights need -- ch0, ch1
 //                      (leftweight 0), ch0-ch1 (the second channel of every
 //                      leftweight > 0) and ch1 + ((ch0-ch1)*lw >> 2) for
-//                      lw = 1..4 -- or the one channel of a mono element.
+//                      each lw > 0 tried (minimum..maximum_interlacing_
+//                      leftweight, 0..4 by default) -- or the one channel of
+//                      a mono element.
 //                      Tukey window (host glibc cos table), 9-lag
 //                      autocorrelation as one left-to-right fp64 sum per lag,
 //                      Levinson, quantisation at orders 4 and 8
@@ -25,7 +27,7 @@
 //                      (alac.c:1020-1100), plus the residual-overflow flag
 //                      the reference longjmps on.
 //   K3 k_alac_decide   lane per frameset: per element the order (bits4 <
-//                      bits8 + 64), the leftweight (strict <, 0..4), the
+//                      bits8 + 64), the leftweight (strict <, in order), the
 //                      uncompressed fallback (< 10 samples or any overflow);
 //                      frameset bytes.
 //   K4 k_alac_scan     lane per track: frameset byte offsets, mdat header.
@@ -50,7 +52,8 @@
 namespace {
 
 constexpr uint32_t kMaxBlock = 65535; // frameset lengths handled (32-bit size field)
-constexpr int kSigStereo = 7;         // distinct signals of a stereo element
+constexpr uint32_t kMaxLw = 255;      // leftweights 0..255 (an 8-bit header field)
+constexpr uint32_t kMaxStSig = kMaxLw + 3; // signals of a stereo element: ch0, ch1, diff, 255 mixes
 
 struct AlacParams {
     uint32_t block_size, initial_history, history_multiplier, maximum_k;
@@ -60,6 +63,12 @@ struct AlacParams {
     int32_t elem_ch[8][2];          // element -> channels (second -1 for mono)
     uint32_t elem_sig[8];           // element -> first signal within the frameset
     uint32_t n_fs, n_tracks;
+    // interlacing leftweights tried, lw_lo..lw_hi (alac.c:459-481); a stereo
+    // element's n_st signals are, in order: ch0 and ch1 (when 0 is in the
+    // range), ch0 - ch1 and the mix of every leftweight > 0 in the range
+    uint32_t lw_lo, lw_hi, n_st;
+    uint32_t sig_first_mix;         // index of leftweight max(lo, 1)'s mix within the element
+    uint16_t st_kind[kMaxStSig];    // stereo signal index -> kind (see sig_at)
 };
 
 struct FsInfo {
@@ -92,8 +101,7 @@ struct ElemDesc {
     uint8_t compressed;   // 0 = write_uncompressed_frame
     uint8_t lw;           // interlacing leftweight (stereo)
     uint8_t order[2];     // chosen order of each channel's signal
-    uint8_t sig[2];       // chosen signal (within the frameset) of each channel
-    uint8_t pad[2];
+    uint16_t sig[2];      // chosen signal (within the frameset) of each channel
 };
 
 struct FsDesc {
@@ -140,7 +148,7 @@ __device__ __forceinline__ void sig_decode(uint32_t s, uint32_t &elem, uint32_t 
     for (uint32_t k = 1; k < c_p.n_elem; ++k)
         e = s >= c_p.elem_sig[k] ? k : e;
     elem = e;
-    kind = s - c_p.elem_sig[e];
+    kind = c_p.elem_ch[e][1] >= 0 ? (uint32_t)c_p.st_kind[s - c_p.elem_sig[e]] : 0u;
 }
 
 // sample size of an element's signals (alac.c:570-573, 629-641)
@@ -413,53 +421,69 @@ __global__ __launch_bounds__(64) void k_alac_decide(const FsInfo *__restrict__ f
     uint32_t total = 0;
     for (uint32_t e = 0; e < c_p.n_elem; ++e) {
         const uint32_t nch = c_p.elem_ch[e][1] >= 0 ? 2u : 1u;
-        const uint32_t nsig = nch == 2 ? (uint32_t)kSigStereo : 1u;
         const uint64_t s0 = (uint64_t)f * c_p.n_sig + c_p.elem_sig[e];
-        // per signal: chosen order and residual bits (compute_coefficients)
-        uint32_t ord[kSigStereo], rb[kSigStereo];
-        uint32_t overflow = 0;
-        for (uint32_t s = 0; s < nsig; ++s) {
+        // a signal's chosen order and residual bits (compute_coefficients)
+        auto pick = [&](uint32_t s, uint32_t &ord, uint32_t &rb) {
             const SigLpc &L = lpc[s0 + s];
             const ChainOut a = c4[s0 + s], b = c8[s0 + s];
-            overflow |= a.overflow | (L.zero ? 0u : b.overflow);
             if (L.zero || a.bits < b.bits + 64u) {
-                ord[s] = 4;
-                rb[s] = a.bits;
+                ord = 4;
+                rb = a.bits;
             } else {
-                ord[s] = 8;
-                rb[s] = b.bits;
+                ord = 8;
+                rb = b.bits;
             }
+        };
+        // any residual overflow of a signal the leftweights use makes the
+        // reference longjmp to write_uncompressed_frame (alac.c:426-436)
+        uint32_t overflow = 0;
+        const uint32_t nsig = nch == 2 ? c_p.n_st : 1u;
+        for (uint32_t s = 0; s < nsig; ++s) {
+            const SigLpc &L = lpc[s0 + s];
+            overflow |= c4[s0 + s].overflow | (L.zero ? 0u : c8[s0 + s].overflow);
         }
         ElemDesc d;
-        d.pad[0] = d.pad[1] = 0;
         const uint32_t lsb_bits = N * nch * c_p.lshift;
         if (N >= 10 && !overflow) {
             d.compressed = 1;
             if (nch == 1) {
+                uint32_t o0, r0;
+                pick(0, o0, r0);
                 d.lw = 0;
-                d.sig[0] = (uint8_t)c_p.elem_sig[e];
+                d.sig[0] = (uint16_t)c_p.elem_sig[e];
                 d.sig[1] = 0;
-                d.order[0] = (uint8_t)ord[0];
+                d.order[0] = (uint8_t)o0;
                 d.order[1] = 0;
-                d.bits = frame_head_bits(N) + 16u + 16u + 16u * ord[0] + lsb_bits + rb[0];
+                d.bits = frame_head_bits(N) + 16u + 16u + 16u * o0 + lsb_bits + r0;
             } else {
-                // write_compressed_frame: leftweights 0..4, strict < (alac.c:459-481)
-                uint32_t best = 0xFFFFFFFFu, best_lw = 0;
-                for (uint32_t lw = 0; lw <= 4; ++lw) {
-                    const uint32_t a = lw ? 3u + lw - 1u : 0u, b = lw ? 2u : 1u;
-                    const uint32_t bits = frame_head_bits(N) + 16u + 2u * 16u + 16u * ord[a] +
-                                          16u * ord[b] + lsb_bits + rb[a] + rb[b];
+                // write_compressed_frame: leftweights lo..hi in order, the
+                // smallest frame kept (strict <, alac.c:459-481); leftweight
+                // 0 codes (ch0, ch1), lw > 0 (mix(lw), ch0 - ch1)
+                const uint32_t diff = c_p.lw_lo == 0 ? 2u : 0u;
+                uint32_t best = 0xFFFFFFFFu, best_a = 0, best_b = 1, best_lw = 0;
+                uint32_t oa = 0, ob = 0;
+                for (uint32_t lw = c_p.lw_lo; lw <= c_p.lw_hi; ++lw) {
+                    const uint32_t a = lw ? c_p.sig_first_mix + lw - max(c_p.lw_lo, 1u) : 0u;
+                    const uint32_t b = lw ? diff : 1u;
+                    uint32_t o1, r1, o2, r2;
+                    pick(a, o1, r1);
+                    pick(b, o2, r2);
+                    const uint32_t bits = frame_head_bits(N) + 16u + 2u * 16u + 16u * o1 +
+                                          16u * o2 + lsb_bits + r1 + r2;
                     if (bits < best) {
                         best = bits;
                         best_lw = lw;
+                        best_a = a;
+                        best_b = b;
+                        oa = o1;
+                        ob = o2;
                     }
                 }
-                const uint32_t a = best_lw ? 3u + best_lw - 1u : 0u, b = best_lw ? 2u : 1u;
                 d.lw = (uint8_t)best_lw;
-                d.sig[0] = (uint8_t)(c_p.elem_sig[e] + a);
-                d.sig[1] = (uint8_t)(c_p.elem_sig[e] + b);
-                d.order[0] = (uint8_t)ord[a];
-                d.order[1] = (uint8_t)ord[b];
+                d.sig[0] = (uint16_t)(c_p.elem_sig[e] + best_a);
+                d.sig[1] = (uint16_t)(c_p.elem_sig[e] + best_b);
+                d.order[0] = (uint8_t)oa;
+                d.order[1] = (uint8_t)ob;
                 d.bits = best;
             }
         } else {
@@ -732,7 +756,8 @@ __global__ __launch_bounds__(64) void k_alac_pack(const T *__restrict__ pcm,
             }
         }
         for (uint32_t c = 0; c < nch; ++c) {
-            const uint32_t kind = d.sig[c] - c_p.elem_sig[e];
+            const uint32_t k = d.sig[c] - c_p.elem_sig[e];
+            const uint32_t kind = nch == 2 ? (uint32_t)c_p.st_kind[k] : 0u;
             pack_signal(bw, pcm, F, e, kind, d.order[c], L[c]);
         }
     }
@@ -871,6 +896,11 @@ atg_status alac_plan(atg_alac_encoder *enc, const atg_alac_options *o, const atg
         return afail(ATG_ERR_UNSUPPORTED, "block_size must be 1..65535");
     if (o->maximum_k < 1 || o->maximum_k > 24)
         return afail(ATG_ERR_UNSUPPORTED, "maximum_k must be 1..24");
+    // the reference writes the leftweight in 8 bits and, with min > max,
+    // copies a stale recorder as the frame (alac.c:459-481): both refused
+    if (o->minimum_interlacing_leftweight > o->maximum_interlacing_leftweight ||
+        o->maximum_interlacing_leftweight > kMaxLw)
+        return afail(ATG_ERR_INVALID, "interlacing leftweights must satisfy 0 <= min <= max <= 255");
     AlacParams &p = P.p;
     std::memset(&p, 0, sizeof(p));
     p.block_size = o->block_size;
@@ -880,6 +910,22 @@ atg_status alac_plan(atg_alac_encoder *enc, const atg_alac_options *o, const atg
     p.channels = channels;
     p.bps = bps;
     p.lshift = bps <= 16 ? 0u : ((bps - 16) / 8) * 8;
+    p.lw_lo = o->minimum_interlacing_leftweight;
+    p.lw_hi = o->maximum_interlacing_leftweight;
+    {
+        uint32_t k = 0;
+        if (p.lw_lo == 0) {
+            p.st_kind[k++] = 0; // ch0
+            p.st_kind[k++] = 1; // ch1
+        }
+        if (p.lw_hi > 0) {
+            p.st_kind[k++] = 2; // ch0 - ch1
+            p.sig_first_mix = k;
+            for (uint32_t lw = std::max(p.lw_lo, 1u); lw <= p.lw_hi; ++lw)
+                p.st_kind[k++] = (uint16_t)(2u + lw); // ch1 + ((ch0 - ch1) lw >> 2)
+        }
+        p.n_st = k;
+    }
     int32_t g[8][2];
     p.n_elem = alac_groups(channels, g);
     uint32_t ns = 0;
@@ -887,7 +933,7 @@ atg_status alac_plan(atg_alac_encoder *enc, const atg_alac_options *o, const atg
         p.elem_ch[e][0] = g[e][0];
         p.elem_ch[e][1] = g[e][1];
         p.elem_sig[e] = ns;
-        ns += g[e][1] >= 0 ? kSigStereo : 1;
+        ns += g[e][1] >= 0 ? p.n_st : 1;
     }
     p.n_sig = ns;
     P.fs.clear();

@@ -12,6 +12,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <deque>
 #include <map>
 #include <memory>
 #include <string>
@@ -115,6 +116,7 @@ void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16])
 
 namespace {
 struct Plan;
+struct HostJob;
 }
 
 // One batch in flight: its device workspace, its MD5/header stream and the
@@ -148,11 +150,18 @@ struct EncSlot {
     std::string end_error;
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
+    bool host = false;               // a chunk of a host-memory job
     uint64_t ticket = 0;
     atg_status status = ATG_OK;
     std::string error;
     float times[kNumTimed] = {};
 };
+
+// development switch (tools/build_exp.sh): the slots' aux streams at high
+// stream priority
+#ifndef ATG_AUX_HIPRIO
+#define ATG_AUX_HIPRIO 0
+#endif
 
 // batches in flight on an engine (each its own device workspace): the MD5
 // chains of a batch run ~12 ms, longer than a batch's search chain, so a
@@ -184,6 +193,14 @@ struct atg_engine {
     HostStage hs[kEncSlots];
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     uint64_t chunk_bytes = 256ull << 20; // PCM bytes per chunk
+    // host jobs (atg_flac_encode_host_async), oldest first; their chunks
+    // flow through the stages in submission order, kEncSlots in flight
+    std::deque<std::unique_ptr<HostJob>> hjobs;
+    std::deque<std::pair<HostJob *, size_t>> hflight; // (job, chunk): enqueued, not collected
+    HostJob *hcopy_job = nullptr;                     // staged chunk whose host copy is pending
+    size_t hcopy_chunk = 0;
+    uint64_t hseq = 0;                                // chunks enqueued so far (stage = seq % 3)
+    uint64_t next_hjob = 1;
     std::map<uint32_t, uint32_t> win_off;
     std::vector<double> win_host;
     size_t win_uploaded = 0;
@@ -542,7 +559,8 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
 // Returns without waiting.
 atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan> &plp,
                          const void *d_pcm, int fmt, uint8_t *d_out, uint64_t out_cap,
-                         bool want_fdesc, hipEvent_t wait_before = nullptr, bool pipelined = false)
+                         bool want_fdesc, hipEvent_t wait_before = nullptr, bool pipelined = false,
+                         bool md5_early = false)
 {
     Plan &pl = *plp;
     FlacParams &p = pl.p;
@@ -626,9 +644,13 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // track's blocks now, part 1 after the next batch's LPC kernel
     // (batch_end), so no chain runs beside an LPC grid; otherwise the whole
     // chain now (a caller waiting on each batch gains nothing from a split)
-    const bool split_md5 = pipelined && ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
-                                         (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, ev[1], 0));
+    // md5_early (host pipeline chunks): the whole chain as soon as the
+    // chunk's PCM is uploaded -- a host caller waits for its last chunk's
+    // chains, so they start as early as possible
+    const bool split_md5 = pipelined && !md5_early &&
+                           ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
+                            (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, md5_early && wait_before ? wait_before : ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
     if (!pl.frames_only)
         HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
@@ -855,6 +877,216 @@ atg_status wait_ticket(atg_engine *e, uint64_t t, EncSlot *&out)
     return ATG_OK;
 }
 
+
+// ---- host-memory jobs (atg_flac_encode_host[_async]) ----------------------
+// A job is cut into chunks of consecutive tracks (~chunk_bytes of PCM); the
+// chunks of all jobs flow through the kEncSlots pipeline stages in
+// submission order: chunk c+1's upload, chunk c's encode (its MD5 chains
+// from the moment its PCM is on the device) and chunk c-1's download
+// overlap, across job boundaries too, so back-to-back jobs keep the PCIe
+// link busy.
+struct HostChunk {
+    uint32_t t0 = 0, t1 = 0;          // tracks [t0, t1) of the job
+    uint64_t pcm0 = 0, samples = 0;   // first sample and samples of the chunk's PCM span
+    std::vector<atg_track> tr;
+    std::shared_ptr<Plan> plan;
+    uint64_t ticket = 0;
+    size_t stage = 0;
+    uint64_t out0 = 0, out_bytes = 0; // packed span in the job's `out`
+    bool staged_out = false;          // D2H went to pinned staging
+};
+
+struct HostJob {
+    uint64_t id = 0;
+    const uint8_t *pcm = nullptr;
+    size_t elem = 2;
+    int fmt = ATG_PCM_S16;
+    uint8_t *out = nullptr;
+    atg_track_result *results = nullptr;
+    uint64_t *frame_offsets = nullptr;
+    uint32_t *frame_pcm_frames = nullptr;
+    bool pin_in = false, pin_out = false;
+    Plan whole;
+    std::vector<HostChunk> chunks;
+    size_t collected = 0;             // chunks whose results are filled
+    uint64_t out_pos = 0;
+    atg_status status = ATG_OK;
+    std::string error;
+};
+
+unsigned host_threads()
+{
+    return std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
+}
+
+// the staged chunk's bytes to the caller's buffer once its D2H is done
+atg_status host_finish_copy(atg_engine *e)
+{
+    if (!e->hcopy_job)
+        return ATG_OK;
+    HostJob &j = *e->hcopy_job;
+    HostChunk &c = j.chunks[e->hcopy_chunk];
+    e->hcopy_job = nullptr;
+    HostStage &h = e->hs[c.stage];
+    HIP_TRY(hipEventSynchronize(h.ev_d2h));
+    if (c.staged_out && c.out_bytes)
+        par_memcpy(j.out + c.out0, h.p_out, c.out_bytes, host_threads());
+    return ATG_OK;
+}
+
+// the oldest chunk in flight: wait for its batch, pack its images on the
+// device, queue their copy to host memory, fill its results
+atg_status host_collect(atg_engine *e)
+{
+    HostJob &j = *e->hflight.front().first;
+    const size_t ci = e->hflight.front().second;
+    e->hflight.pop_front();
+    HostChunk &c = j.chunks[ci];
+    HostStage &h = e->hs[c.stage];
+    EncSlot *sl = nullptr;
+    atg_status s2 = wait_ticket(e, c.ticket, sl);
+    if (s2 != ATG_OK)
+        return s2;
+    sl->host = false;
+    const Plan &cp = *c.plan;
+    const size_t nt = cp.tracks.size();
+    HIP_TRY(ensure_pinned(h.p_off, h.p_off_cap, std::max<size_t>(nt, 1)));
+    uint64_t pos = 0;
+    for (size_t k = 0; k < nt; ++k) {
+        h.p_off[k] = pos;
+        pos += (sl->tout_h[k].bytes + 15u) & ~15ull;
+    }
+    c.out0 = j.out_pos;
+    c.out_bytes = pos;
+    j.out_pos += pos;
+    HIP_TRY(h.d_off.ensure(std::max<size_t>(nt, 1) * sizeof(uint64_t)));
+    HIP_TRY(h.d_pack.ensure(std::max<uint64_t>(pos, 16)));
+    if (nt)
+        HIP_TRY(hipMemcpyAsync(h.d_off.p, h.p_off, nt * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               e->s_d2h));
+    HIP_TRY(launch_pack_images((const uint8_t *)h.d_img.p, (const TrackInfo *)sl->tracks.p,
+                               (const TrackOut *)sl->tout.p, (const uint64_t *)h.d_off.p,
+                               (uint32_t)nt, (uint8_t *)h.d_pack.p, e->s_d2h));
+    HIP_TRY(hipEventRecord(h.ev_packed, e->s_d2h));
+    c.staged_out = !j.pin_out;
+    uint8_t *dst = j.out + c.out0;
+    if (c.staged_out) {
+        HIP_TRY(ensure_pinned(h.p_out, h.p_out_cap, std::max<uint64_t>(pos, 16)));
+        dst = h.p_out;
+    }
+    if (pos)
+        HIP_TRY(hipMemcpyAsync(dst, h.d_pack.p, pos, hipMemcpyDeviceToHost, e->s_d2h));
+    HIP_TRY(hipEventRecord(h.ev_d2h, e->s_d2h));
+    for (size_t k = 0; k < nt; ++k) {
+        const uint32_t t = c.t0 + (uint32_t)k;
+        const TrackOut &to = sl->tout_h[k];
+        atg_track_result &r = j.results[t];
+        r.out_offset = c.out0 + h.p_off[k];
+        r.bytes = to.bytes;
+        r.first_frame = j.whole.track_frame_pos[t];
+        r.n_frames = j.whole.tracks[t].n_frames;
+        r.min_frame_bytes = to.min_fs;
+        r.max_frame_bytes = to.max_fs;
+        std::memcpy(r.md5, to.md5, 16);
+        r.status = 0;
+        r.reserved = 0;
+        const TrackInfo &ti = cp.tracks[k];
+        for (uint32_t i = 0; i < ti.n_frames; ++i) {
+            const uint32_t f = cp.order[ti.first_pos + i];
+            if (j.frame_offsets)
+                j.frame_offsets[r.first_frame + i] = sl->fdesc_h[f].out_off;
+            if (j.frame_pcm_frames)
+                j.frame_pcm_frames[r.first_frame + i] = cp.frames[f].n;
+        }
+    }
+    // the previous staged chunk's bytes are in host memory by now
+    s2 = host_finish_copy(e);
+    if (s2 != ATG_OK)
+        return s2;
+    e->hcopy_job = &j;
+    e->hcopy_chunk = ci;
+    ++j.collected;
+    return ATG_OK;
+}
+
+// a failure inside the pipeline: drain the device, fail every job in
+// flight (their device state is gone) and free the slots
+atg_status host_drain(atg_engine *e, atg_status err)
+{
+    const std::string msg = g_err;
+    (void)hipDeviceSynchronize();
+    for (EncSlot &s2 : e->slot)
+        if (s2.busy && s2.host) {
+            s2.busy = false;
+            s2.done = false;
+            s2.host = false;
+            s2.ticket = 0;
+            s2.end_pending = false;
+        }
+    for (auto &jp : e->hjobs)
+        if (jp->collected < jp->chunks.size() && jp->status == ATG_OK) {
+            jp->status = err;
+            jp->error = msg;
+        }
+    e->hflight.clear();
+    e->hcopy_job = nullptr;
+    g_err = msg;
+    return err;
+}
+
+// upload chunk ci of job j and enqueue its encode; the oldest chunk is
+// collected first when every stage is busy
+atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_options *opts)
+{
+    (void)opts;
+    if (e->hflight.size() >= kEncSlots) {
+        atg_status st = host_collect(e);
+        if (st != ATG_OK)
+            return st;
+    }
+    HostChunk &c = j.chunks[ci];
+    c.stage = (size_t)(e->hseq % kEncSlots);
+    HostStage &h = e->hs[c.stage];
+    const uint64_t in_bytes = c.samples * j.elem;
+    // stage c.stage last held the chunk three enqueues back, collected
+    // (waited, packed) by now; its device buffers are reused in stream order
+    HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
+    HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
+    const uint8_t *src = j.pcm + c.pcm0 * j.elem;
+    if (in_bytes && !j.pin_in) {
+        HIP_TRY(ensure_pinned(h.p_in, h.p_in_cap, in_bytes + 16));
+        HIP_TRY(hipEventSynchronize(h.ev_h2d)); // its previous upload has finished
+        par_memcpy(h.p_in, src, in_bytes, host_threads());
+        src = h.p_in;
+    }
+    // the encode overwrites d_img: the previous occupant's images must have
+    // been packed first
+    HIP_TRY(hipStreamWaitEvent(e->s_h2d, h.ev_packed, 0));
+    if (in_bytes)
+        HIP_TRY(hipMemcpyAsync(h.d_pcm.p, src, in_bytes, hipMemcpyHostToDevice, e->s_h2d));
+    HIP_TRY(hipEventRecord(h.ev_h2d, e->s_h2d));
+    EncSlot *sl = nullptr;
+    uint64_t ticket = 0;
+    atg_status st = take_slot(e, sl, ticket);
+    if (st == ATG_OK)
+        st = enqueue_batch(e, *sl, c.plan, h.d_pcm.p, j.fmt, (uint8_t *)h.d_img.p, h.d_img.cap,
+                           true, h.ev_h2d, true, true);
+    if (st != ATG_OK) {
+        if (sl) {
+            sl->uploaded = nullptr;
+            sl->ticket = 0;
+            sl->end_pending = false;
+        }
+        return st;
+    }
+    sl->busy = true;
+    sl->host = true;
+    c.ticket = ticket;
+    ++e->hseq;
+    e->hflight.emplace_back(&j, ci);
+    return ATG_OK;
+}
+
 } // namespace
 
 extern "C" {
@@ -878,7 +1110,14 @@ atg_status atg_engine_create(int device, atg_engine **out)
     e->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
     for (EncSlot &sl : e->slot) {
+#if ATG_AUX_HIPRIO
+        // the MD5 / header streams at the highest stream priority
+        int prio_lo = 0, prio_hi = 0;
+        HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+        HIP_TRY(hipStreamCreateWithPriority(&sl.s_aux, hipStreamNonBlocking, prio_hi));
+#else
         HIP_TRY(hipStreamCreateWithFlags(&sl.s_aux, hipStreamNonBlocking));
+#endif
         for (auto &ev : sl.ev)
             HIP_TRY(hipEventCreate(&ev));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_tables, hipEventDisableTiming));
@@ -968,6 +1207,8 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
+    if (!e->hflight.empty())
+        return fail(ATG_ERR_INVALID, "a host encode job is in flight: wait for it first");
     std::shared_ptr<Plan> pl;
     atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, pl);
     if (st != ATG_OK)
@@ -1024,48 +1265,47 @@ atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
     return atg_flac_encode_wait(e, t, results);
 }
 
-atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, const void *pcm,
-                                atg_pcm_format format, const atg_track *tracks,
-                                uint32_t n_tracks, uint32_t channels, uint32_t bps,
-                                uint32_t rate, uint8_t *out, uint64_t out_cap,
-                                atg_track_result *results, uint64_t *frame_offsets,
-                                uint32_t *frame_pcm_frames)
+atg_status atg_flac_encode_host_async(atg_engine *e, const atg_flac_options *opts,
+                                      const void *pcm, atg_pcm_format format,
+                                      const atg_track *tracks, uint32_t n_tracks,
+                                      uint32_t channels, uint32_t bps, uint32_t rate,
+                                      uint8_t *out, uint64_t out_cap, atg_track_result *results,
+                                      uint64_t *frame_offsets, uint32_t *frame_pcm_frames,
+                                      uint64_t *ticket)
 {
-    if (!e || (!tracks && n_tracks) || (!results && n_tracks))
+    if (!e || (!tracks && n_tracks) || (!results && n_tracks) || !ticket)
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    // the whole batch's layout (what atg_flac_batch_bounds sized)
-    Plan whole;
-    atg_status st = make_plan(opts, tracks, n_tracks, channels, bps, rate, whole);
+    auto jp = std::make_unique<HostJob>();
+    HostJob &j = *jp;
+    // the whole job's layout (what atg_flac_batch_bounds sized)
+    atg_status st = make_plan(opts, tracks, n_tracks, channels, bps, rate, j.whole);
     if (st != ATG_OK)
         return st;
-    if (whole.out_bytes > out_cap)
+    if (j.whole.out_bytes > out_cap)
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
-    const size_t elem = format == ATG_PCM_S16 ? 2 : 4;
     HIP_TRY(hipSetDevice(e->device));
-    // the slots' device state is reused below: an unwaited async batch
-    // would lose its results
+    // the slots' device state is shared: an unwaited device batch would
+    // lose its results
     for (EncSlot &s2 : e->slot)
-        if (s2.busy)
+        if (s2.busy && !s2.host)
             return fail(ATG_ERR_INVALID, "an async encode batch is in flight: wait for it first");
-
-    // chunks of consecutive tracks, ~chunk_bytes of PCM each
-    // (atg_engine_set_host_chunk_bytes)
-    struct Chunk {
-        uint32_t t0, t1;          // tracks [t0, t1)
-        uint64_t pcm0, samples;   // first sample and samples of the chunk's PCM span
-        std::vector<atg_track> tr;
-        std::shared_ptr<Plan> plan;
-        uint64_t ticket = 0;
-        uint64_t out0 = 0, out_bytes = 0; // packed span in `out`
-        bool staged_out = false;          // D2H went to pinned staging
-    };
-    std::vector<Chunk> chunks;
+    j.elem = format == ATG_PCM_S16 ? 2 : 4;
+    j.fmt = (int)format;
+    j.pcm = (const uint8_t *)pcm;
+    j.out = out;
+    j.results = results;
+    j.frame_offsets = frame_offsets;
+    j.frame_pcm_frames = frame_pcm_frames;
+    // page-locked caller buffers are copied by DMA directly; pageable ones
+    // go through pinned staging (copied on host threads)
+    j.pin_in = is_pinned(pcm);
+    j.pin_out = is_pinned(out);
     {
         uint32_t t = 0;
         while (t < n_tracks) {
-            Chunk c;
+            HostChunk c;
             c.t0 = t;
             uint64_t lo = UINT64_MAX, hi = 0;
             do {
@@ -1074,7 +1314,7 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
                                                 channels);
                 ++t;
             } while (t < n_tracks && (hi - std::min<uint64_t>(lo, tracks[t].pcm_offset * channels) +
-                                      tracks[t].pcm_frames * channels) * elem <= e->chunk_bytes);
+                                      tracks[t].pcm_frames * channels) * j.elem <= e->chunk_bytes);
             c.t1 = t;
             c.pcm0 = lo == UINT64_MAX ? 0 : lo;
             c.samples = hi > c.pcm0 ? hi - c.pcm0 : 0;
@@ -1087,170 +1327,69 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
             st = make_plan(opts, c.tr.data(), (uint32_t)c.tr.size(), channels, bps, rate, *c.plan);
             if (st != ATG_OK)
                 return st;
-            chunks.push_back(std::move(c));
+            j.chunks.push_back(std::move(c));
         }
     }
-    // page-locked caller buffers are copied by DMA directly; pageable ones
-    // go through pinned staging (copied on host threads)
-    const bool pin_in = is_pinned(pcm), pin_out = is_pinned(out);
-    const unsigned host_threads = std::min<unsigned>(16, std::max(1u, std::thread::hardware_concurrency()));
-    auto par_copy = [&](void *dst, const void *src, size_t n) {
-        if (n)
-            par_memcpy(dst, src, n, host_threads);
-    };
-    // chunk c's images are packed back to back (16-byte aligned) at
-    // out + c.out0: the caller reads each at results[t].out_offset
-    uint64_t out_pos = 0;
-    // a staged chunk whose D2H is queued but not yet copied to `out`
-    int pending_copy = -1;
-
-    auto finish_copy = [&](int ci) -> atg_status {
-        Chunk &c = chunks[(size_t)ci];
-        HostStage &h = e->hs[(size_t)ci % kEncSlots];
-        HIP_TRY(hipEventSynchronize(h.ev_d2h));
-        if (c.staged_out)
-            par_copy(out + c.out0, h.p_out, c.out_bytes);
-        return ATG_OK;
-    };
-
-    // finish chunk ci: wait for its batch, pack its images on the device,
-    // queue their copy to host memory, fill its results
-    auto collect = [&](size_t ci) -> atg_status {
-        Chunk &c = chunks[ci];
-        HostStage &h = e->hs[ci % kEncSlots];
-        EncSlot *sl = nullptr;
-        atg_status s2 = wait_ticket(e, c.ticket, sl);
-        if (s2 != ATG_OK)
-            return s2;
-        const Plan &cp = *c.plan;
-        const size_t nt = cp.tracks.size();
-        HIP_TRY(ensure_pinned(h.p_off, h.p_off_cap, std::max<size_t>(nt, 1)));
-        uint64_t pos = 0;
-        for (size_t j = 0; j < nt; ++j) {
-            h.p_off[j] = pos;
-            pos += (sl->tout_h[j].bytes + 15u) & ~15ull;
-        }
-        c.out0 = out_pos;
-        c.out_bytes = pos;
-        out_pos += pos;
-        HIP_TRY(h.d_off.ensure(std::max<size_t>(nt, 1) * sizeof(uint64_t)));
-        HIP_TRY(h.d_pack.ensure(std::max<uint64_t>(pos, 16)));
-        if (nt)
-            HIP_TRY(hipMemcpyAsync(h.d_off.p, h.p_off, nt * sizeof(uint64_t),
-                                   hipMemcpyHostToDevice, e->s_d2h));
-        HIP_TRY(launch_pack_images((const uint8_t *)h.d_img.p, (const TrackInfo *)sl->tracks.p,
-                                   (const TrackOut *)sl->tout.p, (const uint64_t *)h.d_off.p,
-                                   (uint32_t)nt, (uint8_t *)h.d_pack.p, e->s_d2h));
-        HIP_TRY(hipEventRecord(h.ev_packed, e->s_d2h));
-        c.staged_out = !pin_out;
-        uint8_t *dst = out + c.out0;
-        if (c.staged_out) {
-            HIP_TRY(ensure_pinned(h.p_out, h.p_out_cap, std::max<uint64_t>(pos, 16)));
-            dst = h.p_out;
-        }
-        if (pos)
-            HIP_TRY(hipMemcpyAsync(dst, h.d_pack.p, pos, hipMemcpyDeviceToHost, e->s_d2h));
-        HIP_TRY(hipEventRecord(h.ev_d2h, e->s_d2h));
-        for (size_t j = 0; j < nt; ++j) {
-            const uint32_t t = c.t0 + (uint32_t)j;
-            const TrackOut &to = sl->tout_h[j];
-            atg_track_result &r = results[t];
-            r.out_offset = c.out0 + h.p_off[j];
-            r.bytes = to.bytes;
-            r.first_frame = whole.track_frame_pos[t];
-            r.n_frames = whole.tracks[t].n_frames;
-            r.min_frame_bytes = to.min_fs;
-            r.max_frame_bytes = to.max_fs;
-            std::memcpy(r.md5, to.md5, 16);
-            r.status = 0;
-            r.reserved = 0;
-            const TrackInfo &ti = cp.tracks[j];
-            for (uint32_t i = 0; i < ti.n_frames; ++i) {
-                const uint32_t f = cp.order[ti.first_pos + i];
-                if (frame_offsets)
-                    frame_offsets[r.first_frame + i] = sl->fdesc_h[f].out_off;
-                if (frame_pcm_frames)
-                    frame_pcm_frames[r.first_frame + i] = cp.frames[f].n;
-            }
-        }
-        // the previous staged chunk's bytes are in host memory by now
-        if (pending_copy >= 0) {
-            s2 = finish_copy(pending_copy);
-            if (s2 != ATG_OK)
-                return s2;
-        }
-        pending_copy = (int)ci;
-        return ATG_OK;
-    };
-
-    auto drain = [&](atg_status err) {
-        (void)hipDeviceSynchronize();
-        for (EncSlot &s2 : e->slot)
-            if (s2.busy) {
-                s2.busy = false;
-                s2.done = false;
-                s2.ticket = 0;
-                s2.end_pending = false;
-            }
-        return err;
-    };
-
-    for (size_t ci = 0; ci < chunks.size(); ++ci) {
-        Chunk &c = chunks[ci];
-        HostStage &h = e->hs[ci % kEncSlots];
-        const uint64_t in_bytes = c.samples * elem;
-        // stage ci % 3 last held chunk ci - 3, collected (waited, packed)
-        // two iterations ago; its device buffers are reused in stream order
-        HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
-        HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
-        const uint8_t *src = (const uint8_t *)pcm + c.pcm0 * elem;
-        if (in_bytes && !pin_in) {
-            HIP_TRY(ensure_pinned(h.p_in, h.p_in_cap, in_bytes + 16));
-            HIP_TRY(hipEventSynchronize(h.ev_h2d)); // its previous upload has finished
-            par_copy(h.p_in, src, in_bytes);
-            src = h.p_in;
-        }
-        // the encode overwrites d_img: the previous occupant's images must
-        // have been packed first
-        HIP_TRY(hipStreamWaitEvent(e->s_h2d, h.ev_packed, 0));
-        if (in_bytes)
-            HIP_TRY(hipMemcpyAsync(h.d_pcm.p, src, in_bytes, hipMemcpyHostToDevice, e->s_h2d));
-        HIP_TRY(hipEventRecord(h.ev_h2d, e->s_h2d));
-        EncSlot *sl = nullptr;
-        uint64_t ticket = 0;
-        st = take_slot(e, sl, ticket);
-        if (st == ATG_OK)
-            st = enqueue_batch(e, *sl, c.plan, h.d_pcm.p, (int)format, (uint8_t *)h.d_img.p,
-                               h.d_img.cap, true, h.ev_h2d, true);
+    j.id = e->next_hjob++;
+    e->hjobs.push_back(std::move(jp));
+    for (size_t ci = 0; ci < j.chunks.size(); ++ci) {
+        st = host_enqueue(e, j, ci, opts);
         if (st != ATG_OK) {
-            if (sl) {
-                sl->uploaded = nullptr;
-                sl->ticket = 0;
-                sl->end_pending = false;
-            }
-            return drain(st);
-        }
-        sl->busy = true;
-        c.ticket = ticket;
-        // keep kEncSlots chunks in flight: chunk ci - 2 finishes now
-        if (ci + 1 >= kEncSlots) {
-            st = collect(ci + 1 - kEncSlots);
-            if (st != ATG_OK)
-                return drain(st);
+            host_drain(e, st);
+            break;
         }
     }
-    for (size_t ci = chunks.size() >= kEncSlots ? chunks.size() + 1 - kEncSlots : 0;
-         ci < chunks.size(); ++ci) {
-        st = collect(ci);
+    *ticket = j.id;
+    return ATG_OK; // a failure above is reported by the job's wait
+}
+
+atg_status atg_flac_encode_host_wait(atg_engine *e, uint64_t ticket)
+{
+    if (!e)
+        return fail(ATG_ERR_INVALID, "NULL engine");
+    size_t k = 0;
+    while (k < e->hjobs.size() && e->hjobs[k]->id != ticket)
+        ++k;
+    if (k == e->hjobs.size())
+        return fail(ATG_ERR_INVALID, "unknown or expired host job ticket");
+    HostJob *j = e->hjobs[k].get();
+    HIP_TRY(hipSetDevice(e->device));
+    // chunks are collected in submission order: everything up to this job's
+    // last chunk, then its last staged copy
+    while (j->status == ATG_OK && j->collected < j->chunks.size()) {
+        if (e->hflight.empty())
+            break;
+        atg_status st = host_collect(e);
         if (st != ATG_OK)
-            return drain(st);
+            host_drain(e, st);
     }
-    if (pending_copy >= 0) {
-        st = finish_copy(pending_copy);
+    if (j->status == ATG_OK && e->hcopy_job == j) {
+        atg_status st = host_finish_copy(e);
         if (st != ATG_OK)
-            return drain(st);
+            host_drain(e, st);
     }
+    const atg_status st = j->status;
+    const std::string msg = j->error;
+    e->hjobs.erase(e->hjobs.begin() + (std::ptrdiff_t)k);
+    if (st != ATG_OK)
+        return fail(st, msg);
     return ATG_OK;
+}
+
+atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, const void *pcm,
+                                atg_pcm_format format, const atg_track *tracks,
+                                uint32_t n_tracks, uint32_t channels, uint32_t bps,
+                                uint32_t rate, uint8_t *out, uint64_t out_cap,
+                                atg_track_result *results, uint64_t *frame_offsets,
+                                uint32_t *frame_pcm_frames)
+{
+    uint64_t t = 0;
+    atg_status st = atg_flac_encode_host_async(e, opts, pcm, format, tracks, n_tracks, channels,
+                                               bps, rate, out, out_cap, results, frame_offsets,
+                                               frame_pcm_frames, &t);
+    if (st != ATG_OK)
+        return st;
+    return atg_flac_encode_host_wait(e, t);
 }
 
 uint64_t atg_flac_stream_header(const atg_flac_options *o, uint32_t channels, uint32_t bps,

@@ -24,11 +24,13 @@
 //                      prefix over tracks) writes the frame and subframe jobs.
 //   K4 k_dec_subframe  lane per (frame, channel): restart at the recorded bit
 //                      offset, Rice-decode and restore FIXED/LPC samples with
-//                      the predictor history in registers (one instantiation
-//                      per order), planar output.
-//   K5 k_dec_interleave block per frame: decorrelate (L-S, S-R, mid-side),
-//                      interleave to the FrameList layout (int32), and emit
-//                      the little-endian PCM byte stream the MD5 hashes.
+//                      the predictor history in registers (one window
+//                      predictor for all orders), one row per residual-loop
+//                      iteration into a [row][lane] scratch (coalesced).
+//   K5 k_dec_emit      block per 64-job slot: rows -> samples (gather),
+//                      decorrelate (L-S, S-R, mid-side), interleave to the
+//                      FrameList layout (int32), and the little-endian PCM
+//                      byte stream the MD5 hashes, in one pass.
 //   K6 k_bytes_md5     lane per track (md5.hip): STREAMINFO MD5 check input.
 //
 // Only K2 and K4 do real work; K1 and K5 are HBM passes.  Status codes are
@@ -311,7 +313,7 @@ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
 
 template <int W>
 struct WinPred {
-    int32_t *out;   // planar samples (warm-up only)
+    int32_t *out;   // the job's warm-up cell
     int4 *row;      // wave row scratch, [row/4][lane][4]: lane column at row[.. * 64]
     int32_t q0, q1, q2, q3; // the 4 rows stored together
     uint32_t i, n, t, wasted, shift, half, porder;
@@ -831,14 +833,14 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
     return p.fast && p.bad;
 }
 
-// K4: one subframe per lane.  Warm-up samples go straight to the planar
-// scratch; every residual-loop iteration stores to its row of the wave's
-// [row][lane] scratch (coalesced); K4b maps rows back to samples.
+// K4: one subframe per lane.  Warm-up samples go to the job's 32-entry
+// warm-up cell; every residual-loop iteration stores to its row of the
+// wave's [row][lane] scratch (coalesced); K5 maps rows back to samples.
 __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict__ w, uint64_t nw,
                                                      const DecTrack *__restrict__ tr,
                                                      const DecFrame *__restrict__ frames,
                                                      const uint2 *__restrict__ jobs,
-                                                     uint64_t njobs, int32_t *__restrict__ planar,
+                                                     uint64_t njobs, int32_t *__restrict__ warm,
                                                      int32_t *__restrict__ rows, uint32_t nrows,
                                                      JobMeta *__restrict__ meta)
 {
@@ -851,7 +853,7 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     BitR r;
     r.init(w, nw, f.pos * 8 + f.sub_bit[c], tr[f.track].end * 8);
     const uint32_t N = f.n;
-    int32_t *out = planar + f.pcm_start + (uint64_t)c * N;
+    int32_t *out = warm + j * 32u; // warm-up samples (orders <= 32)
     // [row/4][lane][4] scratch: this lane's 16-byte cells, every 64th int4
     int4 *row = (int4 *)(rows + (uint64_t)blockIdx.x * nrows * 64) + threadIdx.x;
     JobMeta m;
@@ -892,156 +894,181 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     meta[j] = m;
 }
 
-// K4b: rows -> samples.  Block = (wave slot of 64 jobs, tile of 64 rows):
-// the tile is read with coalesced row loads into LDS, then each job's
-// samples are written as contiguous runs.  Row t of a FIXED/LPC job is
-// partition header 0 (t = 0), residual t-1 of partition 0 (t <= p0), or,
-// past that, header/residual m of partition 1 + (t-p0-1)/(plen+1) -- the
-// residual loop reads a header before every partition (flac.c:1150-1209).
-__global__ __launch_bounds__(256) void k_dec_unrow(const DecFrame *__restrict__ frames,
-                                                   const uint2 *__restrict__ jobs, uint64_t njobs,
-                                                   const JobMeta *__restrict__ meta,
-                                                   const int32_t *__restrict__ rows,
-                                                   uint32_t nrows, int32_t *__restrict__ planar)
+// Row of sample i of a FIXED/LPC job's residual loop : row 0 is partition 0's header, residual rr < p0 sits
+// at row rr + 1, and every later partition q has its header at row
+// p0 + 1 + q (plen + 1) followed by its plen residuals.
+__device__ __forceinline__ uint32_t row_of_sample(uint32_t i, uint32_t order, uint32_t porder,
+                                                  uint32_t n)
 {
-    __shared__ int32_t tile[64 * 65];
-    __shared__ JobMeta jm[64];
-    __shared__ uint64_t joff[64];
-    __shared__ uint32_t jn[64];
-    __shared__ uint32_t maxit;
-    const uint32_t slot = blockIdx.x, t0 = blockIdx.y * 64;
+    const uint32_t rr = i - order;
+    const uint32_t plen = n >> porder;
+    const uint32_t p0 = plen > order ? plen - order : 0u;
+    if (rr < p0)
+        return rr + 1u;
+    const uint32_t tp = rr - p0;
+    uint32_t q = (uint32_t)((float)tp * (1.0f / (float)plen));
+    q -= q * plen > tp ? 1u : 0u;
+    q += (q + 1u) * plen <= tp ? 1u : 0u;
+    return p0 + 2u + q * (plen + 1u) + (tp - q * plen);
+}
+
+// K5: rows -> samples -> flacdec_decorrelate_channels (flac.c:1212-1269) ->
+// the interleaved FrameList int32 and the little-endian byte stream of
+// FrameList.to_bytes (MD5 input), in one pass.  Block = the frames whose
+// first (frame, channel) job lies in 64-job slot blockIdx.x (their other
+// channels' jobs may run into the next slot).  Per tile of kEmitTile
+// samples: every job's samples are gathered from the K4 row scratch (lanes
+// across jobs: the row cells of a slot's jobs sit 16 bytes apart) or the
+// warm-up buffer into an LDS tile, then the frames are written channel-
+// interleaved, contiguous per frame.
+constexpr uint32_t kEmitTile = 64;
+constexpr uint32_t kEmitJobs = 64 + 7;
+
+__global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ tr,
+                                                  const DecFrame *__restrict__ frames,
+                                                  const uint2 *__restrict__ jobs, uint64_t njobs,
+                                                  const JobMeta *__restrict__ meta,
+                                                  const int32_t *__restrict__ rows, uint32_t nrows,
+                                                  const int32_t *__restrict__ warm,
+                                                  int32_t *__restrict__ pcm,
+                                                  uint8_t *__restrict__ bytes)
+{
+    __shared__ int32_t tile[kEmitJobs][kEmitTile + 1];
+    __shared__ JobMeta jm[kEmitJobs];
+    __shared__ uint32_t jn[kEmitJobs];
+    __shared__ uint32_t fr[64];     // the block's frames
+    __shared__ uint32_t fj[64];     // their first job, relative to the slot
+    __shared__ uint32_t fcnt[65];   // prefix of (tile samples x channels) per frame
+    __shared__ uint32_t nfr, nj, maxn;
+    const uint64_t j0 = (uint64_t)blockIdx.x * 64;
     const uint32_t tid = threadIdx.x;
-    if (tid == 0)
-        maxit = 0;
+    if (tid == 0) {
+        nfr = 0;
+        nj = 0;
+        maxn = 0;
+    }
     __syncthreads();
     if (tid < 64) {
-        const uint64_t j = (uint64_t)slot * 64 + tid;
+        const uint64_t j = j0 + tid;
+        const bool start = j < njobs && jobs[j].y == 0u;
+        const uint64_t bal = __ballot(start);
+        if (start) {
+            const uint32_t k = (uint32_t)__popcll(bal & ((1ull << tid) - 1ull));
+            const uint32_t f = jobs[j].x;
+            fr[k] = f;
+            fj[k] = tid;
+            atomicMax(&nj, tid + (uint32_t)frames[f].ch);
+            atomicMax(&maxn, frames[f].n);
+        }
+        if (tid == 0)
+            nfr = (uint32_t)__popcll(bal);
+    }
+    __syncthreads();
+    const uint32_t NJ = min(nj, kEmitJobs), NF = nfr;
+    if (tid < NJ) {
+        const uint64_t j = j0 + tid;
         JobMeta m;
         m.kind = 3;
+        m.order = 0;
+        m.porder = 0;
         m.iters = 0;
+        uint32_t n = 0;
         if (j < njobs) {
             m = meta[j];
-            const uint2 jb = jobs[j];
-            const DecFrame f = frames[jb.x];
-            joff[tid] = f.pcm_start + (uint64_t)jb.y * f.n;
-            jn[tid] = f.n;
-        } else {
-            joff[tid] = 0;
-            jn[tid] = 0;
+            n = frames[jobs[j].x].n;
         }
         jm[tid] = m;
-        const uint32_t need = m.kind == 0 ? jn[tid] : (m.kind == 3 ? 0u : m.iters);
-        atomicMax(&maxit, need);
+        jn[tid] = n;
     }
     __syncthreads();
-    if (t0 >= maxit)
-        return;
-    const int32_t *src = rows + ((uint64_t)slot * nrows + t0) * 64;
-    for (uint32_t o = tid; o < 64 * 64; o += 256) {
-        // block element o = ((x / 4) * 64 + l) * 4 + x % 4
-        const uint32_t x = ((o >> 8) << 2) | (o & 3), l = (o >> 2) & 63;
-        tile[x * 65 + l] = src[o];
-    }
-    __syncthreads();
-    for (uint32_t k = tid; k < 64 * 64; k += 256) {
-        const uint32_t l = k >> 6, x = k & 63;
-        const JobMeta m = jm[l];
-        const uint32_t t = t0 + x, n = jn[l];
-        uint32_t i;
-        int32_t v = tile[x * 65 + l];
-        if (m.kind == 0) {
-            i = t;
-            v = m.value;
-        } else if (m.kind == 1) {
-            i = t;
-        } else if (m.kind == 2) {
-            if (t >= m.iters)
-                continue;
-            const uint32_t order = m.order;
-            const uint32_t plen = n >> m.porder;
-            const uint32_t p0 = plen > order ? plen - order : 0u;
-            uint32_t rr;
-            if (t == 0)
-                continue;
-            if (t <= p0) {
-                rr = t - 1;
-            } else {
-                const uint32_t tp = t - p0 - 1, L = plen + 1;
-                uint32_t q = (uint32_t)((float)tp * (1.0f / (float)L));
-                while (q * L > tp)
-                    --q;
-                while ((q + 1) * L <= tp)
-                    ++q;
-                const uint32_t mm = tp - q * L;
-                if (mm == 0)
-                    continue;
-                rr = p0 + q * plen + mm - 1;
+    for (uint32_t i0 = 0; i0 < maxn; i0 += kEmitTile) {
+        if (tid == 0) {
+            uint32_t acc = 0;
+            for (uint32_t k = 0; k < NF; ++k) {
+                fcnt[k] = acc;
+                const DecFrame &f = frames[fr[k]];
+                const uint32_t left = f.n > i0 ? min(f.n - i0, kEmitTile) : 0u;
+                acc += left * f.ch;
             }
-            i = order + rr;
-        } else {
-            continue;
+            fcnt[NF] = acc;
         }
-        if (i < n)
-            planar[joff[l] + i] = v;
-    }
-}
-
-// K5: flacdec_decorrelate_channels (flac.c:1212-1269) + interleave + the
-// little-endian signed byte stream of FrameList.to_bytes (MD5 input)
-__global__ __launch_bounds__(256) void k_dec_interleave(const DecTrack *__restrict__ tr,
-                                                        const DecFrame *__restrict__ frames,
-                                                        const int32_t *__restrict__ planar,
-                                                        int32_t *__restrict__ pcm,
-                                                        uint8_t *__restrict__ bytes)
-{
-    const DecFrame f = frames[blockIdx.x];
-    const DecTrack t = tr[f.track];
-    const uint32_t N = f.n, ch = f.ch;
-    const uint32_t bb = (t.bps + 7) / 8;
-    const int32_t *src = planar + f.pcm_start;
-    int32_t *dst = pcm + f.pcm_start;
-    uint8_t *bdst = bytes + t.md5_base + (f.pcm_start - t.pcm_base) * bb;
-    for (uint32_t k = threadIdx.x; k < N; k += blockDim.x) {
-        int32_t o[8];
-        if (f.assign >= 8 && f.assign <= 10) {
-            const int32_t a = src[k], b = src[N + k];
-            if (f.assign == 8) {
-                o[0] = a;
-                o[1] = (int32_t)((uint32_t)a - (uint32_t)b);
-            } else if (f.assign == 9) {
-                o[0] = (int32_t)((uint32_t)a + (uint32_t)b);
-                o[1] = b;
-            } else {
-                const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
-                o[0] = (int32_t)((mid + b) >> 1);
-                o[1] = (int32_t)((mid - b) >> 1);
+        // gather: lane = job, consecutive lanes read adjacent 16-byte cells
+        for (uint32_t e = tid; e < NJ * kEmitTile; e += 256) {
+            const uint32_t l = e % NJ, x = e / NJ;
+            const uint32_t i = i0 + x;
+            const JobMeta m = jm[l];
+            const uint32_t n = jn[l];
+            if (i >= n)
+                continue;
+            const uint64_t j = j0 + l;
+            int32_t v = 0;
+            uint32_t t = 0xFFFFFFFFu;
+            if (m.kind == 0)
+                v = m.value;
+            else if (m.kind == 1)
+                t = i;
+            else if (m.kind == 2) {
+                if (i < m.order)
+                    v = warm[j * 32u + i];
+                else
+                    t = row_of_sample(i, m.order, m.porder, n);
             }
-        } else {
-            for (uint32_t c = 0; c < ch && c < 8; ++c)
-                o[c] = src[(uint64_t)c * N + k];
+            // K4's [slot][row / 4][lane][4] scratch (nrows rows per slot)
+            if (t != 0xFFFFFFFFu)
+                v = rows[(j >> 6) * nrows * 64u + (uint64_t)(t >> 2) * 256u + (j & 63u) * 4u +
+                         (t & 3u)];
+            tile[l][x] = v;
         }
-        // FrameList.to_bytes saturates samples outside the bps range
-        // (src/pcm.c:1826-1948): only a corrupt stream can produce them
-        const int32_t hi = t.bps >= 1 && t.bps <= 31 ? (int32_t)((1u << (t.bps - 1)) - 1u)
-                                                      : 0x7FFFFFFF;
-        const int32_t lo = -hi - 1;
-        for (uint32_t c = 0; c < ch && c < 8; ++c) {
-            const uint64_t s = (uint64_t)k * ch + c;
-            dst[s] = o[c];
-            const int32_t v = o[c] > hi ? hi : (o[c] < lo ? lo : o[c]);
+        __syncthreads();
+        const uint32_t total = fcnt[NF];
+        for (uint32_t e = tid; e < total; e += 256) {
+            uint32_t k = 0;
+            for (uint32_t b = 32; b; b >>= 1)
+                if (k + b < NF && fcnt[k + b] <= e)
+                    k += b;
+            const DecFrame f = frames[fr[k]];
+            const DecTrack t = tr[f.track];
+            const uint32_t ch = f.ch, rel = e - fcnt[k];
+            const uint32_t x = rel / ch, c = rel - x * ch;
+            const uint32_t l = fj[k];
+            int32_t o;
+            if (f.assign >= 8 && f.assign <= 10 && ch == 2) {
+                const int32_t a = tile[l][x], b = tile[l + 1][x];
+                if (f.assign == 8)
+                    o = c == 0 ? a : (int32_t)((uint32_t)a - (uint32_t)b);
+                else if (f.assign == 9)
+                    o = c == 0 ? (int32_t)((uint32_t)a + (uint32_t)b) : b;
+                else {
+                    const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
+                    o = c == 0 ? (int32_t)((mid + b) >> 1) : (int32_t)((mid - b) >> 1);
+                }
+            } else {
+                o = tile[l + c][x];
+            }
+            const uint64_t s = (uint64_t)(i0 + x) * ch + c;
+            pcm[f.pcm_start + s] = o;
+            // FrameList.to_bytes saturates samples outside the bps range
+            // (src/pcm.c:1826-1948): only a corrupt stream can produce them
+            const uint32_t bb = (t.bps + 7) / 8;
+            const int32_t hi = t.bps >= 1 && t.bps <= 31 ? (int32_t)((1u << (t.bps - 1)) - 1u)
+                                                          : 0x7FFFFFFF;
+            const int32_t lo = -hi - 1;
+            const int32_t v = o > hi ? hi : (o < lo ? lo : o);
+            uint8_t *bdst = bytes + t.md5_base + (f.pcm_start - t.pcm_base + s) * bb;
             if (bb == 2) {
-                ((int16_t *)bdst)[s] = (int16_t)v;
+                *(int16_t *)bdst = (int16_t)v;
             } else {
                 for (uint32_t q = 0; q < bb; ++q)
-                    bdst[s * bb + q] = (uint8_t)((uint32_t)v >> (8 * q));
+                    bdst[q] = (uint8_t)((uint32_t)v >> (8 * q));
             }
         }
+        __syncthreads();
     }
 }
 
-const int kDecTimed = 8;
-const char *kDecNames[kDecTimed] = {"dec_scan",  "dec_parse",      "dec_chain", "dec_subframe",
-                                    "dec_unrow", "dec_interleave", "dec_md5",   "dec_total"};
+const int kDecTimed = 7;
+const char *kDecNames[kDecTimed] = {"dec_scan",     "dec_parse", "dec_chain", "dec_subframe",
+                                    "dec_emit",     "dec_md5",   "dec_total"};
 
 } // namespace
 
@@ -1092,7 +1119,7 @@ struct DBuf {
 struct DecSlot {
     DBuf pcm, bytes, md5, md5meta;
     hipStream_t s_md5 = nullptr;
-    hipEvent_t ev[kDecTimed + 1] = {}; // phase events (interleave end = ev[6])
+    hipEvent_t ev[kDecTimed + 1] = {}; // phase events (emit end = ev[5])
     hipEvent_t ev_done = nullptr;
     uint8_t *md5_h = nullptr;          // pinned
     size_t md5_cap = 0;
@@ -1110,7 +1137,7 @@ struct atg_decoder {
     hipStream_t s = nullptr;
     float times[kDecTimed] = {};
     bool have_times = false;
-    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, planar, rows, meta;
+    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, warm, rows, meta;
     DecSlot slot[2];
     uint64_t next_ticket = 1;
     int last = -1; // slot of the last waited batch (decode_fetch)
@@ -1305,7 +1332,7 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs, &d->frames, &d->jobs, &d->planar, &d->rows, &d->meta})
+                    &d->recs, &d->frames, &d->jobs, &d->warm, &d->rows, &d->meta})
         b->release();
     for (DecSlot &sl : d->slot) {
         (void)hipStreamSynchronize(sl.s_md5);
@@ -1417,7 +1444,7 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     sl.total_frames = fb;
     DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
     DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
-    DHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
+    DHIP(d->warm.ensure(sizeof(int32_t) * 32 * std::max<uint64_t>(jb, 1)));
     // row scratch: a residual loop runs at most N + 2^porder <= 2N iterations
     uint32_t max_bs = 1;
     for (uint32_t t = 0; t < n; ++t)
@@ -1442,23 +1469,17 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     if (jb)
         hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
                            nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
-                           (int32_t *)d->planar.p, (int32_t *)d->rows.p, nrows,
+                           (int32_t *)d->warm.p, (int32_t *)d->rows.p, nrows,
                            (JobMeta *)d->meta.p);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(ev[4], s));
     if (jb)
-        hipLaunchKernelGGL(k_dec_unrow, dim3((unsigned)nslots, (nrows + 63) / 64), dim3(256), 0,
-                           s, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
+        hipLaunchKernelGGL(k_dec_emit, dim3((unsigned)nslots), dim3(256), 0, s, dtr,
+                           (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
                            (const JobMeta *)d->meta.p, (const int32_t *)d->rows.p, nrows,
-                           (int32_t *)d->planar.p);
+                           (const int32_t *)d->warm.p, (int32_t *)sl.pcm.p, (uint8_t *)sl.bytes.p);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(ev[5], s));
-    if (fb)
-        hipLaunchKernelGGL(k_dec_interleave, dim3((unsigned)fb), dim3(256), 0, s, dtr,
-                           (const DecFrame *)d->frames.p, (const int32_t *)d->planar.p,
-                           (int32_t *)sl.pcm.p, (uint8_t *)sl.bytes.p);
-    DHIP(hipGetLastError());
-    DHIP(hipEventRecord(ev[6], s));
     // MD5 of the decoded bytes on the slot's stream: the next batch's scan,
     // parse and restore run on the decoder stream meanwhile
     sl.md5_meta.assign(2 * (size_t)n, 0);
@@ -1478,14 +1499,14 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
                            hipHostMallocDefault));
         sl.md5_cap = 16 * (size_t)std::max<uint32_t>(n, 1);
     }
-    DHIP(hipStreamWaitEvent(sl.s_md5, ev[6], 0));
+    DHIP(hipStreamWaitEvent(sl.s_md5, ev[5], 0));
     if (n)
         DHIP(hipMemcpyAsync(sl.md5meta.p, sl.md5_meta.data(), sizeof(uint64_t) * 2 * n,
                             hipMemcpyHostToDevice, sl.s_md5));
-    DHIP(hipEventRecord(ev[7], sl.s_md5));
+    DHIP(hipEventRecord(ev[6], sl.s_md5));
     DHIP(launch_bytes_md5((const uint8_t *)sl.bytes.p, (const uint64_t *)sl.md5meta.p,
                           (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p, sl.s_md5));
-    DHIP(hipEventRecord(ev[8], sl.s_md5));
+    DHIP(hipEventRecord(ev[7], sl.s_md5));
     if (n)
         DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
                             sl.s_md5));
@@ -1500,8 +1521,8 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
 {
     DHIP(hipEventSynchronize(sl.ev_done));
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
-    // unrow, interleave, md5, total (scan start -> md5 end)
-    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {5, 6}, {7, 8}, {0, 8}};
+    // emit, md5, total (scan start -> md5 end)
+    const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {0, 7}};
     for (int k = 0; k < kDecTimed; ++k)
         if (hipEventElapsedTime(&d->times[k], sl.ev[map[k][0]], sl.ev[map[k][1]]) != hipSuccess)
             d->times[k] = 0.f;

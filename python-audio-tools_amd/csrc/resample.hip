@@ -61,8 +61,10 @@ struct RsTrack {
     double float_increment, scale;
     int32_t increment, mode;
     uint64_t chunk_base; // first work chunk of the track (k_rs_filter)
-    uint64_t span;       // k_rs_phase: outputs per task (64 x period x rows)
+    uint64_t span;       // k_rs_phase: outputs per task (64 x lspan x rows)
     uint32_t period;     // k_rs_phase: outputs per phase cycle (out_rate / gcd)
+    uint32_t lspan;      // k_rs_phase: outputs between a wave's lanes (a multiple of period)
+    uint32_t wext;       // k_rs_phase: window frames staged past the task's last centre's taps
     uint32_t pad;
 };
 
@@ -264,29 +266,39 @@ __device__ __forceinline__ void wave_lds_sync()
 // The phase-sharing filter.  The output positions of a rational ratio
 // repeat their fractional part every `period` = out_rate / gcd outputs, so
 // outputs n, n + period, n + 2 period, ... have the same start filter index
-// and the same interpolated coefficients.  A wave takes 64 such outputs (one
-// per lane, input frames `period / ratio` apart): the lanes compute the
-// row's coefficients once, tap j in lane j % 64, into a per-wave LDS list,
-// and every tap then costs a broadcast LDS read of the coefficient, a read
-// of the lane's input sample and one multiply + add per channel.  A task is
-// 64 x period x rows consecutive outputs of one track, whose input window is
-// staged in LDS as float x / 2^(bps-1).  Each lane still computes its own
-// exact position; a row whose lanes disagree on the start index (the fp64
-// recurrence drifting across a rounding boundary) takes the per-lane path
-// with the coefficients read from the global table.
-template <int CH>
-__global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__restrict__ tr,
-                                                   const uint2 *__restrict__ tasks,
-                                                   uint32_t n_tasks, const int2 *__restrict__ pos,
-                                                   const uint32_t *__restrict__ table_bits,
-                                                   const int32_t *__restrict__ in,
-                                                   int32_t *__restrict__ out, uint32_t tmax)
+// and the same interpolated coefficients.  A lane computes M consecutive
+// outputs n0 .. n0 + M - 1 (their input windows overlap almost entirely);
+// the 64 lanes of a wave are `lspan` outputs apart (a multiple of the
+// period), so output m of every lane has the same phase.  Per work item
+// (one group of M phases of one row of 64 lanes) the wave tabulates each
+// output's coefficients once in LDS, zero-padded onto a common sample
+// index: output m's left half is the taps x[c_m - ccL_m .. c_m] in order,
+// so with s running over the union of the M windows, tap s of output m is
+// coefficient (s - (c_m - ccL_m)) or 0.  Adding a zero product leaves an
+// accumulator unchanged bit for bit (it starts at +0.0 and +0 + -0 = +0),
+// and the nonzero taps keep the reference's order, so every output is
+// exactly calc_output's.  One LDS read of a sample (and its float -> double
+// conversion) then feeds M outputs' multiply + add per channel, and the
+// coefficient reads are wave-uniform (LDS broadcast).  The right half runs
+// the same way over s descending.  A task is 64 x lspan x rows consecutive
+// outputs of one track, whose input window is staged in LDS as float
+// x / 2^(bps-1).  Each lane still computes its own exact position; a work
+// item whose lanes disagree on a phase (the fp64 recurrence drifting
+// across a rounding boundary) takes the per-lane path with the
+// coefficients read from the global table.
+template <int CH, int M>
+__global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__restrict__ tr,
+                                                  const uint2 *__restrict__ tasks,
+                                                  uint32_t n_tasks, const int2 *__restrict__ pos,
+                                                  const uint32_t *__restrict__ table_bits,
+                                                  const int32_t *__restrict__ in,
+                                                  int32_t *__restrict__ out, uint32_t wmax)
 {
     extern __shared__ double lds_d[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-    double *coefL = lds_d + (size_t)wave * 2 * tmax;
-    double *coefR = coefL + tmax;
-    float *X = reinterpret_cast<float *>(lds_d + (size_t)nwaves * 2 * tmax);
+    double *cL = lds_d + (size_t)wave * 2 * M * wmax; // [M][wmax] left, then right
+    double *cR = cL + (size_t)M * wmax;
+    float *X = reinterpret_cast<float *>(lds_d + (size_t)nwaves * 2 * M * wmax);
     const float *Cg = reinterpret_cast<const float *>(table_bits);
     const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
     for (uint32_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
@@ -301,7 +313,10 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
         position(T, pos, B0, c_first, s_tmp);
         position(T, pos, Bend - 1, c_last, s_tmp);
         const int64_t w0 = c_first - reach;
-        const uint32_t wn = (uint32_t)(c_last + reach + 1 - w0);
+        // wext more frames: a lane whose later outputs fall past the task's
+        // end still reads their taps' samples (times zero coefficients for
+        // its live outputs), so they must be finite -- staged, not stale LDS
+        const uint32_t wn = (uint32_t)(c_last + reach + 1 - w0) + T.wext;
         for (uint32_t i = threadIdx.x; i < wn * CH; i += blockDim.x) {
             const int64_t f = w0 + (int64_t)(i / CH);
             float v = 0.0f;
@@ -310,77 +325,153 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
             X[i] = v;
         }
         __syncthreads();
-        const uint32_t per = T.period;
-        const uint64_t row_len = 64ull * per;
+        const uint32_t L = T.lspan;
+        const uint32_t G = (L + M - 1) / M; // phase groups per row
+        const uint64_t row_len = 64ull * L;
         const uint32_t rows = (uint32_t)((Bend - B0 + row_len - 1) / row_len);
-        for (uint32_t tr_i = wave; tr_i < rows * per; tr_i += nwaves) {
-            const uint64_t base = B0 + (uint64_t)(tr_i / per) * row_len + (tr_i % per);
-            if (base >= Bend)
-                continue; // wave-uniform
-            const uint64_t n = base + (uint64_t)per * lane;
-            const bool active = n < Bend;
-            int64_t c;
-            int32_t sfi;
-            position(T, pos, active ? n : base, c, sfi);
-            const int32_t sfi0 = __builtin_amdgcn_readfirstlane(sfi); // lane 0: n = base
-            double left[CH], right[CH];
+        for (uint32_t item = wave; item < rows * G; item += nwaves) {
+            const uint32_t g = item % G;
+            const uint64_t rbase = B0 + (uint64_t)(item / G) * row_len + (uint64_t)M * g;
+            if (rbase >= Bend)
+                continue; // wave-uniform: the last row's tail
+            // output m of this lane; m is wave-valid when lane 0's is inside
+            // the task and the group
+            int64_t c[M];
+            int32_t sfi[M];
+            bool valid[M], active[M];
+            bool uni = true;
 #pragma unroll
-            for (int k = 0; k < CH; ++k)
-                left[k] = right[k] = 0.0;
-            const int32_t ccL = (max_fi - sfi0) / inc;
-            const int32_t fiL = sfi0 + ccL * inc;
-            const int32_t frR = inc - sfi0;
-            const int32_t ccR = (max_fi - frR) / inc;
-            const int32_t fiR = frR + ccR * inc;
-            if (__all(sfi == sfi0)) {
-                const int32_t nL = fiL / inc + 1, nR = (fiR - 1) / inc + 1;
-                for (int32_t j = (int32_t)lane; j < nL; j += 64)
-                    coefL[j] = interp_coeff(Cg, fiL - j * inc);
-                for (int32_t j = (int32_t)lane; j < nR; j += 64)
-                    coefR[j] = interp_coeff(Cg, fiR - j * inc);
-                wave_lds_sync();
-                const float *xl = X + (int64_t)(c - ccL - w0) * CH;
-#pragma unroll 4
-                for (int32_t j = 0; j < nL; ++j) {
-                    const double ic = coefL[j];
-#pragma unroll
-                    for (int k = 0; k < CH; ++k)
-                        left[k] = left[k] + ic * (double)xl[j * CH + k];
-                }
-                const float *xr = X + (int64_t)(c + 1 + ccR - w0) * CH;
-#pragma unroll 4
-                for (int32_t j = 0; j < nR; ++j) {
-                    const double ic = coefR[j];
-#pragma unroll
-                    for (int k = 0; k < CH; ++k)
-                        right[k] = right[k] + ic * (double)xr[-j * CH + k];
-                }
-                wave_lds_sync(); // the list is rewritten by the next row
-            } else {
-                const int32_t ccl = (max_fi - sfi) / inc;
-                half_filter<CH, true, false>(Cg, X, sfi + ccl * inc, inc,
-                                             (int32_t)(c - ccl - w0), left);
-                const int32_t fr = inc - sfi;
-                const int32_t ccr = (max_fi - fr) / inc;
-                half_filter<CH, false, false>(Cg, X, fr + ccr * inc, inc,
-                                              (int32_t)(c + 1 + ccr - w0), right);
+            for (int m = 0; m < M; ++m) {
+                valid[m] = (uint32_t)(M * g + m) < L && rbase + m < Bend;
+                const uint64_t n = rbase + m + (uint64_t)L * lane;
+                active[m] = valid[m] && n < Bend;
+                position(T, pos, active[m] ? n : rbase + (valid[m] ? m : 0), c[m], sfi[m]);
             }
-            if (active) {
-                int32_t *o = out + T.out_base + n * CH;
+            // phases and relative centres uniform over the wave?
+            int32_t sfi0[M];
+            int32_t dc[M]; // c_m - c_0 (lane 0's)
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                sfi0[m] = __builtin_amdgcn_readfirstlane(sfi[m]);
+                const int32_t d = (int32_t)(c[m] - c[0]);
+                dc[m] = __builtin_amdgcn_readfirstlane(d);
+                uni = uni && (!active[m] || (sfi[m] == sfi0[m] && d == dc[m]));
+            }
+            double left[M][CH], right[M][CH];
+#pragma unroll
+            for (int m = 0; m < M; ++m)
+#pragma unroll
+                for (int k = 0; k < CH; ++k)
+                    left[m][k] = right[m][k] = 0.0;
+            if (__all(uni)) {
+                // tap windows relative to c_0: left [dL_m, dc_m], right
+                // [dc_m + 1, top_m] (descending), as calc_output_* walks them
+                int32_t dL[M], fiL[M], nL[M], top[M], fiR[M], nR[M];
+                int32_t sl0 = 1 << 30, sl1 = -(1 << 30), sr0 = 1 << 30, sr1 = -(1 << 30);
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    const int32_t ccL = (max_fi - sfi0[m]) / inc;
+                    fiL[m] = sfi0[m] + ccL * inc;
+                    nL[m] = valid[m] ? fiL[m] / inc + 1 : 0;
+                    dL[m] = dc[m] - ccL;
+                    const int32_t frR = inc - sfi0[m];
+                    const int32_t ccR = (max_fi - frR) / inc;
+                    fiR[m] = frR + ccR * inc;
+                    nR[m] = valid[m] ? (fiR[m] - 1) / inc + 1 : 0;
+                    top[m] = dc[m] + 1 + ccR;
+                    if (valid[m]) {
+                        sl0 = min(sl0, dL[m]);
+                        sl1 = max(sl1, dc[m]);
+                        sr0 = min(sr0, dc[m] + 1);
+                        sr1 = max(sr1, top[m]);
+                    }
+                }
+                const int32_t WL = sl1 - sl0 + 1, WR = sr1 - sr0 + 1;
+                for (int32_t k = (int32_t)lane; k < WL; k += 64) {
+#pragma unroll
+                    for (int m = 0; m < M; ++m) {
+                        const int32_t j = k + sl0 - dL[m];
+                        cL[m * wmax + k] = (j >= 0 && j < nL[m]) ? interp_coeff(Cg, fiL[m] - j * inc)
+                                                                 : 0.0;
+                    }
+                }
+                for (int32_t k = (int32_t)lane; k < WR; k += 64) {
+#pragma unroll
+                    for (int m = 0; m < M; ++m) {
+                        const int32_t j = top[m] - sr1 + k;
+                        cR[m * wmax + k] = (j >= 0 && j < nR[m]) ? interp_coeff(Cg, fiR[m] - j * inc)
+                                                                 : 0.0;
+                    }
+                }
+                wave_lds_sync();
+                const float *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
+#pragma unroll 2
+                for (int32_t k = 0; k < WL; ++k) {
+                    double x[CH];
+#pragma unroll
+                    for (int q = 0; q < CH; ++q)
+                        x[q] = (double)xl[k * CH + q];
+#pragma unroll
+                    for (int m = 0; m < M; ++m) {
+                        const double ic = cL[m * wmax + k];
+#pragma unroll
+                        for (int q = 0; q < CH; ++q)
+                            left[m][q] = left[m][q] + ic * x[q];
+                    }
+                }
+                const float *xr = X + (int64_t)(c[0] + sr1 - w0) * CH;
+#pragma unroll 2
+                for (int32_t k = 0; k < WR; ++k) {
+                    double x[CH];
+#pragma unroll
+                    for (int q = 0; q < CH; ++q)
+                        x[q] = (double)xr[-k * CH + q];
+#pragma unroll
+                    for (int m = 0; m < M; ++m) {
+                        const double ic = cR[m * wmax + k];
+#pragma unroll
+                        for (int q = 0; q < CH; ++q)
+                            right[m][q] = right[m][q] + ic * x[q];
+                    }
+                }
+                wave_lds_sync(); // the tables are rewritten by the next item
+            } else {
+#pragma unroll
+                for (int m = 0; m < M; ++m) {
+                    if (!valid[m])
+                        continue;
+                    const int32_t ccl = (max_fi - sfi[m]) / inc;
+                    half_filter<CH, true, false>(Cg, X, sfi[m] + ccl * inc, inc,
+                                                 (int32_t)(c[m] - ccl - w0), left[m]);
+                    const int32_t fr = inc - sfi[m];
+                    const int32_t ccr = (max_fi - fr) / inc;
+                    half_filter<CH, false, false>(Cg, X, fr + ccr * inc, inc,
+                                                  (int32_t)(c[m] + 1 + ccr - w0), right[m]);
+                }
+            }
+#pragma unroll
+            for (int m = 0; m < M; ++m) {
+                if (!active[m])
+                    continue;
+                int32_t *o = out + T.out_base + (rbase + m + (uint64_t)L * lane) * CH;
 #pragma unroll
                 for (int k = 0; k < CH; ++k) {
-                    const float f = (float)(T.scale * (left[k] + right[k]));
-                    const float g = f * P.q;
-                    int32_t s = (g >= 2147483648.0f || g < -2147483648.0f || g != g)
-                                    ? (int32_t)0x80000000
-                                    : (int32_t)g;
-                    o[k] = s > P.hi ? P.hi : (s < P.lo ? P.lo : s);
+                    const float f = (float)(T.scale * (left[m][k] + right[m][k]));
+                    const float gq = f * P.q;
+                    int32_t sv = (gq >= 2147483648.0f || gq < -2147483648.0f || gq != gq)
+                                     ? (int32_t)0x80000000
+                                     : (int32_t)gq;
+                    o[k] = sv > P.hi ? P.hi : (sv < P.lo ? P.lo : sv);
                 }
             }
         }
         __syncthreads();
     }
 }
+
+// outputs per lane of k_rs_phase: as many as the accumulators allow
+template <int CH>
+constexpr int phase_m() { return CH <= 2 ? 4 : 2; }
 
 // ------------------------------------------------------------------ host
 thread_local std::string g_rs_err;
@@ -673,19 +764,21 @@ void launch_filter(const FilterArgs &A, bool hoist, bool xd, unsigned grid, unsi
 #undef RS_GO
 }
 
+constexpr unsigned kPhaseThreads = 512;
+
 template <int CH>
-void launch_phase(const FilterArgs &A, const uint2 *tasks, uint32_t n_tasks, uint32_t tmax,
+void launch_phase(const FilterArgs &A, const uint2 *tasks, uint32_t n_tasks, uint32_t wmax,
                   unsigned grid, size_t lds, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_rs_phase<CH>), dim3(grid), dim3(1024), lds, s, A.P, A.tr, tasks, n_tasks,
-                       A.pos, A.table, A.in, A.out, tmax);
+    hipLaunchKernelGGL((k_rs_phase<CH, phase_m<CH>()>), dim3(grid), dim3(kPhaseThreads), lds, s,
+                       A.P, A.tr, tasks, n_tasks, A.pos, A.table, A.in, A.out, wmax);
 }
 
 template <int CH>
 hipError_t set_lds_attr()
 {
     const hipFuncAttribute a = hipFuncAttributeMaxDynamicSharedMemorySize;
-    hipError_t e = hipFuncSetAttribute((const void *)k_rs_phase<CH>, a, 160 * 1024);
+    hipError_t e = hipFuncSetAttribute((const void *)k_rs_phase<CH, phase_m<CH>()>, a, 160 * 1024);
     if (e == hipSuccess)
         e = hipFuncSetAttribute((const void *)k_rs_filter<CH, true, double>, a, 160 * 1024);
     if (e == hipSuccess)
@@ -768,44 +861,51 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             return rsfail(ATG_ERR_INVALID, "SRC ratio outside [1/256, 256]");
     }
     // Phase-sharing plan (k_rs_phase): a track whose rational ratio repeats
-    // its phases every `period` outputs goes there when a task of 64 x period
+    // its phases every `period` outputs goes there when a task of 64 x lspan
     // outputs fits the LDS with its input window and the per-wave
-    // coefficient lists; the rest go to the per-output kernel k_rs_filter.
+    // coefficient tables; the rest go to the per-output kernel k_rs_filter.
     const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
     const size_t kLds = 160 * 1024;
-    std::vector<uint32_t> per(n, 0), rows(n, 0);
+    const uint32_t pm = channels <= 2 ? 4u : 2u; // phase_m<CH>()
+    const size_t waves = kPhaseThreads / 64;
+    std::vector<uint32_t> per(n, 0), rows(n, 0), lspan(n, 0);
     std::vector<char> phase(n, 0);
-    uint32_t tmax = 0;
+    uint32_t wmax = 0;
     for (int it = 0; it < 2; ++it) {
-        uint32_t tm = 0;
+        uint32_t wm = 0;
         for (uint32_t t = 0; t < n; ++t) {
             const uint64_t g = std::gcd((uint64_t)tracks[t].in_rate, (uint64_t)tracks[t].out_rate);
             const uint64_t p_out = tracks[t].out_rate / g, q_in = tracks[t].in_rate / g;
             const uint64_t reach = (uint64_t)(max_fi / conv[t].increment) + 2;
-            const uint32_t tm_t = std::max<uint32_t>(tmax, (uint32_t)reach);
-            const size_t coef = (size_t)16 * 2 * tm_t * sizeof(double);
+            const uint64_t step = (tracks[t].in_rate + tracks[t].out_rate - 1) / tracks[t].out_rate;
+            const uint32_t wm_t = (uint32_t)(reach + (pm - 1) * step + 2);
+            const size_t coef = waves * 2 * pm * std::max<uint32_t>(wmax, wm_t) * sizeof(double);
             phase[t] = 0;
             if (p_out > 65536)
                 continue;
+            const uint64_t L = p_out * ((pm + p_out - 1) / p_out);
             uint64_t r = 0;
             for (uint64_t R = 1; R <= 64; R *= 2) {
-                const size_t win = (size_t)(64 * q_in * R + 2 * reach + 8) * channels * 4;
+                const size_t win =
+                    (size_t)(64 * (L / p_out) * q_in * R + 2 * reach + 8 + (pm - 1) * step + 2) *
+                    channels * 4;
                 if (coef + win > kLds)
                     break;
                 r = R;
-                if (64 * p_out * R >= std::max<uint64_t>(tracks[t].pcm_frames, 1) * 2)
+                if (64 * L * R >= std::max<uint64_t>(tracks[t].pcm_frames, 1) * 2)
                     break; // one task already covers the track
             }
             if (!r)
                 continue;
             phase[t] = 1;
             per[t] = (uint32_t)p_out;
+            lspan[t] = (uint32_t)L;
             rows[t] = (uint32_t)r;
-            tm = std::max<uint32_t>(tm, (uint32_t)reach);
+            wm = std::max<uint32_t>(wm, wm_t);
         }
-        if (tm <= tmax)
+        if (wm <= wmax)
             break;
-        tmax = tm;
+        wmax = wm;
     }
     // k_rs_filter: the window as doubles when a chunk of >= 512 outputs fits
     // (no conversion per tap), else as floats with the largest chunk that fits
@@ -862,6 +962,8 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         T.pos_base = 0;
         T.span = 0;
         T.period = per[t];
+        T.lspan = lspan[t];
+        T.wext = (pm - 1) * (uint32_t)((a.in_rate + a.out_rate - 1) / a.out_rate) + 2;
         T.pad = 0;
         if (v.mode == POS_TABLE) {
             T.pos_base = posn;
@@ -870,14 +972,15 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         }
         T.chunk_base = chunk_track.size();
         if (phase[t]) {
-            T.span = 64ull * per[t] * rows[t];
+            T.span = 64ull * lspan[t] * rows[t];
             for (uint64_t k = 0; k * T.span < T.out_frames; ++k)
                 ptasks.push_back(make_uint2(t, (uint32_t)k));
             const uint64_t g = std::gcd((uint64_t)a.in_rate, (uint64_t)a.out_rate);
             const uint64_t reach = (uint64_t)(max_fi / v.increment) + 2;
-            lds_phase = std::max(lds_phase, (size_t)16 * 2 * tmax * sizeof(double) +
-                                                (size_t)(64 * (a.in_rate / g) * rows[t] +
-                                                         2 * reach + 8) * channels * 4);
+            lds_phase = std::max(lds_phase, waves * 2 * pm * wmax * sizeof(double) +
+                                                (size_t)(64 * (lspan[t] / per[t]) * (a.in_rate / g) *
+                                                         rows[t] + 2 * reach + 8 + T.wext) *
+                                                    channels * 4);
         } else {
             for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
                 chunk_track.push_back(t);
@@ -960,14 +1063,14 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         const uint2 *tk = (const uint2 *)X.ptasks;
         const uint32_t nt = (uint32_t)ptasks.size();
         switch (channels) {
-        case 1: launch_phase<1>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 2: launch_phase<2>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 3: launch_phase<3>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 4: launch_phase<4>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 5: launch_phase<5>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 6: launch_phase<6>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        case 7: launch_phase<7>(A, tk, nt, tmax, grid, lds_phase, s); break;
-        default: launch_phase<8>(A, tk, nt, tmax, grid, lds_phase, s); break;
+        case 1: launch_phase<1>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 2: launch_phase<2>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 3: launch_phase<3>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 4: launch_phase<4>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 5: launch_phase<5>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 6: launch_phase<6>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 7: launch_phase<7>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        default: launch_phase<8>(A, tk, nt, wmax, grid, lds_phase, s); break;
         }
         RSHIP(hipGetLastError());
     }

@@ -48,6 +48,12 @@ def enc_cases():
     return out
 
 
+LW_RANGES = ((0, 0), (1, 1), (4, 4), (0, 2), (2, 7), (5, 9), (0, 16), (250, 255))
+LW_SIGNALS = (("tone_c2_b16", "tone", 4096 * 2 + 333, 2, 16, 7),
+              ("chirp_c2_b24", "chirp", 4096 + 95, 2, 24, 8),
+              ("noise_c6_b16", "noise", 4096 + 11, 6, 16, 9))
+
+
 def make_pcm(kind, n, ch, bps, seed):
     return signals.make(kind, n, ch, bps, seed=seed)
 
@@ -66,6 +72,28 @@ def main():
         enc.append(dict(name=name, kind=kind, n=n, channels=ch, bps=bps, block_size=bs,
                         seed=seed, bytes=len(ref), sha256=hashlib.sha256(ref).hexdigest(),
                         framesets=len(fs)))
+    # interlacing leftweight ranges other than the reference standalone's
+    # fixed 0..4 (alac.c:57-72, 459-481): the reference encoder cannot be
+    # driven with them here, so each port mdat is pinned by the REFERENCE
+    # decoder decoding it back to the source exactly (and 0..4 by the
+    # encoder vectors above); the GPU must reproduce the port's bytes
+    lws = []
+    for (lo, hi) in LW_RANGES:
+        for name, kind, n, ch, bps, seed in LW_SIGNALS:
+            x = make_pcm(kind, n, ch, bps, seed)
+            mine, fs = oracle_port.alac_encode(x, ch, bps, minimum_interlacing_leftweight=lo,
+                                               maximum_interlacing_leftweight=hi)
+            img = m4a.m4a_file(ch, bps, 44100, 4096, n, mine, fs, create_date=1)
+            rc, out, err = oracle_port.ref_alac_decode(img)
+            # a leftweight above 4 can push the mixed channel past the
+            # element's sample size on full-scale input: the reference
+            # decoder then does not return the source (recorded, not a
+            # port failure)
+            ok = rc == 0 and out == oracle_port.pcm_bytes(x, bps)
+            lws.append(dict(name="%s_lw%d_%d" % (name, lo, hi), kind=kind, n=n, channels=ch,
+                            bps=bps, seed=seed, lw_min=lo, lw_max=hi, bytes=len(mine),
+                            sha256=hashlib.sha256(mine).hexdigest(), framesets=len(fs),
+                            reference_decoder_lossless=ok))
     # decoder: containers around reference mdats, clean + corrupted
     rng = np.random.default_rng(2024)
     for name, kind, n, ch, bps, seed in (("d_tone_c2_b16", "tone", 4096 * 3 + 111, 2, 16, 1),
@@ -109,10 +137,12 @@ def main():
     json.dump({"generator": "tests/golden/make_alac_golden.py",
                "reference": "src/encoders/alac.c, src/decoders/alac.c standalone "
                             "(oracle/_ref/alacenc, alacdec)",
-               "encoder": enc, "decoder": dec, "fixture": fixture},
+               "encoder": enc, "leftweights": lws, "decoder": dec, "fixture": fixture},
               open(OUT, "w"), indent=1)
-    print("%d encoder vectors (%d port mismatches), %d decoder streams -> %s"
-          % (len(enc), bad, len(dec), OUT))
+    print("%d encoder vectors (%d port mismatches), %d leftweight vectors (%d decode back "
+          "losslessly), %d decoder streams -> %s"
+          % (len(enc), bad, len(lws), sum(v["reference_decoder_lossless"] for v in lws),
+             len(dec), OUT))
     sys.exit(1 if bad else 0)
 
 

@@ -373,12 +373,14 @@ def rg_apply(pcm, channels, bps, multiplier, chunk_frames, dither):
 # --- ALAC (oracle/alac_port.c; pinned to oracle/_ref/alacenc / alacdec) ---
 REF_ALACENC = os.path.join(ORACLE_DIR, "_ref", "alacenc")
 REF_ALACDEC = os.path.join(ORACLE_DIR, "_ref", "alacdec")
-ALAC_DEFAULTS = dict(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14)
+ALAC_DEFAULTS = dict(block_size=4096, initial_history=10, history_multiplier=40, maximum_k=14,
+                     minimum_interlacing_leftweight=0, maximum_interlacing_leftweight=4)
 
 
 class AlacOptions(ctypes.Structure):
     _fields_ = [("block_size", c_u32), ("initial_history", c_u32),
-                ("history_multiplier", c_u32), ("maximum_k", c_u32)]
+                ("history_multiplier", c_u32), ("maximum_k", c_u32),
+                ("min_leftweight", c_u32), ("max_leftweight", c_u32)]
 
 
 class AlacInfo(ctypes.Structure):
@@ -428,7 +430,8 @@ def alac_encode(pcm, channels, bps, **opts):
     o = dict(ALAC_DEFAULTS)
     o.update(opts)
     op = AlacOptions(o["block_size"], o["initial_history"], o["history_multiplier"],
-                     o["maximum_k"])
+                     o["maximum_k"], o["minimum_interlacing_leftweight"],
+                     o["maximum_interlacing_leftweight"])
     a = np.ascontiguousarray(pcm, dtype=np.int32)
     frames = len(a) // channels
     cap = lib.alacport_max_mdat_bytes(frames, channels, bps, op.block_size)

@@ -28,6 +28,28 @@ def test_encoder_vectors(v):
     assert len(fs) == v["framesets"] and sum(fs) + 8 == len(mdat)
 
 
+@pytest.mark.parametrize("v", G["leftweights"], ids=lambda v: v["name"])
+def test_leftweight_vectors(v):
+    """minimum/maximum_interlacing_leftweight (alac.c:57-72, 459-481): the
+    port's mdat for each range is the recorded one, whose reference-decoder
+    round trip make_alac_golden.py checked (0..4 is pinned to the reference
+    encoder by test_encoder_vectors; the leftweight loop is the same code)"""
+    x = alac_cases.enc_pcm(v)
+    mdat, fs = op.alac_encode(x, v["channels"], v["bps"],
+                              minimum_interlacing_leftweight=v["lw_min"],
+                              maximum_interlacing_leftweight=v["lw_max"])
+    assert hashlib.sha256(mdat).hexdigest() == v["sha256"]
+    assert len(fs) == v["framesets"]
+
+
+def test_leftweight_vectors_mostly_lossless():
+    """all but the full-scale cases whose mixed channel outgrows the sample
+    size (leftweights above 4) decode back to the source in the reference
+    decoder"""
+    lossy = [v["name"] for v in G["leftweights"] if not v["reference_decoder_lossless"]]
+    assert sorted(lossy) == ["noise_c6_b16_lw5_9", "tone_c2_b16_lw250_255"]
+
+
 def _decode_all(data):
     st, info, _ = op.alac_read_info(data)
     if st:

@@ -54,6 +54,42 @@ def test_encoder_vectors_batch(key, vecs):
         assert r.pcm_frames == v["n"]
 
 
+def _lw_groups():
+    g = defaultdict(list)
+    for v in G["leftweights"]:
+        g[(v["channels"], v["bps"], v["lw_min"], v["lw_max"])].append(v)
+    return sorted(g.items())
+
+
+@pytest.mark.parametrize("key,vecs", _lw_groups(), ids=lambda x: str(x) if isinstance(x, tuple)
+                         else None)
+def test_leftweight_vectors_batch(key, vecs):
+    """minimum/maximum_interlacing_leftweight ranges (alac.c:57-72,
+    459-481): the GPU writes the recorded mdat bytes"""
+    ch, bps, lo, hi = key
+    pcms = [alac_cases.enc_pcm(v) for v in vecs]
+    mdats, sizes, res = _gpu_encode(pcms, ch, bps, minimum_interlacing_leftweight=lo,
+                                    maximum_interlacing_leftweight=hi)
+    for v, m, fs, r in zip(vecs, mdats, sizes, res):
+        assert r.status == 0
+        assert hashlib.sha256(m).hexdigest() == v["sha256"], v["name"]
+        assert len(fs) == v["framesets"]
+
+
+def test_leftweight_errors():
+    import audiotools
+    from audiotools import _atgpu, encoders
+    pcm = signals.make("tone", 5000, 2, 16, seed=1)
+    for lo, hi in ((3, 2), (0, 256), (-1, 4)):
+        with pytest.raises(ValueError):
+            encoders.encode_alac(io.BytesIO(), audiotools.FrameListReader(pcm, 44100, 2, 16),
+                                 4096, 10, 40, 14, lo, hi)
+    enc = _atgpu.alac_encoder()
+    with pytest.raises(_atgpu.ATGError):
+        enc.encode(enc.options(minimum_interlacing_leftweight=5, maximum_interlacing_leftweight=4),
+                   pcm.astype(np.int16), [(0, 2500)], 2, 16)
+
+
 @pytest.mark.parametrize("ch,bps", [(2, 16), (2, 24), (1, 16), (6, 24), (8, 16), (3, 24)])
 def test_matches_oracle_mixed_batch(ch, bps):
     kinds = ["tone", "noise", "silence", "chirp", "sine", "wasted"]

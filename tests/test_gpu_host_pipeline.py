@@ -133,3 +133,63 @@ def test_pinned_buffers_direct_dma(pin_in, pin_out, chunked):
         got = [(int(offs[r.first_frame + i]), int(fpcm[r.first_frame + i]))
                for i in range(r.n_frames)]
         assert got == woffs, k
+
+
+@pytest.mark.parametrize("pinned", [True, False])
+def test_async_host_jobs_overlap(pinned, chunked):
+    """atg_flac_encode_host_async: three jobs queued back to back share the
+    chunk pipeline (a job's first chunks ride behind the previous job's
+    last ones; 1 MB chunks wrap the three stages within and across jobs);
+    waited in order, then a fourth waited before it could overlap.  Every
+    job's images and frame tables equal the synchronous call's, which are
+    the port's (test_chunked_host_encode_matches_port)."""
+    eng, A = chunked
+    eng.set_host_chunk_bytes(1 << 20)
+    opts = A.make_options(**oracle_port.PRESETS["8"])
+    jobs, want = [], []
+    for seed in range(4):
+        rng = np.random.default_rng(40 + seed)
+        lens, parts = _tracks(rng, 7 + 3 * seed, 1000, 150000)
+        host = np.concatenate(parts)
+        pcm = A.pinned_empty(host.shape, np.int16) if pinned else host
+        pcm[:] = host
+        tracks, pos = [], 0
+        for m in lens:
+            tracks.append((pos, m))
+            pos += m
+        _, nb = eng.bounds(opts, tracks, 2, 16)
+        out = A.pinned_empty(nb, np.uint8) if pinned else None
+        jobs.append((pcm, tracks, out))
+        o, r, f, p = eng.encode(opts, pcm, tracks, 2, 16, 44100)
+        want.append(([bytes(o[x.out_offset:x.out_offset + x.bytes]) for x in r],
+                     f.copy(), p.copy()))
+    queued = [eng.encode_async(opts, pcm, tracks, 2, 16, 44100, out=out)
+              for pcm, tracks, out in jobs[:3]]
+    got = [j.wait() for j in queued]
+    got.append(eng.encode_async(opts, *jobs[3][:2], 2, 16, 44100, out=jobs[3][2]).wait())
+    for k, (out, res, offs, fpcm) in enumerate(got):
+        imgs = [bytes(out[x.out_offset:x.out_offset + x.bytes]) for x in res]
+        assert imgs == want[k][0], k
+        assert np.array_equal(offs, want[k][1]) and np.array_equal(fpcm, want[k][2]), k
+
+
+def test_async_host_job_refuses_device_batches(chunked, gpu_engine):
+    """a host job in flight and an unwaited device batch exclude each other
+    (they share the engine's slots); a ticket is waited once"""
+    eng, A = chunked
+    eng.set_host_chunk_bytes(1 << 20)
+    rng = np.random.default_rng(3)
+    lens, parts = _tracks(rng, 9, 50000, 150000)
+    pcm = np.concatenate(parts)
+    tracks, pos = [], 0
+    for m in lens:
+        tracks.append((pos, m))
+        pos += m
+    opts = A.make_options(**oracle_port.PRESETS["8"])
+    job = eng.encode_async(opts, pcm, tracks, 2, 16, 44100)
+    with pytest.raises(A.ATGError):
+        eng.encode_device_async(opts, 0, A.PCM_S16, tracks, 2, 16, 44100, 0, 0)
+    out, res, _, _ = job.wait()
+    assert all(r.bytes for r in res)
+    with pytest.raises(A.ATGError):
+        A._check(eng.lib, eng.lib.atg_flac_encode_host_wait(eng.handle, job.ticket))

@@ -22,3 +22,5 @@ for lib in "$R"/exp/libatgpu_k2e*.so; do
     n=$(basename "$lib" .so)
     run "${n#libatgpu_}" "$lib"
 done
+cd "$R"
+timeout -k 10 120 python -u tools/queue_probe.py > "$OUT/queue_probe.log" 2>&1

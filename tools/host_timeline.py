@@ -36,9 +36,20 @@ def main():
         t0 = time.perf_counter()
         eng.encode(opts, pcm, tracks, 2, 16, 44100, out=out)
         dt = time.perf_counter() - t0
-        print("batch %.2f ms  %.3f M frames/s (%s)" % (dt * 1e3, 65536 / dt / 1e6,
-                                                        "pinned" if pinned else "pageable"),
-              flush=True)
+        print("batch %.2f ms  %.3f M frames/s (%s, sync)"
+              % (dt * 1e3, 65536 / dt / 1e6, "pinned" if pinned else "pageable"), flush=True)
+    # batches queued back to back (atg_flac_encode_host_async), two in flight
+    outs = [out, _atgpu.pinned_empty(nb, np.uint8) if pinned else None]
+    t0 = time.perf_counter()
+    pend = []
+    for k in range(steps):
+        pend.append(eng.encode_async(opts, pcm, tracks, 2, 16, 44100, out=outs[k % 2]))
+        if len(pend) > 1:
+            pend.pop(0).wait()
+    pend.pop(0).wait()
+    dt = (time.perf_counter() - t0) / steps
+    print("batch %.2f ms  %.3f M frames/s (%s, queued)"
+          % (dt * 1e3, 65536 / dt / 1e6, "pinned" if pinned else "pageable"), flush=True)
 
 
 if __name__ == "__main__":

@@ -22,8 +22,8 @@ names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
          "k_stream_header": "stream_header",
          # decoder (flac_decode.hip, md5.hip)
          "k_dec_scan": "dec_scan", "k_dec_parse": "dec_parse", "k_dec_chain": "dec_chain",
-         "k_dec_subframe": "dec_subframe", "k_dec_unrow": "dec_unrow",
-         "k_dec_interleave": "dec_interleave", "k_bytes_md5": "dec_md5", "k_bytes_md5_pair": "dec_md5",
+         "k_dec_subframe": "dec_subframe", "k_dec_emit": "dec_emit",
+         "k_bytes_md5": "dec_md5", "k_bytes_md5_pair": "dec_md5",
          "k_pcm_bps": "pcm_bps",
          # resampler (resample.hip)
          "k_rs_phase": "rs_filter", "k_rs_filter": "rs_filter_deep"}
