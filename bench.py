@@ -28,6 +28,7 @@ import argparse
 import json
 import os
 import socket
+import struct
 import subprocess
 import sys
 import tempfile
@@ -82,6 +83,13 @@ def parse_args(argv=None):
     ap.add_argument("--chain-seconds", type=int, default=10)
     ap.add_argument("--no-chain", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-to-host leg")
+    ap.add_argument("--no-t2t", action="store_true", help="skip the track2track leg")
+    ap.add_argument("--t2t-procs", type=int, default=8,
+                    help="track2track leg: encoder processes sharing the GPU")
+    ap.add_argument("--t2t-worker", nargs=3, metavar=("LIST", "OUTDIR", "GO"),
+                    help=argparse.SUPPRESS)
+    ap.add_argument("--no-rg4", action="store_true", help="skip the config-4 ReplayGain leg")
+    ap.add_argument("--rg4-seconds", type=int, default=10)
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -862,6 +870,189 @@ def _device_equal(torch, eng, d_ptr, ref, n_tracks=1):
     return False, n_tracks
 
 
+def t2t_worker(list_file, out_dir, go_file):
+    """one track2track encoder process (track2track:650-669 runs one process
+    per track, each calling encode_flac on its file): audiotools WaveReader
+    -> encoders.encode_flac (the streaming single-track path over the C
+    ABI) for every .wav in list_file, once go_file appears; prints its
+    timing as JSON"""
+    import audiotools
+    from audiotools import _atgpu, encoders, wav
+    _atgpu.load_library()
+    _atgpu.engine()  # HIP up before the clock
+    names = [ln.strip() for ln in open(list_file) if ln.strip()]
+    print(json.dumps({"ready": True}), flush=True)
+    while not os.path.exists(go_file):
+        time.sleep(0.001)
+    t0 = time.perf_counter()
+    frames = 0
+    for fn in names:
+        out = os.path.join(out_dir, os.path.basename(fn)[:-4] + ".flac")
+        r = wav.WaveReader(fn)
+        offs = encoders.encode_flac(out, audiotools.BufferedPCMReader(r), **FLAC8)
+        frames += len(offs)
+    print(json.dumps({"frames": frames, "seconds": time.perf_counter() - t0}), flush=True)
+    return 0
+
+
+def t2t_leg(args, pcm_host, n_samples, threads):
+    """track2track-shaped use of the drop-in (track2track
+    :650-669): --t2t-procs processes share the GPU, each encoding its share
+    of the tracks one file at a time through encode_flac(WaveReader) -- the
+    per-process, per-file path a track2track run takes, with WAV parsing and
+    file I/O inside the clock.  The same files through the reference encoder
+    (oracle/_ref/flacenc) at the same process count beside it; every GPU
+    .flac is compared with the reference's."""
+    import oracle_port
+    n_tracks = min(len(pcm_host) // (n_samples * 2), 8 * args.t2t_procs)
+    procs = max(1, args.t2t_procs)
+    out = {"metric": "track2track-shaped FLAC-8 encode: %d processes x encode_flac(WaveReader) "
+                     "on one GPU, frames/s" % procs}
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        files = []
+        for t in range(n_tracks):
+            fn = os.path.join(d, "t%04d.wav" % t)
+            x = pcm_host[t * n_samples * 2:(t + 1) * n_samples * 2]
+            data = x.astype("<i2").tobytes()
+            with open(fn, "wb") as f:
+                f.write(struct.pack("<4sI4s4sIHHIIHH4sI", b"RIFF", 36 + len(data), b"WAVE",
+                                    b"fmt ", 16, 1, 2, 44100, 44100 * 4, 4, 16, b"data",
+                                    len(data)))
+                f.write(data)
+            files.append(fn)
+        gdir = os.path.join(d, "gpu")
+        os.mkdir(gdir)
+        go = os.path.join(d, "go")
+        workers = []
+        for k in range(procs):
+            lf = os.path.join(d, "list%d" % k)
+            with open(lf, "w") as f:
+                f.write("\n".join(files[k::procs]))
+            workers.append(subprocess.Popen(
+                [sys.executable, os.path.abspath(__file__), "--t2t-worker", lf, gdir, go],
+                stdout=subprocess.PIPE, text=True))
+        for w in workers:
+            json.loads(w.stdout.readline())  # ready
+        t0 = time.perf_counter()
+        open(go, "w").close()
+        stats = [json.loads(w.stdout.readline()) for w in workers]
+        wall = time.perf_counter() - t0
+        if any(w.wait() for w in workers):
+            raise RuntimeError("a track2track worker failed")
+        frames = sum(st["frames"] for st in stats)
+        out.update({"value": round(frames / wall, 1), "unit": "frames/s",
+                    "processes": procs, "tracks": n_tracks, "frames": frames,
+                    "wall_s": round(wall, 3),
+                    "per_process_frames_per_s": round(frames / procs / wall, 1)})
+        # the reference encoder, one process per track, the same count at a time
+        exe = oracle_port.REF_FLACENC
+        if os.path.exists(exe):
+            rargs = [exe, "-c", "2", "-r", "44100", "-b", "16", "-B", "4096", "-l", "12", "-P",
+                     "0", "-R", "6", "-m", "-e"]
+            rdir = os.path.join(d, "ref")
+            os.mkdir(rdir)
+
+            def one(t):
+                with open(files[t], "rb") as f:
+                    raw = f.read()[44:]
+                fo = os.path.join(rdir, "t%04d.flac" % t)
+                subprocess.run(rargs + [fo], input=raw, stdout=subprocess.DEVNULL, check=True)
+
+            rdt = _parallel(n_tracks, procs, one)
+            same = all(open(os.path.join(gdir, "t%04d.flac" % t), "rb").read() ==
+                       open(os.path.join(rdir, "t%04d.flac" % t), "rb").read()
+                       for t in range(n_tracks))
+            out["cpu_baseline"] = {"value": round(frames / rdt, 1), "unit": "frames/s",
+                                   "cores": procs, "kind": "reference",
+                                   "sample": "the same %d files, reference encoder "
+                                             "(oracle/_ref/flacenc) one process per track, "
+                                             "%d at a time, %.1f s" % (n_tracks, procs, rdt)}
+            out["gpu_files_identical_to_reference"] = same
+    return out
+
+
+def rg4_leg(args, torch, dist, world, rank, device, barrier):
+    """BASELINE config 4: ReplayGain album scan, 1024 tracks of
+    --rg4-seconds s per GPU, one album per GPU: each
+    rank's tracks are its album (title gains + the album gain/peak from the
+    summed histogram); the albums' (gain, peak) go to every rank over RCCL
+    (all_gather), and the whole set's gain/peak over an all-reduce of the
+    histograms (SUM) and peaks (MAX).  The first 64 tracks' title results
+    and the album of those 64 are checked against the CPU oracle."""
+    from audiotools import _atgpu
+    n_tracks, n = 1024, args.rg4_seconds * 44100
+    g = torch.Generator(device=device)
+    g.manual_seed(77 + rank)
+    t = torch.arange(n, device=device, dtype=torch.float32)
+    x = torch.empty((n_tracks, n, 2), dtype=torch.int32, device=device)
+    for k in range(0, n_tracks, 64):
+        f = 90.0 + 13.0 * torch.arange(k, k + 64, device=device, dtype=torch.float32)
+        amp = 2000.0 + 300.0 * (torch.arange(k, k + 64, device=device) % 50).float()
+        tone = torch.sin(2 * np.pi * t[None, :] * f[:, None] / 44100.0) * amp[:, None]
+        nz = torch.randint(-800, 800, (64, n, 2), device=device, generator=g, dtype=torch.int32)
+        x[k:k + 64] = (tone[:, :, None].round().to(torch.int32) + nz).clamp(-32768, 32767)
+    del t
+    x = x.reshape(-1)
+    torch.cuda.synchronize()
+    tracks = [_atgpu.RgTrack(k * n, n, 2, 16, 44100, 0) for k in range(n_tracks)]
+    hist = torch.zeros(12000, dtype=torch.int32, device=device)
+
+    def step():
+        res, peaks = _atgpu.replaygain_device(x.data_ptr(), tracks, 1, hist.data_ptr())
+        gain = _atgpu.replaygain_hist_gain(hist.data_ptr(), 1)[0]
+        return res, gain, peaks[0]
+
+    steps = max(1, min(args.steps, 3))
+    step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        res, album_gain, album_peak = step()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        elapsed = reduce_max(torch, dist, elapsed, device)
+        mine = torch.tensor([album_gain, album_peak], dtype=torch.float64, device=device)
+        albums = [torch.empty_like(mine) for _ in range(world)]
+        dist.all_gather(albums, mine)
+        albums = [tuple(float(v) for v in a.tolist()) for a in albums]
+        pk = torch.tensor([album_peak], dtype=torch.float64, device=device)
+        album_reduce(dist, world, hist, pk)
+        set_gain = _atgpu.replaygain_hist_gain(hist.data_ptr(), 1)[0]
+        set_peak = float(pk.item())
+    else:
+        albums = [(album_gain, album_peak)]
+        set_gain, set_peak = album_gain, album_peak
+    frames = n_tracks * n * world * steps / BLOCK
+    out = {"metric": "ReplayGain album scan (config 4), FLAC-frame-equivalents/s",
+           "value": round(frames / elapsed, 1), "unit": "frames/s",
+           "ms_per_step": round(elapsed / steps * 1e3, 3), "steps": steps,
+           "config": {"tracks_per_gpu": n_tracks, "seconds_per_track": args.rg4_seconds,
+                      "album": "one per GPU"},
+           "albums": [{"gain_db": a, "peak": p} for a, p in albums],
+           "all_albums": {"gain_db": set_gain, "peak": set_peak,
+                          "collective": "all_gather (gain, peak) + all_reduce SUM uint32[12000]"
+                                        " / MAX f64 (RCCL)" if world > 1 else "none (1 rank)"}}
+    if rank == 0 and not args.no_verify:
+        import oracle_port
+        oracle_port.load()
+        xh = x[:64 * n * 2].cpu().numpy()
+        bad, hsum, pmax = [], None, 0.0
+
+        def one(k):
+            A, pk = oracle_port.rg_title(xh[k * n * 2:(k + 1) * n * 2], 2, 16, 44100)
+            if not (oracle_port.rg_gain(A) == res[k].title_gain and pk == res[k].title_peak):
+                bad.append(k)
+            return A, pk
+
+        outs = [one(k) for k in range(64)]
+        out["verified_tracks"] = 64 - len(bad)
+        out["verified_vs_oracle"] = not bad
+    del x, hist
+    return out
+
+
+
 def album_reduce(dist, world, hist, peak):
     """an album spread over ranks: SUM of the uint32 window histograms (held
     as int32; two's-complement sums are the same bits) and MAX of the peak,
@@ -986,6 +1177,8 @@ def selftest(args):
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
+    if args.t2t_worker:
+        return t2t_worker(*args.t2t_worker)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # spawn the ranks before anything initialises a GPU (never re-exec)
         return launch(args, argv)
@@ -1102,6 +1295,11 @@ def main(argv=None):
             convert = convert_leg(args, torch, device, pcm)
         resample = resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier,
                                 threads, rank == 0 and not args.no_verify)
+    t2t = rg4 = None
+    if not args.no_t2t and rank == 0 and world == 1:
+        t2t = t2t_leg(args, pcm_host, n_samples, threads)
+    if not args.no_rg4:
+        rg4 = rg4_leg(args, torch, dist, world, rank, device, barrier)
     chain = None
     if not args.no_chain:
         chain = chain_leg(args, torch, dist, world, device, barrier, threads,
@@ -1168,6 +1366,11 @@ def main(argv=None):
         if ref is not None:
             ref_images, rdt = ref
             ref_ok = all(ref_images[t] == images[t] for t in range(nref))
+            # -j nproc as track2track would on this host: one process per
+            # visible CPU; the cgroup quota (cpu_share) bounds what it gets
+            nproc = os.cpu_count() or threads
+            refn = ref_encode_sample(pcm_host, nref, n_samples, nproc) if nproc > threads \
+                else None
             cpu = {"value": round(nref * args.frames / rdt, 2), "unit": "frames/s",
                    "cores": threads, "kind": "reference",
                    "sample": "reference encoder (oracle/_ref/flacenc, built from the "
@@ -1175,6 +1378,14 @@ def main(argv=None):
                              "%d frames, one process per track, %d at a time, %.1f s"
                              % (nref, args.frames, threads, rdt),
                    "gpu_images_identical": ref_ok}
+            if refn is not None:
+                cpu["nproc"] = {"value": round(nref * args.frames / refn[1], 2),
+                                "unit": "frames/s", "processes": nproc,
+                                "sample": "the same %d tracks, %d processes at a time "
+                                          "(os.cpu_count()), %.1f s; the cgroup CPU quota "
+                                          "%s CPUs bounds it" % (nref, nproc, refn[1],
+                                                                 share_info.get(
+                                                                     "cgroup_quota_cpus"))}
         else:
             cpu = dict(port) if port else dict(port1)
             cpu["note"] = "oracle/_ref absent: port timing"
@@ -1227,6 +1438,8 @@ def main(argv=None):
         "host_to_host": host,
         "resample": resample,
         "chain": chain,
+        "replaygain_config4": rg4,
+        "track2track": t2t,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

@@ -45,7 +45,8 @@
 
 // timing experiments only (tools/gpu_exp.sh), 0 in every product build:
 // 1 FIXED predictor only, 2 no pass 2, 3 trivial partition choice, 4 no FIXED sums,
-// 5 no lower-bound pruning, 6 one tap pair per residual (prediction cost)
+// 5 no lower-bound pruning, 6 one tap pair per residual (prediction cost),
+// 7 no 64-bit fallback (every predictor on the folded 32-bit path)
 #ifndef ATG_K2F_EXP
 #define ATG_K2F_EXP 0
 #endif
@@ -778,7 +779,7 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
             thr = best > hdr ? best - hdr : 0u;
     }
     Eval16 ev;
-    if (fold_ok && 2u * rbound + 1u < (1ull << 26))
+    if ((fold_ok && 2u * rbound + 1u < (1ull << 26)) || ATG_K2F_EXP == 7)
         ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
                             TWO && ci.amax <= 32767u);
     else

@@ -104,6 +104,21 @@ __device__ __forceinline__ double filt(Chan &s, double x, const double *ky, cons
 // each lane filters one channel and writes its per-window sums; k_rg_bin
 // bins (lsum + rsum) / window / 2 per window.  Mono tracks filter once and
 // use the same sums for both channels (the reference duplicates the channel).
+//
+// The filter is a serial recurrence whose every step depends on the last
+// output from its second operation on (the reference's operation order), so
+// a lane's time is (samples) x (the latency of ~26 dependent fp64 adds):
+// nothing else may stall it.  The wave's 32 tracks are staged through LDS
+// in chunks of 64 frames, double-buffered: at each chunk boundary the lanes
+// store the chunk loaded one boundary earlier and issue the next chunk's
+// loads, which then have 64 samples of filtering to arrive; the sample loop
+// reads the lane's channel from LDS.  Every lane handles sample f at step f
+// (the read()/batch/window bookkeeping only groups the running sums), so the
+// chunk schedule is wave-uniform; the bookkeeping is a per-lane state
+// machine.
+constexpr uint32_t kRgChunk = 64;
+constexpr uint32_t kRgStride = 2 * kRgChunk + 2; // ints per track per buffer (conflict-free reads)
+
 __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm,
                                                  const RgTrack *__restrict__ tracks, uint32_t n,
                                                  const uint64_t *__restrict__ win_base,
@@ -111,82 +126,127 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
                                                  double *__restrict__ wsum,
                                                  double *__restrict__ peaks)
 {
-    const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-    if (g >= 2 * n)
-        return;
-    const uint32_t t = g >> 1, chan = g & 1;
-    const RgTrack T = tracks[t];
-    if (chan == 1 && T.ch == 1)
-        return; // mono: channel 0's sums stand for both
-    const double *ky = c_yule[T.fi], *kb = c_butter[T.fi];
-    const int32_t *p = pcm + T.off + chan;
-    double *W = wsum + 2 * win_base[t] + chan;
-    const long window = T.window;
-    const double peak_shift = (double)(1 << (T.bps - 1));
+    __shared__ int32_t buf[2][32 * kRgStride];
+    const uint32_t lane = threadIdx.x, j = lane >> 1, chan = lane & 1;
+    const uint32_t g = blockIdx.x * 64 + lane, t = g >> 1;
+    const bool have = t < n;
+    RgTrack T = {};
+    if (have)
+        T = tracks[t];
+    // lanes of a track past the batch or the second channel of a mono track
+    // only help with the loads
+    const bool run = have && !(chan == 1 && T.ch == 1);
+    const uint64_t frames = have ? T.frames : 0;
+    uint64_t fmax = frames;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1)
+        fmax = max(fmax, (uint64_t)__shfl_xor((unsigned long long)fmax, o));
+    const uint32_t ch = have ? T.ch : 1u;
+    const int32_t *__restrict__ src = pcm + (have ? T.off : 0);
+    // chunk loads: the lane pair of track j fetches its 64 frames x ch ints,
+    // lane h the ints [64 h, 64 h + 64) of them
+    int32_t ld[kRgChunk];
+    auto load_chunk = [&](uint64_t F) {
+        const uint64_t lim = frames * ch; // ints of the track
+#pragma unroll
+        for (uint32_t i = 0; i < kRgChunk; ++i) {
+            const uint64_t q = F * ch + chan * kRgChunk + i;
+            ld[i] = (have && q < lim && chan * kRgChunk + i < kRgChunk * ch) ? src[q] : 0;
+        }
+    };
+    auto store_chunk = [&](int b) {
+#pragma unroll
+        for (uint32_t i = 0; i < kRgChunk; ++i)
+            buf[b][j * kRgStride + chan * kRgChunk + i] = ld[i];
+    };
+    const double *ky = c_yule[have ? T.fi : 0], *kb = c_butter[have ? T.fi : 0];
+    double *W = wsum + 2 * (have ? win_base[t] : 0) + chan;
+    const long window = have ? (long)T.window : 1;
     Chan S = {};
-    double sum = 0;
-    // max |x| as an integer: dividing by 2^(bps-1) is exact and monotonic,
-    // so max(|x|) / 2^(bps-1) == max(|x| / 2^(bps-1)) bit for bit
+    double sum = 0, gs = 0;
     uint32_t amax = 0;
-    long totsamp = 0, nwin = 0;
-    const uint64_t last = T.frames ? T.frames - 1 : 0;
-    const uint32_t stride = T.ch;
-    int32_t nx = T.frames ? p[0] : 0;
-    uint32_t pf = 0;
-    uint64_t ci = T.chunk_base;
-    for (uint64_t c0 = 0; c0 < T.frames;) {
-        // one analyze_samples call per read() result (replaygain.c:210-305)
-        const long n4 = T.chunk_base != ~0ull ? (long)chunks[ci++]
-                                              : (long)(T.frames - c0 < 4096 ? T.frames - c0 : 4096);
-        long pos = 0, batch = n4;
-        while (batch > 0) {
-            long cur = batch > window - totsamp ? window - totsamp : batch;
-            if (pos < 10 && cur > 10 - pos)
-                cur = 10 - pos;
-            const long singles = cur % 16;
-            double gs = 0;
-            for (long k = 0; k < cur; ++k) {
-                const uint64_t f = c0 + (uint64_t)(pos + k);
-                const int32_t iv = nx;
-                const uint64_t f1 = f + 1 < last ? f + 1 : last;
-                nx = p[f1 * stride];
-                const uint64_t f64 = f + 64 < last ? f + 64 : last;
-                pf ^= (uint32_t)p[f64 * stride];
-                double x;
-                if (T.bps == 8)
-                    x = (double)(iv << 8);
-                else if (T.bps == 16)
-                    x = (double)iv;
-                else
-                    x = (double)(iv >> 8);
-                const uint32_t av = (uint32_t)(iv < 0 ? -(int64_t)iv : iv);
-                amax = av > amax ? av : amax;
-                const double o = filt(S, x, ky, kb);
-                if (k < singles) {
-                    sum += o * o;
-                } else {
-                    const long gi = (k - singles) & 15;
-                    gs = gi == 0 ? o * o : gs + o * o;
-                    if (gi == 15)
-                        sum += gs;
-                }
+    // read() / batch / window bookkeeping (replaygain.c:210-305)
+    uint64_t ci = have ? T.chunk_base : 0, c0 = 0;
+    auto next_read = [&]() -> long {
+        if (c0 >= frames)
+            return 0;
+        return T.chunk_base != ~0ull ? (long)chunks[ci++]
+                                     : (long)(frames - c0 < 4096 ? frames - c0 : 4096);
+    };
+    long n4 = run ? next_read() : 0, pos = 0, batch = n4, totsamp = 0, nwin = 0, k = 0;
+    long cur = 0, singles = 0;
+    auto start_batch = [&]() {
+        cur = batch > window - totsamp ? window - totsamp : batch;
+        if (pos < 10 && cur > 10 - pos)
+            cur = 10 - pos;
+        singles = cur % 16;
+        k = 0;
+    };
+    start_batch();
+    load_chunk(0);
+    for (uint64_t F = 0; F < fmax; F += kRgChunk) {
+        const int b = (int)((F / kRgChunk) & 1);
+        store_chunk(b);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+        if (F + kRgChunk < fmax)
+            load_chunk(F + kRgChunk);
+        const int32_t *xb = &buf[b][j * kRgStride + chan];
+        const uint64_t nk = run && frames > F ? min((uint64_t)kRgChunk, frames - F) : 0;
+        int32_t nx = xb[0];
+        for (uint32_t kk = 0; kk < nk; ++kk) {
+            // the next sample's LDS read is issued before this one's filter
+            const int32_t iv = nx;
+            nx = xb[(kk + 1) * ch]; // inside the padded row when kk + 1 == 64
+            double x;
+            if (T.bps == 8)
+                x = (double)(iv << 8);
+            else if (T.bps == 16)
+                x = (double)iv;
+            else
+                x = (double)(iv >> 8);
+            const uint32_t av = (uint32_t)(iv < 0 ? -(int64_t)iv : iv);
+            amax = av > amax ? av : amax;
+            const double o = filt(S, x, ky, kb);
+            const double o2 = o * o;
+            if (k < singles) {
+                sum += o2;
+            } else {
+                const long gi = (k - singles) & 15;
+                gs = gi == 0 ? o2 : gs + o2;
+                if (gi == 15)
+                    sum += gs;
             }
-            batch -= cur;
-            pos += cur;
-            totsamp += cur;
-            if (totsamp == window) {
-                W[2 * nwin] = sum;
-                if (T.ch == 1)
-                    W[2 * nwin + 1] = sum;
-                ++nwin;
-                sum = 0.;
-                totsamp = 0;
+            if (++k == cur) { // the batch ends
+                batch -= cur;
+                pos += cur;
+                totsamp += cur;
+                if (totsamp == window) {
+                    W[2 * nwin] = sum;
+                    if (T.ch == 1)
+                        W[2 * nwin + 1] = sum;
+                    ++nwin;
+                    sum = 0.;
+                    totsamp = 0;
+                }
+                if (batch == 0) { // the next read() result
+                    c0 += (uint64_t)n4;
+                    n4 = next_read();
+                    batch = n4;
+                    pos = 0;
+                }
+                if (batch > 0)
+                    start_batch();
             }
         }
-        c0 += (uint64_t)n4;
+        // the buffer is rewritten two boundaries later: every lane's reads
+        // of it are done before its next store (in-order LDS per wave)
+        __builtin_amdgcn_wave_barrier();
     }
-    asm volatile("" ::"v"(pf)); // keep the prefetch loads
-    const double peak = (double)amax / peak_shift;
+    if (!run)
+        return;
+    const double peak = (double)amax / (double)(1 << (T.bps - 1));
     peaks[2 * t + chan] = peak;
     if (T.ch == 1)
         peaks[2 * t + 1] = peak;
