@@ -305,7 +305,10 @@ typedef struct {
    offsets() view (flac.c:365-443, which never checks CRC-16): walk_frames
    frames are walked (frame arrays first_frame .. first_frame+walk_frames-1,
    decoded PCM continuing after pcm_frames) before walk_status stops it.
-   The two differ only when a frame fails its CRC-16. */
+   The two differ only when a frame fails its CRC-16.  walk_end = the byte
+   (from the track's first frame) where the walk stopped: the frame that
+   stopped it, or the end of the last frame once remaining reached 0 -- a
+   streaming caller resumes a window there. */
 typedef struct {
     uint64_t pcm_offset;
     uint64_t pcm_frames;
@@ -316,6 +319,7 @@ typedef struct {
     uint8_t md5[16];
     int32_t walk_status;
     uint32_t reserved;
+    uint64_t walk_end;
 } atg_flac_dec_result;
 
 typedef struct atg_decoder atg_decoder;

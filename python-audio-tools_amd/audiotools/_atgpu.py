@@ -110,7 +110,7 @@ class DecResult(ctypes.Structure):
                 ("first_frame", c_u32), ("n_frames", c_u32),
                 ("status", c_i32), ("walk_frames", c_u32),
                 ("md5", ctypes.c_uint8 * 16), ("walk_status", c_i32),
-                ("reserved", c_u32)]
+                ("reserved", c_u32), ("walk_end", c_u64)]
 
 
 # decode status codes (include/atgpu.h ATG_FD_*) and the reference's

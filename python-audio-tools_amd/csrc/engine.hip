@@ -650,7 +650,9 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     const bool split_md5 = pipelined && !md5_early &&
                            ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
                             (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, md5_early && wait_before ? wait_before : ev[1], 0));
+    // (md5_early: after the chunk's upload and this batch's track tables --
+    // ev_tables is recorded on the main stream behind both)
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, md5_early ? sl.ev_tables : ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
     if (!pl.frames_only)
         HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));

@@ -83,6 +83,7 @@ struct DecCount {
     uint64_t crc_pcm;    // PCM frames before the first bad CRC-16 frame
     uint32_t crc_frame;  // index of that frame, ~0u if none
     uint32_t pad;
+    uint64_t stop;       // byte where the walk stopped (from the track's start)
 };
 
 struct ParseRec {
@@ -774,6 +775,7 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
         dc.crc_pcm = crc_pcm;
         dc.crc_frame = crc_frame;
         dc.pad = 0;
+        dc.stop = pos - t.start;
         counts[ti] = dc;
     }
 }
@@ -1553,6 +1555,7 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
                 r.status = FD_MD5;
         }
         r.reserved = 0;
+        r.walk_end = c.stop;
     }
     sl.busy = false;
     d->last = (int)(&sl - d->slot);

@@ -54,6 +54,11 @@
 #ifndef ATG_K2F_FEW
 #define ATG_K2F_FEW 0
 #endif
+// 1: predictors that fail the 32-bit fold's bound take the split fold
+// (eval_split) instead of the 64-bit loop
+#ifndef ATG_K2F_SPLIT
+#define ATG_K2F_SPLIT 1
+#endif
 // waves per SIMD the register allocation targets
 #ifndef ATG_K2F_WPE
 #define ATG_K2F_WPE 4
@@ -434,6 +439,253 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     return eval_tail(lane_sum, u, c, order, warm, thr);
 }
 
+// ---- split fold: the 32-bit fold for predictors whose worst-case sum
+// could leave int32 (loud side channels, large coefficient sums).  Each
+// int16 sample is s = 256 h + l (h = s >> 8 signed, l = s & 255), split
+// per packed word with one v_pk_ashrrev_i16 and one v_and; the same tap
+// pairs run on the h words into A and on the l words into B (|A| < 2^24,
+// |B| < 2^26: exact), and the shifted prediction of the 64-bit sum is
+//     shv >= 8:  (A + (B >> 8)) >> (shv - 8)
+//     shv <  8:  (A << (8 - shv)) + (B >> shv)
+// with the -2^shv seed in A or B, so the result is ~r exactly as the fold
+// gives it and everything after pass 1 is shared.  Linear, so the side
+// channel's (L, R) words with taps (c, -c) split the same way.
+__device__ __forceinline__ uint32_t pk_hi8(uint32_t w)
+{
+    return __builtin_bit_cast(uint32_t, __builtin_bit_cast(short2_t, w) >> (short)8);
+}
+__device__ __forceinline__ uint32_t pk_lo8(uint32_t w) { return w & 0x00FF00FFu; }
+__device__ __forceinline__ uint4 split4(const uint4 &a, bool hi)
+{
+    return hi ? make_uint4(pk_hi8(a.x), pk_hi8(a.y), pk_hi8(a.z), pk_hi8(a.w))
+              : make_uint4(pk_lo8(a.x), pk_lo8(a.y), pk_lo8(a.z), pk_lo8(a.w));
+}
+
+template <bool BIG>
+__device__ __forceinline__ int split_n(int a, int b, int sa_v, int sb_v)
+{
+    return BIG ? (a + (b >> 8)) >> sa_v : (a << sa_v) + (b >> sb_v);
+}
+
+template <int D, bool BIG>
+__device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, const int (&cp)[14],
+                                            int seed_h, int seed_l, int sa_v, int sb_v,
+                                            bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                            uint32_t &sabs, bool subr)
+{
+    int tap0 = cp[0];
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+    Win A, B;
+    {
+        const uint4 h0 = load_run4(run - 12, subr), h1 = load_run4(run - 8, subr);
+        const uint4 g[2] = {h0, h1};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const uint4 hh = split4(g[q], true), ll = split4(g[q], false);
+            A.W[8 + 4 * q] = hh.x; A.W[9 + 4 * q] = hh.y; A.W[10 + 4 * q] = hh.z; A.W[11 + 4 * q] = hh.w;
+            B.W[8 + 4 * q] = ll.x; B.W[9 + 4 * q] = ll.y; B.W[10 + 4 * q] = ll.z; B.W[11 + 4 * q] = ll.w;
+        }
+#pragma unroll
+        for (int k = 9; k < 16; ++k) {
+            A.E[k] = align16(A.W[k], A.W[k - 1]);
+            B.E[k] = align16(B.W[k], B.W[k - 1]);
+        }
+        A.E[8] = B.E[8] = 0;
+    }
+    uint4 n0 = load_run4(run, subr), n1 = load_run4(run + 4, subr);
+    uint32_t sa = 0;
+#pragma unroll
+    for (int c = 0; c < ATG_RUN / 16; ++c) {
+        asm volatile("" ::: "memory");
+        const uint4 a0 = n0, a1 = n1;
+        if (c + 1 < ATG_RUN / 16) {
+            n0 = load_run4(run + 8 * (c + 1), subr);
+            n1 = load_run4(run + 8 * (c + 1) + 4, subr);
+        }
+        win_next(split4(a0, true), split4(a1, true), A);
+        win_next(split4(a0, false), split4(a1, false), B);
+#pragma unroll
+        for (int ii = 0; ii < 16; ii += 2) {
+            int ah[2], al[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                ah[h] = dot2_first(win_pair(A, ii + h, 0), tap0, seed_h);
+                al[h] = dot2_first(win_pair(B, ii + h, 0), tap0, seed_l);
+            }
+#pragma unroll
+            for (int j = 1; j < D; ++j)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    ah[h] = dot2(win_pair(A, ii + h, j), cp[j], ah[h]);
+                    al[h] = dot2(win_pair(B, ii + h, j), cp[j], al[h]);
+                }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 16 * c + ii + h;
+                int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
+                if (i < ATG_FAST_ORDER)
+                    n = (lane0 && i < order) ? -1 : n;
+                const uint32_t s31 = (uint32_t)(n >> 31);
+                const uint32_t v = (uint32_t)n ^ s31;
+                u[i] = v;
+                add3_acc(sa, v, s31);
+            }
+        }
+    }
+    sabs = sa + (uint32_t)ATG_RUN;
+}
+
+// the side channel on (L, R) words, split: TAPS = min(2D, 13) as pass1_lr
+template <int D, bool BIG>
+__device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run, const int (&cl)[14],
+                                               int seed_h, int seed_l, int sa_v, int sb_v,
+                                               bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                               uint32_t &sabs)
+{
+    constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
+    const uint32_t *__restrict__ runR = run + PK_WORDS;
+    int tap0 = cl[0];
+    asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+    uint32_t WH[20], WL[20];
+    {
+        uint32_t h[16];
+        lr_words(*(const uint4 *)(run - 12), *(const uint4 *)(runR - 12), h);
+        lr_words(*(const uint4 *)(run - 8), *(const uint4 *)(runR - 8), h + 8);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            WH[8 + k] = pk_hi8(h[4 + k]);
+            WL[8 + k] = pk_lo8(h[4 + k]);
+        }
+    }
+    uint4 nl = *(const uint4 *)run, nr = *(const uint4 *)runR;
+    uint32_t sa = 0;
+#pragma unroll
+    for (int c = 0; c < ATG_RUN / 8; ++c) {
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int k = 0; k < 12; ++k) {
+            WH[k] = WH[8 + k];
+            WL[k] = WL[8 + k];
+        }
+        {
+            uint32_t w8[8];
+            lr_words(nl, nr, w8);
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                WH[12 + k] = pk_hi8(w8[k]);
+                WL[12 + k] = pk_lo8(w8[k]);
+            }
+        }
+        if (c + 1 < ATG_RUN / 8) {
+            nl = *(const uint4 *)(run + 4 * (c + 1));
+            nr = *(const uint4 *)(runR + 4 * (c + 1));
+        }
+#pragma unroll
+        for (int ii = 0; ii < 8; ii += 2) {
+            int ah[2], al[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                ah[h] = dot2_first(WH[12 + ii + h], tap0, seed_h);
+                al[h] = dot2_first(WL[12 + ii + h], tap0, seed_l);
+            }
+#pragma unroll
+            for (int k = 1; k < TAPS; ++k)
+#pragma unroll
+                for (int h = 0; h < 2; ++h) {
+                    ah[h] = dot2(WH[12 + ii + h - k], cl[k], ah[h]);
+                    al[h] = dot2(WL[12 + ii + h - k], cl[k], al[h]);
+                }
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int i = 8 * c + ii + h;
+                int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
+                if (i < ATG_FAST_ORDER)
+                    n = (lane0 && i < order) ? -1 : n;
+                const uint32_t s31 = (uint32_t)(n >> 31);
+                const uint32_t v = (uint32_t)n ^ s31;
+                u[i] = v;
+                add3_acc(sa, v, s31);
+            }
+        }
+    }
+    sabs = sa + (uint32_t)ATG_RUN;
+}
+
+template <bool BIG>
+__device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run, bool lr,
+                                                const int (&cq)[14], int seed_h, int seed_l,
+                                                int sa_v, int sb_v, bool lane0, int order,
+                                                uint32_t (&u)[ATG_RUN], uint32_t &sabs, bool subr)
+{
+    if (lr) {
+        switch (order / 2 + 1) {
+        case 1: pass1_lr_split<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 2: pass1_lr_split<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 3: pass1_lr_split<3, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 4: pass1_lr_split<4, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 5: pass1_lr_split<5, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 6: pass1_lr_split<6, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        default: pass1_lr_split<7, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        }
+    } else {
+        switch (order / 2 + 1) {
+        case 1: pass1_split<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        case 2: pass1_split<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        case 3: pass1_split<3, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        case 4: pass1_split<4, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        case 5: pass1_split<5, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        case 6: pass1_split<6, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        default: pass1_split<7, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, subr); break;
+        }
+    }
+}
+
+// One predictor on the split fold (caller checked split_ok); run: the
+// lane's run in the packed image, or in the L image (TWO)
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, const RunCtx &c,
+                                             const uint32_t (&cw)[7], int order, int sh, uint32_t w,
+                                             uint32_t thr, bool s16)
+{
+    const bool lr = TWO && !s16;
+    int cq[14];
+    if (lr) {
+        cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
+#pragma unroll
+        for (int k = 1; k < 14; ++k) {
+            const uint32_t d = cw[(k - 1) >> 1];
+            const int ck = ((k - 1) & 1) ? hi16(d) : lo16(d);
+            cq[k] = (int)(((uint32_t)ck & 0xFFFFu) | ((uint32_t)(-ck) << 16));
+        }
+    } else {
+        cq[0] = (int)((cw[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
+#pragma unroll
+        for (int j = 1; j < 7; ++j)
+            cq[j] = (int)((cw[j] & 0xFFFFu) | (cw[j - 1] & 0xFFFF0000u));
+#pragma unroll
+        for (int j = 7; j < 14; ++j)
+            cq[j] = 0;
+    }
+    const int shv = sh + (int)w;
+    const bool big = shv >= 8;
+    const int seed_h = big ? -(1 << (shv - 8)) : 0;
+    const int seed_l = big ? 0 : -(1 << shv);
+    int sa_v = big ? shv - 8 : 8 - shv, sb_v = shv;
+    asm volatile("v_mov_b32 %0, %0" : "+v"(sa_v)); // shift amounts in VGPRs
+    asm volatile("v_mov_b32 %0, %0" : "+v"(sb_v));
+    const bool lane0 = c.lane == 0;
+    const int warm = lane0 ? order : 0;
+    uint32_t u[ATG_RUN];
+    uint32_t lane_sum;
+    if (big)
+        pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+                              TWO);
+    else
+        pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+                               TWO);
+    return eval_tail(lane_sum, u, c, order, warm, thr);
+}
+
 // After pass 1 (every predictor form): the lower-bound pruning, the
 // partition search and the exact bit count from the kept v = |r| - [r < 0]
 __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
@@ -778,10 +1030,22 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
         if (best != 0xFFFFFFFFu)
             thr = best > hdr ? best - hdr : 0u;
     }
+    // split fold (eval_split): the partial sums stay within int32 whatever
+    // the coefficients (|h| <= 128 (255 for L - R), l <= 255); the tap pair
+    // (-2^sh, 2^sh) of the side channel needs sh <= 14; shv < 8 shifts A
+    // left, which must stay inside int32
+    const uint64_t hsum = ((uint64_t)csum + (1ull << shift)) * (TWO ? 510ull : 255ull);
+    const int shv = shift + (int)ci.w;
+    const bool split_ok = (!TWO || shift <= 14) && hsum + (1ull << shv) < (1ull << 30) &&
+                          (shv >= 8 || (hsum << (8 - shv)) < (1ull << 30));
+    const bool codes_ok = 2u * rbound + 1u < (1ull << 26);
     Eval16 ev;
-    if ((fold_ok && 2u * rbound + 1u < (1ull << 26)) || ATG_K2F_EXP == 7)
+    if ((fold_ok && codes_ok) || ATG_K2F_EXP == 7)
         ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
                             TWO && ci.amax <= 32767u);
+    else if (split_ok && codes_ok && ATG_K2F_SPLIT)
+        ev = eval_split<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
+                             TWO && ci.amax <= 32767u);
     else
         ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
     if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)

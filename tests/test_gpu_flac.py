@@ -232,3 +232,23 @@ def _port_frames(x, ch, bps, cut, opts):
                                 bps, 44100)
     r = res[0]
     return out[r.out_offset:r.out_offset + r.bytes].tobytes()
+
+
+def test_loud_side_channel_split_fold(gpu_engine):
+    """stereo whose side channel L - R runs near +-65535 (anti-phase full
+    scale, uncorrelated full-scale noise, a hard-clipped square pair): the
+    side candidate's predictors leave the 32-bit fold's bound and take the
+    split fold (flac_search16.hip eval_split) or the 64-bit loop; images
+    byte-identical to the oracle at FLAC-8 and the low presets"""
+    rng = np.random.default_rng(99)
+    n = 4096 * 3 + 17
+    t = np.arange(n)
+    a = np.round(32767 * np.sin(2 * np.pi * 997 * t / 44100)).astype(np.int64)
+    anti = np.stack([a, -a], 1).reshape(-1).clip(-32768, 32767).astype(np.int32)
+    noise = rng.integers(-32768, 32768, 2 * n).astype(np.int32)
+    sq = np.where((t // 37) % 2, 32767, -32768)
+    square = np.stack([sq, -sq], 1).reshape(-1).astype(np.int32)
+    mix = (anti // 2 + noise // 2).clip(-32768, 32767).astype(np.int32)
+    for preset in ("8", "5"):
+        check_batch(gpu_engine, [anti, noise, square, mix], 2, 16,
+                    dict(oracle_port.PRESETS[preset]))

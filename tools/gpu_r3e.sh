@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-r3e}
 mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 600 python -u -m pytest tests/test_gpu_resample.py tests/test_gpu_alac.py tests/test_gpu_replaygain.py tests/test_gpu_decode.py tests/test_gpu_seek.py tests/test_gpu_host_pipeline.py \
+timeout -k 10 600 python -u -m pytest tests/test_gpu_flac.py tests/test_gpu_resample.py tests/test_gpu_alac.py tests/test_gpu_replaygain.py tests/test_gpu_decoder_stream.py tests/test_gpu_decode.py tests/test_gpu_seek.py tests/test_gpu_host_pipeline.py \
     tests/test_gpu_ext.py tests/test_gpu_async.py tests/test_gpu_config1.py tests/test_gpu_flacaudio.py \
     -x -v --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
 timeout -k 10 120 python -u tools/queue_probe.py > $OUT/queue_probe.log 2>&1
