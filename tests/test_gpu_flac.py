@@ -247,7 +247,7 @@ def test_loud_side_channel_split_fold(gpu_engine):
     anti = np.stack([a, -a], 1).reshape(-1).clip(-32768, 32767).astype(np.int32)
     noise = rng.integers(-32768, 32768, 2 * n).astype(np.int32)
     sq = np.where((t // 37) % 2, 32767, -32768)
-    square = np.stack([sq, -sq], 1).reshape(-1).astype(np.int32)
+    square = np.stack([sq, -sq], 1).reshape(-1).clip(-32768, 32767).astype(np.int32)
     mix = (anti // 2 + noise // 2).clip(-32768, 32767).astype(np.int32)
     for preset in ("8", "5"):
         check_batch(gpu_engine, [anti, noise, square, mix], 2, 16,
