@@ -45,6 +45,7 @@
 
 #include "../../include/atgpu.h"
 #include "launch.h"
+#include "wave.h"
 
 #ifndef ATG_DEC_EXP
 #define ATG_DEC_EXP 0 // timing experiments only (exp/ builds); 0 in the product
@@ -918,11 +919,12 @@ __device__ __forceinline__ uint32_t row_of_sample(uint32_t i, uint32_t order, ui
 // the interleaved FrameList int32 and the little-endian byte stream of
 // FrameList.to_bytes (MD5 input), in one pass.  Block = the frames whose
 // first (frame, channel) job lies in 64-job slot blockIdx.x (their other
-// channels' jobs may run into the next slot).  Per tile of kEmitTile
-// samples: every job's samples are gathered from the K4 row scratch (lanes
-// across jobs: the row cells of a slot's jobs sit 16 bytes apart) or the
-// warm-up buffer into an LDS tile, then the frames are written channel-
-// interleaved, contiguous per frame.
+// channels' jobs may run into the next slot).  The block's frame and job
+// descriptors are read once into LDS.  Per tile of kEmitTile samples: lane
+// l of every wave gathers job l's samples (x = wave, wave + 4, ...) from the
+// K4 row scratch -- adjacent lanes read adjacent 16-byte cells -- or the
+// warm-up cell into an LDS tile; then each wave writes whole frames (frame
+// k on wave k mod 4), channel-interleaved and contiguous.
 constexpr uint32_t kEmitTile = 64;
 constexpr uint32_t kEmitJobs = 64 + 7;
 
@@ -938,32 +940,45 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
     __shared__ int32_t tile[kEmitJobs][kEmitTile + 1];
     __shared__ JobMeta jm[kEmitJobs];
     __shared__ uint32_t jn[kEmitJobs];
-    __shared__ uint32_t fr[64];     // the block's frames
-    __shared__ uint32_t fj[64];     // their first job, relative to the slot
-    __shared__ uint32_t fcnt[65];   // prefix of (tile samples x channels) per frame
+    // the block's frames: first job (slot-relative), samples, channels,
+    // assignment, bytes per MD5 sample, the bps clamp, output positions
+    __shared__ uint32_t fj[64], fn[64], fch[64], fas[64], fbb[64];
+    __shared__ int32_t fhi[64];
+    __shared__ uint64_t fpcm[64], fmd5[64];
     __shared__ uint32_t nfr, nj, maxn;
     const uint64_t j0 = (uint64_t)blockIdx.x * 64;
-    const uint32_t tid = threadIdx.x;
-    if (tid == 0) {
-        nfr = 0;
-        nj = 0;
-        maxn = 0;
-    }
-    __syncthreads();
+    const uint32_t tid = threadIdx.x, lane = tid & 63u, wv = tid >> 6;
     if (tid < 64) {
         const uint64_t j = j0 + tid;
         const bool start = j < njobs && jobs[j].y == 0u;
         const uint64_t bal = __ballot(start);
+        const uint32_t nf = (uint32_t)__popcll(bal);
+        uint32_t jend = 0, n = 0;
         if (start) {
             const uint32_t k = (uint32_t)__popcll(bal & ((1ull << tid) - 1ull));
-            const uint32_t f = jobs[j].x;
-            fr[k] = f;
+            const DecFrame f = frames[jobs[j].x];
+            const DecTrack t = tr[f.track];
+            const uint32_t bb = (t.bps + 7u) / 8u;
             fj[k] = tid;
-            atomicMax(&nj, tid + (uint32_t)frames[f].ch);
-            atomicMax(&maxn, frames[f].n);
+            fn[k] = f.n;
+            fch[k] = f.ch;
+            fas[k] = f.assign;
+            fbb[k] = bb;
+            // FrameList.to_bytes saturates samples outside the bps range
+            // (src/pcm.c:1826-1948): only a corrupt stream can produce them
+            fhi[k] = t.bps >= 1 && t.bps <= 31 ? (int32_t)((1u << (t.bps - 1)) - 1u) : 0x7FFFFFFF;
+            fpcm[k] = f.pcm_start;
+            fmd5[k] = t.md5_base + (f.pcm_start - t.pcm_base) * bb;
+            jend = tid + (uint32_t)f.ch;
+            n = f.n;
         }
-        if (tid == 0)
-            nfr = (uint32_t)__popcll(bal);
+        jend = wave_max_u32(jend);
+        n = wave_max_u32(n);
+        if (tid == 0) {
+            nfr = nf;
+            nj = jend;
+            maxn = n;
+        }
     }
     __syncthreads();
     const uint32_t NJ = min(nj, kEmitJobs), NF = nfr;
@@ -984,84 +999,70 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
     }
     __syncthreads();
     for (uint32_t i0 = 0; i0 < maxn; i0 += kEmitTile) {
-        if (tid == 0) {
-            uint32_t acc = 0;
-            for (uint32_t k = 0; k < NF; ++k) {
-                fcnt[k] = acc;
-                const DecFrame &f = frames[fr[k]];
-                const uint32_t left = f.n > i0 ? min(f.n - i0, kEmitTile) : 0u;
-                acc += left * f.ch;
-            }
-            fcnt[NF] = acc;
-        }
         // gather: lane = job, consecutive lanes read adjacent 16-byte cells
-        for (uint32_t e = tid; e < NJ * kEmitTile; e += 256) {
-            const uint32_t l = e % NJ, x = e / NJ;
-            const uint32_t i = i0 + x;
+        for (uint32_t l = lane; l < NJ; l += 64) {
             const JobMeta m = jm[l];
             const uint32_t n = jn[l];
-            if (i >= n)
-                continue;
             const uint64_t j = j0 + l;
-            int32_t v = 0;
-            uint32_t t = 0xFFFFFFFFu;
-            if (m.kind == 0)
-                v = m.value;
-            else if (m.kind == 1)
-                t = i;
-            else if (m.kind == 2) {
-                if (i < m.order)
-                    v = warm[j * 32u + i];
-                else
-                    t = row_of_sample(i, m.order, m.porder, n);
-            }
             // K4's [slot][row / 4][lane][4] scratch (nrows rows per slot)
-            if (t != 0xFFFFFFFFu)
-                v = rows[(j >> 6) * nrows * 64u + (uint64_t)(t >> 2) * 256u + (j & 63u) * 4u +
-                         (t & 3u)];
-            tile[l][x] = v;
+            const int32_t *__restrict__ cell = rows + (j >> 6) * nrows * 64u + (j & 63u) * 4u;
+            for (uint32_t x = wv; x < kEmitTile; x += 4) {
+                const uint32_t i = i0 + x;
+                if (i >= n)
+                    break;
+                int32_t v = 0;
+                uint32_t t = 0xFFFFFFFFu;
+                if (m.kind == 0)
+                    v = m.value;
+                else if (m.kind == 1)
+                    t = i;
+                else if (m.kind == 2) {
+                    if (i < m.order)
+                        v = warm[j * 32u + i];
+                    else
+                        t = row_of_sample(i, m.order, m.porder, n);
+                }
+                if (t != 0xFFFFFFFFu)
+                    v = cell[(uint64_t)(t >> 2) * 256u + (t & 3u)];
+                tile[l][x] = v;
+            }
         }
         __syncthreads();
-        const uint32_t total = fcnt[NF];
-        for (uint32_t e = tid; e < total; e += 256) {
-            uint32_t k = 0;
-            for (uint32_t b = 32; b; b >>= 1)
-                if (k + b < NF && fcnt[k + b] <= e)
-                    k += b;
-            const DecFrame f = frames[fr[k]];
-            const DecTrack t = tr[f.track];
-            const uint32_t ch = f.ch, rel = e - fcnt[k];
-            const uint32_t x = rel / ch, c = rel - x * ch;
-            const uint32_t l = fj[k];
-            int32_t o;
-            if (f.assign >= 8 && f.assign <= 10 && ch == 2) {
-                const int32_t a = tile[l][x], b = tile[l + 1][x];
-                if (f.assign == 8)
-                    o = c == 0 ? a : (int32_t)((uint32_t)a - (uint32_t)b);
-                else if (f.assign == 9)
-                    o = c == 0 ? (int32_t)((uint32_t)a + (uint32_t)b) : b;
-                else {
-                    const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
-                    o = c == 0 ? (int32_t)((mid + b) >> 1) : (int32_t)((mid - b) >> 1);
+        // write: wave wv takes frames wv, wv + 4, ...
+        for (uint32_t k = wv; k < NF; k += 4) {
+            const uint32_t n = fn[k];
+            const uint32_t left = n > i0 ? min(n - i0, kEmitTile) : 0u;
+            const uint32_t ch = fch[k], as = fas[k], l = fj[k], bb = fbb[k];
+            const int32_t hi = fhi[k], lo = -hi - 1;
+            const bool pair = as >= 8 && as <= 10 && ch == 2;
+            int32_t *__restrict__ dst = pcm + fpcm[k] + (uint64_t)i0 * ch;
+            uint8_t *__restrict__ bdst = bytes + fmd5[k] + (uint64_t)i0 * ch * bb;
+            const uint32_t cnt = left * ch;
+            for (uint32_t rel = lane; rel < cnt; rel += 64) {
+                const uint32_t x = ch == 2 ? rel >> 1 : rel / ch;
+                const uint32_t c = rel - x * ch;
+                int32_t o;
+                if (pair) {
+                    const int32_t a = tile[l][x], b = tile[l + 1][x];
+                    if (as == 8)
+                        o = c == 0 ? a : (int32_t)((uint32_t)a - (uint32_t)b);
+                    else if (as == 9)
+                        o = c == 0 ? (int32_t)((uint32_t)a + (uint32_t)b) : b;
+                    else {
+                        const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
+                        o = c == 0 ? (int32_t)((mid + b) >> 1) : (int32_t)((mid - b) >> 1);
+                    }
+                } else {
+                    o = tile[l + c][x];
                 }
-            } else {
-                o = tile[l + c][x];
-            }
-            const uint64_t s = (uint64_t)(i0 + x) * ch + c;
-            pcm[f.pcm_start + s] = o;
-            // FrameList.to_bytes saturates samples outside the bps range
-            // (src/pcm.c:1826-1948): only a corrupt stream can produce them
-            const uint32_t bb = (t.bps + 7) / 8;
-            const int32_t hi = t.bps >= 1 && t.bps <= 31 ? (int32_t)((1u << (t.bps - 1)) - 1u)
-                                                          : 0x7FFFFFFF;
-            const int32_t lo = -hi - 1;
-            const int32_t v = o > hi ? hi : (o < lo ? lo : o);
-            uint8_t *bdst = bytes + t.md5_base + (f.pcm_start - t.pcm_base + s) * bb;
-            if (bb == 2) {
-                *(int16_t *)bdst = (int16_t)v;
-            } else {
-                for (uint32_t q = 0; q < bb; ++q)
-                    bdst[q] = (uint8_t)((uint32_t)v >> (8 * q));
+                dst[rel] = o;
+                const int32_t v = o > hi ? hi : (o < lo ? lo : o);
+                if (bb == 2) {
+                    *(int16_t *)(bdst + 2u * rel) = (int16_t)v;
+                } else {
+                    for (uint32_t q = 0; q < bb; ++q)
+                        bdst[(uint64_t)rel * bb + q] = (uint8_t)((uint32_t)v >> (8 * q));
+                }
             }
         }
         __syncthreads();

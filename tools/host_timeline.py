@@ -19,6 +19,8 @@ def main():
     from audiotools import _atgpu
     steps = int(sys.argv[1]) if len(sys.argv) > 1 else 3
     pinned = (sys.argv[2] if len(sys.argv) > 2 else "pinned") == "pinned"
+    chunk_mb = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+    inflight = int(sys.argv[4]) if len(sys.argv) > 4 else 2
     dev = torch.device("cuda", 0)
     n_samples = 64 * 4096
     pcm = bench.synth_batch(torch, list(range(1024)), n_samples, dev).cpu().numpy()
@@ -31,6 +33,7 @@ def main():
         p[:] = pcm
         pcm = p
     out = _atgpu.pinned_empty(nb, np.uint8) if pinned else None
+    eng.set_host_chunk_bytes(chunk_mb << 20)
     eng.encode(opts, pcm, tracks, 2, 16, 44100, out=out)
     for _ in range(steps):
         t0 = time.perf_counter()
@@ -38,18 +41,22 @@ def main():
         dt = time.perf_counter() - t0
         print("batch %.2f ms  %.3f M frames/s (%s, sync)"
               % (dt * 1e3, 65536 / dt / 1e6, "pinned" if pinned else "pageable"), flush=True)
-    # batches queued back to back (atg_flac_encode_host_async), two in flight
-    outs = [out, _atgpu.pinned_empty(nb, np.uint8) if pinned else None]
+    # batches queued back to back (atg_flac_encode_host_async), `inflight`
+    # jobs in flight
+    outs = [out] + [_atgpu.pinned_empty(nb, np.uint8) if pinned else None
+                    for _ in range(inflight - 1)]
     t0 = time.perf_counter()
     pend = []
     for k in range(steps):
-        pend.append(eng.encode_async(opts, pcm, tracks, 2, 16, 44100, out=outs[k % 2]))
-        if len(pend) > 1:
+        pend.append(eng.encode_async(opts, pcm, tracks, 2, 16, 44100, out=outs[k % inflight]))
+        if len(pend) >= inflight:
             pend.pop(0).wait()
-    pend.pop(0).wait()
+    while pend:
+        pend.pop(0).wait()
     dt = (time.perf_counter() - t0) / steps
-    print("batch %.2f ms  %.3f M frames/s (%s, queued)"
-          % (dt * 1e3, 65536 / dt / 1e6, "pinned" if pinned else "pageable"), flush=True)
+    print("batch %.2f ms  %.3f M frames/s (%s, queued, chunk %d MB, %d in flight, HW queues %s)"
+          % (dt * 1e3, 65536 / dt / 1e6, "pinned" if pinned else "pageable", chunk_mb, inflight,
+             os.environ.get("GPU_MAX_HW_QUEUES", "default")), flush=True)
 
 
 if __name__ == "__main__":
