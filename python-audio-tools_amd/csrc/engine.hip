@@ -157,10 +157,15 @@ struct EncSlot {
     float times[kNumTimed] = {};
 };
 
-// development switch (tools/build_exp.sh): the slots' aux streams at high
-// stream priority
+// the slots' aux streams (MD5 chains, stream headers, result copies) at
+// high stream priority.  With GPU_MAX_HW_QUEUES = 4 (HIP's default) the
+// engine's six streams otherwise share hardware queues, and a host job's
+// chunks queue their MD5 chains behind one another on a shared queue: the
+// host-to-host leg runs 1.09 M frames/s at normal priority, 1.83 M at high
+// (profiles/r03_d_*); the device-resident step is the same either way.
+// 0 only for experiments (tools/build_exp.sh)
 #ifndef ATG_AUX_HIPRIO
-#define ATG_AUX_HIPRIO 0
+#define ATG_AUX_HIPRIO 1
 #endif
 
 // batches in flight on an engine (each its own device workspace): the MD5

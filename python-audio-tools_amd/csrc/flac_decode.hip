@@ -999,32 +999,56 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
     }
     __syncthreads();
     for (uint32_t i0 = 0; i0 < maxn; i0 += kEmitTile) {
-        // gather: lane = job, consecutive lanes read adjacent 16-byte cells
+        // gather: lane = job, consecutive lanes read adjacent 16-byte cells;
+        // wave wv takes the tile's samples [16 wv, 16 wv + 16), its row
+        // found once and then stepped (one more at each partition header)
         for (uint32_t l = lane; l < NJ; l += 64) {
             const JobMeta m = jm[l];
             const uint32_t n = jn[l];
             const uint64_t j = j0 + l;
             // K4's [slot][row / 4][lane][4] scratch (nrows rows per slot)
             const int32_t *__restrict__ cell = rows + (j >> 6) * nrows * 64u + (j & 63u) * 4u;
-            for (uint32_t x = wv; x < kEmitTile; x += 4) {
+            const uint32_t xa = 16u * wv, ia = i0 + xa;
+            const uint32_t plen = n >> m.porder;
+            const bool step = m.kind == 2 && plen > m.order;
+            uint32_t t = 0, rem = 0; // row of the next residual, residuals left in its partition
+            if (m.kind == 1)
+                t = ia;
+            else if (step) {
+                const uint32_t i = max(ia, (uint32_t)m.order);
+                const uint32_t rr = i - m.order, p0 = plen - m.order;
+                t = row_of_sample(i, m.order, m.porder, n);
+                rem = rr < p0 ? p0 - rr : plen - (rr - p0) % plen;
+            }
+#pragma unroll 4
+            for (uint32_t x = xa; x < xa + 16u; ++x) {
                 const uint32_t i = i0 + x;
                 if (i >= n)
                     break;
                 int32_t v = 0;
-                uint32_t t = 0xFFFFFFFFu;
+                bool rd = false;
                 if (m.kind == 0)
                     v = m.value;
                 else if (m.kind == 1)
-                    t = i;
+                    rd = true;
                 else if (m.kind == 2) {
                     if (i < m.order)
                         v = warm[j * 32u + i];
+                    else if (!step)
+                        t = row_of_sample(i, m.order, m.porder, n), rd = true;
                     else
-                        t = row_of_sample(i, m.order, m.porder, n);
+                        rd = true;
                 }
-                if (t != 0xFFFFFFFFu)
-                    v = cell[(uint64_t)(t >> 2) * 256u + (t & 3u)];
+                if (rd)
+                    v = cell[(t >> 2) * 256u + (t & 3u)];
                 tile[l][x] = v;
+                if (m.kind == 1 || (step && i >= m.order)) {
+                    ++t;
+                    if (step && --rem == 0) {
+                        ++t; // the next partition's header row
+                        rem = plen;
+                    }
+                }
             }
         }
         __syncthreads();

@@ -65,7 +65,7 @@ struct RsTrack {
     uint32_t period;     // k_rs_phase: outputs per phase cycle (out_rate / gcd)
     uint32_t lspan;      // k_rs_phase: outputs between a wave's lanes (a multiple of period)
     uint32_t wext;       // k_rs_phase: window frames staged past the task's last centre's taps
-    uint32_t pad;
+    uint32_t cls;        // k_rs_phase: ratio class (its phase tables)
 };
 
 struct RsParams {
@@ -256,11 +256,154 @@ __device__ __forceinline__ double interp_coeff(const float *__restrict__ C, int3
     return __builtin_fma(fraction, (double)(c1 - c0), (double)c0);
 }
 
+// output m's coefficient of one tap from the [tap][M] table: the M doubles
+// of a tap are contiguous, so one ds_read_b128 (a wave-uniform address: an
+// LDS broadcast) returns two outputs' coefficients
+template <int M>
+__device__ __forceinline__ void load_coefs(const double *__restrict__ p, double (&ic)[M])
+{
+    if constexpr (M % 2 == 0) {
+#pragma unroll
+        for (int m = 0; m < M; m += 2) {
+            const double2 v = *(const double2 *)(p + m);
+            ic[m] = v.x;
+            ic[m + 1] = v.y;
+        }
+    } else {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+            ic[m] = p[m];
+    }
+}
+
 __device__ __forceinline__ void wave_lds_sync()
 {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
+// Tap windows of a phase group (M outputs of one lane row, the phases and
+// centres lane 0 computed), relative to c_0: output m's left half is
+// [dL_m, dc_m] ascending, its right half [dc_m + 1, top_m] descending, as
+// calc_output_* walks them; the union windows are [sl0, sl1] and [sr0, sr1].
+template <int M>
+struct PhaseGeom {
+    int32_t dL[M], fiL[M], nL[M], top[M], fiR[M], nR[M];
+    int32_t sl0, sl1, sr0, sr1;
+};
+
+template <int M>
+__device__ __forceinline__ void phase_geom(const int32_t (&sfi0)[M], const int32_t (&dc)[M],
+                                           const bool (&valid)[M], int32_t inc, PhaseGeom<M> &q)
+{
+    const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
+    q.sl0 = 1 << 30;
+    q.sl1 = -(1 << 30);
+    q.sr0 = 1 << 30;
+    q.sr1 = -(1 << 30);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        const int32_t ccL = (max_fi - sfi0[m]) / inc;
+        q.fiL[m] = sfi0[m] + ccL * inc;
+        q.nL[m] = valid[m] ? q.fiL[m] / inc + 1 : 0;
+        q.dL[m] = dc[m] - ccL;
+        const int32_t frR = inc - sfi0[m];
+        const int32_t ccR = (max_fi - frR) / inc;
+        q.fiR[m] = frR + ccR * inc;
+        q.nR[m] = valid[m] ? (q.fiR[m] - 1) / inc + 1 : 0;
+        q.top[m] = dc[m] + 1 + ccR;
+        if (valid[m]) {
+            q.sl0 = min(q.sl0, q.dL[m]);
+            q.sl1 = max(q.sl1, dc[m]);
+            q.sr0 = min(q.sr0, dc[m] + 1);
+            q.sr1 = max(q.sr1, q.top[m]);
+        }
+    }
+}
+
+// the group's zero-padded coefficient tables, [tap][M] (cL: left half over
+// s = sl0 .. sl1, cR: right half over s = sr1 .. sr0), lanes over taps
+template <int M>
+__device__ __forceinline__ void phase_fill(const float *__restrict__ Cg, const PhaseGeom<M> &q,
+                                           int32_t inc, uint32_t lane, double *__restrict__ cL,
+                                           double *__restrict__ cR)
+{
+    const int32_t WL = q.sl1 - q.sl0 + 1, WR = q.sr1 - q.sr0 + 1;
+    for (int32_t k = (int32_t)lane; k < WL; k += 64) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t j = k + q.sl0 - q.dL[m];
+            cL[k * M + m] = (j >= 0 && j < q.nL[m]) ? interp_coeff(Cg, q.fiL[m] - j * inc) : 0.0;
+        }
+    }
+    for (int32_t k = (int32_t)lane; k < WR; k += 64) {
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            const int32_t j = q.top[m] - q.sr1 + k;
+            cR[k * M + m] = (j >= 0 && j < q.nR[m]) ? interp_coeff(Cg, q.fiR[m] - j * inc) : 0.0;
+        }
+    }
+}
+
+// Phase tables of a ratio class, computed once per launch: group g of the
+// first lane row (outputs M g .. M g + M - 1 of the class's first track)
+// -> header (sl0, WL, sr1, WR, the M phases and relative centres it was
+// built for) + left and right [tap][M] tables.  A filter item whose lane 0
+// finds the same phases and centres (exact periodicity of the positions)
+// copies them instead of evaluating c0 + fraction (c1 - c0) per tap.
+constexpr uint32_t kTabHdr = 8; // header doubles (16 int32)
+
+template <int M>
+__global__ __launch_bounds__(64) void k_rs_phase_tab(const RsTrack *__restrict__ tr,
+                                                     const uint32_t *__restrict__ class_track,
+                                                     const int2 *__restrict__ pos,
+                                                     const uint32_t *__restrict__ table_bits,
+                                                     double *__restrict__ tabs, uint32_t G,
+                                                     uint32_t wmax, uint64_t stride)
+{
+    const uint32_t g = blockIdx.x, cls = blockIdx.y, lane = threadIdx.x;
+    const RsTrack T = tr[class_track[cls]];
+    const uint32_t L = T.lspan;
+    double *tb = tabs + ((uint64_t)cls * G + g) * stride;
+    int32_t *th = reinterpret_cast<int32_t *>(tb);
+    if (M * g >= L) {
+        if (lane < 2 * kTabHdr)
+            th[lane] = 0; // WL = 0: never taken
+        return;
+    }
+    int64_t c[M];
+    int32_t sfi[M], sfi0[M], dc[M];
+    bool valid[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        valid[m] = M * g + m < L && (uint64_t)(M * g + m) < T.out_frames;
+        position(T, pos, valid[m] ? M * g + m : M * g, c[m], sfi[m]);
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+        sfi0[m] = sfi[m];
+        dc[m] = (int32_t)(c[m] - c[0]);
+    }
+    PhaseGeom<M> q;
+    phase_geom<M>(sfi0, dc, valid, T.increment, q);
+    bool all = true;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+        all = all && valid[m];
+    if (lane == 0) {
+        th[0] = q.sl0;
+        th[1] = all ? q.sl1 - q.sl0 + 1 : 0; // partial groups: never taken from the table
+        th[2] = q.sr1;
+        th[3] = all ? q.sr1 - q.sr0 + 1 : 0;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+            th[4 + m] = sfi0[m];
+            th[4 + M + m] = dc[m];
+        }
+    }
+    phase_fill<M>(reinterpret_cast<const float *>(table_bits), q, T.increment, lane, tb + kTabHdr,
+                  tb + kTabHdr + (uint64_t)M * wmax);
 }
 
 // The phase-sharing filter.  The output positions of a rational ratio
@@ -292,11 +435,13 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
                                                   uint32_t n_tasks, const int2 *__restrict__ pos,
                                                   const uint32_t *__restrict__ table_bits,
                                                   const int32_t *__restrict__ in,
-                                                  int32_t *__restrict__ out, uint32_t wmax)
+                                                  int32_t *__restrict__ out, uint32_t wmax,
+                                                  const double *__restrict__ tabs, uint32_t tab_G,
+                                                  uint64_t tab_stride)
 {
     extern __shared__ double lds_d[];
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
-    double *cL = lds_d + (size_t)wave * 2 * M * wmax; // [M][wmax] left, then right
+    double *cL = lds_d + (size_t)wave * 2 * M * wmax; // [wmax][M] left, then right
     double *cR = cL + (size_t)M * wmax;
     float *X = reinterpret_cast<float *>(lds_d + (size_t)nwaves * 2 * M * wmax);
     const float *Cg = reinterpret_cast<const float *>(table_bits);
@@ -317,12 +462,25 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
         // end still reads their taps' samples (times zero coefficients for
         // its live outputs), so they must be finite -- staged, not stale LDS
         const uint32_t wn = (uint32_t)(c_last + reach + 1 - w0) + T.wext;
-        for (uint32_t i = threadIdx.x; i < wn * CH; i += blockDim.x) {
-            const int64_t f = w0 + (int64_t)(i / CH);
-            float v = 0.0f;
-            if (f >= 0 && (uint64_t)f < T.in_frames)
-                v = (float)in[T.in_base + (uint64_t)f * CH + (i % CH)] * P.inv_q;
-            X[i] = v;
+        // kStage loads in flight per thread before their conversions
+        constexpr uint32_t kStage = 8;
+        const uint32_t nx = wn * CH;
+        for (uint32_t i0 = threadIdx.x; i0 < nx; i0 += kStage * blockDim.x) {
+            int32_t v[kStage];
+#pragma unroll
+            for (uint32_t b = 0; b < kStage; ++b) {
+                const uint32_t i = i0 + b * blockDim.x;
+                const int64_t f = w0 + (int64_t)(i / CH);
+                v[b] = 0;
+                if (i < nx && f >= 0 && (uint64_t)f < T.in_frames)
+                    v[b] = in[T.in_base + (uint64_t)f * CH + (i % CH)];
+            }
+#pragma unroll
+            for (uint32_t b = 0; b < kStage; ++b) {
+                const uint32_t i = i0 + b * blockDim.x;
+                if (i < nx)
+                    X[i] = (float)v[b] * P.inv_q;
+            }
         }
         __syncthreads();
         const uint32_t L = T.lspan;
@@ -364,44 +522,44 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
                 for (int k = 0; k < CH; ++k)
                     left[m][k] = right[m][k] = 0.0;
             if (__all(uni)) {
-                // tap windows relative to c_0: left [dL_m, dc_m], right
-                // [dc_m + 1, top_m] (descending), as calc_output_* walks them
-                int32_t dL[M], fiL[M], nL[M], top[M], fiR[M], nR[M];
-                int32_t sl0 = 1 << 30, sl1 = -(1 << 30), sr0 = 1 << 30, sr1 = -(1 << 30);
+                // the class's table for this group when lane 0's phases and
+                // centres are the ones it was built for, else evaluated here
+                const double *__restrict__ tb = tabs + ((uint64_t)T.cls * tab_G + g) * tab_stride;
+                const int32_t *__restrict__ th = reinterpret_cast<const int32_t *>(tb);
+                bool hit = th[1] != 0;
 #pragma unroll
-                for (int m = 0; m < M; ++m) {
-                    const int32_t ccL = (max_fi - sfi0[m]) / inc;
-                    fiL[m] = sfi0[m] + ccL * inc;
-                    nL[m] = valid[m] ? fiL[m] / inc + 1 : 0;
-                    dL[m] = dc[m] - ccL;
-                    const int32_t frR = inc - sfi0[m];
-                    const int32_t ccR = (max_fi - frR) / inc;
-                    fiR[m] = frR + ccR * inc;
-                    nR[m] = valid[m] ? (fiR[m] - 1) / inc + 1 : 0;
-                    top[m] = dc[m] + 1 + ccR;
-                    if (valid[m]) {
-                        sl0 = min(sl0, dL[m]);
-                        sl1 = max(sl1, dc[m]);
-                        sr0 = min(sr0, dc[m] + 1);
-                        sr1 = max(sr1, top[m]);
+                for (int m = 0; m < M; ++m)
+                    hit = hit && valid[m] && th[4 + m] == sfi0[m] && th[4 + M + m] == dc[m];
+                int32_t sl0, sr1, WL, WR;
+                if (hit) {
+                    sl0 = th[0];
+                    WL = th[1];
+                    sr1 = th[2];
+                    WR = th[3];
+                    const double2 *__restrict__ gl = reinterpret_cast<const double2 *>(tb + kTabHdr);
+                    const double2 *__restrict__ gr =
+                        reinterpret_cast<const double2 *>(tb + kTabHdr + (uint64_t)M * wmax);
+                    double2 *dl = reinterpret_cast<double2 *>(cL), *dr = reinterpret_cast<double2 *>(cR);
+                    const int32_t nl = WL * M / 2, nr = WR * M / 2;
+                    for (int32_t k = (int32_t)lane; k < max(nl, nr); k += 64) {
+                        double2 a, b;
+                        if (k < nl)
+                            a = gl[k];
+                        if (k < nr)
+                            b = gr[k];
+                        if (k < nl)
+                            dl[k] = a;
+                        if (k < nr)
+                            dr[k] = b;
                     }
-                }
-                const int32_t WL = sl1 - sl0 + 1, WR = sr1 - sr0 + 1;
-                for (int32_t k = (int32_t)lane; k < WL; k += 64) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) {
-                        const int32_t j = k + sl0 - dL[m];
-                        cL[m * wmax + k] = (j >= 0 && j < nL[m]) ? interp_coeff(Cg, fiL[m] - j * inc)
-                                                                 : 0.0;
-                    }
-                }
-                for (int32_t k = (int32_t)lane; k < WR; k += 64) {
-#pragma unroll
-                    for (int m = 0; m < M; ++m) {
-                        const int32_t j = top[m] - sr1 + k;
-                        cR[m * wmax + k] = (j >= 0 && j < nR[m]) ? interp_coeff(Cg, fiR[m] - j * inc)
-                                                                 : 0.0;
-                    }
+                } else {
+                    PhaseGeom<M> q;
+                    phase_geom<M>(sfi0, dc, valid, inc, q);
+                    phase_fill<M>(Cg, q, inc, lane, cL, cR);
+                    sl0 = q.sl0;
+                    sr1 = q.sr1;
+                    WL = q.sl1 - q.sl0 + 1;
+                    WR = q.sr1 - q.sr0 + 1;
                 }
                 wave_lds_sync();
                 const float *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
@@ -411,12 +569,13 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
                         x[q] = (double)xl[k * CH + q];
+                    double ic[M];
+                    load_coefs<M>(cL + k * M, ic);
 #pragma unroll
                     for (int m = 0; m < M; ++m) {
-                        const double ic = cL[m * wmax + k];
 #pragma unroll
                         for (int q = 0; q < CH; ++q)
-                            left[m][q] = left[m][q] + ic * x[q];
+                            left[m][q] = left[m][q] + ic[m] * x[q];
                     }
                 }
                 const float *xr = X + (int64_t)(c[0] + sr1 - w0) * CH;
@@ -426,12 +585,13 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
                         x[q] = (double)xr[-k * CH + q];
+                    double ic[M];
+                    load_coefs<M>(cR + k * M, ic);
 #pragma unroll
                     for (int m = 0; m < M; ++m) {
-                        const double ic = cR[m * wmax + k];
 #pragma unroll
                         for (int q = 0; q < CH; ++q)
-                            right[m][q] = right[m][q] + ic * x[q];
+                            right[m][q] = right[m][q] + ic[m] * x[q];
                     }
                 }
                 wave_lds_sync(); // the tables are rewritten by the next item
@@ -766,12 +926,23 @@ void launch_filter(const FilterArgs &A, bool hoist, bool xd, unsigned grid, unsi
 
 constexpr unsigned kPhaseThreads = 512;
 
+struct PhaseTabs {
+    const uint32_t *class_track; // a track of each ratio class
+    uint32_t n_classes, G;       // classes, phase groups per class
+    double *tabs;
+    uint64_t stride;             // doubles per group table
+};
+
 template <int CH>
 void launch_phase(const FilterArgs &A, const uint2 *tasks, uint32_t n_tasks, uint32_t wmax,
-                  unsigned grid, size_t lds, hipStream_t s)
+                  unsigned grid, size_t lds, const PhaseTabs &pt, hipStream_t s)
 {
-    hipLaunchKernelGGL((k_rs_phase<CH, phase_m<CH>()>), dim3(grid), dim3(kPhaseThreads), lds, s,
-                       A.P, A.tr, tasks, n_tasks, A.pos, A.table, A.in, A.out, wmax);
+    constexpr int M = phase_m<CH>();
+    hipLaunchKernelGGL((k_rs_phase_tab<M>), dim3(pt.G, pt.n_classes), dim3(64), 0, s, A.tr,
+                       pt.class_track, A.pos, A.table, pt.tabs, pt.G, wmax, pt.stride);
+    hipLaunchKernelGGL((k_rs_phase<CH, M>), dim3(grid), dim3(kPhaseThreads), lds, s, A.P, A.tr,
+                       tasks, n_tasks, A.pos, A.table, A.in, A.out, wmax,
+                       (const double *)pt.tabs, pt.G, pt.stride);
 }
 
 template <int CH>
@@ -792,8 +963,9 @@ hipError_t set_lds_attr()
 
 struct RsCtx {
     void *tracks = nullptr, *chunk_track = nullptr, *pos = nullptr, *table = nullptr,
-         *ids = nullptr, *ptasks = nullptr;
-    size_t cap_tracks = 0, cap_chunks = 0, cap_pos = 0, cap_ids = 0, cap_ptasks = 0;
+         *ids = nullptr, *ptasks = nullptr, *ctrack = nullptr, *tabs = nullptr;
+    size_t cap_tracks = 0, cap_chunks = 0, cap_pos = 0, cap_ids = 0, cap_ptasks = 0,
+           cap_ctrack = 0, cap_tabs = 0;
     bool table_up = false;
     hipEvent_t ev[3] = {nullptr, nullptr, nullptr};
     float ms[2] = {0.0f, 0.0f};
@@ -945,6 +1117,10 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         return rsfail(ATG_ERR_UNSUPPORTED, "resampling ratio too low for the LDS window");
     std::vector<uint2> ptasks;
     size_t lds_phase = 0;
+    // ratio classes of the phase tracks (one table set each)
+    std::vector<uint32_t> class_track;
+    std::vector<std::pair<uint64_t, uint32_t>> class_key; // (in_rate << 32 | out_rate, class)
+    uint32_t tab_G = 0;
     uint64_t out = 0, posn = 0;
     for (uint32_t t = 0; t < n; ++t) {
         const atg_rs_track &a = tracks[t];
@@ -964,7 +1140,7 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         T.period = per[t];
         T.lspan = lspan[t];
         T.wext = (pm - 1) * (uint32_t)((a.in_rate + a.out_rate - 1) / a.out_rate) + 2;
-        T.pad = 0;
+        T.cls = 0;
         if (v.mode == POS_TABLE) {
             T.pos_base = posn;
             posn += T.out_frames;
@@ -972,6 +1148,17 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         }
         T.chunk_base = chunk_track.size();
         if (phase[t]) {
+            const uint64_t key = ((uint64_t)a.in_rate << 32) | a.out_rate;
+            uint32_t cls = (uint32_t)class_track.size();
+            for (const auto &kc : class_key)
+                if (kc.first == key)
+                    cls = kc.second;
+            if (cls == class_track.size()) {
+                class_key.emplace_back(key, cls);
+                class_track.push_back(t);
+                tab_G = std::max<uint32_t>(tab_G, (lspan[t] + pm - 1) / pm);
+            }
+            T.cls = cls;
             T.span = 64ull * lspan[t] * rows[t];
             for (uint64_t k = 0; k * T.span < T.out_frames; ++k)
                 ptasks.push_back(make_uint2(t, (uint32_t)k));
@@ -1011,6 +1198,13 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
     RSHIP(grow(X.pos, X.cap_pos, sizeof(int2) * std::max<uint64_t>(posn, 1)));
     RSHIP(grow(X.ids, X.cap_ids, sizeof(uint32_t) * std::max<size_t>(serial.size(), 1)));
     RSHIP(grow(X.ptasks, X.cap_ptasks, sizeof(uint2) * std::max<size_t>(ptasks.size(), 1)));
+    const uint64_t tab_stride = kTabHdr + 2ull * pm * wmax;
+    RSHIP(grow(X.ctrack, X.cap_ctrack, sizeof(uint32_t) * std::max<size_t>(class_track.size(), 1)));
+    RSHIP(grow(X.tabs, X.cap_tabs,
+               sizeof(double) * std::max<uint64_t>(tab_stride * tab_G * class_track.size(), 1)));
+    if (!class_track.empty())
+        RSHIP(hipMemcpyAsync(X.ctrack, class_track.data(), sizeof(uint32_t) * class_track.size(),
+                             hipMemcpyHostToDevice, s));
     if (!ptasks.empty())
         RSHIP(hipMemcpyAsync(X.ptasks, ptasks.data(), sizeof(uint2) * ptasks.size(),
                              hipMemcpyHostToDevice, s));
@@ -1062,15 +1256,17 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
         const unsigned grid = (unsigned)std::min<size_t>(ptasks.size(), 256u * per_cu);
         const uint2 *tk = (const uint2 *)X.ptasks;
         const uint32_t nt = (uint32_t)ptasks.size();
+        const PhaseTabs pt{(const uint32_t *)X.ctrack, (uint32_t)class_track.size(), tab_G,
+                           (double *)X.tabs, tab_stride};
         switch (channels) {
-        case 1: launch_phase<1>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 2: launch_phase<2>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 3: launch_phase<3>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 4: launch_phase<4>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 5: launch_phase<5>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 6: launch_phase<6>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        case 7: launch_phase<7>(A, tk, nt, wmax, grid, lds_phase, s); break;
-        default: launch_phase<8>(A, tk, nt, wmax, grid, lds_phase, s); break;
+        case 1: launch_phase<1>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 2: launch_phase<2>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 3: launch_phase<3>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 4: launch_phase<4>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 5: launch_phase<5>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 6: launch_phase<6>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        case 7: launch_phase<7>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
+        default: launch_phase<8>(A, tk, nt, wmax, grid, lds_phase, pt, s); break;
         }
         RSHIP(hipGetLastError());
     }

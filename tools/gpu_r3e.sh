@@ -1,7 +1,7 @@
 #!/bin/bash
 # Round-3 GPU recipe: fused decoder emit kernel, async host jobs: their GPU
 # tests, the stream/queue probe, host-pipeline timelines (product library
-# and the high-priority aux stream build), then the default bench.
+# and the normal-priority aux stream build), then the default bench.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$R/gpurun_out/${1:-r3e}
@@ -14,8 +14,8 @@ timeout -k 10 120 python -u tools/queue_probe.py > $OUT/queue_probe.log 2>&1
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats -d "$OUT/prof" -o run \
     --output-format csv -- python3 "$R/tools/host_timeline.py" 3 pinned > "$OUT/prof.log" 2>&1
-ATGPU_LIB=$R/exp/libatgpu_hiprio.so timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
-    -d "$OUT/prof_hiprio" -o run --output-format csv -- python3 "$R/tools/host_timeline.py" 3 pinned \
-    > "$OUT/prof_hiprio.log" 2>&1
+ATGPU_LIB=$R/exp/libatgpu_loprio.so timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace --stats \
+    -d "$OUT/prof_loprio" -o run --output-format csv -- python3 "$R/tools/host_timeline.py" 3 pinned \
+    > "$OUT/prof_loprio.log" 2>&1
 cd "$R"
 timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
