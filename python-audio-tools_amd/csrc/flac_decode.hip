@@ -1052,40 +1052,53 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
             }
         }
         __syncthreads();
-        // write: wave wv takes frames wv, wv + 4, ...
+        // write: wave wv takes frames wv, wv + 4, ...; lane = sample of the
+        // tile, all its channels (stereo: one 8-byte PCM store and one
+        // 4-byte MD5 store per lane, 512 + 256 contiguous bytes per wave)
         for (uint32_t k = wv; k < NF; k += 4) {
             const uint32_t n = fn[k];
             const uint32_t left = n > i0 ? min(n - i0, kEmitTile) : 0u;
-            const uint32_t ch = fch[k], as = fas[k], l = fj[k], bb = fbb[k];
+            if (lane >= left)
+                continue;
+            const uint32_t ch = fch[k], as = fas[k], l = fj[k], bb = fbb[k], x = lane;
             const int32_t hi = fhi[k], lo = -hi - 1;
-            const bool pair = as >= 8 && as <= 10 && ch == 2;
-            int32_t *__restrict__ dst = pcm + fpcm[k] + (uint64_t)i0 * ch;
-            uint8_t *__restrict__ bdst = bytes + fmd5[k] + (uint64_t)i0 * ch * bb;
-            const uint32_t cnt = left * ch;
-            for (uint32_t rel = lane; rel < cnt; rel += 64) {
-                const uint32_t x = ch == 2 ? rel >> 1 : rel / ch;
-                const uint32_t c = rel - x * ch;
-                int32_t o;
-                if (pair) {
-                    const int32_t a = tile[l][x], b = tile[l + 1][x];
-                    if (as == 8)
-                        o = c == 0 ? a : (int32_t)((uint32_t)a - (uint32_t)b);
-                    else if (as == 9)
-                        o = c == 0 ? (int32_t)((uint32_t)a + (uint32_t)b) : b;
-                    else {
-                        const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
-                        o = c == 0 ? (int32_t)((mid + b) >> 1) : (int32_t)((mid - b) >> 1);
-                    }
-                } else {
-                    o = tile[l + c][x];
+            int32_t *__restrict__ dst = pcm + fpcm[k] + (uint64_t)(i0 + x) * ch;
+            uint8_t *__restrict__ bdst = bytes + fmd5[k] + (uint64_t)(i0 + x) * ch * bb;
+            if (ch == 2) {
+                const int32_t a = tile[l][x], b = tile[l + 1][x];
+                int32_t o0 = a, o1 = b;
+                if (as == 8) {
+                    o1 = (int32_t)((uint32_t)a - (uint32_t)b);
+                } else if (as == 9) {
+                    o0 = (int32_t)((uint32_t)a + (uint32_t)b);
+                } else if (as == 10) {
+                    const int64_t mid = (int64_t)((uint64_t)(int64_t)a << 1) | (b & 1);
+                    o0 = (int32_t)((mid + b) >> 1);
+                    o1 = (int32_t)((mid - b) >> 1);
                 }
-                dst[rel] = o;
-                const int32_t v = o > hi ? hi : (o < lo ? lo : o);
+                *(int2 *)dst = make_int2(o0, o1);
+                // FrameList.to_bytes saturates samples outside the bps range
+                // (src/pcm.c:1826-1948): only a corrupt stream can produce them
+                const int32_t v0 = o0 > hi ? hi : (o0 < lo ? lo : o0);
+                const int32_t v1 = o1 > hi ? hi : (o1 < lo ? lo : o1);
                 if (bb == 2) {
-                    *(int16_t *)(bdst + 2u * rel) = (int16_t)v;
+                    *(uint32_t *)bdst = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
                 } else {
-                    for (uint32_t q = 0; q < bb; ++q)
-                        bdst[(uint64_t)rel * bb + q] = (uint8_t)((uint32_t)v >> (8 * q));
+                    for (uint32_t q = 0; q < bb; ++q) {
+                        bdst[q] = (uint8_t)((uint32_t)v0 >> (8 * q));
+                        bdst[bb + q] = (uint8_t)((uint32_t)v1 >> (8 * q));
+                    }
+                }
+            } else {
+                for (uint32_t c = 0; c < ch; ++c) {
+                    const int32_t o = tile[l + c][x];
+                    dst[c] = o;
+                    const int32_t v = o > hi ? hi : (o < lo ? lo : o);
+                    if (bb == 2)
+                        *(int16_t *)(bdst + 2u * c) = (int16_t)v;
+                    else
+                        for (uint32_t q = 0; q < bb; ++q)
+                            bdst[c * bb + q] = (uint8_t)((uint32_t)v >> (8 * q));
                 }
             }
         }

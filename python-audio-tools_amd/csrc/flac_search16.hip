@@ -262,7 +262,9 @@ __device__ __forceinline__ void lr_words(const uint4 &l, const uint4 &r, uint32_
     }
 }
 
-template <int D>
+// DBL (shift 15): the fold tap 2^15 does not fit int16, so tap 0 is
+// (-2^14, 2^14) and is applied twice
+template <int D, bool DBL = false>
 __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const int (&cl)[14],
                                          int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
                                          uint32_t &sabs)
@@ -299,8 +301,11 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
         for (int ii = 0; ii < 8; ii += 2) {
             int accs[2];
 #pragma unroll
-            for (int h = 0; h < 2; ++h)
+            for (int h = 0; h < 2; ++h) {
                 accs[h] = dot2_first(W[12 + ii + h], tap0, c0acc);
+                if constexpr (DBL)
+                    accs[h] = dot2(W[12 + ii + h], tap0, accs[h]);
+            }
 #pragma unroll
             for (int k = 1; k < TAPS; ++k)
 #pragma unroll
@@ -365,10 +370,12 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     // s16 (side channel, every |S| <= 32767): the packed path on L - R
     // words formed on the fly -- 2 taps per v_dot2 instead of 1
     const bool lr = TWO && !s16;
+    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
     int cq[14];
     if (lr) {
         // (L, R) taps: (-2^sh, 2^sh), then (c_k, -c_k)
-        cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
+        const int t0 = dbl ? 1 << 14 : 1 << sh;
+        cq[0] = (int)(((uint32_t)(-t0) & 0xFFFFu) | ((uint32_t)t0 << 16));
 #pragma unroll
         for (int k = 1; k < 14; ++k) {
             const uint32_t d = cw[(k - 1) >> 1];
@@ -406,6 +413,17 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         else
             pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
 #else
+        if (dbl) {
+            switch (order / 2 + 1) {
+            case 1: pass1_lr<1, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            case 2: pass1_lr<2, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            case 3: pass1_lr<3, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            case 4: pass1_lr<4, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            case 5: pass1_lr<5, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            case 6: pass1_lr<6, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            default: pass1_lr<7, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+            }
+        } else
         switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
         case 1: pass1_lr<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         case 2: pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
@@ -536,7 +554,7 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
 }
 
 // the side channel on (L, R) words, split: TAPS = min(2D, 13) as pass1_lr
-template <int D, bool BIG>
+template <int D, bool BIG, bool DBL = false>
 __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run, const int (&cl)[14],
                                                int seed_h, int seed_l, int sa_v, int sb_v,
                                                bool lane0, int order, uint32_t (&u)[ATG_RUN],
@@ -587,6 +605,10 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
             for (int h = 0; h < 2; ++h) {
                 ah[h] = dot2_first(WH[12 + ii + h], tap0, seed_h);
                 al[h] = dot2_first(WL[12 + ii + h], tap0, seed_l);
+                if constexpr (DBL) {
+                    ah[h] = dot2(WH[12 + ii + h], tap0, ah[h]);
+                    al[h] = dot2(WL[12 + ii + h], tap0, al[h]);
+                }
             }
 #pragma unroll
             for (int k = 1; k < TAPS; ++k)
@@ -615,9 +637,20 @@ template <bool BIG>
 __device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run, bool lr,
                                                 const int (&cq)[14], int seed_h, int seed_l,
                                                 int sa_v, int sb_v, bool lane0, int order,
-                                                uint32_t (&u)[ATG_RUN], uint32_t &sabs, bool subr)
+                                                uint32_t (&u)[ATG_RUN], uint32_t &sabs, bool subr,
+                                                bool dbl)
 {
-    if (lr) {
+    if (lr && dbl) {
+        switch (order / 2 + 1) {
+        case 1: pass1_lr_split<1, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 2: pass1_lr_split<2, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 3: pass1_lr_split<3, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 4: pass1_lr_split<4, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 5: pass1_lr_split<5, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 6: pass1_lr_split<6, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        default: pass1_lr_split<7, BIG, true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        }
+    } else if (lr) {
         switch (order / 2 + 1) {
         case 1: pass1_lr_split<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
         case 2: pass1_lr_split<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
@@ -648,9 +681,11 @@ __device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, c
                                              uint32_t thr, bool s16)
 {
     const bool lr = TWO && !s16;
+    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
     int cq[14];
     if (lr) {
-        cq[0] = (int)(((uint32_t)(-(1 << sh)) & 0xFFFFu) | ((uint32_t)(1 << sh) << 16));
+        const int t0 = dbl ? 1 << 14 : 1 << sh;
+        cq[0] = (int)(((uint32_t)(-t0) & 0xFFFFu) | ((uint32_t)t0 << 16));
 #pragma unroll
         for (int k = 1; k < 14; ++k) {
             const uint32_t d = cw[(k - 1) >> 1];
@@ -679,10 +714,10 @@ __device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, c
     uint32_t lane_sum;
     if (big)
         pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
-                              TWO);
+                              TWO, dbl);
     else
         pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
-                               TWO);
+                               TWO, dbl);
     return eval_tail(lane_sum, u, c, order, warm, thr);
 }
 
@@ -1013,12 +1048,13 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     c.max_rice = p.max_rice;
     c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
     // folded int32 sum exact: |sum c s| + 2^sh |s| + 2^(sh + w) < 2^31 on
-    // unshifted samples (TWO: the tap (-2^sh, 2^sh) needs 2^sh <= 32767);
+    // unshifted samples (TWO on (L, R) words, shift 15: the fold tap
+    // (-2^15, 2^15) does not fit int16 and runs as (-2^14, 2^14) twice);
     // 32-bit run sums: codes < 2^26
     const uint64_t mu = ci.amax, ms = ci.amax >> ci.w;
     const bool fold_ok = (uint64_t)csum * mu + (mu << shift) + (1ull << (shift + (int)ci.w)) <
                              (1ull << 31) &&
-                         (!TWO || shift <= 14);
+                         shift <= 15;
     const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
     // LPC jobs: the subframe total is hdr + the residual section; a job
     // whose residual bound exceeds (best finished total - hdr) is skipped
@@ -1031,12 +1067,11 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
             thr = best > hdr ? best - hdr : 0u;
     }
     // split fold (eval_split): the partial sums stay within int32 whatever
-    // the coefficients (|h| <= 128 (255 for L - R), l <= 255); the tap pair
-    // (-2^sh, 2^sh) of the side channel needs sh <= 14; shv < 8 shifts A
-    // left, which must stay inside int32
+    // the coefficients (|h| <= 128 (255 for L - R), l <= 255); shv < 8
+    // shifts A left, which must stay inside int32
     const uint64_t hsum = ((uint64_t)csum + (1ull << shift)) * (TWO ? 510ull : 255ull);
     const int shv = shift + (int)ci.w;
-    const bool split_ok = (!TWO || shift <= 14) && hsum + (1ull << shv) < (1ull << 30) &&
+    const bool split_ok = shift <= 15 && hsum + (1ull << shv) < (1ull << 30) &&
                           (shv >= 8 || (hsum << (8 - shv)) < (1ull << 30));
     const bool codes_ok = 2u * rbound + 1u < (1ull << 26);
     Eval16 ev;
