@@ -90,6 +90,8 @@ def parse_args(argv=None):
                     help=argparse.SUPPRESS)
     ap.add_argument("--no-rg4", action="store_true", help="skip the config-4 ReplayGain leg")
     ap.add_argument("--rg4-seconds", type=int, default=10)
+    ap.add_argument("--dec-inflight", type=int, default=3,
+                    help="decode batches in flight (the decoder's slot count)")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -324,22 +326,25 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     kt_sum = {}
 
     def run(k_steps, timed):
-        # two batches in flight (atg_flac_decode_device_async): batch k's
-        # per-track MD5 runs on its own stream under batch k+1's parse and
-        # restore; the last batch's drain is inside the timed region
-        pending, last = None, None
+        # three batches in flight (atg_flac_decode_device_async): batch k's
+        # restore, emit and per-track MD5 run on its slot's stream under
+        # batch k+1's scan and parse; every batch is waited (drained) inside
+        # the timed region
+        pending, last = [], None
+
+        def wait_one():
+            r = dec.decode_wait(pending.pop(0))
+            if timed:
+                for k, v in dec.kernel_times().items():
+                    kt_sum[k] = kt_sum.get(k, 0.0) + v
+            return r
+
         for _ in range(k_steps):
-            t = dec.decode_device_async(out.data_ptr(), nbytes, tracks)
-            if pending is not None:
-                last = dec.decode_wait(pending)
-                if timed:
-                    for k, v in dec.kernel_times().items():
-                        kt_sum[k] = kt_sum.get(k, 0.0) + v
-            pending = t
-        last = dec.decode_wait(pending)
-        if timed:
-            for k, v in dec.kernel_times().items():
-                kt_sum[k] = kt_sum.get(k, 0.0) + v
+            if len(pending) == args.dec_inflight:
+                last = wait_one()
+            pending.append(dec.decode_device_async(out.data_ptr(), nbytes, tracks))
+        while pending:
+            last = wait_one()
         return last
 
     if args.warmup:
@@ -386,7 +391,8 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4),
                      "selection": "longest kernel on the decoder (critical-path) stream"},
-        "pipelining": "two batches in flight: MD5 of batch k beside the restore of batch k+1",
+        "pipelining": "%d batches in flight: restore, emit and MD5 of batch k on its slot's "
+                      "stream beside the scan and parse of batch k+1" % args.dec_inflight,
         "step_hbm": {"alg_bytes_per_step": step_alg,
                      "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)},
         "verified_md5_round_trip": ok,

@@ -1039,7 +1039,7 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
                     else
                         rd = true;
                 }
-                if (rd)
+                if (rd && ATG_DEC_EXP != 5) // 5: timing experiment, no row loads
                     v = cell[(t >> 2) * 256u + (t & 3u)];
                 tile[l][x] = v;
                 if (m.kind == 1 || (step && i >= m.order)) {
@@ -1058,7 +1058,7 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
         for (uint32_t k = wv; k < NF; k += 4) {
             const uint32_t n = fn[k];
             const uint32_t left = n > i0 ? min(n - i0, kEmitTile) : 0u;
-            if (lane >= left)
+            if (lane >= left || ATG_DEC_EXP == 4) // 4: timing experiment, no writes
                 continue;
             const uint32_t ch = fch[k], as = fas[k], l = fj[k], bb = fbb[k], x = lane;
             const int32_t hi = fhi[k], lo = -hi - 1;
@@ -1154,12 +1154,24 @@ struct DBuf {
 };
 
 // One batch in flight: its PCM / MD5 byte buffers, the MD5 stream, and the
-// host copies its results are computed from.  Two slots let batch k's
-// per-track MD5 chains run under batch k+1's parse and restore.
+// host copies its results are computed from.  Three slots let batch k's
+// restore, emit and per-track MD5 (on the slot's stream, with the slot's
+// frame table, jobs and row scratch) run beside batch k+1's scan, parse and
+// chain on the decoder stream: a batch's MD5 chains (~12 ms per 1 MB track,
+// whatever the batch width) outlast its scan-to-emit path, and a slot is
+// free again only after them (config 2, 30 steps: 14.4 ms per step with
+// two slots, 11.1 with three, 13.4 with four -- more batches in flight only
+// add contention; profiles/r03_f_decode_slots.txt).
+#ifndef ATG_DEC_SLOTS
+#define ATG_DEC_SLOTS 3
+#endif
+constexpr int kDecSlots = ATG_DEC_SLOTS;
 struct DecSlot {
     DBuf pcm, bytes, md5, md5meta;
-    hipStream_t s_md5 = nullptr;
+    DBuf tracks, frames, jobs, warm, rows, meta; // the restore's tables and scratch
+    hipStream_t s_md5 = nullptr;       // the slot's stream: restore, emit, MD5
     hipEvent_t ev[kDecTimed + 1] = {}; // phase events (emit end = ev[5])
+    hipEvent_t ev_chain = nullptr;     // the chain's second pass is done (decoder stream)
     hipEvent_t ev_done = nullptr;
     uint8_t *md5_h = nullptr;          // pinned
     size_t md5_cap = 0;
@@ -1177,13 +1189,10 @@ struct atg_decoder {
     hipStream_t s = nullptr;
     float times[kDecTimed] = {};
     bool have_times = false;
-    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, frames, jobs, warm, rows, meta;
-    DecSlot slot[2];
+    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs;
+    DecSlot slot[kDecSlots];
     uint64_t next_ticket = 1;
     int last = -1; // slot of the last waited batch (decode_fetch)
-    // ticket of the newest enqueued batch: the shared device frame table
-    // (frames) belongs to it
-    uint64_t frames_ticket = 0;
 };
 
 static void build_dec_tables(uint8_t *t8, uint16_t t16[4][256])
@@ -1359,6 +1368,7 @@ atg_status atg_decoder_create(int device, atg_decoder **out)
         DHIP(hipStreamCreateWithFlags(&sl.s_md5, hipStreamNonBlocking));
         for (auto &e : sl.ev)
             DHIP(hipEventCreate(&e));
+        DHIP(hipEventCreateWithFlags(&sl.ev_chain, hipEventDisableTiming));
         DHIP(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
     }
     *out = d;
@@ -1372,14 +1382,16 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs, &d->frames, &d->jobs, &d->warm, &d->rows, &d->meta})
+                    &d->recs})
         b->release();
     for (DecSlot &sl : d->slot) {
         (void)hipStreamSynchronize(sl.s_md5);
-        for (DBuf *b : {&sl.pcm, &sl.bytes, &sl.md5, &sl.md5meta})
+        for (DBuf *b : {&sl.pcm, &sl.bytes, &sl.md5, &sl.md5meta, &sl.tracks, &sl.frames, &sl.jobs,
+                        &sl.warm, &sl.rows, &sl.meta})
             b->release();
         for (auto &e : sl.ev)
             (void)hipEventDestroy(e);
+        (void)hipEventDestroy(sl.ev_chain);
         (void)hipEventDestroy(sl.ev_done);
         if (sl.md5_h)
             (void)hipHostFree(sl.md5_h);
@@ -1392,9 +1404,10 @@ void atg_decoder_destroy(atg_decoder *d)
 } // extern "C"
 
 // Enqueue the device-resident decode of a batch on slot `sl`: scan ->
-// parse -> chain (two host round trips for the counts) -> restore ->
-// interleave on the decoder stream, then the per-track MD5 on the slot's
-// stream.  Returns once the restore is queued; finish_decode waits.
+// parse -> chain (two host round trips for the counts) on the decoder
+// stream, then restore -> emit -> per-track MD5 on the slot's stream, so the
+// next batch's scan and parse start while this one restores.  Returns once
+// everything is queued; finish_decode waits.
 static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_data,
                                  uint64_t len, const atg_flac_dec_track *tracks, uint32_t n)
 {
@@ -1482,9 +1495,10 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     }
     sl.total_samples = pb;
     sl.total_frames = fb;
-    DHIP(d->frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
-    DHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
-    DHIP(d->warm.ensure(sizeof(int32_t) * 32 * std::max<uint64_t>(jb, 1)));
+    // the slot's buffers: its previous batch was waited (take_dec_slot)
+    DHIP(sl.frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
+    DHIP(sl.jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
+    DHIP(sl.warm.ensure(sizeof(int32_t) * 32 * std::max<uint64_t>(jb, 1)));
     // row scratch: a residual loop runs at most N + 2^porder <= 2N iterations
     uint32_t max_bs = 1;
     for (uint32_t t = 0; t < n; ++t)
@@ -1492,34 +1506,42 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
             max_bs = std::max(max_bs, tr[t].max_bs);
     const uint32_t nrows = (2 * max_bs + 1 + 63) & ~63u; // whole 64-row tiles
     const uint64_t nslots = (jb + 63) / 64;
-    DHIP(d->rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
-    DHIP(d->meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
+    DHIP(sl.rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
+    DHIP(sl.meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
     DHIP(sl.pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
     DHIP(sl.bytes.ensure(std::max<uint64_t>(mb, 64)));
     DHIP(sl.md5.ensure(16 * std::max<uint32_t>(n, 1)));
-    DHIP(hipMemcpyAsync(d->tracks.p, tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
+    // the placed track table: the slot's own copy (the next batch re-uploads
+    // the decoder's while this one restores)
+    DHIP(sl.tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
+    DecTrack *str = (DecTrack *)sl.tracks.p;
+    DHIP(hipMemcpyAsync(str, tr.data(), sizeof(DecTrack) * n, hipMemcpyHostToDevice, s));
     if (n)
-        hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, dtr, n,
+        hipLaunchKernelGGL(k_dec_chain, tg, dim3(64), 0, s, w, nw, (const DecTrack *)str, n,
                            (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
                            (const uint32_t *)d->cand_idx.p, (const ParseRec *)d->recs.p,
-                           (DecCount *)d->counts.p, 2, (DecFrame *)d->frames.p,
-                           (uint2 *)d->jobs.p);
+                           (DecCount *)d->counts.p, 2, (DecFrame *)sl.frames.p,
+                           (uint2 *)sl.jobs.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(ev[3], s));
+    DHIP(hipEventRecord(sl.ev_chain, s));
+    hipStream_t ss = sl.s_md5;
+    DHIP(hipStreamWaitEvent(ss, sl.ev_chain, 0));
+    DHIP(hipEventRecord(ev[3], ss));
     if (jb)
-        hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, s, w,
-                           nw, dtr, (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
-                           (int32_t *)d->warm.p, (int32_t *)d->rows.p, nrows,
-                           (JobMeta *)d->meta.p);
+        hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, ss, w,
+                           nw, (const DecTrack *)str, (const DecFrame *)sl.frames.p,
+                           (const uint2 *)sl.jobs.p, jb, (int32_t *)sl.warm.p,
+                           (int32_t *)sl.rows.p, nrows, (JobMeta *)sl.meta.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(ev[4], s));
+    DHIP(hipEventRecord(ev[4], ss));
     if (jb)
-        hipLaunchKernelGGL(k_dec_emit, dim3((unsigned)nslots), dim3(256), 0, s, dtr,
-                           (const DecFrame *)d->frames.p, (const uint2 *)d->jobs.p, jb,
-                           (const JobMeta *)d->meta.p, (const int32_t *)d->rows.p, nrows,
-                           (const int32_t *)d->warm.p, (int32_t *)sl.pcm.p, (uint8_t *)sl.bytes.p);
+        hipLaunchKernelGGL(k_dec_emit, dim3((unsigned)nslots), dim3(256), 0, ss,
+                           (const DecTrack *)str, (const DecFrame *)sl.frames.p,
+                           (const uint2 *)sl.jobs.p, jb, (const JobMeta *)sl.meta.p,
+                           (const int32_t *)sl.rows.p, nrows, (const int32_t *)sl.warm.p,
+                           (int32_t *)sl.pcm.p, (uint8_t *)sl.bytes.p);
     DHIP(hipGetLastError());
-    DHIP(hipEventRecord(ev[5], s));
+    DHIP(hipEventRecord(ev[5], ss));
     // MD5 of the decoded bytes on the slot's stream: the next batch's scan,
     // parse and restore run on the decoder stream meanwhile
     sl.md5_meta.assign(2 * (size_t)n, 0);
@@ -1539,7 +1561,6 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
                            hipHostMallocDefault));
         sl.md5_cap = 16 * (size_t)std::max<uint32_t>(n, 1);
     }
-    DHIP(hipStreamWaitEvent(sl.s_md5, ev[5], 0));
     if (n)
         DHIP(hipMemcpyAsync(sl.md5meta.p, sl.md5_meta.data(), sizeof(uint64_t) * 2 * n,
                             hipMemcpyHostToDevice, sl.s_md5));
@@ -1551,8 +1572,6 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
         DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
                             sl.s_md5));
     DHIP(hipEventRecord(sl.ev_done, sl.s_md5));
-    // the device frame table now belongs to this batch (decode_fetch)
-    d->frames_ticket = sl.ticket;
     return ATG_OK;
 }
 
@@ -1600,14 +1619,15 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
     return ATG_OK;
 }
 
-// the slot for a new batch: the older of the two, waited for if still busy
+// the slot for a new batch: the oldest, which must have been waited
 static atg_status take_dec_slot(atg_decoder *d, DecSlot **out)
 {
     DecSlot *sl = &d->slot[0];
-    if (d->slot[1].ticket < sl->ticket)
-        sl = &d->slot[1];
+    for (int k = 1; k < kDecSlots; ++k)
+        if (d->slot[k].ticket < sl->ticket)
+            sl = &d->slot[k];
     if (sl->busy)
-        return dfail(ATG_ERR_INVALID, "two decode batches already in flight: wait for one");
+        return dfail(ATG_ERR_INVALID, "three decode batches already in flight: wait for one");
     sl->ticket = d->next_ticket++;
     *out = sl;
     return ATG_OK;
@@ -1720,11 +1740,11 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
         return dfail(ATG_ERR_INVALID, "no decoded batch");
     DecSlot &sl = d->slot[d->last];
     const bool want_frames = frame_offsets || frame_block_sizes;
-    // the frame table lives in one device buffer shared by the slots: only
-    // the newest batch's is there
-    if (want_frames && sl.ticket != d->frames_ticket)
-        return dfail(ATG_ERR_INVALID, "frame table of the last waited batch was replaced by a "
-                                      "newer batch: fetch it before enqueueing another");
+    // the slot's buffers hold the last waited batch until a newer batch takes
+    // the slot
+    if (sl.busy)
+        return dfail(ATG_ERR_INVALID, "the last waited batch's slot holds a newer batch: fetch "
+                                      "before enqueueing three more");
     if ((pcm && pcm_cap < sl.total_samples) || (want_frames && frame_cap < sl.total_frames))
         return dfail(ATG_ERR_CAPACITY, "output buffer too small for the decoded batch");
     DHIP(hipSetDevice(d->device));
@@ -1734,7 +1754,7 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
     std::vector<DecFrame> fr;
     if (want_frames && sl.total_frames) {
         fr.resize(sl.total_frames);
-        DHIP(hipMemcpyAsync(fr.data(), d->frames.p, sizeof(DecFrame) * sl.total_frames,
+        DHIP(hipMemcpyAsync(fr.data(), sl.frames.p, sizeof(DecFrame) * sl.total_frames,
                             hipMemcpyDeviceToHost, d->s));
     }
     DHIP(hipStreamSynchronize(d->s));

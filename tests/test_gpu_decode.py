@@ -167,10 +167,11 @@ def test_truncated_stream_raises_ioerror():
             pass
 
 
-def test_async_decode_two_in_flight(gpu_engine):
-    """atg_flac_decode_device_async: two batches in flight (batch k's MD5
-    under batch k+1's restore) give the synchronous decode's results and
-    PCM; a third enqueue before a wait is refused"""
+def test_async_decode_three_in_flight(gpu_engine):
+    """atg_flac_decode_device_async: three batches in flight (batch k's
+    restore, emit and MD5 on its slot's stream under batch k+1's scan and
+    parse) give the synchronous decode's results and PCM; a fourth enqueue
+    before a wait is refused"""
     import torch
     from audiotools import _atgpu
     opts = dict(oracle_port.PRESETS["8"])
@@ -192,9 +193,10 @@ def test_async_decode_two_in_flight(gpu_engine):
     want = [(r.status, r.pcm_frames, bytes(r.md5)) for r in want]
     t1 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
     t2 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    t3 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
     with pytest.raises(_atgpu.ATGError):
         dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
-    for t in (t1, t2):
+    for t in (t1, t2, t3):
         got, d_pcm, n = dec.decode_wait(t)
         assert [(r.status, r.pcm_frames, bytes(r.md5)) for r in got] == want
         assert n == wn == len(allpcm)
