@@ -810,7 +810,8 @@ def chain_verify(args, threads, ch, bps, rin, rout, n_tracks, n_in, n_out, info,
            "verified_tracks": n_tracks - len(set(sum(bad.values(), []))),
            "verify_seconds": round(dt, 1)}
     # CPU baseline: reference binaries where they exist
-    ref_ok = os.path.exists(oracle_port.REF_ALACDEC) and os.path.exists(oracle_port.REF_FLACENC)
+    ref_ok = (os.path.exists(oracle_port.REF_ALACDEC) and os.path.exists(oracle_port.REF_FLACENC)
+              and not args.no_cpu_baseline)
     nb = min(n_tracks, max(1, threads))
     fargs = [oracle_port.REF_FLACENC, "-c", str(ch), "-r", str(rout), "-b", str(bps), "-B",
              "4096", "-l", "12", "-P", "0", "-R", "6", "-m", "-e"]
@@ -951,8 +952,10 @@ def t2t_leg(args, pcm_host, n_samples, threads):
                     "wall_s": round(wall, 3),
                     "per_process_frames_per_s": round(frames / procs / wall, 1)})
         # the reference encoder, one process per track, the same count at a time
+        # (skipped with --no-cpu-baseline: e.g. under a profiler, whose
+        # preloaded library the child processes would inherit)
         exe = oracle_port.REF_FLACENC
-        if os.path.exists(exe):
+        if os.path.exists(exe) and not args.no_cpu_baseline:
             rargs = [exe, "-c", "2", "-r", "44100", "-b", "16", "-B", "4096", "-l", "12", "-P",
                      "0", "-R", "6", "-m", "-e"]
             rdir = os.path.join(d, "ref")
