@@ -1304,6 +1304,8 @@ def main(argv=None):
             convert = convert_leg(args, torch, device, pcm)
         resample = resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier,
                                 threads, rank == 0 and not args.no_verify)
+        rg, rg_res = replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks,
+                                    barrier)
     t2t = rg4 = None
     if not args.no_t2t and rank == 0 and world == 1:
         t2t = t2t_leg(args, pcm_host, n_samples, threads)
@@ -1313,8 +1315,6 @@ def main(argv=None):
     if not args.no_chain:
         chain = chain_leg(args, torch, dist, world, device, barrier, threads,
                           rank == 0 and not args.no_verify)
-        rg, rg_res = replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks,
-                                    barrier)
 
     if rank != 0:
         if world > 1:

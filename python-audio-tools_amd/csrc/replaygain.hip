@@ -76,6 +76,31 @@ struct Chan {
     double in[10], yo[10], bo0, bo1; // newest first
 };
 
+// filt on a ring history: step R of a 10-sample cycle finds the newest
+// input / output at slot (10 - R) % 10 and writes the new ones one slot
+// down, so an unrolled cycle of 10 samples moves no registers (the shift
+// of filt costs ~30 v_mov_b64 per sample in a loop).  Same operations in
+// the same order as filt.
+template <int R>
+__device__ __forceinline__ double filt_r(Chan &s, double x, const double *ky, const double *kb)
+{
+    constexpr int h = (10 - R % 10) % 10; // slot of the newest sample
+    double y = 1e-10 + x * ky[0];
+#pragma unroll
+    for (int k = 1; k <= 10; ++k) {
+        y = y - s.yo[(h + k - 1) % 10] * ky[2 * k - 1];
+        y = y + s.in[(h + k - 1) % 10] * ky[2 * k];
+    }
+    const double b = y * kb[0] - s.bo0 * kb[1] + s.yo[h] * kb[2] - s.bo1 * kb[3] +
+                     s.yo[(h + 1) % 10] * kb[4];
+    constexpr int nh = (h + 9) % 10;
+    s.in[nh] = x;
+    s.yo[nh] = y;
+    s.bo1 = s.bo0;
+    s.bo0 = b;
+    return b;
+}
+
 // filterYule then filterButter for one sample (replaygain.c:566-610):
 // left-to-right sums exactly as the reference's expressions
 __device__ __forceinline__ double filt(Chan &s, double x, const double *ky, const double *kb)
@@ -116,7 +141,7 @@ __device__ __forceinline__ double filt(Chan &s, double x, const double *ky, cons
 // (the read()/batch/window bookkeeping only groups the running sums), so the
 // chunk schedule is wave-uniform; the bookkeeping is a per-lane state
 // machine.
-constexpr uint32_t kRgChunk = 64;
+constexpr uint32_t kRgChunk = 80; // a multiple of filt_r's 10-sample cycle
 constexpr uint32_t kRgStride = 2 * kRgChunk + 2; // ints per track per buffer (conflict-free reads)
 
 __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm,
@@ -159,7 +184,24 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
         for (uint32_t i = 0; i < kRgChunk; ++i)
             buf[b][j * kRgStride + chan * kRgChunk + i] = ld[i];
     };
-    const double *ky = c_yule[have ? T.fi : 0], *kb = c_butter[have ? T.fi : 0];
+    // the lane's coefficients in registers, opaque to the compiler (it
+    // otherwise re-loads them from the constant table inside the unrolled
+    // sample cycle to save registers; a lone wave per SIMD has 512)
+    double ky[21], kb[5];
+    {
+        const double *gy = c_yule[have ? T.fi : 0], *gb = c_butter[have ? T.fi : 0];
+#pragma unroll
+        for (int i = 0; i < 21; ++i) {
+            ky[i] = gy[i];
+            asm volatile("" : "+v"(ky[i]));
+        }
+#pragma unroll
+        for (int i = 0; i < 5; ++i) {
+            kb[i] = gb[i];
+            asm volatile("" : "+v"(kb[i]));
+        }
+    }
+    const int xsl = T.bps == 8 ? 8 : 0, xsr = T.bps == 24 ? 8 : 0;
     double *W = wsum + 2 * (have ? win_base[t] : 0) + chan;
     const long window = have ? (long)T.window : 1;
     Chan S = {};
@@ -173,12 +215,14 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
         return T.chunk_base != ~0ull ? (long)chunks[ci++]
                                      : (long)(frames - c0 < 4096 ? frames - c0 : 4096);
     };
-    long n4 = run ? next_read() : 0, pos = 0, batch = n4, totsamp = 0, nwin = 0, k = 0;
-    long cur = 0, singles = 0;
+    long n4 = run ? next_read() : 0, pos = 0, batch = n4, totsamp = 0, nwin = 0;
+    // per-sample state in 32 bits: a batch is at most one window (< 2^31)
+    int32_t k = 0, cur = 0, singles = 0;
     auto start_batch = [&]() {
-        cur = batch > window - totsamp ? window - totsamp : batch;
-        if (pos < 10 && cur > 10 - pos)
-            cur = 10 - pos;
+        long c = batch > window - totsamp ? window - totsamp : batch;
+        if (pos < 10 && c > 10 - pos)
+            c = 10 - pos;
+        cur = (int32_t)c;
         singles = cur % 16;
         k = 0;
     };
@@ -195,25 +239,38 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
         const int32_t *xb = &buf[b][j * kRgStride + chan];
         const uint64_t nk = run && frames > F ? min((uint64_t)kRgChunk, frames - F) : 0;
         int32_t nx = xb[0];
-        for (uint32_t kk = 0; kk < nk; ++kk) {
+        // samples in cycles of 10 (filt_r's ring); a chunk is 8 cycles
+        for (uint32_t k10 = 0; k10 < nk; k10 += 10) {
+#pragma unroll
+        for (int r = 0; r < 10; ++r) {
+            const uint32_t kk = k10 + (uint32_t)r;
+            if (kk < nk) {
             // the next sample's LDS read is issued before this one's filter
             const int32_t iv = nx;
-            nx = xb[(kk + 1) * ch]; // inside the padded row when kk + 1 == 64
-            double x;
-            if (T.bps == 8)
-                x = (double)(iv << 8);
-            else if (T.bps == 16)
-                x = (double)iv;
-            else
-                x = (double)(iv >> 8);
+            nx = xb[(kk + 1) * ch]; // inside the padded row when kk + 1 == kRgChunk
+            // 8-bit: x << 8, 16-bit: x, 24-bit: x >> 8 (as shift amounts: no
+            // per-sample branches on the lane's format)
+            const double x = (double)((iv << xsl) >> xsr);
             const uint32_t av = (uint32_t)(iv < 0 ? -(int64_t)iv : iv);
             amax = av > amax ? av : amax;
-            const double o = filt(S, x, ky, kb);
+            double o;
+            switch (r) {
+            case 0: o = filt_r<0>(S, x, ky, kb); break;
+            case 1: o = filt_r<1>(S, x, ky, kb); break;
+            case 2: o = filt_r<2>(S, x, ky, kb); break;
+            case 3: o = filt_r<3>(S, x, ky, kb); break;
+            case 4: o = filt_r<4>(S, x, ky, kb); break;
+            case 5: o = filt_r<5>(S, x, ky, kb); break;
+            case 6: o = filt_r<6>(S, x, ky, kb); break;
+            case 7: o = filt_r<7>(S, x, ky, kb); break;
+            case 8: o = filt_r<8>(S, x, ky, kb); break;
+            default: o = filt_r<9>(S, x, ky, kb); break;
+            }
             const double o2 = o * o;
             if (k < singles) {
                 sum += o2;
             } else {
-                const long gi = (k - singles) & 15;
+                const int32_t gi = (k - singles) & 15;
                 gs = gi == 0 ? o2 : gs + o2;
                 if (gi == 15)
                     sum += gs;
@@ -239,6 +296,8 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
                 if (batch > 0)
                     start_batch();
             }
+        }
+        }
         }
         // the buffer is rewritten two boundaries later: every lane's reads
         // of it are done before its next store (in-order LDS per wave)
