@@ -238,34 +238,37 @@ __global__ __launch_bounds__(64) void k_rg_title(const int32_t *__restrict__ pcm
             load_chunk(F + kRgChunk);
         const int32_t *xb = &buf[b][j * kRgStride + chan];
         const uint64_t nk = run && frames > F ? min((uint64_t)kRgChunk, frames - F) : 0;
-        int32_t nx = xb[0];
-        // samples in cycles of 10 (filt_r's ring); a chunk is 8 cycles
+        // samples in cycles of 10 (filt_r's ring; a chunk is 8 cycles).  A
+        // cycle's 10 filter steps are one straight-line block, so one
+        // sample's Butterworth stage and the next one's Yule products fill
+        // the gaps of the dependent Yule chain; the bookkeeping follows.
+        // Past nk (the lane's track ends inside this chunk) the row's stale
+        // words are filtered and never used.
         for (uint32_t k10 = 0; k10 < nk; k10 += 10) {
+            int32_t iv[10];
+#pragma unroll
+            for (int r = 0; r < 10; ++r)
+                iv[r] = xb[(k10 + (uint32_t)r) * ch];
+            // 8-bit: x << 8, 16-bit: x, 24-bit: x >> 8 (as shift amounts: no
+            // per-sample branches on the lane's format)
+            double ov[10];
+            ov[0] = filt_r<0>(S, (double)((iv[0] << xsl) >> xsr), ky, kb);
+            ov[1] = filt_r<1>(S, (double)((iv[1] << xsl) >> xsr), ky, kb);
+            ov[2] = filt_r<2>(S, (double)((iv[2] << xsl) >> xsr), ky, kb);
+            ov[3] = filt_r<3>(S, (double)((iv[3] << xsl) >> xsr), ky, kb);
+            ov[4] = filt_r<4>(S, (double)((iv[4] << xsl) >> xsr), ky, kb);
+            ov[5] = filt_r<5>(S, (double)((iv[5] << xsl) >> xsr), ky, kb);
+            ov[6] = filt_r<6>(S, (double)((iv[6] << xsl) >> xsr), ky, kb);
+            ov[7] = filt_r<7>(S, (double)((iv[7] << xsl) >> xsr), ky, kb);
+            ov[8] = filt_r<8>(S, (double)((iv[8] << xsl) >> xsr), ky, kb);
+            ov[9] = filt_r<9>(S, (double)((iv[9] << xsl) >> xsr), ky, kb);
 #pragma unroll
         for (int r = 0; r < 10; ++r) {
             const uint32_t kk = k10 + (uint32_t)r;
             if (kk < nk) {
-            // the next sample's LDS read is issued before this one's filter
-            const int32_t iv = nx;
-            nx = xb[(kk + 1) * ch]; // inside the padded row when kk + 1 == kRgChunk
-            // 8-bit: x << 8, 16-bit: x, 24-bit: x >> 8 (as shift amounts: no
-            // per-sample branches on the lane's format)
-            const double x = (double)((iv << xsl) >> xsr);
-            const uint32_t av = (uint32_t)(iv < 0 ? -(int64_t)iv : iv);
+            const uint32_t av = (uint32_t)(iv[r] < 0 ? -(int64_t)iv[r] : iv[r]);
             amax = av > amax ? av : amax;
-            double o;
-            switch (r) {
-            case 0: o = filt_r<0>(S, x, ky, kb); break;
-            case 1: o = filt_r<1>(S, x, ky, kb); break;
-            case 2: o = filt_r<2>(S, x, ky, kb); break;
-            case 3: o = filt_r<3>(S, x, ky, kb); break;
-            case 4: o = filt_r<4>(S, x, ky, kb); break;
-            case 5: o = filt_r<5>(S, x, ky, kb); break;
-            case 6: o = filt_r<6>(S, x, ky, kb); break;
-            case 7: o = filt_r<7>(S, x, ky, kb); break;
-            case 8: o = filt_r<8>(S, x, ky, kb); break;
-            default: o = filt_r<9>(S, x, ky, kb); break;
-            }
+            const double o = ov[r];
             const double o2 = o * o;
             if (k < singles) {
                 sum += o2;
