@@ -182,7 +182,7 @@ uint64_t atg_flac_stream_header(const atg_flac_options *opts, uint32_t channels,
                                 uint32_t max_frame_bytes, const uint8_t *md5, uint8_t *out,
                                 uint64_t cap);
 
-/* PCM bytes per chunk of atg_flac_encode_host's pipeline (default 256 MiB):
+/* PCM bytes per chunk of atg_flac_encode_host's pipeline (default 512 MiB):
    consecutive tracks are grouped into chunks of about this much PCM, and
    chunk c+1's upload, chunk c's encode and chunk c-1's download overlap. */
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *eng, uint64_t bytes);

@@ -197,7 +197,12 @@ struct atg_engine {
     // chunk c's encode and chunk c-1's download overlap
     HostStage hs[kEncSlots];
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
-    uint64_t chunk_bytes = 256ull << 20; // PCM bytes per chunk
+    // PCM bytes per chunk.  A chunk's MD5 chains take ~15 ms per MiB of
+    // track whatever its track count, so fewer, larger chunks keep fewer
+    // chains in flight: config 2, queued jobs, 256 MB 28.8 ms per batch,
+    // 512 MB 27.0 ms, 768 MB 40.3 ms; one synchronous call 41.1 / 37.9 /
+    // 48.2 ms (profiles/r03_h_host_chunks.txt)
+    uint64_t chunk_bytes = 512ull << 20;
     // host jobs (atg_flac_encode_host_async), oldest first; their chunks
     // flow through the stages in submission order, kEncSlots in flight
     std::deque<std::unique_ptr<HostJob>> hjobs;

@@ -14,7 +14,7 @@ import oracle_port
 pytestmark = pytest.mark.gpu
 
 
-DEFAULT_CHUNK = 256 << 20
+DEFAULT_CHUNK = 512 << 20
 
 
 @pytest.fixture
