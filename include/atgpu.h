@@ -351,12 +351,14 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
                                   atg_flac_dec_result *results, const int32_t **d_pcm,
                                   uint64_t *total_samples);
 
-/* Asynchronous form of atg_flac_decode_device (two batches in flight):
-   returns once batch k's restore is queued, with its per-track MD5 on a
-   second stream, so batch k's MD5 runs under batch k+1's parse and restore.
-   d_data must stay valid until the wait; the PCM pointer the wait returns
-   stays valid until the batch after next is enqueued.  A third enqueue
-   before a wait fails with ATG_ERR_INVALID. */
+/* Asynchronous form of atg_flac_decode_device (three batches in flight):
+   the scan, parse and frame walk run on the decoder's stream (two host
+   round trips for the counts), then the restore, emit and per-track MD5 on
+   the batch's own slot stream with its own buffers, so batch k's back half
+   runs under batch k+1's scan and parse.  Returns once everything is
+   queued.  d_data must stay valid until the wait; the PCM pointer the wait
+   returns stays valid until the slot is reused (the third enqueue after
+   it).  A fourth enqueue before a wait fails with ATG_ERR_INVALID. */
 atg_status atg_flac_decode_device_async(atg_decoder *dec, const void *d_data, uint64_t len,
                                         const atg_flac_dec_track *tracks, uint32_t n_tracks,
                                         uint64_t *ticket);
