@@ -342,8 +342,12 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
 // pairs with 16-byte loads: no sample LDS, twice the occupancy.  Used for
 // the leading full-length (4096) frames of a 16-bit mid/side batch whose
 // frame starts are 16-byte aligned (engine.hip counts them: n_reg_frames).
+// waves per SIMD the pack kernel's registers are budgeted for
+#ifndef ATG_K5_WPE
+#define ATG_K5_WPE 2
+#endif
 template <typename T, bool REG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2))) void k_frame_pack(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))) void k_frame_pack(
     FlacParams p, uint32_t f0, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)

@@ -430,7 +430,7 @@ __global__ __launch_bounds__(64) void k_rs_phase_tab(const RsTrack *__restrict__
 // across a rounding boundary) takes the per-lane path with the
 // coefficients read from the global table.
 template <int CH, int M>
-__global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__restrict__ tr,
+__global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__restrict__ tr,
                                                   const uint2 *__restrict__ tasks,
                                                   uint32_t n_tasks, const int2 *__restrict__ pos,
                                                   const uint32_t *__restrict__ table_bits,
@@ -540,7 +540,7 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
                     const double2 *__restrict__ gr =
                         reinterpret_cast<const double2 *>(tb + kTabHdr + (uint64_t)M * wmax);
                     double2 *dl = reinterpret_cast<double2 *>(cL), *dr = reinterpret_cast<double2 *>(cR);
-                    const int32_t nl = WL * M / 2, nr = WR * M / 2;
+                    const int32_t nl = (WL * M + 1) / 2, nr = (WR * M + 1) / 2;
                     for (int32_t k = (int32_t)lane; k < max(nl, nr); k += 64) {
                         double2 a, b;
                         if (k < nl)
@@ -631,7 +631,7 @@ __global__ __launch_bounds__(512) void k_rs_phase(RsParams P, const RsTrack *__r
 
 // outputs per lane of k_rs_phase: as many as the accumulators allow
 template <int CH>
-constexpr int phase_m() { return CH <= 2 ? 4 : 2; }
+constexpr int phase_m() { return CH <= 2 ? 5 : 2; }
 
 // ------------------------------------------------------------------ host
 thread_local std::string g_rs_err;
@@ -924,7 +924,12 @@ void launch_filter(const FilterArgs &A, bool hoist, bool xd, unsigned grid, unsi
 #undef RS_GO
 }
 
-constexpr unsigned kPhaseThreads = 512;
+// threads per k_rs_phase block: its waves share the block's input window.
+// <= 2 channels: 16 waves (4 per SIMD) over M = 5, 32 groups of a 160-output
+// lane span = 2 items per wave (config 3: 7.86 -> 7.34 ms against 8 waves,
+// M = 4); more channels: 8 waves (the 6-channel config-5 resample ran 16.1
+// -> 18.2 ms at 16)
+constexpr unsigned phase_threads(uint32_t channels) { return channels <= 2 ? 1024u : 512u; }
 
 struct PhaseTabs {
     const uint32_t *class_track; // a track of each ratio class
@@ -940,7 +945,7 @@ void launch_phase(const FilterArgs &A, const uint2 *tasks, uint32_t n_tasks, uin
     constexpr int M = phase_m<CH>();
     hipLaunchKernelGGL((k_rs_phase_tab<M>), dim3(pt.G, pt.n_classes), dim3(64), 0, s, A.tr,
                        pt.class_track, A.pos, A.table, pt.tabs, pt.G, wmax, pt.stride);
-    hipLaunchKernelGGL((k_rs_phase<CH, M>), dim3(grid), dim3(kPhaseThreads), lds, s, A.P, A.tr,
+    hipLaunchKernelGGL((k_rs_phase<CH, M>), dim3(grid), dim3(phase_threads(CH)), lds, s, A.P, A.tr,
                        tasks, n_tasks, A.pos, A.table, A.in, A.out, wmax,
                        (const double *)pt.tabs, pt.G, pt.stride);
 }
@@ -1038,8 +1043,8 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
     // coefficient tables; the rest go to the per-output kernel k_rs_filter.
     const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
     const size_t kLds = 160 * 1024;
-    const uint32_t pm = channels <= 2 ? 4u : 2u; // phase_m<CH>()
-    const size_t waves = kPhaseThreads / 64;
+    const uint32_t pm = channels <= 2 ? 5u : 2u; // phase_m<CH>()
+    const size_t waves = phase_threads(channels) / 64;
     std::vector<uint32_t> per(n, 0), rows(n, 0), lspan(n, 0);
     std::vector<char> phase(n, 0);
     uint32_t wmax = 0;
@@ -1050,7 +1055,8 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             const uint64_t p_out = tracks[t].out_rate / g, q_in = tracks[t].in_rate / g;
             const uint64_t reach = (uint64_t)(max_fi / conv[t].increment) + 2;
             const uint64_t step = (tracks[t].in_rate + tracks[t].out_rate - 1) / tracks[t].out_rate;
-            const uint32_t wm_t = (uint32_t)(reach + (pm - 1) * step + 2);
+            // even: the [tap][M] tables stay 16-byte aligned for odd M
+            const uint32_t wm_t = (uint32_t)(reach + (pm - 1) * step + 2 + 1) & ~1u;
             const size_t coef = waves * 2 * pm * std::max<uint32_t>(wmax, wm_t) * sizeof(double);
             phase[t] = 0;
             if (p_out > 65536)
