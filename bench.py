@@ -585,6 +585,12 @@ def resample_leg(args, torch, dist, world, device, pcm, n_tracks, barrier, threa
                         "peak": F64_PEAK_TFLOPS, "unit": "TFLOP/s",
                         "frac": round(achieved / F64_PEAK_TFLOPS, 4) if achieved else None,
                         "alg_flops_per_launch": flops, "launch_ms": round(f_ms, 4),
+                        # the reference rounds each product (no FMA): a tap is a
+                        # v_mul_f64 + v_add_f64 pair, so the attainable rate is
+                        # half the FMA peak
+                        "peak_no_fma": F64_PEAK_TFLOPS / 2,
+                        "frac_no_fma": round(achieved / (F64_PEAK_TFLOPS / 2), 4)
+                        if achieved else None,
                         "hbm_alg_bytes": hbm,
                         "hbm_frac": round(hbm / (f_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 4)
                         if f_ms else None},
