@@ -1,14 +1,16 @@
 #!/bin/bash
-# GPU-box recipe for round end: the whole -m gpu suite, then a rocprofv3
-# kernel-stats pass of the encoder-leg bench (the headline workload only, so
-# the per-kernel averages are the bench line's launches).
+# GPU-box recipe (round end): the GPU test suite, smoke(), the default bench
+# (every leg), its rocprof kernel stats, and the PMC passes.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-mkdir -p "$R/gpurun_out"
+OUT=$R/gpurun_out/${1:-final}
+mkdir -p "$OUT"
 cd "$R"
-timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread \
-    > gpurun_out/pytest_gpu.log 2>&1
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
+timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$R/gpurun_out/prof_enc" -o run --output-format csv \
-    -- python3 "$R/bench.py" --steps 10 --warmup 3 --no-cpu-baseline --no-decode --no-chain --no-host \
-    > "$R/gpurun_out/prof_enc.log" 2>&1
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+    -- python3 $R/bench.py --no-cpu-baseline > "$OUT/prof.log" 2>&1
+cd "$R"
+bash tools/gpu_pmc.sh
