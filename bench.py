@@ -863,7 +863,8 @@ def chain_verify(args, threads, ch, bps, rin, rout, n_tracks, n_in, n_out, info,
                      "reference alacdec + flacenc processes (built from the reference's "
                      "src/decoders/alac.c, src/encoders/flac.c) around the resample port "
                      "(the reference's BEST-table resampler is unbuildable)" if ref_ok else
-                     "CPU restatements (oracle/_ref absent)"),
+                     ("CPU restatements (--no-cpu-baseline: reference processes skipped)"
+                      if args.no_cpu_baseline else "CPU restatements (oracle/_ref absent)")),
         "gpu_images_identical": all(same)}
     del yh, sh, fh, alac_h
     return out
