@@ -338,12 +338,17 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 // partition search of a predictor that cannot win (flac.c:1326-1505 picks
 // the smallest exact total, so one whose bound exceeds a finished total
 // cannot be chosen).
+#ifndef ATG_K2F_FIXPRUNE
+#define ATG_K2F_FIXPRUNE 1
+#endif
 #define K2F_PRUNED 0x3FFFFFFFu
 __device__ __forceinline__ uint32_t residual_lb(uint32_t lane_sum, uint32_t cnt)
 {
     const float cf = (float)cnt;
     const float U = fmaxf(2.0f * (float)lane_sum - cf, 0.0f);
     const float x = (U + cf) * 0.69314718f / cf;
+    // (the integer-k minimum, two exp2 evaluations, pruned no more jobs per
+    // ms of K2 than this: 6.23 vs 6.14 ms)
     const float lb = x >= 1.0f ? cf * __log2f(x) + cf * 1.44269504f : U + cf;
     const uint32_t lbi = (uint32_t)fmaxf(lb - 4.0f, 0.0f);
     return dpp_wave_sum<uint32_t>(lbi);
@@ -1060,11 +1065,16 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     // whose residual bound exceeds (best finished total - hdr) is skipped
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
+    // FIXED (ATG_K2F_FIXPRUNE): it wins only below every LPC total
+    // (flac.c:727-809, strict <), so a bound above a finished LPC total
+    // rules it out the same way; its header is 7 + wf + o (sbps - w)
+    const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     uint32_t thr = 0xFFFFFFFFu;
-    if (!is_fixed && ATG_K2F_EXP != 5) {
+    if ((!is_fixed || ATG_K2F_FIXPRUNE) && ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+        const uint32_t hh = is_fixed ? hdr_f : hdr;
         if (best != 0xFFFFFFFFu)
-            thr = best > hdr ? best - hdr : 0u;
+            thr = best > hh ? best - hh : 0u;
     }
     // split fold (eval_split): the partial sums stay within int32 whatever
     // the coefficients (|h| <= 128 (255 for L - R), l <= 255); shv < 8
@@ -1776,11 +1786,16 @@ __device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
     const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
+    // FIXED (ATG_K2F_FIXPRUNE): it wins only below every LPC total
+    // (flac.c:727-809, strict <), so a bound above a finished LPC total
+    // rules it out the same way; its header is 7 + wf + o (sbps - w)
+    const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     uint32_t thr = 0xFFFFFFFFu;
-    if (!is_fixed && ATG_K2F_EXP != 5) {
+    if ((!is_fixed || ATG_K2F_FIXPRUNE) && ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+        const uint32_t hh = is_fixed ? hdr_f : hdr;
         if (best != 0xFFFFFFFFu)
-            thr = best > hdr ? best - hdr : 0u;
+            thr = best > hh ? best - hh : 0u;
     }
     Eval16 ev;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
