@@ -39,6 +39,18 @@ class FrameList(object):
             raise ValueError(
                 "number of samples must be divisible by bits-per-sample "
                 "and number of channels")
+        self.channels = channels
+        self.bits_per_sample = bits_per_sample
+        # the common containers straight through numpy's own dtypes
+        # (WAVE: 16-bit signed little-endian, 8-bit unsigned)
+        if width == 2 and is_signed:
+            self._samples = np.frombuffer(
+                data, dtype=">i2" if is_big_endian else "<i2").astype(np.int32)
+            return
+        if width == 1:
+            v = np.frombuffer(data, dtype=np.int8 if is_signed else np.uint8)
+            self._samples = v.astype(np.int32) - (0 if is_signed else 128)
+            return
         raw = np.frombuffer(data, dtype=np.uint8).reshape(-1, width)
         if is_big_endian:
             raw = raw[:, ::-1]
@@ -51,8 +63,6 @@ class FrameList(object):
         else:
             value = value - (np.int64(1) << (bits_per_sample - 1))
         self._samples = value.astype(np.int32)
-        self.channels = channels
-        self.bits_per_sample = bits_per_sample
 
     @classmethod
     def _wrap(cls, samples, channels, bits_per_sample):

@@ -206,3 +206,50 @@ def test_async_decode_three_in_flight(gpu_engine):
     with pytest.raises(_atgpu.ATGError):
         dec.decode_wait(t1)
     dec.close()
+
+
+def test_async_decode_fetch_frame_table(gpu_engine):
+    """atg_flac_decode_fetch after an async batch: the frame table lives in
+    the batch's slot, so the last waited batch's offsets and block sizes are
+    readable while two newer batches are in flight, equal to the host
+    decode's; once a newer batch takes that slot, fetch is refused"""
+    import ctypes
+    import torch
+    from audiotools import _atgpu
+    opts = dict(oracle_port.PRESETS["5"])
+    pcms = [signals.make(k, 4096 * 3 + 129 * i, 2, 16, seed=70 + i)
+            for i, k in enumerate(["tone", "noise", "chirp"])]
+    o = _atgpu.make_options(**opts)
+    tracks, start = [], 0
+    for p in pcms:
+        tracks.append((start, len(p) // 2))
+        start += len(p) // 2
+    allpcm = np.concatenate(pcms).astype(np.int16)
+    out, res, _, _ = gpu_engine.encode(o, allpcm, tracks, 2, 16, 44100)
+    images = [out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res]
+    dtracks, blob, _ = _batch(images)
+    dec = _atgpu.Decoder(0)
+    _, want, woffs, wbs = dec.decode(blob, dtracks)
+    d_blob = torch.frombuffer(bytearray(blob + b"\0" * 64), dtype=torch.uint8).cuda()
+    torch.cuda.synchronize()
+    t1 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    t2 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    t3 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)
+    dec.decode_wait(t1)
+    nf = len(woffs)
+    offs = np.empty(nf, dtype=np.uint64)
+    bss = np.empty(nf, dtype=np.uint32)
+    lib = dec.lib
+    st = lib.atg_flac_decode_fetch(dec.handle, None, 0, offs.ctypes.data_as(ctypes.c_void_p),
+                                   bss.ctypes.data_as(ctypes.c_void_p), nf)
+    assert st == 0, lib.atg_decoder_last_error()
+    assert np.array_equal(offs, woffs) and np.array_equal(bss, wbs)
+    t4 = dec.decode_device_async(d_blob.data_ptr(), len(blob), dtracks)  # t1's slot
+    st = lib.atg_flac_decode_fetch(dec.handle, None, 0, offs.ctypes.data_as(ctypes.c_void_p),
+                                   bss.ctypes.data_as(ctypes.c_void_p), nf)
+    assert st != 0
+    for t in (t2, t3, t4):
+        got, _, _ = dec.decode_wait(t)
+        assert [(r.status, r.pcm_frames) for r in got] == [(r.status, r.pcm_frames) for r in want]
+    dec.close()
+
