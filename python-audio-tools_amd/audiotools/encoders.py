@@ -37,6 +37,7 @@ src/encoders/alac.c:30-189; GPU kernels alac_encode.hip).
 """
 
 import hashlib
+import threading
 
 import numpy as np
 
@@ -174,10 +175,17 @@ def encode_flac(filename, pcmreader, block_size, max_lpc_order,
             pcm = np.concatenate(seg)
             if bps <= 16:
                 pcm = pcm.astype(np.int16)
-            # the engine comes up with the first frames: reader errors and
-            # type errors surface first, as in the reference's frame loop
-            data, fbytes = _atgpu.engine().encode_frames(opts, pcm, channels, bps, rate,
-                                                         state["frame"], sizes)
+            # the segment's MD5 bytes hash on a thread while the GPU encodes
+            # them (hashlib and the ctypes call both release the GIL)
+            hasher = threading.Thread(target=md5.update, args=(pcm_le_bytes(pcm, bps),))
+            hasher.start()
+            try:
+                # the engine comes up with the first frames: reader errors and
+                # type errors surface first, as in the reference's frame loop
+                data, fbytes = _atgpu.engine().encode_frames(opts, pcm, channels, bps, rate,
+                                                             state["frame"], sizes)
+            finally:
+                hasher.join()
             f.write(memoryview(data))
             for nb, n in zip(fbytes, sizes):
                 offsets.append((state["offset"], n))
@@ -195,7 +203,6 @@ def encode_flac(filename, pcmreader, block_size, max_lpc_order,
                 break
             if fl.channels != channels:
                 raise ValueError("FrameList channel count does not match pcmreader")
-            md5.update(pcm_le_bytes(fl.samples, bps))
             seg.append(fl.samples)
             sizes.append(fl.frames)
             state["total"] += fl.frames

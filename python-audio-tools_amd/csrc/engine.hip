@@ -856,6 +856,35 @@ atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *t
     return ATG_OK;
 }
 
+// Streams are created on first use: a process that only streams segments
+// (atg_flac_encode_frames, one slot) holds s_main and one aux stream, not
+// six streams -- under track2track many such processes share one GPU, and
+// with every process at GPU_MAX_HW_QUEUES hardware queues the device's
+// queue slots are oversubscribed and time-sliced.
+atg_status ensure_aux_stream(EncSlot &sl)
+{
+    if (sl.s_aux)
+        return ATG_OK;
+#if ATG_AUX_HIPRIO
+    // the MD5 / header streams at the highest stream priority
+    int prio_lo = 0, prio_hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIP_TRY(hipStreamCreateWithPriority(&sl.s_aux, hipStreamNonBlocking, prio_hi));
+#else
+    HIP_TRY(hipStreamCreateWithFlags(&sl.s_aux, hipStreamNonBlocking));
+#endif
+    return ATG_OK;
+}
+
+atg_status ensure_host_streams(atg_engine *e)
+{
+    if (!e->s_h2d)
+        HIP_TRY(hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking));
+    if (!e->s_d2h)
+        HIP_TRY(hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking));
+    return ATG_OK;
+}
+
 // the slot for a new batch: the one after the last ticket's.  A slot still
 // holding an unwaited batch is never reused (its results would be lost):
 // the caller must wait the oldest ticket first, as with the decoder
@@ -864,6 +893,9 @@ atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
     EncSlot &sl = e->slot[e->next_ticket % kEncSlots];
     if (sl.busy)
         return fail(ATG_ERR_INVALID, "three encode batches already in flight: wait for the oldest");
+    atg_status st = ensure_aux_stream(sl);
+    if (st != ATG_OK)
+        return st;
     ticket = e->next_ticket++;
     sl.ticket = ticket;
     sl.done = false;
@@ -1051,6 +1083,11 @@ atg_status host_drain(atg_engine *e, atg_status err)
 atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_options *opts)
 {
     (void)opts;
+    {
+        const atg_status st = ensure_host_streams(e);
+        if (st != ATG_OK)
+            return st;
+    }
     if (e->hflight.size() >= kEncSlots) {
         atg_status st = host_collect(e);
         if (st != ATG_OK)
@@ -1122,22 +1159,12 @@ atg_status atg_engine_create(int device, atg_engine **out)
     e->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
     for (EncSlot &sl : e->slot) {
-#if ATG_AUX_HIPRIO
-        // the MD5 / header streams at the highest stream priority
-        int prio_lo = 0, prio_hi = 0;
-        HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
-        HIP_TRY(hipStreamCreateWithPriority(&sl.s_aux, hipStreamNonBlocking, prio_hi));
-#else
-        HIP_TRY(hipStreamCreateWithFlags(&sl.s_aux, hipStreamNonBlocking));
-#endif
         for (auto &ev : sl.ev)
             HIP_TRY(hipEventCreate(&ev));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_tables, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_pack, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
     }
-    HIP_TRY(hipStreamCreateWithFlags(&e->s_h2d, hipStreamNonBlocking));
-    HIP_TRY(hipStreamCreateWithFlags(&e->s_d2h, hipStreamNonBlocking));
     for (HostStage &h : e->hs) {
         HIP_TRY(hipEventCreateWithFlags(&h.ev_h2d, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&h.ev_packed, hipEventDisableTiming));
@@ -1158,7 +1185,8 @@ void atg_engine_destroy(atg_engine *e)
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->s_main);
     for (EncSlot &sl : e->slot) {
-        (void)hipStreamSynchronize(sl.s_aux);
+        if (sl.s_aux)
+            (void)hipStreamSynchronize(sl.s_aux);
         for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
                           &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch})
             b->release();
@@ -1173,10 +1201,12 @@ void atg_engine_destroy(atg_engine *e)
             (void)hipHostFree(sl.fdesc_h);
         if (sl.err_h)
             (void)hipHostFree(sl.err_h);
-        (void)hipStreamDestroy(sl.s_aux);
+        if (sl.s_aux)
+            (void)hipStreamDestroy(sl.s_aux);
     }
-    (void)hipStreamSynchronize(e->s_h2d);
-    (void)hipStreamSynchronize(e->s_d2h);
+    for (hipStream_t q : {e->s_h2d, e->s_d2h})
+        if (q)
+            (void)hipStreamSynchronize(q);
     for (HostStage &h : e->hs) {
         for (DevBuf *b : {&h.d_pcm, &h.d_img, &h.d_pack, &h.d_off})
             b->release();
@@ -1187,8 +1217,9 @@ void atg_engine_destroy(atg_engine *e)
         (void)hipEventDestroy(h.ev_packed);
         (void)hipEventDestroy(h.ev_d2h);
     }
-    (void)hipStreamDestroy(e->s_h2d);
-    (void)hipStreamDestroy(e->s_d2h);
+    for (hipStream_t q : {e->s_h2d, e->s_d2h})
+        if (q)
+            (void)hipStreamDestroy(q);
     e->windows.release();
     (void)hipStreamDestroy(e->s_main);
     delete e;
@@ -1498,6 +1529,9 @@ atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, c
     HIP_TRY(hipStreamWaitEvent(e->s_main, h.ev_packed, 0));
     if (in_bytes)
         HIP_TRY(hipMemcpyAsync(h.d_pcm.p, pcm, in_bytes, hipMemcpyHostToDevice, e->s_main));
+    // a synchronous segment (no slot busy, checked above) always takes slot
+    // 0: one aux stream for a streaming process's whole life
+    e->next_ticket += (kEncSlots - e->next_ticket % kEncSlots) % kEncSlots;
     EncSlot *sl = nullptr;
     uint64_t ticket = 0;
     st = take_slot(e, sl, ticket);

@@ -17,12 +17,13 @@ def worker(list_file, out_dir, go):
     _atgpu.load_library()
     eng = _atgpu.engine()
     orig = eng.encode_frames
-    acc = {"eng": 0.0, "calls": 0}
+    acc = {"eng": 0.0, "calls": 0, "each_ms": []}
 
     def timed(*a, **k):
         t = time.perf_counter()
         r = orig(*a, **k)
         acc["eng"] += time.perf_counter() - t
+        acc["each_ms"].append(round(1e3 * (time.perf_counter() - t), 2))
         acc["calls"] += 1
         return r
     eng.encode_frames = timed
@@ -36,7 +37,8 @@ def worker(list_file, out_dir, go):
         out = os.path.join(out_dir, os.path.basename(fn)[:-4] + ".flac")
         frames += len(encoders.encode_flac(out, audiotools.BufferedPCMReader(wav.WaveReader(fn)),
                                            **FLAC8))
-    print(json.dumps({"frames": frames, "seconds": time.perf_counter() - t0, **acc}), flush=True)
+    print(json.dumps({"frames": frames, "seconds": time.perf_counter() - t0, **acc,
+                      "kernel_ms": eng.kernel_times()}), flush=True)
 
 
 def main():
@@ -79,7 +81,9 @@ def main():
                           "eng_ms_per_call": round(1e3 * sum(s["eng"] for s in st) /
                                                    sum(s["calls"] for s in st), 2),
                           "other_ms_per_track": round(1e3 * sum(s["seconds"] - s["eng"] for s in st)
-                                                      / tracks, 2)}), flush=True)
+                                                      / tracks, 2),
+                          "last_call_kernel_ms": st[0]["kernel_ms"],
+                          "worker0_calls_ms": st[0]["each_ms"]}), flush=True)
 
 
 if __name__ == "__main__":
