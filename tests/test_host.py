@@ -134,3 +134,44 @@ def test_batch_requires_matching_formats(tmp_path):
     with pytest.raises(ValueError):
         encoders.encode_flac_batch([str(tmp_path / "a"), str(tmp_path / "b")], [a, b],
                                    4096, 12, 0, 6)
+
+
+class _SegmentEngine(object):
+    """stands in for the GPU engine: records the segments encode_flac hands
+    over and returns one 10-byte frame per PCM frame list"""
+
+    def __init__(self):
+        self.calls = []
+
+    def encode_frames(self, opts, pcm_, channels, bps, rate, first, sizes):
+        self.calls.append((pcm_.copy(), first, list(sizes)))
+        return np.zeros(10 * len(sizes), np.uint8), np.full(len(sizes), 10, np.uint32)
+
+
+@pytest.mark.parametrize("bps", [8, 16, 24])
+def test_encode_flac_streaming_segments_and_md5(tmp_path, monkeypatch, bps):
+    """the streaming path (flac.c:244-274): SEGMENT_FRAMES frames per engine
+    call, numbered on, in order; STREAMINFO's MD5 is the MD5 of the whole
+    stream's little-endian sample bytes (hashed per segment on a thread)"""
+    import hashlib
+    from audiotools import _atgpu
+    eng = _SegmentEngine()
+    monkeypatch.setattr(_atgpu, "engine", lambda: eng)
+    rng = np.random.default_rng(bps)
+    n = 2 * (2 * encoders.SEGMENT_FRAMES * 256 + 1000)  # two full segments + a tail
+    lim = 1 << (bps - 1)
+    samples = rng.integers(-lim, lim, n).astype(np.int32)
+    r = audiotools.BufferedPCMReader(audiotools.FrameListReader(samples, 44100, 2, bps))
+    out = tmp_path / "s.flac"
+    offs = encoders.encode_flac(str(out), r, 256, 8, 0, 5)
+    nfr = (n // 2 + 255) // 256
+    assert len(offs) == nfr
+    assert [c[1] for c in eng.calls] == [0, encoders.SEGMENT_FRAMES, 2 * encoders.SEGMENT_FRAMES]
+    got = np.concatenate([c[0].astype(np.int32) for c in eng.calls])
+    assert np.array_equal(got, samples)
+    data = out.read_bytes()
+    assert data[:4] == b"fLaC"
+    md5 = hashlib.md5(pcm.FrameList._wrap(samples, 2, bps).to_bytes(False, True)).digest()
+    assert data[26:42] == md5
+    # frame byte offsets follow the stream header, 10 bytes apart
+    assert [o[0] for o in offs[:3]] == [0, 10, 20]
