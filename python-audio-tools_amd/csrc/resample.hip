@@ -30,6 +30,7 @@
 //                   order, contraction off), scale, float, then
 //                   (int)(f * 2^(bps-1)) clamped -- fb_export_frames.
 #include <hip/hip_runtime.h>
+#include <type_traits>
 
 #include <algorithm>
 #include <numeric>
@@ -406,6 +407,15 @@ __global__ __launch_bounds__(64) void k_rs_phase_tab(const RsTrack *__restrict__
                   tb + kTabHdr + (uint64_t)M * wmax);
 }
 
+// k_rs_phase's input window in LDS: floats (converted per tap) or, with
+// ATG_RS_PXD=1, the same values widened to double once at staging (twice
+// the LDS, no v_cvt_f64_f32 in the tap loop)
+#ifndef ATG_RS_PXD
+#define ATG_RS_PXD 0
+#endif
+typedef std::conditional_t<ATG_RS_PXD != 0, double, float> PhaseX;
+constexpr size_t kPhaseXBytes = sizeof(PhaseX);
+
 // The phase-sharing filter.  The output positions of a rational ratio
 // repeat their fractional part every `period` = out_rate / gcd outputs, so
 // outputs n, n + period, n + 2 period, ... have the same start filter index
@@ -443,7 +453,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
     double *cL = lds_d + (size_t)wave * 2 * M * wmax; // [wmax][M] left, then right
     double *cR = cL + (size_t)M * wmax;
-    float *X = reinterpret_cast<float *>(lds_d + (size_t)nwaves * 2 * M * wmax);
+    PhaseX *X = reinterpret_cast<PhaseX *>(lds_d + (size_t)nwaves * 2 * M * wmax);
     const float *Cg = reinterpret_cast<const float *>(table_bits);
     const int32_t max_fi = SRC_MEDIUM_HALF_LEN << kShift;
     for (uint32_t task = blockIdx.x; task < n_tasks; task += gridDim.x) {
@@ -479,7 +489,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
             for (uint32_t b = 0; b < kStage; ++b) {
                 const uint32_t i = i0 + b * blockDim.x;
                 if (i < nx)
-                    X[i] = (float)v[b] * P.inv_q;
+                    X[i] = (PhaseX)((float)v[b] * P.inv_q);
             }
         }
         __syncthreads();
@@ -562,7 +572,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                     WR = q.sr1 - q.sr0 + 1;
                 }
                 wave_lds_sync();
-                const float *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
+                const PhaseX *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
 #pragma unroll 2
                 for (int32_t k = 0; k < WL; ++k) {
                     double x[CH];
@@ -578,7 +588,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                             left[m][q] = left[m][q] + ic[m] * x[q];
                     }
                 }
-                const float *xr = X + (int64_t)(c[0] + sr1 - w0) * CH;
+                const PhaseX *xr = X + (int64_t)(c[0] + sr1 - w0) * CH;
 #pragma unroll 2
                 for (int32_t k = 0; k < WR; ++k) {
                     double x[CH];
@@ -1066,7 +1076,7 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             for (uint64_t R = 1; R <= 64; R *= 2) {
                 const size_t win =
                     (size_t)(64 * (L / p_out) * q_in * R + 2 * reach + 8 + (pm - 1) * step + 2) *
-                    channels * 4;
+                    channels * kPhaseXBytes;
                 if (coef + win > kLds)
                     break;
                 r = R;
@@ -1173,7 +1183,7 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             lds_phase = std::max(lds_phase, waves * 2 * pm * wmax * sizeof(double) +
                                                 (size_t)(64 * (lspan[t] / per[t]) * (a.in_rate / g) *
                                                          rows[t] + 2 * reach + 8 + T.wext) *
-                                                    channels * 4);
+                                                    channels * kPhaseXBytes);
         } else {
             for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
                 chunk_track.push_back(t);
