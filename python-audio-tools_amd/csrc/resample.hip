@@ -571,6 +571,10 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                     WL = q.sl1 - q.sl0 + 1;
                     WR = q.sr1 - q.sr0 + 1;
                 }
+                // wave-uniform by construction (the table header, or the
+                // geometry of lane 0's phases): scalar loop control
+                WL = __builtin_amdgcn_readfirstlane(WL);
+                WR = __builtin_amdgcn_readfirstlane(WR);
                 wave_lds_sync();
                 const PhaseX *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
 #pragma unroll 2
