@@ -943,9 +943,12 @@ def t2t_leg(args, pcm_host, n_samples, threads):
             lf = os.path.join(d, "list%d" % k)
             with open(lf, "w") as f:
                 f.write("\n".join(files[k::procs]))
+            # one engine per process, streams created on first use (the
+            # many-processes-per-GPU setting)
             workers.append(subprocess.Popen(
                 [sys.executable, os.path.abspath(__file__), "--t2t-worker", lf, gdir, go],
-                stdout=subprocess.PIPE, text=True))
+                stdout=subprocess.PIPE, text=True,
+                env=dict(os.environ, ATG_ENGINE_STREAMS="lazy")))
         for w in workers:
             json.loads(w.stdout.readline())  # ready
         t0 = time.perf_counter()
@@ -956,7 +959,7 @@ def t2t_leg(args, pcm_host, n_samples, threads):
             raise RuntimeError("a track2track worker failed")
         frames = sum(st["frames"] for st in stats)
         out.update({"value": round(frames / wall, 1), "unit": "frames/s",
-                    "processes": procs, "tracks": n_tracks, "frames": frames,
+                    "processes": procs, "engine_streams": "lazy", "tracks": n_tracks, "frames": frames,
                     "wall_s": round(wall, 3),
                     "per_process_frames_per_s": round(frames / procs / wall, 1)})
         # the reference encoder, one process per track, the same count at a time

@@ -168,6 +168,7 @@ struct EncSlot {
 #define ATG_AUX_HIPRIO 1
 #endif
 
+
 // batches in flight on an engine (each its own device workspace): the MD5
 // chains of a batch run ~12 ms, longer than a batch's search chain, so a
 // third slot keeps them off the critical path at normal wave priority
@@ -856,11 +857,12 @@ atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *t
     return ATG_OK;
 }
 
-// Streams are created on first use: a process that only streams segments
-// (atg_flac_encode_frames, one slot) holds s_main and one aux stream, not
-// six streams -- under track2track many such processes share one GPU, and
-// with every process at GPU_MAX_HW_QUEUES hardware queues the device's
-// queue slots are oversubscribed and time-sliced.
+// With ATG_ENGINE_STREAMS=lazy streams are created on first use: a process
+// that only streams segments (atg_flac_encode_frames, one slot) holds
+// s_main and one aux stream, not six -- under track2track many such
+// processes share one GPU, and with every process at GPU_MAX_HW_QUEUES
+// hardware queues the device's queue slots are oversubscribed and
+// time-sliced.
 atg_status ensure_aux_stream(EncSlot &sl)
 {
     if (sl.s_aux)
@@ -1158,6 +1160,20 @@ atg_status atg_engine_create(int device, atg_engine **out)
     atg_engine *e = new atg_engine();
     e->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
+    // every stream now, in this order, unless ATG_ENGINE_STREAMS=lazy: the
+    // order fixes the streams' hardware queues, and the device-resident
+    // step is 9.4 ms with it against 10.3 ms with streams created on first
+    // use (profiles/r03_l_streams_ab.txt).  "lazy" is for many processes
+    // per GPU (track2track): a streaming process then holds two streams
+    // and 8 processes run 49.8 k frames/s against 17.6 k
+    const char *mode = getenv("ATG_ENGINE_STREAMS");
+    if (!(mode && strcmp(mode, "lazy") == 0)) {
+        for (EncSlot &sl : e->slot)
+            if (ensure_aux_stream(sl) != ATG_OK)
+                return ATG_ERR_DEVICE;
+        if (ensure_host_streams(e) != ATG_OK)
+            return ATG_ERR_DEVICE;
+    }
     for (EncSlot &sl : e->slot) {
         for (auto &ev : sl.ev)
             HIP_TRY(hipEventCreate(&ev));

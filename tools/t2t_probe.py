@@ -66,7 +66,9 @@ def main():
             lf = os.path.join(d, "l%d" % k)
             open(lf, "w").write("\n".join(files[k::procs]))
             ws.append(subprocess.Popen([sys.executable, __file__, "--worker", lf, d, go],
-                                       stdout=subprocess.PIPE, text=True))
+                                       stdout=subprocess.PIPE, text=True,
+                                       env=dict(os.environ, ATG_ENGINE_STREAMS=os.environ.get(
+                                           "ATG_ENGINE_STREAMS", "lazy"))))
         for w in ws:
             json.loads(w.stdout.readline())
         t0 = time.perf_counter()
