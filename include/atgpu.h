@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define ATG_ABI_VERSION 3
+#define ATG_ABI_VERSION 4
 
 typedef enum {
     ATG_OK = 0,
@@ -101,6 +101,16 @@ typedef struct atg_engine atg_engine;
 int atg_abi_version(void);
 const char *atg_last_error(void);
 atg_status atg_engine_create(int device, atg_engine **out);
+/* flags for atg_engine_create_ex */
+#define ATG_ENGINE_STREAMING 1u /* streams on first use: a process that only
+                                   encodes one track at a time through
+                                   atg_flac_encode_frames (encode_flac, one
+                                   process per track under track2track -j N)
+                                   then holds two HIP streams, so many such
+                                   processes fit the device's hardware queues */
+/* atg_engine_create with flags.  Without ATG_ENGINE_STREAMING every stream
+   is created at once in a fixed order (the batch APIs' queue layout). */
+atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out);
 void atg_engine_destroy(atg_engine *eng);
 
 /* Number of FLAC frames and worst-case output bytes of a batch, so callers

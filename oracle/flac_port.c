@@ -1017,12 +1017,37 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
                     uint64_t *frame_offsets, uint32_t *frame_lengths,
                     size_t max_frames, size_t *n_frames)
 {
+    return flacport_encode_sizes(pcm, pcm_frames, channels, bits_per_sample,
+                                 sample_rate, opts, NULL, 0, out, out_cap, out_len,
+                                 frame_offsets, frame_lengths, max_frames, n_frames);
+}
+
+int flacport_encode_sizes(const int32_t *pcm, uint64_t pcm_frames,
+                          uint32_t channels, uint32_t bits_per_sample,
+                          uint32_t sample_rate, const flacport_options *opts,
+                          const uint32_t *read_sizes, size_t n_read_sizes,
+                          uint8_t *out, size_t out_cap, size_t *out_len,
+                          uint64_t *frame_offsets, uint32_t *frame_lengths,
+                          size_t max_frames, size_t *n_frames)
+{
     crc_init();
     if (!opts || channels < 1 || channels > 8 || opts->block_size == 0 ||
         opts->max_lpc_order > MAX_LPC ||
         opts->max_residual_partition_order > MAX_PART_ORDER)
         return -1;
+    /* N = the block_size option: it derives qlp precision and STREAMINFO's
+       min/max block size (flac.c:164-178, 193-194).  A frame holds whatever
+       one read() returned (flac.c:244-274), so the scratch buffers are sized
+       for the largest listed read; a listed 0 is an empty read and ends the
+       stream, as the reference's `while (samples->_[0]->len > 0)`. */
     const unsigned N = opts->block_size;
+    unsigned NA = N;
+    for (size_t i = 0; i < n_read_sizes; i++) {
+        if (read_sizes[i] > 0xFFFF)
+            return -1;  /* a frame header holds at most a 16-bit size */
+        if (read_sizes[i] > NA)
+            NA = read_sizes[i];
+    }
     const size_t vlen = strlen(VENDOR_STRING);
     const size_t head = 4 + 4 + 34 + 4 + 4 + vlen + 4 + 4 + opts->padding_size;
     if (out_cap < head)
@@ -1034,18 +1059,18 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
     e.qlp_precision = N <= 192 ? 7 : N <= 384 ? 8 : N <= 576 ? 9 : N <= 1152 ? 10
                     : N <= 2304 ? 11 : N <= 4608 ? 12 : 13;
     e.max_rice = bits_per_sample <= 16 ? 14 : 30;
-    e.win = malloc(sizeof(double) * N);
-    e.xw = malloc(sizeof(double) * N);
-    e.resid = malloc(sizeof(int32_t) * (N + 1));
-    e.tmp_resid = malloc(sizeof(int32_t) * (N + 1));
-    int32_t *chan_mem = malloc(sizeof(int32_t) * N * (channels + 4));
-    int32_t *shift_mem = malloc(sizeof(int32_t) * N * 4);
+    e.win = malloc(sizeof(double) * NA);
+    e.xw = malloc(sizeof(double) * NA);
+    e.resid = malloc(sizeof(int32_t) * (NA + 1));
+    e.tmp_resid = malloc(sizeof(int32_t) * (NA + 1));
+    int32_t *chan_mem = malloc(sizeof(int32_t) * NA * (channels + 4));
+    int32_t *shift_mem = malloc(sizeof(int32_t) * NA * 4);
     subframe_plan *plans = malloc(sizeof(subframe_plan) * 4);
     int32_t *chan[12], *shifted[4];
     for (unsigned c = 0; c < channels + 4 && c < 12; c++)
-        chan[c] = chan_mem + (size_t)c * N;
+        chan[c] = chan_mem + (size_t)c * NA;
     for (unsigned c = 0; c < 4; c++)
-        shifted[c] = shift_mem + (size_t)c * N;
+        shifted[c] = shift_mem + (size_t)c * NA;
 
     /* stream header: fLaC, STREAMINFO, VORBIS_COMMENT, PADDING
        (flac.c:208-238) */
@@ -1081,7 +1106,10 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
     md5_state md5;
     md5_begin(&md5);
     while (done < pcm_frames) {
-        unsigned n = (pcm_frames - done) < N ? (unsigned)(pcm_frames - done) : N;
+        unsigned want = nf < n_read_sizes ? read_sizes[nf] : N;
+        if (want == 0)
+            break;
+        unsigned n = (pcm_frames - done) < want ? (unsigned)(pcm_frames - done) : want;
         const int32_t *fp = pcm + done * channels;
         md5_pcm(&md5, fp, (size_t)n * channels, bits_per_sample);
         uint64_t off = w.pos >> 3;
@@ -1107,7 +1135,7 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
     uint8_t digest[16];
     md5_end(&md5, digest);
     write_streaminfo(streaminfo, N, min_fs, max_fs, sample_rate, channels,
-                     bits_per_sample, pcm_frames, digest);
+                     bits_per_sample, done, digest);
     if (out_len)
         *out_len = (size_t)(p - out) + (size_t)(w.pos >> 3);
     if (n_frames)

@@ -50,6 +50,20 @@ int flacport_encode(const int32_t *pcm, uint64_t pcm_frames,
                     uint64_t *frame_offsets, uint32_t *frame_lengths,
                     size_t max_frames, size_t *n_frames);
 
+/* flacport_encode with the frame cut of a reader whose i-th read() returned
+   read_sizes[i] frames (then block_size frames per read): each read is one
+   frame (reference src/encoders/flac.c:244-274), a size other than the
+   preset's block sizes takes block-size code 0x6/0x7 + an explicit size
+   (flac.c:412-518), STREAMINFO's min/max block size stay the option
+   (flac.c:193-194).  A listed 0 ends the stream there. */
+int flacport_encode_sizes(const int32_t *pcm, uint64_t pcm_frames,
+                          uint32_t channels, uint32_t bits_per_sample,
+                          uint32_t sample_rate, const flacport_options *opts,
+                          const uint32_t *read_sizes, size_t n_read_sizes,
+                          uint8_t *out, size_t out_cap, size_t *out_len,
+                          uint64_t *frame_offsets, uint32_t *frame_lengths,
+                          size_t max_frames, size_t *n_frames);
+
 /* Worst-case output size for flacport_encode / the GPU engine. */
 size_t flacport_max_stream_bytes(uint64_t pcm_frames, uint32_t channels,
                                  uint32_t bits_per_sample, uint32_t block_size,

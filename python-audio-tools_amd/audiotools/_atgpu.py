@@ -28,7 +28,7 @@ PCM_S32 = 1
 
 # every function include/atgpu.h declares (tests check the .so exports them)
 EXPORTS = (
-    "atg_abi_version", "atg_last_error", "atg_engine_create",
+    "atg_abi_version", "atg_last_error", "atg_engine_create", "atg_engine_create_ex",
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_host_async", "atg_flac_encode_host_wait",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
@@ -239,6 +239,8 @@ def load_library():
         lib.atg_last_error.restype = ctypes.c_char_p
         lib.atg_engine_create.argtypes = [ctypes.c_int, ctypes.POINTER(P)]
         lib.atg_engine_create.restype = ctypes.c_int
+        lib.atg_engine_create_ex.argtypes = [ctypes.c_int, c_u32, ctypes.POINTER(P)]
+        lib.atg_engine_create_ex.restype = ctypes.c_int
         lib.atg_engine_destroy.argtypes = [P]
         lib.atg_engine_destroy.restype = None
         lib.atg_flac_batch_bounds.argtypes = [
@@ -459,36 +461,65 @@ class TrackTable(object):
 
 
 class HostJob:
-    """a queued host-memory encode (Engine.encode_async)"""
+    """a queued host-memory encode (Engine.encode_async).
+
+    The engine DMAs into the job's pcm / out / result arrays until the job is
+    waited, so the arrays are held by the Engine (not only by this object)
+    until then, and a job dropped unwaited -- an exception between submit and
+    wait, a discarded result -- is waited by its finalizer."""
 
     def __init__(self, engine, ticket, keep, n, nf):
-        self.engine, self.ticket, self._keep, self.n, self.nf = engine, ticket, keep, n, nf
+        self.engine, self.ticket, self.n, self.nf = engine, ticket, n, nf
+        engine._inflight[ticket] = keep
         self._done = None
 
     def wait(self):
         if self._done is None:
-            _check(self.engine.lib, self.engine.lib.atg_flac_encode_host_wait(
-                self.engine.handle, self.ticket))
-            _pcm, out, res, offs, fpcm, _arr, _k = self._keep
+            keep = self.engine._inflight.get(self.ticket)
+            if keep is None:
+                raise ATGError(ATG_ERR_INVALID, "host job already waited or its engine closed")
+            try:
+                _check(self.engine.lib, self.engine.lib.atg_flac_encode_host_wait(
+                    self.engine.handle, self.ticket))
+            finally:
+                del self.engine._inflight[self.ticket]
+            _pcm, out, res, offs, fpcm, _arr, _k = keep
             self._done = (out, [res[i] for i in range(self.n)], offs[:self.nf], fpcm[:self.nf])
-            self._keep = (out, res, offs, fpcm)
         return self._done
+
+    def __del__(self):
+        if self._done is None:
+            try:
+                if self.engine.handle and self.ticket in self.engine._inflight:
+                    self.wait()
+            except Exception:
+                pass
+
+
+ENGINE_STREAMING = 1  # atg_engine_create_ex flag (include/atgpu.h)
 
 
 class Engine(object):
-    """one libatgpu engine (two HIP streams + workspace) on one device"""
+    """one libatgpu engine (streams + workspace) on one device; streaming=True
+    for a process that encodes one track at a time (streams on first use,
+    ATG_ENGINE_STREAMING)"""
 
-    def __init__(self, device=0):
+    def __init__(self, device=0, streaming=False):
         self.lib = load_library()
         self.device = device
+        self._inflight = {}  # host-job ticket -> the arrays the engine writes
         h = ctypes.c_void_p()
-        _check(self.lib, self.lib.atg_engine_create(int(device), ctypes.byref(h)))
+        _check(self.lib, self.lib.atg_engine_create_ex(
+            int(device), ENGINE_STREAMING if streaming else 0, ctypes.byref(h)))
         self.handle = h
 
     def close(self):
         if self.handle:
+            # atg_engine_destroy drains the device; the arrays of unwaited host
+            # jobs are released only after it
             self.lib.atg_engine_destroy(self.handle)
             self.handle = None
+            self._inflight.clear()
 
     def __del__(self):
         try:

@@ -1,11 +1,13 @@
 """audiotools.decoders — FLAC decoding on the MI355X.
 
-`FlacDecoder` keeps the Python-visible contract of the reference's C type
-audiotools.decoders.FlacDecoder (src/decoders/flac.c, methods :145-166):
+`FlacDecoder` IS the compiled C-API type `audiotools._decoders_c.FlacDecoder`
+(csrc/ext/decoders_c.c over libatgpu's C ABI), with the Python-visible
+contract of the reference's C type audiotools.decoders.FlacDecoder
+(src/decoders/flac.c, methods :145-166):
 
-  FlacDecoder(file)        file object (or filename) positioned at "fLaC";
-                           ValueError / IOError from the metadata reader
-                           (flacdec_read_metadata, flac.c:568-707)
+  FlacDecoder(file)        file object, filename or bytes positioned at
+                           "fLaC"; ValueError / IOError from the metadata
+                           reader (flacdec_read_metadata, flac.c:568-707)
   .sample_rate .bits_per_sample .channels .channel_mask
   .read(n)                 one FLAC frame per call as a pcm.FrameList; an
                            empty FrameList once the stream is done, after
@@ -20,9 +22,9 @@ audiotools.decoders.FlacDecoder (src/decoders/flac.c, methods :145-166):
   .close()                 further reads raise ValueError
 
 The stream is decoded by libatgpu (HIP kernels, flac_decode.hip) in bounded
-segments as read() needs them (SEGMENT_BYTES of compressed data per GPU
-call, the MD5 chained on the host); read() hands out the decoded frames in
-order and raises the decode status at the frame where the reference would.
+segments as read() needs them (8 MiB of compressed data per GPU call, the
+MD5 chained on the host); read() hands out the decoded frames in order and
+raises the decode status at the frame where the reference would.
 `decode_flac_batch` is the batch entry trackverify-style callers use.
 `ALACDecoder` / `decode_alac_batch` do the same for ALAC in M4A
 (reference src/decoders/alac.c; GPU kernels alac_decode.hip).
@@ -35,18 +37,9 @@ import numpy as np
 
 from . import _atgpu
 from . import pcm
-
-
-def _read_all(file):
-    """-> (bytes, seekable): filenames and file objects can seek, raw bytes
-    cannot (the reference seeks only streams from file objects,
-    flac.c:298-307)"""
-    if isinstance(file, str):
-        with open(file, "rb") as f:
-            return f.read(), True
-    if isinstance(file, (bytes, bytearray, memoryview)):
-        return bytes(file), False
-    return file.read(), True
+# the drop-in decoder type: the compiled C-API FlacDecoder
+# (csrc/ext/decoders_c.c over libatgpu), as the reference's is its C type
+from ._decoders_c import FlacDecoder  # noqa: F401
 
 
 def _metadata_error(rc):
@@ -55,197 +48,6 @@ def _metadata_error(rc):
     return IOError("EOF while reading metadata")
 
 
-def _status_error(status):
-    if status == _atgpu.FD_EOF:
-        return IOError(_atgpu.FD_MESSAGES[_atgpu.FD_EOF])
-    return ValueError(_atgpu.FD_MESSAGES.get(status, "Error"))
-
-
-# compressed bytes per GPU decode call of a streaming FlacDecoder: bounds
-# the decoded PCM held in host memory (int32 samples: about 4x this for
-# 16-bit audio) whatever the stream's length
-SEGMENT_BYTES = 8 << 20
-
-
-def _frame_bytes(samples, bits_per_sample):
-    """FrameList.to_bytes(False, True) of int32 samples: little-endian,
-    saturated to the bps range (src/pcm.c:1826-1948)"""
-    bb = (bits_per_sample + 7) // 8
-    hi = (1 << (bits_per_sample - 1)) - 1
-    a = np.clip(np.asarray(samples, dtype=np.int64), -hi - 1, hi).astype("<i4")
-    return a.view(np.uint8).reshape(-1, 4)[:, :bb].tobytes()
-
-
-class FlacDecoder(object):
-    """reference src/decoders/flac.c FlacDecoder, decoded on the GPU in
-    bounded segments: each GPU call decodes the frames of SEGMENT_BYTES of
-    compressed data (a window that ends inside a frame resumes at that
-    frame, whose byte position the decode reports as walk_end; an error is
-    raised only when the frame that stops a walk is the first of its window,
-    so it cannot be the window's cut), and the STREAMINFO MD5 runs over the
-    handed-out PCM on the host, chained across segments"""
-
-    def __init__(self, file):
-        data, self._seekable = _read_all(file)
-        rc, si, points = _atgpu.read_metadata(data)
-        if rc:
-            raise _metadata_error(rc)
-        self._data = data
-        self._si = si
-        self._seekpoints = points
-        self.sample_rate = si.sample_rate
-        self.bits_per_sample = si.bits_per_sample
-        self.channels = si.channels
-        self.channel_mask = si.channel_mask
-        self._closed = False
-        # the bitstream position: byte offset from the first frame and
-        # remaining_samples there; MD5 validation only from sample 0
-        # (FlacDecoder_seek, flac.c:317-352)
-        self._start_byte = 0
-        self._remaining = si.total_samples
-        self._validate = True
-        self._reset()
-
-    def _reset(self):
-        self._finalized = False
-        self._seg_byte = self._start_byte      # next window's first byte
-        self._seg_remaining = self._remaining  # remaining_samples there
-        self._seg = None                       # (pcm, frame starts, byte offsets)
-        self._seg_n = 0
-        self._next = 0
-        self._stop = None                      # status after the current segment
-        # FlacDecoder_verify_okay (flac.c:479-493): a blank MD5 always passes
-        self._md5 = hashlib.md5() if self._validate and any(self._si.md5) else None
-
-    def _body(self):
-        return memoryview(self._data)[self._si.frames_offset:]
-
-    def _decode_segment(self):
-        body = self._body()
-        start, rem = self._seg_byte, self._seg_remaining
-        win = SEGMENT_BYTES
-        while True:
-            end = min(start + win, len(body))
-            final = end >= len(body)
-            chunk = bytes(body[start:end])
-            track = _atgpu.dec_track(0, len(chunk), self._si)
-            track.total_samples = rem
-            track.md5[:] = bytes(16)  # the MD5 is chained on the host
-            pcm_i32, res, offs, bss = _atgpu.decoder().decode(
-                chunk + b"\0" * ((-len(chunk)) % 4), [track])
-            r = res[0]
-            if r.status == _atgpu.FD_OK or final or r.n_frames > 0 or \
-                    r.status == _atgpu.FD_FRAME_CRC:
-                break
-            win *= 4  # the window's first frame may be longer than the window
-        n, ch = r.n_frames, self.channels
-        lens, rems = [], []
-        for bs in bss[r.first_frame:r.first_frame + n]:
-            rems.append(rem)
-            lens.append(min(int(bs), rem))
-            rem = (rem - int(bs)) % (1 << 64)
-        self._seg_rems = rems
-        # where the frame after these n sits (offsets() resumes there)
-        self._after = (start + (int(offs[r.first_frame + n]) if r.walk_frames > n
-                                else int(r.walk_end)), rem)
-        starts = np.concatenate([[0], np.cumsum(lens, dtype=np.int64)]) if lens \
-            else np.zeros(1, dtype=np.int64)
-        pcm_seg = pcm_i32[r.pcm_offset * ch:(r.pcm_offset + int(starts[-1])) * ch]
-        self._seg = (pcm_seg, starts, [start + int(o) for o in
-                                       offs[r.first_frame:r.first_frame + n]])
-        self._seg_n = n
-        self._next = 0
-        if r.status == _atgpu.FD_OK:
-            self._stop = _atgpu.FD_OK          # remaining_samples reached 0
-        elif final or n == 0 or r.status == _atgpu.FD_FRAME_CRC:
-            self._stop = r.status              # a real error at frame n
-        else:                                  # the window's cut: resume there
-            self._stop = None
-            self._seg_byte = start + int(r.walk_end)
-            self._seg_remaining = rem
-
-    def read(self, pcm_frames):
-        """one FLAC frame per call (flac.c:174-285)"""
-        if self._closed:
-            raise ValueError("cannot read closed stream")
-        if self._finalized:
-            return pcm.empty_framelist(self.channels, self.bits_per_sample)
-        while self._seg is None or self._next >= self._seg_n:
-            if self._seg is not None and self._stop is not None:
-                # every good frame handed out: the stream either reached
-                # remaining_samples == 0 (MD5 verdict) or stops on an error
-                if self._stop == _atgpu.FD_OK:
-                    self._finalized = True
-                    if self._md5 is not None and self._md5.digest() != bytes(self._si.md5):
-                        raise ValueError(_atgpu.FD_MESSAGES[_atgpu.FD_MD5])
-                    return pcm.empty_framelist(self.channels, self.bits_per_sample)
-                raise _status_error(self._stop)
-            self._decode_segment()
-        pcm_seg, starts, _ = self._seg
-        k = self._next
-        self._next += 1
-        a = int(starts[k]) * self.channels
-        b = int(starts[k + 1]) * self.channels
-        frame = pcm_seg[a:b].copy()
-        if self._md5 is not None:
-            self._md5.update(_frame_bytes(frame, self.bits_per_sample))
-        return pcm.FrameList._wrap(frame, self.channels, self.bits_per_sample)
-
-    def seek(self, pcm_frame_offset):
-        """position at the last SEEKTABLE point at or before
-        pcm_frame_offset (sample 0 without one) and return its sample
-        number (FlacDecoder_seek, flac.c:287-356); reads then continue from
-        that frame, with MD5 validation only when it is sample 0"""
-        if self._closed:
-            raise ValueError("cannot seek closed stream")
-        if not self._seekable:
-            raise TypeError("can only seek streams from file objects")
-        pcm_frame_offset = int(pcm_frame_offset)
-        if pcm_frame_offset < 0:
-            raise ValueError("cannot seek to negative value")
-        sample, byte = 0, 0
-        for (sample_number, byte_offset, _samples) in self._seekpoints:
-            if sample_number <= pcm_frame_offset:
-                sample, byte = sample_number, byte_offset
-            else:
-                break
-        self._start_byte = int(byte)
-        self._remaining = (self._si.total_samples - sample) % (1 << 64)
-        self._validate = sample == 0
-        self._reset()
-        return sample
-
-    def offsets(self):
-        """[(byte offset from the current position, block size)] of every
-        frame from the current position to the end, CRC-16 unchecked; the
-        stream is then finished (flac.c:365-443)"""
-        # the current position: the next frame read() would hand out
-        if self._seg is not None and self._next < self._seg_n:
-            pos, rem = self._seg[2][self._next], self._seg_rems[self._next]
-        elif self._seg is not None and self._stop == _atgpu.FD_OK:
-            self._finalized = True
-            return []  # remaining_samples already 0
-        elif self._seg is not None:
-            pos, rem = self._after  # the next window, or the frame that failed
-        else:
-            pos, rem = self._seg_byte, self._seg_remaining
-        body = self._body()
-        chunk = bytes(body[pos:])
-        track = _atgpu.dec_track(0, len(chunk), self._si)
-        track.total_samples = rem
-        track.md5[:] = bytes(16)
-        _, res, offs, bss = _atgpu.decoder().decode(chunk + b"\0" * ((-len(chunk)) % 4),
-                                                    [track], fetch_pcm=False)
-        r = res[0]
-        if r.walk_status != _atgpu.FD_OK:
-            raise _status_error(r.walk_status)
-        self._finalized = True
-        return [(int(o), int(b)) for o, b in
-                zip(offs[r.first_frame:r.first_frame + r.walk_frames],
-                    bss[r.first_frame:r.first_frame + r.walk_frames])]
-
-    def close(self):
-        self._closed = True
 
 
 def decode_flac_batch(images):

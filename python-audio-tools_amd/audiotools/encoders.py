@@ -1,7 +1,9 @@
-"""audiotools.encoders — FLAC encoding on the MI355X engine.
+"""audiotools.encoders — FLAC / ALAC encoding on the MI355X engine.
 
-`encode_flac` keeps the reference's Python-visible contract
-(reference src/encoders/flac.c:44-121, registered src/encoders.h:65-67):
+`encode_flac` IS the compiled C-API entry point `audiotools._encoders_c.
+encode_flac` (csrc/ext/encoders_c.c over libatgpu's C ABI), as the
+reference's module function is its C extension (src/encoders/flac.c:44-121,
+registered src/encoders.h:65-67):
 
     encode_flac(filename, pcmreader, block_size, max_lpc_order,
                 min_residual_partition_order, max_residual_partition_order,
@@ -21,12 +23,11 @@
 * on success the reader is closed (flac.c:282) and the list of
   (offset of the frame from the first frame, pcm frames) is returned.
 
-`encode_flac` streams: the PCM is pulled and encoded in bounded segments
-(SEGMENT_FRAMES FLAC frames per GPU call, atg_flac_encode_frames), the
-frames are written as they come, the MD5 of the PCM bytes is updated per
-read on the host (the reference's per-read MD5 callback, pcmconv.c:266-291)
-and STREAMINFO is rewritten at the end (flac.c:276-279) -- so an hour of
-192 kHz / 24-bit 5.1 never sits in host memory whole.
+It streams: up to 256 FLAC frames per GPU call (atg_flac_encode_frames) with
+the GIL released, the MD5 of each segment's PCM bytes on a host thread
+beside the GPU call, STREAMINFO rewritten at the end (flac.c:276-279), on a
+streaming engine (two HIP streams per process, for one process per track
+under track2track).
 
 `encode_flac_batch` is the batch form the engine is built for: many tracks
 in one GPU pass (what track2track -j N achieves with N processes), MD5
@@ -36,17 +37,11 @@ chains on the GPU.
 src/encoders/alac.c:30-189; GPU kernels alac_encode.hip).
 """
 
-import hashlib
-import threading
-
 import numpy as np
 
 from . import pcm as _pcm
 from . import _atgpu
-
-# FLAC frames per GPU call of the streaming encoder: at block size 4096 a
-# segment holds at most 256 x 4096 x 8 channels x 4 B = 32 MB of int32 PCM
-SEGMENT_FRAMES = 256
+from ._encoders_c import encode_flac  # noqa: F401  (the drop-in entry point)
 
 
 def pcm_le_bytes(samples, bits_per_sample):
@@ -138,85 +133,6 @@ def encode_flac_batch(filenames, pcmreaders, block_size, max_lpc_order,
     finally:
         for f in files:
             f.close()
-
-
-def encode_flac(filename, pcmreader, block_size, max_lpc_order,
-                min_residual_partition_order, max_residual_partition_order,
-                mid_side=0, adaptive_mid_side=0, exhaustive_model_search=0,
-                disable_verbatim_subframes=0, disable_constant_subframes=0,
-                disable_fixed_subframes=0, disable_lpc_subframes=0,
-                padding_size=4096):
-    """encode_flac(filename, pcmreader, block_size, max_lpc_order,
-    min_residual_partition_order, max_residual_partition_order, ...)
-    -> [(byte_offset, pcm_frames), ...]
-
-    Streams: every pcmreader.read(block_size) becomes one FLAC frame
-    (flac.c:244-274); SEGMENT_FRAMES of them at a time are encoded on the
-    GPU and written out; the stream header is written first and rewritten
-    with the final STREAMINFO (size range, total, MD5) at the end."""
-    f = open(filename, "wb")
-    try:
-        opts = _atgpu.make_options(
-            block_size, max_lpc_order, min_residual_partition_order,
-            max_residual_partition_order, mid_side, adaptive_mid_side,
-            exhaustive_model_search, disable_verbatim_subframes,
-            disable_constant_subframes, disable_fixed_subframes,
-            disable_lpc_subframes, padding_size)
-        channels = pcmreader.channels
-        bps = pcmreader.bits_per_sample
-        rate = pcmreader.sample_rate
-        f.write(_atgpu.stream_header(opts, channels, bps, rate))
-        md5 = hashlib.md5()
-        state = {"offset": 0, "frame": 0, "total": 0, "min": 0xFFFFFF, "max": 0}
-        offsets = []
-        seg, sizes = [], []
-
-        def flush():
-            pcm = np.concatenate(seg)
-            if bps <= 16:
-                pcm = pcm.astype(np.int16)
-            # the segment's MD5 bytes hash on a thread while the GPU encodes
-            # them (hashlib and the ctypes call both release the GIL)
-            hasher = threading.Thread(target=md5.update, args=(pcm_le_bytes(pcm, bps),))
-            hasher.start()
-            try:
-                # the engine comes up with the first frames: reader errors and
-                # type errors surface first, as in the reference's frame loop
-                data, fbytes = _atgpu.engine().encode_frames(opts, pcm, channels, bps, rate,
-                                                             state["frame"], sizes)
-            finally:
-                hasher.join()
-            f.write(memoryview(data))
-            for nb, n in zip(fbytes, sizes):
-                offsets.append((state["offset"], n))
-                state["offset"] += int(nb)
-                state["min"] = min(state["min"], int(nb))
-                state["max"] = max(state["max"], int(nb))
-            state["frame"] += len(sizes)
-            del seg[:], sizes[:]
-
-        while True:
-            fl = pcmreader.read(block_size)
-            if not isinstance(fl, _pcm.FrameList):
-                raise TypeError("results from pcmreader.read() must be FrameLists")
-            if fl.frames == 0:
-                break
-            if fl.channels != channels:
-                raise ValueError("FrameList channel count does not match pcmreader")
-            seg.append(fl.samples)
-            sizes.append(fl.frames)
-            state["total"] += fl.frames
-            if len(sizes) >= SEGMENT_FRAMES:
-                flush()
-        if sizes:
-            flush()
-        f.seek(0)
-        f.write(_atgpu.stream_header(opts, channels, bps, rate, state["total"],
-                                     state["min"], state["max"], md5.digest()))
-    finally:
-        f.close()
-    pcmreader.close()
-    return offsets
 
 
 def encode_alac_batch(files, pcmreaders, block_size, initial_history, history_multiplier,

@@ -37,11 +37,16 @@ class _Converter(object):
     def __init__(self, pcmreader):
         self.pcmreader = pcmreader
         self.sample_rate = pcmreader.sample_rate
+        self._closed = False
 
     def close(self):
+        """closes the wrapped reader; later reads raise ValueError"""
+        self._closed = True
         self.pcmreader.close()
 
     def _input(self):
+        if self._closed:
+            raise ValueError("cannot read closed stream")
         fl = self.pcmreader.read(4096)
         if not isinstance(fl, pcm.FrameList):
             raise TypeError("pcmreader.read() must return a FrameList")
@@ -137,6 +142,7 @@ class Resampler(object):
         self.channel_mask = pcmreader.channel_mask
         self.bits_per_sample = pcmreader.bits_per_sample
         self._chunks = None
+        self._closed = False
 
     def _run(self):
         ratio = float(self.sample_rate) / float(self.pcmreader.sample_rate)
@@ -166,6 +172,8 @@ class Resampler(object):
         self._pos = 0
 
     def read(self, pcm_frames):
+        if self._closed:
+            raise ValueError("cannot read closed stream")
         if self._chunks is None:
             self._run()
         if self._next >= len(self._chunks):
@@ -178,4 +186,5 @@ class Resampler(object):
                                    self.bits_per_sample)
 
     def close(self):
+        self._closed = True
         self.pcmreader.close()

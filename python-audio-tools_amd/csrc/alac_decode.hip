@@ -28,6 +28,7 @@
 //   K4 k_adec_interleave block per frameset: stereo decorrelation,
 //                      uncompressed LSBs, ALAC -> wave channel order,
 //                      interleaved int32 (the FrameList layout).
+#include "handle_lock.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -577,6 +578,7 @@ bool find_path(const uint8_t *d, uint64_t off, uint64_t end, std::initializer_li
 } // namespace
 
 struct atg_alac_decoder {
+    std::recursive_mutex mu; // held by every public entry point (handle_lock.h)
     int device = 0;
     hipStream_t s = nullptr;
     hipEvent_t ev[kADTimed] = {};
@@ -888,6 +890,7 @@ atg_status atg_alac_decode_device(atg_alac_decoder *d, const void *d_data, uint6
                                   atg_alac_dec_result *results, const int32_t **d_pcm,
                                   uint64_t *total_samples)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || (!tracks && n) || (!results && n) || (!d_data && len))
         return adfail(ATG_ERR_INVALID, "NULL argument");
     if (((uintptr_t)d_data) & 3)
@@ -908,6 +911,7 @@ atg_status atg_alac_decode_host(atg_alac_decoder *d, const uint8_t *data, uint64
                                 atg_alac_dec_result *results, uint64_t *total_samples,
                                 uint64_t *total_framesets)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || (!tracks && n) || (!results && n) || (!data && len))
         return adfail(ATG_ERR_INVALID, "NULL argument");
     ADHIP(hipSetDevice(d->device));
@@ -929,6 +933,7 @@ atg_status atg_alac_decode_fetch(atg_alac_decoder *d, int32_t *pcm, uint64_t pcm
                                  uint32_t *frameset_frames, uint64_t *frameset_offsets,
                                  uint64_t fs_cap)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d)
         return adfail(ATG_ERR_INVALID, "NULL decoder");
     if ((pcm && pcm_cap < d->total_samples) ||
@@ -956,6 +961,7 @@ atg_status atg_alac_decode_fetch(atg_alac_decoder *d, int32_t *pcm, uint64_t pcm
 
 int atg_alac_decoder_kernel_times(atg_alac_decoder *d, const char **names, float *ms, int cap)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || !d->have_times)
         return 0;
     const int k = cap < kADTimed ? cap : kADTimed;

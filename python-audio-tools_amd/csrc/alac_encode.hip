@@ -35,6 +35,7 @@
 //                      writes the element's bits MSB-first into its bit
 //                      range (whole words stored, the two shared edge words
 //                      OR-ed atomically), the frameset's trailing '111'.
+#include "handle_lock.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -862,6 +863,7 @@ uint64_t fs_bound(uint32_t N, uint32_t nch, uint32_t bps)
 } // namespace
 
 struct atg_alac_encoder {
+    std::recursive_mutex mu; // held by every public entry point (handle_lock.h)
     int device = 0;
     hipStream_t s = nullptr;
     hipEvent_t ev[kATimed] = {};
@@ -1132,6 +1134,7 @@ atg_status atg_alac_batch_bounds(atg_alac_encoder *e, const atg_alac_options *o,
                                  const atg_track *tracks, uint32_t n, uint32_t channels,
                                  uint32_t bps, uint64_t *total_framesets, uint64_t *out_bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n))
         return afail(ATG_ERR_INVALID, "NULL argument");
     APlan P;
@@ -1151,6 +1154,7 @@ atg_status atg_alac_encode_device(atg_alac_encoder *e, const atg_alac_options *o
                                   uint64_t out_cap, atg_alac_track_result *results,
                                   uint32_t *frameset_bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n) || (!results && n))
         return afail(ATG_ERR_INVALID, "NULL argument");
     if (((uintptr_t)d_out) & 3)
@@ -1174,6 +1178,7 @@ atg_status atg_alac_encode_host(atg_alac_encoder *e, const atg_alac_options *o, 
                                 uint32_t channels, uint32_t bps, uint8_t *out, uint64_t out_cap,
                                 atg_alac_track_result *results, uint32_t *frameset_bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n) || (!results && n) || (!pcm && n))
         return afail(ATG_ERR_INVALID, "NULL argument");
     AHIP(hipSetDevice(e->device));
@@ -1207,6 +1212,7 @@ atg_status atg_alac_encode_host(atg_alac_encoder *e, const atg_alac_options *o, 
 
 int atg_alac_encoder_kernel_times(atg_alac_encoder *e, const char **names, float *ms, int cap)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || !e->have_times)
         return 0;
     const int k = cap < kATimed ? cap : kATimed;

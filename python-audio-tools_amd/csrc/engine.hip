@@ -5,6 +5,7 @@
 // The engine owns two HIP streams: the encoder chain runs on `main`, the
 // per-track MD5 chain (a serial hash per track) runs concurrently on `aux`
 // and joins before the stream headers are written.
+#include "handle_lock.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -187,6 +188,7 @@ struct HostStage {
 };
 
 struct atg_engine {
+    std::recursive_mutex mu; // held by every public entry point (handle_lock.h)
     int device = 0;
     bool sync_call = false; // inside atg_flac_encode_device (enqueue + wait)
     hipStream_t s_main = nullptr;
@@ -857,7 +859,7 @@ atg_status get_plan(atg_engine *e, const atg_flac_options *o, const atg_track *t
     return ATG_OK;
 }
 
-// With ATG_ENGINE_STREAMS=lazy streams are created on first use: a process
+// A streaming engine (ATG_ENGINE_STREAMING) creates streams on first use: a process
 // that only streams segments (atg_flac_encode_frames, one slot) holds
 // s_main and one aux stream, not six -- under track2track many such
 // processes share one GPU, and with every process at GPU_MAX_HW_QUEUES
@@ -1060,7 +1062,21 @@ atg_status host_collect(atg_engine *e)
 atg_status host_drain(atg_engine *e, atg_status err)
 {
     const std::string msg = g_err;
-    (void)hipDeviceSynchronize();
+    const bool device_ok = hipDeviceSynchronize() == hipSuccess;
+    // a fully collected job may still have its last chunk's images in pinned
+    // staging: its D2H is complete now, so finish the copy (or fail the job
+    // if the device itself failed) rather than drop it
+    if (e->hcopy_job) {
+        HostJob &j = *e->hcopy_job;
+        const HostChunk &c = j.chunks[e->hcopy_chunk];
+        if (device_ok && c.staged_out && c.out_bytes)
+            par_memcpy(j.out + c.out0, e->hs[c.stage].p_out, c.out_bytes, host_threads());
+        else if (!device_ok && j.status == ATG_OK) {
+            j.status = err;
+            j.error = msg;
+        }
+        e->hcopy_job = nullptr;
+    }
     for (EncSlot &s2 : e->slot)
         if (s2.busy && s2.host) {
             s2.busy = false;
@@ -1075,7 +1091,6 @@ atg_status host_drain(atg_engine *e, atg_status err)
             jp->error = msg;
         }
     e->hflight.clear();
-    e->hcopy_job = nullptr;
     g_err = msg;
     return err;
 }
@@ -1148,6 +1163,11 @@ const char *atg_last_error(void) { return g_err.c_str(); }
 
 atg_status atg_engine_create(int device, atg_engine **out)
 {
+    return atg_engine_create_ex(device, 0, out);
+}
+
+atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
+{
     if (!out)
         return fail(ATG_ERR_INVALID, "out is NULL");
     *out = nullptr;
@@ -1160,14 +1180,14 @@ atg_status atg_engine_create(int device, atg_engine **out)
     atg_engine *e = new atg_engine();
     e->device = device;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
-    // every stream now, in this order, unless ATG_ENGINE_STREAMS=lazy: the
-    // order fixes the streams' hardware queues, and the device-resident
-    // step is 9.4 ms with it against 10.3 ms with streams created on first
-    // use (profiles/r03_l_streams_ab.txt).  "lazy" is for many processes
-    // per GPU (track2track): a streaming process then holds two streams
-    // and 8 processes run 49.8 k frames/s against 17.6 k
-    const char *mode = getenv("ATG_ENGINE_STREAMS");
-    if (!(mode && strcmp(mode, "lazy") == 0)) {
+    // every stream now, in this order, unless the caller streams one track
+    // at a time (ATG_ENGINE_STREAMING): the order fixes the streams'
+    // hardware queues, and the device-resident step is 9.4 ms with it
+    // against 10.3 ms with streams created on first use
+    // (profiles/r03_l_streams_ab.txt).  A streaming engine (encode_flac, one
+    // process per track under track2track) holds two streams, and 8 such
+    // processes run 49.8 k frames/s against 17.6 k
+    if (!(flags & ATG_ENGINE_STREAMING)) {
         for (EncSlot &sl : e->slot)
             if (ensure_aux_stream(sl) != ATG_OK)
                 return ATG_ERR_DEVICE;
@@ -1262,6 +1282,7 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
                                         uint32_t channels, uint32_t bps, uint32_t rate,
                                         void *d_out, uint64_t out_cap, uint64_t *ticket)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n_tracks) || !ticket)
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
@@ -1295,6 +1316,7 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
 
 atg_status atg_flac_encode_wait(atg_engine *e, uint64_t ticket, atg_track_result *results)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     EncSlot *sl = nullptr;
@@ -1312,6 +1334,7 @@ atg_status atg_flac_encode_device(atg_engine *e, const atg_flac_options *opts,
                                   uint32_t channels, uint32_t bps, uint32_t rate, void *d_out,
                                   uint64_t out_cap, atg_track_result *results)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n_tracks) || (!results && n_tracks))
         return fail(ATG_ERR_INVALID, "NULL argument");
     uint64_t t = 0;
@@ -1332,6 +1355,7 @@ atg_status atg_flac_encode_host_async(atg_engine *e, const atg_flac_options *opt
                                       uint64_t *frame_offsets, uint32_t *frame_pcm_frames,
                                       uint64_t *ticket)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!tracks && n_tracks) || (!results && n_tracks) || !ticket)
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
@@ -1404,6 +1428,7 @@ atg_status atg_flac_encode_host_async(atg_engine *e, const atg_flac_options *opt
 
 atg_status atg_flac_encode_host_wait(atg_engine *e, uint64_t ticket)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     size_t k = 0;
@@ -1442,6 +1467,7 @@ atg_status atg_flac_encode_host(atg_engine *e, const atg_flac_options *opts, con
                                 atg_track_result *results, uint64_t *frame_offsets,
                                 uint32_t *frame_pcm_frames)
 {
+    ATG_HANDLE_LOCK(e);
     uint64_t t = 0;
     atg_status st = atg_flac_encode_host_async(e, opts, pcm, format, tracks, n_tracks, channels,
                                                bps, rate, out, out_cap, results, frame_offsets,
@@ -1510,6 +1536,7 @@ atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, c
                                   uint64_t first_frame_number, uint8_t *out, uint64_t out_cap,
                                   uint64_t *out_bytes, uint32_t *frame_bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || (!pcm && pcm_frames) || !out_bytes)
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
@@ -1600,6 +1627,7 @@ uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_fr
 
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || !bytes)
         return fail(ATG_ERR_INVALID, "NULL engine or zero chunk size");
     e->chunk_bytes = bytes;
@@ -1608,6 +1636,7 @@ atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)
 
 int atg_engine_kernel_times(atg_engine *e, const char **names, float *ms, int cap)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || !e->have_times)
         return 0;
     const int n = cap < kNumTimed ? cap : kNumTimed;
@@ -1622,6 +1651,7 @@ int atg_engine_kernel_times(atg_engine *e, const char **names, float *ms, int ca
 
 atg_status atg_device_alloc(atg_engine *e, uint64_t bytes, void **d_ptr)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e || !d_ptr)
         return fail(ATG_ERR_INVALID, "NULL argument");
     HIP_TRY(hipSetDevice(e->device));
@@ -1631,6 +1661,7 @@ atg_status atg_device_alloc(atg_engine *e, uint64_t bytes, void **d_ptr)
 
 atg_status atg_device_free(atg_engine *e, void *d_ptr)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -1659,6 +1690,7 @@ void atg_host_free(void *ptr)
 
 atg_status atg_copy_to_device(atg_engine *e, void *d_dst, const void *src, uint64_t bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -1668,6 +1700,7 @@ atg_status atg_copy_to_device(atg_engine *e, void *d_dst, const void *src, uint6
 
 atg_status atg_copy_device(atg_engine *e, void *d_dst, const void *d_src, uint64_t bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));
@@ -1677,6 +1710,7 @@ atg_status atg_copy_device(atg_engine *e, void *d_dst, const void *d_src, uint64
 
 atg_status atg_copy_to_host(atg_engine *e, void *dst, const void *d_src, uint64_t bytes)
 {
+    ATG_HANDLE_LOCK(e);
     if (!e)
         return fail(ATG_ERR_INVALID, "NULL engine");
     HIP_TRY(hipSetDevice(e->device));

@@ -22,14 +22,17 @@
  * The frames are encoded on the GPU in bounded segments of SEGMENT_FRAMES
  * frames (atg_flac_encode_frames), with the GIL released around each
  * segment as the reference releases it around each frame (flac.c:255-270);
- * the STREAMINFO MD5 of the PCM bytes is updated per read on the host
- * (RFC 1321 below), as the reference's read callback does
- * (pcmconv.c:266-291).  Host memory stays bounded by one segment.
+ * the STREAMINFO MD5 of the PCM bytes (what the reference's read callback
+ * hashes, pcmconv.c:266-291; RFC 1321 below) runs over each segment on a
+ * host thread while the GPU encodes it.  Host memory stays bounded by one
+ * segment.  The engine is a streaming one (ATG_ENGINE_STREAMING): one
+ * process per track, as track2track runs encoders, holds two HIP streams.
  */
 #define PY_SSIZE_T_CLEAN
 #include <Python.h>
 
 #include <errno.h>
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -37,107 +40,40 @@
 
 #include "../../../include/atgpu.h"
 
-#define SEGMENT_FRAMES 256
+#define SEGMENT_FRAMES 256 /* the most frames per GPU call */
+static unsigned g_segment_frames = SEGMENT_FRAMES; /* _set_segment_frames (tests) */
 
-/* ------------------------------------------------------------------ MD5 */
+#include "md5_host.h"
+
+/* the MD5 bytes of a segment: FrameList.to_bytes(little_endian, signed) of
+   its samples (flac.c:187-188), from the segment's int16 / int32 container */
 typedef struct {
-    uint32_t h[4];
-    uint64_t len;
-    uint8_t buf[64];
-} md5_ctx;
+    md5_ctx *md5;
+    const uint8_t *pcm;
+    size_t samples, elem;
+    unsigned width;
+} md5_job;
 
-static uint32_t rol(uint32_t x, int c) { return (x << c) | (x >> (32 - c)); }
-
-static void md5_block(uint32_t h[4], const uint8_t *p)
+static void *md5_segment(void *arg)
 {
-    static const uint32_t K[64] = {
-        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613,
-        0xfd469501, 0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193,
-        0xa679438e, 0x49b40821, 0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d,
-        0x02441453, 0xd8a1e681, 0xe7d3fbc8, 0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed,
-        0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a, 0xfffa3942, 0x8771f681, 0x6d9d6122,
-        0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70, 0x289b7ec6, 0xeaa127fa,
-        0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665, 0xf4292244,
-        0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
-        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb,
-        0xeb86d391};
-    static const int S[64] = {7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22, 7, 12, 17, 22,
-                              5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20, 5, 9,  14, 20,
-                              4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23, 4, 11, 16, 23,
-                              6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21, 6, 10, 15, 21};
-    uint32_t X[16];
-    for (int i = 0; i < 16; ++i)
-        X[i] = (uint32_t)p[4 * i] | ((uint32_t)p[4 * i + 1] << 8) |
-               ((uint32_t)p[4 * i + 2] << 16) | ((uint32_t)p[4 * i + 3] << 24);
-    uint32_t a = h[0], b = h[1], c = h[2], d = h[3];
-    for (int i = 0; i < 64; ++i) {
-        uint32_t f;
-        int g;
-        if (i < 16) {
-            f = (b & c) | (~b & d);
-            g = i;
-        } else if (i < 32) {
-            f = (d & b) | (~d & c);
-            g = (5 * i + 1) & 15;
-        } else if (i < 48) {
-            f = b ^ c ^ d;
-            g = (3 * i + 5) & 15;
-        } else {
-            f = c ^ (b | ~d);
-            g = (7 * i) & 15;
+    md5_job *j = (md5_job *)arg;
+    if (j->width == j->elem) { /* 16-bit in int16, 32-bit in int32: as stored */
+        md5_update(j->md5, j->pcm, j->samples * j->elem);
+        return NULL;
+    }
+    uint8_t tmp[4096];
+    size_t tl = 0;
+    for (size_t i = 0; i < j->samples; ++i) {
+        const uint8_t *x = j->pcm + i * j->elem; /* little-endian container */
+        for (unsigned k = 0; k < j->width; ++k)
+            tmp[tl++] = x[k];
+        if (tl + 4 > sizeof(tmp)) {
+            md5_update(j->md5, tmp, tl);
+            tl = 0;
         }
-        const uint32_t t = d;
-        d = c;
-        c = b;
-        b = b + rol(a + f + K[i] + X[g], S[i]);
-        a = t;
     }
-    h[0] += a;
-    h[1] += b;
-    h[2] += c;
-    h[3] += d;
-}
-
-static void md5_init(md5_ctx *m)
-{
-    m->h[0] = 0x67452301u;
-    m->h[1] = 0xefcdab89u;
-    m->h[2] = 0x98badcfeu;
-    m->h[3] = 0x10325476u;
-    m->len = 0;
-}
-
-static void md5_update(md5_ctx *m, const uint8_t *p, size_t n)
-{
-    size_t have = (size_t)(m->len & 63u);
-    m->len += n;
-    if (have) {
-        const size_t take = 64 - have < n ? 64 - have : n;
-        memcpy(m->buf + have, p, take);
-        p += take;
-        n -= take;
-        if (have + take < 64)
-            return;
-        md5_block(m->h, m->buf);
-    }
-    for (; n >= 64; p += 64, n -= 64)
-        md5_block(m->h, p);
-    memcpy(m->buf, p, n);
-}
-
-static void md5_final(md5_ctx *m, uint8_t out[16])
-{
-    const uint64_t bits = m->len * 8u;
-    static const uint8_t pad[64] = {0x80};
-    const size_t have = (size_t)(m->len & 63u);
-    md5_update(m, pad, have < 56 ? 56 - have : 120 - have);
-    uint8_t lb[8];
-    for (int i = 0; i < 8; ++i)
-        lb[i] = (uint8_t)(bits >> (8 * i));
-    md5_update(m, lb, 8);
-    for (int i = 0; i < 4; ++i)
-        for (int k = 0; k < 4; ++k)
-            out[4 * i + k] = (uint8_t)(m->h[i] >> (8 * k));
+    md5_update(j->md5, tmp, tl);
+    return NULL;
 }
 
 /* ------------------------------------------------------------- module */
@@ -176,6 +112,7 @@ typedef struct {
     size_t out_cap;
     uint32_t *frame_bytes;
     PyObject *list;
+    md5_ctx md5;
 } enc_state;
 
 /* encode and write the collected segment; appends to the offsets list */
@@ -184,7 +121,7 @@ static int flush_segment(enc_state *s)
     if (!s->n_sizes)
         return 0;
     if (!g_eng) {
-        const atg_status st = atg_engine_create(engine_device(), &g_eng);
+        const atg_status st = atg_engine_create_ex(engine_device(), ATG_ENGINE_STREAMING, &g_eng);
         if (st != ATG_OK) {
             raise_atg(st);
             return -1;
@@ -209,10 +146,17 @@ static int flush_segment(enc_state *s)
     }
     uint64_t nb = 0;
     atg_status st;
+    md5_job mj = {&s->md5, s->pcm, (size_t)(frames * s->channels), elem, (s->bps + 7) / 8};
     Py_BEGIN_ALLOW_THREADS
+    pthread_t hasher;
+    const int threaded = pthread_create(&hasher, NULL, md5_segment, &mj) == 0;
+    if (!threaded)
+        md5_segment(&mj);
     st = atg_flac_encode_frames(g_eng, &s->o, s->pcm, s->bps <= 16 ? ATG_PCM_S16 : ATG_PCM_S32,
                                 frames, s->sizes, s->n_sizes, s->channels, s->bps, s->rate,
                                 s->frame_no, s->out, s->out_cap, &nb, s->frame_bytes);
+    if (threaded)
+        pthread_join(hasher, NULL);
     if (st == ATG_OK && nb && fwrite(s->out, 1, nb, s->f) != nb)
         st = (atg_status)1; /* write error, below */
     Py_END_ALLOW_THREADS
@@ -243,9 +187,8 @@ static int flush_segment(enc_state *s)
     return 0;
 }
 
-/* one read's FrameList: its samples appended to the segment, its PCM
-   bytes (little-endian, signed) into the MD5 */
-static int take_framelist(enc_state *s, PyObject *fl, md5_ctx *md5, uint64_t *frames_out)
+/* one read's FrameList: its samples appended to the segment */
+static int take_framelist(enc_state *s, PyObject *fl, uint64_t *frames_out)
 {
     PyObject *samples = PyObject_GetAttrString(fl, "samples");
     if (!samples)
@@ -280,25 +223,13 @@ static int take_framelist(enc_state *s, PyObject *fl, md5_ctx *md5, uint64_t *fr
         s->pcm = p;
         s->pcm_cap = cap;
     }
-    const unsigned width = (s->bps + 7) / 8;
-    uint8_t tmp[4096];
-    size_t tl = 0;
-    for (size_t i = 0; i < n; ++i) {
-        const uint32_t v = (uint32_t)x[i];
-        if (elem == 2) {
-            const int16_t h = (int16_t)x[i];
-            memcpy(s->pcm + s->pcm_len + 2 * i, &h, 2);
-        } else {
-            memcpy(s->pcm + s->pcm_len + 4 * i, &x[i], 4);
-        }
-        for (unsigned k = 0; k < width; ++k)
-            tmp[tl++] = (uint8_t)(v >> (8 * k));
-        if (tl + 4 > sizeof(tmp)) {
-            md5_update(md5, tmp, tl);
-            tl = 0;
-        }
+    if (elem == 2) {
+        int16_t *d = (int16_t *)(s->pcm + s->pcm_len);
+        for (size_t i = 0; i < n; ++i)
+            d[i] = (int16_t)x[i];
+    } else {
+        memcpy(s->pcm + s->pcm_len, x, n * 4);
     }
-    md5_update(md5, tmp, tl);
     s->pcm_len += n * elem;
     rc = 0;
 done:
@@ -357,8 +288,7 @@ static PyObject *encode_flac(PyObject *self, PyObject *args, PyObject *kw)
     PyObject *result = NULL;
     uint8_t *hbuf = (uint8_t *)PyMem_Malloc((size_t)s.o.padding_size + 256);
     const uint8_t zero_md5[16] = {0};
-    md5_ctx md5;
-    md5_init(&md5);
+    md5_init(&s.md5);
     s.list = PyList_New(0);
     s.frame_bytes = (uint32_t *)PyMem_Malloc(sizeof(uint32_t) * SEGMENT_FRAMES);
     if (!hbuf || !s.list || !s.frame_bytes) {
@@ -389,7 +319,7 @@ static PyObject *encode_flac(PyObject *self, PyObject *args, PyObject *kw)
             goto fail;
         }
         uint64_t frames = 0;
-        const int r = take_framelist(&s, fl, &md5, &frames);
+        const int r = take_framelist(&s, fl, &frames);
         Py_DECREF(fl);
         if (r < 0)
             goto fail;
@@ -397,14 +327,14 @@ static PyObject *encode_flac(PyObject *self, PyObject *args, PyObject *kw)
             break;
         s.sizes[s.n_sizes++] = (uint32_t)frames;
         s.total += frames;
-        if (s.n_sizes == SEGMENT_FRAMES && flush_segment(&s) < 0)
+        if (s.n_sizes >= g_segment_frames && flush_segment(&s) < 0)
             goto fail;
     }
     if (flush_segment(&s) < 0)
         goto fail;
     {
         uint8_t digest[16];
-        md5_final(&md5, digest);
+        md5_final(&s.md5, digest);
         const uint64_t hn = atg_flac_stream_header(&s.o, s.channels, s.bps, s.rate, s.total,
                                                    s.min_fs, s.max_fs, digest, hbuf,
                                                    s.o.padding_size + 256);
@@ -438,11 +368,30 @@ fail:
     return result;
 }
 
+/* test hook: frames per GPU call (1..SEGMENT_FRAMES), to exercise
+   segment boundaries on short streams */
+static PyObject *set_segment_frames(PyObject *self, PyObject *arg)
+{
+    (void)self;
+    const long n = PyLong_AsLong(arg);
+    if (n == -1 && PyErr_Occurred())
+        return NULL;
+    if (n < 1 || n > SEGMENT_FRAMES) {
+        PyErr_SetString(PyExc_ValueError, "segment frames must be 1..256");
+        return NULL;
+    }
+    const long old = (long)g_segment_frames;
+    g_segment_frames = (unsigned)n;
+    return PyLong_FromLong(old);
+}
+
 static PyMethodDef methods[] = {
     {"encode_flac", (PyCFunction)(void (*)(void))encode_flac, METH_VARARGS | METH_KEYWORDS,
      "encode_flac(filename, pcmreader, block_size, max_lpc_order, "
      "min_residual_partition_order, max_residual_partition_order, ...) -> "
      "[(byte_offset, pcm_frames), ...]  (FLAC encode on the MI355X)"},
+    {"_set_segment_frames", set_segment_frames, METH_O,
+     "_set_segment_frames(n) -> previous: FLAC frames per GPU call (test hook)"},
     {NULL, NULL, 0, NULL}};
 
 static struct PyModuleDef module = {PyModuleDef_HEAD_INIT, "_encoders_c",

@@ -36,6 +36,7 @@
 // Only K2 and K4 do real work; K1 and K5 are HBM passes.  Status codes are
 // the FD_* values of include/atgpu.h (the reference's flac_status plus the
 // conditions read() raises itself).
+#include "handle_lock.h"
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -1185,6 +1186,7 @@ struct DecSlot {
 };
 
 struct atg_decoder {
+    std::recursive_mutex mu; // held by every public entry point (handle_lock.h)
     int device = 0;
     hipStream_t s = nullptr;
     float times[kDecTimed] = {};
@@ -1647,6 +1649,7 @@ atg_status atg_flac_decode_device_async(atg_decoder *d, const void *d_data, uint
                                         const atg_flac_dec_track *tracks, uint32_t n,
                                         uint64_t *ticket)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || (!tracks && n) || !ticket || (!d_data && len))
         return dfail(ATG_ERR_INVALID, "NULL argument");
     if (((uintptr_t)d_data) & 3)
@@ -1667,6 +1670,7 @@ atg_status atg_flac_decode_device_async(atg_decoder *d, const void *d_data, uint
 atg_status atg_flac_decode_wait(atg_decoder *d, uint64_t ticket, atg_flac_dec_result *results,
                                 const int32_t **d_pcm, uint64_t *total_samples)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d)
         return dfail(ATG_ERR_INVALID, "NULL decoder");
     DecSlot *sl = find_dec_ticket(d, ticket);
@@ -1690,6 +1694,7 @@ atg_status atg_flac_decode_device(atg_decoder *d, const void *d_data, uint64_t l
                                   atg_flac_dec_result *results, const int32_t **d_pcm,
                                   uint64_t *total_samples)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || (!tracks && n) || (!results && n) || (!d_data && len))
         return dfail(ATG_ERR_INVALID, "NULL argument");
     uint64_t ticket = 0;
@@ -1704,6 +1709,7 @@ atg_status atg_flac_decode_host(atg_decoder *d, const uint8_t *data, uint64_t le
                                 atg_flac_dec_result *results, uint64_t *total_samples,
                                 uint64_t *total_frames)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || (!tracks && n) || (!results && n) || (!data && len))
         return dfail(ATG_ERR_INVALID, "NULL argument");
     DHIP(hipSetDevice(d->device));
@@ -1734,6 +1740,7 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
                                  uint64_t *frame_offsets, uint32_t *frame_block_sizes,
                                  uint64_t frame_cap)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d)
         return dfail(ATG_ERR_INVALID, "NULL decoder");
     if (d->last < 0)
@@ -1770,6 +1777,7 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
 
 int atg_decoder_kernel_times(atg_decoder *d, const char **names, float *ms, int cap)
 {
+    ATG_HANDLE_LOCK(d);
     if (!d || !d->have_times)
         return 0;
     const int n = cap < kDecTimed ? cap : kDecTimed;

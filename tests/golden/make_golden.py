@@ -28,7 +28,7 @@ import signals  # noqa: E402
 OUT = os.path.join(HERE, "flac_vectors.json")
 
 KINDS = ["tone", "sine", "noise", "silence", "chirp", "wasted", "fsd"]
-FORMATS = [(1, 8), (1, 16), (2, 16), (2, 24), (6, 16)]
+FORMATS = [(1, 8), (1, 16), (2, 16), (2, 24), (6, 16), (6, 24), (6, 8)]
 
 
 def cases():

@@ -100,34 +100,91 @@ def options(**kw):
                        int(bool(d["disable_lpc_subframes"])), int(d["padding_size"]))
 
 
-def encode(pcm, channels, bps, rate, **opts):
-    """-> (flac bytes, [(offset, pcm_frames), ...])"""
+def encode(pcm, channels, bps, rate, frame_sizes=None, **opts):
+    """-> (flac bytes, [(offset, pcm_frames), ...]).  frame_sizes = the frame
+    counts a reader's successive read() calls returned (then block_size per
+    read): one frame per read, as the reference (flac.c:244-274)."""
     lib = load()
     o = options(**opts)
     a = np.ascontiguousarray(pcm, dtype=np.int32)
     frames = len(a) // channels
+    sizes = None if frame_sizes is None else np.ascontiguousarray(frame_sizes, dtype=np.uint32)
     cap = lib.flacport_max_stream_bytes(frames, channels, bps, o.block_size,
                                         o.padding_size)
+    nfmax = frames // max(1, o.block_size) + 2
+    if sizes is not None and len(sizes):
+        # per listed read: a verbatim frame of its own size plus headers
+        per = 32 + channels * (12 + (sizes.astype(np.int64) * (bps + 1) + 7) // 8)
+        cap += int(per.sum()) + 64
+        nfmax += len(sizes)
     if opts.get("disable_verbatim_subframes"):
         # without VERBATIM a predictor may exceed the verbatim bound (24-bit
         # noise): leave room for twice that
         cap = 2 * cap + (1 << 20)
     out = np.empty(cap, dtype=np.uint8)
     olen = ctypes.c_size_t()
-    nfmax = frames // max(1, o.block_size) + 2
     offs = np.zeros(nfmax, dtype=np.uint64)
     lens = np.zeros(nfmax, dtype=np.uint32)
     nf = ctypes.c_size_t()
-    rc = lib.flacport_encode(a.ctypes.data_as(ctypes.c_void_p), frames, channels, bps,
-                             rate, ctypes.byref(o), out.ctypes.data_as(ctypes.c_void_p),
-                             cap, ctypes.byref(olen),
-                             offs.ctypes.data_as(ctypes.c_void_p),
-                             lens.ctypes.data_as(ctypes.c_void_p), nfmax,
-                             ctypes.byref(nf))
+    if not hasattr(lib, "_sizes_ready"):
+        lib.flacport_encode_sizes.restype = ctypes.c_int
+        lib.flacport_encode_sizes.argtypes = [
+            ctypes.c_void_p, c_u64, c_u32, c_u32, c_u32, ctypes.POINTER(PortOptions),
+            ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.c_void_p, ctypes.c_size_t, ctypes.POINTER(ctypes.c_size_t),
+            ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t,
+            ctypes.POINTER(ctypes.c_size_t)]
+        lib._sizes_ready = True
+    rc = lib.flacport_encode_sizes(
+        a.ctypes.data_as(ctypes.c_void_p), frames, channels, bps, rate, ctypes.byref(o),
+        None if sizes is None else sizes.ctypes.data_as(ctypes.c_void_p),
+        0 if sizes is None else len(sizes), out.ctypes.data_as(ctypes.c_void_p),
+        cap, ctypes.byref(olen), offs.ctypes.data_as(ctypes.c_void_p),
+        lens.ctypes.data_as(ctypes.c_void_p), nfmax, ctypes.byref(nf))
     if rc != 0:
         raise RuntimeError("flacport_encode failed: %d" % rc)
     n = nf.value
     return out[:olen.value].tobytes(), [(int(offs[i]), int(lens[i])) for i in range(n)]
+
+
+def cut_frames(frames, block_size, frame_sizes):
+    """the frame lengths a stream of `frames` PCM frames is cut into when the
+    reader's reads return frame_sizes, then block_size per read"""
+    cut, left = [], frames
+    for n in frame_sizes:
+        if left <= 0 or n == 0:
+            return cut
+        cut.append(min(n, left))
+        left -= cut[-1]
+    while left > 0:
+        cut.append(min(block_size, left))
+        left -= cut[-1]
+    return cut
+
+
+REF_FLACENC_SIZED = os.path.join(ORACLE_DIR, "_ref", "flacenc_sized")
+
+
+def ref_encode_sized(pcm, channels, bps, rate, frame_sizes, **opts):
+    """the REFERENCE encoder (oracle/_ref/flacenc_sized: src/encoders/flac.c's
+    encoders_encode_flac behind oracle/ref_sized_reads.c) with reads of the
+    listed sizes -> .flac bytes (padding fixed at 4096, as the standalone
+    build)"""
+    import tempfile
+    args = [REF_FLACENC_SIZED, "-c", str(channels), "-r", str(rate), "-b", str(bps),
+            "-B", str(opts["block_size"]), "-l", str(opts["max_lpc_order"]),
+            "-P", str(opts.get("min_residual_partition_order", 0)),
+            "-R", str(opts["max_residual_partition_order"]),
+            "-S", ",".join(str(int(x)) for x in frame_sizes)]
+    for k, f in (("mid_side", "-m"), ("adaptive_mid_side", "-M"),
+                 ("exhaustive_model_search", "-e")):
+        if opts.get(k):
+            args.append(f)
+    raw = pcm_bytes(pcm, bps)
+    with tempfile.TemporaryDirectory() as d:
+        fn = os.path.join(d, "o.flac")
+        subprocess.run(args + [fn], input=raw, stdout=subprocess.DEVNULL, check=True)
+        return open(fn, "rb").read()
 
 
 def decode(data):

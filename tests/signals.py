@@ -27,6 +27,14 @@ def sine_mono(n, rate, f1, a1, f2, a2, bps):
     return v.astype(np.int32)
 
 
+def simple_sine(n, max_value, count):
+    """one channel of Sine_Simple (src/decoders/sine.c:393-423):
+    round(max_value * sin(2 pi (i % count) / count))"""
+    i = np.arange(n) % count
+    d = max_value * np.sin((np.pi * 2) * i / count)
+    return (np.sign(d) * np.floor(np.abs(d) + 0.5)).astype(np.int32)  # C round()
+
+
 def noise(n, channels, bps, seed):
     rng = np.random.default_rng(seed)
     return rng.integers(-(1 << (bps - 1)), 1 << (bps - 1), n * channels).astype(np.int32)

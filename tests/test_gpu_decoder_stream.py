@@ -1,5 +1,5 @@
-"""GPU: FlacDecoder decodes in bounded segments (SEGMENT_BYTES of compressed
-data per GPU call, audiotools/decoders.py) -- windows that end inside a
+"""GPU: FlacDecoder (the C extension, csrc/ext/decoders_c.c) decodes in
+bounded segments (8 MiB of compressed data per GPU call by default) -- windows that end inside a
 frame resume at that frame (the decode's walk_end), errors are raised at the
 frame where the reference's read() raises them (src/decoders/flac.c:174-285)
 and the STREAMINFO MD5 is chained over the segments on the host
@@ -29,12 +29,31 @@ def _frames(dec):
     return out, err
 
 
+class _Segments(object):
+    """decoders with a settable segment size (the extension's test hook)"""
+
+    def __init__(self):
+        from audiotools import _decoders_c, decoders
+        self.FlacDecoder = decoders.FlacDecoder
+        self._c = _decoders_c
+
+    @property
+    def SEGMENT_BYTES(self):
+        old = self._c._set_segment_bytes(1)
+        self._c._set_segment_bytes(old)
+        return old
+
+    @SEGMENT_BYTES.setter
+    def SEGMENT_BYTES(self, n):
+        self._c._set_segment_bytes(n)
+
+
 @pytest.fixture
 def small_segments():
-    from audiotools import decoders
-    old = decoders.SEGMENT_BYTES
-    yield decoders
-    decoders.SEGMENT_BYTES = old
+    d = _Segments()
+    old = d.SEGMENT_BYTES
+    yield d
+    d.SEGMENT_BYTES = old
 
 
 @pytest.mark.parametrize("seg", [1 << 10, 5000, 1 << 16])

@@ -87,6 +87,9 @@ def test_encode_flac_extension_irregular_reads(tmp_path):
     assert la == lb and [m for _, m in la][:len(sizes)] == sizes
     data = open(a, "rb").read()
     assert data == open(b, "rb").read()
+    want, wl = oracle_port.encode(x, 2, 16, 44100, frame_sizes=sizes,
+                                  **oracle_port.PRESETS["8"])
+    assert data == want and la == wl
     dec, _, _, _ = oracle_port.decode(data)
     assert np.array_equal(dec, x)
 

@@ -7,6 +7,7 @@ requires identical .flac images, identical frame offset lists, and a clean
 oracle decode round trip.
 """
 import hashlib
+import json
 import os
 
 import numpy as np
@@ -132,15 +133,102 @@ def test_many_tracks_one_batch(gpu_engine):
 
 
 def test_explicit_frame_sizes(gpu_engine):
-    """frames cut exactly where pcmreader.read() returned (flac.c:244-274)"""
+    """frames cut exactly where pcmreader.read() returned (flac.c:244-274):
+    block-size codes 0x6/0x7 + explicit sizes (flac.c:412-518), byte-equal to
+    the port's encode of the same reads"""
     opts = dict(oracle_port.PRESETS["8"])
     pcm = signals.make("tone", 10000, 2, 16, seed=3)
     sizes = [4096, 1000, 4096, 808]
     got = gpu_encode_tracks(gpu_engine, [pcm], 2, 16, 44100, opts, frame_sizes=[sizes])
     img, lst = got[0]
-    assert [n for _, n in lst] == sizes
+    want, wlst = oracle_port.encode(pcm, 2, 16, 44100, frame_sizes=sizes, **opts)
+    assert img == want
+    assert lst == wlst and [n for _, n in lst] == sizes
     dec, ch, b, r = oracle_port.decode(img)
     assert np.array_equal(dec, pcm)
+
+
+VECTORS = json.load(open(os.path.join(GOLDEN, "flac_vectors.json")))["vectors"]
+
+
+def _golden_pcm(v):
+    if v["kind"] == "fsd":
+        mono = signals.fsd(signals.PATTERNS[v["seed"] % len(signals.PATTERNS)], v["n"],
+                           v["bps"])
+        return np.repeat(mono[:, None], v["channels"], 1).reshape(-1).astype(np.int32)
+    return signals.make(v["kind"], v["n"], v["channels"], v["bps"], seed=v["seed"])
+
+
+@pytest.mark.parametrize("preset", sorted(oracle_port.PRESETS))
+def test_golden_vectors_reference_hashes(gpu_engine, preset):
+    """every committed reference-encoder vector (tests/golden/make_golden.py:
+    presets 0-8 x {1,2,6} ch x {8,16,24} bit incl. 5.1 24-bit, config 5's
+    encoder shape) encoded on the GPU, one batch per format: sha256 equal to
+    the reference encoder's"""
+    by_fmt = {}
+    for v in VECTORS:
+        if v["preset"] == preset:
+            by_fmt.setdefault((v["channels"], v["bps"]), []).append(v)
+    assert (6, 24) in by_fmt and (6, 8) in by_fmt
+    opts = dict(oracle_port.PRESETS[preset])
+    for (ch, bps), vs in sorted(by_fmt.items()):
+        got = gpu_encode_tracks(gpu_engine, [_golden_pcm(v) for v in vs], ch, bps, 44100, opts)
+        for v, (img, _) in zip(vs, got):
+            assert len(img) == v["bytes"], v["name"]
+            assert hashlib.sha256(img).hexdigest() == v["sha256"], v["name"]
+
+
+SIZED = json.load(open(os.path.join(GOLDEN, "flac_vectors_sized.json")))["vectors"]
+
+
+@pytest.mark.parametrize("preset", ["8", "5", "2", "0"])
+def test_sized_reads_golden(gpu_engine, preset):
+    """the reference encoder's streams for short/long reads
+    (tests/golden/make_golden_sized.py: 1-frame reads, reads longer than the
+    block, standard-code sizes, an empty read ending the stream) -- one GPU
+    batch per format, every image's sha256 equal to the reference's and the
+    bytes equal to the port's"""
+    cases = [v for v in SIZED if v["preset"] == preset]
+    opts = dict(oracle_port.PRESETS[preset])
+    by_fmt = {}
+    for v in cases:
+        by_fmt.setdefault((v["channels"], v["bps"]), []).append(v)
+    for (ch, bps), vs in sorted(by_fmt.items()):
+        pcms = []
+        for v in vs:
+            x = signals.make(v["kind"], v["n"], ch, bps, seed=v["seed"])
+            pcms.append(x[:sum(v["frame_lengths"]) * ch])
+        got = gpu_encode_tracks(gpu_engine, pcms, ch, bps, 44100, opts,
+                                frame_sizes=[v["frame_lengths"] for v in vs])
+        for v, p, (img, lst) in zip(vs, pcms, got):
+            assert [n for _, n in lst] == v["frame_lengths"], v["name"]
+            assert len(img) == v["bytes"], v["name"]
+            assert hashlib.sha256(img).hexdigest() == v["sha256"], v["name"]
+            want, wlst = oracle_port.encode(p, ch, bps, 44100,
+                                            frame_sizes=v["read_sizes"], **opts)
+            assert img == want and lst == wlst, v["name"]
+
+
+@pytest.mark.parametrize("seed", range(4))
+def test_random_frame_sizes_vs_port(gpu_engine, seed):
+    """random cuts (1..9000 frames per read) over several formats and
+    presets, many tracks per batch, against the port"""
+    rng = np.random.default_rng(500 + seed)
+    preset = ["8", "6", "3", "1"][seed]
+    opts = dict(oracle_port.PRESETS[preset])
+    ch, bps = [(2, 16), (6, 24), (1, 8), (2, 24)][seed]
+    pcms, cuts = [], []
+    for k in range(12):
+        n = int(rng.integers(1, 40000))
+        sizes = [int(x) for x in rng.integers(1, 9000, int(rng.integers(1, 8)))]
+        cut = oracle_port.cut_frames(n, opts["block_size"], sizes)
+        pcms.append(signals.make(["tone", "noise", "chirp", "sine"][k % 4], n, ch, bps,
+                                 seed=seed * 100 + k))
+        cuts.append(cut)
+    got = gpu_encode_tracks(gpu_engine, pcms, ch, bps, 44100, opts, frame_sizes=cuts)
+    for p, cut, (img, lst) in zip(pcms, cuts, got):
+        want, wlst = oracle_port.encode(p, ch, bps, 44100, frame_sizes=cut, **opts)
+        assert img == want and lst == wlst, (cut, len(p) // ch)
 
 
 def test_unsupported_options_raise(gpu_engine):
@@ -192,17 +280,21 @@ class _SizedReader(object):
     (1, 8, 3000, (), 256),
     (2, 16, 0, (), 3),                       # empty stream
 ])
-def test_encode_flac_streaming(tmp_path, monkeypatch, ch, bps, n, sizes, seg):
-    """encode_flac streams in segments of SEGMENT_FRAMES frames (frame
-    numbers continue across segments, host MD5 per read, STREAMINFO rewritten
-    at the end): the file equals the oracle's encode of the same reads"""
-    from audiotools import encoders
-    monkeypatch.setattr(encoders, "SEGMENT_FRAMES", seg)
+def test_encode_flac_streaming(tmp_path, ch, bps, n, sizes, seg):
+    """encode_flac (the C extension) streams in segments of up to 256 frames
+    (frame numbers continue across segments, the MD5 of each segment hashed
+    on a host thread, STREAMINFO rewritten at the end): the file equals the
+    oracle's encode of the same reads"""
+    from audiotools import _encoders_c, encoders
     x = signals.make("tone", n, ch, bps, seed=n + ch) if n else np.zeros(0, np.int32)
     opts = dict(oracle_port.PRESETS["8"])
     r = _SizedReader(x, 44100, ch, bps, sizes)
     fn = str(tmp_path / "s.flac")
-    lst = encoders.encode_flac(fn, r, **opts)
+    old = _encoders_c._set_segment_frames(seg)
+    try:
+        lst = encoders.encode_flac(fn, r, **opts)
+    finally:
+        _encoders_c._set_segment_frames(old)
     assert r.closed
     got = open(fn, "rb").read()
     # the oracle cuts the same frames: explicit sizes
@@ -222,16 +314,9 @@ def test_encode_flac_streaming(tmp_path, monkeypatch, ch, bps, n, sizes, seg):
 
 
 def _port_frames(x, ch, bps, cut, opts):
-    """the oracle stream for explicit frame sizes: the GPU batch path with
-    frame_sizes is itself parity-checked against the port, so encode the
-    same cut through it"""
-    from audiotools import _atgpu
-    eng = _atgpu.engine()
-    pcm = x.astype(np.int16 if bps <= 16 else np.int32)
-    out, res, _, _ = eng.encode(_atgpu.make_options(**opts), pcm, [(0, len(x) // ch, cut)], ch,
-                                bps, 44100)
-    r = res[0]
-    return out[r.out_offset:r.out_offset + r.bytes].tobytes()
+    """the port's stream for explicit frame sizes (flacport_encode_sizes,
+    pinned to the reference encoder by tests/golden/flac_vectors_sized.json)"""
+    return oracle_port.encode(x, ch, bps, 44100, frame_sizes=cut, **opts)[0]
 
 
 def test_loud_side_channel_split_fold(gpu_engine):

@@ -81,6 +81,8 @@ def test_big_and_small_frames_mixed(gpu_engine):
                             frame_sizes=[sizes, None])
     img, lst = got[0]
     assert [n for _, n in lst] == sizes
+    want, wlst = oracle_port.encode(pcm, 2, 16, 44100, frame_sizes=sizes, **opts)
+    assert img == want and lst == wlst
     dec, ch, b, r = oracle_port.decode(img)
     assert np.array_equal(dec, pcm)
     want, wlst = oracle_port.encode(pcm[:2 * 9000], 2, 16, 44100, **opts)

@@ -136,42 +136,73 @@ def test_batch_requires_matching_formats(tmp_path):
                                    4096, 12, 0, 6)
 
 
-class _SegmentEngine(object):
-    """stands in for the GPU engine: records the segments encode_flac hands
-    over and returns one 10-byte frame per PCM frame list"""
-
-    def __init__(self):
-        self.calls = []
-
-    def encode_frames(self, opts, pcm_, channels, bps, rate, first, sizes):
-        self.calls.append((pcm_.copy(), first, list(sizes)))
-        return np.zeros(10 * len(sizes), np.uint8), np.full(len(sizes), 10, np.uint32)
+def test_encode_flac_is_the_compiled_extension():
+    """the drop-in entry point is the C-API function, as the reference's
+    module function is its C extension (src/encoders.h:65-67)"""
+    from audiotools import _encoders_c
+    assert encoders.encode_flac is _encoders_c.encode_flac
+    assert _encoders_c._set_segment_frames(256) == 256
+    with pytest.raises(ValueError):
+        _encoders_c._set_segment_frames(0)
 
 
-@pytest.mark.parametrize("bps", [8, 16, 24])
-def test_encode_flac_streaming_segments_and_md5(tmp_path, monkeypatch, bps):
-    """the streaming path (flac.c:244-274): SEGMENT_FRAMES frames per engine
-    call, numbered on, in order; STREAMINFO's MD5 is the MD5 of the whole
-    stream's little-endian sample bytes (hashed per segment on a thread)"""
-    import hashlib
-    from audiotools import _atgpu
-    eng = _SegmentEngine()
-    monkeypatch.setattr(_atgpu, "engine", lambda: eng)
-    rng = np.random.default_rng(bps)
-    n = 2 * (2 * encoders.SEGMENT_FRAMES * 256 + 1000)  # two full segments + a tail
-    lim = 1 << (bps - 1)
-    samples = rng.integers(-lim, lim, n).astype(np.int32)
-    r = audiotools.BufferedPCMReader(audiotools.FrameListReader(samples, 44100, 2, bps))
-    out = tmp_path / "s.flac"
-    offs = encoders.encode_flac(str(out), r, 256, 8, 0, 5)
-    nfr = (n // 2 + 255) // 256
-    assert len(offs) == nfr
-    assert [c[1] for c in eng.calls] == [0, encoders.SEGMENT_FRAMES, 2 * encoders.SEGMENT_FRAMES]
-    got = np.concatenate([c[0].astype(np.int32) for c in eng.calls])
-    assert np.array_equal(got, samples)
-    data = out.read_bytes()
-    assert data[:4] == b"fLaC"
-    md5 = hashlib.md5(pcm.FrameList._wrap(samples, 2, bps).to_bytes(False, True)).digest()
-    assert data[26:42] == md5
-    # frame byte offsets follow the stream header, 10 bytes apart
-    assert [o[0] for o in offs[:3]] == [0, 10, 20]
+def test_channel_mask_and_helpers():
+    """ChannelMask / most_numerous / resampled_frame_count
+    (reference audiotools/__init__.py:1862-2060, 5012-5031, 2805-2820)"""
+    assert len(audiotools.ChannelMask(0x3F)) == 6
+    assert audiotools.ChannelMask(0x33).channels() == [0x1, 0x2, 0x10, 0x20]
+    assert audiotools.ChannelMask.from_channels(1) == 0x4
+    with pytest.raises(ValueError):
+        audiotools.ChannelMask.from_channels(3)
+    assert audiotools.most_numerous([]) is None
+    assert audiotools.most_numerous([44100]) == 44100
+    assert audiotools.most_numerous([1, 2, 3], all_differ="x") == "x"
+    assert audiotools.most_numerous([48000, 44100, 44100]) == 44100
+    assert audiotools.resampled_frame_count(441000, 44100, 48000) == 480000
+    assert audiotools.resampled_frame_count(10, 44100, 44100) == 10
+    assert audiotools.resampled_frame_count(1, 48000, 44100) == 0
+    assert audiotools.resampled_frame_count(123457, 44100, 8000) == 123457 * 8000 // 44100
+
+
+@pytest.mark.parametrize("src,dst,chain", [
+    ((44100, 2, 0x3, 24), (48000, 2, 0x3, 16), ["BPSConverter", "Resampler"]),
+    ((44100, 6, 0x3F, 16), (44100, 1, 0x4, 16), ["Averager", "Downmixer"]),
+    ((44100, 2, 0x3, 16), (44100, 1, 0, 16), ["Averager"]),
+    ((48000, 6, 0x3F, 24), (44100, 2, 0x3, 16), ["BPSConverter", "Resampler", "Downmixer"]),
+    ((44100, 6, 0x3F, 16), (44100, 4, 0x33, 16), ["RemaskedPCMReader"]),
+    ((44100, 1, 0x4, 16), (44100, 2, 0x3, 8), ["BPSConverter", "ReorderedPCMReader"]),
+    ((44100, 2, 0x3, 16), (44100, 2, 0x3, 16), []),
+])
+def test_pcmconverter_composition(src, dst, chain):
+    """PCMConverter's stage order (reference audiotools/__init__.py:
+    2761-2802): channels, then Resampler, then BPSConverter (outermost)"""
+    base = audiotools.FrameListReader(np.zeros(10 * src[1], np.int32), src[0], src[1], src[3],
+                                      channel_mask=src[2])
+    r = audiotools.PCMConverter(base, *dst)
+    names = []
+    while r is not base:
+        names.append(type(r).__name__)
+        r = r.pcmreader
+    assert names == chain
+
+
+def test_pcmconverter_rejects():
+    base = audiotools.FrameListReader(np.zeros(4, np.int32), 44100, 2, 16, channel_mask=0x3)
+    for args in [(0, 2, 0x3, 16), (44100, 0, 0x3, 16), (44100, 2, 0x3, 12),
+                 (44100, 2, 0x7, 16)]:
+        with pytest.raises(ValueError):
+            audiotools.PCMConverter(base, *args)
+
+
+def test_remasked_reader_maps_speakers():
+    """RemaskedPCMReader forwards matching speakers and fills the rest
+    with silence (reference audiotools/__init__.py:2249-2262)"""
+    x = np.arange(30, dtype=np.int32)  # 5 frames x 6 channels (0x3F)
+    r = audiotools.RemaskedPCMReader(
+        audiotools.FrameListReader(x, 44100, 6, 16, channel_mask=0x3F), 4, 0x1 | 0x2 | 0x100 | 0x10)
+    fl = r.read(10)
+    got = np.asarray(fl.samples).reshape(-1, 4)
+    src = x.reshape(-1, 6)
+    assert np.array_equal(got[:, 0], src[:, 0]) and np.array_equal(got[:, 1], src[:, 1])
+    assert np.array_equal(got[:, 2], src[:, 4])      # back_left 0x10 -> 5th input channel
+    assert not got[:, 3].any()                       # back_center 0x100: absent, silent

@@ -56,6 +56,33 @@ def test_golden_vectors_big_blocks():
         assert hashlib.sha256(data).hexdigest() == v["sha256"], v["name"]
 
 
+SIZED = json.load(open(os.path.join(GOLDEN, "flac_vectors_sized.json")))["vectors"]
+
+
+@pytest.mark.parametrize("preset", ["8", "5", "2", "0"])
+def test_golden_vectors_sized_reads(preset):
+    """reference-encoder sha256 for streams cut by short/long reads
+    (explicit frame sizes, flac.c:244-274, 412-518;
+    tests/golden/make_golden_sized.py)"""
+    cases = [v for v in SIZED if v["preset"] == preset]
+    assert len(cases) == 36
+    for v in cases:
+        pcm = signals.make(v["kind"], v["n"], v["channels"], v["bps"], seed=v["seed"])
+        data, lst = oracle_port.encode(pcm, v["channels"], v["bps"], 44100,
+                                       frame_sizes=v["read_sizes"],
+                                       **oracle_port.PRESETS[preset])
+        assert [n for _, n in lst] == v["frame_lengths"], v["name"]
+        assert oracle_port.cut_frames(v["n"], oracle_port.PRESETS[preset]["block_size"],
+                                      v["read_sizes"]) == v["frame_lengths"]
+        assert len(data) == v["bytes"], v["name"]
+        assert hashlib.sha256(data).hexdigest() == v["sha256"], v["name"]
+        if max(v["frame_lengths"]) <= oracle_port.PRESETS[preset]["block_size"]:
+            # (a longer frame exceeds STREAMINFO's maximum block size, which
+            # the reference writes as the option: its decoder rejects it)
+            dec, _, _, _ = oracle_port.decode(data)
+            assert np.array_equal(dec, pcm[:len(dec)])
+
+
 def test_golden_vectors_round_trip():
     for v in VECTORS[::7]:
         pcm = make_pcm(v)
@@ -148,3 +175,21 @@ def test_port_matches_reference_live():
         ref = make_golden.ref_encode(pcm, ch, bps, preset)
         port, _ = oracle_port.encode(pcm, ch, bps, 44100, **oracle_port.PRESETS[preset])
         assert port == ref, (preset, ch, bps, kind, n)
+
+
+@pytest.mark.skipif(not os.path.exists(oracle_port.REF_FLACENC_SIZED),
+                    reason="reference build oracle/_ref absent (GPU box)")
+def test_port_matches_reference_sized_reads_live():
+    """random read sizes through the reference's encoders_encode_flac
+    (oracle/ref_sized_reads.c) against the port's flacport_encode_sizes"""
+    rng = np.random.default_rng(11)
+    for k in range(10):
+        preset = str(k % 9)
+        ch, bps = [(1, 16), (2, 16), (2, 24), (6, 24), (1, 8)][k % 5]
+        sizes = [int(x) for x in rng.integers(1, 9000, int(rng.integers(1, 6)))]
+        n = int(rng.integers(1, 20000))
+        pcm = signals.make(["tone", "noise", "chirp"][k % 3], n, ch, bps, seed=k)
+        opts = oracle_port.PRESETS[preset]
+        ref = oracle_port.ref_encode_sized(pcm, ch, bps, 44100, sizes, **opts)
+        port, _ = oracle_port.encode(pcm, ch, bps, 44100, frame_sizes=sizes, **opts)
+        assert port == ref, (preset, ch, bps, sizes, n)

@@ -10,4 +10,4 @@ make -s -C "$C" -j8 ../audiotools/libatgpu.so
 mkdir -p "$C/obj_$name" "$R/exp"
 cp -p "$C"/obj/*.o "$C/obj_$name/"
 rm -f "$C/obj_$name/${src%.hip}.o"
-make -s -C "$C" OBJDIR="obj_$name" OUT="$R/exp/libatgpu_$name.so" EXTRA="$*" "$R/exp/libatgpu_$name.so"
+make -s -C "$C" OBJDIR="obj_$name" OUT="$R/exp/libatgpu_$name.so" EXTRA="-DATG_EXPERIMENT_BUILD $*" "$R/exp/libatgpu_$name.so"

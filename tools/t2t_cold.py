@@ -1,0 +1,147 @@
+"""track2track in its true shape: one fresh process per track.
+
+track2track runs every conversion in a new multiprocessing.Process
+(ExecProgressQueue.spawn, reference audiotools/__init__.py:5494-5521;
+track2track:650-669), so under the drop-in each track pays interpreter
+start, imports, HIP init, code-object load, engine creation and its first
+launches before it encodes.  This probe runs N WAV files with at most J
+processes alive, one process per file, from a parent that never touches the
+GPU, and breaks the per-process time into phases; the reference encoder
+(oracle/_ref/flacenc, one process per file, J at a time) runs the same files
+beside it when present.
+
+  python tools/t2t_cold.py J [N] [--frames F]      -> JSON lines
+  python tools/t2t_cold.py --one in.wav out.flac   (a child)
+"""
+import time
+
+T_START = time.time()  # noqa: E402  (first statement: process start, near enough)
+
+import json  # noqa: E402
+import os  # noqa: E402
+import struct  # noqa: E402
+import subprocess  # noqa: E402
+import sys  # noqa: E402
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+FLAC8 = dict(block_size=4096, max_lpc_order=12, min_residual_partition_order=0,
+             max_residual_partition_order=6, mid_side=1, adaptive_mid_side=0,
+             exhaustive_model_search=1)
+
+
+def child(wav_in, flac_out):
+    t = {"start": T_START}
+    import numpy  # noqa: F401
+    t["numpy"] = time.time()
+    sys.path.insert(0, os.path.join(ROOT, "python-audio-tools_amd"))
+    import audiotools
+    from audiotools import encoders, wav
+    t["audiotools"] = time.time()
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    n = ctypes.c_int()
+    hip.hipGetDeviceCount(ctypes.byref(n))  # HIP runtime up (hipInit)
+    t["hip_init"] = time.time()
+    offs = encoders.encode_flac(flac_out, audiotools.BufferedPCMReader(wav.WaveReader(wav_in)),
+                                **FLAC8)
+    t["encode"] = time.time()
+    print(json.dumps({"t": t, "frames": len(offs)}), flush=True)
+    return 0
+
+
+def write_wavs(d, n_files, frames):
+    import numpy as np
+    rng = np.random.default_rng(7)
+    files = []
+    n = frames * 4096
+    for k in range(n_files):
+        x = np.cumsum(rng.integers(-300, 301, 2 * n)).clip(-30000, 30000).astype("<i2")
+        data = x.tobytes()
+        fn = os.path.join(d, "t%04d.wav" % k)
+        with open(fn, "wb") as f:
+            f.write(struct.pack("<4sI4s4sIHHIIHH4sI", b"RIFF", 36 + len(data), b"WAVE",
+                                b"fmt ", 16, 1, 2, 44100, 44100 * 4, 4, 16, b"data",
+                                len(data)))
+            f.write(data)
+        files.append(fn)
+    return files
+
+
+def run_pool(cmds, j):
+    """run the commands, at most j alive; -> (wall s, [(spawn time, stdout)])"""
+    t0 = time.time()
+    pending, alive, done = list(cmds), [], []
+    while pending or alive:
+        while pending and len(alive) < j:
+            c = pending.pop(0)
+            alive.append((time.time(), subprocess.Popen(c, stdout=subprocess.PIPE,
+                                                        stderr=subprocess.PIPE)))
+        still = []
+        for ts, p in alive:
+            if p.poll() is None:
+                still.append((ts, p))
+                continue
+            out, err = p.communicate()
+            if p.returncode:
+                raise RuntimeError("child failed: %s" % err.decode()[-2000:])
+            done.append((ts, out.decode()))
+        alive = still
+        time.sleep(0.0005)
+    return time.time() - t0, done
+
+
+def main():
+    if sys.argv[1] == "--one":
+        return child(sys.argv[2], sys.argv[3])
+    import tempfile
+    j = int(sys.argv[1])
+    n_files = int(sys.argv[2]) if len(sys.argv) > 2 and not sys.argv[2].startswith("-") else 4 * j
+    frames = 64
+    if "--frames" in sys.argv:
+        frames = int(sys.argv[sys.argv.index("--frames") + 1])
+    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
+        files = write_wavs(d, n_files, frames)
+        gdir = os.path.join(d, "gpu")
+        os.mkdir(gdir)
+        cmds = [[sys.executable, os.path.abspath(__file__), "--one", fn,
+                 os.path.join(gdir, os.path.basename(fn)[:-4] + ".flac")] for fn in files]
+        wall, done = run_pool(cmds, j)
+        phases = {}
+        keys = ["numpy", "audiotools", "hip_init", "encode"]
+        for ts, out in done:
+            t = json.loads(out.strip().splitlines()[-1])["t"]
+            prev = ts
+            phases.setdefault("spawn_to_start", []).append(t["start"] - ts)
+            prev = t["start"]
+            for k in keys:
+                phases.setdefault(k, []).append(t[k] - prev)
+                prev = t[k]
+            phases.setdefault("exit", []).append(0.0)
+        total_frames = n_files * frames
+        res = {"processes": j, "files": n_files, "frames_per_file": frames,
+               "wall_s": round(wall, 3), "frames_per_s": round(total_frames / wall, 1),
+               "per_process_ms_mean": {k: round(1e3 * sum(v) / len(v), 1)
+                                       for k, v in phases.items() if k != "exit"},
+               "per_process_ms_max": {k: round(1e3 * max(v), 1)
+                                      for k, v in phases.items() if k != "exit"}}
+        ref = os.path.join(ROOT, "oracle", "_ref", "flacenc")
+        if os.path.exists(ref):
+            rdir = os.path.join(d, "ref")
+            os.mkdir(rdir)
+            rc = [["sh", "-c", "tail -c +45 %s | %s -c 2 -r 44100 -b 16 -B 4096 -l 12 -P 0 "
+                   "-R 6 -m -e %s > /dev/null" % (fn, ref, os.path.join(rdir, os.path.basename(
+                       fn)[:-4] + ".flac"))] for fn in files]
+            rwall, _ = run_pool(rc, j)
+            same = all(open(os.path.join(gdir, os.path.basename(f)[:-4] + ".flac"), "rb").read()
+                       == open(os.path.join(rdir, os.path.basename(f)[:-4] + ".flac"),
+                               "rb").read() for f in files)
+            res["reference"] = {"wall_s": round(rwall, 3),
+                                "frames_per_s": round(total_frames / rwall, 1),
+                                "files_identical": same}
+        print(json.dumps(res), flush=True)
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
