@@ -85,9 +85,9 @@ def parse_args(argv=None):
     ap.add_argument("--no-host", action="store_true", help="skip the host-to-host leg")
     ap.add_argument("--no-t2t", action="store_true", help="skip the track2track leg")
     ap.add_argument("--t2t-procs", type=int, default=8,
-                    help="track2track leg: encoder processes sharing the GPU")
-    ap.add_argument("--t2t-worker", nargs=3, metavar=("LIST", "OUTDIR", "GO"),
-                    help=argparse.SUPPRESS)
+                    help="track2track leg: conversion processes alive at a time (-j)")
+    ap.add_argument("--t2t-files", type=int, default=128,
+                    help="track2track leg: 64-frame WAV files, one process each")
     ap.add_argument("--no-rg4", action="store_true", help="skip the config-4 ReplayGain leg")
     ap.add_argument("--rg4-seconds", type=int, default=10)
     ap.add_argument("--dec-inflight", type=int, default=3,
@@ -885,120 +885,54 @@ def _device_equal(torch, eng, d_ptr, ref, n_tracks=1):
     return False, n_tracks
 
 
-def t2t_worker(list_file, out_dir, go_file):
-    """one track2track encoder process (track2track:650-669 runs one process
-    per track, each calling encode_flac on its file): audiotools WaveReader
-    -> encoders.encode_flac (the streaming single-track path over the C
-    ABI) for every .wav in list_file, once go_file appears; prints its
-    timing as JSON"""
-    import audiotools
-    from audiotools import _atgpu, encoders, wav
-    _atgpu.load_library()
-    _atgpu.engine()  # HIP up before the clock
-    names = [ln.strip() for ln in open(list_file) if ln.strip()]
-    print(json.dumps({"ready": True}), flush=True)
-    while not os.path.exists(go_file):
-        time.sleep(0.001)
-    t0 = time.perf_counter()
-    frames = 0
-    for fn in names:
-        out = os.path.join(out_dir, os.path.basename(fn)[:-4] + ".flac")
-        r = wav.WaveReader(fn)
-        offs = encoders.encode_flac(out, audiotools.BufferedPCMReader(r), **FLAC8)
-        frames += len(offs)
-    print(json.dumps({"frames": frames, "seconds": time.perf_counter() - t0}), flush=True)
-    return 0
-
-
-def t2t_leg(args, pcm_host, n_samples, threads):
-    """track2track-shaped use of the drop-in (track2track
-    :650-669): --t2t-procs processes share the GPU, each encoding its share
-    of the tracks one file at a time through encode_flac(WaveReader) -- the
-    per-process, per-file path a track2track run takes, with WAV parsing and
-    file I/O inside the clock.  The same files through the reference encoder
-    (oracle/_ref/flacenc) at the same process count beside it; every GPU
-    .flac is compared with the reference's."""
-    import oracle_port
-    n_tracks = min(len(pcm_host) // (n_samples * 2), 8 * args.t2t_procs)
+def t2t_leg(args):
+    """track2track in its true shape (reference
+    audiotools/__init__.py:5494-5521, track2track:650-669): a driver process
+    that imported audiotools but never touched the GPU forks one conversion
+    process per WAV file, --t2t-procs at a time, each calling
+    encode_flac(WaveReader) once and exiting -- fork, HIP-side setup and the
+    encode all inside the clock.  The first conversion starts the encoder
+    service (atgpu-encoderd), which then encodes every process's segments,
+    batching concurrent ones.  The reference encoder runs the same files one
+    process per file at the same count; every file is compared with it
+    (tools/t2t_cold.py --fork, run as a child of this process)."""
     procs = max(1, args.t2t_procs)
-    out = {"metric": "track2track-shaped FLAC-8 encode: %d processes x encode_flac(WaveReader) "
-                     "on one GPU, frames/s" % procs}
-    with tempfile.TemporaryDirectory(dir="/dev/shm" if os.path.isdir("/dev/shm") else None) as d:
-        files = []
-        for t in range(n_tracks):
-            fn = os.path.join(d, "t%04d.wav" % t)
-            x = pcm_host[t * n_samples * 2:(t + 1) * n_samples * 2]
-            data = x.astype("<i2").tobytes()
-            with open(fn, "wb") as f:
-                f.write(struct.pack("<4sI4s4sIHHIIHH4sI", b"RIFF", 36 + len(data), b"WAVE",
-                                    b"fmt ", 16, 1, 2, 44100, 44100 * 4, 4, 16, b"data",
-                                    len(data)))
-                f.write(data)
-            files.append(fn)
-        gdir = os.path.join(d, "gpu")
-        os.mkdir(gdir)
-        go = os.path.join(d, "go")
-        workers = []
-        for k in range(procs):
-            lf = os.path.join(d, "list%d" % k)
-            with open(lf, "w") as f:
-                f.write("\n".join(files[k::procs]))
-            # one engine per process, streams created on first use (the
-            # many-processes-per-GPU setting, INTEGRATION.md)
-            workers.append(subprocess.Popen(
-                [sys.executable, os.path.abspath(__file__), "--t2t-worker", lf, gdir, go],
-                stdout=subprocess.PIPE, text=True,
-                env=dict(os.environ, ATG_ENGINE_STREAMS="lazy")))
-        for w in workers:
-            json.loads(w.stdout.readline())  # ready
-        t0 = time.perf_counter()
-        open(go, "w").close()
-        stats = [json.loads(w.stdout.readline()) for w in workers]
-        wall = time.perf_counter() - t0
-        if any(w.wait() for w in workers):
-            raise RuntimeError("a track2track worker failed")
-        frames = sum(st["frames"] for st in stats)
-        out.update({"value": round(frames / wall, 1), "unit": "frames/s",
-                    "processes": procs, "engine_streams": "lazy", "tracks": n_tracks, "frames": frames,
-                    "wall_s": round(wall, 3),
-                    "per_process_frames_per_s": round(frames / procs / wall, 1)})
-        # the reference encoder, one process per track, the same count at a time
-        # (skipped with --no-cpu-baseline: e.g. under a profiler, whose
-        # preloaded library the child processes would inherit)
-        exe = oracle_port.REF_FLACENC
-        if os.path.exists(exe) and not args.no_cpu_baseline:
-            rargs = [exe, "-c", "2", "-r", "44100", "-b", "16", "-B", "4096", "-l", "12", "-P",
-                     "0", "-R", "6", "-m", "-e"]
-            rdir = os.path.join(d, "ref")
-            os.mkdir(rdir)
-
-            def one(t):
-                with open(files[t], "rb") as f:
-                    raw = f.read()[44:]
-                fo = os.path.join(rdir, "t%04d.flac" % t)
-                subprocess.run(rargs + [fo], input=raw, stdout=subprocess.DEVNULL, check=True)
-
-            rdt = _parallel(n_tracks, procs, one)
-            same = all(open(os.path.join(gdir, "t%04d.flac" % t), "rb").read() ==
-                       open(os.path.join(rdir, "t%04d.flac" % t), "rb").read()
-                       for t in range(n_tracks))
-            out["cpu_baseline"] = {"value": round(frames / rdt, 1), "unit": "frames/s",
-                                   "cores": procs, "kind": "reference",
-                                   "sample": "the same %d files, reference encoder "
-                                             "(oracle/_ref/flacenc) one process per track, "
-                                             "%d at a time, %.1f s" % (n_tracks, procs, rdt)}
-            out["gpu_files_identical_to_reference"] = same
+    n_files = max(procs, args.t2t_files)
+    cmd = [sys.executable, os.path.join(ROOT, "tools", "t2t_cold.py"), str(procs), str(n_files),
+           "--fork"]
+    env = dict(os.environ)
+    env.pop("ATG_ENCODER_SERVICE", None)
+    # a socket name of this run's own: never an idle service of another run
+    env["ATG_ENCODER_SOCKET"] = "atgpu-bench-%d" % os.getpid()
+    p = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    if p.returncode:
+        return {"error": p.stderr[-2000:]}
+    r = json.loads(p.stdout.strip().splitlines()[-1])
+    out = {"metric": "track2track FLAC-8 encode, one forked process per file (%d at a time), "
+                     "frames/s" % procs,
+           "value": r["frames_per_s"], "unit": "frames/s", "processes": procs,
+           "files": r["files"], "frames_per_file": r["frames_per_file"], "wall_s": r["wall_s"],
+           "encoder": r["encoder"], "per_process_ms_mean": r["per_process_ms_mean"],
+           "per_process_ms_max": r["per_process_ms_max"]}
+    ref = r.get("reference")
+    if ref:
+        out["cpu_baseline"] = {"value": ref["frames_per_s"], "unit": "frames/s",
+                               "cores": procs, "kind": "reference",
+                               "sample": "the same %d files, reference encoder "
+                                         "(oracle/_ref/flacenc) one process per file, %d at a "
+                                         "time, %.2f s" % (r["files"], procs, ref["wall_s"])}
+        out["gpu_files_identical_to_reference"] = ref["files_identical"]
     return out
 
 
-def rg4_leg(args, torch, dist, world, rank, device, barrier):
+def rg4_leg(args, torch, dist, world, rank, device, barrier, threads=16):
     """BASELINE config 4: ReplayGain album scan, 1024 tracks of
     --rg4-seconds s per GPU, one album per GPU: each
     rank's tracks are its album (title gains + the album gain/peak from the
     summed histogram); the albums' (gain, peak) go to every rank over RCCL
     (all_gather), and the whole set's gain/peak over an all-reduce of the
-    histograms (SUM) and peaks (MAX).  The first 64 tracks' title results
-    and the album of those 64 are checked against the CPU oracle."""
+    histograms (SUM) and peaks (MAX).  Every track's title gain and peak,
+    and the album gain and peak, are checked against the CPU oracle."""
     from audiotools import _atgpu
     n_tracks, n = 1024, args.rg4_seconds * 44100
     g = torch.Generator(device=device)
@@ -1054,20 +988,27 @@ def rg4_leg(args, torch, dist, world, rank, device, barrier):
                           "collective": "all_gather (gain, peak) + all_reduce SUM uint32[12000]"
                                         " / MAX f64 (RCCL)" if world > 1 else "none (1 rank)"}}
     if rank == 0 and not args.no_verify:
+        # every track's title gain and peak, and the album gain from the
+        # summed oracle histograms, against the CPU oracle
         import oracle_port
         oracle_port.load()
-        xh = x[:64 * n * 2].cpu().numpy()
-        bad, hsum, pmax = [], None, 0.0
+        xh = x.cpu().numpy()
+        bad, hists, peaks = [], [None] * n_tracks, [0.0] * n_tracks
 
         def one(k):
             A, pk = oracle_port.rg_title(xh[k * n * 2:(k + 1) * n * 2], 2, 16, 44100)
+            hists[k], peaks[k] = A, pk
             if not (oracle_port.rg_gain(A) == res[k].title_gain and pk == res[k].title_peak):
                 bad.append(k)
-            return A, pk
 
-        outs = [one(k) for k in range(64)]
-        out["verified_tracks"] = 64 - len(bad)
-        out["verified_vs_oracle"] = not bad
+        vdt = _parallel(n_tracks, threads, one)
+        album_ok = (oracle_port.rg_gain(np.sum(hists, axis=0).astype(np.uint32)) == album_gain
+                    and max(peaks) == album_peak)
+        del xh, hists
+        out["verified_tracks"] = n_tracks - len(bad)
+        out["verified_album"] = album_ok
+        out["verified_vs_oracle"] = not bad and album_ok
+        out["verify_s"] = round(vdt, 1)
     del x, hist
     return out
 
@@ -1197,8 +1138,6 @@ def selftest(args):
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
-    if args.t2t_worker:
-        return t2t_worker(*args.t2t_worker)
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # spawn the ranks before anything initialises a GPU (never re-exec)
         return launch(args, argv)
@@ -1274,6 +1213,60 @@ def main(argv=None):
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
     out = outs[(args.steps - 1) % depth]
+    # the batches below write their own buffers: `out` holds the images the
+    # parity check and the decode leg read
+    outs = [torch.empty(out_cap, dtype=torch.uint8, device=device) for _ in range(depth)]
+
+    def timed(tbl, steps):
+        """wall time of `steps` pipelined batches of table `tbl` (a
+        TrackTable, or a callable k -> TrackTable), max over ranks"""
+        barrier()
+        t1 = time.perf_counter()
+        for k in range(steps):
+            tb = tbl(k) if callable(tbl) else tbl
+            t = eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16, tb, 2, 16, 44100,
+                                        outs[k % depth].data_ptr(), out_cap)
+            pending.append(t)
+            if len(pending) >= depth:
+                eng.wait(pending.pop(0))
+        drain()
+        barrier()
+        dt = time.perf_counter() - t1
+        return reduce_max(torch, dist, dt, device) if world > 1 else dt
+
+    # ---- strong scaling (SURVEY 8(e)): the 1024-track batch split over the
+    # ranks, timed in the same run as the weak line above
+    strong = None
+    if world > 1 and args.scaling == "weak":
+        n_s = len(shard(world, rank, args.tracks, "strong"))
+        st_table = _atgpu.TrackTable(tracks[:n_s])
+        timed(st_table, 1)
+        dt = timed(st_table, args.steps)
+        tot = reduce_sum(torch, dist, n_s * args.frames * args.steps, device)
+        strong = {"value": round(tot / dt, 1), "unit": "frames/s",
+                  "ms_per_step": round(dt / args.steps * 1e3, 3),
+                  "tracks_total": args.tracks, "tracks_per_gpu": n_s,
+                  "bound": "per-track MD5 chain (~12 ms per 1 MiB track, serial) once a rank's "
+                           "batch is narrow; three batches in flight"}
+    # ---- per-batch host planning: every step a new track geometry (the
+    # plan cache misses; engine.hip get_plan), against the fixed geometry
+    plan_steps = min(args.steps, 10)
+
+    def varied(k):
+        lens = [n_samples - 4096 * ((i + k) % 3) for i in range(n_tracks)]
+        return _atgpu.TrackTable([(i * n_samples, lens[i]) for i in range(n_tracks)])
+
+    tables = [varied(k) for k in range(plan_steps)]  # built outside the clock
+    dt_var = timed(lambda k: tables[k], plan_steps)
+    dt_fix = timed(table, plan_steps)
+    plan_miss = {"steps": plan_steps,
+                 "ms_per_step_new_geometry": round(dt_var / plan_steps * 1e3, 3),
+                 "ms_per_step_same_geometry": round(dt_fix / plan_steps * 1e3, 3),
+                 "host_plan_ms_per_batch": round((dt_var - dt_fix) / plan_steps * 1e3, 3),
+                 "note": "each step's batch has different track lengths (frames drop per "
+                         "track by 0-2 frames in turn): the host plan, frame/track tables "
+                         "and their upload are redone every step"}
+    del tables
     del outs
     kt = {k: v / args.steps for k, v in kt_sum.items()}
     out_bytes = sum(int(r.bytes) for r in res)
@@ -1319,9 +1312,9 @@ def main(argv=None):
                                     barrier)
     t2t = rg4 = None
     if not args.no_t2t and rank == 0 and world == 1:
-        t2t = t2t_leg(args, pcm_host, n_samples, threads)
+        t2t = t2t_leg(args)
     if not args.no_rg4:
-        rg4 = rg4_leg(args, torch, dist, world, rank, device, barrier)
+        rg4 = rg4_leg(args, torch, dist, world, rank, device, barrier, threads)
     chain = None
     if not args.no_chain:
         chain = chain_leg(args, torch, dist, world, device, barrier, threads,
@@ -1460,6 +1453,8 @@ def main(argv=None):
         "chain": chain,
         "replaygain_config4": rg4,
         "track2track": t2t,
+        "strong_scaling": strong if world > 1 else {"note": "1 GPU: the same batch as value"},
+        "plan_per_batch": plan_miss,
     }
     print(json.dumps(line), flush=True)
     if world > 1:

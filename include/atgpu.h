@@ -178,6 +178,32 @@ atg_status atg_flac_encode_frames(atg_engine *eng, const atg_flac_options *opts,
                                   uint32_t sample_rate, uint64_t first_frame_number,
                                   uint8_t *out, uint64_t out_cap, uint64_t *out_bytes,
                                   uint32_t *frame_bytes);
+/* One segment of atg_flac_encode_frames_batch: PCM frames
+   [pcm_offset, pcm_offset + pcm_frames) of the batch buffer, cut as
+   atg_track, numbered from first_frame_number. */
+typedef struct {
+    uint64_t pcm_offset;
+    uint64_t pcm_frames;
+    const uint32_t *frame_sizes; /* NULL: block_size frames + a short last one */
+    uint64_t n_frame_sizes;
+    uint64_t first_frame_number;
+} atg_segment;
+
+/* atg_flac_encode_frames for many segments (of many tracks, from many
+   callers) in one GPU pass: what the encoder service (atgpu-encoderd)
+   runs for the encode_flac calls of concurrent processes.  Segments share
+   the options and the PCM format.  Segment k's frames land at
+   out + seg_offsets[k] (seg_bytes[k] bytes; offsets 16-byte aligned, packed
+   in segment order; out_cap >= the sum of atg_flac_max_frames_bytes rounded
+   up to 16 each); frame_bytes (may be NULL) receives every frame's size in
+   segment order.  The engine's results of earlier batches are gone. */
+atg_status atg_flac_encode_frames_batch(atg_engine *eng, const atg_flac_options *opts,
+                                        const void *pcm, atg_pcm_format format,
+                                        const atg_segment *segs, uint32_t n_segs,
+                                        uint32_t channels, uint32_t bits_per_sample,
+                                        uint32_t sample_rate, uint8_t *out, uint64_t out_cap,
+                                        uint64_t *seg_offsets, uint64_t *seg_bytes,
+                                        uint32_t *frame_bytes);
 /* worst-case bytes of atg_flac_encode_frames' output (0: invalid options) */
 uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_frames,
                                    const uint32_t *frame_sizes, uint64_t n_frame_sizes,
@@ -191,6 +217,32 @@ uint64_t atg_flac_stream_header(const atg_flac_options *opts, uint32_t channels,
                                 uint64_t total_samples, uint32_t min_frame_bytes,
                                 uint32_t max_frame_bytes, const uint8_t *md5, uint8_t *out,
                                 uint64_t cap);
+
+/* ------------------------------------------------------------------ */
+/* Encoder service.  track2track converts every track in a fresh process */
+/* (reference audiotools/__init__.py:5494-5521), and a process that      */
+/* brings up its own HIP context, engine and code objects pays ~0.3-0.5 s */
+/* for it.  atgpu-encoderd (beside libatgpu.so) owns one engine per GPU  */
+/* and encodes the segments of every client process, batching concurrent */
+/* clients' segments that share options and format into one GPU pass     */
+/* (atg_flac_encode_frames_batch).  The streaming encode_flac uses it.   */
+/* ------------------------------------------------------------------ */
+typedef struct atg_service atg_service;
+/* Connect to `device`'s service; with spawn != 0 start atgpu-encoderd when
+   none listens (never from a process that has opened the GPU itself: it may
+   not exec another program).  The service exits after an idle period. */
+atg_status atg_service_connect(int device, int spawn, atg_service **out);
+void atg_service_close(atg_service *svc);
+const char *atg_service_last_error(void);
+/* atg_flac_encode_frames' contract, encoded by the service */
+atg_status atg_service_encode_frames(atg_service *svc, const atg_flac_options *opts,
+                                     const void *pcm, atg_pcm_format format,
+                                     uint64_t pcm_frames, const uint32_t *frame_sizes,
+                                     uint64_t n_frame_sizes, uint32_t channels,
+                                     uint32_t bits_per_sample, uint32_t sample_rate,
+                                     uint64_t first_frame_number, uint8_t *out,
+                                     uint64_t out_cap, uint64_t *out_bytes,
+                                     uint32_t *frame_bytes);
 
 /* PCM bytes per chunk of atg_flac_encode_host's pipeline (default 512 MiB):
    consecutive tracks are grouped into chunks of about this much PCM, and
@@ -222,7 +274,9 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
    ATG_ERR_INVALID (wait the oldest first); atg_flac_encode_device takes a
    slot too and fails the same way, and atg_flac_encode_host fails while any
    ticket is unwaited.  A waited ticket's
-   results stay readable until its slot is reused three enqueues later. */
+   results stay readable until its slot is reused three enqueues later, or
+   until a streaming call (atg_flac_encode_frames[_batch]), which always
+   takes slot 0. */
 atg_status atg_flac_encode_device_async(atg_engine *eng, const atg_flac_options *opts,
                                         const void *d_pcm, atg_pcm_format format,
                                         const atg_track *tracks, uint32_t n_tracks,

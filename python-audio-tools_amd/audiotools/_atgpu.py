@@ -34,6 +34,8 @@ EXPORTS = (
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
     "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
+    "atg_flac_encode_frames_batch", "atg_service_connect", "atg_service_close",
+    "atg_service_last_error", "atg_service_encode_frames",
     "atg_host_free", "atg_device_alloc",
     "atg_device_free", "atg_copy_to_device", "atg_copy_device", "atg_copy_to_host",
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",

@@ -266,7 +266,8 @@ uint32_t qlp_precision_for(uint32_t n)
 
 atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_t n_tracks,
                      uint32_t channels, uint32_t bps, uint32_t rate, Plan &pl,
-                     bool frames_only = false, uint32_t index_base = 0)
+                     bool frames_only = false, uint32_t index_base = 0,
+                     const uint32_t *index_bases = nullptr)
 {
     if (!o)
         return fail(ATG_ERR_INVALID, "options is NULL");
@@ -368,7 +369,7 @@ atg_status make_plan(const atg_flac_options *o, const atg_track *tracks, uint32_
         f.pcm_start = pl.tracks[t].pcm_start + start[t];
         f.n = lens[i];
         f.track = t;
-        f.index = index_base + idx[t]++;
+        f.index = (index_bases ? index_bases[t] : index_base) + idx[t]++;
         f.win_off = 0;
         start[t] += lens[i];
     }
@@ -1529,42 +1530,52 @@ uint64_t atg_flac_stream_header(const atg_flac_options *o, uint32_t channels, ui
     return need;
 }
 
-atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, const void *pcm,
-                                  atg_pcm_format format, uint64_t pcm_frames,
-                                  const uint32_t *frame_sizes, uint64_t n_frame_sizes,
-                                  uint32_t channels, uint32_t bps, uint32_t rate,
-                                  uint64_t first_frame_number, uint8_t *out, uint64_t out_cap,
-                                  uint64_t *out_bytes, uint32_t *frame_bytes)
+atg_status atg_flac_encode_frames_batch(atg_engine *e, const atg_flac_options *opts,
+                                        const void *pcm, atg_pcm_format format,
+                                        const atg_segment *segs, uint32_t n, uint32_t channels,
+                                        uint32_t bps, uint32_t rate, uint8_t *out,
+                                        uint64_t out_cap, uint64_t *seg_offsets,
+                                        uint64_t *seg_bytes, uint32_t *frame_bytes)
 {
     ATG_HANDLE_LOCK(e);
-    if (!e || (!pcm && pcm_frames) || !out_bytes)
+    if (!e || (!segs && n) || (!seg_offsets && n) || (!seg_bytes && n))
         return fail(ATG_ERR_INVALID, "NULL argument");
     if (format == ATG_PCM_S16 && bps > 16)
         return fail(ATG_ERR_INVALID, "S16 container with bits_per_sample > 16");
-    const uint64_t nfr_max = frame_sizes ? n_frame_sizes
-                                         : (opts && opts->block_size
-                                                ? (pcm_frames + opts->block_size - 1) / opts->block_size
-                                                : 0);
-    // the frame header's UTF-8 number holds 31 bits (flac.c:1531-1566)
-    if (first_frame_number + nfr_max > 0x7FFFFFFFull)
-        return fail(ATG_ERR_INVALID, "frame numbers beyond 2^31 - 1");
     for (EncSlot &s2 : e->slot)
         if (s2.busy)
             return fail(ATG_ERR_INVALID, "an async encode batch is in flight: wait for it first");
-    atg_track tr;
-    tr.pcm_offset = 0;
-    tr.pcm_frames = pcm_frames;
-    tr.frame_sizes = frame_sizes;
-    tr.n_frame_sizes = n_frame_sizes;
+    std::vector<atg_track> tr(n);
+    std::vector<uint32_t> bases(n);
+    uint64_t pcm_end = 0;
+    for (uint32_t k = 0; k < n; ++k) {
+        const atg_segment &g = segs[k];
+        const uint64_t nfr = g.frame_sizes ? g.n_frame_sizes
+                                           : (opts && opts->block_size
+                                                  ? (g.pcm_frames + opts->block_size - 1) /
+                                                        opts->block_size
+                                                  : 0);
+        // the frame header's UTF-8 number holds 31 bits (flac.c:1531-1566)
+        if (g.first_frame_number + nfr > 0x7FFFFFFFull)
+            return fail(ATG_ERR_INVALID, "frame numbers beyond 2^31 - 1");
+        tr[k].pcm_offset = g.pcm_offset;
+        tr[k].pcm_frames = g.pcm_frames;
+        tr[k].frame_sizes = g.frame_sizes;
+        tr[k].n_frame_sizes = g.n_frame_sizes;
+        bases[k] = (uint32_t)g.first_frame_number;
+        pcm_end = std::max<uint64_t>(pcm_end, g.pcm_offset + g.pcm_frames);
+    }
+    if (!pcm && pcm_end)
+        return fail(ATG_ERR_INVALID, "NULL pcm");
     auto pl = std::make_shared<Plan>();
-    atg_status st = make_plan(opts, &tr, 1, channels, bps, rate, *pl, true,
-                              (uint32_t)first_frame_number);
+    atg_status st = make_plan(opts, tr.data(), n, channels, bps, rate, *pl, true, 0,
+                              bases.data());
     if (st != ATG_OK)
         return st;
     HIP_TRY(hipSetDevice(e->device));
     HostStage &h = e->hs[0];
     const size_t elem = format == ATG_PCM_S16 ? 2 : 4;
-    const uint64_t in_bytes = pcm_frames * channels * elem;
+    const uint64_t in_bytes = pcm_end * channels * elem;
     HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
     HIP_TRY(h.d_img.ensure(pl->out_bytes + 16));
     // the previous host-pipeline batch is finished (no slot busy); its
@@ -1572,8 +1583,9 @@ atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, c
     HIP_TRY(hipStreamWaitEvent(e->s_main, h.ev_packed, 0));
     if (in_bytes)
         HIP_TRY(hipMemcpyAsync(h.d_pcm.p, pcm, in_bytes, hipMemcpyHostToDevice, e->s_main));
-    // a synchronous segment (no slot busy, checked above) always takes slot
-    // 0: one aux stream for a streaming process's whole life
+    // a synchronous call (no slot busy, checked above) always takes slot 0:
+    // one aux stream for a streaming process's whole life.  The slot's
+    // earlier results are gone with it (atgpu.h)
     e->next_ticket += (kEncSlots - e->next_ticket % kEncSlots) % kEncSlots;
     EncSlot *sl = nullptr;
     uint64_t ticket = 0;
@@ -1594,20 +1606,73 @@ atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, c
     st = wait_ticket(e, ticket, sl);
     if (st != ATG_OK)
         return st;
-    const uint64_t nb = sl->tout_h[0].bytes;
-    *out_bytes = nb;
-    if (nb > out_cap)
-        return fail(ATG_ERR_CAPACITY, "output buffer too small for the segment's frames");
-    if (nb) {
-        HIP_TRY(hipMemcpyAsync(out, h.d_img.p, nb, hipMemcpyDeviceToHost, e->s_main));
+    // the segments' frames packed back to back, 16-byte aligned
+    uint64_t pos = 0;
+    HIP_TRY(ensure_pinned(h.p_off, h.p_off_cap, std::max<size_t>(n, 1)));
+    for (uint32_t k = 0; k < n; ++k) {
+        seg_offsets[k] = pos;
+        seg_bytes[k] = sl->tout_h[k].bytes;
+        h.p_off[k] = pos;
+        pos += (sl->tout_h[k].bytes + 15u) & ~15ull;
+    }
+    if (pos > out_cap)
+        return fail(ATG_ERR_CAPACITY, "output buffer too small for the segments' frames");
+    if (pos) {
+        HIP_TRY(h.d_off.ensure(std::max<size_t>(n, 1) * sizeof(uint64_t)));
+        HIP_TRY(h.d_pack.ensure(pos));
+        HIP_TRY(hipMemcpyAsync(h.d_off.p, h.p_off, n * sizeof(uint64_t), hipMemcpyHostToDevice,
+                               e->s_main));
+        HIP_TRY(launch_pack_images((const uint8_t *)h.d_img.p, (const TrackInfo *)sl->tracks.p,
+                                   (const TrackOut *)sl->tout.p, (const uint64_t *)h.d_off.p, n,
+                                   (uint8_t *)h.d_pack.p, e->s_main));
+        HIP_TRY(hipEventRecord(h.ev_packed, e->s_main));
+        HIP_TRY(hipMemcpyAsync(out, h.d_pack.p, pos, hipMemcpyDeviceToHost, e->s_main));
         HIP_TRY(hipStreamSynchronize(e->s_main));
     }
     if (frame_bytes) {
-        const TrackInfo &ti = pl->tracks[0];
-        for (uint32_t i = 0; i < ti.n_frames; ++i)
-            frame_bytes[i] = sl->fdesc_h[pl->order[ti.first_pos + i]].bytes;
+        uint64_t q = 0;
+        for (uint32_t k = 0; k < n; ++k) {
+            const TrackInfo &ti = pl->tracks[k];
+            for (uint32_t i = 0; i < ti.n_frames; ++i)
+                frame_bytes[q++] = sl->fdesc_h[pl->order[ti.first_pos + i]].bytes;
+        }
     }
     return ATG_OK;
+}
+
+atg_status atg_flac_encode_frames(atg_engine *e, const atg_flac_options *opts, const void *pcm,
+                                  atg_pcm_format format, uint64_t pcm_frames,
+                                  const uint32_t *frame_sizes, uint64_t n_frame_sizes,
+                                  uint32_t channels, uint32_t bps, uint32_t rate,
+                                  uint64_t first_frame_number, uint8_t *out, uint64_t out_cap,
+                                  uint64_t *out_bytes, uint32_t *frame_bytes)
+{
+    if (!e || (!pcm && pcm_frames) || !out_bytes)
+        return fail(ATG_ERR_INVALID, "NULL argument");
+    atg_segment g;
+    g.pcm_offset = 0;
+    g.pcm_frames = pcm_frames;
+    g.frame_sizes = frame_sizes;
+    g.n_frame_sizes = n_frame_sizes;
+    g.first_frame_number = first_frame_number;
+    uint64_t off = 0;
+    // the packed segment is 16-byte padded: room for it, then the true size
+    const uint64_t need = atg_flac_max_frames_bytes(opts, pcm_frames, frame_sizes,
+                                                    n_frame_sizes, channels, bps);
+    if (need && out_cap < ((need + 15u) & ~15ull)) {
+        std::vector<uint8_t> tmp((need + 15u) & ~15ull);
+        const atg_status st = atg_flac_encode_frames_batch(
+            e, opts, pcm, format, &g, 1, channels, bps, rate, tmp.data(), tmp.size(), &off,
+            out_bytes, frame_bytes);
+        if (st != ATG_OK)
+            return st;
+        if (*out_bytes > out_cap)
+            return fail(ATG_ERR_CAPACITY, "output buffer too small for the segment's frames");
+        std::memcpy(out, tmp.data(), *out_bytes);
+        return ATG_OK;
+    }
+    return atg_flac_encode_frames_batch(e, opts, pcm, format, &g, 1, channels, bps, rate, out,
+                                        out_cap, &off, out_bytes, frame_bytes);
 }
 
 uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_frames,

@@ -78,7 +78,9 @@ static void *md5_segment(void *arg)
 
 /* ------------------------------------------------------------- module */
 static PyObject *g_framelist_type; /* audiotools.pcm.FrameList */
-static atg_engine *g_eng;
+static atg_engine *g_eng;      /* this process's own engine (no service) */
+static atg_service *g_svc;     /* the encoder service (atgpu-encoderd) */
+static int g_svc_mode = -1;    /* -1 undecided, 0 own engine, 1 service */
 
 static int engine_device(void)
 {
@@ -115,26 +117,45 @@ typedef struct {
     md5_ctx md5;
 } enc_state;
 
-/* encode and write the collected segment; appends to the offsets list */
-static int flush_segment(enc_state *s)
+/* where this process's segments are encoded: the encoder service (one
+   process per GPU owning the engine, started on first use; a track2track
+   conversion process then never brings up HIP itself) unless
+   ATG_ENCODER_SERVICE=off, or the service cannot be reached -- then an
+   engine of this process's own.  Decided once per process. */
+static int choose_backend(void)
 {
-    if (!s->n_sizes)
-        return 0;
-    if (!g_eng) {
+    if (g_svc_mode < 0) {
+        const char *v = getenv("ATG_ENCODER_SERVICE");
+        g_svc_mode = !(v && (!strcmp(v, "off") || !strcmp(v, "0")));
+        if (g_svc_mode && atg_service_connect(engine_device(), 1, &g_svc) != ATG_OK)
+            g_svc_mode = 0;
+    }
+    if (!g_svc_mode && !g_eng) {
         const atg_status st = atg_engine_create_ex(engine_device(), ATG_ENGINE_STREAMING, &g_eng);
         if (st != ATG_OK) {
             raise_atg(st);
             return -1;
         }
     }
+    return 0;
+}
+
+/* encode and write the collected segment; appends to the offsets list */
+static int flush_segment(enc_state *s)
+{
+    if (!s->n_sizes)
+        return 0;
+    if (choose_backend() < 0)
+        return -1;
     const size_t elem = s->bps <= 16 ? 2 : 4;
     const uint64_t frames = s->pcm_len / (elem * s->channels);
-    const uint64_t cap = atg_flac_max_frames_bytes(&s->o, frames, s->sizes, s->n_sizes,
-                                                   s->channels, s->bps);
+    uint64_t cap = atg_flac_max_frames_bytes(&s->o, frames, s->sizes, s->n_sizes,
+                                             s->channels, s->bps);
     if (!cap) {
         PyErr_SetString(PyExc_ValueError, "invalid encoder options");
         return -1;
     }
+    cap = (cap + 15u) & ~(uint64_t)15u; /* the engine packs segments 16-byte aligned */
     if (cap > s->out_cap) {
         uint8_t *p = (uint8_t *)PyMem_Realloc(s->out, cap);
         if (!p) {
@@ -147,16 +168,43 @@ static int flush_segment(enc_state *s)
     uint64_t nb = 0;
     atg_status st;
     md5_job mj = {&s->md5, s->pcm, (size_t)(frames * s->channels), elem, (s->bps + 7) / 8};
+    const atg_pcm_format fmt = s->bps <= 16 ? ATG_PCM_S16 : ATG_PCM_S32;
+    const char *svc_err = NULL;
+    int lost = 0;
     Py_BEGIN_ALLOW_THREADS
     pthread_t hasher;
     const int threaded = pthread_create(&hasher, NULL, md5_segment, &mj) == 0;
     if (!threaded)
         md5_segment(&mj);
-    st = atg_flac_encode_frames(g_eng, &s->o, s->pcm, s->bps <= 16 ? ATG_PCM_S16 : ATG_PCM_S32,
-                                frames, s->sizes, s->n_sizes, s->channels, s->bps, s->rate,
-                                s->frame_no, s->out, s->out_cap, &nb, s->frame_bytes);
+    if (g_svc) {
+        st = atg_service_encode_frames(g_svc, &s->o, s->pcm, fmt, frames, s->sizes, s->n_sizes,
+                                       s->channels, s->bps, s->rate, s->frame_no, s->out,
+                                       s->out_cap, &nb, s->frame_bytes);
+        if (st != ATG_OK)
+            svc_err = atg_service_last_error();
+        lost = st == ATG_ERR_DEVICE; /* the service went away: this process's own engine */
+    } else {
+        st = atg_flac_encode_frames(g_eng, &s->o, s->pcm, fmt, frames, s->sizes, s->n_sizes,
+                                    s->channels, s->bps, s->rate, s->frame_no, s->out,
+                                    s->out_cap, &nb, s->frame_bytes);
+    }
     if (threaded)
         pthread_join(hasher, NULL);
+    Py_END_ALLOW_THREADS
+    if (lost) {
+        atg_service_close(g_svc);
+        g_svc = NULL;
+        g_svc_mode = 0;
+        svc_err = NULL;
+        if (choose_backend() < 0)
+            return -1;
+        Py_BEGIN_ALLOW_THREADS
+        st = atg_flac_encode_frames(g_eng, &s->o, s->pcm, fmt, frames, s->sizes, s->n_sizes,
+                                    s->channels, s->bps, s->rate, s->frame_no, s->out,
+                                    s->out_cap, &nb, s->frame_bytes);
+        Py_END_ALLOW_THREADS
+    }
+    Py_BEGIN_ALLOW_THREADS
     if (st == ATG_OK && nb && fwrite(s->out, 1, nb, s->f) != nb)
         st = (atg_status)1; /* write error, below */
     Py_END_ALLOW_THREADS
@@ -165,7 +213,12 @@ static int flush_segment(enc_state *s)
         return -1;
     }
     if (st != ATG_OK) {
-        raise_atg(st);
+        if (svc_err) {
+            PyErr_SetString(st == ATG_ERR_INVALID || st == ATG_ERR_UNSUPPORTED
+                                ? PyExc_ValueError : PyExc_RuntimeError, svc_err);
+        } else {
+            raise_atg(st);
+        }
         return -1;
     }
     for (unsigned i = 0; i < s->n_sizes; ++i) {

@@ -390,8 +390,23 @@ struct NullSink {
 // selects: lanes holding different partition orders and Rice parameters
 // never branch apart (long unary codes, > 32 bits with their LSBs, take a
 // rare slow path).
-template <class P>
-__device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &sink)
+// Residual-loop reads.  A lane's next word is a dependent load every few
+// codes, and at one wave per SIMD (K2 has a lane per frame, ~1 k waves for a
+// config-2 batch) with 256 lanes per CU walking 256 different frames, the
+// vL1D thrashes and every such load is an L2 round trip (~1.9 k cycles per
+// residual measured).  Ring: the lane's words come from a 32-word LDS ring
+// that the wave refills at wave-uniform points -- every kRingG iterations
+// each lane commits the 8 words it loaded one period earlier and issues the
+// next 8 (two 16-byte loads) when the ring has room -- so the loop reads only
+// LDS, and a global load has a whole period to arrive.  A lane that runs
+// ahead of its ring (long codes) reads global memory directly.
+constexpr uint32_t kRing = 32;      // words per lane (power of 2)
+constexpr uint32_t kRingStride = 33; // LDS words between lanes (bank spread)
+constexpr uint32_t kRingG = 4;      // iterations per refill period
+
+template <class P, bool RING = false>
+__device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &sink,
+                                            uint32_t *ring = nullptr)
 {
     const uint32_t method = r.get(2);
     const uint32_t porder = r.get(4);
@@ -418,7 +433,21 @@ __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N,
     uint32_t off = r.pos & 31;
     uint32_t hi = bswap32(r.w[cw < r.last ? cw : r.last]);
     uint32_t lo = bswap32(r.w[cw + 1 < r.last ? cw + 1 : r.last]);
-    uint32_t nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+    uint32_t nx;
+    uint64_t fill = 0, pf = 0; // ring: words [fill - kRing, fill) committed; pending block at pf
+    uint4 pa = make_uint4(0, 0, 0, 0), pb = pa;
+    bool pend = false;
+    uint32_t it = 0;
+    if (RING) {
+        const uint64_t a0 = cw & ~3ull;
+#pragma unroll
+        for (uint32_t i = 0; i < 8; ++i)
+            ring[(a0 + i) & (kRing - 1)] = r.w[a0 + i < r.last ? a0 + i : r.last];
+        fill = a0 + 8;
+        nx = ring[(cw + 2) & (kRing - 1)];
+    } else {
+        nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+    }
 #endif
     while (k < total || hdrs < parts) {
 #if ATG_DEC_READER == 0
@@ -473,7 +502,41 @@ __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N,
             cw += need ? 1u : 0u;
             off -= need ? 32u : 0u;
         }
-        nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+        if (RING) {
+            if (cw + 2 < fill)
+                nx = ring[(cw + 2) & (kRing - 1)];
+            else
+                nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+            if ((++it & (kRingG - 1)) == 0) { // wave-uniform refill point
+                if (pend) {
+                    const uint32_t b = (uint32_t)pf & (kRing - 1); // pf is 4-word aligned
+                    ring[b] = pa.x;
+                    ring[b + 1] = pa.y;
+                    ring[b + 2] = pa.z;
+                    ring[b + 3] = pa.w;
+                    const uint32_t b2 = (b + 4) & (kRing - 1);
+                    ring[b2] = pb.x;
+                    ring[b2 + 1] = pb.y;
+                    ring[b2 + 2] = pb.z;
+                    ring[b2 + 3] = pb.w;
+                    fill = pf + 8;
+                    pend = false;
+                }
+                if (fill + 8 + 2 <= cw + kRing && fill + 8 <= r.last + 1) {
+                    pf = fill;
+                    if ((((uintptr_t)r.w) & 15u) == 0) {
+                        pa = *(const uint4 *)(r.w + fill);
+                        pb = *(const uint4 *)(r.w + fill + 4);
+                    } else { // a caller buffer aligned to 4 bytes only
+                        pa = make_uint4(r.w[fill], r.w[fill + 1], r.w[fill + 2], r.w[fill + 3]);
+                        pb = make_uint4(r.w[fill + 4], r.w[fill + 5], r.w[fill + 6], r.w[fill + 7]);
+                    }
+                    pend = true;
+                }
+            }
+        } else {
+            nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+        }
 #endif
         sink.step(v, !hdr);
         k += hdr ? 0u : 1u;
@@ -519,7 +582,8 @@ __device__ __forceinline__ int dec_subhdr(BitR &r, SubHdr &s)
 }
 
 // parse-only subframe (K2 and the chain's inline path)
-__device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps)
+template <bool RING = false>
+__device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps, uint32_t *ring = nullptr)
 {
     SubHdr sh;
     int rc = dec_subhdr(r, sh);
@@ -544,7 +608,7 @@ __device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps)
             for (uint32_t i = 0; i < sh.order; ++i)
                 r.get_signed(prec);
         }
-        rc = dec_residual(r, sh.order, N, np);
+        rc = dec_residual<NullSink, RING>(r, sh.order, N, np, ring);
         if (rc)
             return rc;
         if (sh.kind == 2 && sh.order > 4)
@@ -582,8 +646,10 @@ __device__ uint32_t crc16_range(const uint32_t *w, uint64_t b0, uint64_t b1,
 
 // one frame of the reference's read() loop, parse only: header, subframes
 // with N = MIN(block size, nlimit), byte align, CRC-16
+template <bool RING = false>
 __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const DecTrack &t,
-                            uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec)
+                            uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec,
+                            uint32_t *ring = nullptr)
 {
     BitR r;
     r.init(w, nw, pos * 8, t.end * 8);
@@ -599,7 +665,7 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
     const uint32_t N = (uint32_t)((uint64_t)h.bs < nlimit ? (uint64_t)h.bs : nlimit);
     for (uint32_t c = 0; c < h.ch; ++c) {
         rec.sub_bit[c] = (uint32_t)(r.abspos() - pos * 8);
-        const int rc = parse_subframe(r, N, sub_bps(h.assign, c, h.bps));
+        const int rc = parse_subframe<RING>(r, N, sub_bps(h.assign, c, h.bps), ring);
         if (rc) {
             rec.status = rc;
             return;
@@ -642,41 +708,69 @@ __device__ __forceinline__ uint32_t find_track(const DecTrack *tr, uint32_t nt, 
     return lo;
 }
 
-// K1: sync-code candidates.  Thread per 32-bit word; a position needs byte
-// 0xFF followed by 0xF8/0xF9 (14-bit sync 0x3FFE, reserved bit 0).
+// K1: sync-code candidates.  A position needs byte 0xFF followed by
+// 0xF8/0xF9 (14-bit sync 0x3FFE, reserved bit 0).  Grid-stride over 16-byte
+// chunks: a lane takes one 16-byte load (plus the next chunk's first word
+// for a sync code straddling the chunks), so the pass streams the buffer at
+// a few TB/s instead of launching a wave per 256 bytes; the header parse
+// runs only for the rare lanes holding a sync pattern.
+__device__ __forceinline__ bool sync_at(uint32_t a, uint32_t b, int k)
+{
+    const uint64_t pair = ((uint64_t)a << 32) | b;
+    return ((uint32_t)(pair >> (48 - 8 * k)) & 0xFFFEu) == 0xFFF8u;
+}
+
 __global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w, uint64_t nw,
                                                   uint64_t len, const DecTrack *__restrict__ tr,
                                                   uint32_t nt, uint32_t *__restrict__ ncand,
                                                   uint32_t cap, uint64_t *__restrict__ cand_pos,
                                                   uint32_t *__restrict__ cand_idx)
 {
-    const uint64_t gw = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (gw >= nw)
-        return;
-    const uint32_t a = bswap32(w[gw]);
-    const uint32_t b = gw + 1 < nw ? bswap32(w[gw + 1]) : 0u;
-    const uint64_t pair = ((uint64_t)a << 32) | b;
+    const uint64_t nchunk = (nw + 3) / 4;
+    const bool a16 = ((uintptr_t)w & 15u) == 0; // the API promises 4-byte alignment only
+    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunk;
+         c += (uint64_t)gridDim.x * blockDim.x) {
+        uint32_t v[5];
+        if (a16 && 4 * c + 4 <= nw) {
+            const uint4 q = *(const uint4 *)(w + 4 * c);
+            v[0] = q.x;
+            v[1] = q.y;
+            v[2] = q.z;
+            v[3] = q.w;
+        } else {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-        const uint32_t hi = (uint32_t)(pair >> (48 - 8 * k)) & 0xFFFFu;
-        if ((hi & 0xFFFEu) != 0xFFF8u)
-            continue;
-        const uint64_t p = gw * 4 + k;
-        if (p + 1 >= len)
-            continue;
-        const uint32_t t = find_track(tr, nt, p);
-        const DecTrack T = tr[t];
-        if (p < T.start || p >= T.end)
-            continue;
-        BitR r;
-        r.init(w, nw, p * 8, T.end * 8);
-        Hdr h;
-        if (dec_header(r, T, h) != FD_OK)
-            continue;
-        const uint32_t i = atomicAdd(ncand, 1u);
-        if (i < cap) { // over capacity: the host re-scans with room for all
-            cand_pos[i] = p;
-            cand_idx[p] = i;
+            for (int i = 0; i < 4; ++i)
+                v[i] = 4 * c + i < nw ? w[4 * c + i] : 0u;
+        }
+        v[4] = 4 * c + 4 < nw ? w[4 * c + 4] : 0u;
+        uint32_t hits = 0; // bit 4j+k: a sync pattern at byte 4j+k of the chunk
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint32_t a = bswap32(v[j]), b = bswap32(v[j + 1]);
+#pragma unroll
+            for (int k = 0; k < 4; ++k)
+                hits |= sync_at(a, b, k) ? 1u << (4 * j + k) : 0u;
+        }
+        while (hits) {
+            const int bit = __builtin_ctz(hits);
+            hits &= hits - 1;
+            const uint64_t p = 16 * c + (uint64_t)bit;
+            if (p + 1 >= len)
+                continue;
+            const uint32_t t = find_track(tr, nt, p);
+            const DecTrack T = tr[t];
+            if (p < T.start || p >= T.end)
+                continue;
+            BitR r;
+            r.init(w, nw, p * 8, T.end * 8);
+            Hdr h;
+            if (dec_header(r, T, h) != FD_OK)
+                continue;
+            const uint32_t i = atomicAdd(ncand, 1u);
+            if (i < cap) { // over capacity: the host re-scans with room for all
+                cand_pos[i] = p;
+                cand_idx[p] = i;
+            }
         }
     }
 }
@@ -689,13 +783,14 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
                                                   ParseRec *__restrict__ recs)
 {
     __shared__ uint16_t T[4][256];
+    __shared__ uint32_t ring[64 * kRingStride]; // the lanes' residual-word rings
     load_crc_lds(T);
     const uint32_t n = *ncand;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t p = cand_pos[i];
         const DecTrack t = tr[find_track(tr, nt, p)];
         ParseRec rec;
-        parse_frame(w, nw, p, t, ~0ull, T, rec);
+        parse_frame<true>(w, nw, p, t, ~0ull, T, rec, ring + threadIdx.x * kRingStride);
         recs[i] = rec;
     }
 }
@@ -1452,10 +1547,12 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     for (int pass = 0; pass < 2; ++pass) {
         DHIP(d->cand_pos.ensure(sizeof(uint64_t) * cap));
         DHIP(hipMemsetAsync(d->ncand.p, 0, sizeof(uint32_t), s));
+        // grid-stride: at most 8 workgroups of 256 per CU (2048 over 256 CUs)
         if (n && len)
-            hipLaunchKernelGGL(k_dec_scan, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, w,
-                               nw, len, dtr, n, (uint32_t *)d->ncand.p, (uint32_t)cap,
-                               (uint64_t *)d->cand_pos.p, (uint32_t *)d->cand_idx.p);
+            hipLaunchKernelGGL(k_dec_scan,
+                               dim3((unsigned)std::min<uint64_t>(((nw + 3) / 4 + 255) / 256, 2048)),
+                               dim3(256), 0, s, w, nw, len, dtr, n, (uint32_t *)d->ncand.p,
+                               (uint32_t)cap, (uint64_t *)d->cand_pos.p, (uint32_t *)d->cand_idx.p);
         DHIP(hipGetLastError());
         DHIP(hipMemcpyAsync(&found, d->ncand.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         DHIP(hipStreamSynchronize(s));

@@ -10,7 +10,10 @@ GPU, and breaks the per-process time into phases; the reference encoder
 (oracle/_ref/flacenc, one process per file, J at a time) runs the same files
 beside it when present.
 
-  python tools/t2t_cold.py J [N] [--frames F]      -> JSON lines
+  python tools/t2t_cold.py J [N] [--frames F] [--fork] [--own-engine]  -> JSON line
+    --fork: the parent imports audiotools and forks a process per file
+    (multiprocessing, as track2track); default: a fresh interpreter each
+    --own-engine: ATG_ENCODER_SERVICE=off (every process its own engine)
   python tools/t2t_cold.py --one in.wav out.flac   (a child)
 """
 import time
@@ -30,6 +33,17 @@ FLAC8 = dict(block_size=4096, max_lpc_order=12, min_residual_partition_order=0,
              exhaustive_model_search=1)
 
 
+def hip_init():
+    """with an engine per process (ATG_ENCODER_SERVICE=off) bring HIP up
+    first to time it apart; with the encoder service the process never does"""
+    if os.environ.get("ATG_ENCODER_SERVICE") == "off":
+        import ctypes
+        hip = ctypes.CDLL("libamdhip64.so")
+        n = ctypes.c_int()
+        hip.hipGetDeviceCount(ctypes.byref(n))
+    return time.time()
+
+
 def child(wav_in, flac_out):
     t = {"start": T_START}
     import numpy  # noqa: F401
@@ -38,16 +52,57 @@ def child(wav_in, flac_out):
     import audiotools
     from audiotools import encoders, wav
     t["audiotools"] = time.time()
-    import ctypes
-    hip = ctypes.CDLL("libamdhip64.so")
-    n = ctypes.c_int()
-    hip.hipGetDeviceCount(ctypes.byref(n))  # HIP runtime up (hipInit)
-    t["hip_init"] = time.time()
+    t["hip_init"] = hip_init()
     offs = encoders.encode_flac(flac_out, audiotools.BufferedPCMReader(wav.WaveReader(wav_in)),
                                 **FLAC8)
     t["encode"] = time.time()
     print(json.dumps({"t": t, "frames": len(offs)}), flush=True)
     return 0
+
+
+def fork_child(wav_in, flac_out, q, t_fork):
+    """the body of a track2track conversion process (a forked
+    multiprocessing.Process, ExecProgressQueue.spawn): audiotools is already
+    imported by the parent, which never touched the GPU"""
+    import audiotools
+    from audiotools import encoders, wav
+    t = {"start": time.time()}
+    t["hip_init"] = hip_init()
+    offs = encoders.encode_flac(flac_out, audiotools.BufferedPCMReader(wav.WaveReader(wav_in)),
+                                **FLAC8)
+    t["encode"] = time.time()
+    q.put(json.dumps({"t": t, "frames": len(offs), "t_fork": t_fork}))
+
+
+def run_forks(files, gdir, j):
+    """one forked process per file, at most j alive (track2track -j);
+    -> (wall s, [(fork time, child JSON)])"""
+    import multiprocessing as mp
+    ctx = mp.get_context("fork")
+    q = ctx.Queue()
+    t0 = time.time()
+    pending, alive, done = list(files), [], []
+    while pending or alive:
+        while pending and len(alive) < j:
+            fn = pending.pop(0)
+            out = os.path.join(gdir, os.path.basename(fn)[:-4] + ".flac")
+            ts = time.time()
+            p = ctx.Process(target=fork_child, args=(fn, out, q, ts))
+            p.start()
+            alive.append((ts, p))
+        still = []
+        for ts, p in alive:
+            if p.exitcode is None:
+                still.append((ts, p))
+            elif p.exitcode:
+                raise RuntimeError("conversion process failed: %d" % p.exitcode)
+            else:
+                done.append(ts)
+        alive = still
+        time.sleep(0.0005)
+    wall = time.time() - t0
+    outs = [q.get() for _ in done]
+    return wall, [(json.loads(o)["t_fork"], o) for o in outs]
 
 
 def write_wavs(d, n_files, frames):
@@ -104,27 +159,40 @@ def main():
         files = write_wavs(d, n_files, frames)
         gdir = os.path.join(d, "gpu")
         os.mkdir(gdir)
-        cmds = [[sys.executable, os.path.abspath(__file__), "--one", fn,
-                 os.path.join(gdir, os.path.basename(fn)[:-4] + ".flac")] for fn in files]
-        wall, done = run_pool(cmds, j)
+        fork = "--fork" in sys.argv
+        own = "--own-engine" in sys.argv
+        if own:  # inherited by the children
+            os.environ["ATG_ENCODER_SERVICE"] = "off"
+        if fork:
+            # the parent imports audiotools (never the GPU), as track2track's
+            # process does before ExecProgressQueue forks the conversions
+            sys.path.insert(0, os.path.join(ROOT, "python-audio-tools_amd"))
+            import audiotools  # noqa: F401
+            from audiotools import encoders  # noqa: F401
+            wall, done = run_forks(files, gdir, j)
+            keys = ["hip_init", "encode"]
+        else:
+            cmds = [[sys.executable, os.path.abspath(__file__), "--one", fn,
+                     os.path.join(gdir, os.path.basename(fn)[:-4] + ".flac")] for fn in files]
+            wall, done = run_pool(cmds, j)
+            keys = ["numpy", "audiotools", "hip_init", "encode"]
         phases = {}
-        keys = ["numpy", "audiotools", "hip_init", "encode"]
         for ts, out in done:
             t = json.loads(out.strip().splitlines()[-1])["t"]
-            prev = ts
-            phases.setdefault("spawn_to_start", []).append(t["start"] - ts)
+            phases.setdefault("spawn_to_start", []).append(max(0.0, t["start"] - ts))
             prev = t["start"]
             for k in keys:
                 phases.setdefault(k, []).append(t[k] - prev)
                 prev = t[k]
-            phases.setdefault("exit", []).append(0.0)
         total_frames = n_files * frames
-        res = {"processes": j, "files": n_files, "frames_per_file": frames,
+        res = {"mode": "fork" if fork else "spawn",
+               "encoder": "engine per process" if own else "encoder service (atgpu-encoderd)",
+               "processes": j, "files": n_files,
+               "frames_per_file": frames,
                "wall_s": round(wall, 3), "frames_per_s": round(total_frames / wall, 1),
                "per_process_ms_mean": {k: round(1e3 * sum(v) / len(v), 1)
-                                       for k, v in phases.items() if k != "exit"},
-               "per_process_ms_max": {k: round(1e3 * max(v), 1)
-                                      for k, v in phases.items() if k != "exit"}}
+                                       for k, v in phases.items()},
+               "per_process_ms_max": {k: round(1e3 * max(v), 1) for k, v in phases.items()}}
         ref = os.path.join(ROOT, "oracle", "_ref", "flacenc")
         if os.path.exists(ref):
             rdir = os.path.join(d, "ref")
