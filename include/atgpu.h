@@ -503,6 +503,14 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
                                  uint32_t n_tracks, uint32_t n_albums, atg_rg_result *results,
                                  uint32_t *d_album_hist, double *album_peaks, void *stream);
 
+/* Test hooks of the time-split analysis (replaygain.hip): the warm-up
+   frames of every segment after a track's first (-1 = the rate-scaled
+   default; 0 = none, so every track fails certification and is analysed
+   again serially), and how many tracks the last atg_replaygain_device call
+   analysed again serially. */
+void atg_replaygain_set_warmup(int frames);
+uint32_t atg_replaygain_fallback_tracks(void);
+
 /* analyzeResult (replaygain.c:754-776) of n device histograms -> gains
    (host); NaN = not enough samples (album_gain raises ValueError). */
 atg_status atg_replaygain_hist_gain(const uint32_t *d_hist, uint32_t n, double *gains,

@@ -2,6 +2,7 @@
 identical per-track 12000-bin window histograms (each track its own album),
 identical peaks, title gains and album gain; the ReplayGain class contract.
 Parity unpinned (no reference fixtures; see the oracle header)."""
+import ctypes
 import math
 
 import numpy as np
@@ -182,3 +183,52 @@ def test_empty_title_and_empty_batch():
     res, peaks, gains, hist = _atgpu.replaygain_host(np.zeros(0, np.int32), [], 2,
                                                      return_hist=True)
     assert peaks == [0.0, 0.0] and not hist.any()
+
+
+def _fallbacks():
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    lib.atg_replaygain_fallback_tracks.restype = ctypes.c_uint32
+    return lib.atg_replaygain_fallback_tracks()
+
+
+def _set_warmup(frames):
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    lib.atg_replaygain_set_warmup.argtypes = [ctypes.c_int]
+    lib.atg_replaygain_set_warmup(frames)
+
+
+@pytest.mark.parametrize("warm", [-1, 0, 500])
+def test_time_split_certified_or_fallback(warm):
+    """the time-split analysis (replaygain.hip k_rg_seg): with the default
+    warm-up every track's histogram equals the oracle's; with no warm-up
+    (0) every multi-segment track fails certification at its seams and is
+    analysed again serially; with a short one some may -- identical
+    histograms, peaks and gains either way"""
+    from audiotools import _atgpu
+    rate, ch, bps = 44100, 2, 16
+    pcms = [make(rate, ch, bps, 90000 + 1000 * k, 40 + k) for k in range(6)]
+    pcms.append(make(rate, ch, bps, 3000, 9))  # one segment: exact by construction
+    tracks, off = [], 0
+    for k, p in enumerate(pcms):
+        tracks.append(_atgpu.RgTrack(off, len(p) // ch, ch, bps, rate, k))  # album per track
+        off += len(p) // ch
+    _set_warmup(warm)
+    try:
+        res, peaks, gains, hist = _atgpu.replaygain_host(np.concatenate(pcms), tracks,
+                                                         len(pcms), return_hist=True)
+        nfb = _fallbacks()
+    finally:
+        _set_warmup(-1)
+    if warm == 0:
+        assert nfb == 6
+    elif warm == -1:
+        assert nfb <= 1  # certification fails only near a bin edge
+    for k, p in enumerate(pcms):
+        A, pk = op.rg_title(p, ch, bps, rate)
+        assert np.array_equal(hist[k], A), (warm, k)
+        assert res[k].title_peak == pk and peaks[k] == pk
+        assert res[k].title_gain == op.rg_gain(A)
+        assert gains[k] == op.rg_gain(A) or (math.isnan(gains[k]) and
+                                             math.isnan(op.rg_gain(A)))

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU-box recipe (round 4): the default bench line, then its rocprof kernel stats.
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-r4e}
+mkdir -p "$OUT"
+cd "$R"
+timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv \
+    -- python3 $R/bench.py --no-cpu-baseline --no-t2t > "$OUT/prof.log" 2>&1
