@@ -108,6 +108,15 @@ atg_status atg_engine_create(int device, atg_engine **out);
                                    process per track under track2track -j N)
                                    then holds two HIP streams, so many such
                                    processes fit the device's hardware queues */
+/* Where a device batch's STREAMINFO MD5 is computed.  By default the engine
+   picks per batch: one GPU hash chain per track (md5.hip) unless the tracks
+   are few and long enough that host cores hash the PCM sooner than the
+   longest serial chain ends (config 5: 64 tracks x 8.6 MB of 24-bit 5.1 PCM
+   -- the PCM goes to pinned host memory and host threads hash it beside the
+   next batch's GPU work).  These flags force one side (the images are the
+   same bytes either way). */
+#define ATG_ENGINE_MD5_GPU 2u
+#define ATG_ENGINE_MD5_HOST 4u
 /* atg_engine_create with flags.  Without ATG_ENGINE_STREAMING every stream
    is created at once in a fixed order (the batch APIs' queue layout). */
 atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out);

@@ -500,20 +500,24 @@ class HostJob:
 
 
 ENGINE_STREAMING = 1  # atg_engine_create_ex flag (include/atgpu.h)
+ENGINE_MD5_GPU = 2  # MD5 always on GPU chains
+ENGINE_MD5_HOST = 4  # MD5 always on host threads
 
 
 class Engine(object):
     """one libatgpu engine (streams + workspace) on one device; streaming=True
     for a process that encodes one track at a time (streams on first use,
-    ATG_ENGINE_STREAMING)"""
+    ATG_ENGINE_STREAMING); md5 = "auto" (the engine picks GPU chains or host
+    threads per batch), "gpu" or "host" (ATG_ENGINE_MD5_GPU / _HOST)"""
 
-    def __init__(self, device=0, streaming=False):
+    def __init__(self, device=0, streaming=False, md5="auto"):
         self.lib = load_library()
         self.device = device
         self._inflight = {}  # host-job ticket -> the arrays the engine writes
+        flags = ENGINE_STREAMING if streaming else 0
+        flags |= {"auto": 0, "gpu": ENGINE_MD5_GPU, "host": ENGINE_MD5_HOST}[md5]
         h = ctypes.c_void_p()
-        _check(self.lib, self.lib.atg_engine_create_ex(
-            int(device), ENGINE_STREAMING if streaming else 0, ctypes.byref(h)))
+        _check(self.lib, self.lib.atg_engine_create_ex(int(device), flags, ctypes.byref(h)))
         self.handle = h
 
     def close(self):

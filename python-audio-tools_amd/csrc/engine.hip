@@ -8,14 +8,20 @@
 #include "handle_lock.h"
 #include <hip/hip_runtime.h>
 
+#include <sched.h>
+
 #include <algorithm>
 #include <cmath>
+#include <condition_variable>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <deque>
+#include <functional>
+#include <future>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -23,6 +29,7 @@
 #include "../../include/atgpu.h"
 #include "flac_dev.h"
 #include "launch.h"
+#include "md5_cpu.h"
 
 // timing experiments only (tools/gpu_exp.sh); 0 in every product build
 #ifndef ATG_EXP
@@ -149,6 +156,16 @@ struct EncSlot {
     bool pend_split = false;         // part 1 of a split MD5 chain still to run
     atg_status end_status = ATG_OK;  // the batch end failed to queue: its wait reports this
     std::string end_error;
+    // host-MD5 mode (want_host_md5): the PCM goes to pinned host memory and
+    // the pool's threads hash it; the digests go back before the headers
+    bool md5_host = false;
+    uint8_t *hpcm = nullptr;         // pinned: the tracks' PCM containers
+    size_t hpcm_cap = 0;
+    uint8_t *hmd5 = nullptr;         // pinned: 16 bytes per track
+    size_t hmd5_cap = 0;
+    DevBuf md5in;                    // the digests on the device
+    hipEvent_t ev_hpcm = nullptr;    // the PCM copies are done
+    std::vector<std::future<void>> hash_jobs;
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
     bool host = false;               // a chunk of a host-memory job
@@ -187,9 +204,59 @@ struct HostStage {
     hipEvent_t ev_d2h = nullptr;    // packed images in host memory
 };
 
+// host threads for the host-MD5 mode: a fixed pool, one task per track
+struct HashPool {
+    std::vector<std::thread> th;
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<std::packaged_task<void()>> q;
+    bool stop = false;
+    explicit HashPool(unsigned n)
+    {
+        for (unsigned i = 0; i < n; ++i)
+            th.emplace_back([this] {
+                for (;;) {
+                    std::packaged_task<void()> job;
+                    {
+                        std::unique_lock<std::mutex> lk(mu);
+                        cv.wait(lk, [this] { return stop || !q.empty(); });
+                        if (q.empty())
+                            return;
+                        job = std::move(q.front());
+                        q.pop_front();
+                    }
+                    job();
+                }
+            });
+    }
+    std::future<void> submit(std::function<void()> f)
+    {
+        std::packaged_task<void()> job(std::move(f));
+        std::future<void> fut = job.get_future();
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            q.push_back(std::move(job));
+        }
+        cv.notify_one();
+        return fut;
+    }
+    ~HashPool()
+    {
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            stop = true;
+        }
+        cv.notify_all();
+        for (std::thread &t : th)
+            t.join();
+    }
+};
+
 struct atg_engine {
     std::recursive_mutex mu; // held by every public entry point (handle_lock.h)
     int device = 0;
+    uint32_t flags = 0;      // atg_engine_create_ex flags
+    std::unique_ptr<HashPool> pool; // host-MD5 threads, created on first use
     bool sync_call = false; // inside atg_flac_encode_device (enqueue + wait)
     hipStream_t s_main = nullptr;
     EncSlot slot[kEncSlots];
@@ -567,6 +634,122 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
     return ATG_OK;
 }
 
+// ---- host-MD5 mode ---------------------------------------------------------
+// Host threads available to this process: the affinity mask, bounded by a
+// cgroup CPU quota (a GPU box shares its host: os.cpu_count() sees every
+// core, cpu.max the share this job may use), at most 32.
+unsigned host_hash_threads()
+{
+    unsigned n = std::max(1u, std::thread::hardware_concurrency());
+    cpu_set_t cs;
+    if (sched_getaffinity(0, sizeof(cs), &cs) == 0)
+        n = std::max(1, CPU_COUNT(&cs));
+    if (FILE *f = std::fopen("/sys/fs/cgroup/cpu.max", "r")) {
+        char q[32] = {0};
+        unsigned long per = 0;
+        if (std::fscanf(f, "%31s %lu", q, &per) == 2 && std::strcmp(q, "max") != 0 && per)
+            n = std::min<unsigned>(n, std::max(1ul, std::strtoul(q, nullptr, 10) / per));
+        std::fclose(f);
+    }
+    return std::min(n, 32u);
+}
+
+// Host or GPU for this batch's MD5.  A GPU chain hashes one 64-byte block
+// per ~0.8 us (one wave per track, md5.hip), so the batch's MD5 ends when
+// its longest track's chain does; host threads hash ~450 MB/s each after a
+// D2H copy (~40 GB/s pinned).  The host side wins only for few, long tracks
+// whose chains would outlast the GPU work they overlap (config 5: 8.6 MB
+// tracks, ~110 ms chains); the GPU otherwise (config 2: 1 MiB tracks, ~13 ms
+// chains under the next batches' search kernels).
+bool want_host_md5(atg_engine *e, const Plan &pl, int fmt, bool md5_early)
+{
+    const FlacParams &p = pl.p;
+    if (pl.frames_only || md5_early || p.bps < 8 || p.bps % 8 || pl.tracks.empty())
+        return false;
+    if (e->flags & ATG_ENGINE_MD5_GPU)
+        return false;
+    if (e->flags & ATG_ENGINE_MD5_HOST)
+        return true;
+    const uint64_t bb = p.bps / 8, cs = fmt == ATG_PCM_S16 ? 2 : 4;
+    uint64_t maxb = 0, tot = 0;
+    for (const TrackInfo &t : pl.tracks) {
+        const uint64_t b = t.pcm_frames * p.channels * bb;
+        maxb = std::max(maxb, b);
+        tot += b;
+    }
+    const double gpu_ms = (double)maxb / 64.0 * 0.8e-3;
+    const double host_ms = (double)tot / (host_hash_threads() * 450e3) +
+                           (double)tot / bb * cs / 40e6;
+    return gpu_ms > 40.0 && host_ms < gpu_ms;
+}
+
+// The tracks' PCM to pinned host memory on the slot's stream (copy engine),
+// then one pool task per track: wait for the copies, hash the containers'
+// little-endian bytes (md5_cpu.h) into sl.hmd5.  finish_batch joins them.
+atg_status start_host_md5(atg_engine *e, EncSlot &sl, const Plan &pl, const void *d_pcm, int fmt)
+{
+    const FlacParams &p = pl.p;
+    const size_t nt = pl.tracks.size();
+    const uint64_t cs = fmt == ATG_PCM_S16 ? 2 : 4;
+    for (std::future<void> &f : sl.hash_jobs) // a failed earlier batch's tasks
+        f.wait();
+    sl.hash_jobs.clear();
+    uint64_t total = 0;
+    for (const TrackInfo &t : pl.tracks)
+        total += t.pcm_frames * p.channels * cs;
+    HIP_TRY(ensure_pinned(sl.hpcm, sl.hpcm_cap, (size_t)std::max<uint64_t>(total, 1)));
+    HIP_TRY(ensure_pinned(sl.hmd5, sl.hmd5_cap, 16 * nt));
+    HIP_TRY(sl.md5in.ensure(16 * nt));
+    if (!sl.ev_hpcm)
+        HIP_TRY(hipEventCreateWithFlags(&sl.ev_hpcm, hipEventDisableTiming));
+    std::vector<uint64_t> off(nt);
+    uint64_t o = 0;
+    for (size_t t = 0; t < nt; ++t) {
+        const TrackInfo &ti = pl.tracks[t];
+        const uint64_t nb = ti.pcm_frames * p.channels * cs;
+        off[t] = o;
+        if (nb)
+            HIP_TRY(hipMemcpyAsync(sl.hpcm + o,
+                                   (const uint8_t *)d_pcm + ti.pcm_start * p.channels * cs, nb,
+                                   hipMemcpyDeviceToHost, sl.s_aux));
+        o += nb;
+    }
+    HIP_TRY(hipEventRecord(sl.ev_hpcm, sl.s_aux));
+    if (!e->pool)
+        e->pool.reset(new HashPool(host_hash_threads()));
+    sl.hash_jobs.clear();
+    const hipEvent_t ev = sl.ev_hpcm;
+    const uint32_t bb = p.bps / 8;
+    for (size_t t = 0; t < nt; ++t) {
+        const uint8_t *src = sl.hpcm + off[t];
+        const uint64_t n = pl.tracks[t].pcm_frames * p.channels;
+        uint8_t *dst = sl.hmd5 + 16 * t;
+        sl.hash_jobs.push_back(e->pool->submit([=] {
+            (void)hipEventSynchronize(ev);
+            if (cs == 2)
+                md5cpu::hash_s16((const int16_t *)src, n, bb, dst);
+            else
+                md5cpu::hash_s32((const int32_t *)src, n, bb, dst);
+        }));
+    }
+    return ATG_OK;
+}
+
+// the host digests into TrackOut on the slot's stream (before the headers)
+atg_status finish_host_md5(EncSlot &sl)
+{
+    for (std::future<void> &f : sl.hash_jobs)
+        f.wait();
+    sl.hash_jobs.clear();
+    const size_t nt = sl.plan->tracks.size();
+    if (nt) {
+        HIP_TRY(hipMemcpyAsync(sl.md5in.p, sl.hmd5, 16 * nt, hipMemcpyHostToDevice, sl.s_aux));
+        HIP_TRY(launch_put_md5((TrackOut *)sl.tout.p, (const uint8_t *)sl.md5in.p, (uint32_t)nt,
+                               sl.s_aux));
+    }
+    return ATG_OK;
+}
+
 // Enqueue one batch on slot `sl`: the search chain on the engine's main
 // stream, the MD5 chains from the start of the batch and the stream headers
 // on the slot's aux stream, then the results back to pinned host memory.
@@ -661,15 +844,26 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // md5_early (host pipeline chunks): the whole chain as soon as the
     // chunk's PCM is uploaded -- a host caller waits for its last chunk's
     // chains, so they start as early as possible
-    const bool split_md5 = pipelined && !md5_early &&
+    // host-MD5 mode (few long tracks, want_host_md5): the PCM copies start
+    // with the batch, the hashes run on host threads, nothing on the GPU
+    sl.md5_host = want_host_md5(e, pl, fmt, md5_early);
+    const bool split_md5 = pipelined && !md5_early && !sl.md5_host &&
                            ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
                             (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
     // (md5_early: after the chunk's upload and this batch's track tables --
     // ev_tables is recorded on the main stream behind both)
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, md5_early ? sl.ev_tables : ev[1], 0));
+    HIP_TRY(hipStreamWaitEvent(sl.s_aux, (md5_early || sl.md5_host) ? sl.ev_tables : ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-    if (!pl.frames_only)
-        HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
+    if (!pl.frames_only) {
+        if (sl.md5_host) {
+            sl.plan = plp; // the pool's tasks read the plan's tracks through the slot
+            st = start_host_md5(e, sl, pl, d_pcm, fmt);
+            if (st != ATG_OK)
+                return st;
+        } else {
+            HIP_TRY(launch_track_md5(p, d_pcm, fmt, dtr, dto, split_md5 ? 0 : 2, sl.s_aux));
+        }
+    }
     HIP_TRY(hipEventRecord(ev[2], e->s_main));
     if (pl.big)
         HIP_TRY(launch_subframe_search_big(p, d_pcm, fmt, dfr, (const int16_t *)sl.coef.p,
@@ -735,15 +929,15 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     sl.pend_fmt = fmt;
     sl.pend_out = d_out;
     sl.pend_split = split_md5;
-    if (!split_md5) {
+    if (!split_md5 && !sl.md5_host) {
         atg_status st2 = batch_end(e, sl, nullptr);
         if (st2 != ATG_OK)
             return st2;
     }
     // the previous batches' second MD5 parts start now that this batch's
-    // LPC kernel is done
+    // LPC kernel is done (a host-MD5 batch ends when it is waited)
     for (EncSlot &o : e->slot)
-        if (&o != &sl && o.end_pending) {
+        if (&o != &sl && o.end_pending && !o.md5_host) {
             atg_status st2 = batch_end(e, o, ev[1]);
             if (st2 != ATG_OK)
                 return st2;
@@ -755,6 +949,15 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
 atg_status finish_batch(atg_engine *e, EncSlot &sl)
 {
     HIP_TRY(hipSetDevice(e->device));
+    if (sl.end_pending && sl.md5_host) {
+        atg_status st = finish_host_md5(sl);
+        if (st != ATG_OK) {
+            sl.end_pending = false;
+            (void)hipStreamSynchronize(e->s_main);
+            (void)hipStreamSynchronize(sl.s_aux);
+            return st;
+        }
+    }
     if (sl.end_pending) {
         atg_status st = batch_end(e, sl, nullptr);
         if (st != ATG_OK)
@@ -1180,6 +1383,7 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
     HIP_TRY(hipSetDevice(device));
     atg_engine *e = new atg_engine();
     e->device = device;
+    e->flags = flags;
     HIP_TRY(hipStreamCreateWithFlags(&e->s_main, hipStreamNonBlocking));
     // every stream now, in this order, unless the caller streams one track
     // at a time (ATG_ENGINE_STREAMING): the order fixes the streams'
@@ -1222,11 +1426,20 @@ void atg_engine_destroy(atg_engine *e)
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->s_main);
     for (EncSlot &sl : e->slot) {
+        for (std::future<void> &f : sl.hash_jobs) // a batch never waited
+            f.wait();
+        sl.hash_jobs.clear();
         if (sl.s_aux)
             (void)hipStreamSynchronize(sl.s_aux);
         for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
-                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch})
+                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch,
+                          &sl.md5in})
             b->release();
+        for (void *q : {(void *)sl.hpcm, (void *)sl.hmd5})
+            if (q)
+                (void)hipHostFree(q);
+        if (sl.ev_hpcm)
+            (void)hipEventDestroy(sl.ev_hpcm);
         for (auto &ev : sl.ev)
             (void)hipEventDestroy(ev);
         (void)hipEventDestroy(sl.ev_tables);

@@ -341,6 +341,11 @@ struct WinPred {
     __device__ __forceinline__ void step(int32_t rv, bool commit)
     {
         int32_t p;
+#if ATG_DEC_EXP == 7 // timing experiment: no prediction (residuals only)
+        if (true) {
+            p = 0;
+        } else
+#endif
         if (fast) {
             int32_t acc = 0;
 #pragma unroll
@@ -790,7 +795,8 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
         const uint64_t p = cand_pos[i];
         const DecTrack t = tr[find_track(tr, nt, p)];
         ParseRec rec;
-        parse_frame<true>(w, nw, p, t, ~0ull, T, rec, ring + threadIdx.x * kRingStride);
+        // 6: timing experiment, residual words straight from global memory
+        parse_frame<ATG_DEC_EXP != 6>(w, nw, p, t, ~0ull, T, rec, ring + threadIdx.x * kRingStride);
         recs[i] = rec;
     }
 }

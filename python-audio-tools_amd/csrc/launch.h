@@ -61,6 +61,8 @@ hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
                              const FrameInfo *frames, const TrackInfo *tracks,
                              const SubDesc *sub, const FrameDesc *fd,
                              uint8_t *out, uint32_t *err, hipStream_t s);
+// md5.hip: host-hashed digests into TrackOut (engine host-MD5 mode)
+hipError_t launch_put_md5(TrackOut *tout, const uint8_t *md5, uint32_t n, hipStream_t s);
 hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
                                 const TrackOut *tout, uint8_t *out,
                                 hipStream_t s);

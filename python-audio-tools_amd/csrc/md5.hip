@@ -819,3 +819,23 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                            (const int32_t *)pcm, tracks, tout, paired);
     return hipGetLastError();
 }
+
+// host-hashed digests (engine host-MD5 mode) into the tracks' TrackOut, for
+// the stream-header kernel that follows on the same stream
+__global__ __launch_bounds__(64) void k_put_md5(TrackOut *__restrict__ tout,
+                                                const uint8_t *__restrict__ md5, uint32_t n)
+{
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n)
+        return;
+    for (int i = 0; i < 16; ++i)
+        tout[t].md5[i] = md5[16u * t + i];
+}
+
+hipError_t launch_put_md5(TrackOut *tout, const uint8_t *md5, uint32_t n, hipStream_t s)
+{
+    if (!n)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_put_md5, dim3((n + 63u) / 64u), dim3(64), 0, s, tout, md5, n);
+    return hipGetLastError();
+}
