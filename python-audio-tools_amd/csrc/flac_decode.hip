@@ -8,10 +8,11 @@
 // its residuals are parsed, so the serial loop is split into passes that are
 // each parallel:
 //
-//   K1 k_dec_scan      thread per 4 input bytes: every byte that starts a
-//                      sync code gets a full frame-header parse (CRC-8 and
-//                      STREAMINFO consistency, flac.c:710-851); survivors are
-//                      "candidates" (cand_pos[i], cand_idx[byte] = i).
+//   K1 k_dec_sync      thread per 16 input bytes: every byte that starts a
+//      k_dec_hdr       sync code is listed, then gets a full frame-header
+//                      parse (CRC-8 and STREAMINFO consistency,
+//                      flac.c:710-851); survivors are "candidates"
+//                      (cand_pos[i], cand_idx[byte] = i).
 //   K2 k_dec_parse     lane per candidate (grid-stride): parse the subframes
 //                      (Rice codes included) without reconstructing samples,
 //                      CRC-16 the frame; record status, length, and the bit
@@ -51,9 +52,6 @@
 #ifndef ATG_DEC_EXP
 #define ATG_DEC_EXP 0 // timing experiments only (exp/ builds); 0 in the product
 #endif
-#ifndef ATG_DEC_READER
-#define ATG_DEC_READER 1 // residual loop reader: 0 random access, 1 register window
-#endif
 
 namespace {
 
@@ -66,6 +64,7 @@ enum {
 
 __constant__ uint8_t c_crc8[256];
 __constant__ uint16_t c_crc16[4][256];
+__constant__ uint16_t c_crc_adv[24][16]; // CRC-16 state advanced by 2^m zero bytes
 
 struct DecTrack {
     uint64_t start;     // absolute byte of the first frame
@@ -316,28 +315,36 @@ __device__ __forceinline__ int32_t mad24(int32_t a, int32_t b, int32_t c)
 
 template <int W>
 struct WinPred {
-    int32_t *out;   // the job's warm-up cell
-    int4 *row;      // wave row scratch, [row/4][lane][4]: lane column at row[.. * 64]
-    int32_t q0, q1, q2, q3; // the 4 rows stored together
-    uint32_t i, n, t, wasted, shift, half, porder;
+    int4 *row;      // the job's samples, [sample/4][lane][4]: lane column at row[.. * 64]
+    int32_t q0, q1, q2, q3; // the 4 samples stored together
+    uint32_t i, n, wasted, shift, half, porder;
     bool fast, bad;
     int32_t c[W];
     int32_t h[W]; // h[0] newest sample
+    // sample i (warm-up or restored) into the job's column: one 16-byte
+    // store per 4 samples (64 lanes of a wave store 1 KB contiguous); the
+    // emitter reads 4 consecutive samples of a job with one 16-byte load
+    __device__ __forceinline__ void put(int32_t v, bool on)
+    {
+        const uint32_t k = i & 3;
+        q0 = on && k == 0 ? v : q0;
+        q1 = on && k == 1 ? v : q1;
+        q2 = on && k == 2 ? v : q2;
+        q3 = on && k == 3 ? v : q3;
+        if (on && k == 3)
+            row[(uint64_t)(i >> 2) * 64] = make_int4(q0, q1, q2, q3);
+        i += on ? 1u : 0u;
+    }
     __device__ __forceinline__ void warm(int32_t s)
     {
 #pragma unroll
         for (int j = W - 1; j > 0; --j)
             h[j] = h[j - 1];
         h[0] = s;
-        if (i < n)
-            out[i] = (int32_t)((uint32_t)s << wasted);
-        ++i;
+        put((int32_t)((uint32_t)s << wasted), true);
     }
     __device__ __forceinline__ void partition_order(uint32_t p) { porder = p; }
-    // one residual-loop iteration (a partition header when !commit): the
-    // value goes to row t of the lane's column -- every lane of the wave
-    // stores to the same row, one 256-byte coalesced store per iteration
-    // (per-lane sample addresses would make 64 scattered line writes)
+    // one residual-loop iteration (a partition header when !commit)
     __device__ __forceinline__ void step(int32_t rv, bool commit)
     {
         int32_t p;
@@ -365,22 +372,12 @@ struct WinPred {
         for (int j = W - 1; j > 0; --j)
             h[j] = commit ? h[j - 1] : h[j];
         h[0] = commit ? s : h[0];
-        const int32_t v = (int32_t)((uint32_t)s << wasted);
-        const uint32_t k = t & 3;
-        q0 = k == 0 ? v : q0;
-        q1 = k == 1 ? v : q1;
-        q2 = k == 2 ? v : q2;
-        q3 = k == 3 ? v : q3;
-        // one 16-byte store per 4 iterations (64 lanes: 1 KB contiguous):
-        // a store waits in the same in-order vmcnt queue as the next load
-        if (k == 3)
-            row[(uint64_t)(t >> 2) * 64] = make_int4(q0, q1, q2, q3);
-        ++t;
+        put((int32_t)((uint32_t)s << wasted), commit);
     }
     __device__ __forceinline__ void flush()
     {
-        if (t & 3)
-            row[(uint64_t)(t >> 2) * 64] = make_int4(q0, q1, q2, q3);
+        if (i & 3)
+            row[(uint64_t)(i >> 2) * 64] = make_int4(q0, q1, q2, q3);
     }
 };
 
@@ -395,20 +392,163 @@ struct NullSink {
 // selects: lanes holding different partition orders and Rice parameters
 // never branch apart (long unary codes, > 32 bits with their LSBs, take a
 // rare slow path).
-// Residual-loop reads.  A lane's next word is a dependent load every few
-// codes, and at one wave per SIMD (K2 has a lane per frame, ~1 k waves for a
-// config-2 batch) with 256 lanes per CU walking 256 different frames, the
-// vL1D thrashes and every such load is an L2 round trip (~1.9 k cycles per
-// residual measured).  Ring: the lane's words come from a 32-word LDS ring
-// that the wave refills at wave-uniform points -- every kRingG iterations
-// each lane commits the 8 words it loaded one period earlier and issues the
-// next 8 (two 16-byte loads) when the ring has room -- so the loop reads only
-// LDS, and a global load has a whole period to arrive.  A lane that runs
-// ahead of its ring (long codes) reads global memory directly.
-constexpr uint32_t kRing = 32;      // words per lane (power of 2)
-constexpr uint32_t kRingStride = 33; // LDS words between lanes (bank spread)
-constexpr uint32_t kRingG = 4;      // iterations per refill period
+// Residual-loop reads.  Lanes hold different subframes, so a lane's words
+// are its own stream, and at one or two waves per SIMD (a lane per frame or
+// per subframe: ~1-2 k waves for a config-2 batch) nothing hides a load's
+// latency: with the next word fetched from global memory one iteration
+// ahead, every word crossing waits an L2 round trip (the subframe kernel
+// ran ~2,000 cycles per residual, and prediction cost nothing measurable,
+// profiles/r04_h_dec_probe.jsonl).  Ring: a lane's words come from a
+// 64-word LDS ring, refilled at wave-uniform points every kRingG
+// iterations by two alternating 16-word buffers (four 16-byte loads each):
+// a buffer issued at refill point k is committed to the ring at point k+2,
+// so a load has 2 kRingG iterations to arrive and the loop itself reads only
+// LDS.  A refill holds 16 words per kRingG = 16 iterations, one word per
+// iteration: what the widest codes that stay on the fast path consume.  A
+// lane that outruns its ring (long codes, the slow path's jumps) reads
+// global memory directly until the ring catches up.
+constexpr uint32_t kRing = 64;       // words per lane (power of 2)
+constexpr uint32_t kRingStride = 68; // LDS words between lanes (16-byte rows)
+constexpr uint32_t kRingG = 16;      // iterations per refill point
+constexpr uint32_t kRingB = 16;      // words per refill buffer
 
+// Refill loads: plain loads whose waits the compiler places.  With both
+// buffers in fixed registers (the loop is unrolled over the two refill
+// points, no phi moves them) and the window's first words waited for before
+// the loop, the compiler's wait for a buffer at its commit is a counted
+// vmcnt past the other buffer's four loads (checked in the ISA), and the
+// residual steps in between wait only for LDS.
+__device__ __forceinline__ void ring_load4(const uint4 *p, uint4 &q0, uint4 &q1, uint4 &q2,
+                                           uint4 &q3)
+{
+    q0 = p[0];
+    q1 = p[1];
+    q2 = p[2];
+    q3 = p[3];
+}
+
+// one refill point for buffer (q, addr, pend): commit what it loaded two
+// points ago, then load the next 16 words (kept only if the ring has room
+// for them).  The four loads are issued whether or not they are kept (a
+// lane without room re-reads a block it already holds), so the compiler
+// can wait for a buffer with a counted vmcnt(4) -- the other buffer's four
+// loads stay in flight -- instead of vmcnt(0).
+#define RING_REFILL(q0, q1, q2, q3, addr, pend)                                        \
+    do {                                                                               \
+        if (pend) {                                                                    \
+            if (addr >= fill) { /* blocks arrive in address order; a gap restarts */   \
+                if (addr > fill)                                                       \
+                    rbeg = addr;                                                       \
+                uint4 *d_ = (uint4 *)(ring + (addr & (kRing - 1)));                    \
+                d_[0] = q0;                                                            \
+                d_[1] = q1;                                                            \
+                d_[2] = q2;                                                            \
+                d_[3] = q3;                                                            \
+                fill = addr + kRingB;                                                  \
+                rbeg = fill > rbeg + kRing ? fill - kRing : rbeg;                      \
+            }                                                                          \
+        }                                                                              \
+        const uint64_t a_ = nf > (S.cw & ~15ull) ? nf : (S.cw & ~15ull);               \
+        pend = a_ + kRingB <= S.cw + kRing && a_ + kRingB <= r.last + 1;               \
+        const uint4 *s_ = (const uint4 *)(r.w + (pend ? a_ : ((r.last + 1 - kRingB) & ~3ull))); \
+        ring_load4(s_, q0, q1, q2, q3);                                                \
+        addr = a_;                                                                     \
+        nf = pend ? a_ + kRingB : nf;                                                  \
+    } while (0)
+
+// Register window of a lane's residual stream: hi:lo = words cw, cw+1 (byte-
+// swapped), off = bits consumed of hi, nx = word cw+2 (raw), plus the
+// partition state of flacdec_read_residual.
+struct ResState {
+    uint64_t cw;
+    uint32_t off, hi, lo, nx;
+    uint32_t k, hdrs, left, rice, esc;
+};
+
+struct ResShape {
+    uint32_t total, parts, p0, plen, pbits, escv;
+};
+
+// One iteration of the flat residual loop: a partition header or one
+// residual, both decoded from the same 32-bit peek and merged with selects
+// (lanes holding different partition orders and Rice parameters never
+// branch apart; long unary codes, > 32 bits with their LSBs, take a rare
+// slow path).  The window moves at most one word (to nx); the caller loads
+// the next nx.  Returns false when the lane is done (end or EOF in `st`).
+template <class P>
+__device__ __forceinline__ bool res_step(BitR &r, ResState &S, const ResShape &Z, P &sink, int &st)
+{
+    const uint32_t p = S.off ? (S.hi << S.off) | (S.lo >> (32 - S.off)) : S.hi;
+    const bool hdr = S.left == 0;
+    // partition header: Rice parameter (+ escape width)
+    const uint32_t hr = p >> (32 - Z.pbits);
+    const bool hesc = hr == Z.escv;
+    const uint32_t hlen = Z.pbits + (hesc ? 5u : 0u);
+    const uint32_t hbits = (p >> (27 - Z.pbits)) & 31u;
+    // residual: Rice code (unary MSBs, stop bit, LSBs) or escaped raw
+    const uint32_t z = __builtin_clz(p | 1u);
+    const uint32_t clen = z + 1 + S.rice;
+    const uint32_t lsb = __builtin_amdgcn_ubfe(p, 31 - z - S.rice, S.rice);
+    const uint32_t value = (z << S.rice) | lsb;
+    int32_t v = (int32_t)(value >> 1) ^ -(int32_t)(value & 1u);
+    uint32_t len = clen;
+    if (S.esc) {
+        v = (int32_t)p >> (32 - S.esc);
+        len = S.esc;
+    }
+    const uint32_t step = hdr ? hlen : len;
+    if (!hdr && !S.esc && (p == 0 || clen > 32)) { // rare: long code
+        r.pos = (uint32_t)((S.cw - r.bw) * 32) + S.off;
+        const uint32_t msb = r.zeros();
+        const uint32_t val = (msb << S.rice) | r.get(S.rice);
+        v = (int32_t)(val >> 1) ^ -(int32_t)(val & 1u);
+        S.cw = r.bw + (r.pos >> 5);
+        S.off = r.pos & 31;
+        S.hi = bswap32(r.w[S.cw < r.last ? S.cw : r.last]);
+        S.lo = bswap32(r.w[S.cw + 1 < r.last ? S.cw + 1 : r.last]);
+    } else {
+        S.off += step;
+        const bool need = S.off >= 32;
+        S.hi = need ? S.lo : S.hi;
+        S.lo = need ? bswap32(S.nx) : S.lo;
+        S.cw += need ? 1u : 0u;
+        S.off -= need ? 32u : 0u;
+    }
+    sink.step(v, !hdr);
+    S.k += hdr ? 0u : 1u;
+    S.left = hdr ? (S.hdrs == 0 ? Z.p0 : Z.plen) : S.left - 1u;
+    S.rice = hdr ? hr : S.rice;
+    S.esc = hdr ? (hesc ? hbits : 0u) : S.esc;
+    S.hdrs += hdr ? 1u : 0u;
+    if (hdr) {
+        r.pos = (uint32_t)((S.cw - r.bw) * 32) + S.off;
+        if (r.eof()) {
+            st = FD_EOF;
+            return false;
+        }
+    }
+    return S.k < Z.total || S.hdrs < Z.parts;
+}
+
+// 16 iterations of the ring loop: the ring word for the next nx (ds_read),
+// or, for a lane that outran its ring, the word from global memory, waited
+// for inside the branch (a select of the two would become a flat load,
+// which waits for every outstanding load -- the refills -- at its use)
+#define RING_STEPS()                                                                       \
+    for (uint32_t s_ = 0; s_ < kRingG; ++s_) {                                             \
+        if (live) {                                                                        \
+            live = res_step(r, S, Z, sink, st);                                            \
+            const uint64_t nw_ = S.cw + 2;                                                 \
+            S.nx = ring[nw_ & (kRing - 1)];                                                \
+            if (nw_ < rbeg || nw_ >= fill) {                                               \
+                const uint32_t g_ = r.w[nw_ < r.last ? nw_ : r.last];                      \
+                asm volatile("" : : "v"(g_));                                              \
+                S.nx = g_;                                                                 \
+            }                                                                              \
+        }                                                                                  \
+    }
+
+// flacdec_read_residual (flac.c:1135-1209), residuals handed to `sink`.
 template <class P, bool RING = false>
 __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N, P &sink,
                                             uint32_t *ring = nullptr)
@@ -422,143 +562,253 @@ __device__ __forceinline__ int dec_residual(BitR &r, uint32_t order, uint32_t N,
         return FD_ERROR;
     if (method > 1)
         RET(FD_CODING); // raised at the first partition (flac.c:1160-1170)
-    const uint32_t plen_all = N >> porder;
-    const uint32_t p0 = plen_all > order ? plen_all - order : 0u;
-    const uint32_t parts = 1u << porder;
-    const uint32_t total = p0 + (parts - 1u) * plen_all;
-    const uint32_t pbits = method ? 5u : 4u, escv = method ? 0x1Fu : 0xFu;
-    uint32_t k = 0, hdrs = 0, left = 0, rice = 0, esc = 0;
-#if ATG_DEC_READER == 0
-    uint32_t wa, wb;
-    r.words(wa, wb);
-#else
-    // register window: hi:lo = words cw, cw+1; nx = word cw+2 (raw), reloaded
-    // every iteration (one L1-resident load, issued before the MACs)
-    uint64_t cw = r.bw + (r.pos >> 5);
-    uint32_t off = r.pos & 31;
-    uint32_t hi = bswap32(r.w[cw < r.last ? cw : r.last]);
-    uint32_t lo = bswap32(r.w[cw + 1 < r.last ? cw + 1 : r.last]);
-    uint32_t nx;
-    uint64_t fill = 0, pf = 0; // ring: words [fill - kRing, fill) committed; pending block at pf
-    uint4 pa = make_uint4(0, 0, 0, 0), pb = pa;
-    bool pend = false;
-    uint32_t it = 0;
-    if (RING) {
-        const uint64_t a0 = cw & ~3ull;
-#pragma unroll
-        for (uint32_t i = 0; i < 8; ++i)
-            ring[(a0 + i) & (kRing - 1)] = r.w[a0 + i < r.last ? a0 + i : r.last];
-        fill = a0 + 8;
-        nx = ring[(cw + 2) & (kRing - 1)];
+    ResShape Z;
+    Z.plen = N >> porder;
+    Z.p0 = Z.plen > order ? Z.plen - order : 0u;
+    Z.parts = 1u << porder;
+    Z.total = Z.p0 + (Z.parts - 1u) * Z.plen;
+    Z.pbits = method ? 5u : 4u;
+    Z.escv = method ? 0x1Fu : 0xFu;
+    ResState S;
+    S.k = S.hdrs = S.left = S.rice = S.esc = 0;
+    S.cw = r.bw + (r.pos >> 5);
+    S.off = r.pos & 31;
+    S.hi = bswap32(r.w[S.cw < r.last ? S.cw : r.last]);
+    S.lo = bswap32(r.w[S.cw + 1 < r.last ? S.cw + 1 : r.last]);
+    int st = FD_OK;
+    bool live = true; // parts >= 1: at least one header
+    if (RING && (((uintptr_t)r.w) & 15u) == 0 && r.last >= 2 * kRingB) {
+        // ring: words [rbeg, fill) are in the LDS ring, loads issued up to
+        // nf; two blocks up front (the first refill lands 2 kRingG
+        // iterations on); blocks sit at multiples of 16 words, so a block
+        // never wraps the ring
+        const uint64_t a0 = (S.cw & ~15ull) + 2 * kRingB <= r.last + 1
+                                ? (S.cw & ~15ull) : ((r.last + 1 - 2 * kRingB) & ~15ull);
+        {
+            uint4 x0, x1, x2, x3, y0, y1, y2, y3;
+            ring_load4((const uint4 *)(r.w + a0), x0, x1, x2, x3);
+            ring_load4((const uint4 *)(r.w + a0 + kRingB), y0, y1, y2, y3);
+            uint4 *d0 = (uint4 *)(ring + (a0 & (kRing - 1)));
+            uint4 *d1 = (uint4 *)(ring + ((a0 + kRingB) & (kRing - 1)));
+            d0[0] = x0;
+            d0[1] = x1;
+            d0[2] = x2;
+            d0[3] = x3;
+            d1[0] = y0;
+            d1[1] = y1;
+            d1[2] = y2;
+            d1[3] = y3;
+        }
+        uint64_t rbeg = a0, fill = a0 + 2 * kRingB, nf = fill;
+        {
+            const uint64_t nw = S.cw + 2;
+            S.nx = nw >= rbeg && nw < fill ? ring[nw & (kRing - 1)]
+                                           : r.w[nw < r.last ? nw : r.last];
+        }
+        // the window's first words are waited for here: a load still in
+        // flight into them at the loop entry would make the compiler wait
+        // for every outstanding load (the refills) at each use in the loop
+        asm volatile("" : : "v"(S.nx), "v"(S.hi), "v"(S.lo));
+        uint4 qa0, qa1, qa2, qa3, qb0, qb1, qb2, qb3; // the two refill buffers
+        uint64_t aa = 0, ab = 0;
+        bool pa = false, pb = false;
+        // every lane of the wave that runs this loop entered it together:
+        // refill points are wave-uniform; a buffer's loads are committed two
+        // points later (its registers never move, so the wait is a counted
+        // vmcnt past the other buffer's loads)
+        while (__ballot(live) != 0ull) {
+            RING_STEPS();
+            RING_REFILL(qa0, qa1, qa2, qa3, aa, pa);
+            RING_STEPS();
+            RING_REFILL(qb0, qb1, qb2, qb3, ab, pb);
+        }
     } else {
-        nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
+        S.nx = r.w[S.cw + 2 < r.last ? S.cw + 2 : r.last];
+        while (live) {
+            live = res_step(r, S, Z, sink, st);
+            S.nx = r.w[S.cw + 2 < r.last ? S.cw + 2 : r.last];
+        }
     }
-#endif
-    while (k < total || hdrs < parts) {
-#if ATG_DEC_READER == 0
-        const uint32_t p = r.window(wa, wb);
-#else
-        const uint32_t p = off ? (hi << off) | (lo >> (32 - off)) : hi;
-#endif
-        const bool hdr = left == 0;
-        // partition header: Rice parameter (+ escape width)
-        const uint32_t hr = p >> (32 - pbits);
-        const bool hesc = hr == escv;
-        const uint32_t hlen = pbits + (hesc ? 5u : 0u);
-        const uint32_t hbits = (p >> (27 - pbits)) & 31u;
-        // residual: Rice code (unary MSBs, stop bit, LSBs) or escaped raw
-        const uint32_t z = __builtin_clz(p | 1u);
-        const uint32_t clen = z + 1 + rice;
-        const uint32_t lsb = __builtin_amdgcn_ubfe(p, 31 - z - rice, rice);
-        const uint32_t value = (z << rice) | lsb;
-        int32_t v = (int32_t)(value >> 1) ^ -(int32_t)(value & 1u);
-        uint32_t len = clen;
-        if (esc) {
-            v = (int32_t)p >> (32 - esc);
-            len = esc;
-        }
-        const uint32_t step = hdr ? hlen : len;
-#if ATG_DEC_READER == 0
-        if (!hdr && !esc && (p == 0 || clen > 32)) { // rare: long code
-            const uint32_t msb = r.zeros();
-            const uint32_t val = (msb << rice) | r.get(rice);
-            v = (int32_t)(val >> 1) ^ -(int32_t)(val & 1u);
-        } else {
-            r.skip(step);
-        }
-        // the next code's words are requested before this sample's
-        // prediction, whose MACs then cover the load latency
-        r.words(wa, wb);
-#else
-        if (!hdr && !esc && (p == 0 || clen > 32)) { // rare: long code
-            r.pos = (uint32_t)((cw - r.bw) * 32) + off;
-            const uint32_t msb = r.zeros();
-            const uint32_t val = (msb << rice) | r.get(rice);
-            v = (int32_t)(val >> 1) ^ -(int32_t)(val & 1u);
-            cw = r.bw + (r.pos >> 5);
-            off = r.pos & 31;
-            hi = bswap32(r.w[cw < r.last ? cw : r.last]);
-            lo = bswap32(r.w[cw + 1 < r.last ? cw + 1 : r.last]);
-        } else {
-            off += step;
-            const bool need = off >= 32;
-            hi = need ? lo : hi;
-            lo = need ? bswap32(nx) : lo;
-            cw += need ? 1u : 0u;
-            off -= need ? 32u : 0u;
-        }
-        if (RING) {
-            if (cw + 2 < fill)
-                nx = ring[(cw + 2) & (kRing - 1)];
-            else
-                nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
-            if ((++it & (kRingG - 1)) == 0) { // wave-uniform refill point
-                if (pend) {
-                    const uint32_t b = (uint32_t)pf & (kRing - 1); // pf is 4-word aligned
-                    ring[b] = pa.x;
-                    ring[b + 1] = pa.y;
-                    ring[b + 2] = pa.z;
-                    ring[b + 3] = pa.w;
-                    const uint32_t b2 = (b + 4) & (kRing - 1);
-                    ring[b2] = pb.x;
-                    ring[b2 + 1] = pb.y;
-                    ring[b2 + 2] = pb.z;
-                    ring[b2 + 3] = pb.w;
-                    fill = pf + 8;
-                    pend = false;
-                }
-                if (fill + 8 + 2 <= cw + kRing && fill + 8 <= r.last + 1) {
-                    pf = fill;
-                    if ((((uintptr_t)r.w) & 15u) == 0) {
-                        pa = *(const uint4 *)(r.w + fill);
-                        pb = *(const uint4 *)(r.w + fill + 4);
-                    } else { // a caller buffer aligned to 4 bytes only
-                        pa = make_uint4(r.w[fill], r.w[fill + 1], r.w[fill + 2], r.w[fill + 3]);
-                        pb = make_uint4(r.w[fill + 4], r.w[fill + 5], r.w[fill + 6], r.w[fill + 7]);
-                    }
-                    pend = true;
-                }
-            }
-        } else {
-            nx = r.w[cw + 2 < r.last ? cw + 2 : r.last];
-        }
-#endif
-        sink.step(v, !hdr);
-        k += hdr ? 0u : 1u;
-        left = hdr ? (hdrs == 0 ? p0 : plen_all) : left - 1u;
-        rice = hdr ? hr : rice;
-        esc = hdr ? (hesc ? hbits : 0u) : esc;
-        hdrs += hdr ? 1u : 0u;
-#if ATG_DEC_READER != 0
-        if (hdr)
-            r.pos = (uint32_t)((cw - r.bw) * 32) + off;
-#endif
-        if (hdr && r.eof())
-            return FD_EOF;
+    if (st != FD_OK)
+        return st;
+    r.pos = (uint32_t)((S.cw - r.bw) * 32) + S.off;
+    if (r.eof())
+        return FD_EOF;
+    return FD_OK;
+}
+
+// The residual walk on a 64-bit window (the parse kernel's and, with
+// values, the restore kernel's loop).  W holds the stream's next `avail`
+// bits MSB-first; cw indexes the next word to enter it, nx = that word (raw,
+// read from the lane's LDS ring one iteration ahead).  An iteration consumes
+// one partition header or one residual (at most 37 bits, after a refill of
+// one word whenever fewer than 32 bits are left, so the window never runs
+// dry on the fast path) with selects only: lanes in different partitions,
+// Rice parameters or escapes stay in lockstep, ~25 VALU per residual
+// against ~120 for the word-window step with its per-lane branches (the
+// parse loop was instruction-issue bound at one wave per SIMD).  Codes
+// longer than the window (> 32 zero bits, or LSBs past the window) and
+// lanes whose ring does not hold cw take wave-uniform slow paths.
+constexpr uint32_t kWalkInit = 3; // ring blocks loaded before the loop
+
+template <bool VALUES, class P>
+__device__ __forceinline__ int walk_residual(BitR &r, uint32_t order, uint32_t N, P &sink,
+                                             uint32_t *ring)
+{
+    const uint32_t method = r.get(2);
+    const uint32_t porder = r.get(4);
+    sink.partition_order(porder);
+    if (!r.eof() && method <= 1 && ((N >> porder) << porder) != N)
+        return FD_ERROR;
+    if (method > 1)
+        RET(FD_CODING); // raised at the first partition (flac.c:1160-1170)
+    const uint32_t plen = N >> porder;
+    const uint32_t p0 = plen > order ? plen - order : 0u;
+    const uint32_t parts = 1u << porder;
+    const uint32_t pbits = method ? 5u : 4u, escv = method ? 0x1Fu : 0xFu;
+    uint32_t units = p0 + (parts - 1u) * plen + parts; // headers + residuals left
+    uint32_t left = 0, rice = 0, esc = 0, hdrs = 0;
+    // ring: blocks of 16 words at multiples of 16; kWalkInit up front
+    const uint64_t p_abs = r.abspos();
+    uint64_t cw = p_abs >> 5;
+    const uint64_t lastw = r.last;
+    const uint64_t a0 = (cw & ~15ull) + kWalkInit * kRingB <= lastw + 1
+                            ? (cw & ~15ull) : ((lastw + 1 - kWalkInit * kRingB) & ~15ull);
+    {
+        uint4 x0, x1, x2, x3, y0, y1, y2, y3, z0, z1, z2, z3;
+        ring_load4((const uint4 *)(r.w + a0), x0, x1, x2, x3);
+        ring_load4((const uint4 *)(r.w + a0 + kRingB), y0, y1, y2, y3);
+        ring_load4((const uint4 *)(r.w + a0 + 2 * kRingB), z0, z1, z2, z3);
+        uint4 *d0 = (uint4 *)(ring + (a0 & (kRing - 1)));
+        uint4 *d1 = (uint4 *)(ring + ((a0 + kRingB) & (kRing - 1)));
+        uint4 *d2 = (uint4 *)(ring + ((a0 + 2 * kRingB) & (kRing - 1)));
+        d0[0] = x0; d0[1] = x1; d0[2] = x2; d0[3] = x3;
+        d1[0] = y0; d1[1] = y1; d1[2] = y2; d1[3] = y3;
+        d2[0] = z0; d2[1] = z1; d2[2] = z2; d2[3] = z3;
     }
-#if ATG_DEC_READER != 0
-    r.pos = (uint32_t)((cw - r.bw) * 32) + off;
-#endif
+    uint64_t rbeg = a0, fill = a0 + kWalkInit * kRingB, nf = fill;
+    // the window: the bits from p_abs to the end of word cw + 1
+    uint32_t avail;
+    uint64_t W;
+    {
+        const uint32_t w0 = bswap32(r.w[cw < lastw ? cw : lastw]);
+        const uint32_t w1 = bswap32(r.w[cw + 1 < lastw ? cw + 1 : lastw]);
+        const uint32_t sh = (uint32_t)(p_abs & 31);
+        W = (((uint64_t)w0 << 32) | w1) << sh;
+        avail = 64 - sh;
+        cw += 2;
+    }
+    uint32_t nx = cw >= rbeg && cw < fill ? ring[cw & (kRing - 1)] : r.w[cw < lastw ? cw : lastw];
+    asm volatile("" : : "v"(nx), "v"(W)); // waited before the loop (see RING_STEPS)
+    uint4 qa0, qa1, qa2, qa3, qb0, qb1, qb2, qb3;
+    uint64_t aa = 0, ab = 0;
+    bool pa = false, pb = false;
+    bool live = units != 0, eof = false;
+    struct Nop {
+    } nop;
+    (void)nop;
+#define WALK_STEPS()                                                                       \
+    for (uint32_t s_ = 0; s_ < kRingG; ++s_) {                                             \
+        bool slow = false;                                                                 \
+        if (live) {                                                                        \
+            const bool need = avail < 32;                                                  \
+            W = need ? W | ((uint64_t)bswap32(nx) << (32 - avail)) : W;                    \
+            avail += need ? 32u : 0u;                                                      \
+            cw += need ? 1u : 0u;                                                          \
+            const uint32_t top = (uint32_t)(W >> 32);                                      \
+            const bool hdr = left == 0;                                                    \
+            const uint32_t hr = top >> (32 - pbits);                                       \
+            const bool hesc = hr == escv;                                                  \
+            const uint32_t hlen = pbits + (hesc ? 5u : 0u);                                \
+            const uint32_t hbits = (top >> (27 - pbits)) & 31u;                            \
+            const uint32_t z = __builtin_clz(top | 1u);                                    \
+            const uint32_t clen = z + 1u + rice;                                           \
+            const uint32_t len = hdr ? hlen : (esc ? esc : clen);                          \
+            slow = !hdr && !esc && (top == 0u || clen > avail);                            \
+            if (VALUES) {                                                                  \
+                const uint32_t mid = (uint32_t)((W << (z + 1u)) >> 32);                    \
+                const uint32_t value = (z << rice) | __builtin_amdgcn_ubfe(mid, 32u - rice, rice); \
+                int32_t v = (int32_t)(value >> 1) ^ -(int32_t)(value & 1u);                \
+                v = esc ? (int32_t)top >> (32u - esc) : v;                                 \
+                if (!slow)                                                                 \
+                    sink.step(v, !hdr);                                                    \
+            }                                                                              \
+            const uint32_t sl = slow ? 0u : len;                                           \
+            W = sl >= 64u ? 0ull : W << sl;                                                \
+            avail -= sl;                                                                   \
+            left = hdr ? (hdrs == 0u ? p0 : plen) : left - (slow ? 0u : 1u);               \
+            rice = hdr ? hr : rice;                                                        \
+            esc = hdr ? (hesc ? hbits : 0u) : esc;                                         \
+            hdrs += hdr ? 1u : 0u;                                                         \
+            units -= slow ? 0u : 1u;                                                       \
+            /* a header past the track end: the reference aborts (EOF) */                  \
+            if (hdr && cw * 32 - avail > r.bw * 32 + r.end) {                              \
+                eof = true;                                                                \
+                slow = false;                                                              \
+            }                                                                              \
+            live = units != 0u && !eof;                                                    \
+            nx = ring[cw & (kRing - 1)];                                                   \
+        }                                                                                  \
+        if (__ballot(slow || (live && (cw < rbeg || cw >= fill))) != 0ull) {               \
+            if (slow) { /* a code the window cannot hold: the bit reader */                \
+                r.pos = (uint32_t)(cw * 32 - avail - r.bw * 32);                           \
+                const uint32_t msb = r.zeros();                                            \
+                const uint32_t val = (msb << rice) | r.get(rice);                          \
+                if (VALUES)                                                                \
+                    sink.step((int32_t)(val >> 1) ^ -(int32_t)(val & 1u), true);           \
+                const uint64_t pa_ = r.abspos();                                           \
+                cw = pa_ >> 5;                                                             \
+                const uint32_t w0 = bswap32(r.w[cw < lastw ? cw : lastw]);                 \
+                const uint32_t w1 = bswap32(r.w[cw + 1 < lastw ? cw + 1 : lastw]);         \
+                const uint32_t sh = (uint32_t)(pa_ & 31);                                  \
+                W = (((uint64_t)w0 << 32) | w1) << sh;                                     \
+                avail = 64 - sh;                                                           \
+                cw += 2;                                                                   \
+                left -= 1u;                                                                \
+                units -= 1u;                                                               \
+                eof = r.eof();                                                             \
+                live = units != 0u && !eof;                                                \
+            }                                                                              \
+            if (live && (cw < rbeg || cw >= fill)) {                                       \
+                const uint32_t g_ = r.w[cw < lastw ? cw : lastw];                          \
+                asm volatile("" : : "v"(g_));                                              \
+                nx = g_;                                                                   \
+            } else if (live) {                                                             \
+                nx = ring[cw & (kRing - 1)];                                               \
+            }                                                                              \
+        }                                                                                  \
+    }
+#define WALK_REFILL(q0, q1, q2, q3, addr, pend)                                            \
+    do {                                                                                   \
+        if (pend && addr >= fill) {                                                        \
+            if (addr > fill)                                                               \
+                rbeg = addr;                                                               \
+            uint4 *d_ = (uint4 *)(ring + (addr & (kRing - 1)));                            \
+            d_[0] = q0;                                                                    \
+            d_[1] = q1;                                                                    \
+            d_[2] = q2;                                                                    \
+            d_[3] = q3;                                                                    \
+            fill = addr + kRingB;                                                          \
+            rbeg = fill > rbeg + kRing ? fill - kRing : rbeg;                              \
+        }                                                                                  \
+        const uint64_t a_ = nf > (cw & ~15ull) ? nf : (cw & ~15ull);                       \
+        pend = a_ + kRingB <= cw + kRing && a_ + kRingB <= lastw + 1;                      \
+        ring_load4((const uint4 *)(r.w + (pend ? a_ : ((lastw + 1 - kRingB) & ~3ull))), q0, q1, \
+                   q2, q3);                                                                \
+        addr = a_;                                                                         \
+        nf = pend ? a_ + kRingB : nf;                                                      \
+    } while (0)
+    while (__ballot(live) != 0ull) {
+        WALK_STEPS();
+        WALK_REFILL(qa0, qa1, qa2, qa3, aa, pa);
+        WALK_STEPS();
+        WALK_REFILL(qb0, qb1, qb2, qb3, ab, pb);
+    }
+#undef WALK_STEPS
+#undef WALK_REFILL
+    if (eof)
+        return FD_EOF;
+    r.pos = (uint32_t)(cw * 32 - avail - r.bw * 32);
     if (r.eof())
         return FD_EOF;
     return FD_OK;
@@ -599,11 +849,11 @@ __device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps, uint32_t *ring 
     if (sh.kind == 0) {
         r.get_signed(bps);
     } else if (sh.kind == 1) {
-        for (uint32_t i = 0; i < N; ++i) {
-            r.get_signed(bps);
-            if ((i & 255) == 255 && r.eof())
-                break;
-        }
+        // VERBATIM: N raw samples of bps bits (0 bits asks for 2^32-1
+        // magnitude bits per sample: EOF); the parse only skips them -- read
+        // one by one, each a dependent load, they set the pace of every wave
+        // holding a white-noise frame
+        r.skip_far(bps ? (uint64_t)N * bps : (N ? 1ull << 33 : 0ull));
     } else {
         for (uint32_t i = 0; i < sh.order; ++i)
             r.get_signed(bps);
@@ -613,7 +863,9 @@ __device__ int parse_subframe(BitR &r, uint32_t N, uint32_t bps, uint32_t *ring 
             for (uint32_t i = 0; i < sh.order; ++i)
                 r.get_signed(prec);
         }
-        rc = dec_residual<NullSink, RING>(r, sh.order, N, np, ring);
+        rc = RING && (((uintptr_t)r.w) & 15u) == 0 && r.last >= kWalkInit * kRingB
+                 ? walk_residual<false>(r, sh.order, N, np, ring)
+                 : dec_residual<NullSink, false>(r, sh.order, N, np);
         if (rc)
             return rc;
         if (sh.kind == 2 && sh.order > 4)
@@ -651,7 +903,8 @@ __device__ uint32_t crc16_range(const uint32_t *w, uint64_t b0, uint64_t b1,
 
 // one frame of the reference's read() loop, parse only: header, subframes
 // with N = MIN(block size, nlimit), byte align, CRC-16
-template <bool RING = false>
+// CRC = false: the frame's CRC-16 is left to k_dec_crc (status stays OK)
+template <bool RING = false, bool CRC = true>
 __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const DecTrack &t,
                             uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec,
                             uint32_t *ring = nullptr)
@@ -686,12 +939,10 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
     }
     const uint64_t endb = r.abspos() >> 3;
     rec.bytes = (uint32_t)(endb - pos);
-#if ATG_DEC_EXP == 3 // timing experiment only: no CRC-16
-    rec.status = FD_OK;
-    (void)T;
-#else
-    rec.status = crc16_range(w, pos, endb, T) ? FD_FRAME_CRC : FD_OK;
-#endif
+    if (CRC)
+        rec.status = crc16_range(w, pos, endb, T) ? FD_FRAME_CRC : FD_OK;
+    else
+        rec.status = FD_OK;
 }
 
 __device__ __forceinline__ void load_crc_lds(uint16_t (*T)[256])
@@ -725,16 +976,42 @@ __device__ __forceinline__ bool sync_at(uint32_t a, uint32_t b, int k)
     return ((uint32_t)(pair >> (48 - 8 * k)) & 0xFFFEu) == 0xFFF8u;
 }
 
-__global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w, uint64_t nw,
-                                                  uint64_t len, const DecTrack *__restrict__ tr,
-                                                  uint32_t nt, uint32_t *__restrict__ ncand,
-                                                  uint32_t cap, uint64_t *__restrict__ cand_pos,
-                                                  uint32_t *__restrict__ cand_idx)
+// K1a: the sync-pattern positions, streamed: a lane takes one 16-byte load
+// (plus the next chunk's first word for a pattern straddling the chunks)
+// and appends its hits to the list -- the rare lanes with a hit do one
+// atomic each; no header is parsed here, so the pass runs at streaming rate
+// (the single-pass scan parsed each hit's header in place, serialising its
+// dependent loads on the wave that found it: 1.0 ms per config-2 batch).
+// Only the bytes inside tracks are read: the host lists them as segments of
+// at most kSegChunks 16-byte chunks (a batch laid out in per-track output
+// slots, as the encoder leaves it, is half gaps); a workgroup streams one
+// segment at a time.
+constexpr uint32_t kSegChunks = 4096; // 64 KB
+
+struct ScanSeg {
+    uint64_t c0; // first 16-byte chunk
+    uint32_t n;  // chunks
+    uint32_t pad;
+};
+
+__global__ __launch_bounds__(256) void k_dec_sync(const uint32_t *__restrict__ w, uint64_t nw,
+                                                  uint64_t len, const ScanSeg *__restrict__ segs,
+                                                  uint32_t nseg, uint32_t *__restrict__ nhit,
+                                                  uint64_t hcap, uint64_t *__restrict__ hits)
 {
-    const uint64_t nchunk = (nw + 3) / 4;
+    // the workgroup's hits gather in LDS and go out with one global atomic
+    // per workgroup: one atomic per hit-holding wave (~80 k, one address)
+    // held the pass at 0.87 ms whatever the bytes scanned
+    constexpr uint32_t kLocal = 2048;
+    __shared__ uint64_t lpos[kLocal];
+    __shared__ uint32_t lcnt, lbase;
+    if (threadIdx.x == 0)
+        lcnt = 0;
+    __syncthreads();
     const bool a16 = ((uintptr_t)w & 15u) == 0; // the API promises 4-byte alignment only
-    for (uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; c < nchunk;
-         c += (uint64_t)gridDim.x * blockDim.x) {
+    for (uint32_t sg = blockIdx.x; sg < nseg; sg += gridDim.x)
+    for (uint64_t c = segs[sg].c0 + threadIdx.x, ce = segs[sg].c0 + segs[sg].n; c < ce;
+         c += blockDim.x) {
         uint32_t v[5];
         if (a16 && 4 * c + 4 <= nw) {
             const uint4 q = *(const uint4 *)(w + 4 * c);
@@ -748,34 +1025,69 @@ __global__ __launch_bounds__(256) void k_dec_scan(const uint32_t *__restrict__ w
                 v[i] = 4 * c + i < nw ? w[4 * c + i] : 0u;
         }
         v[4] = 4 * c + 4 < nw ? w[4 * c + 4] : 0u;
-        uint32_t hits = 0; // bit 4j+k: a sync pattern at byte 4j+k of the chunk
+        uint32_t m = 0; // bit 4j+k: a sync pattern at byte 4j+k of the chunk
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint32_t a = bswap32(v[j]), b = bswap32(v[j + 1]);
 #pragma unroll
             for (int k = 0; k < 4; ++k)
-                hits |= sync_at(a, b, k) ? 1u << (4 * j + k) : 0u;
+                m |= sync_at(a, b, k) ? 1u << (4 * j + k) : 0u;
         }
-        while (hits) {
-            const int bit = __builtin_ctz(hits);
-            hits &= hits - 1;
+        while (m) {
+            const int bit = __builtin_ctz(m);
+            m &= m - 1;
             const uint64_t p = 16 * c + (uint64_t)bit;
-            if (p + 1 >= len)
-                continue;
-            const uint32_t t = find_track(tr, nt, p);
-            const DecTrack T = tr[t];
-            if (p < T.start || p >= T.end)
-                continue;
-            BitR r;
-            r.init(w, nw, p * 8, T.end * 8);
-            Hdr h;
-            if (dec_header(r, T, h) != FD_OK)
-                continue;
-            const uint32_t i = atomicAdd(ncand, 1u);
-            if (i < cap) { // over capacity: the host re-scans with room for all
-                cand_pos[i] = p;
-                cand_idx[p] = i;
+            const uint64_t pp = p < len ? p : len; // (a pattern in the pad past len)
+            const uint32_t i = atomicAdd(&lcnt, 1u);
+            if (i < kLocal) {
+                lpos[i] = pp;
+            } else { // a dense run of patterns: straight to the list
+                const uint32_t g = atomicAdd(nhit, 1u);
+                if (g < hcap) // over capacity: the host re-scans with room for all
+                    hits[g] = pp;
             }
+        }
+    }
+    __syncthreads();
+    const uint32_t nl = min(lcnt, kLocal);
+    if (threadIdx.x == 0)
+        lbase = nl ? atomicAdd(nhit, nl) : 0u;
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < nl; i += blockDim.x)
+        if (lbase + i < hcap)
+            hits[lbase + i] = lpos[i];
+}
+
+// K1b: lane per sync position: the full frame-header parse (CRC-8 and the
+// STREAMINFO checks, flac.c:710-851); survivors are the candidates
+// (cand_pos[i], cand_idx[byte] = i)
+__global__ __launch_bounds__(256) void k_dec_hdr(const uint32_t *__restrict__ w, uint64_t nw,
+                                                 uint64_t len, const DecTrack *__restrict__ tr,
+                                                 uint32_t nt, const uint32_t *__restrict__ nhit,
+                                                 uint64_t hcap, const uint64_t *__restrict__ hits,
+                                                 uint32_t *__restrict__ ncand, uint32_t cap,
+                                                 uint64_t *__restrict__ cand_pos,
+                                                 uint32_t *__restrict__ cand_idx)
+{
+    const uint64_t n = min((uint64_t)*nhit, hcap);
+    for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n;
+         h += (uint64_t)gridDim.x * blockDim.x) {
+        const uint64_t p = hits[h];
+        if (p + 1 >= len)
+            continue;
+        const uint32_t t = find_track(tr, nt, p);
+        const DecTrack T = tr[t];
+        if (p < T.start || p >= T.end)
+            continue;
+        BitR r;
+        r.init(w, nw, p * 8, T.end * 8);
+        Hdr hd;
+        if (dec_header(r, T, hd) != FD_OK)
+            continue;
+        const uint32_t i = atomicAdd(ncand, 1u);
+        if (i < cap) { // over capacity: the host re-scans with room for all
+            cand_pos[i] = p;
+            cand_idx[p] = i;
         }
     }
 }
@@ -788,7 +1100,7 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
                                                   ParseRec *__restrict__ recs)
 {
     __shared__ uint16_t T[4][256];
-    __shared__ uint32_t ring[64 * kRingStride]; // the lanes' residual-word rings
+    __shared__ __align__(16) uint32_t ring[64 * kRingStride]; // the lanes' residual-word rings
     load_crc_lds(T);
     const uint32_t n = *ncand;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
@@ -796,8 +1108,121 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
         const DecTrack t = tr[find_track(tr, nt, p)];
         ParseRec rec;
         // 6: timing experiment, residual words straight from global memory
-        parse_frame<ATG_DEC_EXP != 6>(w, nw, p, t, ~0ull, T, rec, ring + threadIdx.x * kRingStride);
+        parse_frame<ATG_DEC_EXP != 6, false>(w, nw, p, t, ~0ull, T, rec,
+                                             ring + threadIdx.x * kRingStride);
         recs[i] = rec;
+    }
+}
+
+// CRC-16 advance: the state after 2^m more zero bytes (GF(2) matrix m)
+__device__ __forceinline__ uint32_t dcrc_adv(uint32_t c, int m)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        r ^= ((c >> i) & 1u) ? (uint32_t)c_crc_adv[m][i] : 0u;
+    return r;
+}
+
+// big-endian 32 bits at absolute byte b of the buffer (two aligned loads)
+__device__ __forceinline__ uint32_t be32_at(const uint32_t *w, uint64_t last, uint64_t b)
+{
+    const uint64_t i = b >> 2;
+    const uint32_t x = bswap32(w[i < last ? i : last]);
+    const uint32_t r = (uint32_t)(b & 3u);
+    if (!r)
+        return x;
+    const uint32_t y = bswap32(w[i + 1 < last ? i + 1 : last]);
+    return (x << (8u * r)) | (y >> (32u - 8u * r));
+}
+
+// K2b: CRC-16 of every parsed candidate frame (header to CRC bytes, whose
+// residue is 0 for an intact frame), a wave per frame: 64 chunks of
+// Lc = 2^m bytes of a virtually zero-prefixed image (leading zeros leave a
+// zero-init CRC unchanged), slicing by 4 from LDS tables, tree-combined with
+// the advance matrices.  The serial per-lane CRC in k_dec_parse cost 0.8 of
+// its 4.7 ms (profiles/r04_h_dec_probe.jsonl, ATG_DEC_EXP 3).
+__global__ __launch_bounds__(256) void k_dec_crc(const uint32_t *__restrict__ w, uint64_t nw,
+                                                 const uint32_t *__restrict__ ncand,
+                                                 const uint64_t *__restrict__ cand_pos,
+                                                 ParseRec *__restrict__ recs)
+{
+    __shared__ uint16_t T[4][256];
+    load_crc_lds(T);
+    const uint32_t n = *ncand;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+        const int st = recs[i].status;
+        const uint32_t L = recs[i].bytes;
+        if (st != FD_OK || L < 2u) // wave-uniform: one candidate per wave
+            continue;
+        const uint64_t pos = cand_pos[i];
+        if (L > (64u << 17)) { // beyond any real frame (the matrices reach 2^23)
+            if (lane == 0 && crc16_range(w, pos, pos + L, T))
+                recs[i].status = FD_FRAME_CRC;
+            continue;
+        }
+        uint32_t lc_log = 2;
+        while ((64u << lc_log) < L)
+            lc_log++;
+        const uint32_t Lc = 1u << lc_log;
+        const int64_t z = (int64_t)(64u << lc_log) - (int64_t)L;
+        uint32_t crc = 0;
+        int64_t q = (int64_t)lane * Lc - z; // image byte of this lane's first group
+        const int64_t qe = q + Lc;
+        if (q < 0) { // groups in the zero prefix leave crc = 0
+            q += ((-q) >> 2) << 2; // now -4 < q <= 0
+            if (q < 0 && q < qe) {
+                const uint32_t t = be32_at(w, nw - 1, pos) >> (8u * (uint32_t)(-q));
+                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
+                      T[0][t & 0xFFu];
+                q += 4;
+            }
+        }
+        // 256 bytes at a time: the 65 aligned words under them loaded at once
+        // (one memory latency per 256 bytes of the lane's chunk -- the wave
+        // spent 94 % of its cycles waiting with a latency per 64 bytes,
+        // profiles/r04_k_dec_pmc.txt), then the 64 big-endian words
+        for (; q + 256 <= qe; q += 256) {
+            const uint64_t b0 = pos + (uint64_t)q, i0 = b0 >> 2;
+            const uint32_t sb = 8u * (uint32_t)(b0 & 3);
+            uint32_t x[65];
+#pragma unroll
+            for (int u = 0; u < 65; ++u)
+                x[u] = bswap32(w[i0 + u < nw - 1 ? i0 + u : nw - 1]);
+#pragma unroll
+            for (int u = 0; u < 64; ++u) {
+                const uint32_t wd = sb ? (x[u] << sb) | (x[u + 1] >> (32u - sb)) : x[u];
+                const uint32_t t = wd ^ (crc << 16);
+                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
+                      T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
+            }
+        }
+        for (; q + 64 <= qe; q += 64) {
+            uint32_t x[16];
+#pragma unroll
+            for (int u = 0; u < 16; ++u)
+                x[u] = be32_at(w, nw - 1, pos + (uint64_t)(q + 4 * u));
+#pragma unroll
+            for (int u = 0; u < 16; ++u) {
+                const uint32_t t = x[u] ^ (crc << 16);
+                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
+                      T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
+            }
+        }
+        for (; q < qe; q += 4) {
+            const uint32_t t = be32_at(w, nw - 1, pos + (uint64_t)q) ^ (crc << 16);
+            crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
+                  T[0][t & 0xFFu];
+        }
+#pragma unroll
+        for (int k = 0; k < 6; ++k) {
+            const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << k, 64);
+            if ((lane & ((2u << k) - 1u)) == 0)
+                crc = dcrc_adv(crc, (int)lc_log + k) ^ other;
+        }
+        if (lane == 0 && crc)
+            recs[i].status = FD_FRAME_CRC;
     }
 }
 
@@ -886,12 +1311,12 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
 template <int W>
 __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
                                             uint32_t kind, uint32_t order, int32_t *out,
-                                            int4 *row, JobMeta &m, bool allow_fast)
+                                            int4 *row, JobMeta &m, bool allow_fast,
+                                            uint32_t *ring)
 {
     WinPred<W> p;
-    p.out = out;
     p.row = row;
-    p.t = 0;
+    p.q0 = p.q1 = p.q2 = p.q3 = 0;
     p.porder = 0;
     p.n = N;
     p.i = 0;
@@ -930,17 +1355,19 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
 #if ATG_DEC_EXP == 2 // timing experiment: int64 sums only
     p.fast = false;
 #endif
-    p.q0 = p.q1 = p.q2 = p.q3 = 0;
-    dec_residual(r, order, N, p);
+    if ((((uintptr_t)r.w) & 15u) == 0 && r.last >= kWalkInit * kRingB)
+        walk_residual<true>(r, order, N, p, ring);
+    else
+        dec_residual<WinPred<W>, false>(r, order, N, p);
     p.flush();
     m.porder = (uint8_t)p.porder;
-    m.iters = p.t;
+    m.iters = p.i;
     return p.fast && p.bad;
 }
 
-// K4: one subframe per lane.  Warm-up samples go to the job's 32-entry
-// warm-up cell; every residual-loop iteration stores to its row of the
-// wave's [row][lane] scratch (coalesced); K5 maps rows back to samples.
+// K4: one subframe per lane.  Every sample (warm-up, restored or verbatim)
+// goes to the job's column of the wave's [sample/4][lane][4] scratch
+// (coalesced 16-byte stores); K5 gathers 4 samples of a job per load.
 __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict__ w, uint64_t nw,
                                                      const DecTrack *__restrict__ tr,
                                                      const DecFrame *__restrict__ frames,
@@ -949,11 +1376,13 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
                                                      int32_t *__restrict__ rows, uint32_t nrows,
                                                      JobMeta *__restrict__ meta)
 {
+    __shared__ __align__(16) uint32_t rings[64 * kRingStride]; // the lanes' residual-word rings
+    uint32_t *ring = rings + threadIdx.x * kRingStride;
     const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= njobs)
         return;
     const uint2 jb = jobs[j];
-    const DecFrame f = frames[jb.x];
+    const DecFrame &f = frames[jb.x];
     const uint32_t c = jb.y;
     BitR r;
     r.init(w, nw, f.pos * 8 + f.sub_bit[c], tr[f.track].end * 8);
@@ -979,42 +1408,45 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
         } else if (sh.kind == 1) {
             m.kind = 1;
             m.iters = N;
-            for (uint32_t i = 0; i < N; ++i)
-                ((int32_t *)(row + (uint64_t)(i >> 2) * 64))[i & 3] =
-                    (int32_t)((uint32_t)r.get_signed(bps) << ws);
+            if (bps >= 1 && bps <= 32) {
+                // sample i sits at a known bit offset: the loads of a group
+                // of four are independent (no chain through the reader)
+                const uint64_t b0 = r.abspos();
+                for (uint32_t i = 0; i < N; i += 4) {
+                    int32_t v[4];
+#pragma unroll
+                    for (int q = 0; q < 4; ++q) {
+                        const uint64_t b = b0 + (uint64_t)(i + q) * bps;
+                        const uint64_t wi = b >> 5;
+                        const uint32_t a = bswap32(w[wi < r.last ? wi : r.last]);
+                        const uint32_t c = bswap32(w[wi + 1 < r.last ? wi + 1 : r.last]);
+                        const uint32_t sb = (uint32_t)(b & 31);
+                        const uint32_t x = sb ? (a << sb) | (c >> (32 - sb)) : a;
+                        v[q] = (int32_t)((uint32_t)((int32_t)x >> (32 - bps)) << ws);
+                    }
+                    row[(uint64_t)(i >> 2) * 64] = make_int4(v[0], v[1], v[2], v[3]);
+                }
+                r.skip_far((uint64_t)N * bps);
+            } else {
+                for (uint32_t i = 0; i < N; ++i)
+                    ((int32_t *)(row + (uint64_t)(i >> 2) * 64))[i & 3] =
+                        (int32_t)((uint32_t)r.get_signed(bps) << ws);
+            }
         } else {
             m.kind = 2;
             m.order = (uint8_t)sh.order;
             if (sh.order <= 12) {
                 const uint32_t at = r.pos;
-                if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, true)) {
+                if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, true, ring)) {
                     r.pos = at; // a sample left the bps range: redo with int64 sums
-                    restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false);
+                    restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring);
                 }
             } else {
-                restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false);
+                restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring);
             }
         }
     }
     meta[j] = m;
-}
-
-// Row of sample i of a FIXED/LPC job's residual loop : row 0 is partition 0's header, residual rr < p0 sits
-// at row rr + 1, and every later partition q has its header at row
-// p0 + 1 + q (plen + 1) followed by its plen residuals.
-__device__ __forceinline__ uint32_t row_of_sample(uint32_t i, uint32_t order, uint32_t porder,
-                                                  uint32_t n)
-{
-    const uint32_t rr = i - order;
-    const uint32_t plen = n >> porder;
-    const uint32_t p0 = plen > order ? plen - order : 0u;
-    if (rr < p0)
-        return rr + 1u;
-    const uint32_t tp = rr - p0;
-    uint32_t q = (uint32_t)((float)tp * (1.0f / (float)plen));
-    q -= q * plen > tp ? 1u : 0u;
-    q += (q + 1u) * plen <= tp ? 1u : 0u;
-    return p0 + 2u + q * (plen + 1u) + (tp - q * plen);
 }
 
 // K5: rows -> samples -> flacdec_decorrelate_channels (flac.c:1212-1269) ->
@@ -1041,7 +1473,6 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
 {
     __shared__ int32_t tile[kEmitJobs][kEmitTile + 1];
     __shared__ JobMeta jm[kEmitJobs];
-    __shared__ uint32_t jn[kEmitJobs];
     // the block's frames: first job (slot-relative), samples, channels,
     // assignment, bytes per MD5 sample, the bps clamp, output positions
     __shared__ uint32_t fj[64], fn[64], fch[64], fas[64], fbb[64];
@@ -1091,66 +1522,40 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
         m.order = 0;
         m.porder = 0;
         m.iters = 0;
-        uint32_t n = 0;
-        if (j < njobs) {
+        m.value = 0;
+        if (j < njobs)
             m = meta[j];
-            n = frames[jobs[j].x].n;
-        }
         jm[tid] = m;
-        jn[tid] = n;
     }
     __syncthreads();
     for (uint32_t i0 = 0; i0 < maxn; i0 += kEmitTile) {
-        // gather: lane = job, consecutive lanes read adjacent 16-byte cells;
-        // wave wv takes the tile's samples [16 wv, 16 wv + 16), its row
-        // found once and then stepped (one more at each partition header)
+        // gather: lane = job; K4 left every FIXED/LPC/VERBATIM job's samples
+        // (warm-up included) in sample order, [sample / 4][lane][4] per 64-job
+        // slot, so wave wv's 16 samples [16 wv, 16 wv + 16) of a job are four
+        // 16-byte loads (adjacent lanes: adjacent cells)
         for (uint32_t l = lane; l < NJ; l += 64) {
             const JobMeta m = jm[l];
-            const uint32_t n = jn[l];
             const uint64_t j = j0 + l;
-            // K4's [slot][row / 4][lane][4] scratch (nrows rows per slot)
-            const int32_t *__restrict__ cell = rows + (j >> 6) * nrows * 64u + (j & 63u) * 4u;
+            const int4 *__restrict__ cell =
+                (const int4 *)(rows + (j >> 6) * nrows * 64u) + (j & 63u);
             const uint32_t xa = 16u * wv, ia = i0 + xa;
-            const uint32_t plen = n >> m.porder;
-            const bool step = m.kind == 2 && plen > m.order;
-            uint32_t t = 0, rem = 0; // row of the next residual, residuals left in its partition
-            if (m.kind == 1)
-                t = ia;
-            else if (step) {
-                const uint32_t i = max(ia, (uint32_t)m.order);
-                const uint32_t rr = i - m.order, p0 = plen - m.order;
-                t = row_of_sample(i, m.order, m.porder, n);
-                rem = rr < p0 ? p0 - rr : plen - (rr - p0) % plen;
+            int4 q[4];
+            if (m.kind == 1 || m.kind == 2) {
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4)
+                    q[c4] = cell[(uint64_t)((ia >> 2) + c4) * 64];
+            } else {
+                const int32_t v = m.kind == 0 ? m.value : 0;
+#pragma unroll
+                for (int c4 = 0; c4 < 4; ++c4)
+                    q[c4] = make_int4(v, v, v, v);
             }
-#pragma unroll 4
-            for (uint32_t x = xa; x < xa + 16u; ++x) {
-                const uint32_t i = i0 + x;
-                if (i >= n)
-                    break;
-                int32_t v = 0;
-                bool rd = false;
-                if (m.kind == 0)
-                    v = m.value;
-                else if (m.kind == 1)
-                    rd = true;
-                else if (m.kind == 2) {
-                    if (i < m.order)
-                        v = warm[j * 32u + i];
-                    else if (!step)
-                        t = row_of_sample(i, m.order, m.porder, n), rd = true;
-                    else
-                        rd = true;
-                }
-                if (rd && ATG_DEC_EXP != 5) // 5: timing experiment, no row loads
-                    v = cell[(t >> 2) * 256u + (t & 3u)];
-                tile[l][x] = v;
-                if (m.kind == 1 || (step && i >= m.order)) {
-                    ++t;
-                    if (step && --rem == 0) {
-                        ++t; // the next partition's header row
-                        rem = plen;
-                    }
-                }
+#pragma unroll
+            for (int c4 = 0; c4 < 4; ++c4) {
+                tile[l][xa + 4 * c4] = q[c4].x;
+                tile[l][xa + 4 * c4 + 1] = q[c4].y;
+                tile[l][xa + 4 * c4 + 2] = q[c4].z;
+                tile[l][xa + 4 * c4 + 3] = q[c4].w;
             }
         }
         __syncthreads();
@@ -1292,11 +1697,30 @@ struct atg_decoder {
     hipStream_t s = nullptr;
     float times[kDecTimed] = {};
     bool have_times = false;
-    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs;
+    DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, hits, segs;
+    std::vector<ScanSeg> segs_h; // the scan's segments (upload source)
     DecSlot slot[kDecSlots];
     uint64_t next_ticket = 1;
     int last = -1; // slot of the last waited batch (decode_fetch)
 };
+
+static void build_dec_adv(const uint16_t t16[4][256], uint16_t adv[24][16])
+{
+    // adv[0]: one zero byte; adv[m] = adv[m-1] applied twice
+    for (int i = 0; i < 16; ++i) {
+        uint32_t c = 1u << i;
+        c = ((c << 8) ^ t16[0][(c >> 8) & 0xFFu]) & 0xFFFFu;
+        adv[0][i] = (uint16_t)c;
+    }
+    for (int m = 1; m < 24; ++m)
+        for (int i = 0; i < 16; ++i) {
+            uint32_t v = adv[m - 1][i], r = 0;
+            for (int j = 0; j < 16; ++j)
+                if ((v >> j) & 1u)
+                    r ^= adv[m - 1][j];
+            adv[m][i] = (uint16_t)r;
+        }
+}
 
 static void build_dec_tables(uint8_t *t8, uint16_t t16[4][256])
 {
@@ -1464,6 +1888,9 @@ atg_status atg_decoder_create(int device, atg_decoder **out)
     build_dec_tables(t8, t16);
     DHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_crc8), t8, sizeof(t8)));
     DHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), t16, sizeof(t16)));
+    static uint16_t adv[24][16];
+    build_dec_adv(t16, adv);
+    DHIP(hipMemcpyToSymbol(HIP_SYMBOL(c_crc_adv), adv, sizeof(adv)));
     atg_decoder *d = new atg_decoder();
     d->device = device;
     DHIP(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
@@ -1485,7 +1912,7 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs})
+                    &d->recs, &d->hits, &d->segs})
         b->release();
     for (DecSlot &sl : d->slot) {
         (void)hipStreamSynchronize(sl.s_md5);
@@ -1538,7 +1965,7 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     const uint64_t nw = std::max<uint64_t>(1, (len + 3) / 4);
     DHIP(d->tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
     DHIP(d->counts.ensure(sizeof(DecCount) * std::max<uint32_t>(n, 1)));
-    DHIP(d->ncand.ensure(sizeof(uint32_t)));
+    DHIP(d->ncand.ensure(2 * sizeof(uint32_t)));
     // candidate scratch: a real frame is >= 10 bytes, but the true count is
     // close to the frame count, so start at one slot per 16 bytes and re-scan
     // with the exact count in the rare batch that needs more
@@ -1549,28 +1976,86 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     DecTrack *dtr = (DecTrack *)d->tracks.p;
     hipEvent_t *ev = sl.ev;
     DHIP(hipEventRecord(ev[0], s));
-    uint32_t found = 0;
-    for (int pass = 0; pass < 2; ++pass) {
+    // the segments of the scan: the tracks' byte ranges (merged where they
+    // touch) in 16-byte chunks, cut at kSegChunks-chunk boundaries
+    {
+        std::vector<ScanSeg> &sg = d->segs_h;
+        sg.clear();
+        const uint64_t nchunk = (nw + 3) / 4;
+        uint64_t c0 = 0, c1 = 0; // the pending range [c0, c1)
+        auto flush = [&](uint64_t a, uint64_t b) {
+            for (uint64_t x = a; x < b; x += kSegChunks) {
+                ScanSeg g;
+                g.c0 = x;
+                g.n = (uint32_t)std::min<uint64_t>(b - x, kSegChunks);
+                g.pad = 0;
+                sg.push_back(g);
+            }
+        };
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint64_t a = tr[t].start / 16, b = std::min(nchunk, (tr[t].end + 15) / 16);
+            if (a >= b)
+                continue;
+            if (c1 > c0 && a <= c1) {
+                c1 = std::max(c1, b);
+            } else {
+                if (c1 > c0)
+                    flush(c0, c1);
+                c0 = a;
+                c1 = b;
+            }
+        }
+        if (c1 > c0)
+            flush(c0, c1);
+    }
+    const uint64_t nseg = d->segs_h.size();
+    DHIP(d->segs.ensure(sizeof(ScanSeg) * std::max<uint64_t>(nseg, 1)));
+    if (nseg)
+        DHIP(hipMemcpyAsync(d->segs.p, d->segs_h.data(), sizeof(ScanSeg) * nseg,
+                            hipMemcpyHostToDevice, s));
+    // counters: [0] candidates, [1] sync positions
+    uint32_t cnt_h[2] = {0, 0};
+    uint32_t &found = cnt_h[0];
+    uint64_t hcap = cap;
+    for (int pass = 0; pass < 3; ++pass) {
         DHIP(d->cand_pos.ensure(sizeof(uint64_t) * cap));
-        DHIP(hipMemsetAsync(d->ncand.p, 0, sizeof(uint32_t), s));
+        DHIP(d->hits.ensure(sizeof(uint64_t) * hcap));
+        DHIP(hipMemsetAsync(d->ncand.p, 0, 2 * sizeof(uint32_t), s));
         // grid-stride: at most 8 workgroups of 256 per CU (2048 over 256 CUs)
-        if (n && len)
-            hipLaunchKernelGGL(k_dec_scan,
-                               dim3((unsigned)std::min<uint64_t>(((nw + 3) / 4 + 255) / 256, 2048)),
-                               dim3(256), 0, s, w, nw, len, dtr, n, (uint32_t *)d->ncand.p,
-                               (uint32_t)cap, (uint64_t *)d->cand_pos.p, (uint32_t *)d->cand_idx.p);
+        if (n && len) {
+            hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)std::min<uint64_t>(nseg, 2048)),
+                               dim3(256), 0, s, w, nw, len, (const ScanSeg *)d->segs.p,
+                               (uint32_t)nseg, (uint32_t *)d->ncand.p + 1, hcap,
+                               (uint64_t *)d->hits.p);
+            hipLaunchKernelGGL(k_dec_hdr, dim3((unsigned)std::min<uint64_t>((hcap + 255) / 256, 1024)),
+                               dim3(256), 0, s, w, nw, len, dtr, n,
+                               (const uint32_t *)d->ncand.p + 1, hcap, (const uint64_t *)d->hits.p,
+                               (uint32_t *)d->ncand.p, (uint32_t)cap, (uint64_t *)d->cand_pos.p,
+                               (uint32_t *)d->cand_idx.p);
+        }
         DHIP(hipGetLastError());
-        DHIP(hipMemcpyAsync(&found, d->ncand.p, sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+        DHIP(hipMemcpyAsync(cnt_h, d->ncand.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
         DHIP(hipStreamSynchronize(s));
-        if (found <= cap)
-            break;
-        cap = found; // every sync position of the buffer is now known
+        if (cnt_h[1] > hcap) { // every sync position of the buffer is now known
+            hcap = cnt_h[1];
+            continue;
+        }
+        if (found > cap) {
+            cap = found;
+            continue;
+        }
+        break;
     }
     DHIP(d->recs.ensure(sizeof(ParseRec) * std::max<uint64_t>(found, 1)));
     DHIP(hipEventRecord(ev[1], s));
     hipLaunchKernelGGL(k_dec_parse, dim3(4096), dim3(64), 0, s, w, nw, dtr, n,
                        (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
                        (ParseRec *)d->recs.p);
+    DHIP(hipGetLastError());
+    if (found)
+        hipLaunchKernelGGL(k_dec_crc, dim3((unsigned)std::min<uint64_t>((found + 3) / 4, 8192)),
+                           dim3(256), 0, s, w, nw, (const uint32_t *)d->ncand.p,
+                           (const uint64_t *)d->cand_pos.p, (ParseRec *)d->recs.p);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(ev[2], s));
     const dim3 tg((n + 63) / 64);

@@ -69,6 +69,9 @@ def main():
     src = pcm.cpu().numpy().astype(np.int32)
     same = bool(np.array_equal(got, src))
     # pipelined
+    if a.steps == 0:
+        print(json.dumps({"tag": a.tag, "sync_kernel_ms": kt, "ok": ok, "pcm_same": same}))
+        return
     pend = []
     torch.cuda.synchronize()
     t0 = time.perf_counter()
@@ -76,12 +79,22 @@ def main():
         if len(pend) == a.inflight:
             dec.decode_wait(pend.pop(0))
         pend.append(dec.decode_device_async(out.data_ptr(), nbytes, dtr))
+    bad = {}
     while pend:
         last = dec.decode_wait(pend.pop(0))
+        for i, r in enumerate(last[0]):
+            if r.status != 0 or r.pcm_frames != ns:
+                bad.setdefault(int(r.status), []).append(i)
     dt = time.perf_counter() - t0
-    ok2 = all(r.status == 0 for r in last[0])
+    ok2 = not bad
+    same2 = False
+    if last[2] == pcm.numel():
+        got2 = np.empty(int(last[2]), dtype=np.int32)
+        eng.copy_to_host(got2, last[1])
+        same2 = bool(np.array_equal(got2, src))
     print(json.dumps({"tag": a.tag, "sync_kernel_ms": kt, "ok": ok, "pcm_same": same,
-                      "pipelined_ms_per_step": round(dt / a.steps * 1e3, 3), "pipelined_ok": ok2,
+                      "pipelined_ms_per_step": round(dt / a.steps * 1e3, 3), "pipelined_ok": ok2, "pipelined_bad": {k: v[:8] for k, v in bad.items()},
+                      "pipelined_last_pcm_same": same2,
                       "compressed_bytes": comp, "tracks": a.tracks}), flush=True)
 
 
