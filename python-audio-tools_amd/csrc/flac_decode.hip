@@ -1099,16 +1099,15 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
                                                   const uint64_t *__restrict__ cand_pos,
                                                   ParseRec *__restrict__ recs)
 {
-    __shared__ uint16_t T[4][256];
     __shared__ __align__(16) uint32_t ring[64 * kRingStride]; // the lanes' residual-word rings
-    load_crc_lds(T);
     const uint32_t n = *ncand;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t p = cand_pos[i];
         const DecTrack t = tr[find_track(tr, nt, p)];
         ParseRec rec;
-        // 6: timing experiment, residual words straight from global memory
-        parse_frame<ATG_DEC_EXP != 6, false>(w, nw, p, t, ~0ull, T, rec,
+        // (the frame's CRC-16 is k_dec_crc's; 6: timing experiment, residual
+        // words straight from global memory)
+        parse_frame<ATG_DEC_EXP != 6, false>(w, nw, p, t, ~0ull, nullptr, rec,
                                              ring + threadIdx.x * kRingStride);
         recs[i] = rec;
     }
@@ -2089,12 +2088,12 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     DHIP(sl.frames.ensure(sizeof(DecFrame) * std::max<uint64_t>(fb, 1)));
     DHIP(sl.jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
     DHIP(sl.warm.ensure(sizeof(int32_t) * 32 * std::max<uint64_t>(jb, 1)));
-    // row scratch: a residual loop runs at most N + 2^porder <= 2N iterations
     uint32_t max_bs = 1;
     for (uint32_t t = 0; t < n; ++t)
         if (sl.cnt[t].n_frames)
             max_bs = std::max(max_bs, tr[t].max_bs);
-    const uint32_t nrows = (2 * max_bs + 1 + 63) & ~63u; // whole 64-row tiles
+    // sample rows (warm-up samples included: at least 32), whole 64-row tiles
+    const uint32_t nrows = (std::max(max_bs, 32u) + 63) & ~63u;
     const uint64_t nslots = (jb + 63) / 64;
     DHIP(sl.rows.ensure(sizeof(int32_t) * std::max<uint64_t>(nslots, 1) * nrows * 64));
     DHIP(sl.meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
@@ -2217,7 +2216,7 @@ static atg_status take_dec_slot(atg_decoder *d, DecSlot **out)
         if (d->slot[k].ticket < sl->ticket)
             sl = &d->slot[k];
     if (sl->busy)
-        return dfail(ATG_ERR_INVALID, "three decode batches already in flight: wait for one");
+        return dfail(ATG_ERR_INVALID, "every decode slot holds a batch in flight: wait for one");
     sl->ticket = d->next_ticket++;
     *out = sl;
     return ATG_OK;
