@@ -182,6 +182,12 @@ struct EncSlot {
 // host-to-host leg runs 1.09 M frames/s at normal priority, 1.83 M at high
 // (profiles/r03_d_*); the device-resident step is the same either way.
 // 0 only for experiments (tools/build_exp.sh)
+// K1 (and the batch's table uploads) on the slot's stream rather than the
+// main one: the LPC kernels of the batches behind run beside this batch's
+// search and pack (tools/gpu_r4p.sh: 9.22 -> 8.87 ms per config-2 step)
+#ifndef ATG_K1_AUX
+#define ATG_K1_AUX 1
+#endif
 #ifndef ATG_AUX_HIPRIO
 #define ATG_AUX_HIPRIO 1
 #endif
@@ -503,7 +509,8 @@ void tukey(uint32_t N, double *w)
     }
 }
 
-atg_status prepare_windows(atg_engine *e, Plan &pl)
+// (uploaded on stream s, the one the batch's LPC kernel runs on)
+atg_status prepare_windows(atg_engine *e, Plan &pl, hipStream_t s)
 {
     if (!pl.p.try_lpc)
         return ATG_OK;
@@ -524,7 +531,7 @@ atg_status prepare_windows(atg_engine *e, Plan &pl)
         HIP_TRY(e->windows.ensure(e->win_host.size() * sizeof(double) + 64));
         HIP_TRY(hipMemcpyAsync(e->windows.p, e->win_host.data(),
                                e->win_host.size() * sizeof(double), hipMemcpyHostToDevice,
-                               e->s_main));
+                               s));
         e->win_uploaded = e->win_host.size();
     }
     return ATG_OK;
@@ -765,7 +772,19 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
     p.n_reg_frames = (fmt == ATG_PCM_S16 && ((uintptr_t)d_pcm & 15u) == 0) ? pl.n_reg_prefix : 0u;
     HIP_TRY(hipSetDevice(e->device));
-    atg_status st = prepare_windows(e, pl);
+#if ATG_K1_AUX
+    // the tables, the LPC kernel and the MD5 chains on the slot's stream:
+    // the next batches' LPC kernels run beside this batch's search and pack.
+    // Whatever the LPC kernel reads is written on this stream (or waited
+    // for through wait_before): nothing the caller queued on the main
+    // stream is ordered before it
+    hipStream_t s_pre = sl.s_aux;
+#else
+    hipStream_t s_pre = e->s_main;
+#endif
+    if (wait_before)
+        HIP_TRY(hipStreamWaitEvent(s_pre, wait_before, 0));
+    atg_status st = prepare_windows(e, pl, s_pre);
     if (st != ATG_OK)
         return st;
     const size_t nf = pl.frames.size(), nt = pl.tracks.size();
@@ -806,19 +825,17 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     if (want_fdesc)
         HIP_TRY(ensure_pinned(sl.fdesc_h, sl.fdesc_cap, nf));
     sl.uploaded = nullptr;
-    if (wait_before)
-        HIP_TRY(hipStreamWaitEvent(e->s_main, wait_before, 0));
     if (upload && nf)
         HIP_TRY(hipMemcpyAsync(sl.frames.p, pl.frames.data(), nf * sizeof(FrameInfo),
-                               hipMemcpyHostToDevice, e->s_main));
+                               hipMemcpyHostToDevice, s_pre));
     if (upload && nt)
         HIP_TRY(hipMemcpyAsync(sl.tracks.p, pl.tracks.data(), nt * sizeof(TrackInfo),
-                               hipMemcpyHostToDevice, e->s_main));
+                               hipMemcpyHostToDevice, s_pre));
     if (upload && nf)
         HIP_TRY(hipMemcpyAsync(sl.order.p, pl.order.data(), nf * sizeof(uint32_t),
-                               hipMemcpyHostToDevice, e->s_main));
-    HIP_TRY(hipMemsetAsync(sl.err.p, 0, sizeof(uint32_t), e->s_main));
-    HIP_TRY(hipEventRecord(sl.ev_tables, e->s_main));
+                               hipMemcpyHostToDevice, s_pre));
+    HIP_TRY(hipMemsetAsync(sl.err.p, 0, sizeof(uint32_t), s_pre));
+    HIP_TRY(hipEventRecord(sl.ev_tables, s_pre));
 
     const FrameInfo *dfr = (const FrameInfo *)sl.frames.p;
     const TrackInfo *dtr = (const TrackInfo *)sl.tracks.p;
@@ -826,17 +843,17 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     uint32_t *derr = (uint32_t *)sl.err.p;
     hipEvent_t *ev = sl.ev;
 
-    HIP_TRY(hipEventRecord(ev[14], e->s_main));
-    HIP_TRY(hipEventRecord(ev[0], e->s_main));
+    HIP_TRY(hipEventRecord(ev[14], s_pre));
+    HIP_TRY(hipEventRecord(ev[0], s_pre));
     HIP_TRY(launch_lpc_analyze(p, d_pcm, fmt, dfr, (const double *)e->windows.p,
                                (int16_t *)sl.coef.p, (int8_t *)sl.shift.p, (uint8_t *)sl.est.p,
-                               e->s_main));
-    HIP_TRY(hipEventRecord(ev[1], e->s_main));
+                               s_pre));
+    HIP_TRY(hipEventRecord(ev[1], s_pre));
+#if ATG_K1_AUX
+    HIP_TRY(hipStreamWaitEvent(e->s_main, ev[1], 0));
+#endif
     // MD5 chains (a serial hash per track, high-priority waves) on the slot's
-    // stream, after the LPC kernel: its grid is only ~1.3 waves per SIMD deep,
-    // so a SIMD shared with a chain would leave straggler waves; the search
-    // and pack grids are deep enough to absorb them
-    // MD5 chains on the slot's stream once the LPC kernel is done.  Split
+    // stream once the LPC kernel is done.  Split
     // (pipelined device batches of 16-bit PCM): part 0 = 60 % of every
     // track's blocks now, part 1 after the next batch's LPC kernel
     // (batch_end), so no chain runs beside an LPC grid; otherwise the whole
@@ -851,7 +868,7 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                            ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
                             (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
     // (md5_early: after the chunk's upload and this batch's track tables --
-    // ev_tables is recorded on the main stream behind both)
+    // ev_tables is recorded behind both)
     HIP_TRY(hipStreamWaitEvent(sl.s_aux, (md5_early || sl.md5_host) ? sl.ev_tables : ev[1], 0));
     HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
     if (!pl.frames_only) {
@@ -1796,6 +1813,7 @@ atg_status atg_flac_encode_frames_batch(atg_engine *e, const atg_flac_options *o
     HIP_TRY(hipStreamWaitEvent(e->s_main, h.ev_packed, 0));
     if (in_bytes)
         HIP_TRY(hipMemcpyAsync(h.d_pcm.p, pcm, in_bytes, hipMemcpyHostToDevice, e->s_main));
+    HIP_TRY(hipEventRecord(h.ev_h2d, e->s_main)); // the batch's LPC kernel waits for it
     // a synchronous call (no slot busy, checked above) always takes slot 0:
     // one aux stream for a streaming process's whole life.  The slot's
     // earlier results are gone with it (atgpu.h)
@@ -1805,7 +1823,7 @@ atg_status atg_flac_encode_frames_batch(atg_engine *e, const atg_flac_options *o
     st = take_slot(e, sl, ticket);
     if (st == ATG_OK)
         st = enqueue_batch(e, *sl, pl, h.d_pcm.p, (int)format, (uint8_t *)h.d_img.p,
-                           h.d_img.cap, true, nullptr, false);
+                           h.d_img.cap, true, h.ev_h2d, false);
     if (st != ATG_OK) {
         (void)hipDeviceSynchronize();
         if (sl) {

@@ -337,3 +337,21 @@ def test_loud_side_channel_split_fold(gpu_engine):
     for preset in ("8", "5"):
         check_batch(gpu_engine, [anti, noise, square, mix], 2, 16,
                     dict(oracle_port.PRESETS[preset]))
+
+
+def test_encode_frames_back_to_back_uploads(gpu_engine):
+    """atg_flac_encode_frames twice on one engine with the same geometry and
+    different PCM (4 MiB each): the second call's frames equal the port's
+    for ITS PCM.  The upload and the LPC kernel sit on different streams
+    (engine.hip: K1 on the slot stream), so an LPC kernel not ordered after
+    the upload would analyse the first call's samples still in the device
+    buffer"""
+    from audiotools import _atgpu
+    opts = dict(oracle_port.PRESETS["8"])
+    n = 4096 * 256
+    for k, seed in enumerate((5, 6, 7)):
+        x = signals.make("tone" if k % 2 else "noise", n, 2, 16, seed=seed).astype(np.int16)
+        got, sizes = gpu_engine.encode_frames(_atgpu.make_options(**opts), x, 2, 16, 44100)
+        want = oracle_port.split_flac(oracle_port.encode(x.astype(np.int32), 2, 16, 44100,
+                                                         **opts)[0])[1]
+        assert bytes(got) == want, "call %d" % k
