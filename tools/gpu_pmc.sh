@@ -4,7 +4,7 @@
 # kernel-trace only alongside the counters.
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
-OUT="$R/gpurun_out/pmc"
+OUT="$R/gpurun_out/${1:-pmc}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 ARGS="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host --no-chain --no-t2t --no-rg4"
