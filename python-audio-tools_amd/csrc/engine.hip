@@ -290,6 +290,10 @@ struct atg_engine {
     std::map<uint32_t, uint32_t> win_off;
     std::vector<double> win_host;
     size_t win_uploaded = 0;
+    // recorded after the last window upload (on the uploading batch's slot
+    // stream): every later batch's LPC kernel, on whichever slot stream,
+    // waits for it
+    hipEvent_t ev_win = nullptr;
     float times[kNumTimed] = {};
     bool have_times = false;
     uint64_t next_ticket = 1;
@@ -528,11 +532,21 @@ atg_status prepare_windows(atg_engine *e, Plan &pl, hipStream_t s)
         f.win_off = it->second;
     }
     if (e->win_host.size() != e->win_uploaded) {
-        HIP_TRY(e->windows.ensure(e->win_host.size() * sizeof(double) + 64));
+        const size_t need = e->win_host.size() * sizeof(double) + 64;
+        // a larger table replaces the buffer: earlier batches' LPC kernels
+        // (other slot streams) may still read the old one
+        if (need > e->windows.cap && e->windows.p)
+            HIP_TRY(hipDeviceSynchronize());
+        HIP_TRY(e->windows.ensure(need));
         HIP_TRY(hipMemcpyAsync(e->windows.p, e->win_host.data(),
                                e->win_host.size() * sizeof(double), hipMemcpyHostToDevice,
                                s));
         e->win_uploaded = e->win_host.size();
+        if (!e->ev_win)
+            HIP_TRY(hipEventCreateWithFlags(&e->ev_win, hipEventDisableTiming));
+        HIP_TRY(hipEventRecord(e->ev_win, s));
+    } else if (e->ev_win) {
+        HIP_TRY(hipStreamWaitEvent(s, e->ev_win, 0));
     }
     return ATG_OK;
 }
@@ -1488,6 +1502,8 @@ void atg_engine_destroy(atg_engine *e)
         if (q)
             (void)hipStreamDestroy(q);
     e->windows.release();
+    if (e->ev_win)
+        (void)hipEventDestroy(e->ev_win);
     (void)hipStreamDestroy(e->s_main);
     delete e;
 }

@@ -120,3 +120,27 @@ def test_fourth_enqueue_refused_results_survive(gpu_engine):
         _check(eng, torch, outs[k], eng.wait(t), per, "ticket %d" % k)
     with pytest.raises(_atgpu.ATGError):   # waited twice after its slot was reused
         eng.wait(ts[0])
+
+
+def test_async_batches_new_frame_lengths_fresh_engine():
+    """a fresh engine (empty window table), three batches enqueued back to
+    back whose tracks end in frame lengths no earlier batch had: every
+    batch uploads new Tukey windows on its own slot stream, and the table
+    grows (the buffer is replaced) while earlier LPC kernels may still run
+    (engine.hip prepare_windows, ev_win).  Each image equals the port's"""
+    import torch
+    from audiotools import _atgpu
+    eng = _atgpu.Engine(0)
+    opts = _atgpu.make_options(**FLAC8)
+    shapes = [[(0, 4096 * 2 + 1000 + 37 * k + 100 * b) for k in range(6)] for b in range(3)]
+    batches = [_batch(300 + i, s) for i, s in enumerate(shapes)]
+    dev = []
+    for pcm, tracks, per in batches:
+        _, cap = eng.bounds(opts, tracks, 2, 16)
+        dev.append((_dev(torch, pcm), torch.empty(cap, dtype=torch.uint8, device="cuda"), cap))
+    torch.cuda.synchronize()
+    tickets = [eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, tracks, 2, 16,
+                                       44100, d_out.data_ptr(), cap)
+               for (d_pcm, d_out, cap), (_, tracks, _) in zip(dev, batches)]
+    for i, t in enumerate(tickets):
+        _check(eng, torch, dev[i][1], eng.wait(t), batches[i][2], "fresh-engine batch %d" % i)
