@@ -86,7 +86,8 @@ const char *kTimedNames[kNumTimed] = {"lpc_analyze", "subframe_search", "frame_d
 
 // CRC-16 (0x8005) slicing tables t16[k][b] = CRC of byte b followed by k
 // zero bytes, the CRC-8 table, and "advance by 2^m zero bytes" matrices
-void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16])
+void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16],
+                      uint16_t advq[kCrcQ][6][16])
 {
     for (uint32_t b = 0; b < 256; ++b) {
         uint32_t c = b << 8, c8 = b;
@@ -118,6 +119,23 @@ void build_crc_tables(uint32_t t16[4][256], uint32_t *t8, uint16_t adv[24][16])
             adv[m][i] = (uint16_t)r;
         }
     }
+    // advq[q - 1][s]: 4 q 2^s zero bytes = (4 bytes)^q, squared s times
+    auto apply = [](const uint16_t *a, uint32_t v) {
+        uint32_t r = 0;
+        for (int j = 0; j < 16; ++j)
+            if ((v >> j) & 1u)
+                r ^= a[j];
+        return (uint16_t)r;
+    };
+    for (int i = 0; i < 16; ++i)
+        advq[0][0][i] = adv[2][i];
+    for (int q = 1; q < kCrcQ; ++q)
+        for (int i = 0; i < 16; ++i)
+            advq[q][0][i] = apply(adv[2], advq[q - 1][0][i]);
+    for (int q = 0; q < kCrcQ; ++q)
+        for (int s = 1; s < 6; ++s)
+            for (int i = 0; i < 16; ++i)
+                advq[q][s][i] = apply(advq[q][s - 1], advq[q][s - 1][i]);
 }
 
 } // namespace
@@ -1443,9 +1461,9 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
         HIP_TRY(hipEventCreateWithFlags(&h.ev_d2h, hipEventDisableTiming));
     }
     static uint32_t t16[4][256], t8[256];
-    static uint16_t adv[24][16];
-    build_crc_tables(t16, t8, adv);
-    HIP_TRY(upload_crc_tables(&adv[0][0], &t16[0][0], t8));
+    static uint16_t adv[24][16], advq[kCrcQ][6][16];
+    build_crc_tables(t16, t8, adv, advq);
+    HIP_TRY(upload_crc_tables(&adv[0][0], &t16[0][0], t8, &advq[0][0][0]));
     *out = e;
     return ATG_OK;
 }

@@ -28,14 +28,18 @@
 __constant__ uint16_t c_crc_adv[24][16]; // advance CRC-16 state by 2^m zero bytes
 __constant__ uint32_t c_crc16[4][256]; // slicing tables: byte + k zero bytes
 __constant__ uint32_t c_crc8[256];
+__constant__ uint16_t c_crc_advq[kCrcQ][6][16]; // advance by 4q * 2^s zero bytes (q - 1, s)
 
 #define VENDOR "Python Audio Tools 2.22alpha1"
 #define VENDOR_LEN 29
 
 hipError_t upload_crc_tables(const uint16_t *adv, const uint32_t *crc16_tab,
-                             const uint32_t *crc8_tab)
+                             const uint32_t *crc8_tab, const uint16_t *advq)
 {
     hipError_t e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_adv), adv, sizeof(uint16_t) * 24 * 16);
+    if (e != hipSuccess)
+        return e;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc_advq), advq, sizeof(uint16_t) * kCrcQ * 6 * 16);
     if (e != hipSuccess)
         return e;
     e = hipMemcpyToSymbol(HIP_SYMBOL(c_crc16), crc16_tab, sizeof(uint32_t) * 1024);
@@ -323,6 +327,16 @@ __device__ __forceinline__ uint32_t crc_adv(uint32_t c, int m)
 #pragma unroll
     for (int i = 0; i < 16; ++i)
         r ^= ((c >> i) & 1u) ? (uint32_t)c_crc_adv[m][i] : 0u;
+    return r;
+}
+
+// the same by 4 (q + 1) 2^s zero bytes
+__device__ __forceinline__ uint32_t crc_advq(uint32_t c, uint32_t q, int s)
+{
+    uint32_t r = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+        r ^= ((c >> i) & 1u) ? (uint32_t)c_crc_advq[q][s][i] : 0u;
     return r;
 }
 
@@ -616,16 +630,20 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))
     }
     __syncthreads();
 
-    // CRC-16 of bytes [0, L): 64 chunks of Lc = 2^m >= 4 bytes over a
-    // virtually zero-prefixed image (leading zeros leave a zero-init CRC
-    // unchanged), 4 bytes per step with slicing tables, tree-combined with
-    // the "advance by 2^m zero bytes" matrices.
+    // CRC-16 of bytes [0, L): 64 chunks of Lc bytes over a virtually
+    // zero-prefixed image (leading zeros leave a zero-init CRC unchanged),
+    // 4 bytes per step with slicing tables, tree-combined with "advance by
+    // Lc 2^s zero bytes" matrices.  Lc = 4 ceil(L / 256) for frames up to
+    // 256 kCrcQ bytes (fewer than 256 prefix bytes: every lane has work),
+    // else the power of two 2^m >= L / 64
     const uint32_t L = fd.bytes - 2u;
+    const uint32_t cq = (L + 255u) >> 8;
+    const bool qlen = cq >= 1u && cq <= (uint32_t)kCrcQ;
     uint32_t lc_log = 2;
     while ((64u << lc_log) < L)
         lc_log++;
-    const uint32_t Lc = 1u << lc_log;
-    const int z = (int)(64u << lc_log) - (int)L;
+    const uint32_t Lc = qlen ? 4u * cq : 1u << lc_log;
+    const int z = (int)(64u * Lc) - (int)L;
     uint32_t crc = 0;
     {
         int q = lane * (int)Lc - z; // image byte of this lane's first group
@@ -653,7 +671,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))
     for (int s = 0; s < 6; ++s) {
         const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << s, 64);
         if ((lane & ((2 << s) - 1)) == 0)
-            crc = crc_adv(crc, (int)lc_log + s) ^ other;
+            crc = (qlen ? crc_advq(crc, cq - 1u, s) : crc_adv(crc, (int)lc_log + s)) ^ other;
     }
     if (lane == 0)
         put_bits(fb, 8u * L, 16, crc);

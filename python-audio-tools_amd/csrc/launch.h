@@ -69,9 +69,13 @@ hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
 // host pipeline: track images from their slots to dst + dst_off[t]
 hipError_t launch_pack_images(const uint8_t *img, const TrackInfo *tracks, const TrackOut *tout,
                               const uint64_t *dst_off, uint32_t n, uint8_t *dst, hipStream_t s);
+// CRC-16 chunk lengths 4q bytes (q = 1..kCrcQ) for frames up to 256 kCrcQ
+// bytes: every lane of the pack kernel's CRC pass gets ceil(L / 256) words
+constexpr int kCrcQ = 64;
 hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
                              const uint32_t *crc16_tab /*[4][256] slicing tables*/,
-                             const uint32_t *crc8_tab /*[256]*/);
+                             const uint32_t *crc8_tab /*[256]*/,
+                             const uint16_t *advq /*[kCrcQ][6][16]: advance by 4q 2^s bytes*/);
 // md5.hip
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                             const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s);
