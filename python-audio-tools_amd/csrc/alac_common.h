@@ -106,31 +106,159 @@ struct ABitR {
     }
 };
 
-// read_residual (decoders/alac.c:1087-1120)
-__device__ __forceinline__ uint32_t alac_read_residual(ABitR &r, uint32_t k, uint32_t ss)
+// The same reader for long sequential walks (residual blocks, frameset
+// parses): the words under pos come from two 16-byte chunks held in
+// registers (cur = chunk pos >> 7, nxt = the one after).  Entering the next
+// chunk moves nxt to cur and issues the loads of the chunk after it, so a
+// chunk's loads are in flight for the ~128 bits (several codes) before they
+// are used -- ABitR waits for two dependent loads per code.  Loads are four
+// dword loads (no alignment assumed) clamped to the last readable word
+// (one whole word past `end`, as ABitR reads).
+struct ABitRC {
+    const uint32_t *w;
+    uint64_t pos, end; // bit positions
+    bool eof;
+    uint64_t c, lim;   // chunk held in c0..c3; last readable word
+    // (plain words, not a vector type: a dynamically indexed uint4 sends
+    // the reader to LDS or scratch and every load is waited at once)
+    uint32_t c0, c1, c2, c3, n0, n1, n2, n3;
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const { return w[i < lim ? i : lim]; }
+    __device__ __forceinline__ void load_next(uint64_t ch)
+    {
+        const uint64_t i = ch * 4u;
+        n0 = ld(i);
+        n1 = ld(i + 1);
+        n2 = ld(i + 2);
+        n3 = ld(i + 3);
+    }
+    __device__ __forceinline__ void init(const uint32_t *words, uint64_t bit0, uint64_t bit_end)
+    {
+        w = words;
+        pos = bit0;
+        end = bit_end;
+        eof = false;
+        lim = (bit_end >> 5) + 1u;
+        c = bit0 >> 7;
+        load_next(c);
+        c0 = n0;
+        c1 = n1;
+        c2 = n2;
+        c3 = n3;
+        load_next(c + 1u);
+    }
+    __device__ __forceinline__ uint32_t peek32()
+    {
+        const uint64_t pc = pos >> 7;
+        if (pc != c) {
+            if (pc != c + 1u) // a skip past the next chunk
+                load_next(pc);
+            c0 = n0;
+            c1 = n1;
+            c2 = n2;
+            c3 = n3;
+            load_next(pc + 1u);
+            c = pc;
+        }
+        // word k and k + 1 of the eight by bit masks, not selects: a select
+        // of two struct fields becomes a load through a selected address,
+        // and the reader then lives in memory
+        const uint32_t k = (uint32_t)(pos >> 5) & 3u;
+        uint32_t m0 = 0u - (uint32_t)(k == 0u), m1 = 0u - (uint32_t)(k == 1u);
+        uint32_t m2 = 0u - (uint32_t)(k == 2u), m3 = 0u - (uint32_t)(k == 3u);
+        asm volatile("" : "+v"(m0), "+v"(m1), "+v"(m2), "+v"(m3));
+        const uint32_t a = (c0 & m0) | (c1 & m1) | (c2 & m2) | (c3 & m3);
+        const uint32_t b = (c1 & m0) | (c2 & m1) | (c3 & m2) | (n0 & m3);
+        const uint32_t sh = (uint32_t)(pos & 31u);
+        const uint32_t ha = __builtin_bswap32(a), hb = __builtin_bswap32(b);
+        return sh ? (ha << sh) | (hb >> (32u - sh)) : ha;
+    }
+    __device__ __forceinline__ uint32_t get(uint32_t n) // n <= 32
+    {
+        if (!n)
+            return 0;
+        if (pos + n > end) {
+            eof = true;
+            pos = end;
+            return 0;
+        }
+        const uint32_t v = peek32() >> (32u - n);
+        pos += n;
+        return v;
+    }
+    __device__ __forceinline__ int32_t get_signed(uint32_t n)
+    {
+        const uint32_t v = get(n);
+        if (n == 0 || n >= 32)
+            return (int32_t)v;
+        return (v & (1u << (n - 1))) ? (int32_t)(v - (1u << n)) : (int32_t)v;
+    }
+    __device__ __forceinline__ int32_t unary9()
+    {
+        const uint64_t avail = end > pos ? end - pos : 0;
+        const uint32_t x = peek32();
+        uint32_t ones = (uint32_t)__clz(~x);
+        if (ones >= 9) {
+            if (avail < 9) {
+                eof = true;
+                pos = end;
+                return 0;
+            }
+            pos += 9;
+            return -1;
+        }
+        if (avail < ones + 1u) {
+            eof = true;
+            pos = end;
+            return 0;
+        }
+        pos += ones + 1u;
+        return (int32_t)ones;
+    }
+};
+
+// read_residual (decoders/alac.c:1087-1120): read_limited_unary(0, 9),
+// then k bits of which an LSB field of 0 or 1 gives one back.  One peek
+// covers both fields when they fit in 32 bits (ones <= 8 and k <= 23), with
+// the reference's EOF order: the unary bits first, then all k bits
+template <class R>
+__device__ __forceinline__ uint32_t alac_read_residual(R &r, uint32_t k, uint32_t ss)
 {
-    const int32_t msb = r.unary9();
-    if (r.eof)
-        return 0;
-    if (msb < 0)
+    const uint64_t avail = r.end > r.pos ? r.end - r.pos : 0;
+    const uint32_t x = r.peek32();
+    const uint32_t ones = (uint32_t)__clz(~x); // leading ones (32 if all ones)
+    if (ones >= 9u) { // escape: a raw ss-bit value
+        if (avail < 9u) {
+            r.eof = true;
+            r.pos = r.end;
+            return 0;
+        }
+        r.pos += 9;
         return r.get(ss);
-    if (k == 0)
-        return (uint32_t)msb;
-    const uint32_t m = (1u << k) - 1u;
-    // read k bits; an LSB field of 0 or 1 gives one bit back (unread)
-    if (r.pos + k > r.end) {
-        // the reference reads k bits first: EOF if they are not all there
+    }
+    if (avail < ones + 1u || (k && avail < ones + 1u + k)) {
         r.eof = true;
         r.pos = r.end;
         return 0;
     }
-    const uint32_t lsb = r.peek32() >> (32u - k);
-    if (lsb > 1u) {
-        r.pos += k;
-        return (uint32_t)msb * m + (lsb - 1u);
+    if (k == 0) {
+        r.pos += ones + 1u;
+        return ones;
     }
-    r.pos += k - 1u;
-    return (uint32_t)msb * m;
+    const uint32_t m = (1u << k) - 1u;
+    uint32_t lsb;
+    if (ones + 1u + k <= 32u) {
+        lsb = (x << (ones + 1u)) >> (32u - k);
+    } else {
+        r.pos += ones + 1u;
+        lsb = r.peek32() >> (32u - k);
+        r.pos -= ones + 1u;
+    }
+    if (lsb > 1u) {
+        r.pos += ones + 1u + k;
+        return ones * m + (lsb - 1u);
+    }
+    r.pos += ones + k; // ones + 1 + (k - 1)
+    return ones * m;
 }
 
 // the decoder's LOG2 (decoders/alac.c:1006-1015): -1 for 0
@@ -160,7 +288,8 @@ struct AResidualReader {
         run_left = 0;
     }
     // next residual; false at the end or on EOF (r.eof)
-    __device__ __forceinline__ bool next(ABitR &r, int32_t &out)
+    template <class R>
+    __device__ __forceinline__ bool next(R &r, int32_t &out)
     {
         if (run_left) { // zeros of a zero block (the reference appends them
             --run_left; // inside the same loop iteration)

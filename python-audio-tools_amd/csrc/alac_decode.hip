@@ -88,7 +88,7 @@ struct ACount {
 // one frameset at absolute byte `start` (read_frame x elements, alac.c:204-233)
 __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AFs &F)
 {
-    ABitR r;
+    ABitRC r;
     const uint64_t b0 = start * 8;
     r.init(w, b0, T.end * 8);
     F.start = start;
@@ -266,8 +266,8 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
 
 // decode_subframe (alac.c:1147-1235) for one channel, ORDER coefficients in
 // registers; out[i] for i < n
-template <int ORDER>
-__device__ void restore_fixed(ABitR &r, AResidualReader &g, const int32_t *coef_in,
+template <int ORDER, class R>
+__device__ __forceinline__ void restore_fixed(R &r, AResidualReader &g, const int32_t *coef_in,
                               uint32_t qshift, uint32_t ss, uint32_t n, int32_t *out)
 {
     int32_t c[ORDER], h[ORDER + 1]; // h[0] newest
@@ -319,7 +319,8 @@ __device__ void restore_fixed(ABitR &r, AResidualReader &g, const int32_t *coef_
 }
 
 // any other order (the encoder writes only 4 and 8): history in the output
-__device__ void restore_generic(ABitR &r, AResidualReader &g, int32_t *c, uint32_t order,
+template <class R>
+__device__ __forceinline__ void restore_generic(R &r, AResidualReader &g, int32_t *c, uint32_t order,
                                 uint32_t qshift, uint32_t ss, uint32_t n, int32_t *out)
 {
     if (order >= 31) { // the reference's verbatim branch advances i twice
@@ -421,21 +422,22 @@ __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict_
     for (uint32_t k = 0; k < order; ++k)
         coef[k] = r.get_signed(16);
     const uint32_t ss = T.bps - E.lsbs * 8u + (E.cc - 1u);
-    r.init(w, b0 + E.res_bit[c], T.end * 8);
+    ABitRC rc;
+    rc.init(w, b0 + E.res_bit[c], T.end * 8);
     AResidualReader g;
     g.init(E.N, ss, T.ih, T.hm, T.mk);
     const uint32_t n = E.nres[c];
     if (order == 4 && qshift >= 1) {
         int32_t c4[4] = {coef[0], coef[1], coef[2], coef[3]};
-        restore_fixed<4>(r, g, c4, qshift, ss, n, out);
+        restore_fixed<4>(rc, g, c4, qshift, ss, n, out);
     } else if (order == 8 && qshift >= 1) {
         int32_t c8[8];
 #pragma unroll
         for (int k = 0; k < 8; ++k)
             c8[k] = coef[k];
-        restore_fixed<8>(r, g, c8, qshift, ss, n, out);
+        restore_fixed<8>(rc, g, c8, qshift, ss, n, out);
     } else {
-        restore_generic(r, g, coef, order, qshift, ss, n, out);
+        restore_generic(rc, g, coef, order, qshift, ss, n, out);
     }
 }
 
