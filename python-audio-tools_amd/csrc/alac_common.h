@@ -126,10 +126,21 @@ struct ABitRC {
     __device__ __forceinline__ void load_next(uint64_t ch)
     {
         const uint64_t i = ch * 4u;
-        n0 = ld(i);
-        n1 = ld(i + 1);
-        n2 = ld(i + 2);
-        n3 = ld(i + 3);
+        if (i + 3u <= lim && (((uintptr_t)w & 15u) == 0u)) {
+            // one 16-byte load: the lanes read 64 different streams, so
+            // every vector load touches up to 64 cache lines -- four dword
+            // loads cost four times the address work of one dwordx4
+            const uint4 v = *(const uint4 *)(w + i);
+            n0 = v.x;
+            n1 = v.y;
+            n2 = v.z;
+            n3 = v.w;
+        } else {
+            n0 = ld(i);
+            n1 = ld(i + 1);
+            n2 = ld(i + 2);
+            n3 = ld(i + 3);
+        }
     }
     __device__ __forceinline__ void init(const uint32_t *words, uint64_t bit0, uint64_t bit_end)
     {
