@@ -32,6 +32,9 @@
 // 2) + 1 v_dot2 + 4 VALU per residual, wasted bits included for free.
 // v = |r| - [r < 0] is kept per sample (u >> k = v >> (k - 1) for the
 // zig-zag code u = 2v + [r < 0], k >= 1); #neg = 64 + sum (n >> 31).
+// With ATG_K2F_BIAS (the default) the seed also carries + 2^31: a logical
+// shift gives x = n + 2^(31 - sh - w), sum |r| is one v_sad_u32 per sample
+// (2 VALU per residual after the v_dot2s), and x is kept instead of v.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -130,6 +133,23 @@ __device__ __forceinline__ void add3_acc(uint32_t &sa, uint32_t v, uint32_t s31)
     asm("v_add3_u32 %0, %0, %1, %2" : "+v"(sa) : "v"(v), "v"(s31));
 }
 
+// Pass-1 post-processing with a biased accumulator (ATG_K2F_BIAS 1): the
+// fold's seed carries + 2^31, so x = acc >>> shv (a full-rate logical
+// shift) is n + B with n = ~r and B = 2^(31 - shv) (acc + 2^31 is the true
+// int32 sum offset into [0, 2^32), and 2^31 is a multiple of 2^shv); the
+// run's sum |r| = sum |x - (B - 1)| is one v_sad_u32 per sample.  Two VALU
+// per residual instead of four; pass 2 recovers n = x - B.  The split and
+// hi/lo folds keep their arithmetic n and store x = n ^ 2^31 (B = 2^31).
+// A/B (profiles/r04_af_k2_bias_ab.jsonl): K2 6.75 -> 6.65 ms live, 7.52 ->
+// 7.63 M frames/s; 0 selects the previous four-VALU form.
+#ifndef ATG_K2F_BIAS
+#define ATG_K2F_BIAS 1
+#endif
+__device__ __forceinline__ void sad_acc(uint32_t &sa, uint32_t x, uint32_t b)
+{
+    asm("v_sad_u32 %0, %1, %2, %0" : "+v"(sa) : "v"(x), "v"(b));
+}
+
 // packed int16 L - R per half word (v_pk_sub_u16): the side channel's
 // packed words, exact when every |L - R| fits int16
 __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b)
@@ -203,6 +223,9 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap pair in a VGPR
+#if ATG_K2F_BIAS
+    const uint32_t bm1 = (0x80000000u >> shv) - 1u; // B - 1
+#endif
     Win A;
     win_init(run, A, subr);
     // chunk c + 1's words are read while chunk c is computed
@@ -234,6 +257,13 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 16 * c + ii + h;
+#if ATG_K2F_BIAS
+                uint32_t x = (uint32_t)acc[h] >> shv;
+                if (i < ATG_FAST_ORDER)
+                    x = (lane0 && i < order) ? bm1 : x;
+                u[i] = x;
+                sad_acc(sa, x, bm1);
+#else
                 int n = acc[h] >> shv;
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
@@ -241,10 +271,11 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
                 add3_acc(sa, v, s31);
+#endif
             }
         }
     }
-    sabs = sa + (uint32_t)ATG_RUN;
+    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
 }
 
 // The same for the side channel S = L - R (17 bits): tap k of sample t is
@@ -273,6 +304,9 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
     const uint32_t *__restrict__ runR = run + PK_WORDS;
     int tap0 = cl[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap in a VGPR
+#if ATG_K2F_BIAS
+    const uint32_t bm1 = (0x80000000u >> shv) - 1u; // B - 1
+#endif
     uint32_t W[20]; // (L, R) words of samples t0 - 12 .. t0 + 7 of the current chunk
     {
         // packed words -8..-1 = samples a-16 .. a-1; keep a-12 .. a-1
@@ -314,6 +348,13 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 8 * c + ii + h;
+#if ATG_K2F_BIAS
+                uint32_t x = (uint32_t)accs[h] >> shv;
+                if (i < ATG_FAST_ORDER)
+                    x = (lane0 && i < order) ? bm1 : x;
+                u[i] = x;
+                sad_acc(sa, x, bm1);
+#else
                 int n = accs[h] >> shv;
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
@@ -321,10 +362,11 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
                 add3_acc(sa, v, s31);
+#endif
             }
         }
     }
-    sabs = sa + (uint32_t)ATG_RUN;
+    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
 }
 
 // A lower bound on the Rice-coded bits of the wave's residuals under any
@@ -360,7 +402,8 @@ struct Eval16 {
 };
 
 __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
-                                            const RunCtx &c, int order, int warm, uint32_t thr);
+                                            const RunCtx &c, int order, int warm, uint32_t thr,
+                                            uint32_t bias);
 
 // One predictor with the folded 32-bit arithmetic (caller checked the
 // bounds): pass 1, partition search, exact bits.  run: the lane's run in a
@@ -398,7 +441,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         for (int j = 7; j < 14; ++j)
             cq[j] = 0;
     }
-    const int c0acc = -(1 << (sh + (int)w));
+    const int c0acc = ATG_K2F_BIAS ? (int)(0x80000000u - (1u << (sh + (int)w))) : -(1 << (sh + (int)w));
     int shv = sh + (int)w;
     asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
     // lane 0's first `order` samples are warm-up: (lane0 && i < order) is a
@@ -459,7 +502,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         }
 #endif
     }
-    return eval_tail(lane_sum, u, c, order, warm, thr);
+    return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u >> shv);
 }
 
 // ---- split fold: the 32-bit fold for predictors whose worst-case sum
@@ -498,6 +541,10 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+#if ATG_K2F_BIAS
+    uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
+    asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
+#endif
     Win A, B;
     {
         const uint4 h0 = load_run4(run - 12, subr), h1 = load_run4(run - 8, subr);
@@ -548,14 +595,20 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
+#if ATG_K2F_BIAS
+                const uint32_t x = (uint32_t)n ^ 0x80000000u;
+                u[i] = x;
+                sad_acc(sa, x, bm1);
+#else
                 const uint32_t s31 = (uint32_t)(n >> 31);
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
                 add3_acc(sa, v, s31);
+#endif
             }
         }
     }
-    sabs = sa + (uint32_t)ATG_RUN;
+    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
 }
 
 // the side channel on (L, R) words, split: TAPS = min(2D, 13) as pass1_lr
@@ -569,6 +622,10 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
     const uint32_t *__restrict__ runR = run + PK_WORDS;
     int tap0 = cl[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+#if ATG_K2F_BIAS
+    uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
+    asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
+#endif
     uint32_t WH[20], WL[20];
     {
         uint32_t h[16];
@@ -628,14 +685,20 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
+#if ATG_K2F_BIAS
+                const uint32_t x = (uint32_t)n ^ 0x80000000u;
+                u[i] = x;
+                sad_acc(sa, x, bm1);
+#else
                 const uint32_t s31 = (uint32_t)(n >> 31);
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
                 add3_acc(sa, v, s31);
+#endif
             }
         }
     }
-    sabs = sa + (uint32_t)ATG_RUN;
+    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
 }
 
 template <bool BIG>
@@ -723,13 +786,14 @@ __device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, c
     else
         pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
                                TWO, dbl);
-    return eval_tail(lane_sum, u, c, order, warm, thr);
+    return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u);
 }
 
 // After pass 1 (every predictor form): the lower-bound pruning, the
 // partition search and the exact bit count from the kept v = |r| - [r < 0]
 __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
-                                            const RunCtx &c, int order, int warm, uint32_t thr)
+                                            const RunCtx &c, int order, int warm, uint32_t thr,
+                                            uint32_t bias)
 {
     Eval16 ev;
     if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
@@ -758,9 +822,19 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
 #if ATG_K2F_EXP == 2
     sh2 = u[kv & 63];
 #else
+#if ATG_K2F_BIAS
+    // v >> kv = (n >> kv) ^ (n >> 31) for n = x - B (arithmetic shifts)
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; t += 2) {
+        const int n0 = (int)(u[t] - bias), n1 = (int)(u[t + 1] - bias);
+        sh2 = sh2 + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
+    }
+#else
+    (void)bias;
 #pragma unroll
     for (int t = 0; t < ATG_RUN; t += 2)
         sh2 = sh2 + (u[t] >> kv) + (u[t + 1] >> kv); // v_add3_u32
+#endif
 #endif
     // k = 0: sum u = 2 sum v + #neg = sum v + sum |r| (sh2 = sum v)
     const uint32_t lb = cnt * (1u + k) + (k ? sh2 : sh2 + lane_sum);
@@ -1575,6 +1649,10 @@ __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
+#if ATG_K2F_BIAS
+    uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
+    asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
+#endif
     Win A, B;
     win_init(run, A, false);
     win_init(run + PK_WORDS, B, false);
@@ -1614,14 +1692,20 @@ __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const
                 int n = BIG ? (ah[h] + (al[h] >> 12)) >> sa_v : (ah[h] << sa_v) + (al[h] >> sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
+#if ATG_K2F_BIAS
+                const uint32_t x = (uint32_t)n ^ 0x80000000u;
+                u[i] = x;
+                sad_acc(sa, x, bm1);
+#else
                 const uint32_t s31 = (uint32_t)(n >> 31);
                 const uint32_t v = (uint32_t)n ^ s31;
                 u[i] = v;
                 add3_acc(sa, v, s31);
+#endif
             }
         }
     }
-    sabs = sa + (uint32_t)ATG_RUN;
+    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
 }
 
 template <bool BIG>
@@ -1669,7 +1753,7 @@ __device__ __forceinline__ Eval16 eval_fold_hl(const uint32_t *__restrict__ run,
         pass1_hl_any<true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
     else
         pass1_hl_any<false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
-    return eval_tail(lane_sum, u, c, order, warm, thr);
+    return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u);
 }
 
 // FIXED order (flac.c:856-916) on the hi/lo images: differences in int32
