@@ -429,11 +429,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))
         // where used (one v_dot2 + one shift) instead of held in 80 VGPRs
         const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
                            : cand == 2u ? 0x00010001u : 0xFFFF0001u;
-        const int xsh = (cand == 2u ? 1 : 0) + (int)w;
-        auto xs = [&](int i) -> int {
-            return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, pr[i]),
-                                          __builtin_bit_cast(short2_t, wts), 0, false) >> xsh;
-        };
+        int xsh = (cand == 2u ? 1 : 0) + (int)w;
+#if ATG_K5_VOP3
+        // the shift in a VGPR (a shift by an SGPR operand issues at half rate)
+        asm volatile("v_mov_b32 %0, %0" : "+v"(xsh));
+#endif
+        auto xs = [&](int i) -> int { return dot2_z(pr[i], (int)wts) >> xsh; };
         if (!REG)
             stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,
                                 [&](uint32_t i, int32_t s) { sl[saddr((int)i)] = s >> w; });

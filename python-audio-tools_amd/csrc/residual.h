@@ -32,6 +32,25 @@ __device__ __forceinline__ uint32_t iabs_u(int32_t r)
 
 typedef short short2_t __attribute__((ext_vector_type(2)));
 
+// First v_dot2 of a sum that starts at 0: the VOP3 form with the inline
+// constant 0 as the accumulator, so no v_mov seeds it (the compiler's
+// v_dot2c form accumulates into its destination and copies a zero in
+// first).  b is wave-uniform (an SGPR operand).
+#ifndef ATG_K5_VOP3
+#define ATG_K5_VOP3 1
+#endif
+__device__ __forceinline__ int dot2_z(uint32_t a, int b_uniform)
+{
+#if ATG_K5_VOP3
+    int d;
+    asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "s"(b_uniform));
+    return d;
+#else
+    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a),
+                                  __builtin_bit_cast(short2_t, b_uniform), 0, false);
+#endif
+}
+
 // Residuals of samples [a, a+len) (len <= 64) with a 12-tap predictor whose
 // taps >= order are 0, exact in 32 bits (caller checks sum|c| * max|s| <
 // 2^31).  cf[] must be wave-uniform.  Two kernels of arithmetic:
@@ -319,8 +338,9 @@ __device__ __forceinline__ void lane_residuals_regs(X &&xs, const int (&cf)[ATG_
         const int s = xs(16 + t);
         int acc = 0;
         if (DOT2) {
+            acc = dot2_z((uint32_t)qw[0], cp[0]);
 #pragma unroll
-            for (int j = 0; j < W / 2; ++j) {
+            for (int j = 1; j < W / 2; ++j) {
                 short2_t av = __builtin_bit_cast(short2_t, qw[2 * j]);
                 short2_t bv = __builtin_bit_cast(short2_t, cp[j]);
                 acc = __builtin_amdgcn_sdot2(av, bv, acc, false);
