@@ -206,6 +206,11 @@ struct EncSlot {
 #ifndef ATG_K1_AUX
 #define ATG_K1_AUX 1
 #endif
+// K3-K5 of pipelined device batches on an engine-wide pack stream (section
+// 4a''' of DESIGN.md); 0 keeps them on the main stream
+#ifndef ATG_PACK_STREAM
+#define ATG_PACK_STREAM 1
+#endif
 #ifndef ATG_AUX_HIPRIO
 #define ATG_AUX_HIPRIO 1
 #endif
@@ -283,6 +288,10 @@ struct atg_engine {
     std::unique_ptr<HashPool> pool; // host-MD5 threads, created on first use
     bool sync_call = false; // inside atg_flac_encode_device (enqueue + wait)
     hipStream_t s_main = nullptr;
+    // pipelined device batches (atg_flac_encode_device_async): K3-K5 of
+    // batch k on their own stream, so batch k+1's search starts beside
+    // batch k's pack (ATG_PACK_STREAM; null: everything on s_main)
+    hipStream_t s_pack = nullptr;
     EncSlot slot[kEncSlots];
     DevBuf windows;
     // host-memory API (atg_flac_encode_host): per pipeline stage, device
@@ -945,29 +954,35 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                                        (const int8_t *)sl.shift.p, (const uint8_t *)sl.est.p,
                                        (SubDesc *)sl.sub.p, derr, e->s_main));
     HIP_TRY(hipEventRecord(ev[3], e->s_main));
-    HIP_TRY(hipEventRecord(ev[4], e->s_main));
+    // K3-K5: on the pack stream for pipelined device batches (each reads
+    // only its own slot's tables and writes its own output), else in order
+    // on the main stream.  Everything after them waits for ev_pack.
+    hipStream_t s_k5 = (e->s_pack && pipelined && !md5_early) ? e->s_pack : e->s_main;
+    if (s_k5 != e->s_main)
+        HIP_TRY(hipStreamWaitEvent(s_k5, ev[3], 0));
+    HIP_TRY(hipEventRecord(ev[4], s_k5));
     HIP_TRY(launch_frame_decide(p, dfr, (const SubDesc *)sl.sub.p, (FrameDesc *)sl.fdesc.p,
-                                e->s_main));
-    HIP_TRY(hipEventRecord(ev[5], e->s_main));
-    HIP_TRY(hipEventRecord(ev[6], e->s_main));
+                                s_k5));
+    HIP_TRY(hipEventRecord(ev[5], s_k5));
+    HIP_TRY(hipEventRecord(ev[6], s_k5));
     HIP_TRY(launch_track_scan(p, dtr, (const uint32_t *)sl.order.p, (FrameDesc *)sl.fdesc.p, dto,
-                              e->s_main));
-    HIP_TRY(hipEventRecord(ev[7], e->s_main));
-    HIP_TRY(hipEventRecord(ev[8], e->s_main));
+                              s_k5));
+    HIP_TRY(hipEventRecord(ev[7], s_k5));
+    HIP_TRY(hipEventRecord(ev[8], s_k5));
     if (pl.big) {
         // the large-frame packer ORs bits into a zeroed image
-        HIP_TRY(hipMemsetAsync(d_out, 0, pl.out_bytes, e->s_main));
+        HIP_TRY(hipMemsetAsync(d_out, 0, pl.out_bytes, s_k5));
         HIP_TRY(launch_frame_pack_big(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
                                       (const uint8_t *)sl.rice_big.p, rice_stride,
                                       (const FrameDesc *)sl.fdesc.p, d_out, derr,
                                       (uint8_t *)sl.scratch.p, big_slot_bytes(pl),
-                                      (uint32_t)std::min<uint64_t>(kBigGrid, nf), e->s_main));
+                                      (uint32_t)std::min<uint64_t>(kBigGrid, nf), s_k5));
     } else {
         HIP_TRY(launch_frame_pack(p, d_pcm, fmt, dfr, dtr, (const SubDesc *)sl.sub.p,
-                                  (const FrameDesc *)sl.fdesc.p, d_out, derr, e->s_main));
+                                  (const FrameDesc *)sl.fdesc.p, d_out, derr, s_k5));
     }
-    HIP_TRY(hipEventRecord(ev[9], e->s_main));
-    HIP_TRY(hipEventRecord(sl.ev_pack, e->s_main));
+    HIP_TRY(hipEventRecord(ev[9], s_k5));
+    HIP_TRY(hipEventRecord(sl.ev_pack, s_k5));
     sl.uploaded = &pl;
     sl.plan = plp;
     sl.end_status = ATG_OK;
@@ -1003,6 +1018,8 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
         if (st != ATG_OK) {
             sl.end_pending = false;
             (void)hipStreamSynchronize(e->s_main);
+            if (e->s_pack)
+                (void)hipStreamSynchronize(e->s_pack);
             (void)hipStreamSynchronize(sl.s_aux);
             return st;
         }
@@ -1015,6 +1032,8 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
     if (sl.end_status != ATG_OK) {
         // ev_done was never recorded: drain the slot's streams, report the error
         (void)hipStreamSynchronize(e->s_main);
+        if (e->s_pack)
+            (void)hipStreamSynchronize(e->s_pack);
         (void)hipStreamSynchronize(sl.s_aux);
         return fail(sl.end_status, sl.end_error);
     }
@@ -1447,6 +1466,10 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
                 return ATG_ERR_DEVICE;
         if (ensure_host_streams(e) != ATG_OK)
             return ATG_ERR_DEVICE;
+#if ATG_PACK_STREAM
+        // created last: the streams above keep their hardware queues
+        HIP_TRY(hipStreamCreateWithFlags(&e->s_pack, hipStreamNonBlocking));
+#endif
     }
     for (EncSlot &sl : e->slot) {
         for (auto &ev : sl.ev)
@@ -1474,6 +1497,8 @@ void atg_engine_destroy(atg_engine *e)
         return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->s_main);
+    if (e->s_pack)
+        (void)hipStreamSynchronize(e->s_pack);
     for (EncSlot &sl : e->slot) {
         for (std::future<void> &f : sl.hash_jobs) // a batch never waited
             f.wait();
@@ -1522,6 +1547,8 @@ void atg_engine_destroy(atg_engine *e)
     e->windows.release();
     if (e->ev_win)
         (void)hipEventDestroy(e->ev_win);
+    if (e->s_pack)
+        (void)hipStreamDestroy(e->s_pack);
     (void)hipStreamDestroy(e->s_main);
     delete e;
 }
@@ -1568,6 +1595,8 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
     if (st != ATG_OK) {
         // nothing of this batch may be relied on: drain what was queued
         (void)hipStreamSynchronize(e->s_main);
+        if (e->s_pack)
+            (void)hipStreamSynchronize(e->s_pack);
         (void)hipStreamSynchronize(sl->s_aux);
         sl->uploaded = nullptr;
         sl->ticket = 0;
