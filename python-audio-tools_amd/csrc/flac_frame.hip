@@ -340,14 +340,21 @@ __device__ __forceinline__ uint32_t crc_advq(uint32_t c, uint32_t q, int s)
     return r;
 }
 
-// rice-coded residual section of one lane from its kept zig-zag codes
+// rice-coded residual section of one lane from its kept zig-zag codes.
+// FULL (the register-staged kernel: every lane holds a whole 64-sample run,
+// hi = 64, and only lane 0 skips warm-up codes, lo <= 12): codes 12..63 are
+// written unconditionally, so no per-code lane mask is formed for them
+#ifndef ATG_K5_FULLEMIT
+#define ATG_K5_FULLEMIT 1
+#endif
+template <bool FULL>
 __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[ATG_RUN], int lo,
                                            int hi, uint32_t k)
 {
     const uint32_t kmask = (1u << k) - 1u;
 #pragma unroll
     for (int t = 0; t < ATG_RUN; ++t)
-        if (t >= lo && t < hi)
+        if ((FULL && ATG_K5_FULLEMIT) ? (t >= ATG_FAST_ORDER || t >= lo) : (t >= lo && t < hi))
             w.put(u[t] >> k, k + 1u, (1u << k) | (u[t] & kmask));
 }
 
@@ -585,7 +592,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))
                     if (part_head)
                         wr.put(0, pbits, k);
 #if ATG_EXP != 8
-                    emit_codes(wr, u, warm, len, k);
+                    emit_codes<REG>(wr, u, warm, len, k);
 #endif
                 } else {
                     // any order <= 32 / wide samples: 64-bit accumulator
