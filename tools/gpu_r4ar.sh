@@ -1,0 +1,11 @@
+#!/bin/bash
+# Round-4 close: the exact tree the driver will run -- GPU suite, smoke,
+# default bench.
+set -e -o pipefail
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$R/gpurun_out/${1:-r4ar}
+mkdir -p "$OUT"
+cd "$R"
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread > $OUT/pytest.log 2>&1
+timeout -k 10 120 python -u -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > $OUT/smoke.log 2>&1
+timeout -k 10 600 python -u bench.py > $OUT/bench.log 2>&1
