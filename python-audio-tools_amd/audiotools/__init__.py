@@ -11,6 +11,13 @@ find the same names with the same meaning:
   audiotools.PCMConverter ....... reference audiotools/__init__.py:2729-2802
   audiotools.resampled_frame_count reference audiotools/__init__.py:2805-2820
   audiotools.calculate_replay_gain reference audiotools/__init__.py:2845-2912
+  audiotools.AudioFile.convert .. reference audiotools/__init__.py:3760-3774
+  audiotools.AudioFile.verify ... reference audiotools/__init__.py:3939-3970
+  audiotools.FlacAudio / WaveAudio / ALACAudio (flac.py, wav.py, m4a.py)
+
+track2track's per-file step is `AudioFile.convert(target, FlacAudio, "8")`
+and trackverify's is `AudioFile.verify()`; both run through these classes,
+so under the drop-in they reach the GPU encoder and decoders.
 
 The encoding itself runs in libatgpu.so (HIP kernels for gfx950) through
 the C ABI declared in include/atgpu.h.  There is no CPU encoding path: if
@@ -37,6 +44,20 @@ class EncodingError(IOError):
 
     def __str__(self):
         return str(self.error_message)
+
+
+class InvalidFile(Exception):
+    """raised if a file is invalid in some way
+    (reference audiotools/__init__.py:1276-1279)"""
+
+
+class DecodingError(IOError):
+    """raised if a decoder exits with an error
+    (reference audiotools/__init__.py:1342-1350)"""
+
+    def __init__(self, error_message):
+        IOError.__init__(self, error_message)
+        self.error_message = error_message
 
 
 class PCMReader(object):
@@ -208,6 +229,181 @@ class PCMReaderProgress(object):
 
     def close(self):
         self._close()
+
+
+def to_pcm_progress(audiofile, progress):
+    """audiofile.to_pcm(), wrapped in a PCMReaderProgress when a progress
+    callback is given (reference audiotools/__init__.py:2158-2164)"""
+    if progress is None:
+        return audiofile.to_pcm()
+    return PCMReaderProgress(audiofile.to_pcm(), audiofile.total_frames(), progress)
+
+
+class CounterPCMReader(object):
+    """a PCMReader counting the frames read through it
+    (reference audiotools/__init__.py:2608-2631)"""
+
+    def __init__(self, pcmreader):
+        self.sample_rate = pcmreader.sample_rate
+        self.channels = pcmreader.channels
+        self.channel_mask = pcmreader.channel_mask
+        self.bits_per_sample = pcmreader.bits_per_sample
+        self.__pcmreader = pcmreader
+        self.frames_written = 0
+
+    def bytes_written(self):
+        return self.frames_written * self.channels * (self.bits_per_sample // 8)
+
+    def read(self, pcm_frames):
+        frame = self.__pcmreader.read(pcm_frames)
+        self.frames_written += frame.frames
+        return frame
+
+    def close(self):
+        self.__pcmreader.close()
+
+
+def transfer_data(from_function, to_function):
+    """BUFFER_SIZE strings from from_function to to_function until an empty
+    one; an IOError ends the transfer quietly
+    (reference audiotools/__init__.py:2301-2314)"""
+    try:
+        s = from_function(BUFFER_SIZE)
+        while len(s) > 0:
+            to_function(s)
+            s = from_function(BUFFER_SIZE)
+    except IOError:
+        pass
+
+
+def transfer_framelist_data(pcmreader, to_function, signed=True, big_endian=False):
+    """FrameLists from pcmreader as bytes to to_function until an empty one
+    (reference audiotools/__init__.py:2317-2328)"""
+    f = pcmreader.read(FRAMELIST_SIZE)
+    while len(f) > 0:
+        to_function(f.to_bytes(big_endian, signed))
+        f = pcmreader.read(FRAMELIST_SIZE)
+
+
+def pcm_cmp(pcmreader1, pcmreader2):
+    """True if the two readers' PCM data are equal
+    (reference audiotools/__init__.py:2384-2409)"""
+    if (pcmreader1.sample_rate != pcmreader2.sample_rate or
+            pcmreader1.channels != pcmreader2.channels or
+            pcmreader1.bits_per_sample != pcmreader2.bits_per_sample):
+        return False
+    reader1 = BufferedPCMReader(pcmreader1)
+    reader2 = BufferedPCMReader(pcmreader2)
+    s1 = reader1.read(FRAMELIST_SIZE)
+    s2 = reader2.read(FRAMELIST_SIZE)
+    while len(s1) > 0 and len(s2) > 0:
+        if s1 != s2:
+            return False
+        s1 = reader1.read(FRAMELIST_SIZE)
+        s2 = reader2.read(FRAMELIST_SIZE)
+    return True
+
+
+def pcm_frame_cmp(pcmreader1, pcmreader2):
+    """the PCM frame number of the first mismatch, None if the streams
+    match (reference audiotools/__init__.py:2445-2481); may raise IOError
+    or ValueError from the readers"""
+    if (pcmreader1.sample_rate != pcmreader2.sample_rate or
+            pcmreader1.channels != pcmreader2.channels or
+            pcmreader1.bits_per_sample != pcmreader2.bits_per_sample):
+        return 0
+    if (int(pcmreader1.channel_mask) != 0 and int(pcmreader2.channel_mask) != 0 and
+            int(pcmreader1.channel_mask) != int(pcmreader2.channel_mask)):
+        return 0
+    frame_number = 0
+    reader1 = BufferedPCMReader(pcmreader1)
+    reader2 = BufferedPCMReader(pcmreader2)
+    framelist1 = reader1.read(FRAMELIST_SIZE)
+    framelist2 = reader2.read(FRAMELIST_SIZE)
+    while len(framelist1) > 0 and len(framelist2) > 0:
+        if framelist1 != framelist2:
+            n = min(framelist1.frames, framelist2.frames)
+            for i in range(n):
+                if framelist1.frame(i) != framelist2.frame(i):
+                    return frame_number + i
+            return frame_number + max(n - 1, 0)
+        frame_number += framelist1.frames
+        framelist1 = reader1.read(FRAMELIST_SIZE)
+        framelist2 = reader2.read(FRAMELIST_SIZE)
+    if len(framelist1) == 0 and len(framelist2) == 0:
+        return None
+    return frame_number
+
+
+class AudioFile(object):
+    """the format-independent part of the reference's AudioFile
+    (audiotools/__init__.py:3595-3990) the transcode callers use:
+    convert() is track2track's per-file step, verify() trackverify's."""
+
+    SUFFIX = ""
+    NAME = ""
+
+    def __init__(self, filename):
+        self.filename = filename
+
+    def lossless(self):
+        return False
+
+    def convert(self, target_path, target_class, compression=None, progress=None):
+        """encode a new target_class file from this one
+        (reference audiotools/__init__.py:3760-3774); EncodingError on a
+        problem"""
+        return target_class.from_pcm(
+            target_path, to_pcm_progress(self, progress), compression,
+            total_pcm_frames=(self.total_frames() if self.lossless() else None))
+
+    @classmethod
+    def __unlink__(cls, filename):
+        import os
+        try:
+            os.unlink(filename)
+        except OSError:
+            pass
+
+    def __eq__(self, audiofile):
+        """equal PCM data (reference audiotools/__init__.py:3926-3934)"""
+        if hasattr(audiofile, "to_pcm") and callable(audiofile.to_pcm):
+            try:
+                return pcm_frame_cmp(self.to_pcm(), audiofile.to_pcm()) is None
+            except (ValueError, IOError):
+                return False
+        return False
+
+    def __ne__(self, audiofile):
+        return not self.__eq__(audiofile)
+
+    __hash__ = object.__hash__
+
+    def verify(self, progress=None):
+        """decode the whole file; True if it is sound, InvalidFile with the
+        decoder's message otherwise (reference
+        audiotools/__init__.py:3939-3970)"""
+        try:
+            total_frames = self.total_frames()
+            decoder = self.to_pcm()
+            pcm_frame_count = 0
+            framelist = decoder.read(FRAMELIST_SIZE)
+            while len(framelist) > 0:
+                pcm_frame_count += framelist.frames
+                if progress is not None:
+                    progress(pcm_frame_count, total_frames)
+                framelist = decoder.read(FRAMELIST_SIZE)
+        except (IOError, ValueError) as err:
+            raise InvalidFile(str(err))
+        try:
+            decoder.close()
+        except DecodingError as err:
+            raise InvalidFile(err.error_message)
+        if self.lossless():
+            if pcm_frame_count == total_frames:
+                return True
+            raise InvalidFile("incorrect PCM frame count")
+        return True
 
 
 def _check_mask(channel_mask, channels):
@@ -391,3 +587,9 @@ def calculate_replay_gain(tracks, progress=None):
     album_gain, album_peak = rg.album_gain()
     for track, gain, peak in gains:
         yield (track, gain, peak, album_gain, album_peak)
+
+
+# the format classes (their modules import the names above)
+from .flac import FlacAudio, InvalidFLAC  # noqa: E402,F401
+from .wav import WaveAudio, InvalidWave  # noqa: E402,F401
+from .m4a import ALACAudio, InvalidALAC  # noqa: E402,F401

@@ -15,7 +15,12 @@ turns encoder output into the finished file:
     - metadata rewritten in place, PADDING shrunk by the growth
       (FlacMetaData.add_block ordering flac.py:53-75, update_metadata
       :1369-1427)
-  FlacAudio(filename).to_pcm() -> audiotools.decoders.FlacDecoder (GPU)
+  FlacAudio(filename).to_pcm() -> audiotools.decoders.FlacDecoder (GPU),
+    positioned past any ID3v2 prefix; PCMReaderError if the decoder cannot
+    open the stream                                flac.py:1674-1693
+  FlacAudio.convert / verify (AudioFile's, flac.py:2360-2398 and
+    __init__.py:3939-3970) -- the track2track / trackverify steps
+  FlacAudio.channel_mask()                         flac.py:1284-1341
 
 The rewrite is byte-level host work; encoding and decoding run in libatgpu.
 """
@@ -23,8 +28,9 @@ The rewrite is byte-level host work; encoding and decoding run in libatgpu.
 import struct
 from bisect import bisect_right
 
-from . import BufferedPCMReader, EncodingError
+from . import AudioFile, BufferedPCMReader, ChannelMask, EncodingError, InvalidFile
 from . import _atgpu
+from .id3 import skip_id3v2_comment
 
 # FLAC metadata block ids
 STREAMINFO, PADDING, APPLICATION, SEEKTABLE, VORBIS_COMMENT, CUESHEET, PICTURE = \
@@ -61,6 +67,15 @@ _VALID_MASKS = (0x0001, 0x0004, 0x0003, 0x0007, 0x0033, 0x0603, 0x0037, 0x0607,
                 0x003F, 0x060F)
 
 
+class InvalidFLAC(InvalidFile):
+    """reference audiotools/flac.py:32-33"""
+
+
+# FLAC's channel assignments for 3..8 channels without a
+# WAVEFORMATEXTENSIBLE_CHANNEL_MASK comment (flac.py:1312-1341)
+_FLAC_MASKS = {3: 0x007, 4: 0x033, 5: 0x037, 6: 0x03F, 7: 0x70F, 8: 0x63F}
+
+
 class UnsupportedChannelCount(EncodingError):
     def __init__(self, filename, count):
         EncodingError.__init__(self, "unsupported channel count %d for %s"
@@ -85,6 +100,21 @@ def _blocks(data):
         pos += 4 + length
         if h & 0x80:
             return out, pos
+
+
+def _comment_values(body, key):
+    """the values of KEY=value entries of a VORBIS_COMMENT body (keys
+    compared case-insensitively, as VorbisComment's lookup does)"""
+    vl = int.from_bytes(body[:4], "little")
+    n = int.from_bytes(body[4 + vl:8 + vl], "little")
+    pos, prefix, out = 8 + vl, (key + "=").upper().encode("ascii"), []
+    for _ in range(n):
+        ll = int.from_bytes(body[pos:pos + 4], "little")
+        line = body[pos + 4:pos + 4 + ll]
+        if line[:len(prefix)].upper() == prefix:
+            out.append(line[len(prefix):].decode("utf-8", "replace"))
+        pos += 4 + ll
+    return out
 
 
 def _build(blocks):
@@ -150,20 +180,60 @@ def _set_comment(body, key, value):
     return b"".join(out)
 
 
-class FlacAudio(object):
+class FlacAudio(AudioFile):
     NAME = "flac"
     SUFFIX = "flac"
     DEFAULT_COMPRESSION = DEFAULT_COMPRESSION
     COMPRESSION_MODES = tuple(map(str, range(0, 9)))
 
     def __init__(self, filename):
-        self.filename = filename
-        with open(filename, "rb") as f:
-            data = f.read()
+        """read STREAMINFO past any ID3v2 prefix (__read_streaminfo__,
+        flac.py:2420-2470); InvalidFLAC if the file cannot be read"""
+        AudioFile.__init__(self, filename)
+        try:
+            with open(filename, "rb") as f:
+                f.seek(0, 2)
+                size = f.tell()
+                self.__stream_suffix = 0
+                if size >= 128:
+                    f.seek(-128, 2)
+                    if f.read(3) == b"TAG":
+                        self.__stream_suffix = 128
+                f.seek(0, 0)
+                self.__stream_offset = skip_id3v2_comment(f)
+                data = f.read()
+        except IOError as err:
+            raise InvalidFLAC(str(err))
         rc, si, _ = _atgpu.read_metadata(data)
         if rc:
-            raise ValueError("not a FLAC file" if rc == 1 else "EOF while reading metadata")
+            raise InvalidFLAC("Invalid FLAC file" if rc == 1 else "EOF while reading metadata")
         self._si = si
+        self._comments = []
+        try:
+            blocks, _ = _blocks(data)
+            for t, body in blocks:
+                if t == VORBIS_COMMENT:
+                    self._comments.append(body)
+        except (ValueError, IndexError):
+            pass
+
+    def lossless(self):
+        return True
+
+    def channel_mask(self):
+        """ChannelMask of the track's layout (flac.py:1284-1341): stereo and
+        mono fixed, else the WAVEFORMATEXTENSIBLE_CHANNEL_MASK comment when
+        its speaker count matches, else FLAC's default for the count"""
+        if self.channels() <= 2:
+            return ChannelMask.from_channels(self.channels())
+        try:
+            if not self._comments:
+                raise ValueError()
+            mask = ChannelMask(int(_comment_values(
+                self._comments[0], u"WAVEFORMATEXTENSIBLE_CHANNEL_MASK")[0], 16))
+            return mask if len(mask) == self.channels() else ChannelMask(0)
+        except (IndexError, KeyError, ValueError):
+            return ChannelMask(_FLAC_MASKS.get(self.channels(), 0))
 
     def sample_rate(self):
         return self._si.sample_rate
@@ -178,8 +248,31 @@ class FlacAudio(object):
         return self._si.total_samples
 
     def to_pcm(self):
+        """FlacDecoder over the stream from the "fLaC" marker on; if it
+        cannot be opened (the file changed since), a PCMReaderError
+        carrying the message (flac.py:1674-1693)"""
         from .decoders import FlacDecoder
-        return FlacDecoder(self.filename)
+        from . import PCMReaderError
+        try:
+            with open(self.filename, "rb") as flac:
+                if self.__stream_offset > 0:
+                    flac.seek(self.__stream_offset)
+                return FlacDecoder(flac)
+        except (IOError, ValueError) as msg:
+            return PCMReaderError(error_message=str(msg),
+                                  sample_rate=self.sample_rate(),
+                                  channels=self.channels(),
+                                  channel_mask=int(self.channel_mask()),
+                                  bits_per_sample=self.bits_per_sample())
+
+    def convert(self, target_path, target_class, compression=None, progress=None):
+        """FlacAudio.convert (flac.py:2360-2398): files with foreign RIFF /
+        AIFF chunks go through the target's from_wave / from_aiff, which no
+        class here has, so every conversion is from_pcm with the exact
+        frame count"""
+        from . import to_pcm_progress
+        return target_class.from_pcm(target_path, to_pcm_progress(self, progress),
+                                     compression, total_pcm_frames=self.total_frames())
 
     @classmethod
     def from_pcm(cls, filename, pcmreader, compression=None, total_pcm_frames=None,

@@ -13,6 +13,9 @@ path uses:
       byte for byte as the reference's atom builders write them
       (m4a.py:1126-1400, m4a_atoms.py)
   ALACAudio(filename).to_pcm() -> audiotools.decoders.ALACDecoder (GPU)
+  ALACAudio.convert / verify (AudioFile's, __init__.py:3760-3774,
+    3939-3970): the config-5 chain's source side under track2track /
+    trackverify; InvalidALAC for a file the decoder cannot open
 
 The container is host byte work; the ALAC bitstreams are encoded and
 decoded by libatgpu (alac_encode.hip / alac_decode.hip).
@@ -21,7 +24,7 @@ decoded by libatgpu (alac_encode.hip / alac_decode.hip).
 import struct
 import time
 
-from . import BufferedPCMReader, EncodingError, VERSION
+from . import AudioFile, BufferedPCMReader, ChannelMask, EncodingError, InvalidFile, VERSION
 
 INITIAL_HISTORY = 10      # m4a.py:759-762
 HISTORY_MULTIPLIER = 40
@@ -33,6 +36,10 @@ APPLE_EPOCH = 2082844800
 VALID_MASKS = (0x0001, 0x0004, 0x0003, 0x0007, 0x0107, 0x0037, 0x003F, 0x013F, 0x00FF,
                0x0000)
 _MATRIX = (0x10000, 0, 0, 0, 0x10000, 0, 0, 0, 0x40000000)
+
+
+class InvalidALAC(InvalidFile):
+    """reference audiotools/m4a.py:745-746"""
 
 
 class UnsupportedBitsPerSample(EncodingError):
@@ -172,7 +179,7 @@ def m4a_file(channels, bps, rate, block_size, total, mdat, frame_sizes, create_d
     return ftyp + moov + free + bytes(mdat)
 
 
-class ALACAudio(object):
+class ALACAudio(AudioFile):
     """the reference's ALACAudio (m4a.py:750-1124), transcode slice"""
 
     SUFFIX = "m4a"
@@ -185,8 +192,11 @@ class ALACAudio(object):
 
     def __init__(self, filename):
         from . import decoders
-        self.filename = filename
-        d = decoders.ALACDecoder(filename)
+        AudioFile.__init__(self, filename)
+        try:
+            d = decoders.ALACDecoder(filename)
+        except (IOError, ValueError) as err:
+            raise InvalidALAC(str(err))
         self._channels = d.channels
         self._rate = d.sample_rate
         self._bps = d.bits_per_sample
@@ -204,7 +214,7 @@ class ALACAudio(object):
         return self._bps
 
     def channel_mask(self):
-        return self._mask
+        return ChannelMask(self._mask)
 
     def total_frames(self):
         return self._total

@@ -10,8 +10,9 @@ ATG_PCM_S32 container without a copy.
 
 import numpy as np
 
-__all__ = ["FrameList", "from_list", "from_frames", "from_channels",
-           "empty_framelist"]
+__all__ = ["FrameList", "FloatFrameList", "from_list", "from_frames",
+           "from_channels", "from_float_frames", "from_float_channels",
+           "empty_framelist", "empty_float_framelist"]
 
 
 def _check_bps(bits_per_sample):
@@ -83,8 +84,11 @@ class FrameList(object):
         return self._samples
 
     def frame_count(self, bytes_count):
-        """number of whole PCM frames in `bytes_count` bytes"""
-        return bytes_count // (self.channels * (self.bits_per_sample // 8))
+        """whole PCM frames in `bytes_count` bytes, at least 1
+        (FrameList_frame_count, src/pcm.c:618-631)"""
+        per = self.channels * (self.bits_per_sample // 8)
+        bytes_count -= bytes_count % per
+        return bytes_count // per if bytes_count else 1
 
     # --- sequence protocol ------------------------------------------
     def __len__(self):
@@ -157,7 +161,126 @@ class FrameList(object):
         return out.tobytes()
 
     def to_float(self):
-        return self._samples.astype(np.float64) / float(1 << (self.bits_per_sample - 1))
+        """-> FloatFrameList of samples / 2^(bps-1) in fp64
+        (FrameList_to_float, src/pcm.c:599-615)"""
+        return FloatFrameList._wrap(
+            self._samples.astype(np.float64) / float(1 << (self.bits_per_sample - 1)),
+            self.channels)
+
+
+def _cvttsd2si(values):
+    """(int) of fp64 values with x86 cvttsd2si semantics: truncation toward
+    zero, and INT_MIN for NaN and anything outside int32 (the reference's
+    C cast, src/pcm.c:1222, compiled for x86-64)"""
+    v = np.asarray(values, dtype=np.float64)
+    out = np.full(v.shape, -(1 << 31), dtype=np.int64)
+    ok = np.isfinite(v) & (v > -2147483649.0) & (v < 2147483648.0)
+    out[ok] = np.trunc(v[ok]).astype(np.int64)
+    return out
+
+
+class FloatFrameList(object):
+    """FloatFrameList(float_list, channels): `frames` PCM frames of
+    `channels` interleaved fp64 samples in [-1.0, 1.0) (reference C type
+    pcm.FloatFrameList, src/pcm.c:907-1380)"""
+
+    __slots__ = ("_samples", "channels")
+
+    def __init__(self, data, channels):
+        if isinstance(data, (str, bytes)) or not hasattr(data, "__len__"):
+            raise TypeError("FloatFrameList requires a sequence of floats")
+        if channels < 1:
+            raise ValueError("number of channels must be > 0")
+        if len(data) % channels:
+            raise ValueError("number of samples must be divisible by number of channels")
+        try:
+            self._samples = np.array([float(x) for x in data], dtype=np.float64)
+        except (TypeError, ValueError):
+            raise TypeError("FloatFrameList samples must be floats")
+        self.channels = channels
+
+    @classmethod
+    def _wrap(cls, samples, channels):
+        fl = cls.__new__(cls)
+        fl._samples = np.ascontiguousarray(samples, dtype=np.float64)
+        fl.channels = channels
+        return fl
+
+    @property
+    def frames(self):
+        return len(self._samples) // self.channels
+
+    @property
+    def samples(self):
+        return self._samples
+
+    def __len__(self):
+        return len(self._samples)
+
+    def __getitem__(self, i):
+        if i < 0 or i >= len(self._samples):
+            raise IndexError("index out of range")
+        return float(self._samples[i])
+
+    def __iter__(self):
+        return iter(float(x) for x in self._samples)
+
+    def __eq__(self, other):
+        return (isinstance(other, FloatFrameList) and self.channels == other.channels and
+                np.array_equal(self._samples, other._samples))
+
+    def __ne__(self, other):
+        return not self.__eq__(other)
+
+    def __add__(self, other):
+        if not isinstance(other, FloatFrameList):
+            raise TypeError("can only concatenate FloatFrameList with other FloatFrameLists")
+        if other.channels != self.channels:
+            raise ValueError("both FloatFrameLists must have the same number of channels")
+        return FloatFrameList._wrap(np.concatenate([self._samples, other._samples]),
+                                    self.channels)
+
+    def __mul__(self, count):
+        return FloatFrameList._wrap(np.tile(self._samples, max(int(count), 0)), self.channels)
+
+    def __repr__(self):
+        return "FloatFrameList(frames=%d, channels=%d)" % (self.frames, self.channels)
+
+    def frame(self, index):
+        if index < 0 or index >= self.frames:
+            raise IndexError("frame number out of range")
+        c = self.channels
+        return FloatFrameList._wrap(self._samples[index * c:(index + 1) * c], c)
+
+    def channel(self, index):
+        if index < 0 or index >= self.channels:
+            raise IndexError("channel number out of range")
+        return FloatFrameList._wrap(self._samples[index::self.channels], 1)
+
+    def split(self, count):
+        """split(frames) -> (head, tail) (FloatFrameList_split,
+        src/pcm.c:1229-1288); IndexError for a negative split point"""
+        if count < 0:
+            raise IndexError("split point must be positive")
+        cut = min(count, self.frames) * self.channels
+        return (FloatFrameList._wrap(self._samples[:cut], self.channels),
+                FloatFrameList._wrap(self._samples[cut:], self.channels))
+
+    @staticmethod
+    def from_frames(frames):
+        return from_float_frames(frames)
+
+    @staticmethod
+    def from_channels(channels):
+        return from_float_channels(channels)
+
+    def to_int(self, bits_per_sample):
+        """-> FrameList of (int)(sample * 2^(bps-1)) clamped to the bps range
+        (FloatFrameList_to_int, src/pcm.c:1198-1227)"""
+        adjustment = 1 << (bits_per_sample - 1)
+        v = _cvttsd2si(self._samples * adjustment)
+        v = np.maximum(np.minimum(v, adjustment - 1), -adjustment)
+        return FrameList._wrap(v, self.channels, bits_per_sample)
 
 
 def from_list(values, channels, bits_per_sample, is_signed=True):
@@ -201,3 +324,40 @@ def from_channels(channels):
 
 def empty_framelist(channels, bits_per_sample):
     return FrameList._wrap(np.zeros(0, dtype=np.int32), channels, bits_per_sample)
+
+
+def empty_float_framelist(channels):
+    return FloatFrameList._wrap(np.zeros(0, dtype=np.float64), channels)
+
+
+def from_float_frames(frames):
+    """concatenate single-frame FloatFrameLists (src/pcm.c FloatFrameList_from_frames)"""
+    frames = list(frames)
+    if not frames:
+        raise IndexError("list index out of range")
+    for f in frames:
+        if not isinstance(f, FloatFrameList):
+            raise TypeError("frames must be of type FloatFrameList")
+        if f.channels != frames[0].channels:
+            raise ValueError("all subframes must have the same number of channels")
+        if f.frames != 1:
+            raise ValueError("all subframes must be 1 frame long")
+    return FloatFrameList._wrap(np.concatenate([f.samples for f in frames]),
+                                frames[0].channels)
+
+
+def from_float_channels(channels):
+    """interleave single-channel FloatFrameLists (src/pcm.c
+    FloatFrameList_from_channels)"""
+    channels = list(channels)
+    if not channels:
+        raise IndexError("list index out of range")
+    for c in channels:
+        if not isinstance(c, FloatFrameList):
+            raise TypeError("channels must be of type FloatFrameList")
+        if c.frames != channels[0].frames:
+            raise ValueError("all channels must have the same number of frames")
+        if c.channels != 1:
+            raise ValueError("all channels must be 1 channel wide")
+    return FloatFrameList._wrap(np.stack([c.samples for c in channels], axis=1).reshape(-1),
+                                len(channels))
