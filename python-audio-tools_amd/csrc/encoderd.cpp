@@ -7,7 +7,14 @@
 // (atg_flac_encode_frames_batch): eight track2track conversion processes
 // each sending a 64-frame track become one 512-frame batch.  A group that
 // fails is retried request by request so an error reaches only its sender.
-// Exits after --idle-ms without a connected client (default 3000).
+// Exits after --idle-ms without a connected client (default 3000), after
+// taking any connection still queued in the listen backlog.
+//
+// The socket name is abstract (no file permissions): a connecting process
+// of another user is dropped on accept (SO_PEERCRED), and the clients check
+// the daemon the same way (service.hip).  Replies are queued per client and
+// written from the poll loop without blocking, so a client that stops
+// reading holds only its own reply, never the other clients' batches.
 //
 //   atgpu-encoderd [--device N] [--idle-ms MS]
 #include <errno.h>
@@ -47,7 +54,18 @@ struct Client {
     bool have_header = false;
     bool ready = false;       // a complete request waits in buf
     bool dead = false;
+    std::vector<uint8_t> outq; // reply bytes not yet written
+    size_t out_off = 0;
 };
+
+bool peer_is_me(int fd)
+{
+    ucred cr;
+    socklen_t n = sizeof(cr);
+    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &n) != 0 || n != sizeof(cr))
+        return false;
+    return cr.uid == getuid();
+}
 
 const atg_svc_request &hdr(const Client &c) { return *(const atg_svc_request *)c.buf.data(); }
 
@@ -65,26 +83,32 @@ bool valid_header(const atg_svc_request &q)
     return q.pcm_bytes == q.pcm_frames * q.channels * elem;
 }
 
-bool send_all(int fd, const void *p, size_t n)
+// write what the socket takes now; the rest waits for POLLOUT
+void flush(Client &c)
 {
-    const uint8_t *b = (const uint8_t *)p;
-    while (n) {
-        const ssize_t k = send(fd, b, n, MSG_NOSIGNAL);
+    while (!c.dead && c.out_off < c.outq.size()) {
+        const ssize_t k = send(c.fd, c.outq.data() + c.out_off, c.outq.size() - c.out_off,
+                               MSG_NOSIGNAL | MSG_DONTWAIT);
         if (k < 0) {
             if (errno == EINTR)
                 continue;
-            if (errno == EAGAIN || errno == EWOULDBLOCK) {
-                pollfd p1{fd, POLLOUT, 0};
-                if (poll(&p1, 1, 10000) <= 0)
-                    return false;
-                continue;
-            }
-            return false;
+            if (errno != EAGAIN && errno != EWOULDBLOCK)
+                c.dead = true;
+            return;
         }
-        b += k;
-        n -= (size_t)k;
+        c.out_off += (size_t)k;
     }
-    return true;
+    if (c.out_off == c.outq.size()) {
+        c.outq.clear();
+        c.outq.shrink_to_fit();
+        c.out_off = 0;
+    }
+}
+
+void put(std::vector<uint8_t> &q, const void *p, size_t n)
+{
+    const uint8_t *b = (const uint8_t *)p;
+    q.insert(q.end(), b, b + n);
 }
 
 void respond(Client &c, int32_t status, const std::string &msg, const uint8_t *out,
@@ -92,14 +116,17 @@ void respond(Client &c, int32_t status, const std::string &msg, const uint8_t *o
 {
     atg_svc_response r;
     r.status = status;
-    r.msg_len = (uint32_t)msg.size();
+    const std::string m = msg.substr(0, ATG_SVC_MAX_MSG);
+    r.msg_len = (uint32_t)m.size();
     r.out_bytes = status == ATG_OK ? out_bytes : 0;
     r.n_frames = status == ATG_OK ? nf : 0;
-    bool ok = send_all(c.fd, &r, sizeof(r)) && (msg.empty() || send_all(c.fd, msg.data(), msg.size()));
-    if (ok && status == ATG_OK)
-        ok = (!nf || send_all(c.fd, fb, 4 * nf)) && (!out_bytes || send_all(c.fd, out, out_bytes));
-    if (!ok)
-        c.dead = true;
+    put(c.outq, &r, sizeof(r));
+    put(c.outq, m.data(), m.size());
+    if (status == ATG_OK) {
+        put(c.outq, fb, 4 * nf);
+        put(c.outq, out, out_bytes);
+    }
+    flush(c);
     // ready for the next request
     c.buf.clear();
     c.need = sizeof(atg_svc_request);
@@ -171,6 +198,26 @@ atg_status encode_group(atg_engine *eng, std::vector<Client *> &mem, std::string
     return ATG_OK;
 }
 
+// accept every queued connection of this user; true if any was taken
+bool accept_all(int lfd, std::vector<std::unique_ptr<Client>> &clients)
+{
+    bool any = false;
+    for (;;) {
+        const int cfd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
+        if (cfd < 0)
+            break;
+        if (!peer_is_me(cfd)) {
+            close(cfd);
+            continue;
+        }
+        auto c = std::make_unique<Client>();
+        c->fd = cfd;
+        clients.push_back(std::move(c));
+        any = true;
+    }
+    return any;
+}
+
 } // namespace
 
 int main(int argc, char **argv)
@@ -215,22 +262,16 @@ int main(int argc, char **argv)
         std::vector<pollfd> pf;
         pf.push_back(pollfd{lfd, POLLIN, 0});
         for (auto &c : clients)
-            pf.push_back(pollfd{c->fd, POLLIN, 0});
+            pf.push_back(pollfd{c->fd, (short)(POLLIN | (c->outq.empty() ? 0 : POLLOUT)), 0});
         const int pr = poll(pf.data(), pf.size(), 100);
         if (pr < 0 && errno != EINTR)
             break;
-        if (pf[0].revents & POLLIN) {
-            for (;;) {
-                const int cfd = accept4(lfd, nullptr, nullptr, SOCK_NONBLOCK | SOCK_CLOEXEC);
-                if (cfd < 0)
-                    break;
-                auto c = std::make_unique<Client>();
-                c->fd = cfd;
-                clients.push_back(std::move(c));
-            }
-        }
+        if (pf[0].revents & POLLIN)
+            accept_all(lfd, clients);
         for (size_t i = 1; i < pf.size(); ++i) {
             Client &c = *clients[i - 1];
+            if (pf[i].revents & POLLOUT)
+                flush(c);
             if (!(pf[i].revents & (POLLIN | POLLHUP | POLLERR)))
                 continue;
             // read until the request is complete or the socket is drained
@@ -293,10 +334,16 @@ int main(int argc, char **argv)
                 ++i;
             }
         }
-        if (!clients.empty())
+        if (!clients.empty()) {
             last_active = now_ms();
-        else if (now_ms() - last_active > idle_ms)
+        } else if (now_ms() - last_active > idle_ms) {
+            // a connect that landed after the last poll() sits in the
+            // backlog: serve it rather than reset it
+            pollfd p0{lfd, POLLIN, 0};
+            if (poll(&p0, 1, 0) > 0 && accept_all(lfd, clients))
+                continue;
             break;
+        }
     }
     close(lfd);
     atg_engine_destroy(eng);

@@ -22,6 +22,7 @@
 // bounds a request may not exceed (a malformed one is refused, not trusted)
 #define ATG_SVC_MAX_FRAMES 65536u
 #define ATG_SVC_MAX_PCM_BYTES (1ull << 31)
+#define ATG_SVC_MAX_MSG 4096u
 
 // request: this header, then uint32 frame_sizes[n_frame_sizes], then
 // pcm_bytes of interleaved PCM (int16 for ATG_PCM_S16, int32 otherwise)
@@ -41,6 +42,10 @@ typedef struct {
 } atg_svc_response;
 
 // the service's socket name for a device (abstract namespace: no file to
-// clean up; per user): "\0atgpu-encoderd.<uid>.<device>", or
-// ATG_ENCODER_SOCKET's value when set
+// clean up): "\0atgpu-encoderd.<uid>.<device>", or ATG_ENCODER_SOCKET's
+// value when set.  An abstract name has no permissions, so both ends check
+// the peer's uid (SO_PEERCRED) and drop a connection from another user; the
+// client also checks every reply against its request (frame count, sizes,
+// the segment's byte bound) and gives up on a reply that misses its
+// deadline (ATG_SERVICE_TIMEOUT_MS + 1 ms per 50 KB of PCM)
 #define ATG_SVC_NAME_FMT "atgpu-encoderd.%u.%d"

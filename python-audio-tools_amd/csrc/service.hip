@@ -18,6 +18,7 @@
 #include <unistd.h>
 
 #include <string>
+#include <vector>
 
 #include "../../include/atgpu.h"
 #include "service.h"
@@ -53,6 +54,20 @@ socklen_t service_addr(int device, sockaddr_un &a)
     return (socklen_t)(offsetof(sockaddr_un, sun_path) + 1 + n);
 }
 
+// abstract sockets carry no file permissions: whoever binds the name first
+// owns it.  The peer must be a process of this user (SO_PEERCRED), or the
+// socket is dropped -- PCM is never sent to, and frames never taken from,
+// another user's process.  (The daemon checks its clients the same way.)
+bool peer_is_me(int fd)
+{
+    ucred cr;
+    socklen_t n = sizeof(cr);
+    if (getsockopt(fd, SOL_SOCKET, SO_PEERCRED, &cr, &n) != 0 || n != sizeof(cr))
+        return false;
+    return cr.uid == getuid();
+}
+
+// -1: nothing listens; -2: a listener of another user holds the name
 int try_connect(int device)
 {
     const int fd = socket(AF_UNIX, SOCK_STREAM | SOCK_CLOEXEC, 0);
@@ -60,8 +75,12 @@ int try_connect(int device)
         return -1;
     sockaddr_un a;
     const socklen_t len = service_addr(device, a);
-    if (connect(fd, (const sockaddr *)&a, len) == 0)
-        return fd;
+    if (connect(fd, (const sockaddr *)&a, len) == 0) {
+        if (peer_is_me(fd))
+            return fd;
+        close(fd);
+        return -2;
+    }
     close(fd);
     return -1;
 }
@@ -146,12 +165,30 @@ bool send_all(int fd, const void *p, size_t n)
     return true;
 }
 
-bool recv_all(int fd, void *p, size_t n)
+double mono_ms()
+{
+    timespec t;
+    clock_gettime(CLOCK_MONOTONIC, &t);
+    return t.tv_sec * 1e3 + t.tv_nsec * 1e-6;
+}
+
+// receive exactly n bytes before the absolute deadline (CLOCK_MONOTONIC ms);
+// false on EOF, error or timeout
+bool recv_all(int fd, void *p, size_t n, double deadline)
 {
     uint8_t *b = (uint8_t *)p;
     while (n) {
+        const double left = deadline - mono_ms();
+        if (left <= 0)
+            return false;
+        pollfd pf{fd, POLLIN, 0};
+        const int pr = poll(&pf, 1, left > 1e9 ? 1000000000 : (int)left + 1);
+        if (pr < 0 && errno == EINTR)
+            continue;
+        if (pr <= 0)
+            return false;
         const ssize_t k = recv(fd, b, n, 0);
-        if (k < 0 && errno == EINTR)
+        if (k < 0 && (errno == EINTR || errno == EAGAIN))
             continue;
         if (k <= 0)
             return false;
@@ -167,6 +204,26 @@ void sleep_ms(unsigned ms)
     nanosleep(&ts, nullptr);
 }
 
+// how long a segment may take the service: a fixed allowance for HIP
+// start-up and the batch it joins, plus its PCM at a rate far below any
+// real encode (50 MB/s); the service's stall past this is treated as its
+// loss, and the caller encodes on an engine of its own
+double segment_deadline_ms(uint64_t pcm_bytes)
+{
+    const char *env = getenv("ATG_SERVICE_TIMEOUT_MS");
+    const double base = env && *env ? atof(env) : 30000.0;
+    return mono_ms() + base + (double)pcm_bytes / 50e3;
+}
+
+// the connection is out of step (timeout, malformed reply): drop it
+atg_status lose(atg_service *s, const char *m)
+{
+    if (s->fd >= 0)
+        close(s->fd);
+    s->fd = -1;
+    return sfail(ATG_ERR_DEVICE, m);
+}
+
 } // namespace
 
 extern "C" {
@@ -179,6 +236,8 @@ atg_status atg_service_connect(int device, int spawn, atg_service **out)
         return sfail(ATG_ERR_INVALID, "out is NULL");
     *out = nullptr;
     int fd = try_connect(device);
+    if (fd == -2)
+        return sfail(ATG_ERR_DEVICE, "the encoder service's name is held by another user");
     if (fd < 0 && spawn) {
         if (gpu_opened())
             return sfail(ATG_ERR_DEVICE, "this process has opened the GPU: not starting the "
@@ -187,11 +246,13 @@ atg_status atg_service_connect(int device, int spawn, atg_service **out)
             return sfail(ATG_ERR_DEVICE, "atgpu-encoderd not found or not started");
         // the service binds its socket first, then brings up HIP; connects
         // queue in its backlog meanwhile
-        for (unsigned waited = 0, step = 2; fd < 0 && waited < 30000; waited += step) {
+        for (unsigned waited = 0, step = 2; fd == -1 && waited < 30000; waited += step) {
             sleep_ms(step);
             fd = try_connect(device);
             step = step < 64 ? 2 * step : 64;
         }
+        if (fd == -2)
+            return sfail(ATG_ERR_DEVICE, "the encoder service's name is held by another user");
     }
     if (fd < 0)
         return sfail(ATG_ERR_DEVICE, "no encoder service for this device");
@@ -218,8 +279,10 @@ atg_status atg_service_encode_frames(atg_service *s, const atg_flac_options *opt
                                      uint64_t first_frame_number, uint8_t *out, uint64_t out_cap,
                                      uint64_t *out_bytes, uint32_t *frame_bytes)
 {
-    if (!s || s->fd < 0 || !opts || (!pcm && pcm_frames) || !out_bytes)
+    if (!s || !opts || (!pcm && pcm_frames) || !out_bytes)
         return sfail(ATG_ERR_INVALID, "NULL argument");
+    if (s->fd < 0)
+        return sfail(ATG_ERR_DEVICE, "encoder service connection lost");
     if (channels < 1 || channels > 8 || n_frame_sizes > ATG_SVC_MAX_FRAMES ||
         (frame_sizes == nullptr && n_frame_sizes))
         return sfail(ATG_ERR_INVALID, "invalid segment");
@@ -239,35 +302,62 @@ atg_status atg_service_encode_frames(atg_service *s, const atg_flac_options *opt
     q.pcm_bytes = pcm_frames * channels * elem;
     if (q.pcm_bytes > ATG_SVC_MAX_PCM_BYTES)
         return sfail(ATG_ERR_UNSUPPORTED, "segment too large for the encoder service");
+    // the frames the reply must describe: one per given size, else one per
+    // block (the service's own count, encoderd.cpp n_frames_of)
+    const uint64_t want_frames =
+        q.n_frame_sizes ? q.n_frame_sizes
+                        : (opts->block_size ? (pcm_frames + opts->block_size - 1) / opts->block_size
+                                            : 0);
+    const double deadline = segment_deadline_ms(q.pcm_bytes);
     if (!send_all(s->fd, &q, sizeof(q)) ||
         (q.n_frame_sizes && !send_all(s->fd, frame_sizes, 4 * q.n_frame_sizes)) ||
         (q.pcm_bytes && !send_all(s->fd, pcm, q.pcm_bytes)))
-        return sfail(ATG_ERR_DEVICE, "encoder service connection lost (send)");
+        return lose(s, "encoder service connection lost (send)");
     atg_svc_response r;
-    if (!recv_all(s->fd, &r, sizeof(r)))
-        return sfail(ATG_ERR_DEVICE, "encoder service connection lost (receive)");
+    if (!recv_all(s->fd, &r, sizeof(r), deadline))
+        return lose(s, "encoder service lost or timed out (receive)");
+    if (r.msg_len > ATG_SVC_MAX_MSG)
+        return lose(s, "encoder service: malformed response");
     std::string msg(r.msg_len, '\0');
-    if (r.msg_len && !recv_all(s->fd, &msg[0], r.msg_len))
-        return sfail(ATG_ERR_DEVICE, "encoder service connection lost (receive)");
-    if (r.status != ATG_OK)
+    if (r.msg_len && !recv_all(s->fd, &msg[0], r.msg_len, deadline))
+        return lose(s, "encoder service lost or timed out (receive)");
+    if (r.status != ATG_OK) {
+        if (r.n_frames || r.out_bytes)
+            return lose(s, "encoder service: malformed response");
         return sfail((atg_status)r.status, msg);
-    if (r.n_frames > ATG_SVC_MAX_FRAMES * 64ull)
-        return sfail(ATG_ERR_DEVICE, "encoder service: malformed response");
-    std::string fb(4 * r.n_frames, '\0');
-    if (r.n_frames && !recv_all(s->fd, &fb[0], fb.size()))
-        return sfail(ATG_ERR_DEVICE, "encoder service connection lost (receive)");
+    }
+    // the reply is checked against the request before any byte of it is
+    // stored: exactly the requested frame count (frame_bytes holds that many),
+    // frame sizes that add up to out_bytes, and out_bytes within the bound
+    // the segment's options allow
+    if (r.n_frames != want_frames)
+        return lose(s, "encoder service: response frame count differs from the request");
+    const uint64_t bound = atg_flac_max_frames_bytes(opts, pcm_frames, q.n_frame_sizes ? frame_sizes
+                                                                                       : nullptr,
+                                                     q.n_frame_sizes, channels, bps);
+    if (r.out_bytes > bound)
+        return lose(s, "encoder service: response larger than the segment's bound");
+    std::vector<uint32_t> fb((size_t)r.n_frames);
+    if (r.n_frames && !recv_all(s->fd, fb.data(), 4 * fb.size(), deadline))
+        return lose(s, "encoder service lost or timed out (receive)");
+    uint64_t sum = 0;
+    for (uint32_t b : fb)
+        sum += b;
+    if (sum != r.out_bytes)
+        return lose(s, "encoder service: frame sizes do not add up to the response");
     if (r.out_bytes > out_cap) {
         // drain the frames to keep the stream in step, then report
-        std::string sink(r.out_bytes, '\0');
-        recv_all(s->fd, &sink[0], sink.size());
+        std::vector<uint8_t> sink((size_t)r.out_bytes);
+        if (!recv_all(s->fd, sink.data(), sink.size(), deadline))
+            return lose(s, "encoder service lost or timed out (receive)");
         *out_bytes = r.out_bytes;
         return sfail(ATG_ERR_CAPACITY, "output buffer too small for the segment's frames");
     }
-    if (r.out_bytes && !recv_all(s->fd, out, r.out_bytes))
-        return sfail(ATG_ERR_DEVICE, "encoder service connection lost (receive)");
+    if (r.out_bytes && !recv_all(s->fd, out, r.out_bytes, deadline))
+        return lose(s, "encoder service lost or timed out (receive)");
     *out_bytes = r.out_bytes;
     if (frame_bytes && r.n_frames)
-        std::memcpy(frame_bytes, fb.data(), fb.size());
+        std::memcpy(frame_bytes, fb.data(), 4 * fb.size());
     return ATG_OK;
 }
 
