@@ -75,6 +75,11 @@ def parse_args(argv=None):
     ap.add_argument("--cpu-threads", type=int, default=0)
     ap.add_argument("--cpu-ref-tracks", type=int, default=256,
                     help="tracks the reference encoder baseline encodes")
+    ap.add_argument("--narrow", default="512,256,128",
+                    help="track counts of the narrow-batch leg (a strong-scaling rank's "
+                         "share, on one GPU); empty to skip")
+    ap.add_argument("--narrow-depths", default="3,12,16",
+                    help="batches in flight for the narrow leg (atg_engine_set_inflight)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--chain-tracks", type=int, default=64,
@@ -1134,6 +1139,76 @@ def selftest(args):
         dist.destroy_process_group()
 
 
+def strong_depth(n_tracks):
+    """batches in flight for a rank batch of n_tracks config-2 tracks: the
+    kernels of a batch take ~8.3 ms x n/1024, its MD5 chains ~12.5 ms
+    whatever n, so a narrow batch needs chain / kernels + 2 batches in
+    flight (rolled MD5 slices the chain over depth - 2 enqueues); measured
+    best: 16 up to 256 tracks, 12 up to 512 (profiles/r05_narrow.json)"""
+    return 16 if n_tracks <= 256 else 12 if n_tracks <= 512 else 3
+
+
+def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_full, res_full,
+               barrier):
+    """frames/s of narrow batches (the first n tracks of the config-2 batch)
+    at each in-flight depth; every image of the last batch byte-compared
+    with the full batch's image of the same track"""
+    from audiotools import _atgpu
+    widths = [int(x) for x in args.narrow.split(",") if x.strip()]
+    depths = [int(x) for x in args.narrow_depths.split(",") if x.strip()]
+    out = {}
+    for n in widths:
+        n = min(n, len(tracks))
+        sub = tracks[:n]
+        _, cap = eng.bounds(opts, sub, 2, 16)
+        table = _atgpu.TrackTable(sub)
+        per = {}
+        for d in depths:
+            eng.set_inflight(d)
+            bufs = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(d)]
+            pend = []
+
+            def run(steps):
+                last = None
+                for k in range(steps):
+                    pend.append(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16,
+                                                        table, 2, 16, 44100,
+                                                        bufs[k % d].data_ptr(), cap))
+                    if len(pend) >= d:
+                        last = eng.wait(pend.pop(0))
+                while pend:
+                    last = eng.wait(pend.pop(0))
+                return last
+
+            run(d + 1)
+            barrier()
+            t0 = time.perf_counter()
+            r = run(args.steps)
+            barrier()
+            dt = time.perf_counter() - t0
+            if world > 1:
+                dt = reduce_max(torch, dist, dt, device)
+            kt = eng.kernel_times()
+            last = bufs[(args.steps - 1) % d]
+            bad = 0
+            for t in range(n):
+                a = last[r[t].out_offset:r[t].out_offset + r[t].bytes]
+                b = out_full[res_full[t].out_offset:res_full[t].out_offset + res_full[t].bytes]
+                if r[t].bytes != res_full[t].bytes or not torch.equal(a, b):
+                    bad += 1
+            per["inflight_%d" % d] = {
+                "value": round(n * args.frames * args.steps / dt, 1), "unit": "frames/s",
+                "ms_per_step": round(dt / args.steps * 1e3, 3),
+                "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
+                "verified_tracks": n - bad, "mismatches": bad}
+            del bufs
+        eng.set_inflight(args.inflight if args.inflight >= 3 else 3)
+        out[str(n)] = per
+    return {"tracks_per_batch": out,
+            "note": "the first n tracks of the config-2 batch per step, pipelined; "
+                    "images compared with the full batch's (the same tracks' bytes)"}
+
+
 def main(argv=None):
     argv = list(sys.argv[1:] if argv is None else argv)
     args = parse_args(argv)
@@ -1239,14 +1314,48 @@ def main(argv=None):
     if world > 1 and args.scaling == "weak":
         n_s = len(shard(world, rank, args.tracks, "strong"))
         st_table = _atgpu.TrackTable(tracks[:n_s])
-        timed(st_table, 1)
-        dt = timed(st_table, args.steps)
+        # a narrow rank batch keeps more batches in flight so the per-track
+        # MD5 chains (~12.5 ms per 1 MiB track whatever the width) stay off
+        # the step: rolled MD5 (atg_engine_set_inflight)
+        s_depth = strong_depth(n_s)
+        _, s_cap = eng.bounds(opts, tracks[:n_s], 2, 16)
+        s_outs = [torch.empty(s_cap, dtype=torch.uint8, device=device) for _ in range(s_depth)]
+        eng.set_inflight(s_depth)
+
+        def s_timed(steps):
+            barrier()
+            t1 = time.perf_counter()
+            pend = []
+            for k in range(steps):
+                pend.append(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16,
+                                                    st_table, 2, 16, 44100,
+                                                    s_outs[k % s_depth].data_ptr(), s_cap))
+                if len(pend) >= s_depth:
+                    eng.wait(pend.pop(0))
+            while pend:
+                eng.wait(pend.pop(0))
+            barrier()
+            dt = time.perf_counter() - t1
+            return reduce_max(torch, dist, dt, device)
+
+        s_timed(s_depth + 1)
+        dt = s_timed(args.steps)
+        eng.set_inflight(3)
+        del s_outs
         tot = reduce_sum(torch, dist, n_s * args.frames * args.steps, device)
         strong = {"value": round(tot / dt, 1), "unit": "frames/s",
                   "ms_per_step": round(dt / args.steps * 1e3, 3),
-                  "tracks_total": args.tracks, "tracks_per_gpu": n_s,
-                  "bound": "per-track MD5 chain (~12 ms per 1 MiB track, serial) once a rank's "
-                           "batch is narrow; three batches in flight"}
+                  "tracks_total": args.tracks, "tracks_per_gpu": n_s, "inflight": s_depth,
+                  "bound": "per-track MD5 chain (~12.5 ms per 1 MiB track, serial): a narrow "
+                           "rank keeps %d batches in flight, their chains advanced together "
+                           "(rolled MD5)" % s_depth}
+    # ---- narrow batches (SURVEY 8(e) strong scaling: a rank's share of the
+    # 1024-track job), one GPU, pipelined at several in-flight depths; the
+    # last batch's images are compared with the full batch's (the same
+    # tracks' PCM, so the same bytes: the full batch is checked against the
+    # port below)
+    narrow = narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out, res,
+                        barrier) if args.narrow else None
     # ---- the search kernel with one batch in flight: in the pipelined loop
     # above the batches behind run their LPC kernels (slot stream) beside it
     alone = []
@@ -1471,6 +1580,7 @@ def main(argv=None):
         "replaygain_config4": rg4,
         "track2track": t2t,
         "strong_scaling": strong if world > 1 else {"note": "1 GPU: the same batch as value"},
+        "narrow_batches": narrow,
         "plan_per_batch": plan_miss,
     }
     print(json.dumps(line), flush=True)

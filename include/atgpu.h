@@ -258,6 +258,16 @@ atg_status atg_service_encode_frames(atg_service *svc, const atg_flac_options *o
    chunk c+1's upload, chunk c's encode and chunk c-1's download overlap. */
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *eng, uint64_t bytes);
 
+/* Batches atg_flac_encode_device_async keeps in flight (slots in rotation,
+   each its own device workspace): 3 (default) .. 16.  Every track's MD5 is
+   one serial hash (~12.5 ms per MiB of track on the GPU, whatever the batch
+   width), so a narrow batch -- a rank's share of a strong-scaling job --
+   needs more batches in flight to keep the chains off its step.  From 4
+   on, the chains of all batches in flight advance together, one launch per
+   enqueue on one stream, each batch's chain in n - 2 slices.  Fails
+   with ATG_ERR_INVALID while any batch or host job is unwaited. */
+atg_status atg_engine_set_inflight(atg_engine *eng, uint32_t n);
+
 /* Device-memory entry points run on the library's own non-blocking HIP
    streams: device inputs must be complete (e.g. the producing stream
    synchronized) when the call is made. */
@@ -274,16 +284,16 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
                                   uint64_t out_cap, atg_track_result *results);
 
 /* The same batch encode, enqueued: returns once the work is queued, with a
-   ticket for atg_flac_encode_wait.  The engine keeps three batches in flight
-   (each its own device workspace): batch k's MD5 chains and stream headers
-   run on their own stream while batches k+1 and k+2 are analysed, so a
-   caller that waits for ticket k after enqueueing k+2 (or k+1) overlaps
-   them.  d_pcm and d_out must stay untouched until the ticket is waited.
-   A fourth enqueue while three tickets are unwaited fails with
-   ATG_ERR_INVALID (wait the oldest first); atg_flac_encode_device takes a
-   slot too and fails the same way, and atg_flac_encode_host fails while any
-   ticket is unwaited.  A waited ticket's
-   results stay readable until its slot is reused three enqueues later, or
+   ticket for atg_flac_encode_wait.  The engine keeps D batches in flight
+   (D = 3 unless atg_engine_set_inflight says otherwise; each its own device
+   workspace): batch k's MD5 chains and stream headers run on their own
+   stream while batches k+1 .. k+D-1 are analysed, so a caller that waits
+   for ticket k after enqueueing k+D-1 overlaps them.  d_pcm and d_out must
+   stay untouched until the ticket is waited.  Enqueue number D+1 while D
+   tickets are unwaited fails with ATG_ERR_INVALID (wait the oldest first);
+   atg_flac_encode_device takes a slot too and fails the same way, and
+   atg_flac_encode_host fails while any ticket is unwaited.  A waited
+   ticket's results stay readable until its slot is reused D enqueues later, or
    until a streaming call (atg_flac_encode_frames[_batch]), which always
    takes slot 0. */
 atg_status atg_flac_encode_device_async(atg_engine *eng, const atg_flac_options *opts,

@@ -32,7 +32,8 @@ EXPORTS = (
     "atg_engine_destroy", "atg_flac_batch_bounds", "atg_flac_encode_host",
     "atg_flac_encode_host_async", "atg_flac_encode_host_wait",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
-    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_flac_encode_frames",
+    "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_engine_set_inflight",
+    "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
     "atg_flac_encode_frames_batch", "atg_service_connect", "atg_service_close",
     "atg_service_last_error", "atg_service_encode_frames",
@@ -288,6 +289,8 @@ def load_library():
         lib.atg_host_free.restype = None
         lib.atg_engine_set_host_chunk_bytes.argtypes = [P, c_u64]
         lib.atg_engine_set_host_chunk_bytes.restype = ctypes.c_int
+        lib.atg_engine_set_inflight.argtypes = [P, c_u32]
+        lib.atg_engine_set_inflight.restype = ctypes.c_int
         lib.atg_engine_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -675,6 +678,10 @@ class Engine(object):
             out.ctypes.data_as(ctypes.c_void_p), cap, ctypes.byref(nb),
             fb.ctypes.data_as(ctypes.c_void_p)))
         return out[:nb.value], fb[:n_fr]
+
+    def set_inflight(self, n):
+        """batches encode_device_async keeps in flight (3..16)"""
+        _check(self.lib, self.lib.atg_engine_set_inflight(self.handle, int(n)))
 
     def set_host_chunk_bytes(self, nbytes):
         """PCM bytes per chunk of the host-memory pipeline (encode())"""

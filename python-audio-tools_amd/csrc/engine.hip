@@ -184,6 +184,11 @@ struct EncSlot {
     DevBuf md5in;                    // the digests on the device
     hipEvent_t ev_hpcm = nullptr;    // the PCM copies are done
     std::vector<std::future<void>> hash_jobs;
+    // rolled mode (e->depth >= ATG_ROLL_MIN_DEPTH, pipelined device
+    // batches): the chain runs as roll_parts slices on the engine's MD5
+    // stream, one per later enqueue; the tail follows the last slice there
+    bool rolled = false;
+    uint32_t roll_parts = 0, roll_done = 0;
     bool busy = false;               // enqueued, not yet waited
     bool done = false;               // waited: results below are valid
     bool host = false;               // a chunk of a host-memory job
@@ -217,9 +222,20 @@ struct EncSlot {
 
 
 // batches in flight on an engine (each its own device workspace): the MD5
-// chains of a batch run ~12 ms, longer than a batch's search chain, so a
-// third slot keeps them off the critical path at normal wave priority
+// chains of a batch run ~12 ms (one serial hash per 1 MiB track, whatever
+// the batch width), longer than a wide batch's search chain, so a third slot
+// keeps them off the critical path.  A narrow batch (a rank's share of a
+// strong-scaling job: 128 tracks need ~1.2 ms of kernels) needs more
+// batches in flight to hide the same chain: atg_engine_set_inflight raises
+// the slot rotation up to kMaxSlots (default kEncSlots)
 constexpr uint64_t kEncSlots = 3;
+constexpr uint64_t kMaxSlots = 16;
+static_assert(kMaxSlots <= kRollMax, "one rolled launch covers every slot");
+// rolled MD5 from this depth on (atg_engine_set_inflight); below it every
+// slot keeps its own aux stream and the two-part split
+#ifndef ATG_ROLL_MIN_DEPTH
+#define ATG_ROLL_MIN_DEPTH 4
+#endif
 
 // one stage of the host pipeline (chunk c uses stage c % kEncSlots)
 struct HostStage {
@@ -292,7 +308,17 @@ struct atg_engine {
     // batch k on their own stream, so batch k+1's search starts beside
     // batch k's pack (ATG_PACK_STREAM; null: everything on s_main)
     hipStream_t s_pack = nullptr;
-    EncSlot slot[kEncSlots];
+    EncSlot slot[kMaxSlots];
+    uint64_t depth = kEncSlots; // slots in rotation (atg_engine_set_inflight)
+    // rolled mode: every batch's MD5 slices, tails, stream headers and
+    // result copies on s_md5 (high priority: one stream whatever the depth,
+    // instead of one aux stream per slot); the tables + LPC kernels on the
+    // default slots' aux streams in turn (a stream created after s_md5 for
+    // them landed on s_md5's hardware queue and serialised with the slices,
+    // profiles/r05_e_narrow_trace.txt); roll_q = rolled batches with
+    // slices to run, oldest first
+    hipStream_t s_md5 = nullptr;
+    std::deque<EncSlot *> roll_q;
     DevBuf windows;
     // host-memory API (atg_flac_encode_host): per pipeline stage, device
     // PCM / image / packed-image buffers and pinned host staging (used only
@@ -658,28 +684,104 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
     TrackOut *dto = (TrackOut *)sl.tout.p;
     uint32_t *derr = (uint32_t *)sl.err.p;
     hipEvent_t *ev = sl.ev;
-    if (sl.pend_split && !pl.frames_only) {
+    // a rolled batch's tail runs on the engine's MD5 stream right after its
+    // last slice; the others on the slot's aux stream
+    hipStream_t q = sl.rolled ? e->s_md5 : sl.s_aux;
+    if (sl.rolled) {
+        if (!pl.frames_only)
+            HIP_TRY(launch_track_md5_finish(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, q));
+    } else if (sl.pend_split && !pl.frames_only) {
         if (after)
-            HIP_TRY(hipStreamWaitEvent(sl.s_aux, after, 0));
-        HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, sl.s_aux));
+            HIP_TRY(hipStreamWaitEvent(q, after, 0));
+        HIP_TRY(launch_track_md5(p, sl.pend_pcm, sl.pend_fmt, dtr, dto, 1, q));
     }
-    HIP_TRY(hipEventRecord(ev[2 * 5 + 1], sl.s_aux));
+    HIP_TRY(hipEventRecord(ev[2 * 5 + 1], q));
     // headers once both the pack and the MD5 chains are done
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, sl.ev_pack, 0));
-    HIP_TRY(hipEventRecord(ev[12], sl.s_aux));
+    HIP_TRY(hipStreamWaitEvent(q, sl.ev_pack, 0));
+    HIP_TRY(hipEventRecord(ev[12], q));
     if (!pl.frames_only)
-        HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, sl.s_aux));
-    HIP_TRY(hipEventRecord(ev[13], sl.s_aux));
-    HIP_TRY(hipEventRecord(ev[15], sl.s_aux));
+        HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, q));
+    HIP_TRY(hipEventRecord(ev[13], q));
+    HIP_TRY(hipEventRecord(ev[15], q));
     if (nt)
-        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost,
-                               sl.s_aux));
+        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost, q));
     if (sl.want_fdesc && nf)
         HIP_TRY(hipMemcpyAsync(sl.fdesc_h, sl.fdesc.p, nf * sizeof(FrameDesc),
-                               hipMemcpyDeviceToHost, sl.s_aux));
-    HIP_TRY(hipMemcpyAsync(sl.err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, sl.s_aux));
-    HIP_TRY(hipEventRecord(sl.ev_done, sl.s_aux));
+                               hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipMemcpyAsync(sl.err_h, derr, sizeof(uint32_t), hipMemcpyDeviceToHost, q));
+    HIP_TRY(hipEventRecord(sl.ev_done, q));
     return ATG_OK;
+}
+
+atg_status ensure_aux_stream(EncSlot &sl);
+
+// ---- rolled mode -------------------------------------------------------------
+atg_status ensure_roll_streams(atg_engine *e)
+{
+    if (e->s_md5)
+        return ATG_OK;
+    int prio_lo = 0, prio_hi = 0;
+    HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+    HIP_TRY(hipStreamCreateWithPriority(&e->s_md5, hipStreamNonBlocking, prio_hi));
+    return ATG_OK;
+}
+
+// One rolled launch on s_md5 after `after`: every batch in roll_q advances by
+// its next slice (or, with `only`, that batch alone by all its remaining
+// slices -- a wait that cannot count on later enqueues); batches whose last
+// slice ran get their tail queued behind it and leave roll_q.
+atg_status roll_step(atg_engine *e, hipEvent_t after, EncSlot *only)
+{
+    MdRollArgs a;
+    std::memset(&a, 0, sizeof(a));
+    std::vector<EncSlot *> starting, finished;
+    uint32_t wg = 0;
+    for (EncSlot *sl : e->roll_q) {
+        if (only && sl != only)
+            continue;
+        const FlacParams &p = sl->plan->p;
+        MdRollBatch &b = a.b[a.n++];
+        b.pcm = sl->pend_pcm;
+        b.tracks = (const TrackInfo *)sl->tracks.p;
+        b.tout = (TrackOut *)sl->tout.p;
+        b.n_tracks = p.n_tracks;
+        b.channels = p.channels;
+        b.bps = p.bps;
+        b.fmt = (uint32_t)sl->pend_fmt;
+        b.wg0 = wg;
+        b.parts = sl->roll_parts;
+        b.part = sl->roll_done;
+        b.part_end = only ? sl->roll_parts : sl->roll_done + 1u;
+        wg += (p.n_tracks + 63u) / 64u;
+        if (b.part == 0)
+            starting.push_back(sl);
+        sl->roll_done = b.part_end;
+        if (sl->roll_done == sl->roll_parts)
+            finished.push_back(sl);
+    }
+    if (!a.n)
+        return ATG_OK;
+    if (after)
+        HIP_TRY(hipStreamWaitEvent(e->s_md5, after, 0));
+    for (EncSlot *sl : starting)
+        HIP_TRY(hipEventRecord(sl->ev[2 * 5], e->s_md5));
+    HIP_TRY(launch_track_md5_roll(a, e->s_md5));
+    for (EncSlot *sl : finished) {
+        e->roll_q.erase(std::find(e->roll_q.begin(), e->roll_q.end(), sl));
+        const atg_status st = batch_end(e, *sl, nullptr);
+        if (st != ATG_OK)
+            return st;
+    }
+    return ATG_OK;
+}
+
+// every stream a slot's batch may have work on
+void drain_slot(atg_engine *e, EncSlot &sl)
+{
+    (void)hipStreamSynchronize(e->s_main);
+    for (hipStream_t q : {e->s_pack, e->s_md5, sl.s_aux})
+        if (q)
+            (void)hipStreamSynchronize(q);
 }
 
 // ---- host-MD5 mode ---------------------------------------------------------
@@ -813,13 +915,28 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
         return fail(ATG_ERR_CAPACITY, "output buffer too small for this batch");
     p.n_reg_frames = (fmt == ATG_PCM_S16 && ((uintptr_t)d_pcm & 15u) == 0) ? pl.n_reg_prefix : 0u;
     HIP_TRY(hipSetDevice(e->device));
+    sl.md5_host = want_host_md5(e, pl, fmt, md5_early);
+    // rolled mode: many narrow batches in flight (atg_engine_set_inflight)
+    sl.rolled = pipelined && !md5_early && !sl.md5_host && !pl.frames_only &&
+                e->depth >= ATG_ROLL_MIN_DEPTH && track_md5_paired(p, fmt);
+    // a rolled batch's tables and LPC kernel go on one of the default slots'
+    // aux streams in turn (high priority, a hardware queue each, created
+    // before s_md5), so batch k+1's LPC kernel runs beside batch k's search
+    EncSlot &pre = sl.rolled ? e->slot[sl.ticket % kEncSlots] : sl;
+    {
+        atg_status st0 = sl.rolled ? ensure_aux_stream(pre) : ensure_aux_stream(sl);
+        if (st0 == ATG_OK && sl.rolled)
+            st0 = ensure_roll_streams(e);
+        if (st0 != ATG_OK)
+            return st0;
+    }
 #if ATG_K1_AUX
     // the tables, the LPC kernel and the MD5 chains on the slot's stream:
     // the next batches' LPC kernels run beside this batch's search and pack.
     // Whatever the LPC kernel reads is written on this stream (or waited
     // for through wait_before): nothing the caller queued on the main
     // stream is ordered before it
-    hipStream_t s_pre = sl.s_aux;
+    hipStream_t s_pre = pre.s_aux;
 #else
     hipStream_t s_pre = e->s_main;
 #endif
@@ -904,15 +1021,17 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     // chains, so they start as early as possible
     // host-MD5 mode (few long tracks, want_host_md5): the PCM copies start
     // with the batch, the hashes run on host threads, nothing on the GPU
-    sl.md5_host = want_host_md5(e, pl, fmt, md5_early);
-    const bool split_md5 = pipelined && !md5_early && !sl.md5_host &&
+    const bool split_md5 = !sl.rolled && pipelined && !md5_early && !sl.md5_host &&
                            ((fmt == ATG_PCM_S16 && p.bps == 16u) ||
                             (fmt == ATG_PCM_S32 && p.bps % 8u == 0u));
     // (md5_early: after the chunk's upload and this batch's track tables --
-    // ev_tables is recorded behind both)
-    HIP_TRY(hipStreamWaitEvent(sl.s_aux, (md5_early || sl.md5_host) ? sl.ev_tables : ev[1], 0));
-    HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
-    if (!pl.frames_only) {
+    // ev_tables is recorded behind both).  Rolled batches: below.
+    if (!sl.rolled) {
+        HIP_TRY(hipStreamWaitEvent(sl.s_aux, (md5_early || sl.md5_host) ? sl.ev_tables : ev[1],
+                                   0));
+        HIP_TRY(hipEventRecord(ev[2 * 5], sl.s_aux));
+    }
+    if (!pl.frames_only && !sl.rolled) {
         if (sl.md5_host) {
             sl.plan = plp; // the pool's tasks read the plan's tracks through the slot
             st = start_host_md5(e, sl, pl, d_pcm, fmt);
@@ -988,12 +1107,26 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     sl.end_status = ATG_OK;
     sl.end_error.clear();
     sl.want_fdesc = want_fdesc;
-    sl.end_pending = true;
+    sl.end_pending = !sl.rolled;
     sl.pend_pcm = d_pcm;
     sl.pend_fmt = fmt;
     sl.pend_out = d_out;
     sl.pend_split = split_md5;
-    if (!split_md5 && !sl.md5_host) {
+    if (sl.rolled) {
+        // the chain in depth - 2 slices: one per enqueue from this one on,
+        // all batches' slices in one launch, so the tail of batch k is queued
+        // with batch k + depth - 3's enqueue, two launches before a caller
+        // that keeps `depth` batches in flight waits for it: the MD5 stream
+        // always holds the next launch while the host waits.  The launch
+        // needs only this batch's track table (ev_tables), not its LPC
+        // kernel: at these widths the chains are the step
+        sl.roll_parts = (uint32_t)e->depth - 2u;
+        sl.roll_done = 0;
+        e->roll_q.push_back(&sl);
+        atg_status st2 = roll_step(e, sl.ev_tables, nullptr);
+        if (st2 != ATG_OK)
+            return st2;
+    } else if (!split_md5 && !sl.md5_host) {
         atg_status st2 = batch_end(e, sl, nullptr);
         if (st2 != ATG_OK)
             return st2;
@@ -1013,6 +1146,16 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
 atg_status finish_batch(atg_engine *e, EncSlot &sl)
 {
     HIP_TRY(hipSetDevice(e->device));
+    // a rolled batch with slices left (no later enqueue ran them): advance
+    // every rolled batch together until this one is through -- the batches
+    // behind it then drain concurrently rather than one after another
+    while (sl.rolled && sl.roll_done < sl.roll_parts) {
+        atg_status st = roll_step(e, nullptr, nullptr);
+        if (st != ATG_OK) {
+            drain_slot(e, sl);
+            return st;
+        }
+    }
     if (sl.end_pending && sl.md5_host) {
         atg_status st = finish_host_md5(sl);
         if (st != ATG_OK) {
@@ -1031,10 +1174,7 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
     }
     if (sl.end_status != ATG_OK) {
         // ev_done was never recorded: drain the slot's streams, report the error
-        (void)hipStreamSynchronize(e->s_main);
-        if (e->s_pack)
-            (void)hipStreamSynchronize(e->s_pack);
-        (void)hipStreamSynchronize(sl.s_aux);
+        drain_slot(e, sl);
         return fail(sl.end_status, sl.end_error);
     }
     HIP_TRY(hipEventSynchronize(sl.ev_done));
@@ -1166,12 +1306,10 @@ atg_status ensure_host_streams(atg_engine *e)
 // the caller must wait the oldest ticket first, as with the decoder
 atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 {
-    EncSlot &sl = e->slot[e->next_ticket % kEncSlots];
+    EncSlot &sl = e->slot[e->next_ticket % e->depth];
     if (sl.busy)
-        return fail(ATG_ERR_INVALID, "three encode batches already in flight: wait for the oldest");
-    atg_status st = ensure_aux_stream(sl);
-    if (st != ATG_OK)
-        return st;
+        return fail(ATG_ERR_INVALID, "as many encode batches in flight as the engine has slots "
+                                     "(atg_engine_set_inflight): wait for the oldest");
     ticket = e->next_ticket++;
     sl.ticket = ticket;
     sl.done = false;
@@ -1182,7 +1320,7 @@ atg_status take_slot(atg_engine *e, EncSlot *&out, uint64_t &ticket)
 // results of ticket t (waits if still running)
 atg_status wait_ticket(atg_engine *e, uint64_t t, EncSlot *&out)
 {
-    EncSlot &sl = e->slot[t % kEncSlots];
+    EncSlot &sl = e->slot[t % e->depth];
     if (sl.ticket != t || (!sl.busy && !sl.done))
         return fail(ATG_ERR_INVALID, "unknown or expired encode ticket");
     if (sl.busy) {
@@ -1461,8 +1599,10 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
     // process per track under track2track) holds two streams, and 8 such
     // processes run 49.8 k frames/s against 17.6 k
     if (!(flags & ATG_ENGINE_STREAMING)) {
-        for (EncSlot &sl : e->slot)
-            if (ensure_aux_stream(sl) != ATG_OK)
+        // the default rotation's aux streams; more slots (set_inflight) run
+        // rolled, on two engine streams created on first use
+        for (uint64_t k = 0; k < kEncSlots; ++k)
+            if (ensure_aux_stream(e->slot[k]) != ATG_OK)
                 return ATG_ERR_DEVICE;
         if (ensure_host_streams(e) != ATG_OK)
             return ATG_ERR_DEVICE;
@@ -1497,8 +1637,9 @@ void atg_engine_destroy(atg_engine *e)
         return;
     (void)hipSetDevice(e->device);
     (void)hipStreamSynchronize(e->s_main);
-    if (e->s_pack)
-        (void)hipStreamSynchronize(e->s_pack);
+    for (hipStream_t q : {e->s_pack, e->s_md5})
+        if (q)
+            (void)hipStreamSynchronize(q);
     for (EncSlot &sl : e->slot) {
         for (std::future<void> &f : sl.hash_jobs) // a batch never waited
             f.wait();
@@ -1547,8 +1688,9 @@ void atg_engine_destroy(atg_engine *e)
     e->windows.release();
     if (e->ev_win)
         (void)hipEventDestroy(e->ev_win);
-    if (e->s_pack)
-        (void)hipStreamDestroy(e->s_pack);
+    for (hipStream_t q : {e->s_pack, e->s_md5})
+        if (q)
+            (void)hipStreamDestroy(q);
     (void)hipStreamDestroy(e->s_main);
     delete e;
 }
@@ -1594,10 +1736,10 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
                        !e->sync_call);
     if (st != ATG_OK) {
         // nothing of this batch may be relied on: drain what was queued
-        (void)hipStreamSynchronize(e->s_main);
-        if (e->s_pack)
-            (void)hipStreamSynchronize(e->s_pack);
-        (void)hipStreamSynchronize(sl->s_aux);
+        drain_slot(e, *sl);
+        auto it = std::find(e->roll_q.begin(), e->roll_q.end(), sl);
+        if (it != e->roll_q.end())
+            e->roll_q.erase(it);
         sl->uploaded = nullptr;
         sl->ticket = 0;
         sl->end_pending = false;
@@ -1880,7 +2022,7 @@ atg_status atg_flac_encode_frames_batch(atg_engine *e, const atg_flac_options *o
     // a synchronous call (no slot busy, checked above) always takes slot 0:
     // one aux stream for a streaming process's whole life.  The slot's
     // earlier results are gone with it (atgpu.h)
-    e->next_ticket += (kEncSlots - e->next_ticket % kEncSlots) % kEncSlots;
+    e->next_ticket += (e->depth - e->next_ticket % e->depth) % e->depth;
     EncSlot *sl = nullptr;
     uint64_t ticket = 0;
     st = take_slot(e, sl, ticket);
@@ -1982,6 +2124,25 @@ uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_fr
     if (make_plan(opts, &tr, 1, channels, bps, 44100, pl, true, 0) != ATG_OK)
         return 0;
     return pl.out_bytes;
+}
+
+atg_status atg_engine_set_inflight(atg_engine *e, uint32_t n)
+{
+    ATG_HANDLE_LOCK(e);
+    if (!e || n < kEncSlots || n > kMaxSlots)
+        return fail(ATG_ERR_INVALID, "in-flight batches must be 3..16");
+    for (EncSlot &sl : e->slot)
+        if (sl.busy)
+            return fail(ATG_ERR_INVALID, "an encode batch is in flight: wait for it first");
+    if (!e->hjobs.empty())
+        return fail(ATG_ERR_INVALID, "a host job is in flight: wait for it first");
+    // tickets map to slots by ticket % depth: start the new rotation clean
+    for (EncSlot &sl : e->slot) {
+        sl.ticket = 0;
+        sl.done = false;
+    }
+    e->depth = n;
+    return ATG_OK;
 }
 
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)

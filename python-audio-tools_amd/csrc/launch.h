@@ -79,6 +79,25 @@ hipError_t upload_crc_tables(const uint16_t *adv /*[24][16]*/,
 // md5.hip
 hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                             const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s);
+// rolled chains (engine rolled mode): one launch advances up to kRollMax
+// batches' whole-block chains by their own slices (md5.hip k_track_md5_roll)
+constexpr uint32_t kRollMax = 16;
+struct MdRollBatch {
+    const void *pcm;
+    const TrackInfo *tracks;
+    TrackOut *tout;
+    uint32_t n_tracks, channels, bps, fmt; // fmt: 0 = ATG_PCM_S16, 1 = ATG_PCM_S32
+    uint32_t wg0;                          // first workgroup of this batch
+    uint32_t part, part_end, parts;        // slice [part, part_end) of `parts`
+};
+struct MdRollArgs {
+    uint32_t n;
+    MdRollBatch b[kRollMax];
+};
+bool track_md5_paired(const FlacParams &p, int fmt);
+hipError_t launch_track_md5_roll(const MdRollArgs &a, hipStream_t s);
+hipError_t launch_track_md5_finish(const FlacParams &p, const void *pcm, int fmt,
+                                   const TrackInfo *tracks, TrackOut *tout, hipStream_t s);
 // MD5 of n byte streams base[off[t] .. off[t] + len[t]) (off 64-aligned),
 // digests to md5[16 t] (the decoder's STREAMINFO check)
 hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint64_t *len,

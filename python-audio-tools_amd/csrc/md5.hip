@@ -703,6 +703,112 @@ __global__ __launch_bounds__(64) void k_track_md5(FlacParams p, const T *__restr
     md5_put(tout[t].md5, h);
 }
 
+// Rolled chains (engine "rolled" mode, many narrow batches in flight): one
+// launch advances the whole-block chains of up to kRollMax batches at once,
+// each by its own slice [full * part / parts, full * part_end / parts) of
+// every track's blocks (int32 containers: of its sample groups), from the
+// state the previous slice left in tout[t].md5.  A batch's chain thus runs
+// as `parts` slices, one per later batch's enqueue, and every batch in
+// flight shares ONE launch per step on one stream -- instead of one long
+// kernel per batch, each on a stream of its own, whose chains serialise
+// once the batches in flight outnumber the hardware queues.  Workgroup w
+// belongs to the batch whose [wg0, wg0 + ceil(n_tracks / 64)) holds it.
+__global__ __launch_bounds__(128) void k_track_md5_roll(MdRollArgs a)
+{
+    uint32_t k = 0;
+    while (k + 1u < a.n && blockIdx.x >= a.b[k + 1].wg0)
+        ++k;
+    const MdRollBatch &B = a.b[k];
+    __shared__ Md5Pair pair_lds;
+    const uint32_t t = (blockIdx.x - B.wg0) * 64u + (threadIdx.x & 63u);
+    const bool valid = t < B.n_tracks;
+    const TrackInfo ti = B.tracks[valid ? t : 0u];
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (B.fmt == 0) {
+        // S16 at 16 bits, 16-byte aligned (md5_track_raw)
+        const int16_t *s = (const int16_t *)B.pcm + ti.pcm_start * B.channels;
+        const uint64_t full = ti.pcm_frames * B.channels * 2u / 64u;
+        const bool raw = valid && B.bps == 16u && (((uintptr_t)s) & 15u) == 0 &&
+                         full < (1ull << 32);
+        const uint32_t b0 = raw ? (uint32_t)(full * B.part / B.parts) : 0u;
+        const uint32_t b1 = raw ? (uint32_t)(full * B.part_end / B.parts) : 0u;
+        const uint32_t n = b1 - b0;
+        const uint32_t nbmax = wave_max_u32(n);
+        if (!nbmax)
+            return;
+        if (b0 && threadIdx.x < 64u)
+            md5_get(B.tout[t].md5, h);
+        md5_vgpr_192();
+        md5_pair_init(pair_lds);
+        md5_pair_blocks((const uint4 *)s + (size_t)b0 * 4u, n, nbmax, h, pair_lds);
+        if (threadIdx.x < 64u && n)
+            md5_put(B.tout[t].md5, h);
+        return;
+    }
+    const uint32_t bb = B.bps / 8u;
+    const int32_t *s = (const int32_t *)B.pcm + ti.pcm_start * B.channels;
+    const uint32_t G = bb == 2u ? 32u : 64u, BPG = bb == 3u ? 3u : 1u, Q = G / 4u;
+    const uint64_t groups64 = valid && (((uintptr_t)s) & 15u) == 0
+                                  ? ti.pcm_frames * B.channels / G : 0u;
+    const uint32_t groups = groups64 * BPG < (1ull << 32) ? (uint32_t)groups64 : 0u;
+    const uint32_t g0 = (uint32_t)((uint64_t)groups * B.part / B.parts);
+    const uint32_t g1 = (uint32_t)((uint64_t)groups * B.part_end / B.parts);
+    const uint32_t n = (g1 - g0) * BPG;
+    const uint32_t nbmax = wave_max_u32(n);
+    if (!nbmax)
+        return;
+    if (g0 && threadIdx.x < 64u)
+        md5_get(B.tout[t].md5, h);
+    md5_vgpr_192();
+    md5_pair_init(pair_lds);
+    const uint4 *q = (const uint4 *)s + (size_t)g0 * Q;
+    if (bb == 3u)
+        md5_pair_blocks_s32<3>(q, n, nbmax, h, pair_lds);
+    else if (bb == 2u)
+        md5_pair_blocks_s32<2>(q, n, nbmax, h, pair_lds);
+    else
+        md5_pair_blocks_s32<1>(q, n, nbmax, h, pair_lds);
+    if (threadIdx.x < 64u && n)
+        md5_put(B.tout[t].md5, h);
+}
+
+// true when launch_track_md5 would hash this batch's whole blocks on wave
+// pairs (the formats the rolled mode takes)
+bool track_md5_paired(const FlacParams &p, int fmt)
+{
+    const uint32_t bb = p.bps / 8u;
+    return (fmt == 0 && p.bps == 16u) || (fmt == 1 && p.bps % 8u == 0u && bb >= 1u && bb <= 3u);
+}
+
+hipError_t launch_track_md5_roll(const MdRollArgs &a, hipStream_t s)
+{
+    uint32_t wgs = 0;
+    for (uint32_t k = 0; k < a.n; ++k)
+        wgs = a.b[k].wg0 + (a.b[k].n_tracks + 63u) / 64u;
+    if (!wgs)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_track_md5_roll, dim3(wgs), dim3(128), 0, s, a);
+    return hipGetLastError();
+}
+
+// the finishing kernel alone: every track's tail + padding after its rolled
+// whole-block chain (the lane-per-track path for what the pairs skipped)
+hipError_t launch_track_md5_finish(const FlacParams &p, const void *pcm, int fmt,
+                                   const TrackInfo *tracks, TrackOut *tout, hipStream_t s)
+{
+    if (!p.n_tracks)
+        return hipSuccess;
+    const dim3 grid((p.n_tracks + 63u) / 64u);
+    const int paired = track_md5_paired(p, fmt);
+    if (fmt == 0)
+        hipLaunchKernelGGL((k_track_md5<int16_t>), grid, dim3(64), 0, s, p,
+                           (const int16_t *)pcm, tracks, tout, paired);
+    else
+        hipLaunchKernelGGL((k_track_md5<int32_t>), grid, dim3(64), 0, s, p,
+                           (const int32_t *)pcm, tracks, tout, paired);
+    return hipGetLastError();
+}
+
 // MD5 of a plain byte stream per lane (the decoder hashes the little-endian
 // PCM bytes K5 of flac_decode.hip wrote; streams start 64-byte aligned):
 // whole blocks on the wave pair, state to md5[16 t]

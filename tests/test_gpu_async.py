@@ -144,3 +144,80 @@ def test_async_batches_new_frame_lengths_fresh_engine():
                for (d_pcm, d_out, cap), (_, tracks, _) in zip(dev, batches)]
     for i, t in enumerate(tickets):
         _check(eng, torch, dev[i][1], eng.wait(t), batches[i][2], "fresh-engine batch %d" % i)
+
+
+def _batch32(seed, shapes, bps):
+    """int32 containers of `bps`-bit samples (the rolled s32 path)"""
+    rng = np.random.default_rng(seed)
+    parts, tracks, per, pos = [], [], [], 0
+    for gap, n in shapes:
+        if gap:
+            parts.append(rng.integers(-99, 99, 2 * gap).astype(np.int32))
+            pos += gap
+        p = signals.make(["noise", "tone", "chirp"][len(per) % 3], n, 2, bps,
+                         seed=int(rng.integers(1 << 30))) if n else np.zeros(0, np.int32)
+        parts.append(p.astype(np.int32))
+        tracks.append((pos, n))
+        per.append(p.astype(np.int32))
+        pos += n
+    return np.concatenate(parts), tracks, per
+
+
+@pytest.mark.parametrize("depth", [4, 8, 16])
+def test_rolled_md5_many_in_flight_match_port(depth):
+    """atg_engine_set_inflight(depth >= 4): every batch's MD5 chain runs in
+    depth - 2 slices on the engine's MD5 stream, all batches' slices in one
+    launch per enqueue (md5.hip k_track_md5_roll).  Batches of 16-bit and
+    24-bit (int32 container) PCM, mixed shapes incl. unaligned and
+    sub-block tracks, more batches than slots, waited oldest first and out
+    of order: every image equals the port's; a (depth + 1)-th unwaited
+    enqueue is refused; the default depth comes back"""
+    import torch
+    from audiotools import _atgpu
+    eng = _atgpu.Engine(0)
+    eng.set_inflight(depth)
+    opts = _atgpu.make_options(**FLAC8)
+    jobs = []
+    for i in range(depth + 3):
+        if i % 3 == 2:
+            pcm, tracks, per = _batch32(500 + i, SHAPES[i % 3], 24)
+            fmt, bps = _atgpu.PCM_S32, 24
+        else:
+            pcm, tracks, per = _batch(500 + i, SHAPES[i % 3])
+            fmt, bps = _atgpu.PCM_S16, 16
+        _, cap = eng.bounds(opts, tracks, 2, bps)
+        jobs.append((_dev(torch, pcm), torch.empty(cap, dtype=torch.uint8, device="cuda"), cap,
+                     tracks, per, fmt, bps))
+    torch.cuda.synchronize()
+
+    def check(j, res, label):
+        d_pcm, d_out, cap, tracks, per, fmt, bps = j
+        host = d_out.cpu().numpy()
+        for t, (r, p) in enumerate(zip(res, per)):
+            want, _ = oracle_port.encode(p, 2, bps, 44100, **FLAC8)
+            got = host[r.out_offset:r.out_offset + r.bytes].tobytes()
+            assert got == want, "%s track %d" % (label, t)
+
+    def enq(j):
+        d_pcm, d_out, cap, tracks, per, fmt, bps = j
+        return eng.encode_device_async(opts, d_pcm.data_ptr(), fmt, tracks, 2, bps, 44100,
+                                       d_out.data_ptr(), cap)
+
+    pending = []
+    for i, j in enumerate(jobs):
+        pending.append((i, enq(j)))
+        if len(pending) == depth:
+            k, t = pending.pop(0)
+            check(jobs[k], eng.wait(t), "rolled batch %d" % k)
+    # the slot contract at this depth
+    with pytest.raises(_atgpu.ATGError):
+        while True:
+            pending.append((0, enq(jobs[0])))
+    # drain newest first: waits that cannot count on later enqueues
+    for k, t in reversed(pending):
+        check(jobs[k], eng.wait(t), "rolled batch %d (drain)" % k)
+    eng.set_inflight(3)
+    ts = [enq(jobs[k]) for k in range(3)]
+    for k, t in enumerate(ts):
+        check(jobs[k], eng.wait(t), "depth 3 again, batch %d" % k)
+    eng.close()
