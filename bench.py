@@ -94,8 +94,9 @@ def parse_args(argv=None):
                     help="track2track leg: 64-frame WAV files, one process each")
     ap.add_argument("--no-rg4", action="store_true", help="skip the config-4 ReplayGain leg")
     ap.add_argument("--rg4-seconds", type=int, default=10)
-    ap.add_argument("--dec-inflight", type=int, default=3,
-                    help="decode batches in flight (the decoder's slot count)")
+    ap.add_argument("--dec-inflight", type=int, default=8,
+                    help="decode batches in flight (the decoder's slot count; from 4 on the "
+                         "MD5 hashes are rolled, atg_decoder_set_inflight)")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -317,6 +318,9 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     PCM (lossless round trip).  Returns the JSON object."""
     from audiotools import _atgpu
     dec = _atgpu.Decoder(int(os.environ.get("LOCAL_RANK", "0")))
+    if args.dec_inflight > 3:
+        # rolled MD5 hashes (atg_decoder_set_inflight)
+        dec.set_inflight(args.dec_inflight)
     tracks = []
     for r in res:
         si = _atgpu.StreamInfo()
@@ -395,8 +399,12 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
                      "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
                      "alg_bytes_per_launch": alg[dom], "launch_ms": round(kernels[dom], 4),
                      "selection": "longest kernel on the decoder (critical-path) stream"},
-        "pipelining": "%d batches in flight: restore, emit and MD5 of batch k on its slot's "
-                      "stream beside the scan and parse of batch k+1" % args.dec_inflight,
+        "pipelining": ("%d batches in flight: restore, emit and MD5 of batch k on its slot's "
+                       "stream beside the scan and parse of batch k+1" % args.dec_inflight)
+                      if args.dec_inflight <= 3 else
+                      ("%d batches in flight: restore and emit beside the next batch's scan and "
+                       "parse, every batch's MD5 hashes advanced together in %d slices (rolled)"
+                       % (args.dec_inflight, args.dec_inflight - 2)),
         "step_hbm": {"alg_bytes_per_step": step_alg,
                      "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)},
         "verified_md5_round_trip": ok,

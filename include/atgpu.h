@@ -434,6 +434,14 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
                                   atg_flac_dec_result *results, const int32_t **d_pcm,
                                   uint64_t *total_samples);
 
+/* Decode batches atg_flac_decode_device_async keeps in flight: 3 (default)
+   .. 8.  A batch's STREAMINFO MD5 checks are serial hashes (~12 ms per 1 MB
+   of decoded PCM whatever the batch width); from 4 on, the hashes of every
+   batch in flight advance together, one launch per enqueue on one stream,
+   each batch's in n - 2 slices.  Fails while a batch is unwaited; the last
+   waited batch's buffers are no longer fetchable afterwards. */
+atg_status atg_decoder_set_inflight(atg_decoder *dec, uint32_t n);
+
 /* Asynchronous form of atg_flac_decode_device (three batches in flight):
    the scan, parse and frame walk run on the decoder's stream (two host
    round trips for the counts), then the restore, emit and per-track MD5 on

@@ -42,7 +42,7 @@ EXPORTS = (
     "atg_flac_read_metadata", "atg_decoder_create", "atg_decoder_destroy",
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
     "atg_flac_decode_device", "atg_flac_decode_device_async", "atg_flac_decode_wait",
-    "atg_decoder_kernel_times",
+    "atg_decoder_kernel_times", "atg_decoder_set_inflight",
     "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
@@ -329,6 +329,8 @@ def load_library():
         lib.atg_flac_decode_wait.argtypes = [
             P, c_u64, ctypes.POINTER(DecResult), ctypes.POINTER(P), ctypes.POINTER(c_u64)]
         lib.atg_flac_decode_wait.restype = ctypes.c_int
+        lib.atg_decoder_set_inflight.argtypes = [P, c_u32]
+        lib.atg_decoder_set_inflight.restype = ctypes.c_int
         lib.atg_decoder_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -789,6 +791,10 @@ class Decoder(object):
             self.close()
         except Exception:
             pass
+
+    def set_inflight(self, n):
+        """decode batches decode_device_async keeps in flight (3..8)"""
+        self._check(self.lib.atg_decoder_set_inflight(self.handle, int(n)))
 
     def decode(self, data, tracks, fetch_pcm=True):
         """decode a batch in host memory.  data: bytes-like holding every

@@ -1668,10 +1668,15 @@ struct DBuf {
 // free again only after them (config 2, 30 steps: 14.4 ms per step with
 // two slots, 11.1 with three, 13.4 with four -- more batches in flight only
 // add contention; profiles/r03_f_decode_slots.txt).
-#ifndef ATG_DEC_SLOTS
-#define ATG_DEC_SLOTS 3
-#endif
-constexpr int kDecSlots = ATG_DEC_SLOTS;
+//
+// atg_decoder_set_inflight raises the rotation up to kDecMaxSlots: from 4
+// slots on the batches' MD5 chains are rolled (as the encoder's, md5.hip
+// k_bytes_md5_roll): every batch in flight advances by one slice per
+// enqueue, in ONE launch on the decoder's MD5 stream, so more batches in
+// flight no longer queue their chains behind one another on shared hardware
+// queues (the 13.4 ms at four slots above).
+constexpr int kDecSlots = 3;
+constexpr int kDecMaxSlots = 8;
 struct DecSlot {
     DBuf pcm, bytes, md5, md5meta;
     DBuf tracks, frames, jobs, warm, rows, meta; // the restore's tables and scratch
@@ -1688,6 +1693,10 @@ struct DecSlot {
     uint64_t total_samples = 0, total_frames = 0;
     uint64_t ticket = 0;
     bool busy = false;
+    // rolled mode: the chains in roll_parts slices on d->s_roll
+    bool rolled = false;
+    uint32_t roll_parts = 0, roll_done = 0;
+    uint32_t n_md5 = 0; // streams hashed (the batch's track count)
 };
 
 struct atg_decoder {
@@ -1698,7 +1707,10 @@ struct atg_decoder {
     bool have_times = false;
     DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, hits, segs;
     std::vector<ScanSeg> segs_h; // the scan's segments (upload source)
-    DecSlot slot[kDecSlots];
+    DecSlot slot[kDecMaxSlots];
+    int depth = kDecSlots;          // slots in rotation (atg_decoder_set_inflight)
+    hipStream_t s_roll = nullptr;   // rolled mode: every batch's MD5 slices and tails
+    std::vector<DecSlot *> roll_q;  // rolled batches with slices to run, oldest first
     uint64_t next_ticket = 1;
     int last = -1; // slot of the last waited batch (decode_fetch)
 };
@@ -1894,7 +1906,10 @@ atg_status atg_decoder_create(int device, atg_decoder **out)
     d->device = device;
     DHIP(hipStreamCreateWithFlags(&d->s, hipStreamNonBlocking));
     for (DecSlot &sl : d->slot) {
-        DHIP(hipStreamCreateWithFlags(&sl.s_md5, hipStreamNonBlocking));
+        // the default rotation's streams; rolled mode runs the restores of
+        // every slot on these in turn and the chains on s_roll
+        if (&sl - d->slot < kDecSlots)
+            DHIP(hipStreamCreateWithFlags(&sl.s_md5, hipStreamNonBlocking));
         for (auto &e : sl.ev)
             DHIP(hipEventCreate(&e));
         DHIP(hipEventCreateWithFlags(&sl.ev_chain, hipEventDisableTiming));
@@ -1913,8 +1928,11 @@ void atg_decoder_destroy(atg_decoder *d)
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
                     &d->recs, &d->hits, &d->segs})
         b->release();
+    if (d->s_roll)
+        (void)hipStreamSynchronize(d->s_roll);
     for (DecSlot &sl : d->slot) {
-        (void)hipStreamSynchronize(sl.s_md5);
+        if (sl.s_md5)
+            (void)hipStreamSynchronize(sl.s_md5);
         for (DBuf *b : {&sl.pcm, &sl.bytes, &sl.md5, &sl.md5meta, &sl.tracks, &sl.frames, &sl.jobs,
                         &sl.warm, &sl.rows, &sl.meta})
             b->release();
@@ -1924,13 +1942,74 @@ void atg_decoder_destroy(atg_decoder *d)
         (void)hipEventDestroy(sl.ev_done);
         if (sl.md5_h)
             (void)hipHostFree(sl.md5_h);
-        (void)hipStreamDestroy(sl.s_md5);
+        if (sl.s_md5)
+            (void)hipStreamDestroy(sl.s_md5);
     }
+    if (d->s_roll)
+        (void)hipStreamDestroy(d->s_roll);
     (void)hipStreamDestroy(d->s);
     delete d;
 }
 
 } // extern "C"
+
+// the tail of a rolled batch on s_roll: tails + padding + digests, the
+// digests to the host, done
+static atg_status dec_roll_tail(atg_decoder *d, DecSlot &sl)
+{
+    const uint32_t n = sl.n_md5;
+    DHIP(launch_bytes_md5_finish((const uint8_t *)sl.bytes.p, (const uint64_t *)sl.md5meta.p,
+                                 (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p,
+                                 d->s_roll));
+    DHIP(hipEventRecord(sl.ev[7], d->s_roll));
+    if (n)
+        DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
+                            d->s_roll));
+    DHIP(hipEventRecord(sl.ev_done, d->s_roll));
+    return ATG_OK;
+}
+
+// one rolled launch on s_roll after `after`: every rolled batch in flight
+// advances by one slice; finished batches get their tails
+static atg_status dec_roll_step(atg_decoder *d, hipEvent_t after)
+{
+    MdBytesRollArgs a;
+    std::memset(&a, 0, sizeof(a));
+    std::vector<DecSlot *> starting, finished;
+    uint32_t wg = 0;
+    for (DecSlot *sl : d->roll_q) {
+        MdBytesRoll &b = a.b[a.n++];
+        b.base = (const uint8_t *)sl->bytes.p;
+        b.off = (const uint64_t *)sl->md5meta.p;
+        b.len = (const uint64_t *)sl->md5meta.p + sl->n_md5;
+        b.md5 = (uint8_t *)sl->md5.p;
+        b.n = sl->n_md5;
+        b.wg0 = wg;
+        b.parts = sl->roll_parts;
+        b.part = sl->roll_done;
+        b.part_end = sl->roll_done + 1u;
+        wg += (sl->n_md5 + 63u) / 64u;
+        if (b.part == 0)
+            starting.push_back(sl);
+        sl->roll_done = b.part_end;
+        if (sl->roll_done == sl->roll_parts)
+            finished.push_back(sl);
+    }
+    if (!a.n)
+        return ATG_OK;
+    if (after)
+        DHIP(hipStreamWaitEvent(d->s_roll, after, 0));
+    for (DecSlot *sl : starting)
+        DHIP(hipEventRecord(sl->ev[6], d->s_roll));
+    DHIP(launch_bytes_md5_roll(a, d->s_roll));
+    for (DecSlot *sl : finished) {
+        d->roll_q.erase(std::find(d->roll_q.begin(), d->roll_q.end(), sl));
+        const atg_status st = dec_roll_tail(d, *sl);
+        if (st != ATG_OK)
+            return st;
+    }
+    return ATG_OK;
+}
 
 // Enqueue the device-resident decode of a batch on slot `sl`: scan ->
 // parse -> chain (two host round trips for the counts) on the decoder
@@ -2113,7 +2192,10 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
                            (uint2 *)sl.jobs.p);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(sl.ev_chain, s));
-    hipStream_t ss = sl.s_md5;
+    // the restore / emit stream: the slot's own, or in rolled mode the
+    // default slots' streams in turn
+    sl.rolled = d->depth > kDecSlots;
+    hipStream_t ss = sl.rolled ? d->slot[sl.ticket % kDecSlots].s_md5 : sl.s_md5;
     DHIP(hipStreamWaitEvent(ss, sl.ev_chain, 0));
     DHIP(hipEventRecord(ev[3], ss));
     if (jb)
@@ -2152,7 +2234,22 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     }
     if (n)
         DHIP(hipMemcpyAsync(sl.md5meta.p, sl.md5_meta.data(), sizeof(uint64_t) * 2 * n,
-                            hipMemcpyHostToDevice, sl.s_md5));
+                            hipMemcpyHostToDevice, ss));
+    sl.n_md5 = n;
+    if (sl.rolled) {
+        // the chain in depth - 2 slices, one per enqueue, all batches' in one
+        // launch on s_roll once this batch's bytes are written
+        DHIP(hipEventRecord(ev[5], ss));
+        if (!d->s_roll) {
+            int prio_lo = 0, prio_hi = 0;
+            DHIP(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
+            DHIP(hipStreamCreateWithPriority(&d->s_roll, hipStreamNonBlocking, prio_hi));
+        }
+        sl.roll_parts = (uint32_t)d->depth - 2u;
+        sl.roll_done = 0;
+        d->roll_q.push_back(&sl);
+        return dec_roll_step(d, ev[5]);
+    }
     DHIP(hipEventRecord(ev[6], sl.s_md5));
     DHIP(launch_bytes_md5((const uint8_t *)sl.bytes.p, (const uint64_t *)sl.md5meta.p,
                           (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p, sl.s_md5));
@@ -2167,6 +2264,12 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
 // wait for slot `sl`'s batch and fill its results
 static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result *res)
 {
+    // a rolled batch with slices left: advance every rolled batch together
+    while (sl.rolled && sl.roll_done < sl.roll_parts) {
+        const atg_status st = dec_roll_step(d, nullptr);
+        if (st != ATG_OK)
+            return st;
+    }
     DHIP(hipEventSynchronize(sl.ev_done));
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
     // emit, md5, total (scan start -> md5 end)
@@ -2212,7 +2315,7 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
 static atg_status take_dec_slot(atg_decoder *d, DecSlot **out)
 {
     DecSlot *sl = &d->slot[0];
-    for (int k = 1; k < kDecSlots; ++k)
+    for (int k = 1; k < d->depth; ++k)
         if (d->slot[k].ticket < sl->ticket)
             sl = &d->slot[k];
     if (sl->busy)
@@ -2359,6 +2462,19 @@ atg_status atg_flac_decode_fetch(atg_decoder *d, int32_t *pcm, uint64_t pcm_cap,
         if (frame_block_sizes)
             frame_block_sizes[i] = fr[i].bs;
     }
+    return ATG_OK;
+}
+
+atg_status atg_decoder_set_inflight(atg_decoder *d, uint32_t n)
+{
+    ATG_HANDLE_LOCK(d);
+    if (!d || n < (uint32_t)kDecSlots || n > (uint32_t)kDecMaxSlots)
+        return dfail(ATG_ERR_INVALID, "decode batches in flight must be 3..8");
+    for (DecSlot &sl : d->slot)
+        if (sl.busy)
+            return dfail(ATG_ERR_INVALID, "a decode batch is in flight: wait for it first");
+    d->depth = (int)n;
+    d->last = -1; // the oldest-slot rotation starts over
     return ATG_OK;
 }
 

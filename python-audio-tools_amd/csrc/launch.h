@@ -95,6 +95,20 @@ struct MdRollArgs {
     MdRollBatch b[kRollMax];
 };
 bool track_md5_paired(const FlacParams &p, int fmt);
+// the decoder's rolled byte-stream chains (md5.hip k_bytes_md5_roll)
+struct MdBytesRoll {
+    const uint8_t *base;
+    const uint64_t *off, *len;
+    uint8_t *md5;
+    uint32_t n, wg0, part, part_end, parts;
+};
+struct MdBytesRollArgs {
+    uint32_t n;
+    MdBytesRoll b[kRollMax];
+};
+hipError_t launch_bytes_md5_roll(const MdBytesRollArgs &a, hipStream_t s);
+hipError_t launch_bytes_md5_finish(const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                                   uint32_t n, uint8_t *md5, hipStream_t s);
 hipError_t launch_track_md5_roll(const MdRollArgs &a, hipStream_t s);
 hipError_t launch_track_md5_finish(const FlacParams &p, const void *pcm, int fmt,
                                    const TrackInfo *tracks, TrackOut *tout, hipStream_t s);

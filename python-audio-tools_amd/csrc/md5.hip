@@ -872,6 +872,61 @@ __global__ __launch_bounds__(64) void k_bytes_md5(const uint8_t *__restrict__ ba
     md5_put(md5 + 16u * t, h);
 }
 
+// Rolled byte-stream chains (decoder rolled mode, atg_decoder_set_inflight):
+// as k_track_md5_roll, one launch advances every batch in flight by its own
+// slice [full * part / parts, full * part_end / parts) of each stream's
+// whole blocks, from the state the previous slice left in md5[16 t]
+__global__ __launch_bounds__(128) void k_bytes_md5_roll(MdBytesRollArgs a)
+{
+    uint32_t k = 0;
+    while (k + 1u < a.n && blockIdx.x >= a.b[k + 1].wg0)
+        ++k;
+    const MdBytesRoll &B = a.b[k];
+    __shared__ Md5Pair pair_lds;
+    const uint32_t t = (blockIdx.x - B.wg0) * 64u + (threadIdx.x & 63u);
+    const bool valid = t < B.n;
+    const uint64_t full = valid ? B.len[t] / 64u : 0u;
+    const bool pair = full < (1ull << 32);
+    const uint32_t b0 = pair ? (uint32_t)(full * B.part / B.parts) : 0u;
+    const uint32_t b1 = pair ? (uint32_t)(full * B.part_end / B.parts) : 0u;
+    const uint32_t n = b1 - b0;
+    const uint32_t nbmax = wave_max_u32(n);
+    if (!nbmax)
+        return;
+    uint32_t h[4] = {0x67452301u, 0xefcdab89u, 0x98badcfeu, 0x10325476u};
+    if (b0 && threadIdx.x < 64u)
+        md5_get(B.md5 + 16u * t, h);
+    // a SIMD to itself, as k_bytes_md5_pair (192 VGPRs, sharing SIMDs with
+    // the parse and restore waves, measured the same: profiles/r05_dec_depth.json)
+    asm volatile("" ::: "v255", "a255");
+    md5_pair_init(pair_lds);
+    md5_pair_blocks((const uint4 *)(B.base + B.off[valid ? t : 0u]) + (size_t)b0 * 4u, n, nbmax, h,
+                    pair_lds);
+    if (threadIdx.x < 64u && n)
+        md5_put(B.md5 + 16u * t, h);
+}
+
+hipError_t launch_bytes_md5_roll(const MdBytesRollArgs &a, hipStream_t s)
+{
+    uint32_t wgs = 0;
+    for (uint32_t k = 0; k < a.n; ++k)
+        wgs = a.b[k].wg0 + (a.b[k].n + 63u) / 64u;
+    if (!wgs)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_bytes_md5_roll, dim3(wgs), dim3(128), 0, s, a);
+    return hipGetLastError();
+}
+
+// the finishing kernel alone (tails, padding, streams the pairs skipped)
+hipError_t launch_bytes_md5_finish(const uint8_t *base, const uint64_t *off, const uint64_t *len,
+                                   uint32_t n, uint8_t *md5, hipStream_t s)
+{
+    if (!n)
+        return hipSuccess;
+    hipLaunchKernelGGL(k_bytes_md5, dim3((n + 63u) / 64u), dim3(64), 0, s, base, off, len, n, md5);
+    return hipGetLastError();
+}
+
 hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint64_t *len,
                             uint32_t n, uint8_t *md5, hipStream_t s)
 {

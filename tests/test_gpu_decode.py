@@ -253,3 +253,73 @@ def test_async_decode_fetch_frame_table(gpu_engine):
         assert [(r.status, r.pcm_frames) for r in got] == [(r.status, r.pcm_frames) for r in want]
     dec.close()
 
+
+
+@pytest.mark.parametrize("depth", [4, 8])
+def test_rolled_decode_many_in_flight(gpu_engine, depth):
+    """atg_decoder_set_inflight(depth >= 4): every batch's MD5 hashes run in
+    depth - 2 slices on the decoder's roll stream (md5.hip
+    k_bytes_md5_roll).  More batches than slots, alternating between a
+    batch of clean round-trip tracks and a batch of the reference's golden
+    corrupt cases: every batch's statuses, PCM counts and MD5s equal the
+    synchronous depth-3 decode's (the golden cases' also the reference
+    decoder's recorded values), the clean PCM equals the source, waits both
+    oldest-first and out of order, and a (depth + 1)-th enqueue is refused"""
+    import torch
+    from audiotools import _atgpu
+    opts = _atgpu.make_options(**oracle_port.PRESETS["8"])
+    pcms = [signals.make(k, 4096 * 4 + 77 * i, 2, 16, seed=90 + i)
+            for i, k in enumerate(["tone", "noise", "chirp", "sine", "silence"])]
+    tracks, start = [], 0
+    for p in pcms:
+        tracks.append((start, len(p) // 2))
+        start += len(p) // 2
+    allpcm = np.concatenate(pcms).astype(np.int16)
+    out, res, _, _ = gpu_engine.encode(opts, allpcm, tracks, 2, 16, 44100)
+    clean = _batch([out[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res])
+    fname = FILES[len(FILES) // 2]
+    cases = [c for c in CASES if c["file"] == fname]
+    gold = _batch([decode_cases.case_bytes(c) for c in cases])
+    blobs = []
+    for dtracks, blob, _ in (clean, gold):
+        d = torch.frombuffer(bytearray(blob + b"\0" * 64), dtype=torch.uint8).cuda()
+        blobs.append((d, len(blob), dtracks))
+    torch.cuda.synchronize()
+    dec = _atgpu.Decoder(0)
+    want = []
+    for d, n, dt in blobs:
+        w, _, _ = dec.decode_device(d.data_ptr(), n, dt)
+        want.append([(r.status, r.pcm_frames, bytes(r.md5)) for r in w])
+    # the golden batch: the reference decoder's recorded values
+    k = 0
+    for c, (rc, si) in zip(cases, gold[2]):
+        if rc:
+            continue
+        st, nfr, md5 = want[1][k]
+        k += 1
+        assert st == c["code"] and md5.hex() == c["pcm_md5"], c["name"]
+    dec.set_inflight(depth)
+
+    def check(i, got, d_pcm, n):
+        assert [(r.status, r.pcm_frames, bytes(r.md5)) for r in got] == want[i % 2], i
+        if i % 2 == 0:
+            host = np.empty(n, dtype=np.int32)
+            gpu_engine.copy_to_host(host, d_pcm)
+            assert np.array_equal(host, allpcm.astype(np.int32)), i
+
+    pending = []
+    for i in range(depth + 4):
+        if len(pending) == depth:
+            j, t = pending.pop(0)
+            check(j, *dec.decode_wait(t))
+        d, n, dt = blobs[i % 2]
+        pending.append((i, dec.decode_device_async(d.data_ptr(), n, dt)))
+    with pytest.raises(_atgpu.ATGError):
+        d, n, dt = blobs[0]
+        dec.decode_device_async(d.data_ptr(), n, dt)
+    for j, t in reversed(pending):
+        check(j, *dec.decode_wait(t))
+    dec.set_inflight(3)
+    d, n, dt = blobs[0]
+    check(0, *dec.decode_wait(dec.decode_device_async(d.data_ptr(), n, dt)))
+    dec.close()
