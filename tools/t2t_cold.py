@@ -123,8 +123,19 @@ def write_wavs(d, n_files, frames):
     return files
 
 
-def run_pool(cmds, j):
-    """run the commands, at most j alive; -> (wall s, [(spawn time, stdout)])"""
+def _profiler_noise_only(err):
+    """stderr holding nothing but a profiler's own log lines (rocprofv3
+    preloads itself into every child of a profiled run)"""
+    lines = [ln for ln in err.decode(errors="replace").splitlines() if ln.strip()]
+    return all("rocprofv3" in ln or "rocprofiler" in ln for ln in lines)
+
+
+def run_pool(cmds, j, tolerate_profiler=False):
+    """run the commands, at most j alive; -> (wall s, [(spawn time, stdout)]).
+    tolerate_profiler: a child that exits non-zero with only profiler log
+    lines on stderr counts as done (the reference encoder's pipeline under
+    rocprofv3; its output files are compared afterwards, so a real failure
+    still shows as files_identical false)"""
     t0 = time.time()
     pending, alive, done = list(cmds), [], []
     while pending or alive:
@@ -138,7 +149,7 @@ def run_pool(cmds, j):
                 still.append((ts, p))
                 continue
             out, err = p.communicate()
-            if p.returncode:
+            if p.returncode and not (tolerate_profiler and _profiler_noise_only(err)):
                 raise RuntimeError("child failed: %s" % err.decode()[-2000:])
             done.append((ts, out.decode()))
         alive = still
@@ -200,10 +211,17 @@ def main():
             rc = [["sh", "-c", "tail -c +45 %s | %s -c 2 -r 44100 -b 16 -B 4096 -l 12 -P 0 "
                    "-R 6 -m -e %s > /dev/null" % (fn, ref, os.path.join(rdir, os.path.basename(
                        fn)[:-4] + ".flac"))] for fn in files]
-            rwall, _ = run_pool(rc, j)
-            same = all(open(os.path.join(gdir, os.path.basename(f)[:-4] + ".flac"), "rb").read()
-                       == open(os.path.join(rdir, os.path.basename(f)[:-4] + ".flac"),
-                               "rb").read() for f in files)
+            rwall, _ = run_pool(rc, j, tolerate_profiler=True)
+            def _read(path):
+                try:
+                    with open(path, "rb") as fh:
+                        return fh.read()
+                except OSError:
+                    return None
+            same = all(_read(os.path.join(rdir, os.path.basename(f)[:-4] + ".flac")) is not None
+                       and _read(os.path.join(gdir, os.path.basename(f)[:-4] + ".flac"))
+                       == _read(os.path.join(rdir, os.path.basename(f)[:-4] + ".flac"))
+                       for f in files)
             res["reference"] = {"wall_s": round(rwall, 3),
                                 "frames_per_s": round(total_frames / rwall, 1),
                                 "files_identical": same}
