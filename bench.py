@@ -31,6 +31,7 @@ import socket
 import struct
 import subprocess
 import sys
+import queue
 import tempfile
 import threading
 import time
@@ -85,6 +86,9 @@ def parse_args(argv=None):
     ap.add_argument("--chain-tracks", type=int, default=64,
                     help="config-5 chain leg: 192 kHz 5.1 tracks per GPU")
     ap.add_argument("--chain-seconds", type=int, default=10)
+    ap.add_argument("--chain-inflight", type=int, default=4,
+                    help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
+                         "hashes are rolled)")
     ap.add_argument("--no-chain", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-to-host leg")
     ap.add_argument("--no-t2t", action="store_true", help="skip the track2track leg")
@@ -691,68 +695,108 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
             frameset_bytes=fsb[r.first_frameset:r.first_frameset + r.n_framesets]))
     alac_bytes = sum(int(r.bytes) for r in ares)
     nbytes = max(int(r.out_offset + r.bytes) for r in ares)
-    adec = _atgpu.AlacDecoder(local)
+    # the pipeline: a decode thread runs batch k + 1's
+    # ALAC decode on one of two decoders (each owns its PCM buffer) while the
+    # main thread resamples batch k and enqueues its FLAC encode; ctypes
+    # releases the GIL inside every library call, so the GPU sees the ALAC
+    # kernels beside the resampler's and the encoder's.  A decoder is handed
+    # back once the (synchronous) resample has read its buffer.
+    n_dec = 2
+    adecs = [_atgpu.AlacDecoder(local) for _ in range(n_dec)]
     rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
     n_out = _atgpu.resample_output_frames(n_in, ch, rin, rout)
-    # double-buffered resampled PCM and FLAC images: batch k's MD5 chains
-    # and headers (serial per track, ~9 MB per 5.1 track) run under batch
-    # k+1's decode/resample/search (atg_flac_encode_device_async)
-    ys = [torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device) for _ in range(2)]
+    # `depth` resampled-PCM and FLAC buffers: batch k is waited once batch
+    # k + depth - 1 is enqueued; from depth 4 on the encoder rolls every
+    # in-flight batch's MD5 chains forward in one launch per enqueue
+    # (atg_engine_set_inflight), so the serial per-track hashes (~9 MB per
+    # 5.1 track) stay off the step's critical path
+    depth = max(3, args.chain_inflight)
+    ys = [torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device)
+          for _ in range(depth)]
     eng = _atgpu.Engine(local)
+    eng.set_inflight(depth)
     fopts = _atgpu.make_options(**FLAC8)
     ftracks = [(k * n_out, n_out) for k in range(n_tracks)]
     n_flac, fcap = eng.bounds(fopts, ftracks, ch, bps)
     ftable = _atgpu.TrackTable(ftracks)
-    flacs = [torch.empty(fcap, dtype=torch.uint8, device=device) for _ in range(2)]
-    stream = torch.cuda.current_stream(device).cuda_stream
+    flacs = [torch.empty(fcap, dtype=torch.uint8, device=device) for _ in range(depth)]
+    rs_stream = torch.cuda.Stream(device)
+    stream = rs_stream.cuda_stream
     state = {}
     pending = []
+    kt = {}
 
     torch.cuda.synchronize()
 
-    def step(k):
-        dres, d_pcm, nsamp = adec.decode_device(alac.data_ptr(), nbytes, dtracks)
-        # the resampler reads n_in frames per track at fixed offsets: only a
-        # complete decode may feed it
-        if nsamp != src.numel() or any(r.status or r.pcm_frames != n_in for r in dres):
-            raise RuntimeError("ALAC decode incomplete: %d samples, statuses %s"
-                               % (nsamp, sorted({int(r.status) for r in dres})))
-        y = ys[k % 2]
-        _atgpu.resample_device(d_pcm, y.data_ptr(), y.numel(), rtracks, ch, bps, stream)
-        t = eng.encode_device_async(fopts, y.data_ptr(), _atgpu.PCM_S32, ftable, ch, bps, rout,
-                                    flacs[k % 2].data_ptr(), fcap)
-        if pending:
-            state["fres"] = eng.wait(pending.pop())
-        pending.append(t)
-        state.update(dres=dres, d_pcm=d_pcm, nsamp=nsamp, last=k)
+    def decode_thread(first, count, free, ready):
+        try:
+            for k in range(first, first + count):
+                i = free.get()
+                dres, d_pcm, nsamp = adecs[i].decode_device(alac.data_ptr(), nbytes, dtracks)
+                ready.put((k, i, dres, d_pcm, nsamp))
+        except BaseException as e:  # re-raised on the main thread
+            ready.put(e)
 
-    def drain():
-        state["fres"] = eng.wait(pending.pop())
+    def run(first, count, timed):
+        free, ready = queue.Queue(), queue.Queue()
+        for i in range(n_dec):
+            free.put(i)
+        th = threading.Thread(target=decode_thread, args=(first, count, free, ready),
+                              daemon=True)
+        th.start()
+        try:
+            for _ in range(count):
+                item = ready.get()
+                if isinstance(item, BaseException):
+                    raise item
+                k, i, dres, d_pcm, nsamp = item
+                # the resampler reads n_in frames per track at fixed offsets:
+                # only a complete decode may feed it
+                if nsamp != src.numel() or any(r.status or r.pcm_frames != n_in for r in dres):
+                    raise RuntimeError("ALAC decode incomplete: %d samples, statuses %s"
+                                       % (nsamp, sorted({int(r.status) for r in dres})))
+                y = ys[k % depth]
+                _atgpu.resample_device(d_pcm, y.data_ptr(), y.numel(), rtracks, ch, bps, stream)
+                if timed:
+                    for pre, d in (("alac_", adecs[i].kernel_times()),
+                                   ("", _atgpu.resample_kernel_times())):
+                        for name, v in d.items():
+                            key = name if name.startswith(pre) else pre + name
+                            kt[key] = kt.get(key, 0.0) + v / args.steps
+                if k == first + count - 1:
+                    state.update(dres=dres, d_pcm=d_pcm, nsamp=nsamp, last=k)
+                else:
+                    free.put(i)
+                pending.append(eng.encode_device_async(
+                    fopts, y.data_ptr(), _atgpu.PCM_S32, ftable, ch, bps, rout,
+                    flacs[k % depth].data_ptr(), fcap))
+                if len(pending) >= depth:
+                    state["fres"] = eng.wait(pending.pop(0))
+                    if timed:
+                        for name, v in eng.kernel_times().items():
+                            key = name if name.startswith("flac_") else "flac_" + name
+                            kt[key] = kt.get(key, 0.0) + v / args.steps
+            while pending:
+                state["fres"] = eng.wait(pending.pop(0))
+                if timed:
+                    for name, v in eng.kernel_times().items():
+                        key = name if name.startswith("flac_") else "flac_" + name
+                        kt[key] = kt.get(key, 0.0) + v / args.steps
+        finally:
+            th.join()
 
-    for k in range(args.warmup):
-        step(k)
-    if pending:
-        drain()
-    kt = {}
+    if args.warmup:
+        run(0, args.warmup, False)
     barrier()
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        step(k)
-        for pre, d in (("alac_", adec.kernel_times()), ("", _atgpu.resample_kernel_times()),
-                       ("flac_", eng.kernel_times() if k else {})):
-            for name, v in d.items():
-                key = name if name.startswith(pre) else pre + name
-                kt[key] = kt.get(key, 0.0) + v / args.steps
-    drain()
-    for name, v in eng.kernel_times().items():
-        key = name if name.startswith("flac_") else "flac_" + name
-        kt[key] = kt.get(key, 0.0) + v / args.steps
+    run(args.warmup, args.steps, True)
     barrier()
     elapsed = time.perf_counter() - t0
     if world > 1:
         elapsed = reduce_max(torch, dist, elapsed, device)
-    y = ys[(args.steps - 1) % 2]
-    flac = flacs[(args.steps - 1) % 2]
+    last = args.warmup + args.steps - 1
+    y = ys[last % depth]
+    flac = flacs[last % depth]
     dres, fres = state["dres"], state["fres"]
     dec_ok = all(r.status == 0 and r.pcm_frames == n_in for r in dres) and \
         state["nsamp"] == src.numel()
@@ -768,7 +812,9 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
            "config": {"tracks_per_gpu": n_tracks, "seconds_per_track": args.chain_seconds,
                       "channels": ch, "bits": bps, "rates": "%d -> %d" % (rin, rout),
                       "alac_bytes": alac_bytes, "flac_bytes": flac_bytes,
-                      "flac_frames": n_flac},
+                      "flac_frames": n_flac,
+                      "pipeline": "decode thread (2 ALAC decoders) beside resample + FLAC "
+                                  "encode, %d FLAC batches in flight" % depth},
            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
            "verified_alac_lossless": bool(dec_ok and lossless),
            "alac_decode_status": sorted({int(r.status) for r in dres}),
@@ -778,7 +824,8 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     if verify:
         out.update(chain_verify(args, threads, ch, bps, rin, rout, n_tracks, n_in, n_out, info,
                                 ares, fsb, fres, alac, src, y, flac))
-    adec.close()
+    for a in adecs:
+        a.close()
     eng.close()
     del src, alac, y, flac, ys, flacs
     return out
@@ -937,6 +984,16 @@ def t2t_leg(args):
     return out
 
 
+def rg_fallbacks():
+    """tracks the last ReplayGain call could not certify and analysed again
+    serially (replaygain.hip)"""
+    import ctypes
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    lib.atg_replaygain_fallback_tracks.restype = ctypes.c_uint32
+    return int(lib.atg_replaygain_fallback_tracks())
+
+
 def rg4_leg(args, torch, dist, world, rank, device, barrier, threads=16):
     """BASELINE config 4: ReplayGain album scan, 1024 tracks of
     --rg4-seconds s per GPU, one album per GPU: each
@@ -996,6 +1053,7 @@ def rg4_leg(args, torch, dist, world, rank, device, barrier, threads=16):
            "config": {"tracks_per_gpu": n_tracks, "seconds_per_track": args.rg4_seconds,
                       "album": "one per GPU"},
            "albums": [{"gain_db": a, "peak": p} for a, p in albums],
+           "fallback_tracks_last_step": rg_fallbacks(),
            "all_albums": {"gain_db": set_gain, "peak": set_peak,
                           "collective": "all_gather (gain, peak) + all_reduce SUM uint32[12000]"
                                         " / MAX f64 (RCCL)" if world > 1 else "none (1 rank)"}}
@@ -1071,9 +1129,11 @@ def replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks, barrie
     frames = n_tracks * args.frames * args.steps
     if world > 1:
         frames = reduce_sum(torch, dist, frames, device)
+    fallbacks = rg_fallbacks()
     out = {"metric": "ReplayGain title analysis, FLAC-frame-equivalents/s (4096 PCM frames)",
            "value": round(frames / elapsed, 1), "unit": "frames/s",
            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+           "fallback_tracks_last_step": fallbacks,
            "album": {"tracks": int(reduce_sum(torch, dist, n_tracks, device))
                      if world > 1 else n_tracks, "gain_db": album_gain,
                      "peak": album_peak,

@@ -530,6 +530,18 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
                                  uint32_t n_tracks, uint32_t n_albums, atg_rg_result *results,
                                  uint32_t *d_album_hist, double *album_peaks, void *stream);
 
+/* The certification bound of the time-split title analysis for one sample
+   rate (host computation, no GPU), out[6]: out[0] G = max over lags of the
+   Butterworth output's l1 response to a unit error state, out[1] R_s and
+   out[2] R_b the rounding sums into the state and the output, out[3]
+   1 / (1 - ||A^L||_inf), out[4] L the segment length in frames, out[5] G_L
+   = max over lags >= L (see replaygain.hip k_rg_seg).  A warm segment's
+   outputs err by at most G m + G_L (m + R_s) out[3] + 2 R_b for the
+   largest measured seam state difference m. */
+atg_status atg_replaygain_bound(uint32_t sample_rate, double *out);
+/* windows whose histogram bin the host's log10 moved (lifetime count; a
+   window within 1e-9 of a bin edge is binned with the C library's log10) */
+uint64_t atg_replaygain_rebinned_windows(void);
 /* Test hooks of the time-split analysis (replaygain.hip): the warm-up
    frames of every segment after a track's first (-1 = the rate-scaled
    default; 0 = none, so every track fails certification and is analysed

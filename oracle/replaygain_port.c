@@ -65,9 +65,33 @@ static double filter_one(chan_state *s, double x, const double *ky, const double
    Writes the track's window histogram A[12000] and returns the title peak
    (max |x| / 2^(bps-1)).  Returns -1 for unsupported rate / bps / channels
    or chunk sizes that do not add up to frames. */
+static double title_impl(const int32_t *pcm, uint64_t frames, uint32_t channels, uint32_t bps,
+                         uint32_t rate, const uint32_t *chunk, uint64_t n_chunks, uint32_t *A,
+                         double *vals, uint64_t vcap, uint64_t *nvals);
+
 double rgport_title_chunks(const int32_t *pcm, uint64_t frames, uint32_t channels,
                            uint32_t bps, uint32_t rate, const uint32_t *chunk,
                            uint64_t n_chunks, uint32_t *A)
+{
+    return title_impl(pcm, frames, channels, bps, rate, chunk, n_chunks, A, NULL, 0, NULL);
+}
+
+/* the value 1000 log10(...) of every closed window, in order (the number the
+   histogram bins; tests use it to place a window next to a bin edge):
+   returns the window count, -1 as rgport_title_chunks */
+int64_t rgport_window_vals(const int32_t *pcm, uint64_t frames, uint32_t channels,
+                           uint32_t bps, uint32_t rate, double *vals, uint64_t cap)
+{
+    uint32_t *A = (uint32_t *)malloc(sizeof(uint32_t) * RG_BINS);
+    uint64_t n = 0;
+    const double r = title_impl(pcm, frames, channels, bps, rate, NULL, 0, A, vals, cap, &n);
+    free(A);
+    return r < 0 ? -1 : (int64_t)n;
+}
+
+static double title_impl(const int32_t *pcm, uint64_t frames, uint32_t channels, uint32_t bps,
+                         uint32_t rate, const uint32_t *chunk, uint64_t n_chunks, uint32_t *A,
+                         double *vals, uint64_t vcap, uint64_t *nvals)
 {
     const int fi = rgport_freqindex(rate);
     if (fi < 0 || (channels != 1 && channels != 2) || (bps != 8 && bps != 16 && bps != 24))
@@ -136,6 +160,11 @@ double rgport_title_chunks(const int32_t *pcm, uint64_t frames, uint32_t channel
             totsamp += cur;
             if (totsamp == window) {
                 const double val = 100. * 10. * log10((lsum + rsum) / totsamp * 0.5 + 1.e-37);
+                if (nvals) {
+                    if (*nvals < vcap)
+                        vals[*nvals] = val;
+                    ++*nvals;
+                }
                 int ival = (int)val;
                 if (ival < 0)
                     ival = 0;

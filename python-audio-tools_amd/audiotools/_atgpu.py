@@ -47,6 +47,7 @@ EXPORTS = (
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
     "atg_replaygain_set_warmup", "atg_replaygain_fallback_tracks",
+    "atg_replaygain_bound", "atg_replaygain_rebinned_windows",
     "atg_replaygain_multiplier", "atg_pcm_apply_gain_device", "atg_pcm_apply_gain_host",
     "atg_alac_last_error", "atg_alac_encoder_create", "atg_alac_encoder_destroy",
     "atg_alac_batch_bounds", "atg_alac_encode_device", "atg_alac_encode_host",

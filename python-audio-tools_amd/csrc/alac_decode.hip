@@ -45,15 +45,7 @@
 // frameset parse and the channel restore stay at 64: 16 and 32 lanes a
 // wave were slower (17.6 -> 23.4 ms, 12.6 -> 17.1 ms; 8 and 16 slower
 // still), their waves already cover the SIMDs' latency
-#ifndef ATG_ADEC_PARSE_LPW
-#define ATG_ADEC_PARSE_LPW 64
-#endif
-#ifndef ATG_ADEC_CHAIN_LPW
-#define ATG_ADEC_CHAIN_LPW 1
-#endif
-#ifndef ATG_ADEC_CHANNEL_LPW
-#define ATG_ADEC_CHANNEL_LPW 64
-#endif
+constexpr uint32_t kAdecParseLpw = 64, kAdecChainLpw = 1, kAdecChannelLpw = 64;
 
 namespace {
 
@@ -215,9 +207,9 @@ __global__ __launch_bounds__(64) void k_adec_parse(const uint32_t *__restrict__ 
                                                    const uint64_t *__restrict__ pred_start,
                                                    uint64_t npred, AFs *__restrict__ recs)
 {
-    if (threadIdx.x >= ATG_ADEC_PARSE_LPW)
+    if (threadIdx.x >= kAdecParseLpw)
         return;
-    const uint64_t i = (uint64_t)blockIdx.x * ATG_ADEC_PARSE_LPW + threadIdx.x;
+    const uint64_t i = (uint64_t)blockIdx.x * kAdecParseLpw + threadIdx.x;
     if (i >= npred)
         return;
     const ADTrack T = tr[pred_track[i]];
@@ -237,9 +229,9 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
                                                    AFs *__restrict__ dense,
                                                    uint2 *__restrict__ jobs)
 {
-    if (threadIdx.x >= ATG_ADEC_CHAIN_LPW)
+    if (threadIdx.x >= kAdecChainLpw)
         return;
-    const uint32_t t = blockIdx.x * ATG_ADEC_CHAIN_LPW + threadIdx.x;
+    const uint32_t t = blockIdx.x * kAdecChainLpw + threadIdx.x;
     if (t >= nt)
         return;
     const ADTrack T = tr[t];
@@ -409,9 +401,9 @@ __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict_
                                                      const uint2 *__restrict__ jobs,
                                                      uint64_t njobs, int32_t *__restrict__ planar)
 {
-    if (threadIdx.x >= ATG_ADEC_CHANNEL_LPW)
+    if (threadIdx.x >= kAdecChannelLpw)
         return;
-    const uint64_t j = (uint64_t)blockIdx.x * ATG_ADEC_CHANNEL_LPW + threadIdx.x;
+    const uint64_t j = (uint64_t)blockIdx.x * kAdecChannelLpw + threadIdx.x;
     if (j >= njobs)
         return;
     const uint2 jb = jobs[j];
@@ -833,13 +825,13 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
     ADHIP(hipEventRecord(d->ev[0], s));
     if (np)
         hipLaunchKernelGGL(k_adec_parse,
-                           dim3((unsigned)((np + ATG_ADEC_PARSE_LPW - 1) / ATG_ADEC_PARSE_LPW)),
+                           dim3((unsigned)((np + kAdecParseLpw - 1) / kAdecParseLpw)),
                            dim3(64), 0, s, w, dtr,
                            (const uint32_t *)d->ptrack.p, (const uint64_t *)d->pstart.p, np,
                            (AFs *)d->recs.p);
     ADHIP(hipGetLastError());
     ADHIP(hipEventRecord(d->ev[1], s));
-    const dim3 tg((n + ATG_ADEC_CHAIN_LPW - 1) / ATG_ADEC_CHAIN_LPW);
+    const dim3 tg((n + kAdecChainLpw - 1) / kAdecChainLpw);
     if (n)
         hipLaunchKernelGGL(k_adec_chain, tg, dim3(64), 0, s, w, dtr, n,
                            (const uint64_t *)d->pstart.p, (const AFs *)d->recs.p,
@@ -880,7 +872,7 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
     ADHIP(hipEventRecord(d->ev[2], s));
     if (jb)
         hipLaunchKernelGGL(k_adec_channel,
-                           dim3((unsigned)((jb + ATG_ADEC_CHANNEL_LPW - 1) / ATG_ADEC_CHANNEL_LPW)),
+                           dim3((unsigned)((jb + kAdecChannelLpw - 1) / kAdecChannelLpw)),
                            dim3(64), 0, s, w,
                            dtr, (const AFs *)d->dense.p, (const uint2 *)d->jobs.p, jb,
                            (int32_t *)d->planar.p);

@@ -184,7 +184,7 @@ struct EncSlot {
     DevBuf md5in;                    // the digests on the device
     hipEvent_t ev_hpcm = nullptr;    // the PCM copies are done
     std::vector<std::future<void>> hash_jobs;
-    // rolled mode (e->depth >= ATG_ROLL_MIN_DEPTH, pipelined device
+    // rolled mode (e->depth >= kRollMinDepth, pipelined device
     // batches): the chain runs as roll_parts slices on the engine's MD5
     // stream, one per later enqueue; the tail follows the last slice there
     bool rolled = false;
@@ -208,17 +208,8 @@ struct EncSlot {
 // K1 (and the batch's table uploads) on the slot's stream rather than the
 // main one: the LPC kernels of the batches behind run beside this batch's
 // search and pack (tools/gpu_r4p.sh: 9.22 -> 8.87 ms per config-2 step)
-#ifndef ATG_K1_AUX
-#define ATG_K1_AUX 1
-#endif
 // K3-K5 of pipelined device batches on an engine-wide pack stream (section
 // 4a''' of DESIGN.md); 0 keeps them on the main stream
-#ifndef ATG_PACK_STREAM
-#define ATG_PACK_STREAM 1
-#endif
-#ifndef ATG_AUX_HIPRIO
-#define ATG_AUX_HIPRIO 1
-#endif
 
 
 // batches in flight on an engine (each its own device workspace): the MD5
@@ -233,9 +224,7 @@ constexpr uint64_t kMaxSlots = 16;
 static_assert(kMaxSlots <= kRollMax, "one rolled launch covers every slot");
 // rolled MD5 from this depth on (atg_engine_set_inflight); below it every
 // slot keeps its own aux stream and the two-part split
-#ifndef ATG_ROLL_MIN_DEPTH
-#define ATG_ROLL_MIN_DEPTH 4
-#endif
+constexpr uint64_t kRollMinDepth = 4;
 
 // one stage of the host pipeline (chunk c uses stage c % kEncSlots)
 struct HostStage {
@@ -306,7 +295,7 @@ struct atg_engine {
     hipStream_t s_main = nullptr;
     // pipelined device batches (atg_flac_encode_device_async): K3-K5 of
     // batch k on their own stream, so batch k+1's search starts beside
-    // batch k's pack (ATG_PACK_STREAM; null: everything on s_main)
+    // batch k's pack (null: everything on s_main)
     hipStream_t s_pack = nullptr;
     EncSlot slot[kMaxSlots];
     uint64_t depth = kEncSlots; // slots in rotation (atg_engine_set_inflight)
@@ -918,7 +907,7 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     sl.md5_host = want_host_md5(e, pl, fmt, md5_early);
     // rolled mode: many narrow batches in flight (atg_engine_set_inflight)
     sl.rolled = pipelined && !md5_early && !sl.md5_host && !pl.frames_only &&
-                e->depth >= ATG_ROLL_MIN_DEPTH && track_md5_paired(p, fmt);
+                e->depth >= kRollMinDepth && track_md5_paired(p, fmt);
     // a rolled batch's tables and LPC kernel go on one of the default slots'
     // aux streams in turn (high priority, a hardware queue each, created
     // before s_md5), so batch k+1's LPC kernel runs beside batch k's search
@@ -930,16 +919,12 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
         if (st0 != ATG_OK)
             return st0;
     }
-#if ATG_K1_AUX
     // the tables, the LPC kernel and the MD5 chains on the slot's stream:
     // the next batches' LPC kernels run beside this batch's search and pack.
     // Whatever the LPC kernel reads is written on this stream (or waited
     // for through wait_before): nothing the caller queued on the main
     // stream is ordered before it
     hipStream_t s_pre = pre.s_aux;
-#else
-    hipStream_t s_pre = e->s_main;
-#endif
     if (wait_before)
         HIP_TRY(hipStreamWaitEvent(s_pre, wait_before, 0));
     atg_status st = prepare_windows(e, pl, s_pre);
@@ -1007,9 +992,7 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
                                (int16_t *)sl.coef.p, (int8_t *)sl.shift.p, (uint8_t *)sl.est.p,
                                s_pre));
     HIP_TRY(hipEventRecord(ev[1], s_pre));
-#if ATG_K1_AUX
     HIP_TRY(hipStreamWaitEvent(e->s_main, ev[1], 0));
-#endif
     // MD5 chains (a serial hash per track, high-priority waves) on the slot's
     // stream once the LPC kernel is done.  Split
     // (pipelined device batches of 16-bit PCM): part 0 = 60 % of every
@@ -1281,14 +1264,10 @@ atg_status ensure_aux_stream(EncSlot &sl)
 {
     if (sl.s_aux)
         return ATG_OK;
-#if ATG_AUX_HIPRIO
     // the MD5 / header streams at the highest stream priority
     int prio_lo = 0, prio_hi = 0;
     HIP_TRY(hipDeviceGetStreamPriorityRange(&prio_lo, &prio_hi));
     HIP_TRY(hipStreamCreateWithPriority(&sl.s_aux, hipStreamNonBlocking, prio_hi));
-#else
-    HIP_TRY(hipStreamCreateWithFlags(&sl.s_aux, hipStreamNonBlocking));
-#endif
     return ATG_OK;
 }
 
@@ -1606,10 +1585,8 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
                 return ATG_ERR_DEVICE;
         if (ensure_host_streams(e) != ATG_OK)
             return ATG_ERR_DEVICE;
-#if ATG_PACK_STREAM
         // created last: the streams above keep their hardware queues
         HIP_TRY(hipStreamCreateWithFlags(&e->s_pack, hipStreamNonBlocking));
-#endif
     }
     for (EncSlot &sl : e->slot) {
         for (auto &ev : sl.ev)

@@ -344,9 +344,6 @@ __device__ __forceinline__ uint32_t crc_advq(uint32_t c, uint32_t q, int s)
 // FULL (the register-staged kernel: every lane holds a whole 64-sample run,
 // hi = 64, and only lane 0 skips warm-up codes, lo <= 12): codes 12..63 are
 // written unconditionally, so no per-code lane mask is formed for them
-#ifndef ATG_K5_FULLEMIT
-#define ATG_K5_FULLEMIT 1
-#endif
 template <bool FULL>
 __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[ATG_RUN], int lo,
                                            int hi, uint32_t k)
@@ -354,7 +351,7 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
     const uint32_t kmask = (1u << k) - 1u;
 #pragma unroll
     for (int t = 0; t < ATG_RUN; ++t)
-        if ((FULL && ATG_K5_FULLEMIT) ? (t >= ATG_FAST_ORDER || t >= lo) : (t >= lo && t < hi))
+        if (FULL ? (t >= ATG_FAST_ORDER || t >= lo) : (t >= lo && t < hi))
             w.put(u[t] >> k, k + 1u, (1u << k) | (u[t] & kmask));
 }
 
@@ -364,11 +361,9 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
 // the leading full-length (4096) frames of a 16-bit mid/side batch whose
 // frame starts are 16-byte aligned (engine.hip counts them: n_reg_frames).
 // waves per SIMD the pack kernel's registers are budgeted for
-#ifndef ATG_K5_WPE
-#define ATG_K5_WPE 2
-#endif
+constexpr int kK5WavesPerEu = 2;
 template <typename T, bool REG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))) void k_frame_pack(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerEu))) void k_frame_pack(
     FlacParams p, uint32_t f0, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
@@ -437,10 +432,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K5_WPE))
         const uint32_t wts = cand == 0u ? 0x00000001u : cand == 1u ? 0x00010000u
                            : cand == 2u ? 0x00010001u : 0xFFFF0001u;
         int xsh = (cand == 2u ? 1 : 0) + (int)w;
-#if ATG_K5_VOP3
         // the shift in a VGPR (a shift by an SGPR operand issues at half rate)
         asm volatile("v_mov_b32 %0, %0" : "+v"(xsh));
-#endif
         auto xs = [&](int i) -> int { return dot2_z(pr[i], (int)wts) >> xsh; };
         if (!REG)
             stage_candidate_any(pcm, fi.pcm_start, N, p.channels, cand, ms, lane,

@@ -35,13 +35,7 @@
 #pragma clang fp contract(off)
 
 // the VEC4 autocorrelation's PCM loads all issued before the first use
-#ifndef ATG_K1_LFENCE
-#define ATG_K1_LFENCE 1
-#endif
 // its window values loaded one sub-group ahead
-#ifndef ATG_K1_WPF
-#define ATG_K1_WPF 0
-#endif
 
 // (int)x on the reference's x86-64 build is cvttsd2si: NaN and out-of-range
 // inputs produce INT_MIN.  v_cvt_i32_f64 saturates instead, so spell it out.
@@ -159,12 +153,6 @@ __device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs
         // came two at a time, each pair waited before the next was issued:
         // K/2 memory round trips per group)
         const uint4 *__restrict__ q4 = (const uint4 *)pairs;
-#if ATG_K1_WPF
-        double wc[K];
-#pragma unroll
-        for (int u = 0; u < K; ++u)
-            wc[u] = win[min((uint32_t)u, N - 1u)];
-#endif
         for (; j0 + 4u * K <= N; j0 += 4u * K) {
             uint32_t pv[4 * K];
 #pragma unroll
@@ -175,32 +163,18 @@ __device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs
                 pv[4 * i + 2] = v.z;
                 pv[4 * i + 3] = v.w;
             }
-#if ATG_K1_LFENCE
 #pragma unroll
             for (int i = 0; i < 4 * K; ++i)
                 asm volatile("" : "+v"(pv[i]));
-#endif
 #pragma unroll
             for (int sub = 0; sub < 4; ++sub) {
                 double xv[K];
-#if ATG_K1_WPF
-                // the next K window values (scalar loads) in flight while
-                // this sub-group's chains run
-                double wn[K];
-#pragma unroll
-                for (int u = 0; u < K; ++u)
-                    wn[u] = win[min(j0 + (uint32_t)((sub + 1) * K + u), N - 1u)];
-#endif
 #pragma unroll
                 for (int u = 0; u < K; ++u) {
                     const int v = __builtin_amdgcn_sdot2(
                         __builtin_bit_cast(short2_t, pv[sub * K + u]),
                         __builtin_bit_cast(short2_t, wts), 0, false);
-#if ATG_K1_WPF
-                    xv[u] = (double)(v >> gsh) * wc[u];
-#else
                     xv[u] = (double)(v >> gsh) * win[j0 + (uint32_t)(sub * K + u)];
-#endif
                 }
 #pragma unroll
                 for (int u = 0; u < K; ++u) {
@@ -212,13 +186,6 @@ __device__ __forceinline__ void autocorr_ms16(const uint32_t *__restrict__ pairs
                         acc[L] = acc[L] + prod;
                     }
                 }
-#if ATG_K1_WPF
-#pragma unroll
-                for (int u = 0; u < K; ++u) {
-                    asm volatile("" : "+s"(wn[u]));
-                    wc[u] = wn[u];
-                }
-#endif
             }
         }
     }

@@ -34,9 +34,7 @@
 #include "wave.h"
 
 // waves per SIMD the register allocation targets
-#ifndef ATG_K2_WPE
-#define ATG_K2_WPE 2
-#endif
+constexpr int kK2WavesPerEu = 2;
 
 struct Eval {
     uint32_t bits;    // residual section bits
@@ -589,7 +587,7 @@ __device__ __forceinline__ void search_unit(const FlacParams &p, const T *__rest
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2_WPE))) void k_subframe_search(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK2WavesPerEu))) void k_subframe_search(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
@@ -607,7 +605,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2_WPE))
 // The candidates the 16-bit search (flac_search16.hip) handed over: a
 // grid-stride loop over list[0 .. *count) of frame * n_cand + cand.
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2_WPE))) void k_subframe_search_list(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK2WavesPerEu))) void k_subframe_search_list(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,

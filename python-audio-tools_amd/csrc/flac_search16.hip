@@ -32,7 +32,7 @@
 // 2) + 1 v_dot2 + 4 VALU per residual, wasted bits included for free.
 // v = |r| - [r < 0] is kept per sample (u >> k = v >> (k - 1) for the
 // zig-zag code u = 2v + [r < 0], k >= 1); #neg = 64 + sum (n >> 31).
-// With ATG_K2F_BIAS (the default) the seed also carries + 2^31: a logical
+// The seed also carries + 2^31: a logical
 // shift gives x = n + 2^(31 - sh - w), sum |r| is one v_sad_u32 per sample
 // (2 VALU per residual after the v_dot2s), and x is kept instead of v.
 #include <hip/hip_runtime.h>
@@ -53,19 +53,38 @@
 #ifndef ATG_K2F_EXP
 #define ATG_K2F_EXP 0
 #endif
-// 1: three residual-loop variants instead of seven (smaller code image)
-#ifndef ATG_K2F_FEW
-#define ATG_K2F_FEW 0
+// instruction-ledger builds only (tools/gpu_k2ledger.sh, DESIGN 4a''), 0 in
+// every product build.  ATG_K2F_TRUNC n ends k_frame_search_ms after
+// 1 staging, 2 phase 1, 3 phase 2 with pass 1 only (no pruning, partition
+// search or pass 2), 4 phase 2; each writes VERBATIM descriptors so the
+// kernels after K2 still run on valid input.  ATG_K2F_COUNT counts the
+// kernel's dynamic events (jobs per order and path, pruned jobs, partition
+// searches) into k2_counts, read by atg_k2_counters.
+#ifndef ATG_K2F_TRUNC
+#define ATG_K2F_TRUNC 0
 #endif
+#ifndef ATG_K2F_COUNT
+#define ATG_K2F_COUNT 0
+#endif
+#if ATG_K2F_COUNT
+enum { K2C_FRAMES, K2C_ACTIVE, K2C_FIXED, K2C_LPC, K2C_ORDER0, K2C_FOLD = K2C_ORDER0 + 13,
+       K2C_SPLIT, K2C_WIDE, K2C_PRUNED, K2C_FAST32, K2C_PARTS, K2C_LR, K2C_SUBR, K2C_SLOW,
+       K2C_N };
+__device__ unsigned long long k2_counts[K2C_N];
+__device__ __forceinline__ void k2_count(int lane, int k)
+{
+    if (lane == 0)
+        atomicAdd(&k2_counts[k], 1ull);
+}
+#define K2_COUNT(lane, k) k2_count(lane, k)
+#else
+#define K2_COUNT(lane, k) ((void)0)
+#endif
+// 1: three residual-loop variants instead of seven (smaller code image)
 // 1: predictors that fail the 32-bit fold's bound take the split fold
 // (eval_split) instead of the 64-bit loop
-#ifndef ATG_K2F_SPLIT
-#define ATG_K2F_SPLIT 1
-#endif
 // waves per SIMD the register allocation targets
-#ifndef ATG_K2F_WPE
-#define ATG_K2F_WPE 4
-#endif
+constexpr int kK2fWavesPerEu = 4;
 
 #define PK_PRE 16
 #define PK_WORDS (PK_PRE + ATG_MAX_BLOCK / 2 + 4 * (ATG_MAX_BLOCK / 64) + 16)
@@ -112,18 +131,11 @@ __device__ __forceinline__ int dot2(uint32_t a, int b_uniform, int c)
 // First tap of a residual: VOP3 v_dot2 with the tap pair in a VGPR and the
 // accumulator start in an SGPR (one SGPR operand per VALU instruction on
 // gfx950), so no v_mov seeds an accumulator per sample.
-#ifndef ATG_K2F_DOT2FIRST
-#define ATG_K2F_DOT2FIRST 1
-#endif
 __device__ __forceinline__ int dot2_first(uint32_t a, int tap_v, int acc_s)
 {
-#if ATG_K2F_DOT2FIRST
     int d;
     asm("v_dot2_i32_i16 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(tap_v), "s"(acc_s));
     return d;
-#else
-    return dot2(a, tap_v, acc_s);
-#endif
 }
 
 // sa += v + s31 as one v_add3_u32 the compiler cannot re-associate (it
@@ -133,7 +145,7 @@ __device__ __forceinline__ void add3_acc(uint32_t &sa, uint32_t v, uint32_t s31)
     asm("v_add3_u32 %0, %0, %1, %2" : "+v"(sa) : "v"(v), "v"(s31));
 }
 
-// Pass-1 post-processing with a biased accumulator (ATG_K2F_BIAS 1): the
+// Pass-1 post-processing with a biased accumulator: the
 // fold's seed carries + 2^31, so x = acc >>> shv (a full-rate logical
 // shift) is n + B with n = ~r and B = 2^(31 - shv) (acc + 2^31 is the true
 // int32 sum offset into [0, 2^32), and 2^31 is a multiple of 2^shv); the
@@ -142,9 +154,6 @@ __device__ __forceinline__ void add3_acc(uint32_t &sa, uint32_t v, uint32_t s31)
 // hi/lo folds keep their arithmetic n and store x = n ^ 2^31 (B = 2^31).
 // A/B (profiles/r04_af_k2_bias_ab.jsonl): K2 6.75 -> 6.65 ms live, 7.52 ->
 // 7.63 M frames/s; 0 selects the previous four-VALU form.
-#ifndef ATG_K2F_BIAS
-#define ATG_K2F_BIAS 1
-#endif
 __device__ __forceinline__ void sad_acc(uint32_t &sa, uint32_t x, uint32_t b)
 {
     asm("v_sad_u32 %0, %1, %2, %0" : "+v"(sa) : "v"(x), "v"(b));
@@ -223,9 +232,7 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap pair in a VGPR
-#if ATG_K2F_BIAS
     const uint32_t bm1 = (0x80000000u >> shv) - 1u; // B - 1
-#endif
     Win A;
     win_init(run, A, subr);
     // chunk c + 1's words are read while chunk c is computed
@@ -257,25 +264,15 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 16 * c + ii + h;
-#if ATG_K2F_BIAS
                 uint32_t x = (uint32_t)acc[h] >> shv;
                 if (i < ATG_FAST_ORDER)
                     x = (lane0 && i < order) ? bm1 : x;
                 u[i] = x;
                 sad_acc(sa, x, bm1);
-#else
-                int n = acc[h] >> shv;
-                if (i < ATG_FAST_ORDER)
-                    n = (lane0 && i < order) ? -1 : n;
-                const uint32_t s31 = (uint32_t)(n >> 31);
-                const uint32_t v = (uint32_t)n ^ s31;
-                u[i] = v;
-                add3_acc(sa, v, s31);
-#endif
             }
         }
     }
-    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
+    sabs = sa;
 }
 
 // The same for the side channel S = L - R (17 bits): tap k of sample t is
@@ -304,9 +301,7 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
     const uint32_t *__restrict__ runR = run + PK_WORDS;
     int tap0 = cl[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0)); // the first tap in a VGPR
-#if ATG_K2F_BIAS
     const uint32_t bm1 = (0x80000000u >> shv) - 1u; // B - 1
-#endif
     uint32_t W[20]; // (L, R) words of samples t0 - 12 .. t0 + 7 of the current chunk
     {
         // packed words -8..-1 = samples a-16 .. a-1; keep a-12 .. a-1
@@ -348,25 +343,15 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 8 * c + ii + h;
-#if ATG_K2F_BIAS
                 uint32_t x = (uint32_t)accs[h] >> shv;
                 if (i < ATG_FAST_ORDER)
                     x = (lane0 && i < order) ? bm1 : x;
                 u[i] = x;
                 sad_acc(sa, x, bm1);
-#else
-                int n = accs[h] >> shv;
-                if (i < ATG_FAST_ORDER)
-                    n = (lane0 && i < order) ? -1 : n;
-                const uint32_t s31 = (uint32_t)(n >> 31);
-                const uint32_t v = (uint32_t)n ^ s31;
-                u[i] = v;
-                add3_acc(sa, v, s31);
-#endif
             }
         }
     }
-    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
+    sabs = sa;
 }
 
 // A lower bound on the Rice-coded bits of the wave's residuals under any
@@ -380,9 +365,6 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 // partition search of a predictor that cannot win (flac.c:1326-1505 picks
 // the smallest exact total, so one whose bound exceeds a finished total
 // cannot be chosen).
-#ifndef ATG_K2F_FIXPRUNE
-#define ATG_K2F_FIXPRUNE 1
-#endif
 #define K2F_PRUNED 0x3FFFFFFFu
 __device__ __forceinline__ uint32_t residual_lb(uint32_t lane_sum, uint32_t cnt)
 {
@@ -441,7 +423,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         for (int j = 7; j < 14; ++j)
             cq[j] = 0;
     }
-    const int c0acc = ATG_K2F_BIAS ? (int)(0x80000000u - (1u << (sh + (int)w))) : -(1 << (sh + (int)w));
+    const int c0acc = (int)(0x80000000u - (1u << (sh + (int)w)));
     int shv = sh + (int)w;
     asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
     // lane 0's first `order` samples are warm-up: (lane0 && i < order) is a
@@ -451,16 +433,6 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     uint32_t u[ATG_RUN];
     uint32_t lane_sum; // sum |r| of the run
     if (lr) {
-#if ATG_K2F_FEW
-        // three tap counts only (zero taps past the order): a code image that
-        // fits the instruction cache
-        if (order < 4)
-            pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
-        else if (order < 8)
-            pass1_lr<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
-        else
-            pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum);
-#else
         if (dbl) {
             switch (order / 2 + 1) {
             case 1: pass1_lr<1, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
@@ -481,16 +453,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         case 6: pass1_lr<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         default: pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         }
-#endif
     } else {
-#if ATG_K2F_FEW
-        if (order < 4)
-            pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
-        else if (order < 8)
-            pass1<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
-        else
-            pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO);
-#else
         switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
         case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
@@ -500,7 +463,6 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         case 6: pass1<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         default: pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         }
-#endif
     }
     return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u >> shv);
 }
@@ -541,10 +503,8 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
-#if ATG_K2F_BIAS
     uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
     asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
-#endif
     Win A, B;
     {
         const uint4 h0 = load_run4(run - 12, subr), h1 = load_run4(run - 8, subr);
@@ -595,20 +555,13 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
-#if ATG_K2F_BIAS
                 const uint32_t x = (uint32_t)n ^ 0x80000000u;
                 u[i] = x;
                 sad_acc(sa, x, bm1);
-#else
-                const uint32_t s31 = (uint32_t)(n >> 31);
-                const uint32_t v = (uint32_t)n ^ s31;
-                u[i] = v;
-                add3_acc(sa, v, s31);
-#endif
             }
         }
     }
-    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
+    sabs = sa;
 }
 
 // the side channel on (L, R) words, split: TAPS = min(2D, 13) as pass1_lr
@@ -622,10 +575,8 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
     const uint32_t *__restrict__ runR = run + PK_WORDS;
     int tap0 = cl[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
-#if ATG_K2F_BIAS
     uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
     asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
-#endif
     uint32_t WH[20], WL[20];
     {
         uint32_t h[16];
@@ -685,20 +636,13 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
-#if ATG_K2F_BIAS
                 const uint32_t x = (uint32_t)n ^ 0x80000000u;
                 u[i] = x;
                 sad_acc(sa, x, bm1);
-#else
-                const uint32_t s31 = (uint32_t)(n >> 31);
-                const uint32_t v = (uint32_t)n ^ s31;
-                u[i] = v;
-                add3_acc(sa, v, s31);
-#endif
             }
         }
     }
-    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
+    sabs = sa;
 }
 
 template <bool BIG>
@@ -796,8 +740,18 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
                                             uint32_t bias)
 {
     Eval16 ev;
+#if ATG_K2F_TRUNC == 3
+    ev.bits = lane_sum;
+    ev.sel.porder = 0;
+    ev.sel.method = 0;
+    ev.sel.k_lane = 0;
+    ev.sel.k_own = 0;
+    ev.sel.hdr_bits = 0;
+    return ev;
+#endif
     if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
         // cannot beat a finished LPC job: no partition search, no exact bits
+        K2_COUNT(c.lane, K2C_PRUNED);
         ev.bits = K2F_PRUNED;
         ev.sel.porder = 0;
         ev.sel.method = 0;
@@ -811,10 +765,13 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
     ev.sel.hdr_bits = 262;
     if (0)
 #endif
-    if (wave_all(lane_sum < (1u << 25)))
+    if (wave_all(lane_sum < (1u << 25))) {
+        K2_COUNT(c.lane, K2C_FAST32);
         ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
-    else
+    } else {
+        K2_COUNT(c.lane, K2C_PARTS);
         ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
+    }
     const uint32_t k = ev.sel.k_lane;
     const uint32_t cnt = (uint32_t)(ATG_RUN - warm);
     const uint32_t kv = k ? k - 1u : 0u;
@@ -822,19 +779,12 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
 #if ATG_K2F_EXP == 2
     sh2 = u[kv & 63];
 #else
-#if ATG_K2F_BIAS
     // v >> kv = (n >> kv) ^ (n >> 31) for n = x - B (arithmetic shifts)
 #pragma unroll
     for (int t = 0; t < ATG_RUN; t += 2) {
         const int n0 = (int)(u[t] - bias), n1 = (int)(u[t + 1] - bias);
         sh2 = sh2 + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
     }
-#else
-    (void)bias;
-#pragma unroll
-    for (int t = 0; t < ATG_RUN; t += 2)
-        sh2 = sh2 + (u[t] >> kv) + (u[t + 1] >> kv); // v_add3_u32
-#endif
 #endif
     // k = 0: sum u = 2 sum v + #neg = sum v + sum |r| (sh2 = sum v)
     const uint32_t lb = cnt * (1u + k) + (k ? sh2 : sh2 + lane_sum);
@@ -1139,12 +1089,12 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     // whose residual bound exceeds (best finished total - hdr) is skipped
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
-    // FIXED (ATG_K2F_FIXPRUNE): it wins only below every LPC total
+    // FIXED too: it wins only below every LPC total
     // (flac.c:727-809, strict <), so a bound above a finished LPC total
     // rules it out the same way; its header is 7 + wf + o (sbps - w)
     const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     uint32_t thr = 0xFFFFFFFFu;
-    if ((!is_fixed || ATG_K2F_FIXPRUNE) && ATG_K2F_EXP != 5) {
+    if (ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
         const uint32_t hh = is_fixed ? hdr_f : hdr;
         if (best != 0xFFFFFFFFu)
@@ -1159,10 +1109,18 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
                           (shv >= 8 || (hsum << (8 - shv)) < (1ull << 30));
     const bool codes_ok = 2u * rbound + 1u < (1ull << 26);
     Eval16 ev;
+#if ATG_K2F_COUNT
+    K2_COUNT(lane, is_fixed ? K2C_FIXED : K2C_LPC);
+    K2_COUNT(lane, K2C_ORDER0 + (is_fixed ? 0 : (int)o));
+    if (TWO)
+        K2_COUNT(lane, ci.amax <= 32767u ? K2C_SUBR : K2C_LR);
+    K2_COUNT(lane, (fold_ok && codes_ok) ? K2C_FOLD : (split_ok && codes_ok) ? K2C_SPLIT
+                                                                               : K2C_WIDE);
+#endif
     if ((fold_ok && codes_ok) || ATG_K2F_EXP == 7)
         ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
                             TWO && ci.amax <= 32767u);
-    else if (split_ok && codes_ok && ATG_K2F_SPLIT)
+    else if (split_ok && codes_ok)
         ev = eval_split<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
                              TWO && ci.amax <= 32767u);
     else
@@ -1354,8 +1312,36 @@ __device__ __forceinline__ void stage_ms(const T *__restrict__ src, int tid, uin
     }
 }
 
+#if ATG_K2F_TRUNC
+// ledger builds: a VERBATIM descriptor for wave `cand`'s candidate
+__device__ __forceinline__ void trunc_verbatim(const FlacParams &p, uint32_t N, uint32_t unit,
+                                               uint32_t cand, int lane, SubDesc *__restrict__ d)
+{
+    if (lane == 0) {
+        const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
+        d->bits = 8u + sbps * N;
+        d->type = SF_VERBATIM;
+        d->order = 0;
+        d->wasted = 0;
+        d->porder = 0;
+        d->method = 0;
+        d->precision = 0;
+        d->shift = 0;
+        d->sbps = (uint8_t)sbps;
+        d->amax = (1u << (sbps - 1u)) - 1u;
+    }
+}
+#define K2_TRUNC_AT(n)                                                                    \
+    if (ATG_K2F_TRUNC == (n)) {                                                           \
+        trunc_verbatim(p, N, f * 4u + (uint32_t)wave, (uint32_t)wave, lane, out + f * 4u + wave); \
+        return;                                                                           \
+    }
+#else
+#define K2_TRUNC_AT(n)
+#endif
+
 template <typename T>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE))) void k_frame_search_ms(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPerEu))) void k_frame_search_ms(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
@@ -1382,6 +1368,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
             const uint32_t slot = atomicAdd(slow_count, 1u);
             slow_list[slot] = f * 4u + (uint32_t)tid;
         }
+        K2_COUNT(tid, K2C_SLOW);
         return;
     }
     if (tid < 3 * PK_PRE)
@@ -1436,8 +1423,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
             const uint32_t slot = atomicAdd(slow_count, 1u);
             slow_list[slot] = f * 4u + (uint32_t)tid;
         }
+        K2_COUNT(tid, K2C_SLOW);
         return;
     }
+    K2_COUNT(tid, K2C_FRAMES);
+    K2_TRUNC_AT(1)
 
     // phase 1: wave c prepares candidate c
     const uint32_t cand = (uint32_t)wave;
@@ -1460,6 +1450,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
             res[cand].best_lpc = 0xFFFFFFFFu;
     }
     __syncthreads();
+#if ATG_K2F_COUNT
+    if (load_info(&info[cand]).active)
+        K2_COUNT(lane, K2C_ACTIVE);
+#endif
+    K2_TRUNC_AT(2)
 
     // phase 2: the (candidate, predictor) jobs, dynamically shared by the 4
     // waves, the costliest first (highest orders, side channel first): the
@@ -1485,6 +1480,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE
             pred_job<false>(p, N, img + jc * PK_WORDS, ci, pi, lane, lq, ls, &res[jc]);
     }
     __syncthreads();
+    K2_TRUNC_AT(3)
+    K2_TRUNC_AT(4)
 
     // phase 3: wave c writes candidate c
     cand_finish(p, N, load_info(&info[cand]), &res[cand], lane,
@@ -1534,7 +1531,7 @@ __device__ __forceinline__ void stage16(const T *__restrict__ src, uint32_t ch, 
 }
 
 template <typename T>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(ATG_K2F_WPE))) void k_subframe_search16(
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK2fWavesPerEu))) void k_subframe_search16(
     FlacParams p, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const int16_t *__restrict__ coef_tab, const int8_t *__restrict__ shift_tab,
     const uint8_t *__restrict__ est_tab, SubDesc *__restrict__ out,
@@ -1649,10 +1646,8 @@ __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
-#if ATG_K2F_BIAS
     uint32_t bm1 = 0x7FFFFFFFu; // B - 1 for B = 2^31
     asm volatile("v_mov_b32 %0, %0" : "+v"(bm1));
-#endif
     Win A, B;
     win_init(run, A, false);
     win_init(run + PK_WORDS, B, false);
@@ -1692,20 +1687,13 @@ __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const
                 int n = BIG ? (ah[h] + (al[h] >> 12)) >> sa_v : (ah[h] << sa_v) + (al[h] >> sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
-#if ATG_K2F_BIAS
                 const uint32_t x = (uint32_t)n ^ 0x80000000u;
                 u[i] = x;
                 sad_acc(sa, x, bm1);
-#else
-                const uint32_t s31 = (uint32_t)(n >> 31);
-                const uint32_t v = (uint32_t)n ^ s31;
-                u[i] = v;
-                add3_acc(sa, v, s31);
-#endif
             }
         }
     }
-    sabs = ATG_K2F_BIAS ? sa : sa + (uint32_t)ATG_RUN;
+    sabs = sa;
 }
 
 template <bool BIG>
@@ -1870,12 +1858,12 @@ __device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
     const uint64_t rbound = ms + (((uint64_t)csum * ms) >> shift) + 1u;
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
     const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
-    // FIXED (ATG_K2F_FIXPRUNE): it wins only below every LPC total
+    // FIXED too: it wins only below every LPC total
     // (flac.c:727-809, strict <), so a bound above a finished LPC total
     // rules it out the same way; its header is 7 + wf + o (sbps - w)
     const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     uint32_t thr = 0xFFFFFFFFu;
-    if ((!is_fixed || ATG_K2F_FIXPRUNE) && ATG_K2F_EXP != 5) {
+    if (ATG_K2F_EXP != 5) {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
         const uint32_t hh = is_fixed ? hdr_f : hdr;
         if (best != 0xFFFFFFFFu)
@@ -2067,3 +2055,22 @@ hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fm
                            slow_list, slow_count);
     return hipGetLastError();
 }
+
+#if ATG_K2F_COUNT
+// ledger builds: read (and with reset != 0 clear) the K2 event counters
+extern "C" __attribute__((visibility("default"))) int atg_k2_counters(uint64_t *out, int n,
+                                                                       int reset)
+{
+    unsigned long long h[K2C_N] = {};
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(k2_counts), sizeof(h)) != hipSuccess)
+        return -1;
+    for (int k = 0; k < n && k < K2C_N; ++k)
+        out[k] = h[k];
+    if (reset) {
+        const unsigned long long z[K2C_N] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(k2_counts), z, sizeof(z)) != hipSuccess)
+            return -1;
+    }
+    return K2C_N;
+}
+#endif

@@ -25,16 +25,10 @@
 #include "wave.h"
 
 // build-time tuning constants (see launch_track_md5 / launch_bytes_md5)
-#ifndef ATG_MD5_PRIO
-#define ATG_MD5_PRIO 0
-#endif
-#ifndef ATG_DEC_MD5_PRIO
-#define ATG_DEC_MD5_PRIO 1
-#endif
-#ifndef ATG_MD5_SPLIT_PCT
-#define ATG_MD5_SPLIT_PCT 60u
-#endif
-static_assert(ATG_MD5_SPLIT_PCT <= 100u, "ATG_MD5_SPLIT_PCT is a percentage");
+// the decoder's chains at raised wave priority; the encoder's split: part 0
+// takes this share of every track's blocks
+constexpr int kDecMd5Prio = 1;
+constexpr uint32_t kMd5SplitPct = 60u;
 
 #define MD5_D 4
 
@@ -933,9 +927,9 @@ hipError_t launch_bytes_md5(const uint8_t *base, const uint64_t *off, const uint
     if (!n)
         return hipSuccess;
     const dim3 grid((n + 63u) / 64u);
-    // the decoder's chains at raised wave priority (build with
-    // -DATG_DEC_MD5_PRIO=0 for normal priority: no measurable difference)
-    const int prio = ATG_DEC_MD5_PRIO;
+    // the decoder's chains at raised wave priority (normal priority measured
+    // no different)
+    const int prio = kDecMd5Prio;
     hipLaunchKernelGGL(k_bytes_md5_pair, grid, dim3(128), 0, s, base, off, len, n, md5, prio);
     hipLaunchKernelGGL(k_bytes_md5, grid, dim3(64), 0, s, base, off, len, n, md5);
     return hipGetLastError();
@@ -951,13 +945,12 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
     const dim3 grid((p.n_tracks + 63u) / 64u);
     const uint32_t bb = p.bps / 8u;
     const int paired = (fmt == 0 && p.bps == 16u) || (fmt == 1 && bb >= 1u && bb <= 3u);
-    // the chains at normal wave priority (-DATG_MD5_PRIO=1 raises it: no
-    // measurable difference, the engine keeps three batches in flight so the
-    // chains stay off the critical path); part 0 takes ATG_MD5_SPLIT_PCT % of
-    // every track's blocks (50/60/70 measured within 0.5 % of each other).
-    // Build-time constants: a driver's environment cannot change a run.
-    const int prio = ATG_MD5_PRIO;
-    const uint32_t split_pct = ATG_MD5_SPLIT_PCT;
+    // the chains at normal wave priority (raised priority measured no
+    // different: the engine keeps three batches in flight so the chains stay
+    // off the critical path); part 0 takes kMd5SplitPct % of every track's
+    // blocks (50/60/70 measured within 0.5 % of each other)
+    const int prio = 0;
+    const uint32_t split_pct = kMd5SplitPct;
     if (paired && fmt == 0)
         hipLaunchKernelGGL(k_track_md5_pair, grid, dim3(128), 0, s, p, (const int16_t *)pcm, tracks,
                            tout, prio, part, split_pct);

@@ -17,9 +17,6 @@
 #define ATG_EXP 0
 #endif
 // partition-order search: DPP butterflies (1) or lane shuffles (0)
-#ifndef ATG_K2_SEL_DPP
-#define ATG_K2_SEL_DPP 0
-#endif
 
 struct RunCtx {
     int lane;
@@ -51,92 +48,6 @@ __device__ __forceinline__ void part_eval(uint32_t lv, uint32_t j, S Sj, S total
     e = part_estimate<S>(plen, sum, k);
 }
 
-#if ATG_K2_SEL_DPP
-// flacenc_encode_residuals' partition-order search (flac.c:1362-1402) from
-// per-lane |r| sums; the level-lv partition of lane l is l >> (6 - lv).
-// Partition sums of every level come from DPP butterflies (no LDS round
-// trips): after s steps every lane holds the sum of its aligned 2^s-lane
-// group, i.e. its level-(6-s) partition; the four 16-lane row sums are
-// read into SGPRs for levels 1 and 0.  Levels 0..2 (1, 2, 4 partitions)
-// are estimated on those scalars, levels 3..6 in the lanes, one estimate
-// per partition taken from its first lane.  The level with the smallest
-// total wins, the lowest level on ties (strict <), as in the reference.
-template <typename S>
-__device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t order,
-                                                       const RunCtx &c)
-{
-    const int lane = c.lane;
-    const S g6 = lane_sum;
-    const S g5 = dpp_group_sum<1>(g6);
-    const S g4 = g5 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_QUAD_SWAP2>((uint64_t)g5)
-                                      : (S)dpp_u32<DPP_QUAD_SWAP2>((uint32_t)g5));
-    const S g3 = g4 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_ROW_HALF_MIRROR>((uint64_t)g4)
-                                      : (S)dpp_u32<DPP_ROW_HALF_MIRROR>((uint32_t)g4));
-    const S g2 = g3 + (sizeof(S) == 8 ? (S)dpp_u64<DPP_ROW_MIRROR>((uint64_t)g3)
-                                      : (S)dpp_u32<DPP_ROW_MIRROR>((uint32_t)g3));
-    const S r0 = rd_lane(g2, 0), r1 = rd_lane(g2, 16), r2 = rd_lane(g2, 32), r3 = rd_lane(g2, 48);
-    const S h0 = r0 + r1, h1 = r2 + r3;
-    const S total = h0 + h1;
-
-    // levels 0..2 on scalars
-    uint32_t k0, k1a, k1b, k2[4];
-    S e0, e1a, e1b, e2[4];
-    part_eval<S>(0, 0, total, total, order, c, k0, e0);
-    part_eval<S>(1, 0, h0, total, order, c, k1a, e1a);
-    part_eval<S>(1, 1, h1, total, order, c, k1b, e1b);
-    part_eval<S>(2, 0, r0, total, order, c, k2[0], e2[0]);
-    part_eval<S>(2, 1, r1, total, order, c, k2[1], e2[1]);
-    part_eval<S>(2, 2, r2, total, order, c, k2[2], e2[2]);
-    part_eval<S>(2, 3, r3, total, order, c, k2[3], e2[3]);
-    S T[7];
-    T[0] = e0;
-    T[1] = e1a + e1b;
-    T[2] = (e2[0] + e2[1]) + (e2[2] + e2[3]);
-    // levels 3..6 in the lanes
-    uint32_t k3, k4, k5, k6;
-    S e3, e4, e5, e6;
-    part_eval<S>(3, (uint32_t)lane >> 3, g3, total, order, c, k3, e3);
-    part_eval<S>(4, (uint32_t)lane >> 2, g4, total, order, c, k4, e4);
-    part_eval<S>(5, (uint32_t)lane >> 1, g5, total, order, c, k5, e5);
-    part_eval<S>(6, (uint32_t)lane, g6, total, order, c, k6, e6);
-    T[3] = dpp_wave_sum<S>((lane & 7) == 0 ? e3 : (S)0);
-    T[4] = dpp_wave_sum<S>((lane & 3) == 0 ? e4 : (S)0);
-    T[5] = dpp_wave_sum<S>((lane & 1) == 0 ? e5 : (S)0);
-    T[6] = dpp_wave_sum<S>(e6);
-
-    S best_tot = (S)~(S)0;
-    uint32_t best_p = 0;
-#pragma unroll
-    for (int lv = 0; lv <= 6; ++lv) {
-        if (lv <= c.P && T[lv] < best_tot) {
-            best_tot = T[lv];
-            best_p = (uint32_t)lv;
-        }
-    }
-    PartSel r;
-    r.porder = best_p;
-    uint32_t ko;
-    switch (best_p) {
-    case 0: ko = k0; break;
-    case 1: ko = lane < 32 ? k1a : k1b; break;
-    case 2: ko = lane < 16 ? k2[0] : lane < 32 ? k2[1] : lane < 48 ? k2[2] : k2[3]; break;
-    case 3: ko = k3; break;
-    case 4: ko = k4; break;
-    case 5: ko = k5; break;
-    default: ko = k6; break;
-    }
-    r.k_own = ko;
-    const bool degen_best = (c.N >> best_p) < order;
-    const uint32_t kfirst = (uint32_t)__builtin_amdgcn_readfirstlane((int)ko);
-    r.k_lane = degen_best ? kfirst : ko;
-    r.method = 0;
-    if (c.max_rice > 14u)
-        r.method = dpp_wave_max_u32(ko) > 14u ? 1u : 0u;
-    r.hdr_bits = 6u + (1u << best_p) * (r.method ? 5u : 4u);
-    return r;
-}
-
-#else
 // wave primitives on 32- or 64-bit values
 __device__ __forceinline__ uint32_t wshfl_up(uint32_t v, int d)
 {
@@ -232,7 +143,6 @@ __device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t orde
     return r;
 }
 
-#endif
 
 // `small`: the subframe's sum |r| is known to be < 2^31 (32-bit search)
 __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order,

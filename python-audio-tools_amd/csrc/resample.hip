@@ -407,13 +407,10 @@ __global__ __launch_bounds__(64) void k_rs_phase_tab(const RsTrack *__restrict__
                   tb + kTabHdr + (uint64_t)M * wmax);
 }
 
-// k_rs_phase's input window in LDS: floats (converted per tap) or, with
-// ATG_RS_PXD=1, the same values widened to double once at staging (twice
-// the LDS, no v_cvt_f64_f32 in the tap loop)
-#ifndef ATG_RS_PXD
-#define ATG_RS_PXD 0
-#endif
-typedef std::conditional_t<ATG_RS_PXD != 0, double, float> PhaseX;
+// k_rs_phase's input window in LDS: floats, converted per tap (the same
+// values widened to double once at staging measured 25.2 against 7.2 ms:
+// twice the LDS per task halves the rows a task holds)
+typedef float PhaseX;
 constexpr size_t kPhaseXBytes = sizeof(PhaseX);
 
 // The phase-sharing filter.  The output positions of a rational ratio

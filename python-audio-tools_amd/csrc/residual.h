@@ -36,19 +36,11 @@ typedef short short2_t __attribute__((ext_vector_type(2)));
 // constant 0 as the accumulator, so no v_mov seeds it (the compiler's
 // v_dot2c form accumulates into its destination and copies a zero in
 // first).  b is wave-uniform (an SGPR operand).
-#ifndef ATG_K5_VOP3
-#define ATG_K5_VOP3 1
-#endif
 __device__ __forceinline__ int dot2_z(uint32_t a, int b_uniform)
 {
-#if ATG_K5_VOP3
     int d;
     asm("v_dot2_i32_i16 %0, %1, %2, 0" : "=v"(d) : "v"(a), "s"(b_uniform));
     return d;
-#else
-    return __builtin_amdgcn_sdot2(__builtin_bit_cast(short2_t, a),
-                                  __builtin_bit_cast(short2_t, b_uniform), 0, false);
-#endif
 }
 
 // Residuals of samples [a, a+len) (len <= 64) with a 12-tap predictor whose

@@ -399,6 +399,23 @@ def rg_title(pcm, channels, bps, rate, chunks=None):
     return A, peak
 
 
+def rg_window_vals(pcm, channels, bps, rate):
+    """the value 1000 log10(mean square / 2 + 1e-37) of every closed 50 ms
+    window (what the histogram bins), 4096-frame reads"""
+    lib = load()
+    a = np.ascontiguousarray(pcm, dtype=np.int32)
+    P = ctypes.c_void_p
+    lib.rgport_window_vals.argtypes = [P, c_u64, c_u32, c_u32, c_u32, P, c_u64]
+    lib.rgport_window_vals.restype = ctypes.c_int64
+    cap = len(a) // channels // int(np.ceil(rate * 0.05)) + 2
+    vals = np.zeros(cap, dtype=np.float64)
+    n = lib.rgport_window_vals(a.ctypes.data, len(a) // channels, channels, bps, rate,
+                               vals.ctypes.data, cap)
+    if n < 0:
+        raise ValueError("rgport_window_vals rejected the track")
+    return vals[:n]
+
+
 def rg_gain(A):
     lib = load()
     A = np.ascontiguousarray(A, dtype=np.uint32)

@@ -232,3 +232,104 @@ def test_time_split_certified_or_fallback(warm):
         assert res[k].title_gain == op.rg_gain(A)
         assert gains[k] == op.rg_gain(A) or (math.isnan(gains[k]) and
                                              math.isnan(op.rg_gain(A)))
+
+
+def _near_edge_track(closer=False):
+    """a 44.1 kHz stereo track whose window 5 -- inside the second segment,
+    whose filter state starts from a warm-up, not from frame 0 -- has a
+    value 1.4e-7 above a bin edge (found with oracle_port.rg_window_vals:
+    amplitude for the coarse position, then two samples at the window's end
+    moved by -107 and -255).  closer: six more window-end samples moved
+    (tools/rg_near_edge.py: the window's sum of squares is a quadratic form
+    in them, searched on a grid), which puts it 9.1e-12 above the edge.  The
+    precondition is re-checked by the tests with the oracle."""
+    rate, wsz, W = 44100, 2205, 5
+    rng = np.random.default_rng(5)
+    n = wsz * 12
+    t = np.arange(n)
+    amp = 1041.25
+    x = np.stack([amp * np.sin(2 * np.pi * 440 * t / rate) + rng.normal(0, amp / 4, n),
+                  amp * np.sin(2 * np.pi * 660 * t / rate) + rng.normal(0, amp / 4, n)],
+                 1).round().astype(np.int32).reshape(-1)
+    e = (W + 1) * wsz - 1
+    x[2 * e] += -107
+    x[2 * (e - 1)] += -255
+    if closer:
+        for p, d in zip((2 * e, 2 * e + 1, 2 * (e - 1), 2 * (e - 1) + 1, 2 * (e - 2),
+                         2 * (e - 2) + 1), (-36, 19, -38, -40, 14, 14)):
+            x[p] += d
+    v = op.rg_window_vals(x, 2, 16, rate)[W]
+    return x, v
+
+
+def _rebinned():
+    from audiotools import _atgpu
+    lib = _atgpu.load_library()
+    lib.atg_replaygain_rebinned_windows.restype = ctypes.c_uint64
+    return lib.atg_replaygain_rebinned_windows()
+
+
+def _two_tracks(x):
+    from audiotools import _atgpu
+    ok = make(44100, 2, 16, 30000, 3)
+    pcm = np.concatenate([ok, x])
+    tracks = [_atgpu.RgTrack(0, len(ok) // 2, 2, 16, 44100, 0),
+              _atgpu.RgTrack(len(ok) // 2, len(x) // 2, 2, 16, 44100, 1)]
+    r0 = _rebinned()
+    res, peaks, gains, hist = _atgpu.replaygain_host(pcm, tracks, 2, return_hist=True)
+    for k, p in enumerate([ok, x]):
+        A, pk = op.rg_title(p, 2, 16, 44100)
+        assert np.array_equal(hist[k], A), k
+        assert res[k].title_peak == pk and res[k].title_gain == op.rg_gain(A)
+    return _fallbacks(), _rebinned() - r0
+
+
+def test_window_near_bin_edge_after_seam_is_certified_by_the_bound():
+    """a post-seam window 1.4e-7 from a bin edge: the derived bound
+    (replaygain.hip k_rg_bin, delta ~1e-12 here) proves its bin, so no
+    track is analysed again; histogram, peak and gain equal the oracle's"""
+    x, v = _near_edge_track()
+    assert 0 < v - np.floor(v) < 1e-6, v   # the precondition the construction promises
+    nfb, _ = _two_tracks(x)
+    assert nfb == 0
+
+
+def test_window_at_bin_edge_after_seam_is_flagged_and_exact():
+    """a post-seam window 9.1e-12 from a bin edge, inside the log10 guard
+    (kRgLogGuard = 1e-9): certification cannot vouch for its bin, so the
+    track is analysed again serially and the window binned with the host's
+    log10 (replaygain.c:713-724); histogram, peak and gain equal the
+    oracle's"""
+    x, v = _near_edge_track(closer=True)
+    assert 0 < v - np.floor(v) < 1e-10, v
+    nfb, nrb = _two_tracks(x)
+    assert nfb >= 1
+    assert nrb >= 0   # moved only if the device's log10 disagreed
+
+
+@pytest.mark.parametrize("rate", [8000, 44100, 48000, 96000, 192000])
+def test_split_equals_exact_for_full_scale_clipped_and_24bit(rate):
+    """full-scale, clipped and 24-bit tracks (the largest rounding noise the
+    bound must cover) at several rates: the time-split analysis, the forced
+    serial one (atg_replaygain_set_warmup(0)) and the oracle agree bit for
+    bit on every histogram, peak and gain"""
+    from audiotools import _atgpu
+    n = int(rate * 1.3)
+    rng = np.random.default_rng(rate)
+    full = np.clip(rng.normal(0, 20000, 2 * n), -32768, 32767).astype(np.int32)
+    clip = np.clip((np.sin(np.arange(2 * n) * 0.01) * 60000).astype(np.int64),
+                   -32768, 32767).astype(np.int32)
+    b24 = np.clip(rng.normal(0, 3e6, 2 * n), -(1 << 23), (1 << 23) - 1).astype(np.int32)
+    cases = [(full, 16), (clip, 16), (b24, 24)]
+    for pcm, bps in cases:
+        tracks = [_atgpu.RgTrack(0, n, 2, bps, rate, 0)]
+        split = _atgpu.replaygain_host(pcm, tracks, 1, return_hist=True)
+        _set_warmup(0)
+        try:
+            exact = _atgpu.replaygain_host(pcm, tracks, 1, return_hist=True)
+        finally:
+            _set_warmup(-1)
+        A, pk = op.rg_title(pcm, 2, bps, rate)
+        assert np.array_equal(split[3][0], A) and np.array_equal(exact[3][0], A), (rate, bps)
+        assert split[0][0].title_peak == exact[0][0].title_peak == pk
+        assert split[0][0].title_gain == exact[0][0].title_gain == op.rg_gain(A)
