@@ -474,7 +474,9 @@ def host_leg(args, torch, dist, world, device, eng, opts, pcm_host, tracks, n_fr
     it.  Every image is compared with the device-path image of the same
     track."""
     from audiotools import _atgpu
-    steps = max(2, min(args.steps, 6))
+    # up to 20 batches: the pipeline's fill (the first upload) and drain
+    # (the last batch's MD5 chains and download) are inside the clock
+    steps = max(2, min(args.steps, 20))
     nb = eng.bounds(opts, tracks, 2, 16)[1]
     pin_pcm = _atgpu.pinned_empty(pcm_host.shape, np.int16)
     pin_pcm[:] = pcm_host
@@ -521,14 +523,19 @@ def host_leg(args, torch, dist, world, device, eng, opts, pcm_host, tracks, n_fr
         elapsed = time.perf_counter() - t0
         return summary(elapsed, steps, o, res, check(o, res))
 
+    chunk_mb = int(os.environ.get("ATG_BENCH_HOST_CHUNK_MB", "512"))
+    if chunk_mb != 512:
+        eng.set_host_chunk_bytes(chunk_mb << 20)
     pinned = run_async(pin_pcm, pin_outs)
     sync = run_sync(pin_pcm, pin_outs[0])
     pageable = run_sync(pcm_host, None)
+    if chunk_mb != 512:
+        eng.set_host_chunk_bytes(512 << 20)
     del pin_pcm, pin_outs
     out = {"metric": "FLAC-8 encode frames/s, host PCM in -> .flac images in host memory "
                      "(pinned buffers, batches queued back to back, SURVEY 8(d) timer)"}
     out.update(pinned)
-    out["chunk_mb"] = 512
+    out["chunk_mb"] = chunk_mb
     out["sync_per_batch"] = sync
     out["pageable_sync"] = pageable
     return out
@@ -1609,6 +1616,9 @@ def main(argv=None):
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+        # SURVEY 8(d)'s timer: pinned host PCM in, host images out, PCIe
+        # transfers inside the clock (the host_to_host leg, same batch)
+        "value_host_to_host": host.get("value") if isinstance(host, dict) else None,
         "higher_is_better": True,
         "scaling": args.scaling,
         "vs_baseline": None,

@@ -226,7 +226,13 @@ static_assert(kMaxSlots <= kRollMax, "one rolled launch covers every slot");
 // slot keeps its own aux stream and the two-part split
 constexpr uint64_t kRollMinDepth = 4;
 
-// one stage of the host pipeline (chunk c uses stage c % kEncSlots)
+// host pipeline stages (device PCM / image buffers): one more than the
+// batches in flight, so chunk c + 3's upload is queued on the copy engine
+// before the host waits for chunk c's batch (its MD5 chains, ~15-18 ms for
+// a 512 MiB chunk, longer than the next two uploads)
+constexpr uint64_t kHostStages = kEncSlots + 1;
+
+// one stage of the host pipeline (chunk c uses stage c % kHostStages)
 struct HostStage {
     DevBuf d_pcm, d_img, d_pack, d_off;
     uint8_t *p_in = nullptr, *p_out = nullptr; // pinned staging (pageable callers)
@@ -313,7 +319,7 @@ struct atg_engine {
     // PCM / image / packed-image buffers and pinned host staging (used only
     // for pageable caller buffers), plus copy streams, so chunk c+1's upload,
     // chunk c's encode and chunk c-1's download overlap
-    HostStage hs[kEncSlots];
+    HostStage hs[kHostStages];
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
     // PCM bytes per chunk.  A chunk's MD5 chains take ~15 ms per MiB of
     // track whatever its track count, so fewer, larger chunks keep fewer
@@ -327,7 +333,7 @@ struct atg_engine {
     std::deque<std::pair<HostJob *, size_t>> hflight; // (job, chunk): enqueued, not collected
     HostJob *hcopy_job = nullptr;                     // staged chunk whose host copy is pending
     size_t hcopy_chunk = 0;
-    uint64_t hseq = 0;                                // chunks enqueued so far (stage = seq % 3)
+    uint64_t hseq = 0; // chunks enqueued so far (stage = seq % kHostStages)
     uint64_t next_hjob = 1;
     std::map<uint32_t, uint32_t> win_off;
     std::vector<double> win_host;
@@ -1484,8 +1490,10 @@ atg_status host_drain(atg_engine *e, atg_status err)
     return err;
 }
 
-// upload chunk ci of job j and enqueue its encode; the oldest chunk is
-// collected first when every stage is busy
+// upload chunk ci of job j and enqueue its encode.  The upload is queued
+// first; then, when every slot is busy, the oldest chunk is collected (its
+// batch waited) before this chunk's encode is enqueued -- so the copy
+// engine already holds this upload while the host waits
 atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_options *opts)
 {
     (void)opts;
@@ -1494,16 +1502,19 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
         if (st != ATG_OK)
             return st;
     }
-    if (e->hflight.size() >= kEncSlots) {
+    // the stage's previous occupant (kHostStages chunks back) must be
+    // collected: with kEncSlots chunks in flight it is, except when a
+    // caller's pipeline is shallower than the stages
+    while (e->hflight.size() >= kHostStages) {
         atg_status st = host_collect(e);
         if (st != ATG_OK)
             return st;
     }
     HostChunk &c = j.chunks[ci];
-    c.stage = (size_t)(e->hseq % kEncSlots);
+    c.stage = (size_t)(e->hseq % kHostStages);
     HostStage &h = e->hs[c.stage];
     const uint64_t in_bytes = c.samples * j.elem;
-    // stage c.stage last held the chunk three enqueues back, collected
+    // stage c.stage last held the chunk kHostStages enqueues back, collected
     // (waited, packed) by now; its device buffers are reused in stream order
     HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
     HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
@@ -1520,6 +1531,11 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
     if (in_bytes)
         HIP_TRY(hipMemcpyAsync(h.d_pcm.p, src, in_bytes, hipMemcpyHostToDevice, e->s_h2d));
     HIP_TRY(hipEventRecord(h.ev_h2d, e->s_h2d));
+    if (e->hflight.size() >= kEncSlots) {
+        atg_status st = host_collect(e);
+        if (st != ATG_OK)
+            return st;
+    }
     EncSlot *sl = nullptr;
     uint64_t ticket = 0;
     atg_status st = take_slot(e, sl, ticket);

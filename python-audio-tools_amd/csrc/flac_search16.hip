@@ -392,16 +392,15 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
 // packed image, or in the (L, R) word image (TWO).
 // cw: the predictor's taps as the LPC table stores them, int16 pairs
 // (c_2m, c_2m+1) per dword, zero past the order (cw[6] = 0); wave-uniform.
-template <bool TWO>
-__device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
-                                            const uint32_t (&cw)[7], int order, int sh,
-                                            uint32_t w, uint32_t thr, bool s16)
+// The tap words of one predictor: on packed words the pairs (c0, -2^sh),
+// (c2, c1), (c4, c3), ... (halves of adjacent table dwords); on (L, R)
+// words (lr, the side channel of a frame whose |S| exceeds int16) the fold
+// (-2^sh, 2^sh), applied as (-2^14, 2^14) twice when sh = 15 (dbl), then
+// (c_k, -c_k).  cw: the table's int16 pairs (c_2m, c_2m+1), zero past the
+// order (cw[6] = 0).
+__device__ __forceinline__ void make_taps(const uint32_t (&cw)[7], int sh, bool lr, bool dbl,
+                                          int (&cq)[14])
 {
-    // s16 (side channel, every |S| <= 32767): the packed path on L - R
-    // words formed on the fly -- 2 taps per v_dot2 instead of 1
-    const bool lr = TWO && !s16;
-    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
-    int cq[14];
     if (lr) {
         // (L, R) taps: (-2^sh, 2^sh), then (c_k, -c_k)
         const int t0 = dbl ? 1 << 14 : 1 << sh;
@@ -423,6 +422,15 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         for (int j = 7; j < 14; ++j)
             cq[j] = 0;
     }
+}
+
+// One predictor with the folded 32-bit arithmetic from its tap words
+// (make_taps): pass 1, partition search, exact bits
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_fold_q(const uint32_t *__restrict__ run, const RunCtx &c,
+                                              const int (&cq)[14], int order, int sh, uint32_t w,
+                                              uint32_t thr, bool lr, bool dbl)
+{
     const int c0acc = (int)(0x80000000u - (1u << (sh + (int)w)));
     int shv = sh + (int)w;
     asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
@@ -465,6 +473,20 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
         }
     }
     return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u >> shv);
+}
+
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
+                                            const uint32_t (&cw)[7], int order, int sh,
+                                            uint32_t w, uint32_t thr, bool s16)
+{
+    // s16 (side channel, every |S| <= 32767): the packed path on L - R
+    // words formed on the fly -- 2 taps per v_dot2 instead of 1
+    const bool lr = TWO && !s16;
+    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
+    int cq[14];
+    make_taps(cw, sh, lr, dbl, cq);
+    return eval_fold_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl);
 }
 
 // ---- split fold: the 32-bit fold for predictors whose worst-case sum
@@ -688,31 +710,10 @@ __device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run
 // One predictor on the split fold (caller checked split_ok); run: the
 // lane's run in the packed image, or in the L image (TWO)
 template <bool TWO>
-__device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, const RunCtx &c,
-                                             const uint32_t (&cw)[7], int order, int sh, uint32_t w,
-                                             uint32_t thr, bool s16)
+__device__ __forceinline__ Eval16 eval_split_q(const uint32_t *__restrict__ run, const RunCtx &c,
+                                               const int (&cq)[14], int order, int sh, uint32_t w,
+                                               uint32_t thr, bool lr, bool dbl)
 {
-    const bool lr = TWO && !s16;
-    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
-    int cq[14];
-    if (lr) {
-        const int t0 = dbl ? 1 << 14 : 1 << sh;
-        cq[0] = (int)(((uint32_t)(-t0) & 0xFFFFu) | ((uint32_t)t0 << 16));
-#pragma unroll
-        for (int k = 1; k < 14; ++k) {
-            const uint32_t d = cw[(k - 1) >> 1];
-            const int ck = ((k - 1) & 1) ? hi16(d) : lo16(d);
-            cq[k] = (int)(((uint32_t)ck & 0xFFFFu) | ((uint32_t)(-ck) << 16));
-        }
-    } else {
-        cq[0] = (int)((cw[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
-#pragma unroll
-        for (int j = 1; j < 7; ++j)
-            cq[j] = (int)((cw[j] & 0xFFFFu) | (cw[j - 1] & 0xFFFF0000u));
-#pragma unroll
-        for (int j = 7; j < 14; ++j)
-            cq[j] = 0;
-    }
     const int shv = sh + (int)w;
     const bool big = shv >= 8;
     const int seed_h = big ? -(1 << (shv - 8)) : 0;
@@ -731,6 +732,18 @@ __device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, c
         pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
                                TWO, dbl);
     return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u);
+}
+
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, const RunCtx &c,
+                                             const uint32_t (&cw)[7], int order, int sh, uint32_t w,
+                                             uint32_t thr, bool s16)
+{
+    const bool lr = TWO && !s16;
+    const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
+    int cq[14];
+    make_taps(cw, sh, lr, dbl, cq);
+    return eval_split_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl);
 }
 
 // After pass 1 (every predictor form): the lower-bound pruning, the
@@ -1028,22 +1041,44 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
     }
 }
 
-// One predictor of one candidate (one wave, any wave of the workgroup):
-// residual-section bits and partition choice into res[pi].  pi = 0 is
-// FIXED when FIXED is tried, then LPC orders lo, lo + 1, ...
-// lq / ls: the candidate's LPC table rows and shifts, staged in LDS.
-template <bool TWO>
-__device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
-                                         const uint32_t *__restrict__ img, const CandInfo &ci,
-                                         uint32_t pi, int lane, const int16_t *__restrict__ lq,
-                                         const int8_t *__restrict__ ls,
-                                         PredRes *__restrict__ res)
+__device__ __forceinline__ CandInfo load_info(const CandInfo *ci)
 {
-    const bool is_fixed = p.try_fixed && pi == 0;
-    const uint32_t o = is_fixed ? ci.fixed_order : ci.lo + pi - (p.try_fixed ? 1u : 0u);
-    int shift = 0;
+    CandInfo r;
+    r.active = uniform_u32(ci->active);
+    r.w = uniform_u32(ci->w);
+    r.amax = uniform_u32(ci->amax);
+    r.fixed_order = uniform_u32(ci->fixed_order);
+    r.lo = uniform_u32(ci->lo);
+    r.hi = uniform_u32(ci->hi);
+    r.sbps = uniform_u32(ci->sbps);
+    return r;
+}
+
+// The constants of predictor pi of a candidate (pi = 0 is FIXED when FIXED
+// is tried, then LPC orders lo, lo + 1, ...): order, quantisation shift,
+// tap words, the subframe header bits, and which residual path is exact.
+// lq / ls: the candidate's LPC table rows and shifts, staged in LDS.
+struct JobSetup {
+    uint32_t o;
+    int shift;
     uint32_t cw[7];
-    if (is_fixed) {
+    bool is_fixed;
+    uint32_t hdr, hdr_f; // LPC / FIXED header bits (residual section excluded)
+    bool fold, split;    // the 32-bit fold / the split fold is exact (else 64-bit)
+};
+
+template <bool TWO>
+__device__ __forceinline__ JobSetup job_setup(const FlacParams &p, const CandInfo &ci, uint32_t pi,
+                                              const int16_t *__restrict__ lq,
+                                              const int8_t *__restrict__ ls)
+{
+    JobSetup j;
+    j.is_fixed = p.try_fixed && pi == 0;
+    const uint32_t o = j.is_fixed ? ci.fixed_order : ci.lo + pi - (p.try_fixed ? 1u : 0u);
+    j.o = o;
+    int shift = 0;
+    uint32_t *cw = j.cw;
+    if (j.is_fixed) {
         // FIXED predictor of order o as taps (flac.c:918-1016)
         switch (o) {
         case 1: cw[0] = 1u; cw[1] = 0u; break;
@@ -1056,26 +1091,20 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
         for (int m = 2; m < 7; ++m)
             cw[m] = 0u;
     } else {
-        shift = uniform_i32(ls[o - 1u]);
+        shift = ls[o - 1u];
         const uint32_t *__restrict__ rw = (const uint32_t *)(lq + (o - 1u) * p.coef_row);
 #pragma unroll
         for (int m = 0; m < 6; ++m)
-            cw[m] = 2u * (uint32_t)m < p.coef_row ? uniform_u32(rw[m]) : 0u;
+            cw[m] = 2u * (uint32_t)m < p.coef_row ? rw[m] : 0u;
         cw[6] = 0u;
     }
+    j.shift = shift;
     uint32_t csum = 0; // sum |c| < 12 * 2^14
 #pragma unroll
     for (int m = 0; m < 6; ++m) {
         const int a = lo16(cw[m]), b = hi16(cw[m]);
         csum += (uint32_t)(a < 0 ? -a : a) + (uint32_t)(b < 0 ? -b : b);
     }
-    RunCtx c;
-    c.lane = lane;
-    c.a = ATG_RUN * lane;
-    c.len = ATG_RUN;
-    c.N = N;
-    c.max_rice = p.max_rice;
-    c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
     // folded int32 sum exact: |sum c s| + 2^sh |s| + 2^(sh + w) < 2^31 on
     // unshifted samples (TWO on (L, R) words, shift 15: the fold tap
     // (-2^15, 2^15) does not fit int16 and runs as (-2^14, 2^14) twice);
@@ -1088,18 +1117,11 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     // LPC jobs: the subframe total is hdr + the residual section; a job
     // whose residual bound exceeds (best finished total - hdr) is skipped
     const uint32_t wf = ci.w ? ci.w + 1u : 1u;
-    const uint32_t hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
+    j.hdr = 7u + wf + o * (ci.sbps - ci.w) + 9u + o * p.qlp_precision;
     // FIXED too: it wins only below every LPC total
     // (flac.c:727-809, strict <), so a bound above a finished LPC total
     // rules it out the same way; its header is 7 + wf + o (sbps - w)
-    const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
-    uint32_t thr = 0xFFFFFFFFu;
-    if (ATG_K2F_EXP != 5) {
-        const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
-        const uint32_t hh = is_fixed ? hdr_f : hdr;
-        if (best != 0xFFFFFFFFu)
-            thr = best > hh ? best - hh : 0u;
-    }
+    j.hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     // split fold (eval_split): the partial sums stay within int32 whatever
     // the coefficients (|h| <= 128 (255 for L - R), l <= 255); shv < 8
     // shifts A left, which must stay inside int32
@@ -1108,23 +1130,38 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     const bool split_ok = shift <= 15 && hsum + (1ull << shv) < (1ull << 30) &&
                           (shv >= 8 || (hsum << (8 - shv)) < (1ull << 30));
     const bool codes_ok = 2u * rbound + 1u < (1ull << 26);
-    Eval16 ev;
-#if ATG_K2F_COUNT
-    K2_COUNT(lane, is_fixed ? K2C_FIXED : K2C_LPC);
-    K2_COUNT(lane, K2C_ORDER0 + (is_fixed ? 0 : (int)o));
-    if (TWO)
-        K2_COUNT(lane, ci.amax <= 32767u ? K2C_SUBR : K2C_LR);
-    K2_COUNT(lane, (fold_ok && codes_ok) ? K2C_FOLD : (split_ok && codes_ok) ? K2C_SPLIT
-                                                                               : K2C_WIDE);
-#endif
-    if ((fold_ok && codes_ok) || ATG_K2F_EXP == 7)
-        ev = eval_fold<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
-                            TWO && ci.amax <= 32767u);
-    else if (split_ok && codes_ok)
-        ev = eval_split<TWO>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr,
-                             TWO && ci.amax <= 32767u);
-    else
-        ev = eval_wide<TWO>(img, c, cw, (int)o, shift, ci.w);
+    j.fold = (fold_ok && codes_ok) || ATG_K2F_EXP == 7;
+    j.split = !j.fold && split_ok && codes_ok;
+    return j;
+}
+
+// the pruning threshold of a job from the candidate's best finished LPC total
+__device__ __forceinline__ uint32_t job_threshold(const PredRes *__restrict__ res, uint32_t hh)
+{
+    uint32_t thr = 0xFFFFFFFFu;
+    if (ATG_K2F_EXP != 5) {
+        const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+        if (best != 0xFFFFFFFFu)
+            thr = best > hh ? best - hh : 0u;
+    }
+    return thr;
+}
+
+__device__ __forceinline__ RunCtx job_ctx(const FlacParams &p, uint32_t N, int lane)
+{
+    RunCtx c;
+    c.lane = lane;
+    c.a = ATG_RUN * lane;
+    c.len = ATG_RUN;
+    c.N = N;
+    c.max_rice = p.max_rice;
+    c.P = (int)(p.max_porder < (uint32_t)ATG_MAX_PORDER ? p.max_porder : (uint32_t)ATG_MAX_PORDER);
+    return c;
+}
+
+__device__ __forceinline__ void job_store(PredRes *__restrict__ res, uint32_t pi, int lane,
+                                          bool is_fixed, uint32_t hdr, const Eval16 &ev)
+{
     if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)
         atomicMin(&res->best_lpc, hdr + ev.bits);
     res->k[pi][lane] = (uint8_t)ev.sel.k_own;
@@ -1133,6 +1170,123 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
         res->porder[pi] = (uint8_t)ev.sel.porder;
         res->method[pi] = (uint8_t)ev.sel.method;
     }
+}
+
+// One predictor of one candidate (one wave, any wave of the workgroup):
+// residual-section bits and partition choice into res[pi]
+template <bool TWO>
+__device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
+                                         const uint32_t *__restrict__ img, const CandInfo &ci,
+                                         uint32_t pi, int lane, const int16_t *__restrict__ lq,
+                                         const int8_t *__restrict__ ls,
+                                         PredRes *__restrict__ res)
+{
+    const JobSetup j = job_setup<TWO>(p, ci, pi, lq, ls);
+    const RunCtx c = job_ctx(p, N, lane);
+    const uint32_t thr = job_threshold(res, j.is_fixed ? j.hdr_f : j.hdr);
+    Eval16 ev;
+    if (j.fold)
+        ev = eval_fold<TWO>(run_of(img, lane), c, j.cw, (int)j.o, j.shift, ci.w, thr,
+                            TWO && ci.amax <= 32767u);
+    else if (j.split)
+        ev = eval_split<TWO>(run_of(img, lane), c, j.cw, (int)j.o, j.shift, ci.w, thr,
+                             TWO && ci.amax <= 32767u);
+    else
+        ev = eval_wide<TWO>(img, c, j.cw, (int)j.o, j.shift, ci.w);
+    job_store(res, pi, lane, j.is_fixed, j.hdr, ev);
+}
+
+// k_frame_search_ms: every job's constants are formed once per frame, in
+// phase 1, by the candidate's wave with one lane per predictor (vector
+// arithmetic for all 13 at once), and kept in LDS as a descriptor: the tap
+// words ready for v_dot2, the path, the header bits.  A job then reads
+// its descriptor instead of re-deriving the bounds in scalar code (DESIGN
+// 4a'' ledger: ~190 SALU per job went to that).
+struct JobDesc {
+    int cq[14];
+    uint32_t meta; // o | shift << 4 | path << 9 | fixed << 11 | lr << 12 | dbl << 13 | w << 14
+    uint32_t hh;   // header bits the pruning threshold subtracts
+    uint32_t hdr;  // LPC header bits (the candidate's best total)
+    uint32_t pad;
+};
+#define K2F_NOJOB 0xFFFFFFFFu
+
+template <bool TWO>
+__device__ __forceinline__ void jobs_prepare(const FlacParams &p, const CandInfo &ci, int lane,
+                                             const int16_t *__restrict__ lq,
+                                             const int8_t *__restrict__ ls,
+                                             JobDesc *__restrict__ jd)
+{
+    if (lane >= K2F_MAXPRED)
+        return;
+    const uint32_t n_pred = ci.active ? n_pred_of(p, ci) : 0u;
+    JobDesc *d = jd + lane;
+    if ((uint32_t)lane >= n_pred) {
+        d->meta = K2F_NOJOB;
+        return;
+    }
+    const JobSetup j = job_setup<TWO>(p, ci, (uint32_t)lane, lq, ls);
+    const bool lr = TWO && ci.amax > 32767u;
+    const bool dbl = lr && j.shift == 15;
+    int cq[14];
+    make_taps(j.cw, j.shift, lr, dbl, cq);
+#pragma unroll
+    for (int m = 0; m < 14; ++m)
+        d->cq[m] = cq[m];
+    const uint32_t path = j.fold ? 0u : (j.split ? 1u : 2u);
+    d->meta = j.o | ((uint32_t)j.shift << 4) | (path << 9) | ((uint32_t)j.is_fixed << 11) |
+              ((uint32_t)lr << 12) | ((uint32_t)dbl << 13) | (ci.w << 14);
+    d->hh = j.is_fixed ? j.hdr_f : j.hdr;
+    d->hdr = j.hdr;
+}
+
+// one job from its descriptor (k_frame_search_ms); the 64-bit path, which
+// needs the table words, takes them again from the candidate's rows
+template <bool TWO>
+__device__ __forceinline__ void pred_job_d(const FlacParams &p, uint32_t N,
+                                           const uint32_t *__restrict__ img, const JobDesc *jd,
+                                           uint32_t meta, uint32_t pi, int lane,
+                                           const CandInfo *__restrict__ info,
+                                           const int16_t *__restrict__ lq,
+                                           const int8_t *__restrict__ ls,
+                                           PredRes *__restrict__ res)
+{
+    const int o = (int)(meta & 15u), shift = (int)((meta >> 4) & 31u);
+    const uint32_t path = (meta >> 9) & 3u, w = (meta >> 14) & 31u;
+    const bool is_fixed = (meta >> 11) & 1u, lr = (meta >> 12) & 1u, dbl = (meta >> 13) & 1u;
+    const RunCtx c = job_ctx(p, N, lane);
+    const uint32_t thr = job_threshold(res, uniform_u32(jd->hh));
+    Eval16 ev;
+#if ATG_K2F_COUNT
+    K2_COUNT(lane, is_fixed ? K2C_FIXED : K2C_LPC);
+    K2_COUNT(lane, K2C_ORDER0 + (is_fixed ? 0 : o));
+    if (TWO)
+        K2_COUNT(lane, lr ? K2C_LR : K2C_SUBR);
+    K2_COUNT(lane, path == 0u ? K2C_FOLD : path == 1u ? K2C_SPLIT : K2C_WIDE);
+#endif
+    if (path < 2u) {
+        int cq[14];
+#pragma unroll
+        for (int m = 0; m < 7; ++m)
+            cq[m] = (int)uniform_u32((uint32_t)jd->cq[m]);
+        if (lr) {
+#pragma unroll
+            for (int m = 7; m < 14; ++m)
+                cq[m] = (int)uniform_u32((uint32_t)jd->cq[m]);
+        } else {
+#pragma unroll
+            for (int m = 7; m < 14; ++m)
+                cq[m] = 0;
+        }
+        if (path == 0u)
+            ev = eval_fold_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl);
+        else
+            ev = eval_split_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl);
+    } else {
+        const JobSetup j = job_setup<TWO>(p, load_info(info), pi, lq, ls);
+        ev = eval_wide<TWO>(img, c, j.cw, o, shift, w);
+    }
+    job_store(res, pi, lane, is_fixed, uniform_u32(jd->hdr), ev);
 }
 
 // Phase 3 of a candidate (one wave): the subframe choice (flac.c:727-809)
@@ -1223,18 +1377,6 @@ __device__ __forceinline__ void cand_finish(const FlacParams &p, uint32_t N, con
     }
 }
 
-__device__ __forceinline__ CandInfo load_info(const CandInfo *ci)
-{
-    CandInfo r;
-    r.active = uniform_u32(ci->active);
-    r.w = uniform_u32(ci->w);
-    r.amax = uniform_u32(ci->amax);
-    r.fixed_order = uniform_u32(ci->fixed_order);
-    r.lo = uniform_u32(ci->lo);
-    r.hi = uniform_u32(ci->hi);
-    r.sbps = uniform_u32(ci->sbps);
-    return r;
-}
 
 // wave-uniform min / max / OR of per-lane values
 __device__ __forceinline__ CandStats wave_stats(int32_t mn, int32_t mx, uint32_t orv)
@@ -1351,6 +1493,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
     __shared__ int32_t red[4][4][3];                                      // [wave][cand][mn,mx,or]
     __shared__ CandInfo info[4];
     __shared__ PredRes res[4];
+    __shared__ JobDesc jdesc[4][K2F_MAXPRED];
     __shared__ uint32_t qnext;
     // the frame's LPC tables (4 candidates x M rows) and shifts
     __shared__ __attribute__((aligned(16))) uint32_t lq32[4 * ATG_FAST_ORDER * ATG_FAST_ORDER / 2];
@@ -1454,6 +1597,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
     if (load_info(&info[cand]).active)
         K2_COUNT(lane, K2C_ACTIVE);
 #endif
+    // phase 1b: wave c forms candidate c's job descriptors, a lane per job
+    {
+        const CandInfo ci = load_info(&info[cand]);
+        const int16_t *lq = (const int16_t *)lq32 + cand * p.coef_stride;
+        const int8_t *ls = (const int8_t *)ls32 + cand * p.max_lpc_order;
+        if (cand == 3u)
+            jobs_prepare<true>(p, ci, lane, lq, ls, jdesc[3]);
+        else
+            jobs_prepare<false>(p, ci, lane, lq, ls, jdesc[cand]);
+    }
+    __syncthreads();
     K2_TRUNC_AT(2)
 
     // phase 2: the (candidate, predictor) jobs, dynamically shared by the 4
@@ -1469,15 +1623,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
             break;
         const uint32_t jc = (j + 3u) & 3u; // 3, 0, 1, 2
         const uint32_t pi = jmax - 1u - (j >> 2);
-        const CandInfo ci = load_info(&info[jc]);
-        if (!ci.active || pi >= n_pred_of(p, ci))
+        const JobDesc *jd = &jdesc[jc][pi];
+        const uint32_t meta = uniform_u32(jd->meta);
+        if (meta == K2F_NOJOB)
             continue;
         const int16_t *lq = (const int16_t *)lq32 + jc * p.coef_stride;
         const int8_t *ls = (const int8_t *)ls32 + jc * p.max_lpc_order;
         if (jc == 3u)
-            pred_job<true>(p, N, img, ci, pi, lane, lq, ls, &res[3]);
+            pred_job_d<true>(p, N, img, jd, meta, pi, lane, &info[3], lq, ls, &res[3]);
         else
-            pred_job<false>(p, N, img + jc * PK_WORDS, ci, pi, lane, lq, ls, &res[jc]);
+            pred_job_d<false>(p, N, img + jc * PK_WORDS, jd, meta, pi, lane, &info[jc], lq, ls,
+                              &res[jc]);
     }
     __syncthreads();
     K2_TRUNC_AT(3)

@@ -75,8 +75,6 @@ def test_bound_exists_and_g_matches_numpy(rate):
     assert gmax <= g <= 1.03 * gmax, (rate, g, gmax)
 
 
-
-
 def _run(x, ky, kb, xh, yh, bh):
     """filterYule + filterButter in the reference's operation order
     (replaygain.c:566-610) from state (input, Yule and Butterworth outputs,
