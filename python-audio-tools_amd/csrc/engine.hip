@@ -1393,6 +1393,9 @@ atg_status host_collect(atg_engine *e)
     sl->host = false;
     const Plan &cp = *c.plan;
     const size_t nt = cp.tracks.size();
+    // the stage's previous offsets upload (before its pack, same stream)
+    // has read p_off
+    HIP_TRY(hipEventSynchronize(h.ev_packed));
     HIP_TRY(ensure_pinned(h.p_off, h.p_off_cap, std::max<size_t>(nt, 1)));
     uint64_t pos = 0;
     for (size_t k = 0; k < nt; ++k) {
@@ -1402,6 +1405,11 @@ atg_status host_collect(atg_engine *e)
     c.out0 = j.out_pos;
     c.out_bytes = pos;
     j.out_pos += pos;
+    // growth frees the stage's buffers: the previous occupant's offsets
+    // upload, pack and download (same stream) must be done
+    if (std::max<size_t>(nt, 1) * sizeof(uint64_t) > h.d_off.cap ||
+        std::max<uint64_t>(pos, 16) > h.d_pack.cap)
+        HIP_TRY(hipStreamSynchronize(e->s_d2h));
     HIP_TRY(h.d_off.ensure(std::max<size_t>(nt, 1) * sizeof(uint64_t)));
     HIP_TRY(h.d_pack.ensure(std::max<uint64_t>(pos, 16)));
     if (nt)
@@ -1515,13 +1523,17 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
     HostStage &h = e->hs[c.stage];
     const uint64_t in_bytes = c.samples * j.elem;
     // stage c.stage last held the chunk kHostStages enqueues back, collected
-    // (waited, packed) by now; its device buffers are reused in stream order
+    // (waited, packed) by now; its device buffers are reused in stream order.
+    // A buffer that must grow is freed only once the copy stream is idle:
+    // the previous occupant's pack kernel and download may still read it
+    if (in_bytes + 16 > h.d_pcm.cap || c.plan->out_bytes + 16 > h.d_img.cap)
+        HIP_TRY(hipStreamSynchronize(e->s_d2h));
     HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
     HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
     const uint8_t *src = j.pcm + c.pcm0 * j.elem;
     if (in_bytes && !j.pin_in) {
-        HIP_TRY(ensure_pinned(h.p_in, h.p_in_cap, in_bytes + 16));
         HIP_TRY(hipEventSynchronize(h.ev_h2d)); // its previous upload has finished
+        HIP_TRY(ensure_pinned(h.p_in, h.p_in_cap, in_bytes + 16));
         par_memcpy(h.p_in, src, in_bytes, host_threads());
         src = h.p_in;
     }
