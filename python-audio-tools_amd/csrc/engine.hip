@@ -157,6 +157,11 @@ struct EncSlot {
     hipEvent_t ev_tables = nullptr, ev_pack = nullptr, ev_done = nullptr;
     std::shared_ptr<Plan> plan;      // the batch's plan (kept alive while in flight)
     const Plan *uploaded = nullptr;  // plan whose tables this slot's device holds
+    // the host pipeline packs a collected chunk's images on the copy stream
+    // from this slot's track tables after the slot is free: the next batch
+    // in the slot writes its tables only after that pack (ev_reuse)
+    hipEvent_t ev_reuse = nullptr;
+    bool reuse_pending = false;
     TrackOut *tout_h = nullptr;      // pinned
     size_t tout_cap = 0;
     FrameDesc *fdesc_h = nullptr;    // pinned
@@ -321,6 +326,10 @@ struct atg_engine {
     // chunk c's encode and chunk c-1's download overlap
     HostStage hs[kHostStages];
     hipStream_t s_h2d = nullptr, s_d2h = nullptr;
+    // a collected chunk's offsets upload and pack kernel: not behind the
+    // previous chunk's download, since the slot's next batch waits for the
+    // pack (EncSlot::ev_reuse)
+    hipStream_t s_hpack = nullptr;
     // PCM bytes per chunk.  A chunk's MD5 chains take ~15 ms per MiB of
     // track whatever its track count, so fewer, larger chunks keep fewer
     // chains in flight: config 2, queued jobs, 256 MB 28.8 ms per batch,
@@ -933,6 +942,10 @@ atg_status enqueue_batch(atg_engine *e, EncSlot &sl, const std::shared_ptr<Plan>
     hipStream_t s_pre = pre.s_aux;
     if (wait_before)
         HIP_TRY(hipStreamWaitEvent(s_pre, wait_before, 0));
+    if (sl.reuse_pending) {
+        HIP_TRY(hipStreamWaitEvent(s_pre, sl.ev_reuse, 0));
+        sl.reuse_pending = false;
+    }
     atg_status st = prepare_windows(e, pl, s_pre);
     if (st != ATG_OK)
         return st;
@@ -1286,6 +1299,16 @@ atg_status ensure_host_streams(atg_engine *e)
     return ATG_OK;
 }
 
+// the host pipeline's pack stream, created on the first host job: created
+// with the engine it would take the hardware queue s_pack gets (created
+// last for that reason) and serialise the device path's K3-K5 with K2
+atg_status ensure_host_pack_stream(atg_engine *e)
+{
+    if (!e->s_hpack)
+        HIP_TRY(hipStreamCreateWithFlags(&e->s_hpack, hipStreamNonBlocking));
+    return ATG_OK;
+}
+
 // the slot for a new batch: the one after the last ticket's.  A slot still
 // holding an unwaited batch is never reused (its results would be lost):
 // the caller must wait the oldest ticket first, as with the decoder
@@ -1406,19 +1429,26 @@ atg_status host_collect(atg_engine *e)
     c.out_bytes = pos;
     j.out_pos += pos;
     // growth frees the stage's buffers: the previous occupant's offsets
-    // upload, pack and download (same stream) must be done
+    // upload, pack and download must be done
     if (std::max<size_t>(nt, 1) * sizeof(uint64_t) > h.d_off.cap ||
-        std::max<uint64_t>(pos, 16) > h.d_pack.cap)
+        std::max<uint64_t>(pos, 16) > h.d_pack.cap) {
+        HIP_TRY(hipStreamSynchronize(e->s_hpack));
         HIP_TRY(hipStreamSynchronize(e->s_d2h));
+    }
     HIP_TRY(h.d_off.ensure(std::max<size_t>(nt, 1) * sizeof(uint64_t)));
     HIP_TRY(h.d_pack.ensure(std::max<uint64_t>(pos, 16)));
+    // the pack overwrites d_pack: the previous occupant's download is done
+    HIP_TRY(hipStreamWaitEvent(e->s_hpack, h.ev_d2h, 0));
     if (nt)
         HIP_TRY(hipMemcpyAsync(h.d_off.p, h.p_off, nt * sizeof(uint64_t), hipMemcpyHostToDevice,
-                               e->s_d2h));
+                               e->s_hpack));
     HIP_TRY(launch_pack_images((const uint8_t *)h.d_img.p, (const TrackInfo *)sl->tracks.p,
                                (const TrackOut *)sl->tout.p, (const uint64_t *)h.d_off.p,
-                               (uint32_t)nt, (uint8_t *)h.d_pack.p, e->s_d2h));
-    HIP_TRY(hipEventRecord(h.ev_packed, e->s_d2h));
+                               (uint32_t)nt, (uint8_t *)h.d_pack.p, e->s_hpack));
+    HIP_TRY(hipEventRecord(h.ev_packed, e->s_hpack));
+    HIP_TRY(hipEventRecord(sl->ev_reuse, e->s_hpack));
+    sl->reuse_pending = true;
+    HIP_TRY(hipStreamWaitEvent(e->s_d2h, h.ev_packed, 0));
     c.staged_out = !j.pin_out;
     uint8_t *dst = j.out + c.out0;
     if (c.staged_out) {
@@ -1506,7 +1536,9 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
 {
     (void)opts;
     {
-        const atg_status st = ensure_host_streams(e);
+        atg_status st = ensure_host_streams(e);
+        if (st == ATG_OK)
+            st = ensure_host_pack_stream(e);
         if (st != ATG_OK)
             return st;
     }
@@ -1527,7 +1559,7 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
     // A buffer that must grow is freed only once the copy stream is idle:
     // the previous occupant's pack kernel and download may still read it
     if (in_bytes + 16 > h.d_pcm.cap || c.plan->out_bytes + 16 > h.d_img.cap)
-        HIP_TRY(hipStreamSynchronize(e->s_d2h));
+        HIP_TRY(hipStreamSynchronize(e->s_hpack));
     HIP_TRY(h.d_pcm.ensure(in_bytes + 16));
     HIP_TRY(h.d_img.ensure(c.plan->out_bytes + 16));
     const uint8_t *src = j.pcm + c.pcm0 * j.elem;
@@ -1621,6 +1653,7 @@ atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out)
             HIP_TRY(hipEventCreate(&ev));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_tables, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_pack, hipEventDisableTiming));
+        HIP_TRY(hipEventCreateWithFlags(&sl.ev_reuse, hipEventDisableTiming));
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_done, hipEventDisableTiming));
     }
     for (HostStage &h : e->hs) {
@@ -1664,6 +1697,8 @@ void atg_engine_destroy(atg_engine *e)
             (void)hipEventDestroy(ev);
         (void)hipEventDestroy(sl.ev_tables);
         (void)hipEventDestroy(sl.ev_pack);
+        if (sl.ev_reuse)
+            (void)hipEventDestroy(sl.ev_reuse);
         (void)hipEventDestroy(sl.ev_done);
         if (sl.tout_h)
             (void)hipHostFree(sl.tout_h);
@@ -1674,7 +1709,7 @@ void atg_engine_destroy(atg_engine *e)
         if (sl.s_aux)
             (void)hipStreamDestroy(sl.s_aux);
     }
-    for (hipStream_t q : {e->s_h2d, e->s_d2h})
+    for (hipStream_t q : {e->s_h2d, e->s_hpack, e->s_d2h})
         if (q)
             (void)hipStreamSynchronize(q);
     for (HostStage &h : e->hs) {
@@ -1687,7 +1722,7 @@ void atg_engine_destroy(atg_engine *e)
         (void)hipEventDestroy(h.ev_packed);
         (void)hipEventDestroy(h.ev_d2h);
     }
-    for (hipStream_t q : {e->s_h2d, e->s_d2h})
+    for (hipStream_t q : {e->s_h2d, e->s_hpack, e->s_d2h})
         if (q)
             (void)hipStreamDestroy(q);
     e->windows.release();
