@@ -7,7 +7,7 @@ R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT="$R/gpurun_out/${1:-pmc}"
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-ARGS="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host --no-chain --no-t2t --no-rg4"
+ARGS="$R/bench.py --steps 1 --warmup 1 --no-cpu-baseline --no-verify --no-host --no-chain --no-t2t --no-rg4 --narrow="
 # the converter leg (k_pcm_bps) runs inside the decode legs of the same process
 pass() {
     local name=$1; shift

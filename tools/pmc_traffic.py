@@ -24,7 +24,7 @@ names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
          "k_dec_scan": "dec_scan", "k_dec_sync": "dec_scan", "k_dec_hdr": "dec_scan",
          "k_dec_parse": "dec_parse", "k_dec_crc": "dec_parse", "k_dec_chain": "dec_chain",
          "k_dec_subframe": "dec_subframe", "k_dec_emit": "dec_emit",
-         "k_bytes_md5": "dec_md5", "k_bytes_md5_pair": "dec_md5",
+         "k_bytes_md5": "dec_md5", "k_bytes_md5_pair": "dec_md5", "k_bytes_md5_roll": "dec_md5",
          "k_pcm_bps": "pcm_bps",
          # resampler (resample.hip)
          "k_rs_phase": "rs_filter", "k_rs_filter": "rs_filter_deep"}
