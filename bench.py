@@ -79,7 +79,7 @@ def parse_args(argv=None):
     ap.add_argument("--narrow", default="512,256,128",
                     help="track counts of the narrow-batch leg (a strong-scaling rank's "
                          "share, on one GPU); empty to skip")
-    ap.add_argument("--narrow-depths", default="3,12,16",
+    ap.add_argument("--narrow-depths", default="3,16,24,32",
                     help="batches in flight for the narrow leg (atg_engine_set_inflight)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
@@ -1219,8 +1219,9 @@ def strong_depth(n_tracks):
     kernels of a batch take ~8.3 ms x n/1024, its MD5 chains ~12.5 ms
     whatever n, so a narrow batch needs chain / kernels + 2 batches in
     flight (rolled MD5 slices the chain over depth - 2 enqueues); measured
-    best: 16 up to 256 tracks, 12 up to 512 (profiles/r05_narrow.json)"""
-    return 16 if n_tracks <= 256 else 12 if n_tracks <= 512 else 3
+    best: 24 up to 128 tracks, 32 up to 256, 16 up to 512
+    (profiles/r05_narrow.json, r05_zm_narrow_depth.json)"""
+    return 24 if n_tracks <= 128 else 32 if n_tracks <= 256 else 16 if n_tracks <= 512 else 3
 
 
 def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_full, res_full,

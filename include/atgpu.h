@@ -259,7 +259,7 @@ atg_status atg_service_encode_frames(atg_service *svc, const atg_flac_options *o
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *eng, uint64_t bytes);
 
 /* Batches atg_flac_encode_device_async keeps in flight (slots in rotation,
-   each its own device workspace): 3 (default) .. 16.  Every track's MD5 is
+   each its own device workspace): 3 (default) .. 32.  Every track's MD5 is
    one serial hash (~12.5 ms per MiB of track on the GPU, whatever the batch
    width), so a narrow batch -- a rank's share of a strong-scaling job --
    needs more batches in flight to keep the chains off its step.  From 4

@@ -683,7 +683,7 @@ class Engine(object):
         return out[:nb.value], fb[:n_fr]
 
     def set_inflight(self, n):
-        """batches encode_device_async keeps in flight (3..16)"""
+        """batches encode_device_async keeps in flight (3..32)"""
         _check(self.lib, self.lib.atg_engine_set_inflight(self.handle, int(n)))
 
     def set_host_chunk_bytes(self, nbytes):

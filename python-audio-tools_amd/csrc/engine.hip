@@ -225,7 +225,7 @@ struct EncSlot {
 // batches in flight to hide the same chain: atg_engine_set_inflight raises
 // the slot rotation up to kMaxSlots (default kEncSlots)
 constexpr uint64_t kEncSlots = 3;
-constexpr uint64_t kMaxSlots = 16;
+constexpr uint64_t kMaxSlots = 32;
 static_assert(kMaxSlots <= kRollMax, "one rolled launch covers every slot");
 // rolled MD5 from this depth on (atg_engine_set_inflight); below it every
 // slot keeps its own aux stream and the two-part split
@@ -2170,7 +2170,7 @@ atg_status atg_engine_set_inflight(atg_engine *e, uint32_t n)
 {
     ATG_HANDLE_LOCK(e);
     if (!e || n < kEncSlots || n > kMaxSlots)
-        return fail(ATG_ERR_INVALID, "in-flight batches must be 3..16");
+        return fail(ATG_ERR_INVALID, "in-flight batches must be 3..32");
     for (EncSlot &sl : e->slot)
         if (sl.busy)
             return fail(ATG_ERR_INVALID, "an encode batch is in flight: wait for it first");

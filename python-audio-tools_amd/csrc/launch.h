@@ -81,7 +81,7 @@ hipError_t launch_track_md5(const FlacParams &p, const void *pcm, int fmt,
                             const TrackInfo *tracks, TrackOut *tout, int part, hipStream_t s);
 // rolled chains (engine rolled mode): one launch advances up to kRollMax
 // batches' whole-block chains by their own slices (md5.hip k_track_md5_roll)
-constexpr uint32_t kRollMax = 16;
+constexpr uint32_t kRollMax = 32;
 struct MdRollBatch {
     const void *pcm;
     const TrackInfo *tracks;

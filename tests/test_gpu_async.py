@@ -163,7 +163,7 @@ def _batch32(seed, shapes, bps):
     return np.concatenate(parts), tracks, per
 
 
-@pytest.mark.parametrize("depth", [4, 8, 16])
+@pytest.mark.parametrize("depth", [4, 8, 16, 32])
 def test_rolled_md5_many_in_flight_match_port(depth):
     """atg_engine_set_inflight(depth >= 4): every batch's MD5 chain runs in
     depth - 2 slices on the engine's MD5 stream, all batches' slices in one
