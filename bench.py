@@ -67,8 +67,9 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=30)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--inflight", type=int, default=3, choices=(2, 3),
-                    help="encode batches in flight (the engine keeps three slots)")
+    ap.add_argument("--inflight", type=int, default=12,
+                    help="encode batches in flight (2..32; from 4 on the MD5 chains are "
+                         "rolled, atg_engine_set_inflight)")
     ap.add_argument("--tracks", type=int, default=1024,
                     help="tracks per GPU (weak) or in total (strong)")
     ap.add_argument("--frames", type=int, default=64, help="FLAC frames per track")
@@ -359,8 +360,12 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
             last = wait_one()
         return last
 
-    if args.warmup:
-        run(args.warmup, False)
+    # untimed warm-up: every slot of the rotation (each slot's ~5 GB of PCM
+    # rows, PCM and MD5 bytes are allocated on its first batch), then on to
+    # ~40 batches -- in a process whose engine ran host jobs just before, the
+    # first ~40 rolled batches ran 1.5-2 ms per step slower, the MD5 slices
+    # falling behind
+    run(max(args.warmup, 5 * args.dec_inflight), False)
     barrier()
     t0 = time.perf_counter()
     dres, d_pcm, nsamp = run(args.steps, True)
@@ -1278,7 +1283,7 @@ def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_ful
                 "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
                 "verified_tracks": n - bad, "mismatches": bad}
             del bufs
-        eng.set_inflight(args.inflight if args.inflight >= 3 else 3)
+        eng.set_inflight(max(3, args.inflight))
         out[str(n)] = per
     return {"tracks_per_batch": out,
             "note": "the first n tracks of the config-2 batch per step, pipelined; "
@@ -1319,8 +1324,12 @@ def main(argv=None):
     # `depth` output buffers: batch k is waited once batch k + depth - 1 is
     # enqueued (atg_flac_encode_device_async), so batch k's MD5 chains and
     # headers run under the next batches' search chains; every batch is
-    # complete inside the clock
+    # complete inside the clock.  Depth 12 (rolled MD5: each batch's chains
+    # advance a slice per later enqueue) measured 7.99 ms per step against
+    # 8.30 at 3, 8.07-8.11 at 8 and 8.06 at 16 (profiles/r05_zs_inflight.json)
     depth = args.inflight
+    if depth > 3:
+        eng.set_inflight(depth)
     outs = [torch.empty(out_cap, dtype=torch.uint8, device=device) for _ in range(depth)]
     torch.cuda.synchronize()
     pending = []
@@ -1416,7 +1425,7 @@ def main(argv=None):
 
         s_timed(s_depth + 1)
         dt = s_timed(args.steps)
-        eng.set_inflight(3)
+        eng.set_inflight(max(3, args.inflight))
         del s_outs
         tot = reduce_sum(torch, dist, n_s * args.frames * args.steps, device)
         strong = {"value": round(tot / dt, 1), "unit": "frames/s",
@@ -1491,6 +1500,9 @@ def main(argv=None):
         del want
 
     decode = convert = rg = rg_res = resample = host = None
+    # the legs below keep the engine's default rotation (three slots, each
+    # with its aux stream from creation: deeper rotations add streams)
+    eng.set_inflight(3)
     if not args.no_host:
         host = host_leg(args, torch, dist, world, device, eng, opts, pcm_host, tracks, n_frames,
                         images, barrier)
