@@ -99,9 +99,11 @@ def parse_args(argv=None):
                     help="track2track leg: 64-frame WAV files, one process each")
     ap.add_argument("--no-rg4", action="store_true", help="skip the config-4 ReplayGain leg")
     ap.add_argument("--rg4-seconds", type=int, default=10)
-    ap.add_argument("--dec-inflight", type=int, default=8,
-                    help="decode batches in flight (the decoder's slot count; from 4 on the "
-                         "MD5 hashes are rolled, atg_decoder_set_inflight)")
+    ap.add_argument("--dec-inflight", type=int, default=12,
+                    help="decode batches in flight (the decoder's slot count, 3..16; from 4 "
+                         "on the MD5 hashes are rolled, atg_decoder_set_inflight; 12 measured "
+                         "7.03-7.05 ms per step against 7.16-7.23 at 8, 7.08 at 10 and 8.33 "
+                         "at 16, profiles/r05_zz_dec_depth.txt)")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",

@@ -435,7 +435,7 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
                                   uint64_t *total_samples);
 
 /* Decode batches atg_flac_decode_device_async keeps in flight: 3 (default)
-   .. 8.  A batch's STREAMINFO MD5 checks are serial hashes (~12 ms per 1 MB
+   .. 16.  A batch's STREAMINFO MD5 checks are serial hashes (~12 ms per 1 MB
    of decoded PCM whatever the batch width); from 4 on, the hashes of every
    batch in flight advance together, one launch per enqueue on one stream,
    each batch's in n - 2 slices.  Fails while a batch is unwaited; the last

@@ -794,7 +794,7 @@ class Decoder(object):
             pass
 
     def set_inflight(self, n):
-        """decode batches decode_device_async keeps in flight (3..8)"""
+        """decode batches decode_device_async keeps in flight (3..16)"""
         self._check(self.lib.atg_decoder_set_inflight(self.handle, int(n)))
 
     def decode(self, data, tracks, fetch_pcm=True):

@@ -1676,7 +1676,7 @@ struct DBuf {
 // flight no longer queue their chains behind one another on shared hardware
 // queues (the 13.4 ms at four slots above).
 constexpr int kDecSlots = 3;
-constexpr int kDecMaxSlots = 8;
+constexpr int kDecMaxSlots = 16;
 struct DecSlot {
     DBuf pcm, bytes, md5, md5meta;
     DBuf tracks, frames, jobs, warm, rows, meta; // the restore's tables and scratch
@@ -2469,7 +2469,7 @@ atg_status atg_decoder_set_inflight(atg_decoder *d, uint32_t n)
 {
     ATG_HANDLE_LOCK(d);
     if (!d || n < (uint32_t)kDecSlots || n > (uint32_t)kDecMaxSlots)
-        return dfail(ATG_ERR_INVALID, "decode batches in flight must be 3..8");
+        return dfail(ATG_ERR_INVALID, "decode batches in flight must be 3..16");
     for (DecSlot &sl : d->slot)
         if (sl.busy)
             return dfail(ATG_ERR_INVALID, "a decode batch is in flight: wait for it first");

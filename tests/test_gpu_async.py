@@ -220,4 +220,7 @@ def test_rolled_md5_many_in_flight_match_port(depth):
     ts = [enq(jobs[k]) for k in range(3)]
     for k, t in enumerate(ts):
         check(jobs[k], eng.wait(t), "depth 3 again, batch %d" % k)
+    for bad in (2, 33):  # the rotation is 3..32 batches
+        with pytest.raises(_atgpu.ATGError):
+            eng.set_inflight(bad)
     eng.close()

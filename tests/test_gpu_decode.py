@@ -255,7 +255,7 @@ def test_async_decode_fetch_frame_table(gpu_engine):
 
 
 
-@pytest.mark.parametrize("depth", [4, 8])
+@pytest.mark.parametrize("depth", [4, 8, 16])
 def test_rolled_decode_many_in_flight(gpu_engine, depth):
     """atg_decoder_set_inflight(depth >= 4): every batch's MD5 hashes run in
     depth - 2 slices on the decoder's roll stream (md5.hip
@@ -322,4 +322,7 @@ def test_rolled_decode_many_in_flight(gpu_engine, depth):
     dec.set_inflight(3)
     d, n, dt = blobs[0]
     check(0, *dec.decode_wait(dec.decode_device_async(d.data_ptr(), n, dt)))
+    for bad in (2, 17):  # the rotation is 3..16 batches
+        with pytest.raises(_atgpu.ATGError):
+            dec.set_inflight(bad)
     dec.close()
