@@ -104,6 +104,10 @@ def parse_args(argv=None):
                          "on the MD5 hashes are rolled, atg_decoder_set_inflight; 12 measured "
                          "7.03-7.05 ms per step against 7.16-7.23 at 8, 7.08 at 10 and 8.33 "
                          "at 16, profiles/r05_zz_dec_depth.txt)")
+    ap.add_argument("--dec-hypothesis", type=int, default=1, choices=(0, 1, 2),
+                    help="the decoder's frame-end hypothesis (atg_decoder_set_frame_hypothesis):"
+                         " 0 every subframe walked by the parse, 1 (default), 2 every batch "
+                         "redone (self-check)")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
     ap.add_argument("--selftest", action="store_true",
@@ -328,6 +332,8 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     if args.dec_inflight > 3:
         # rolled MD5 hashes (atg_decoder_set_inflight)
         dec.set_inflight(args.dec_inflight)
+    if args.dec_hypothesis != 1:
+        dec.set_frame_hypothesis(args.dec_hypothesis)
     tracks = []
     for r in res:
         si = _atgpu.StreamInfo()
@@ -398,6 +404,7 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     dom = max(kernels, key=kernels.get)
     achieved = alg[dom] / (kernels[dom] / 1e3) / 1e9
     traffic = (load_profile_json("pmc_traffic.json") or {}).get(dom)
+    redos = dec.frame_hypothesis_redos()
     dec.close()
     step_alg = comp + pcm32
     return {
@@ -418,6 +425,11 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
                        % (args.dec_inflight, args.dec_inflight - 2)),
         "step_hbm": {"alg_bytes_per_step": step_alg,
                      "frac": round(step_alg / (elapsed / args.steps) / 1e9 / HBM_PEAK_GBS, 5)},
+        "frame_hypothesis": {"mode": args.dec_hypothesis, "batches_redone": redos,
+                             "note": "the parse takes a frame's end from the next header "
+                                     "candidate with a zero CRC-16 residue and skips the "
+                                     "frame's last subframe; the restore checks it, a failed "
+                                     "check redoes the batch with the full parse"},
         "verified_md5_round_trip": ok,
         "verified_pcm_vs_source": same,
         "verified_tracks": len(dres) if (ok and same) else 0,

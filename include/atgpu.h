@@ -442,6 +442,19 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
    waited batch's buffers are no longer fetchable afterwards. */
 atg_status atg_decoder_set_inflight(atg_decoder *dec, uint32_t n);
 
+/* The parse's frame-end hypothesis (flac_decode.hip k_dec_spec): 1 (default)
+   takes a frame's end from the next frame-header candidate whose bytes give
+   a zero CRC-16 residue, so the parse does not walk the frame's last
+   subframe; the restore checks every such frame on the subframe it walks
+   anyway, and a batch with a failed check is redone with every subframe
+   walked inside atg_flac_decode_wait -- results are those of the full parse
+   (src/decoders/flac.c:174-285) either way.  0: every subframe walked by the
+   parse.  2: as 1, and every batch redone (self-check of the redo path). */
+atg_status atg_decoder_set_frame_hypothesis(atg_decoder *dec, int mode);
+
+/* Batches this decoder redid with the full parse (mode 1: failed checks). */
+uint64_t atg_decoder_frame_hypothesis_redos(atg_decoder *dec);
+
 /* Asynchronous form of atg_flac_decode_device (three batches in flight):
    the scan, parse and frame walk run on the decoder's stream (two host
    round trips for the counts), then the restore, emit and per-track MD5 on

@@ -43,6 +43,7 @@ EXPORTS = (
     "atg_decoder_last_error", "atg_flac_decode_host", "atg_flac_decode_fetch",
     "atg_flac_decode_device", "atg_flac_decode_device_async", "atg_flac_decode_wait",
     "atg_decoder_kernel_times", "atg_decoder_set_inflight",
+    "atg_decoder_set_frame_hypothesis", "atg_decoder_frame_hypothesis_redos",
     "atg_pcm_convert_last_error", "atg_pcm_convert_out_channels",
     "atg_pcm_convert_device", "atg_pcm_convert_host",
     "atg_replaygain_last_error", "atg_replaygain_device", "atg_replaygain_hist_gain",
@@ -332,6 +333,10 @@ def load_library():
         lib.atg_flac_decode_wait.restype = ctypes.c_int
         lib.atg_decoder_set_inflight.argtypes = [P, c_u32]
         lib.atg_decoder_set_inflight.restype = ctypes.c_int
+        lib.atg_decoder_set_frame_hypothesis.argtypes = [P, ctypes.c_int]
+        lib.atg_decoder_set_frame_hypothesis.restype = ctypes.c_int
+        lib.atg_decoder_frame_hypothesis_redos.argtypes = [P]
+        lib.atg_decoder_frame_hypothesis_redos.restype = c_u64
         lib.atg_decoder_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -796,6 +801,15 @@ class Decoder(object):
     def set_inflight(self, n):
         """decode batches decode_device_async keeps in flight (3..16)"""
         self._check(self.lib.atg_decoder_set_inflight(self.handle, int(n)))
+
+    def set_frame_hypothesis(self, mode):
+        """the parse's frame-end hypothesis: 0 off (every subframe walked),
+        1 on (default), 2 on with every batch redone (self-check)"""
+        self._check(self.lib.atg_decoder_set_frame_hypothesis(self.handle, int(mode)))
+
+    def frame_hypothesis_redos(self):
+        """batches redone with the full parse after a failed check"""
+        return int(self.lib.atg_decoder_frame_hypothesis_redos(self.handle))
 
     def decode(self, data, tracks, fetch_pcm=True):
         """decode a batch in host memory.  data: bytes-like holding every

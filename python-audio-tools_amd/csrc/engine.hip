@@ -237,6 +237,9 @@ constexpr uint64_t kRollMinDepth = 4;
 // a 512 MiB chunk, longer than the next two uploads)
 constexpr uint64_t kHostStages = kEncSlots + 1;
 
+// bytes per device-to-host copy of a batch's track results (section 3)
+constexpr size_t kResultCopy = 8192;
+
 // one stage of the host pipeline (chunk c uses stage c % kHostStages)
 struct HostStage {
     DevBuf d_pcm, d_img, d_pack, d_off;
@@ -707,8 +710,12 @@ atg_status batch_end_queue(atg_engine *e, EncSlot &sl, hipEvent_t after)
         HIP_TRY(launch_stream_header(p, dtr, dto, sl.pend_out, q));
     HIP_TRY(hipEventRecord(ev[13], q));
     HIP_TRY(hipEventRecord(ev[15], q));
-    if (nt)
-        HIP_TRY(hipMemcpyAsync(sl.tout_h, dto, nt * sizeof(TrackOut), hipMemcpyDeviceToHost, q));
+    // the track results in 8 KiB copies: one 32 KiB copy per 1024-track
+    // batch measured 8.10-8.12 ms per step, 8 KiB pieces 8.01-8.04
+    // (profiles/r05_zz_dec_spec.txt; past 16 KiB a copy takes another path)
+    for (size_t o = 0, nb = nt * sizeof(TrackOut); o < nb; o += kResultCopy)
+        HIP_TRY(hipMemcpyAsync((uint8_t *)sl.tout_h + o, (const uint8_t *)dto + o,
+                               std::min<size_t>(kResultCopy, nb - o), hipMemcpyDeviceToHost, q));
     if (sl.want_fdesc && nf)
         HIP_TRY(hipMemcpyAsync(sl.fdesc_h, sl.fdesc.p, nf * sizeof(FrameDesc),
                                hipMemcpyDeviceToHost, q));

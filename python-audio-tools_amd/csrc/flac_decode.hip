@@ -101,8 +101,10 @@ struct DecFrame {
     uint32_t n;         // samples per channel decoded (MIN(bs, remaining))
     uint32_t track;
     uint32_t bs;
-    uint8_t assign, ch, bps, pad;
+    uint8_t assign, ch, bps, spec; // spec: length from the frame-end hypothesis
     uint32_t sub_bit[8];
+    uint32_t bytes;     // whole frame incl. CRC-16
+    uint32_t pad;
 };
 
 struct Hdr {
@@ -904,15 +906,19 @@ __device__ uint32_t crc16_range(const uint32_t *w, uint64_t b0, uint64_t b1,
 // one frame of the reference's read() loop, parse only: header, subframes
 // with N = MIN(block size, nlimit), byte align, CRC-16
 // CRC = false: the frame's CRC-16 is left to k_dec_crc (status stays OK)
+// spec_bytes != 0: the frame-end hypothesis (k_dec_spec) -- the last
+// subframe is not walked when the ones before it end inside the frame; the
+// record then carries the hypothesis (pad = 1, CRC-16 already checked)
 template <bool RING = false, bool CRC = true>
 __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const DecTrack &t,
                             uint64_t nlimit, const uint16_t (*T)[256], ParseRec &rec,
-                            uint32_t *ring = nullptr)
+                            uint32_t *ring = nullptr, uint32_t spec_bytes = 0)
 {
     BitR r;
     r.init(w, nw, pos * 8, t.end * 8);
     Hdr h;
     rec.bytes = 0;
+    rec.pad = 0;
     rec.status = dec_header(r, t, h);
     if (rec.status)
         return;
@@ -923,6 +929,13 @@ __device__ void parse_frame(const uint32_t *w, uint64_t nw, uint64_t pos, const 
     const uint32_t N = (uint32_t)((uint64_t)h.bs < nlimit ? (uint64_t)h.bs : nlimit);
     for (uint32_t c = 0; c < h.ch; ++c) {
         rec.sub_bit[c] = (uint32_t)(r.abspos() - pos * 8);
+        if (spec_bytes && c + 1u == h.ch && N == h.bs &&
+            (uint64_t)rec.sub_bit[c] + 8u <= 8ull * (spec_bytes - 2u)) {
+            rec.bytes = spec_bytes;
+            rec.status = FD_OK;
+            rec.pad = 1;
+            return;
+        }
         const int rc = parse_subframe<RING>(r, N, sub_bps(h.assign, c, h.bps), ring);
         if (rc) {
             rec.status = rc;
@@ -1067,7 +1080,9 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint32_t *__restrict__ w,
                                                  uint64_t hcap, const uint64_t *__restrict__ hits,
                                                  uint32_t *__restrict__ ncand, uint32_t cap,
                                                  uint64_t *__restrict__ cand_pos,
-                                                 uint32_t *__restrict__ cand_idx)
+                                                 uint32_t *__restrict__ cand_idx,
+                                                 uint32_t *__restrict__ cand_trk,
+                                                 unsigned long long *__restrict__ cbits)
 {
     const uint64_t n = min((uint64_t)*nhit, hcap);
     for (uint64_t h = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; h < n;
@@ -1088,7 +1103,10 @@ __global__ __launch_bounds__(256) void k_dec_hdr(const uint32_t *__restrict__ w,
         if (i < cap) { // over capacity: the host re-scans with room for all
             cand_pos[i] = p;
             cand_idx[p] = i;
+            cand_trk[i] = t;
         }
+        if (cbits) // the candidate bitmap of the frame-end hypothesis (k_dec_spec)
+            atomicOr(&cbits[p >> 6], 1ull << (p & 63u));
     }
 }
 
@@ -1097,18 +1115,21 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
                                                   const DecTrack *__restrict__ tr, uint32_t nt,
                                                   const uint32_t *__restrict__ ncand,
                                                   const uint64_t *__restrict__ cand_pos,
+                                                  const uint32_t *__restrict__ cand_trk,
+                                                  const uint32_t *__restrict__ spec,
                                                   ParseRec *__restrict__ recs)
 {
     __shared__ __align__(16) uint32_t ring[64 * kRingStride]; // the lanes' residual-word rings
     const uint32_t n = *ncand;
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < n; i += gridDim.x * blockDim.x) {
         const uint64_t p = cand_pos[i];
-        const DecTrack t = tr[find_track(tr, nt, p)];
+        const DecTrack t = tr[cand_trk[i]];
         ParseRec rec;
         // (the frame's CRC-16 is k_dec_crc's; 6: timing experiment, residual
         // words straight from global memory)
         parse_frame<ATG_DEC_EXP != 6, false>(w, nw, p, t, ~0ull, nullptr, rec,
-                                             ring + threadIdx.x * kRingStride);
+                                             ring + threadIdx.x * kRingStride,
+                                             spec ? spec[i] : 0u);
         recs[i] = rec;
     }
 }
@@ -1135,12 +1156,84 @@ __device__ __forceinline__ uint32_t be32_at(const uint32_t *w, uint64_t last, ui
     return (x << (8u * r)) | (y >> (32u - 8u * r));
 }
 
-// K2b: CRC-16 of every parsed candidate frame (header to CRC bytes, whose
-// residue is 0 for an intact frame), a wave per frame: 64 chunks of
-// Lc = 2^m bytes of a virtually zero-prefixed image (leading zeros leave a
-// zero-init CRC unchanged), slicing by 4 from LDS tables, tree-combined with
-// the advance matrices.  The serial per-lane CRC in k_dec_parse cost 0.8 of
-// its 4.7 ms (profiles/r04_h_dec_probe.jsonl, ATG_DEC_EXP 3).
+// CRC-16 residue of bytes [pos, pos + L) on one wave (0 for an intact
+// frame: header to CRC bytes): 64 chunks of Lc = 2^m bytes of a virtually
+// zero-prefixed image (leading zeros leave a zero-init CRC unchanged),
+// slicing by 4 from LDS tables, tree-combined with the advance matrices.
+// Wave-uniform arguments; the result is returned in every lane.
+__device__ uint32_t wave_crc16(const uint32_t *__restrict__ w, uint64_t nw, uint64_t pos, uint32_t L,
+                               const uint16_t (*T)[256], uint32_t lane)
+{
+    if (L > (64u << 17)) { // beyond any real frame (the matrices reach 2^23)
+        const uint32_t c = lane == 0 ? crc16_range(w, pos, pos + L, T) : 0u;
+        return (uint32_t)__shfl((int)c, 0, 64);
+    }
+    uint32_t lc_log = 2;
+    while ((64u << lc_log) < L)
+        lc_log++;
+    const uint32_t Lc = 1u << lc_log;
+    const int64_t z = (int64_t)(64u << lc_log) - (int64_t)L;
+    uint32_t crc = 0;
+    int64_t q = (int64_t)lane * Lc - z; // image byte of this lane's first group
+    const int64_t qe = q + Lc;
+    if (q < 0) { // groups in the zero prefix leave crc = 0
+        q += ((-q) >> 2) << 2; // now -4 < q <= 0
+        if (q < 0 && q < qe) {
+            const uint32_t t = be32_at(w, nw - 1, pos) >> (8u * (uint32_t)(-q));
+            crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
+                  T[0][t & 0xFFu];
+            q += 4;
+        }
+    }
+    // 256 bytes at a time: the 65 aligned words under them loaded at once
+    // (one memory latency per 256 bytes of the lane's chunk -- the wave
+    // spent 94 % of its cycles waiting with a latency per 64 bytes,
+    // profiles/r04_k_dec_pmc.txt), then the 64 big-endian words
+    for (; q + 256 <= qe; q += 256) {
+        const uint64_t b0 = pos + (uint64_t)q, i0 = b0 >> 2;
+        const uint32_t sb = 8u * (uint32_t)(b0 & 3);
+        uint32_t x[65];
+#pragma unroll
+        for (int u = 0; u < 65; ++u)
+            x[u] = bswap32(w[i0 + u < nw - 1 ? i0 + u : nw - 1]);
+#pragma unroll
+        for (int u = 0; u < 64; ++u) {
+            const uint32_t wd = sb ? (x[u] << sb) | (x[u + 1] >> (32u - sb)) : x[u];
+            const uint32_t t = wd ^ (crc << 16);
+            crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
+                  T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
+        }
+    }
+    for (; q + 64 <= qe; q += 64) {
+        uint32_t x[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+            x[u] = be32_at(w, nw - 1, pos + (uint64_t)(q + 4 * u));
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+            const uint32_t t = x[u] ^ (crc << 16);
+            crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
+                  T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
+        }
+    }
+    for (; q < qe; q += 4) {
+        const uint32_t t = be32_at(w, nw - 1, pos + (uint64_t)q) ^ (crc << 16);
+        crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
+              T[0][t & 0xFFu];
+    }
+#pragma unroll
+    for (int k = 0; k < 6; ++k) {
+        const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << k, 64);
+        if ((lane & ((2u << k) - 1u)) == 0)
+            crc = dcrc_adv(crc, (int)lc_log + k) ^ other;
+    }
+    return (uint32_t)__shfl((int)crc, 0, 64);
+}
+
+// K2b: CRC-16 of every parsed candidate frame whose length the parse walked
+// (a wave per frame, wave_crc16; frames the speculative pass measured are
+// checked already).  The serial per-lane CRC in k_dec_parse cost 0.8 of its
+// 4.7 ms (profiles/r04_h_dec_probe.jsonl, ATG_DEC_EXP 3).
 __global__ __launch_bounds__(256) void k_dec_crc(const uint32_t *__restrict__ w, uint64_t nw,
                                                  const uint32_t *__restrict__ ncand,
                                                  const uint64_t *__restrict__ cand_pos,
@@ -1153,75 +1246,80 @@ __global__ __launch_bounds__(256) void k_dec_crc(const uint32_t *__restrict__ w,
     for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
         const int st = recs[i].status;
         const uint32_t L = recs[i].bytes;
-        if (st != FD_OK || L < 2u) // wave-uniform: one candidate per wave
+        if (st != FD_OK || L < 2u || recs[i].pad) // wave-uniform: one candidate per wave
             continue;
-        const uint64_t pos = cand_pos[i];
-        if (L > (64u << 17)) { // beyond any real frame (the matrices reach 2^23)
-            if (lane == 0 && crc16_range(w, pos, pos + L, T))
-                recs[i].status = FD_FRAME_CRC;
-            continue;
-        }
-        uint32_t lc_log = 2;
-        while ((64u << lc_log) < L)
-            lc_log++;
-        const uint32_t Lc = 1u << lc_log;
-        const int64_t z = (int64_t)(64u << lc_log) - (int64_t)L;
-        uint32_t crc = 0;
-        int64_t q = (int64_t)lane * Lc - z; // image byte of this lane's first group
-        const int64_t qe = q + Lc;
-        if (q < 0) { // groups in the zero prefix leave crc = 0
-            q += ((-q) >> 2) << 2; // now -4 < q <= 0
-            if (q < 0 && q < qe) {
-                const uint32_t t = be32_at(w, nw - 1, pos) >> (8u * (uint32_t)(-q));
-                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
-                      T[0][t & 0xFFu];
-                q += 4;
-            }
-        }
-        // 256 bytes at a time: the 65 aligned words under them loaded at once
-        // (one memory latency per 256 bytes of the lane's chunk -- the wave
-        // spent 94 % of its cycles waiting with a latency per 64 bytes,
-        // profiles/r04_k_dec_pmc.txt), then the 64 big-endian words
-        for (; q + 256 <= qe; q += 256) {
-            const uint64_t b0 = pos + (uint64_t)q, i0 = b0 >> 2;
-            const uint32_t sb = 8u * (uint32_t)(b0 & 3);
-            uint32_t x[65];
-#pragma unroll
-            for (int u = 0; u < 65; ++u)
-                x[u] = bswap32(w[i0 + u < nw - 1 ? i0 + u : nw - 1]);
-#pragma unroll
-            for (int u = 0; u < 64; ++u) {
-                const uint32_t wd = sb ? (x[u] << sb) | (x[u + 1] >> (32u - sb)) : x[u];
-                const uint32_t t = wd ^ (crc << 16);
-                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
-                      T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
-            }
-        }
-        for (; q + 64 <= qe; q += 64) {
-            uint32_t x[16];
-#pragma unroll
-            for (int u = 0; u < 16; ++u)
-                x[u] = be32_at(w, nw - 1, pos + (uint64_t)(q + 4 * u));
-#pragma unroll
-            for (int u = 0; u < 16; ++u) {
-                const uint32_t t = x[u] ^ (crc << 16);
-                crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^
-                      T[1][(t >> 8) & 0xFFu] ^ T[0][t & 0xFFu];
-            }
-        }
-        for (; q < qe; q += 4) {
-            const uint32_t t = be32_at(w, nw - 1, pos + (uint64_t)q) ^ (crc << 16);
-            crc = (uint32_t)T[3][t >> 24] ^ T[2][(t >> 16) & 0xFFu] ^ T[1][(t >> 8) & 0xFFu] ^
-                  T[0][t & 0xFFu];
-        }
-#pragma unroll
-        for (int k = 0; k < 6; ++k) {
-            const uint32_t other = (uint32_t)__shfl_down((int)crc, 1 << k, 64);
-            if ((lane & ((2u << k) - 1u)) == 0)
-                crc = dcrc_adv(crc, (int)lc_log + k) ^ other;
-        }
-        if (lane == 0 && crc)
+        if (wave_crc16(w, nw, cand_pos[i], L, T, lane) && lane == 0)
             recs[i].status = FD_FRAME_CRC;
+    }
+}
+
+// The frame-end hypothesis (K2s, before the parse): for candidate p, the
+// next candidates q (the bitmap k_dec_hdr set, bounded by the track end) in
+// turn, up to three: the first whose bytes [p, q) carry a zero CRC-16 residue
+// is taken as the frame, so the parse need not walk the frame's last
+// subframe -- its start is the end of the one before, its end is q.  A
+// frame with no such q (corrupt, cut by the window, or followed by bytes no
+// candidate starts) gets 0: the parse walks every subframe and k_dec_crc
+// checks the walked length, as before.  The restore checks every taken
+// hypothesis on the subframe it walks anyway (k_dec_subframe: no error,
+// aligned end + 16 bits == q); a failed check makes decode_wait redo the
+// batch with the full parse, so the results are the walked parse's.
+constexpr uint32_t kSpecTries = 3;
+constexpr uint32_t kSpecMaxBytes = 1u << 22;
+
+__device__ __forceinline__ uint64_t next_cand(const unsigned long long *__restrict__ cbits,
+                                              uint64_t nwords, uint64_t from, uint64_t te,
+                                              uint32_t lane)
+{
+    uint64_t wi = from >> 6;
+    bool first = true;
+    while (wi * 64u < te) {
+        const uint64_t k = wi + lane;
+        unsigned long long x = k < nwords && k * 64u < te ? cbits[k] : 0ull;
+        if (first && lane == 0)
+            x &= ~0ull << (from & 63u);
+        first = false;
+        const unsigned long long b = __ballot(x != 0ull);
+        if (b) {
+            const uint32_t f = (uint32_t)__builtin_ctzll(b);
+            const unsigned long long xf = (unsigned long long)__shfl((long long)x, (int)f, 64);
+            const uint64_t q = (wi + f) * 64u + (uint64_t)__builtin_ctzll(xf);
+            return q < te ? q : te;
+        }
+        wi += 64u;
+    }
+    return te;
+}
+
+__global__ __launch_bounds__(256) void k_dec_spec(const uint32_t *__restrict__ w, uint64_t nw,
+                                                  const DecTrack *__restrict__ tr, uint32_t nt,
+                                                  const uint32_t *__restrict__ ncand,
+                                                  const uint64_t *__restrict__ cand_pos,
+                                                  const uint32_t *__restrict__ cand_trk,
+                                                  const unsigned long long *__restrict__ cbits,
+                                                  uint64_t nwords, uint32_t *__restrict__ spec)
+{
+    __shared__ uint16_t T[4][256];
+    load_crc_lds(T);
+    const uint32_t n = *ncand;
+    const uint32_t lane = threadIdx.x & 63u;
+    for (uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6); i < n; i += gridDim.x * 4u) {
+        const uint64_t p = cand_pos[i];
+        const uint64_t te = tr[cand_trk[i]].end;
+        uint32_t out = 0;
+        uint64_t from = p + 1u;
+        for (uint32_t k = 0; k < kSpecTries && !out; ++k) {
+            const uint64_t q = next_cand(cbits, nwords, from, te, lane);
+            if (q <= p + 2u || q - p > kSpecMaxBytes)
+                break;
+            if (wave_crc16(w, nw, p, (uint32_t)(q - p), T, lane) == 0u)
+                out = (uint32_t)(q - p);
+            if (q >= te)
+                break;
+            from = q + 1u;
+        }
+        if (lane == 0)
+            spec[i] = out;
     }
 }
 
@@ -1282,6 +1380,8 @@ __global__ __launch_bounds__(64) void k_dec_chain(const uint32_t *__restrict__ w
             f.assign = rec.assign;
             f.ch = rec.ch;
             f.bps = rec.bps;
+            f.spec = rec.pad;
+            f.bytes = rec.bytes;
             f.pad = 0;
             for (int c = 0; c < 8; ++c)
                 f.sub_bit[c] = rec.sub_bit[c];
@@ -1311,7 +1411,7 @@ template <int W>
 __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, uint32_t wasted,
                                             uint32_t kind, uint32_t order, int32_t *out,
                                             int4 *row, JobMeta &m, bool allow_fast,
-                                            uint32_t *ring)
+                                            uint32_t *ring, int &rc)
 {
     WinPred<W> p;
     p.row = row;
@@ -1355,9 +1455,9 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
     p.fast = false;
 #endif
     if ((((uintptr_t)r.w) & 15u) == 0 && r.last >= kWalkInit * kRingB)
-        walk_residual<true>(r, order, N, p, ring);
+        rc = walk_residual<true>(r, order, N, p, ring);
     else
-        dec_residual<WinPred<W>, false>(r, order, N, p);
+        rc = dec_residual<WinPred<W>, false>(r, order, N, p);
     p.flush();
     m.porder = (uint8_t)p.porder;
     m.iters = p.i;
@@ -1373,7 +1473,8 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
                                                      const uint2 *__restrict__ jobs,
                                                      uint64_t njobs, int32_t *__restrict__ warm,
                                                      int32_t *__restrict__ rows, uint32_t nrows,
-                                                     JobMeta *__restrict__ meta)
+                                                     JobMeta *__restrict__ meta,
+                                                     uint32_t *__restrict__ spec_bad)
 {
     __shared__ __align__(16) uint32_t rings[64 * kRingStride]; // the lanes' residual-word rings
     uint32_t *ring = rings + threadIdx.x * kRingStride;
@@ -1398,7 +1499,8 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
     m.iters = 0;
     m.pad2 = 0;
     SubHdr sh;
-    if (dec_subhdr(r, sh) == FD_OK) {
+    int rc = dec_subhdr(r, sh);
+    if (rc == FD_OK) {
         const uint32_t bps = sub_bps(f.assign, c, f.bps) - sh.wasted;
         const uint32_t ws = sh.wasted;
         if (sh.kind == 0) {
@@ -1436,16 +1538,28 @@ __global__ __launch_bounds__(64) void k_dec_subframe(const uint32_t *__restrict_
             m.order = (uint8_t)sh.order;
             if (sh.order <= 12) {
                 const uint32_t at = r.pos;
-                if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, true, ring)) {
+                if (restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, true, ring,
+                                    rc)) {
                     r.pos = at; // a sample left the bps range: redo with int64 sums
-                    restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring);
+                    restore_win<12>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring,
+                                    rc);
                 }
             } else {
-                restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring);
+                restore_win<32>(r, N, bps, ws, sh.kind, sh.order, out, row, m, false, ring, rc);
             }
+            if (sh.kind == 2 && sh.order > 4)
+                rc = FD_FIXED_ORDER;
         }
     }
     meta[j] = m;
+    // the frame-end hypothesis (k_dec_spec) on the subframe the parse did
+    // not walk: the walk the parse would have made must end, byte-aligned,
+    // 16 bits before the hypothesised end, without an error
+    if (f.spec && c + 1u == f.ch) {
+        const uint64_t e = r.abspos() - f.pos * 8u;
+        if (rc != FD_OK || r.eof() || ((e + 7u) >> 3) + 2u != (uint64_t)f.bytes)
+            *spec_bad = 1u;
+    }
 }
 
 // K5: rows -> samples -> flacdec_decorrelate_channels (flac.c:1212-1269) ->
@@ -1587,7 +1701,8 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
                 // (src/pcm.c:1826-1948): only a corrupt stream can produce them
                 const int32_t v0 = o0 > hi ? hi : (o0 < lo ? lo : o0);
                 const int32_t v1 = o1 > hi ? hi : (o1 < lo ? lo : o1);
-                if (bb == 2) {
+                if (ATG_DEC_EXP == 8) { // timing experiment: no MD5 byte image
+                } else if (bb == 2) {
                     *(uint32_t *)bdst = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
                 } else {
                     for (uint32_t q = 0; q < bb; ++q) {
@@ -1697,6 +1812,11 @@ struct DecSlot {
     bool rolled = false;
     uint32_t roll_parts = 0, roll_done = 0;
     uint32_t n_md5 = 0; // streams hashed (the batch's track count)
+    // the batch's input (decode_wait redoes it with the full parse when a
+    // frame-end hypothesis fails the restore's check)
+    const uint8_t *data = nullptr;
+    uint64_t len = 0;
+    bool spec = false; // k_dec_spec ran for this batch
 };
 
 struct atg_decoder {
@@ -1706,6 +1826,11 @@ struct atg_decoder {
     float times[kDecTimed] = {};
     bool have_times = false;
     DBuf data, tracks, counts, ncand, cand_pos, cand_idx, recs, hits, segs;
+    DBuf cand_trk;    // each candidate's track (k_dec_hdr)
+    DBuf cbits, spec; // the frame-end hypothesis: candidate bitmap, lengths
+    int spec_mode = 1; // atg_decoder_set_frame_hypothesis
+    uint64_t spec_redos = 0; // batches redone with the full parse
+    bool spec_off = false; // set while a batch is redone with the full parse
     std::vector<ScanSeg> segs_h; // the scan's segments (upload source)
     DecSlot slot[kDecMaxSlots];
     int depth = kDecSlots;          // slots in rotation (atg_decoder_set_inflight)
@@ -1926,7 +2051,7 @@ void atg_decoder_destroy(atg_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBuf *b : {&d->data, &d->tracks, &d->counts, &d->ncand, &d->cand_pos, &d->cand_idx,
-                    &d->recs, &d->hits, &d->segs})
+                    &d->recs, &d->hits, &d->segs, &d->cbits, &d->spec, &d->cand_trk})
         b->release();
     if (d->s_roll)
         (void)hipStreamSynchronize(d->s_roll);
@@ -1953,6 +2078,21 @@ void atg_decoder_destroy(atg_decoder *d)
 
 } // extern "C"
 
+// the digests and the restore's hypothesis check word to the host, as two
+// copies: one copy of 16 n + 16 bytes (16,400 at 1024 tracks) instead of the
+// 16,384-byte digest copy put ~1 ms on every config-2 decode step
+// (profiles/r05_zz_dec_spec.txt) -- past 16 KiB the copy takes another path
+static hipError_t dec_results_d2h(DecSlot &sl, uint32_t n, hipStream_t q)
+{
+    if (!n)
+        return hipSuccess;
+    hipError_t e = hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost, q);
+    if (e == hipSuccess)
+        e = hipMemcpyAsync(sl.md5_h + 16 * (size_t)n, (uint8_t *)sl.md5.p + 16 * (size_t)n, 16,
+                           hipMemcpyDeviceToHost, q);
+    return e;
+}
+
 // the tail of a rolled batch on s_roll: tails + padding + digests, the
 // digests to the host, done
 static atg_status dec_roll_tail(atg_decoder *d, DecSlot &sl)
@@ -1962,9 +2102,7 @@ static atg_status dec_roll_tail(atg_decoder *d, DecSlot &sl)
                                  (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p,
                                  d->s_roll));
     DHIP(hipEventRecord(sl.ev[7], d->s_roll));
-    if (n)
-        DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
-                            d->s_roll));
+    DHIP(dec_results_d2h(sl, n, d->s_roll));
     DHIP(hipEventRecord(sl.ev_done, d->s_roll));
     return ATG_OK;
 }
@@ -2040,7 +2178,14 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
         b.max_bs = a.max_block_size;
     }
     sl.want.assign(tracks, tracks + n);
+    sl.data = d_data;
+    sl.len = len;
     const uint64_t nw = std::max<uint64_t>(1, (len + 3) / 4);
+    // the frame-end hypothesis (k_dec_spec): a bit per byte of the buffer
+    const bool use_spec = d->spec_mode != 0 && !d->spec_off && n && len;
+    const uint64_t nbw = (len >> 6) + 2;
+    if (use_spec)
+        DHIP(d->cbits.ensure(sizeof(uint64_t) * nbw));
     DHIP(d->tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
     DHIP(d->counts.ensure(sizeof(DecCount) * std::max<uint32_t>(n, 1)));
     DHIP(d->ncand.ensure(2 * sizeof(uint32_t)));
@@ -2097,8 +2242,11 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     uint64_t hcap = cap;
     for (int pass = 0; pass < 3; ++pass) {
         DHIP(d->cand_pos.ensure(sizeof(uint64_t) * cap));
+        DHIP(d->cand_trk.ensure(sizeof(uint32_t) * cap));
         DHIP(d->hits.ensure(sizeof(uint64_t) * hcap));
         DHIP(hipMemsetAsync(d->ncand.p, 0, 2 * sizeof(uint32_t), s));
+        if (use_spec)
+            DHIP(hipMemsetAsync(d->cbits.p, 0, sizeof(uint64_t) * nbw, s));
         // grid-stride: at most 8 workgroups of 256 per CU (2048 over 256 CUs)
         if (n && len) {
             hipLaunchKernelGGL(k_dec_sync, dim3((unsigned)std::min<uint64_t>(nseg, 2048)),
@@ -2109,7 +2257,8 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
                                dim3(256), 0, s, w, nw, len, dtr, n,
                                (const uint32_t *)d->ncand.p + 1, hcap, (const uint64_t *)d->hits.p,
                                (uint32_t *)d->ncand.p, (uint32_t)cap, (uint64_t *)d->cand_pos.p,
-                               (uint32_t *)d->cand_idx.p);
+                               (uint32_t *)d->cand_idx.p, (uint32_t *)d->cand_trk.p,
+                               use_spec ? (unsigned long long *)d->cbits.p : nullptr);
         }
         DHIP(hipGetLastError());
         DHIP(hipMemcpyAsync(cnt_h, d->ncand.p, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -2126,9 +2275,19 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     }
     DHIP(d->recs.ensure(sizeof(ParseRec) * std::max<uint64_t>(found, 1)));
     DHIP(hipEventRecord(ev[1], s));
+    sl.spec = use_spec && found;
+    if (sl.spec) {
+        DHIP(d->spec.ensure(sizeof(uint32_t) * found));
+        hipLaunchKernelGGL(k_dec_spec, dim3((unsigned)std::min<uint64_t>((found + 3) / 4, 8192)),
+                           dim3(256), 0, s, w, nw, dtr, n, (const uint32_t *)d->ncand.p,
+                           (const uint64_t *)d->cand_pos.p, (const uint32_t *)d->cand_trk.p,
+                           (const unsigned long long *)d->cbits.p, nbw, (uint32_t *)d->spec.p);
+        DHIP(hipGetLastError());
+    }
     hipLaunchKernelGGL(k_dec_parse, dim3(4096), dim3(64), 0, s, w, nw, dtr, n,
                        (const uint32_t *)d->ncand.p, (const uint64_t *)d->cand_pos.p,
-                       (ParseRec *)d->recs.p);
+                       (const uint32_t *)d->cand_trk.p,
+                       sl.spec ? (const uint32_t *)d->spec.p : nullptr, (ParseRec *)d->recs.p);
     DHIP(hipGetLastError());
     if (found)
         hipLaunchKernelGGL(k_dec_crc, dim3((unsigned)std::min<uint64_t>((found + 3) / 4, 8192)),
@@ -2178,7 +2337,8 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     DHIP(sl.meta.ensure(sizeof(JobMeta) * std::max<uint64_t>(jb, 1)));
     DHIP(sl.pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(pb, 1)));
     DHIP(sl.bytes.ensure(std::max<uint64_t>(mb, 64)));
-    DHIP(sl.md5.ensure(16 * std::max<uint32_t>(n, 1)));
+    // the digests, then the restore's hypothesis check word (16 n)
+    DHIP(sl.md5.ensure(16 * (size_t)n + 16));
     // the placed track table: the slot's own copy (the next batch re-uploads
     // the decoder's while this one restores)
     DHIP(sl.tracks.ensure(sizeof(DecTrack) * std::max<uint32_t>(n, 1)));
@@ -2197,12 +2357,14 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     sl.rolled = d->depth > kDecSlots;
     hipStream_t ss = sl.rolled ? d->slot[sl.ticket % kDecSlots].s_md5 : sl.s_md5;
     DHIP(hipStreamWaitEvent(ss, sl.ev_chain, 0));
+    uint32_t *spec_bad = (uint32_t *)((uint8_t *)sl.md5.p + 16 * (size_t)n);
+    DHIP(hipMemsetAsync(spec_bad, 0, 16, ss));
     DHIP(hipEventRecord(ev[3], ss));
     if (jb)
         hipLaunchKernelGGL(k_dec_subframe, dim3((unsigned)((jb + 63) / 64)), dim3(64), 0, ss, w,
                            nw, (const DecTrack *)str, (const DecFrame *)sl.frames.p,
                            (const uint2 *)sl.jobs.p, jb, (int32_t *)sl.warm.p,
-                           (int32_t *)sl.rows.p, nrows, (JobMeta *)sl.meta.p);
+                           (int32_t *)sl.rows.p, nrows, (JobMeta *)sl.meta.p, spec_bad);
     DHIP(hipGetLastError());
     DHIP(hipEventRecord(ev[4], ss));
     if (jb)
@@ -2223,14 +2385,13 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
         sl.md5_meta[n + t] = vis * tr[t].channels * ((tr[t].bps + 7) / 8);
     }
     DHIP(sl.md5meta.ensure(sizeof(uint64_t) * 2 * std::max<uint32_t>(n, 1)));
-    if (sl.md5_cap < 16 * (size_t)std::max<uint32_t>(n, 1)) {
+    if (sl.md5_cap < 16 * (size_t)n + 16) {
         if (sl.md5_h)
             (void)hipHostFree(sl.md5_h);
         sl.md5_h = nullptr;
         sl.md5_cap = 0;
-        DHIP(hipHostMalloc((void **)&sl.md5_h, 16 * (size_t)std::max<uint32_t>(n, 1),
-                           hipHostMallocDefault));
-        sl.md5_cap = 16 * (size_t)std::max<uint32_t>(n, 1);
+        DHIP(hipHostMalloc((void **)&sl.md5_h, 16 * (size_t)n + 16, hipHostMallocDefault));
+        sl.md5_cap = 16 * (size_t)n + 16;
     }
     if (n)
         DHIP(hipMemcpyAsync(sl.md5meta.p, sl.md5_meta.data(), sizeof(uint64_t) * 2 * n,
@@ -2254,9 +2415,7 @@ static atg_status enqueue_decode(atg_decoder *d, DecSlot &sl, const uint8_t *d_d
     DHIP(launch_bytes_md5((const uint8_t *)sl.bytes.p, (const uint64_t *)sl.md5meta.p,
                           (const uint64_t *)sl.md5meta.p + n, n, (uint8_t *)sl.md5.p, sl.s_md5));
     DHIP(hipEventRecord(ev[7], sl.s_md5));
-    if (n)
-        DHIP(hipMemcpyAsync(sl.md5_h, sl.md5.p, 16 * (size_t)n, hipMemcpyDeviceToHost,
-                            sl.s_md5));
+    DHIP(dec_results_d2h(sl, n, sl.s_md5));
     DHIP(hipEventRecord(sl.ev_done, sl.s_md5));
     return ATG_OK;
 }
@@ -2271,6 +2430,22 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
             return st;
     }
     DHIP(hipEventSynchronize(sl.ev_done));
+    const size_t nt = sl.tr.size();
+    if (sl.spec && nt && (*(const uint32_t *)(sl.md5_h + 16 * nt) || d->spec_mode == 2)) {
+        // a frame-end hypothesis failed the restore's check (or the
+        // self-check mode): the batch again with every subframe walked
+        const std::vector<atg_flac_dec_track> want = sl.want;
+        d->spec_off = true;
+        atg_status st = enqueue_decode(d, sl, sl.data, sl.len, want.data(), (uint32_t)want.size());
+        d->spec_off = false;
+        if (st != ATG_OK)
+            return st;
+        while (sl.rolled && sl.roll_done < sl.roll_parts)
+            if ((st = dec_roll_step(d, nullptr)) != ATG_OK)
+                return st;
+        DHIP(hipEventSynchronize(sl.ev_done));
+        ++d->spec_redos;
+    }
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
     // emit, md5, total (scan start -> md5 end)
     const int map[kDecTimed][2] = {{0, 1}, {1, 2}, {2, 3}, {3, 4}, {4, 5}, {6, 7}, {0, 7}};
@@ -2476,6 +2651,21 @@ atg_status atg_decoder_set_inflight(atg_decoder *d, uint32_t n)
     d->depth = (int)n;
     d->last = -1; // the oldest-slot rotation starts over
     return ATG_OK;
+}
+
+atg_status atg_decoder_set_frame_hypothesis(atg_decoder *d, int mode)
+{
+    ATG_HANDLE_LOCK(d);
+    if (!d || mode < 0 || mode > 2)
+        return dfail(ATG_ERR_INVALID, "frame hypothesis mode must be 0, 1 or 2");
+    d->spec_mode = mode;
+    return ATG_OK;
+}
+
+uint64_t atg_decoder_frame_hypothesis_redos(atg_decoder *d)
+{
+    ATG_HANDLE_LOCK(d);
+    return d ? d->spec_redos : 0;
 }
 
 int atg_decoder_kernel_times(atg_decoder *d, const char **names, float *ms, int cap)
