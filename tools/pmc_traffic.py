@@ -19,10 +19,11 @@ names = {"k_lpc_analyze": "lpc_analyze", "k_subframe_search": "subframe_search",
          "k_subframe_search_list": "subframe_search",
          "k_frame_decide": "frame_decide", "k_track_scan": "track_scan",
          "k_frame_pack": "frame_pack", "k_track_md5": "track_md5", "k_track_md5_pair": "track_md5",
+         "k_track_md5_roll": "track_md5",
          "k_stream_header": "stream_header",
          # decoder (flac_decode.hip, md5.hip)
          "k_dec_scan": "dec_scan", "k_dec_sync": "dec_scan", "k_dec_hdr": "dec_scan",
-         "k_dec_parse": "dec_parse", "k_dec_crc": "dec_parse", "k_dec_chain": "dec_chain",
+         "k_dec_parse": "dec_parse", "k_dec_crc": "dec_parse", "k_dec_spec": "dec_parse", "k_dec_chain": "dec_chain",
          "k_dec_subframe": "dec_subframe", "k_dec_emit": "dec_emit",
          "k_bytes_md5": "dec_md5", "k_bytes_md5_pair": "dec_md5", "k_bytes_md5_roll": "dec_md5",
          "k_pcm_bps": "pcm_bps",
