@@ -1,7 +1,7 @@
 #!/bin/bash
 # GPU-box recipe: encoder change check.  The FLAC encoder GPU suites, then
 # two encoder-only bench runs (30 steps), then (RQ=1) the host-leg copy
-# timeline (tools/gpu_r5q.sh).
+# timeline (tools/gpu_host_copytrace.sh).
 set -e -o pipefail
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT="$R/gpurun_out/${1:-r5r}"
@@ -15,5 +15,5 @@ for k in 1 2; do
         --no-chain --no-decode --no-t2t --no-rg4 --narrow= > "$OUT/bench$k.log" 2>&1
 done
 if [ "${RQ:-0}" = 1 ]; then
-    bash tools/gpu_r5q.sh "${1:-r5r}_q"
+    bash tools/gpu_host_copytrace.sh "${1:-r5r}_q"
 fi

@@ -1,4 +1,4 @@
-"""print the narrow-batch leg of a bench JSON line (tools/gpu_r5b.sh)"""
+"""print the narrow-batch leg of a bench JSON line (tools/gpu_narrow.sh)"""
 import json
 import sys
 
