@@ -123,3 +123,49 @@ def test_wrong_hypothesis_is_caught_and_redone(gpu_engine):
     _same(got[0], got[1])
     assert got[1][4] == 1  # the hypothesis failed its check: one redo
     assert got[0][0][0][0] != 0  # the full parse stops at the junk
+
+
+@pytest.mark.parametrize("depth", [3, 6])
+def test_redo_inside_a_pipeline(gpu_engine, depth):
+    """device batches in flight (rolled MD5 from 4 on), every other batch
+    holding the stream whose first frame is followed by junk: the failed
+    check redoes that batch inside its decode_wait while the others stay in
+    flight; every batch's results and PCM equal the full parse's"""
+    import torch
+    from audiotools import _atgpu
+    opts = _atgpu.make_options(**oracle_port.PRESETS["8"])
+    pcm = signals.make("tone", 4096 * 6 + 55, 2, 16, seed=12)
+    out, res, _, _ = gpu_engine.encode(opts, pcm.astype(np.int16), [(0, len(pcm) // 2)], 2, 16,
+                                       44100)
+    img = out[res[0].out_offset:res[0].out_offset + res[0].bytes].tobytes()
+    rc, si, _ = _atgpu.read_metadata(img)
+    tracks, blob = _batch([img])
+    _, _, offs, _ = _atgpu.Decoder(0).decode(blob, tracks)
+    cut = si.frames_offset + int(offs[1])
+    bad = img[:cut] + b"\0\0" + img[cut:]
+    batches = [_batch([img, bad, img]), _batch([img, img])]
+    dev = []
+    for tr, bl in batches:
+        d = torch.frombuffer(bytearray(bl + b"\0" * 64), dtype=torch.uint8).cuda()
+        dev.append((d, len(bl), tr))
+    torch.cuda.synchronize()
+    ref = _atgpu.Decoder(0)
+    ref.set_frame_hypothesis(0)
+    want = [[_key(r) for r in ref.decode_device(d.data_ptr(), n, tr)[0]] for d, n, tr in dev]
+    ref.close()
+    dec = _atgpu.Decoder(0)
+    dec.set_inflight(depth)
+    pending = []
+    for i in range(depth + 4):
+        if len(pending) == depth:
+            j, t = pending.pop(0)
+            got, _, _ = dec.decode_wait(t)
+            assert [_key(r) for r in got] == want[j % 2], j
+        d, n, tr = dev[i % 2]
+        pending.append((i, dec.decode_device_async(d.data_ptr(), n, tr)))
+    for j, t in pending:
+        got, _, _ = dec.decode_wait(t)
+        assert [_key(r) for r in got] == want[j % 2], j
+    # one redo per batch holding the junk stream
+    assert dec.frame_hypothesis_redos() == (depth + 5) // 2
+    dec.close()
