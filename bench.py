@@ -347,10 +347,10 @@ def decode_leg(args, torch, dist, world, device, eng, out, res, pcm, pcm_host, n
     kt_sum = {}
 
     def run(k_steps, timed):
-        # three batches in flight (atg_flac_decode_device_async): batch k's
-        # restore, emit and per-track MD5 run on its slot's stream under
-        # batch k+1's scan and parse; every batch is waited (drained) inside
-        # the timed region
+        # dec_inflight batches in flight (atg_flac_decode_device_async):
+        # batch k's restore and emit run under batch k+1's scan and parse,
+        # its MD5 hashes rolled over the batches behind it from 4 in flight
+        # on; every batch is waited (drained) inside the timed region
         pending, last = [], None
 
         def wait_one():
