@@ -1235,12 +1235,15 @@ def selftest(args):
 
 def strong_depth(n_tracks):
     """batches in flight for a rank batch of n_tracks config-2 tracks: the
-    kernels of a batch take ~8.3 ms x n/1024, its MD5 chains ~12.5 ms
+    kernels of a batch take ~8 ms x n/1024, its MD5 chains ~12.5 ms
     whatever n, so a narrow batch needs chain / kernels + 2 batches in
     flight (rolled MD5 slices the chain over depth - 2 enqueues); measured
-    best: 24 up to 128 tracks, 32 up to 256, 16 up to 512
-    (profiles/r05_narrow.json, r05_zm_narrow_depth.json)"""
-    return 24 if n_tracks <= 128 else 32 if n_tracks <= 256 else 16 if n_tracks <= 512 else 3
+    best in the three final round-5 runs (narrow leg, 16/24/32 in flight):
+    32 up to 256 tracks (128: 5.91-5.94 M frames/s against 5.76-5.83 at
+    24), 24 up to 512 (8.12-8.15 M against 7.95-8.05 at 16), 12 above
+    (the headline's depth; profiles/r05_zz_final_bench.json,
+    r05_zm_narrow_depth.json)"""
+    return 32 if n_tracks <= 256 else 24 if n_tracks <= 512 else 12
 
 
 def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_full, res_full,
