@@ -806,8 +806,9 @@ RgBound rg_bound(int fi, uint64_t L)
     return b;
 }
 
-// the counted length of a track's (non-last) segments, as plan_segments cuts them
-uint64_t rg_seg_len(uint32_t wsz)
+// the counted length of a track's (non-last) segments, as plan_segments cuts
+// them: at least `windows` whole windows, a multiple of 10 frames
+uint64_t rg_seg_len(uint32_t wsz, uint32_t windows = kRgSegWindows)
 {
     uint32_t g10 = 10;
     for (uint32_t x = wsz % 10, y = 10; x;) { // gcd(wsz, 10)
@@ -817,18 +818,57 @@ uint64_t rg_seg_len(uint32_t wsz)
         g10 = y;
     }
     uint32_t K = 10 / g10;
-    while (K < kRgSegWindows)
+    while (K < windows)
         K += 10 / g10;
     return (uint64_t)K * wsz;
+}
+
+// Windows per segment for a batch.  A lane filters one segment (its warm-up
+// plus its counted frames) as one serial chain, so a batch takes about
+// max(segment length, lanes x segment length / P) chain steps, P ~ one wave
+// per SIMD (65,536 lanes).  Few long tracks want short segments (more
+// lanes), many want long ones (less warm-up): config 2's title analysis
+// (1024 x 262,144 frames) measured 8.74 / 5.28 / 5.20 ms at 4 / 2 / 1
+// windows, config 4's album scan (1024 x 441,000) 7.37 / 9.78 / 9.73
+// (profiles/r05_zz_rg_segments.txt).  Batches of fewer than 8192 lanes at
+// the default keep it.
+uint32_t rg_seg_windows(const std::vector<RgTrack> &tr, const atg_rg_track *a, uint32_t n)
+{
+    constexpr double kLanes = 65536.0;
+    auto cost = [&](uint32_t K, double &lanes) {
+        lanes = 0.0;
+        double seg = 0.0;
+        for (uint32_t t = 0; t < n; ++t) {
+            const uint64_t L = rg_seg_len(tr[t].window, K);
+            const uint64_t warm = ((uint64_t)kRgWarm44 * a[t].sample_rate / 44100 + 9) / 10 * 10;
+            lanes += (double)((tr[t].frames + L - 1) / L);
+            seg = std::max(seg, (double)(L + warm));
+        }
+        return std::max(seg, lanes * seg / kLanes);
+    };
+    double lanes4 = 0.0;
+    const double c4 = cost(kRgSegWindows, lanes4);
+    if (lanes4 < 8192.0 || g_rg_warm_override >= 0)
+        return kRgSegWindows;
+    uint32_t best = kRgSegWindows;
+    double bc = c4, l = 0.0;
+    for (uint32_t K : {2u, 1u}) {
+        const double c = cost(K, l);
+        if (c < bc) {
+            bc = c;
+            best = K;
+        }
+    }
+    return best;
 }
 
 // the segments of track t (appended to `out`): whole windows, a multiple
 // of 10 frames long (the filter's ring cycle), warm-up a multiple of 10
 void plan_segments(uint32_t t, const RgTrack &T, const atg_rg_track &a, bool exact_only,
-                   std::vector<RgSeg> &out, uint32_t &first_warm_window)
+                   std::vector<RgSeg> &out, uint32_t &first_warm_window, uint32_t windows)
 {
     const uint32_t wsz = T.window;
-    const uint64_t L = exact_only ? T.frames + 10 : rg_seg_len(wsz);
+    const uint64_t L = exact_only ? T.frames + 10 : rg_seg_len(wsz, windows);
     uint64_t warm = (uint64_t)kRgWarm44 * a.sample_rate / 44100;
     warm = (warm + 9) / 10 * 10;
     if (g_rg_warm_override >= 0)
@@ -995,16 +1035,33 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
             chunks.insert(chunks.end(), a.chunk_frames, a.chunk_frames + a.n_chunks);
         }
         const uint32_t wsz = (uint32_t)std::ceil(a.sample_rate * 0.050);
-        const RgBound bd = rg_bound(fi, rg_seg_len(wsz));
         tr[t] = RgTrack{a.pcm_offset * a.channels, a.pcm_frames, a.channels, a.bits_per_sample,
-                        (uint32_t)fi, wsz, cbase, bd.gmax, bd.gl, bd.gs, bd.ginv,
-                        bd.py, bd.pb, bd.qy, bd.qb, bd.sa, bd.sb, bd.ke, bd.ko, bd.rsf};
+                        (uint32_t)fi, wsz, cbase, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0, 0};
         wbase[t + 1] = wbase[t] + a.pcm_frames / tr[t].window;
         if (n_albums) {
             if (!count[a.album])
                 first[a.album] = t;
             ++count[a.album];
         }
+    }
+    // the batch's segment length, then each track's certification bound for it
+    const uint32_t seg_windows = rg_seg_windows(tr, tracks, n);
+    for (uint32_t t = 0; t < n; ++t) {
+        const RgBound bd = rg_bound((int)tr[t].fi, rg_seg_len(tr[t].window, seg_windows));
+        RgTrack &T = tr[t];
+        T.gmax = bd.gmax;
+        T.gl = bd.gl;
+        T.gs = bd.gs;
+        T.ginv = bd.ginv;
+        T.py = bd.py;
+        T.pb = bd.pb;
+        T.qy = bd.qy;
+        T.qb = bd.qb;
+        T.sa = bd.sa;
+        T.sb = bd.sb;
+        T.ke = bd.ke;
+        T.ko = bd.ko;
+        T.rsf = bd.rsf;
     }
     RHIP(g_ctx.tracks.ensure(sizeof(RgTrack) * std::max<uint32_t>(n, 1)));
     RHIP(g_ctx.hist.ensure(sizeof(uint32_t) * kBins * (size_t)std::max<uint32_t>(n, 1)));
@@ -1027,7 +1084,8 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
     std::vector<RgSeg> segs, segs2;
     std::vector<uint32_t> warm_win(n);
     for (uint32_t t = 0; t < n; ++t)
-        plan_segments(t, tr[t], tracks[t], false, tr[t].ch == 1 ? segs : segs2, warm_win[t]);
+        plan_segments(t, tr[t], tracks[t], false, tr[t].ch == 1 ? segs : segs2, warm_win[t],
+                      seg_windows);
     const uint32_t nseg1 = (uint32_t)segs.size();
     segs.insert(segs.end(), segs2.begin(), segs2.end());
     const uint32_t nseg = (uint32_t)segs.size();
@@ -1116,7 +1174,8 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
         std::vector<RgSeg> e1, e2;
         uint32_t unused = 0;
         for (uint32_t t : redo)
-            plan_segments(t, tr[t], tracks[t], true, tr[t].ch == 1 ? e1 : e2, unused);
+            plan_segments(t, tr[t], tracks[t], true, tr[t].ch == 1 ? e1 : e2, unused,
+                          seg_windows);
         const uint32_t m1 = (uint32_t)e1.size();
         e1.insert(e1.end(), e2.begin(), e2.end());
         const uint32_t m = (uint32_t)e1.size();
