@@ -1543,6 +1543,8 @@ def main(argv=None):
                           rank == 0 and not args.no_verify)
 
     if rank != 0:
+        eng.close()
+        _atgpu.close_all()
         if world > 1:
             dist.destroy_process_group()
         return 0
@@ -1692,6 +1694,10 @@ def main(argv=None):
         "plan_per_batch": plan_miss,
     }
     print(json.dumps(line), flush=True)
+    # every handle closed here, in order, not from interpreter teardown
+    # 
+    eng.close()
+    _atgpu.close_all()
     if world > 1:
         dist.destroy_process_group()
     return 0

@@ -6,7 +6,9 @@ library => ImportError, missing GPU => ATGError(ATG_ERR_DEVICE): there is no
 CPU fallback on the product path.
 """
 
+import atexit
 import ctypes
+import itertools
 import os
 import threading
 import weakref
@@ -467,6 +469,34 @@ def _track_array(tracks):
     return arr, len(tracks), keep
 
 
+# Every engine / decoder / encoder handle this process opened, by opening
+# order.  At interpreter exit the atexit hook below closes those still open,
+# newest first, while the interpreter and the HIP runtime are both intact:
+# otherwise their destroy calls run from __del__ during module teardown (or
+# never), interleaved with torch's and the HIP runtime's own teardown.  Round
+# 5's two exit-time crashes came from that path.
+_live_handles = weakref.WeakValueDictionary()
+_handle_serial = itertools.count()
+
+
+def _track_handle(obj):
+    _live_handles[next(_handle_serial)] = obj
+
+
+def close_all():
+    """close every handle still open (newest first); registered with atexit"""
+    for k in sorted(_live_handles.keys(), reverse=True):
+        obj = _live_handles.get(k)
+        if obj is not None:
+            try:
+                obj.close()
+            except Exception:
+                pass
+
+
+atexit.register(close_all)
+
+
 class TrackTable(object):
     """a batch's atg_track array, built once (batches repeat in pipelines)"""
 
@@ -530,6 +560,7 @@ class Engine(object):
         h = ctypes.c_void_p()
         _check(self.lib, self.lib.atg_engine_create_ex(int(device), flags, ctypes.byref(h)))
         self.handle = h
+        _track_handle(self)
 
     def close(self):
         if self.handle:
@@ -739,7 +770,10 @@ def pinned_empty(shape, dtype=np.uint8):
     p = ctypes.c_void_p()
     _check(lib, lib.atg_host_alloc(nbytes, ctypes.byref(p)))
     buf = (ctypes.c_uint8 * nbytes).from_address(p.value)
-    weakref.finalize(buf, lib.atg_host_free, p.value)
+    # not freed by weakref's own atexit hook: that hook runs before
+    # close_all (it registers later), and a buffer an unwaited host job still
+    # DMAs into must outlive the engine; at exit the process takes it back
+    weakref.finalize(buf, lib.atg_host_free, p.value).atexit = False
     return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
 
 
@@ -780,6 +814,7 @@ class Decoder(object):
         h = ctypes.c_void_p()
         self._check(self.lib.atg_decoder_create(int(device), ctypes.byref(h)))
         self.handle = h
+        _track_handle(self)
         self._pending = {}
 
     def _check(self, status):
@@ -884,6 +919,7 @@ class AlacEncoder(object):
         h = ctypes.c_void_p()
         self._check(self.lib.atg_alac_encoder_create(int(device), ctypes.byref(h)))
         self.handle = h
+        _track_handle(self)
 
     def _check(self, status):
         if status != ATG_OK:
@@ -1010,6 +1046,7 @@ class AlacDecoder(object):
         h = ctypes.c_void_p()
         self._check(self.lib.atg_alac_decoder_create(int(device), ctypes.byref(h)))
         self.handle = h
+        _track_handle(self)
 
     def _check(self, status):
         if status != ATG_OK:
