@@ -80,8 +80,9 @@ def parse_args(argv=None):
     ap.add_argument("--narrow", default="512,256,128",
                     help="track counts of the narrow-batch leg (a strong-scaling rank's "
                          "share, on one GPU); empty to skip")
-    ap.add_argument("--narrow-depths", default="3,16,24,32",
-                    help="batches in flight for the narrow leg (atg_engine_set_inflight)")
+    ap.add_argument("--narrow-depths", default="auto,3,32",
+                    help="batches in flight for the narrow leg (atg_engine_set_inflight; "
+                         "auto = the engine's automatic depth)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-verify", action="store_true")
     ap.add_argument("--chain-tracks", type=int, default=64,
@@ -110,6 +111,10 @@ def parse_args(argv=None):
                          "redone (self-check)")
     ap.add_argument("--no-decode", action="store_true",
                     help="skip the decode / convert / ReplayGain legs")
+    ap.add_argument("--k2-profile", action="store_true",
+                    help="only the headline batch's search kernel, one batch at a time "
+                         "(for rocprofv3 --kernel-trace --stats; prints a line that is not "
+                         "a measurement)")
     ap.add_argument("--selftest", action="store_true",
                     help="harness self-test on CPU (gloo, oracle as the step); "
                          "prints a line that is not a measurement")
@@ -1233,27 +1238,77 @@ def selftest(args):
         dist.destroy_process_group()
 
 
-def strong_depth(n_tracks):
-    """batches in flight for a rank batch of n_tracks config-2 tracks: the
-    kernels of a batch take ~8 ms x n/1024, its MD5 chains ~12.5 ms
-    whatever n, so a narrow batch needs chain / kernels + 2 batches in
-    flight (rolled MD5 slices the chain over depth - 2 enqueues); measured
-    best in the three final round-5 runs (narrow leg, 16/24/32 in flight):
-    32 up to 256 tracks (128: 5.91-5.94 M frames/s against 5.76-5.83 at
-    24), 24 up to 512 (8.12-8.15 M against 7.95-8.05 at 16), 12 above
-    (the headline's depth; profiles/r05_zz_final_bench.json,
-    r05_zm_narrow_depth.json)"""
-    return 32 if n_tracks <= 256 else 24 if n_tracks <= 512 else 12
+ALONE_LAUNCHES = 8
+# the committed rocprofv3 kernel-stats pass of `bench.py --k2-profile` (every
+# search launch a 1024-track batch alone on the device): the headline
+# roofline's launch time is checked against its average
+K2_PROFILE = "r06_k2_alone_kernel_stats.csv"
+K2_KERNEL = "k_frame_search_ms"
+
+
+def k2_alone(eng, opts, pcm, table, out_buf, out_cap, n):
+    """mean search-kernel time (HIP events on the engine's main stream
+    around the launch) over n batches encoded one at a time: the kernel's
+    own duration, nothing queued beside or before it"""
+    from audiotools import _atgpu
+    ms = []
+    for k in range(n + 1):
+        eng.wait(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16,
+                                         44100, out_buf.data_ptr(), out_cap))
+        if k:
+            ms.append(eng.kernel_times().get("subframe_search", 0.0))
+    return sum(ms) / len(ms)
+
+
+def k2_profile_avg():
+    """(average ms, launches) of the search kernel in the committed
+    rocprofv3 --kernel-trace --stats summary of `bench.py --k2-profile`"""
+    import csv
+    fn = os.path.join(ROOT, "profiles", K2_PROFILE)
+    if not os.path.exists(fn):
+        return None
+    with open(fn) as f:
+        for row in csv.DictReader(f):
+            if K2_KERNEL in row.get("Name", ""):
+                return float(row["AverageNs"]) / 1e6, int(row["Calls"])
+    return None
+
+
+def k2_profile_main(args):
+    """--k2-profile: only the headline batch's search kernel, every launch
+    one batch alone (what rocprofv3 --kernel-trace --stats summarises into
+    profiles/r06_k2_alone_kernel_stats.csv)"""
+    import torch
+    from audiotools import _atgpu
+    device = torch.device("cuda", 0)
+    eng = _atgpu.Engine(0)
+    opts = _atgpu.make_options(**FLAC8)
+    n_samples = args.frames * BLOCK
+    ids = list(range(args.tracks))
+    pcm = synth_batch(torch, ids, n_samples, device)
+    tracks = [(i * n_samples, n_samples) for i in range(len(ids))]
+    _, out_cap = eng.bounds(opts, tracks, 2, 16)
+    table = _atgpu.TrackTable(tracks)
+    out = torch.empty(out_cap, dtype=torch.uint8, device=device)
+    torch.cuda.synchronize()
+    ms = k2_alone(eng, opts, pcm, table, out, out_cap, args.steps)
+    print(json.dumps({"k2_profile": True, "launches": args.steps + 1,
+                      "event_ms_mean": round(ms, 4), "tracks": len(ids),
+                      "frames_per_track": args.frames}), flush=True)
+    eng.close()
+    return 0
 
 
 def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_full, res_full,
                barrier):
     """frames/s of narrow batches (the first n tracks of the config-2 batch)
-    at each in-flight depth; every image of the last batch byte-compared
-    with the full batch's image of the same track"""
+    at each in-flight depth -- "auto" = the engine's own choice
+    (atg_engine_set_inflight(0), engine.hip auto_depth), the caller keeping
+    eng.inflight() batches in flight; every image of the last batch
+    byte-compared with the full batch's image of the same track"""
     from audiotools import _atgpu
     widths = [int(x) for x in args.narrow.split(",") if x.strip()]
-    depths = [int(x) for x in args.narrow_depths.split(",") if x.strip()]
+    depths = [x.strip() for x in args.narrow_depths.split(",") if x.strip()]
     out = {}
     for n in widths:
         n = min(n, len(tracks))
@@ -1261,42 +1316,48 @@ def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_ful
         _, cap = eng.bounds(opts, sub, 2, 16)
         table = _atgpu.TrackTable(sub)
         per = {}
-        for d in depths:
-            eng.set_inflight(d)
-            bufs = [torch.empty(cap, dtype=torch.uint8, device=device) for _ in range(d)]
+        for spec in depths:
+            eng.set_inflight(0 if spec == "auto" else int(spec))
+            bufs = []
             pend = []
 
             def run(steps):
-                last = None
+                last, d = None, None
                 for k in range(steps):
-                    pend.append(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16,
-                                                        table, 2, 16, 44100,
-                                                        bufs[k % d].data_ptr(), cap))
+                    if d is not None and len(bufs) < d:
+                        bufs.append(torch.empty(cap, dtype=torch.uint8, device=device))
+                    elif d is None and not bufs:
+                        bufs.append(torch.empty(cap, dtype=torch.uint8, device=device))
+                    pend.append((k, eng.encode_device_async(
+                        opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16, 44100,
+                        bufs[k % len(bufs)].data_ptr(), cap)))
+                    d = eng.inflight()  # the automatic depth is set by the first enqueue
                     if len(pend) >= d:
-                        last = eng.wait(pend.pop(0))
+                        last = (pend[0][0], eng.wait(pend.pop(0)[1]))
                 while pend:
-                    last = eng.wait(pend.pop(0))
-                return last
+                    last = (pend[0][0], eng.wait(pend.pop(0)[1]))
+                return last, d
 
-            run(d + 1)
+            run(34)  # warm-up: fills the buffer ring at any depth
             barrier()
             t0 = time.perf_counter()
-            r = run(args.steps)
+            (k_last, r), d = run(args.steps)
             barrier()
             dt = time.perf_counter() - t0
             if world > 1:
                 dt = reduce_max(torch, dist, dt, device)
             kt = eng.kernel_times()
-            last = bufs[(args.steps - 1) % d]
+            last = bufs[k_last % len(bufs)]
             bad = 0
             for t in range(n):
                 a = last[r[t].out_offset:r[t].out_offset + r[t].bytes]
                 b = out_full[res_full[t].out_offset:res_full[t].out_offset + res_full[t].bytes]
                 if r[t].bytes != res_full[t].bytes or not torch.equal(a, b):
                     bad += 1
-            per["inflight_%d" % d] = {
+            key = "inflight_auto" if spec == "auto" else "inflight_%s" % spec
+            per[key] = {
                 "value": round(n * args.frames * args.steps / dt, 1), "unit": "frames/s",
-                "ms_per_step": round(dt / args.steps * 1e3, 3),
+                "ms_per_step": round(dt / args.steps * 1e3, 3), "inflight": d,
                 "kernel_ms": {k: round(v, 3) for k, v in kt.items()},
                 "verified_tracks": n - bad, "mismatches": bad}
             del bufs
@@ -1304,6 +1365,7 @@ def narrow_leg(args, torch, dist, world, device, eng, opts, pcm, tracks, out_ful
         out[str(n)] = per
     return {"tracks_per_batch": out,
             "note": "the first n tracks of the config-2 batch per step, pipelined; "
+                    "inflight_auto = the engine's default (automatic) depth; "
                     "images compared with the full batch's (the same tracks' bytes)"}
 
 
@@ -1315,6 +1377,8 @@ def main(argv=None):
         return launch(args, argv)
     if args.selftest:
         return selftest(args)
+    if args.k2_profile:
+        return k2_profile_main(args)
     import torch
     import torch.distributed as dist
 
@@ -1418,20 +1482,23 @@ def main(argv=None):
         st_table = _atgpu.TrackTable(tracks[:n_s])
         # a narrow rank batch keeps more batches in flight so the per-track
         # MD5 chains (~12.5 ms per 1 MiB track whatever the width) stay off
-        # the step: rolled MD5 (atg_engine_set_inflight)
-        s_depth = strong_depth(n_s)
+        # the step: the engine's automatic depth (engine.hip auto_depth,
+        # rolled MD5), read after the first enqueue
         _, s_cap = eng.bounds(opts, tracks[:n_s], 2, 16)
-        s_outs = [torch.empty(s_cap, dtype=torch.uint8, device=device) for _ in range(s_depth)]
-        eng.set_inflight(s_depth)
+        s_outs = [torch.empty(s_cap, dtype=torch.uint8, device=device) for _ in range(32)]
+        eng.set_inflight(0)
+        s_depth = 0
 
         def s_timed(steps):
+            nonlocal s_depth
             barrier()
             t1 = time.perf_counter()
             pend = []
             for k in range(steps):
                 pend.append(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16,
                                                     st_table, 2, 16, 44100,
-                                                    s_outs[k % s_depth].data_ptr(), s_cap))
+                                                    s_outs[k % 32].data_ptr(), s_cap))
+                s_depth = eng.inflight()
                 if len(pend) >= s_depth:
                     eng.wait(pend.pop(0))
             while pend:
@@ -1440,7 +1507,7 @@ def main(argv=None):
             dt = time.perf_counter() - t1
             return reduce_max(torch, dist, dt, device)
 
-        s_timed(s_depth + 1)
+        s_timed(34)
         dt = s_timed(args.steps)
         eng.set_inflight(max(3, args.inflight))
         del s_outs
@@ -1460,13 +1527,7 @@ def main(argv=None):
                         barrier) if args.narrow else None
     # ---- the search kernel with one batch in flight: in the pipelined loop
     # above the batches behind run their LPC kernels (slot stream) beside it
-    alone = []
-    for k in range(3):
-        eng.wait(eng.encode_device_async(opts, pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16,
-                                         44100, outs[0].data_ptr(), out_cap))
-        if k:
-            alone.append(eng.kernel_times().get("subframe_search", 0.0))
-    sub_alone_ms = sum(alone) / len(alone)
+    sub_alone_ms = k2_alone(eng, opts, pcm, table, outs[0], out_cap, ALONE_LAUNCHES)
     # ---- per-batch host planning: every step a new track geometry (the
     # plan cache misses; engine.hip get_plan), against the fixed geometry
     plan_steps = min(args.steps, 10)
@@ -1559,15 +1620,40 @@ def main(argv=None):
            "frame_decide": 0, "track_scan": 0, "stream_header": out_bytes - frame_bytes}
     main_k = {k: v for k, v in kt.items() if k in MAIN_STREAM}
     dom = max(main_k, key=main_k.get)
-    dom_ms = main_k[dom]
+    dom_ms = main_k[dom]  # live event span in the pipelined loop
     alg_bytes = alg.get(dom, pcm_bytes)
-    achieved = alg_bytes / (dom_ms / 1e3) / 1e9
     traffic = (load_profile_json("pmc_traffic.json") or {}).get(dom)
+    # the roofline's kernel time is the search kernel's own duration (one
+    # batch on the device, HIP events around the launch): the live span
+    # above also holds the time the kernel's stream waits behind the batches
+    # beside it, and can exceed the step
+    ms_step = elapsed / args.steps * 1e3
+    assert sub_alone_ms <= ms_step, (sub_alone_ms, ms_step)
+    achieved = alg_bytes / (sub_alone_ms / 1e3) / 1e9
+    prof = k2_profile_avg()
+    roofline = {"bound": "hbm", "kernel": "subframe_search", "achieved": round(achieved, 2),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
+                "alg_bytes_per_launch": alg_bytes, "launch_ms": round(sub_alone_ms, 4),
+                "launch_ms_source": "HIP events around the search launch, %d batches encoded "
+                                    "one at a time after the clock" % ALONE_LAUNCHES,
+                "launch_ms_le_ms_per_step": True,
+                "live_span_ms": round(dom_ms, 4),
+                "live_span_note": "event span of the longest main-stream kernel (%s) in the "
+                                  "pipelined loop: includes queueing behind the batches in "
+                                  "flight, not a kernel duration, not used for frac" % dom,
+                "profile": None}
+    if prof:
+        roofline["profile"] = {
+            "file": "profiles/" + K2_PROFILE, "kernel": K2_KERNEL + "<short>",
+            "avg_ms": round(prof[0], 4), "calls": prof[1],
+            "frac": round(alg_bytes / (prof[0] / 1e3) / 1e9 / HBM_PEAK_GBS, 5),
+            "launch_ms_vs_profile": round(sub_alone_ms / prof[0], 4)}
     # integer-VALU roofline of the subframe search: algorithmic
     # MACs = sum over the 4 candidate subframes of the 12 LPC orders
     # (1+..+12 = 78 taps x 4096 samples) + FIXED orders 1..4 (10 taps) --
     # 2 MACs per v_dot2 lane-op, 64 lanes per wave instruction
-    sub_ms = kt.get("subframe_search", 0.0)
+    sub_ms = sub_alone_ms  # the kernel's own duration, as the HBM roofline above
     macs_per_frame = 4 * (78 + 10) * BLOCK
     alg_wave_insts = n_frames * macs_per_frame / 2.0 / 64.0
     pmc = (load_profile_json("pmc_valu.json") or {}).get("subframe_search") or {}
@@ -1583,8 +1669,6 @@ def main(argv=None):
         per_launch = pmc["SQ_INSTS_VALU"] * (n_frames / pmc.get("frames", n_frames))
         valu["issued_wave_insts_per_launch"] = per_launch
         valu["issue_frac"] = round(per_launch / (sub_ms / 1e3) / VALU_PEAK_WAVE_INSTS, 4)
-        valu["issue_frac_one_batch"] = round(per_launch / (sub_alone_ms / 1e3)
-                                             / VALU_PEAK_WAVE_INSTS, 4)
         valu["pmc_source"] = pmc.get("source")
     step_alg = pcm_bytes + out_bytes
     step_hbm = {"alg_bytes_per_step": step_alg,
@@ -1663,18 +1747,7 @@ def main(argv=None):
                    "block_size": 4096, "preset": "FLAC-8 (-l 12 -m -e -R 6)",
                    "parallelism": "dp%d (tracks sharded per GPU, %s scaling)"
                                   % (world, args.scaling)},
-        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 2),
-                     "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 5), "traffic": traffic,
-                     "alg_bytes_per_launch": alg_bytes, "launch_ms": round(dom_ms, 4),
-                     "selection": "longest kernel on the main (critical-path) stream",
-                     "launch_ms_one_batch": round(sub_alone_ms, 4)
-                     if dom == "subframe_search" else None,
-                     "frac_one_batch": round(alg_bytes / (sub_alone_ms / 1e3) / 1e9 / HBM_PEAK_GBS, 5)
-                     if dom == "subframe_search" and sub_alone_ms else None,
-                     "note": "launch_ms: live in the timed loop, beside the LPC kernels of the "
-                             "batches behind (slot streams) and the MD5 chains; "
-                             "launch_ms_one_batch: one batch in flight, after the clock"},
+        "roofline": roofline,
         "roofline_valu": valu,
         "step_hbm": step_hbm,
         "kernel_ms": {k: round(v, 4) for k, v in kt.items()},

@@ -259,14 +259,23 @@ atg_status atg_service_encode_frames(atg_service *svc, const atg_flac_options *o
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *eng, uint64_t bytes);
 
 /* Batches atg_flac_encode_device_async keeps in flight (slots in rotation,
-   each its own device workspace): 3 (default) .. 32.  Every track's MD5 is
-   one serial hash (~12.5 ms per MiB of track on the GPU, whatever the batch
-   width), so a narrow batch -- a rank's share of a strong-scaling job --
-   needs more batches in flight to keep the chains off its step.  From 4
-   on, the chains of all batches in flight advance together, one launch per
-   enqueue on one stream, each batch's chain in n - 2 slices.  Fails
-   with ATG_ERR_INVALID while any batch or host job is unwaited. */
+   each its own device workspace, ~2 KB of tables per frame of the batch):
+   3 .. 32, or 0 = automatic (the default).  Every track's MD5 is one serial
+   hash (~12.5 ms per MiB of track on the GPU, whatever the batch width), so
+   a narrow batch -- a rank's share of a strong-scaling job -- needs more
+   batches in flight to keep the chains off its step.  From 4 on, the chains
+   of all batches in flight advance together, one launch per enqueue on one
+   stream, each batch's chain in n - 2 slices.  Automatic: the first device
+   batch enqueued while nothing is in flight sets the depth from the ratio of
+   its longest track's MD5 chain to its kernel time (12, 24 or 32; 3 when
+   the chains are short or hashed on the host), and a host job sets it back
+   to 3.  Lowering the depth frees the workspaces of the slots beyond it.
+   Fails with ATG_ERR_INVALID while any batch or host job is unwaited. */
 atg_status atg_engine_set_inflight(atg_engine *eng, uint32_t n);
+/* The current depth D (the slots in rotation): a pipelined caller keeps up
+   to D batches in flight and waits the oldest before enqueueing the next.
+   With the automatic depth, read it after the pipeline's first enqueue. */
+uint32_t atg_engine_inflight(atg_engine *eng);
 
 /* Device-memory entry points run on the library's own non-blocking HIP
    streams: device inputs must be complete (e.g. the producing stream
@@ -285,8 +294,8 @@ atg_status atg_flac_encode_device(atg_engine *eng, const atg_flac_options *opts,
 
 /* The same batch encode, enqueued: returns once the work is queued, with a
    ticket for atg_flac_encode_wait.  The engine keeps D batches in flight
-   (D = 3 unless atg_engine_set_inflight says otherwise; each its own device
-   workspace): batch k's MD5 chains and stream headers run on their own
+   (atg_engine_inflight: automatic unless atg_engine_set_inflight fixed it;
+   each its own device workspace): batch k's MD5 chains and stream headers run on their own
    stream while batches k+1 .. k+D-1 are analysed, so a caller that waits
    for ticket k after enqueueing k+D-1 overlaps them.  d_pcm and d_out must
    stay untouched until the ticket is waited.  Enqueue number D+1 while D

@@ -35,6 +35,7 @@ EXPORTS = (
     "atg_flac_encode_host_async", "atg_flac_encode_host_wait",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
     "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_engine_set_inflight",
+    "atg_engine_inflight",
     "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
     "atg_flac_encode_frames_batch", "atg_service_connect", "atg_service_close",
@@ -295,6 +296,8 @@ def load_library():
         lib.atg_engine_set_host_chunk_bytes.restype = ctypes.c_int
         lib.atg_engine_set_inflight.argtypes = [P, c_u32]
         lib.atg_engine_set_inflight.restype = ctypes.c_int
+        lib.atg_engine_inflight.argtypes = [P]
+        lib.atg_engine_inflight.restype = c_u32
         lib.atg_engine_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -719,8 +722,14 @@ class Engine(object):
         return out[:nb.value], fb[:n_fr]
 
     def set_inflight(self, n):
-        """batches encode_device_async keeps in flight (3..32)"""
+        """batches encode_device_async keeps in flight (3..32; 0 = automatic,
+        the default: the first batch of a pipeline picks it, include/atgpu.h)"""
         _check(self.lib, self.lib.atg_engine_set_inflight(self.handle, int(n)))
+
+    def inflight(self):
+        """the current depth D: keep up to D device batches in flight (with
+        the automatic depth, read it after the pipeline's first enqueue)"""
+        return int(self.lib.atg_engine_inflight(self.handle))
 
     def set_host_chunk_bytes(self, nbytes):
         """PCM bytes per chunk of the host-memory pipeline (encode())"""

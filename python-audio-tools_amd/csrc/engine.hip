@@ -313,6 +313,9 @@ struct atg_engine {
     hipStream_t s_pack = nullptr;
     EncSlot slot[kMaxSlots];
     uint64_t depth = kEncSlots; // slots in rotation (atg_engine_set_inflight)
+    // the caller fixed the depth (atg_engine_set_inflight n >= 3); otherwise
+    // a pipelined device batch that starts a pipeline sets it (auto_depth)
+    bool depth_user = false;
     // rolled mode: every batch's MD5 slices, tails, stream headers and
     // result copies on s_md5 (high priority: one stream whatever the depth,
     // instead of one aux stream per slot); the tables + LPC kernels on the
@@ -1609,6 +1612,70 @@ atg_status host_enqueue(atg_engine *e, HostJob &j, size_t ci, const atg_flac_opt
     return ATG_OK;
 }
 
+// no batch or host job in flight
+bool engine_idle(const atg_engine *e)
+{
+    for (const EncSlot &sl : e->slot)
+        if (sl.busy)
+            return false;
+    return e->hjobs.empty() && e->hflight.empty();
+}
+
+// a new slot rotation of n slots (the engine idle): tickets map to slots by
+// ticket % depth, so the rotation starts clean; slots past the new depth
+// give their device workspaces back (a 1024-track config-2 slot holds ~130
+// MB of tables)
+void set_depth(atg_engine *e, uint64_t n)
+{
+    for (EncSlot &sl : e->slot) {
+        sl.ticket = 0;
+        sl.done = false;
+    }
+    for (uint64_t k = n; k < kMaxSlots; ++k) {
+        EncSlot &sl = e->slot[k];
+        for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
+                          &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch,
+                          &sl.slow, &sl.md5in})
+            b->release();
+        sl.uploaded = nullptr;
+        sl.plan.reset();
+    }
+    e->depth = n;
+}
+
+// Batches in flight for a pipelined device batch when the caller has not
+// set the depth.  A batch's MD5 chains take ~0.8 us per 64-byte block of its
+// longest track whatever the batch width (md5.hip), its kernels ~8 ms per
+// 65,536 frames of 4096 samples (config 2); with chain / kernels = r the
+// rolled MD5 hides the chains at: 12 in flight for r <= 2 (config 2, 1024
+// tracks: 7.99 ms per step against 8.30 at 3), 24 for r <= 4 (512 tracks:
+// 8.12-8.15 M frames/s against 7.95-8.05 at 16), 32 above (256 and 128
+// tracks: 5.91-5.94 M at 128 tracks against 5.76-5.83 at 24) -- the
+// narrow-leg measurements of round 5 (profiles/r05_zz_final_bench.json,
+// r05_zm_narrow_depth.json).  Bounded so the slots' tables (~2 KB per
+// frame) stay under 16 GB; 3 (the split-chain rotation) when the chains
+// are short next to the kernels or not on the GPU at all.
+uint64_t auto_depth(atg_engine *e, const Plan &pl, int fmt)
+{
+    const FlacParams &p = pl.p;
+    if (pl.frames_only || pl.tracks.empty() || want_host_md5(e, pl, fmt, false) ||
+        !track_md5_paired(p, fmt))
+        return kEncSlots;
+    uint64_t maxb = 0, samples = 0;
+    for (const TrackInfo &t : pl.tracks) {
+        maxb = std::max<uint64_t>(maxb, t.pcm_frames * p.channels * ((p.bps + 7) / 8));
+        samples += t.pcm_frames;
+    }
+    const double chain_ms = (double)maxb / 64.0 * 0.8e-3;
+    // (a batch's seven launches and copies take ~0.5 ms however small it is)
+    const double kernel_ms = std::max(0.5, (double)samples / 4096.0 * (8.0 / 65536.0) *
+                                               (double)p.channels / 2.0);
+    const double r = chain_ms / kernel_ms;
+    uint64_t d = r < 0.25 ? kEncSlots : r <= 2.0 ? 12 : r <= 4.0 ? 24 : kMaxSlots;
+    const uint64_t cap = (16ull << 30) / std::max<uint64_t>(1, pl.frames.size() * 2048ull);
+    return std::max<uint64_t>(kEncSlots, std::min(d, cap));
+}
+
 } // namespace
 
 extern "C" {
@@ -1774,6 +1841,12 @@ atg_status atg_flac_encode_device_async(atg_engine *e, const atg_flac_options *o
     atg_status st = get_plan(e, opts, tracks, n_tracks, channels, bps, rate, pl);
     if (st != ATG_OK)
         return st;
+    // the first batch of a pipeline picks the depth unless the caller set it
+    if (!e->depth_user && !e->sync_call && engine_idle(e)) {
+        const uint64_t d = auto_depth(e, *pl, (int)format);
+        if (d != e->depth)
+            set_depth(e, d);
+    }
     EncSlot *sl = nullptr;
     uint64_t t = 0;
     st = take_slot(e, sl, t);
@@ -1857,6 +1930,11 @@ atg_status atg_flac_encode_host_async(atg_engine *e, const atg_flac_options *opt
     for (EncSlot &s2 : e->slot)
         if (s2.busy && !s2.host)
             return fail(ATG_ERR_INVALID, "an async encode batch is in flight: wait for it first");
+    // the host pipeline runs kEncSlots chunks on the default rotation (the
+    // slots with aux streams from creation); an automatic deeper rotation a
+    // device pipeline left behind is undone
+    if (!e->depth_user && e->depth != kEncSlots && engine_idle(e))
+        set_depth(e, kEncSlots);
     j.elem = format == ATG_PCM_S16 ? 2 : 4;
     j.fmt = (int)format;
     j.pcm = (const uint8_t *)pcm;
@@ -2176,20 +2254,20 @@ uint64_t atg_flac_max_frames_bytes(const atg_flac_options *opts, uint64_t pcm_fr
 atg_status atg_engine_set_inflight(atg_engine *e, uint32_t n)
 {
     ATG_HANDLE_LOCK(e);
-    if (!e || n < kEncSlots || n > kMaxSlots)
-        return fail(ATG_ERR_INVALID, "in-flight batches must be 3..32");
-    for (EncSlot &sl : e->slot)
-        if (sl.busy)
-            return fail(ATG_ERR_INVALID, "an encode batch is in flight: wait for it first");
-    if (!e->hjobs.empty())
-        return fail(ATG_ERR_INVALID, "a host job is in flight: wait for it first");
-    // tickets map to slots by ticket % depth: start the new rotation clean
-    for (EncSlot &sl : e->slot) {
-        sl.ticket = 0;
-        sl.done = false;
-    }
-    e->depth = n;
+    if (!e || (n != 0 && (n < kEncSlots || n > kMaxSlots)))
+        return fail(ATG_ERR_INVALID, "in-flight batches must be 3..32 (or 0: automatic)");
+    if (!engine_idle(e))
+        return fail(ATG_ERR_INVALID, "an encode batch or host job is in flight: wait for it first");
+    e->depth_user = n != 0;
+    if (n)
+        set_depth(e, n);
     return ATG_OK;
+}
+
+uint32_t atg_engine_inflight(atg_engine *e)
+{
+    ATG_HANDLE_LOCK(e);
+    return e ? (uint32_t)e->depth : 0u;
 }
 
 atg_status atg_engine_set_host_chunk_bytes(atg_engine *e, uint64_t bytes)

@@ -98,6 +98,7 @@ def test_fourth_enqueue_refused_results_survive(gpu_engine):
     import torch
     from audiotools import _atgpu
     eng = gpu_engine
+    eng.set_inflight(3)  # the contract at a fixed depth (the default is automatic)
     opts = _atgpu.make_options(**FLAC8)
     pcm, tracks, per = _batch(7, [(0, 4096 * 2 + 11), (1, 333)])
     d_pcm = _dev(torch, pcm)
@@ -120,6 +121,51 @@ def test_fourth_enqueue_refused_results_survive(gpu_engine):
         _check(eng, torch, outs[k], eng.wait(t), per, "ticket %d" % k)
     with pytest.raises(_atgpu.ATGError):   # waited twice after its slot was reused
         eng.wait(ts[0])
+    eng.set_inflight(0)
+
+
+@pytest.mark.parametrize("n_tracks,frames,want", [(4, 64, 32), (1024, 8, 12), (3, 1, 12)])
+def test_automatic_depth(n_tracks, frames, want):
+    """the default (automatic) depth: the first pipelined batch on an idle
+    engine sets it from its longest track's MD5 chain against its kernel
+    time (engine.hip auto_depth) -- 4 one-MiB tracks (a narrow rank batch)
+    32, 1024 short tracks 12, a tiny batch 12; the depth's contract holds
+    (D unwaited enqueues, the next refused), every batch's images are the
+    same bytes (the first batch's checked against the port), and a host
+    job sets the rotation back to 3"""
+    import torch
+    from audiotools import _atgpu
+    eng = _atgpu.Engine(0)
+    opts = _atgpu.make_options(**FLAC8)
+    pcm, tracks, per = _batch(900 + n_tracks, [(0, 4096 * frames)] * n_tracks)
+    d_pcm = _dev(torch, pcm)
+    _, cap = eng.bounds(opts, tracks, 2, 16)
+    outs = [torch.empty(cap, dtype=torch.uint8, device="cuda") for _ in range(want)]
+    torch.cuda.synchronize()
+    table = _atgpu.TrackTable(tracks)
+
+    def enq(k):
+        return eng.encode_device_async(opts, d_pcm.data_ptr(), _atgpu.PCM_S16, table, 2, 16,
+                                       44100, outs[k].data_ptr(), cap)
+
+    ts = [enq(0)]
+    assert eng.inflight() == want
+    ts += [enq(k) for k in range(1, want)]
+    with pytest.raises(_atgpu.ATGError):
+        enq(0)
+    res = [eng.wait(t) for t in ts]
+    first = outs[0].cpu().numpy()
+    imgs = [first[r.out_offset:r.out_offset + r.bytes].tobytes() for r in res[0]]
+    for t in range(min(n_tracks, 4)):
+        want_img, _ = oracle_port.encode(per[t], 2, 16, 44100, **FLAC8)
+        assert imgs[t] == want_img, "track %d" % t
+    for k in range(1, want):
+        host = outs[k].cpu().numpy()
+        assert all(host[r.out_offset:r.out_offset + r.bytes].tobytes() == imgs[t]
+                   for t, r in enumerate(res[k])), "batch %d" % k
+    eng.encode(opts, pcm, tracks, 2, 16, 44100)
+    assert eng.inflight() == 3
+    eng.close()
 
 
 def test_async_batches_new_frame_lengths_fresh_engine():
