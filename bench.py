@@ -1103,13 +1103,37 @@ def rg4_leg(args, torch, dist, world, rank, device, barrier, threads=16):
                 bad.append(k)
 
         vdt = _parallel(n_tracks, threads, one)
-        album_ok = (oracle_port.rg_gain(np.sum(hists, axis=0).astype(np.uint32)) == album_gain
-                    and max(peaks) == album_peak)
-        del xh, hists
+        want_album = oracle_port.rg_gain(np.sum(hists, axis=0).astype(np.uint32))
+        album_ok = want_album == album_gain and max(peaks) == album_peak
         out["verified_tracks"] = n_tracks - len(bad)
         out["verified_album"] = album_ok
         out["verified_vs_oracle"] = not bad and album_ok
         out["verify_s"] = round(vdt, 1)
+        out["cpu_baseline"] = {"value": round(n_tracks * n / BLOCK / vdt, 1),
+                               "unit": "frames/s", "cores": threads, "kind": "port",
+                               "sample": "the album's %d titles through oracle/replaygain_port.c"
+                                         ", %d threads, %.1f s" % (n_tracks, threads, vdt)}
+        # the drop-in: audiotools.calculate_replay_gain over the same album
+        # (the callers' path under track2track --replay-gain: every title
+        # read with read(4096), one GPU batch per device, the album from the
+        # summed histogram), checked title by title against the oracle
+        import audiotools
+        mem = [_MemTrack(xh[k * n * 2:(k + 1) * n * 2], 2, 16, 44100) for k in range(n_tracks)]
+        t1 = time.perf_counter()
+        got = list(audiotools.calculate_replay_gain(mem))
+        ddt = time.perf_counter() - t1
+        dbad = [k for k, g in enumerate(got)
+                if not (g[1] == oracle_port.rg_gain(hists[k]) and g[2] == peaks[k])]
+        out["dropin_calculate_replay_gain"] = {
+            "metric": "audiotools.calculate_replay_gain over the config-4 album, "
+                      "FLAC-frame-equivalents/s (host PCM in, reader to gains)",
+            "value": round(n_tracks * n / BLOCK / ddt, 1), "unit": "frames/s",
+            "seconds": round(ddt, 3), "tracks": n_tracks,
+            "verified_tracks": n_tracks - len(dbad),
+            "verified_album": bool(got) and got[0][3] == want_album and
+            got[0][4] == max(peaks),
+            "gpu_calls": "one replaygain batch per device (replaygain.album_scan)"}
+        del xh, hists
     del x, hist
     return out
 
@@ -1118,10 +1142,50 @@ def rg4_leg(args, torch, dist, world, rank, device, barrier, threads=16):
 def album_reduce(dist, world, hist, peak):
     """an album spread over ranks: SUM of the uint32 window histograms (held
     as int32; two's-complement sums are the same bits) and MAX of the peak,
-    in place -- exact and order-independent (SURVEY 8(e) ReplayGain row)"""
+    in place over RCCL -- the product's replaygain.album_allreduce (SURVEY
+    8(e) ReplayGain row)"""
     if world > 1:
-        dist.all_reduce(hist, op=dist.ReduceOp.SUM)
-        dist.all_reduce(peak, op=dist.ReduceOp.MAX)
+        from audiotools import replaygain
+        replaygain.album_allreduce(hist, peak)
+
+
+class _MemReader(object):
+    """a PCMReader over int32 samples in host memory (bench stand-in for a
+    decoded file: the drop-in leg times the GPU path, not disk reads)"""
+
+    def __init__(self, samples, channels, bits, rate):
+        self.samples, self.channels, self.bits_per_sample = samples, channels, bits
+        self.sample_rate, self.channel_mask, self.pos = rate, 0x3 if channels == 2 else 0x4, 0
+
+    def read(self, frames):
+        from audiotools import pcm as _pcm
+        a = self.samples[self.pos:self.pos + frames * self.channels]
+        self.pos += len(a)
+        return _pcm.FrameList._wrap(a, self.channels, self.bits_per_sample)
+
+    def close(self):
+        pass
+
+
+class _MemTrack(object):
+    """the AudioFile methods calculate_replay_gain calls, over _MemReader"""
+
+    def __init__(self, samples, channels, bits, rate):
+        self.s, self.ch, self.bits, self.rate = samples, channels, bits, rate
+
+    def sample_rate(self):
+        return self.rate
+
+    def channels(self):
+        return self.ch
+
+    def total_frames(self):
+        return len(self.s) // self.ch
+
+    def to_pcm(self):
+        return _MemReader(self.s, self.ch, self.bits, self.rate)
+
+
 
 
 def replaygain_leg(args, torch, dist, world, rank, device, pcm, n_tracks, barrier):

@@ -122,6 +122,19 @@ atg_status atg_engine_create(int device, atg_engine **out);
 atg_status atg_engine_create_ex(int device, uint32_t flags, atg_engine **out);
 void atg_engine_destroy(atg_engine *eng);
 
+/* Device choice for callers that do not name one (the drop-in entry points:
+   encode_flac, FlacDecoder, the process-wide engines), host code only, no
+   HIP call.  atg_pick_device: ATG_DEVICE, else LOCAL_RANK, else the next
+   visible device of a node-wide round robin (a flock'ed counter in
+   /dev/shm, per user; ATG_RR_FILE names another file), so the reference's
+   one-process-per-track conversions (audiotools/__init__.py:5263-5529)
+   spread over the node's GPUs.  Decided once per process (again after a
+   fork).  atg_visible_devices: the entries of HIP_VISIBLE_DEVICES /
+   CUDA_VISIBLE_DEVICES / ROCR_VISIBLE_DEVICES, else the GPU nodes of the KFD
+   topology (ATG_DEVICE_COUNT overrides, for tests); at least 1. */
+int atg_pick_device(void);
+int atg_visible_devices(void);
+
 /* Number of FLAC frames and worst-case output bytes of a batch, so callers
    can size outputs (the reference's recorders grow on demand; a batch
    engine needs bounds up front). */

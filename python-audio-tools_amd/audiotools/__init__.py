@@ -552,9 +552,12 @@ def calculate_replay_gain(tracks, progress=None):
     every AudioFile of `tracks` (reference audiotools/__init__.py:2845-2912):
     the album's most numerous sample rate rounded up to a supported
     ReplayGain rate is the target, each track converted to it (channels
-    above 2 downmixed) by PCMConverter, its title gain and peak measured by
-    one ReplayGain object (replaygain.hip), the album gain from the summed
-    window histogram.  ValueError if a problem occurs."""
+    above 2 downmixed) by PCMConverter and read as the reference's
+    ReplayGain.title_gain reads it; then the whole album is analysed in one
+    GPU batch per device (replaygain.album_scan: titles sharded over the
+    node's GPUs, the shards' window histograms summed and peaks max'd), the
+    album gain from the summed histogram.  Gains and peaks are those of the
+    title-by-title reference computation.  ValueError if a problem occurs."""
     if len(tracks) == 0:
         return
     from bisect import bisect
@@ -565,8 +568,9 @@ def calculate_replay_gain(tracks, progress=None):
     track_frames = [resampled_frame_count(t.total_frames(), t.sample_rate(), target_rate)
                     for t in tracks]
     current, total = 0, sum(track_frames)
-    rg = replaygain.ReplayGain(target_rate)
-    gains = []
+    if target_rate not in replaygain.RATES:
+        raise ValueError("unsupported sample rate")
+    titles = []
     for track, frames in zip(tracks, track_frames):
         reader = track.to_pcm()
         if reader.channels > 2:
@@ -578,15 +582,13 @@ def calculate_replay_gain(tracks, progress=None):
             reader = PCMConverter(reader, target_rate, out_ch, out_mask,
                                   reader.bits_per_sample)
         if progress is not None:
-            gain, peak = rg.title_gain(PCMReaderProgress(reader, total, progress,
-                                                         current_frames=current))
+            reader = PCMReaderProgress(reader, total, progress, current_frames=current)
             current += frames
-        else:
-            gain, peak = rg.title_gain(reader)
-        gains.append((track, gain, peak))
-    album_gain, album_peak = rg.album_gain()
-    for track, gain, peak in gains:
-        yield (track, gain, peak, album_gain, album_peak)
+        titles.append(replaygain._read_title(reader, target_rate))
+    gains, hist, peak = replaygain.album_scan(titles, target_rate)
+    album_gain, album_peak = replaygain.album_gain_of(hist, peak)
+    for track, (gain, tpeak) in zip(tracks, gains):
+        yield (track, gain, tpeak, album_gain, album_peak)
 
 
 # the format classes (their modules import the names above)

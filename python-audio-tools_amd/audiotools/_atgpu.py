@@ -35,7 +35,7 @@ EXPORTS = (
     "atg_flac_encode_host_async", "atg_flac_encode_host_wait",
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
     "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_engine_set_inflight",
-    "atg_engine_inflight",
+    "atg_engine_inflight", "atg_pick_device", "atg_visible_devices",
     "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
     "atg_flac_encode_frames_batch", "atg_service_connect", "atg_service_close",
@@ -298,6 +298,10 @@ def load_library():
         lib.atg_engine_set_inflight.restype = ctypes.c_int
         lib.atg_engine_inflight.argtypes = [P]
         lib.atg_engine_inflight.restype = c_u32
+        lib.atg_pick_device.argtypes = []
+        lib.atg_pick_device.restype = ctypes.c_int
+        lib.atg_visible_devices.argtypes = []
+        lib.atg_visible_devices.restype = ctypes.c_int
         lib.atg_engine_kernel_times.argtypes = [
             P, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_float),
             ctypes.c_int]
@@ -1118,10 +1122,15 @@ _alac_encoder = None
 
 
 def default_device():
-    for var in ("ATG_DEVICE", "LOCAL_RANK"):
-        if os.environ.get(var, "") != "":
-            return int(os.environ[var])
-    return 0
+    """ATG_DEVICE, else LOCAL_RANK, else this process's turn of a node-wide
+    round robin over the visible GPUs (atg_pick_device, csrc/devices.hip):
+    one process per track under track2track -j N lands on N GPUs"""
+    return int(load_library().atg_pick_device())
+
+
+def visible_devices():
+    """GPUs this process may use (atg_visible_devices; no HIP call)"""
+    return int(load_library().atg_visible_devices())
 
 
 def engine():
@@ -1158,6 +1167,91 @@ def alac_encoder():
         if _alac_encoder is None:
             _alac_encoder = AlacEncoder(default_device())
         return _alac_encoder
+
+
+# ---- batches sharded over the node's GPUs ---------------------
+# A batch entry point (encode_flac_batch, decode_flac_batch,
+# calculate_replay_gain) splits its tracks into contiguous groups, one per
+# device, balanced by PCM frames, and runs every group on its device's
+# engine in a thread of its own (the C calls release the GIL); results are
+# merged in track order.  No collective: the groups are independent, except
+# ReplayGain's album histogram / peak, reduced by the caller (replaygain.py).
+_shard_objs = {}
+
+
+def batch_devices():
+    """devices a batch call shards over: the one ATG_DEVICE / LOCAL_RANK
+    names (a process bound to a GPU), else every visible GPU.
+    ATG_SHARD_DEVICES="0,0" lists them explicitly (tests: two shards on one
+    GPU take the multi-device path)"""
+    v = os.environ.get("ATG_SHARD_DEVICES", "")
+    if v.strip():
+        return [int(x) for x in v.split(",") if x.strip()]
+    for var in ("ATG_DEVICE", "LOCAL_RANK"):
+        if os.environ.get(var, "").strip():
+            return [int(os.environ[var])]
+    return list(range(visible_devices()))
+
+
+def shard_ranges(weights, n):
+    """contiguous [t0, t1) ranges of len(weights) tracks over at most n
+    shards, each ending where the running weight first reaches its share
+    of the total; empty ranges dropped"""
+    weights = [max(0, int(w)) for w in weights]
+    t, n = len(weights), max(1, min(n, len(weights)))
+    if t == 0:
+        return []
+    total = float(sum(weights)) or float(t)
+    w = weights if sum(weights) else [1] * t
+    out, t0, run = [], 0, 0
+    for k in range(1, n + 1):
+        goal = total * k / n
+        t1 = t0
+        while t1 < t and (run + w[t1] <= goal or t1 == t0) and (t - t1) > (n - k):
+            run += w[t1]
+            t1 += 1
+        if k == n:
+            t1 = t
+        if t1 > t0:
+            out.append((t0, t1))
+        t0 = t1
+    return out
+
+
+def shard_object(kind, i, device):
+    """the engine / decoder of shard i on `device` (one per shard, kept for
+    the process's lifetime like engine())"""
+    key = (kind, i, device)
+    with _engine_lock:
+        obj = _shard_objs.get(key)
+        if obj is None:
+            obj = {"engine": Engine, "decoder": Decoder, "alac_decoder": AlacDecoder}[kind](
+                device)
+            _shard_objs[key] = obj
+        return obj
+
+
+def run_shards(fn, n):
+    """fn(i) for i in range(n) on n threads (one per device); results in
+    order; the first exception is raised"""
+    if n == 1:
+        return [fn(0)]
+    out, err = [None] * n, []
+
+    def one(i):
+        try:
+            out[i] = fn(i)
+        except BaseException as e:  # noqa: B902 -- re-raised below
+            err.append(e)
+
+    th = [threading.Thread(target=one, args=(i,)) for i in range(n)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    if err:
+        raise err[0]
+    return out
 
 
 def pcm_convert(kind, pcm, channels, in_bps, out_bps=None, channel_mask=0,
@@ -1208,11 +1302,12 @@ def replaygain_hist_gain(d_hist, n):
     return [g[i] for i in range(n)]
 
 
-def replaygain_host(pcm, tracks, n_albums=0, return_hist=False):
-    """same as replaygain_device for int32 PCM in host memory
+def replaygain_host(pcm, tracks, n_albums=0, return_hist=False, eng=None):
+    """same as replaygain_device for int32 PCM in host memory, on `eng`'s
+    device (the process-wide engine's by default)
     -> (results, album_peaks, album_gains[, album histograms uint32])"""
     lib = load_library()
-    eng = engine()
+    eng = eng or engine()
     a = np.ascontiguousarray(pcm, dtype=np.int32)
     d_pcm, d_hist = ctypes.c_void_p(), ctypes.c_void_p()
     _check(lib, lib.atg_device_alloc(eng.handle, max(4, a.nbytes), ctypes.byref(d_pcm)))

@@ -54,22 +54,36 @@ def decode_flac_batch(images):
     """decode a list of .flac images (bytes) in one GPU batch.
     -> list of (status, streaminfo, int32 interleaved PCM); status is an
     ATG_FD_* code (0 = decoded and MD5-verified)."""
-    parts, tracks, infos, pos = [], [], [], 0
+    infos, bodies = [], []
     for img in images:
         rc, si, _ = _atgpu.read_metadata(img)
         if rc:
             raise _metadata_error(rc)
-        body = bytes(img[si.frames_offset:])
-        pad = (-len(body)) % 4
-        tracks.append(_atgpu.dec_track(pos, len(body), si))
-        parts.append(body + b"\0" * pad)
         infos.append(si)
-        pos += len(body) + pad
-    pcm_i32, res, _, _ = _atgpu.decoder().decode(b"".join(parts), tracks)
+        bodies.append(bytes(img[si.frames_offset:]))
+    # the streams sharded over the node's GPUs (_atgpu.batch_devices),
+    # balanced by PCM frames
+    devs = _atgpu.batch_devices()
+    ranges = (_atgpu.shard_ranges([si.total_samples for si in infos], len(devs))
+              if len(devs) > 1 else [(0, len(infos))])
+
+    def shard(i):
+        t0, t1 = ranges[i]
+        parts, tracks, pos = [], [], 0
+        for si, body in zip(infos[t0:t1], bodies[t0:t1]):
+            pad = (-len(body)) % 4
+            tracks.append(_atgpu.dec_track(pos, len(body), si))
+            parts.append(body + b"\0" * pad)
+            pos += len(body) + pad
+        dec = (_atgpu.decoder() if len(ranges) == 1
+               else _atgpu.shard_object("decoder", i, devs[i]))
+        return dec.decode(b"".join(parts), tracks)
+
     out = []
-    for si, r in zip(infos, res):
-        a = r.pcm_offset * si.channels
-        out.append((r.status, si, pcm_i32[a:a + r.pcm_frames * si.channels]))
+    for (t0, t1), (pcm_i32, res, _, _) in zip(ranges, _atgpu.run_shards(shard, len(ranges))):
+        for si, r in zip(infos[t0:t1], res):
+            a = r.pcm_offset * si.channels
+            out.append((r.status, si, pcm_i32[a:a + r.pcm_frames * si.channels]))
     return out
 
 

@@ -31,7 +31,7 @@ under track2track).
 
 `encode_flac_batch` is the batch form the engine is built for: many tracks
 in one GPU pass (what track2track -j N achieves with N processes), MD5
-chains on the GPU.
+chains on the GPU, the tracks sharded over the node's GPUs.
 
 `encode_alac` / `encode_alac_batch` do the same for ALAC (reference
 src/encoders/alac.c:30-189; GPU kernels alac_encode.hip).
@@ -119,14 +119,30 @@ def encode_flac_batch(filenames, pcmreaders, block_size, max_lpc_order,
         pcm = np.concatenate(parts) if parts else np.zeros(0, dtype=np.int32)
         if bps <= 16:
             pcm = pcm.astype(np.int16)
-        out, results, offsets, pcm_frames = _atgpu.engine().encode(
-            opts, pcm, tracks, channels, bps, rate)
+        # the tracks sharded over the node's GPUs (contiguous groups balanced
+        # by frames, one engine per device, _atgpu.batch_devices)
+        devs = _atgpu.batch_devices()
+        ranges = (_atgpu.shard_ranges([t[1] for t in tracks], len(devs))
+                  if len(devs) > 1 else [(0, len(tracks))])
+
+        def shard(i):
+            t0, t1 = ranges[i]
+            s0 = tracks[t0][0]
+            s1 = tracks[t1 - 1][0] + tracks[t1 - 1][1]
+            eng = (_atgpu.engine() if len(ranges) == 1
+                   else _atgpu.shard_object("engine", i, devs[i]))
+            return eng.encode(opts, pcm[s0 * channels:s1 * channels],
+                              [(a - s0, n, fs) for a, n, fs in tracks[t0:t1]],
+                              channels, bps, rate)
+
         lists = []
-        for f, res in zip(files, results):
-            f.write(memoryview(out[res.out_offset:res.out_offset + res.bytes]))
-            lo, n = res.first_frame, res.n_frames
-            lists.append([(int(offsets[lo + i]), int(pcm_frames[lo + i]))
-                          for i in range(n)])
+        for (t0, t1), (out, results, offsets, pcm_frames) in zip(
+                ranges, _atgpu.run_shards(shard, len(ranges))):
+            for f, res in zip(files[t0:t1], results):
+                f.write(memoryview(out[res.out_offset:res.out_offset + res.bytes]))
+                lo, n = res.first_frame, res.n_frames
+                lists.append([(int(offsets[lo + i]), int(pcm_frames[lo + i]))
+                              for i in range(n)])
         for r in pcmreaders:
             r.close()
         return lists

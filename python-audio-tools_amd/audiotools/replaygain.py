@@ -22,6 +22,40 @@ RATES = (48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000, 18900,
          37800, 56000, 64000, 88200, 96000, 112000, 128000, 144000, 176400, 192000)
 
 
+def _read_title(pcmreader, sample_rate):
+    """drain one title the way ReplayGain.title_gain reads it (read(4096)
+    until an empty FrameList, replaygain.c:210-305) -> (int32 samples, read
+    sizes, channels, bits) or None when nothing was read"""
+    if pcmreader.sample_rate != sample_rate:
+        raise ValueError("pcmreader's sample rate doesn't match")
+    parts, sizes = [], []
+    while True:
+        fl = pcmreader.read(4096)
+        if not isinstance(fl, pcm.FrameList):
+            raise TypeError("pcmreader.read() must return a FrameList")
+        if not fl.frames:
+            break
+        if fl.channels not in (1, 2):
+            raise ValueError("FrameList must contain only 1 or 2 channels")
+        parts.append(fl.samples)
+        sizes.append(fl.frames)
+    bps, ch = pcmreader.bits_per_sample, pcmreader.channels
+    if parts and bps not in (8, 16, 24):
+        raise ValueError("unsupported bits per sample")
+    if not parts:
+        return None
+    return np.concatenate(parts), sizes, ch, bps
+
+
+def _rg_track(offset, frames, sizes, ch, bps, rate):
+    t = _atgpu.RgTrack(offset, frames, ch, bps, rate, 0)
+    # each read() result is one analyze_samples call: its size decides the
+    # fp64 summation grouping (replaygain.c:210-305)
+    if any(n != 4096 for n in sizes[:-1]) or sizes[-1] > 4096:
+        t.set_chunks(sizes)
+    return t
+
+
 class ReplayGain(object):
     """ReplayGain(sample_rate) (replaygain.c:115-182).  Like the reference,
     the object keeps only the album state between titles -- the summed
@@ -37,47 +71,118 @@ class ReplayGain(object):
     def title_gain(self, pcmreader):
         """(title gain, title peak) of one reader; its histogram is added
         to the album's (get_title_gain, replaygain.c:776-800)"""
-        if pcmreader.sample_rate != self.sample_rate:
-            raise ValueError("pcmreader's sample rate doesn't match")
-        parts, sizes = [], []
-        while True:
-            fl = pcmreader.read(4096)
-            if not isinstance(fl, pcm.FrameList):
-                raise TypeError("pcmreader.read() must return a FrameList")
-            if not fl.frames:
-                break
-            if fl.channels not in (1, 2):
-                raise ValueError("FrameList must contain only 1 or 2 channels")
-            parts.append(fl.samples)
-            sizes.append(fl.frames)
-        bps, ch = pcmreader.bits_per_sample, pcmreader.channels
-        if parts and bps not in (8, 16, 24):
-            raise ValueError("unsupported bits per sample")
-        if not parts:
+        title = _read_title(pcmreader, self.sample_rate)
+        if title is None:
             return (0.0, 0.0)  # nothing read: no window, peak 0.0
-        samples = np.concatenate(parts)
-        frames = len(samples) // ch
-        track = _atgpu.RgTrack(0, frames, ch, bps, self.sample_rate, 0)
-        # each read() result is one analyze_samples call: its size decides
-        # the fp64 summation grouping (replaygain.c:210-305)
-        if any(n != 4096 for n in sizes[:-1]) or sizes[-1] > 4096:
-            track.set_chunks(sizes)
+        samples, sizes, ch, bps = title
+        track = _rg_track(0, len(samples) // ch, sizes, ch, bps, self.sample_rate)
         (res,), peaks, _, hist = _atgpu.replaygain_host(samples, [track], 1,
                                                         return_hist=True)
         self._album_hist += hist[0]
         self._album_peak = max(self._album_peak, peaks[0])
         return (res.title_gain, res.title_peak)
 
+    def add_album_state(self, hist, peak):
+        """fold another analysis' album histogram and peak into this one
+        (an album scanned in shards, album_scan)"""
+        self._album_hist += np.asarray(hist, dtype=np.uint64)
+        self._album_peak = max(self._album_peak, float(peak))
+
     def album_gain(self):
         """(album gain, album peak) over every title so far
         (get_album_gain, replaygain.c:803-807; ValueError when empty)"""
-        if not self._album_hist.any():
-            raise ValueError("Not enough samples to perform calculation")
-        (gain,) = _atgpu.replaygain_hist_gain_host(
-            (self._album_hist & 0xFFFFFFFF).astype(np.uint32))
-        if math.isnan(gain):
-            raise ValueError("Not enough samples to perform calculation")
-        return (gain, self._album_peak)
+        return album_gain_of(self._album_hist, self._album_peak)
+
+
+def album_gain_of(hist, peak):
+    """(album gain, album peak) of a summed 12000-bin histogram
+    (analyzeResult, replaygain.c:754-776; ValueError when empty)"""
+    hist = np.asarray(hist, dtype=np.uint64)
+    if not hist.any():
+        raise ValueError("Not enough samples to perform calculation")
+    (gain,) = _atgpu.replaygain_hist_gain_host((hist & 0xFFFFFFFF).astype(np.uint32))
+    if math.isnan(gain):
+        raise ValueError("Not enough samples to perform calculation")
+    return (gain, float(peak))
+
+
+def album_scan(titles, sample_rate):
+    """ReplayGain of a whole album in one GPU call per device.
+
+    titles: one entry per track, in album order: None (nothing read) or
+    (int32 samples, read sizes, channels, bits_per_sample) as _read_title
+    gives.  The non-empty titles are sharded over the node's GPUs
+    (_atgpu.batch_devices, contiguous groups balanced by frames); each
+    shard is one atg_replaygain_device batch whose album histogram and peak
+    come back with the titles' gains; the shards' histograms are summed and
+    their peaks max'd -- the album state the reference accumulates title by
+    title (replaygain.c:776-807).
+    -> ([(title_gain, title_peak)], album histogram uint64[12000], album peak)"""
+    if sample_rate not in RATES:
+        raise ValueError("unsupported sample rate")
+    idx = [i for i, t in enumerate(titles) if t is not None]
+    out = [(0.0, 0.0)] * len(titles)
+    hist = np.zeros(12000, dtype=np.uint64)
+    peak = 0.0
+    if not idx:
+        return out, hist, peak
+    devs = _atgpu.batch_devices()
+    frames = [len(titles[i][0]) // titles[i][2] for i in idx]
+    ranges = _atgpu.shard_ranges(frames, len(devs)) if len(devs) > 1 else [(0, len(idx))]
+
+    def shard(k):
+        t0, t1 = ranges[k]
+        # one buffer; a title's pcm_offset counts frames of its own channel
+        # count (sample pcm_offset * channels), so mono and stereo titles
+        # are placed at disjoint sample ranges
+        parts, tracks, spos = [], [], 0
+        for i in idx[t0:t1]:
+            samples, sizes, ch, bps = titles[i]
+            off = -(-spos // ch)
+            tracks.append(_rg_track(off, len(samples) // ch, sizes, ch, bps, sample_rate))
+            parts.append(np.asarray(samples, dtype=np.int32))
+            spos = off * ch + len(samples)
+        buf = np.zeros(max(1, spos), dtype=np.int32)
+        for p, tr in zip(parts, tracks):
+            buf[tr.pcm_offset * tr.channels:tr.pcm_offset * tr.channels + len(p)] = p
+        eng = None if len(ranges) == 1 else _atgpu.shard_object("engine", k, devs[k])
+        res, peaks, _, h = _atgpu.replaygain_host(buf, tracks, 1, return_hist=True, eng=eng)
+        return res, peaks[0], h[0]
+
+    for (t0, t1), (res, pk, h) in zip(ranges, _atgpu.run_shards(shard, len(ranges))):
+        for i, r in zip(idx[t0:t1], res):
+            out[i] = (r.title_gain, r.title_peak)
+        hist += h.astype(np.uint64)
+        peak = max(peak, pk)
+    return out, hist, peak
+
+
+def album_allreduce(hist, peak, group=None):
+    """an album scanned by several processes (one per GPU, torch.distributed
+    initialised -- the config-4 layout): SUM of the 12000-bin
+    window histograms and MAX of the peaks over the group -- exact and
+    order-independent.  torch tensors on the device (the histogram as int32:
+    two's-complement sums are the uint32 bits) are reduced in place over
+    RCCL ("nccl" backend) and returned; numpy / float inputs go through a
+    tensor on the process's device (gloo: on the host).
+    -> (hist, peak)"""
+    import torch
+    import torch.distributed as dist
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return hist, peak
+    if torch.is_tensor(hist):
+        pk = peak if torch.is_tensor(peak) else torch.tensor(
+            [float(peak)], dtype=torch.float64, device=hist.device)
+        dist.all_reduce(hist, op=dist.ReduceOp.SUM, group=group)
+        dist.all_reduce(pk, op=dist.ReduceOp.MAX, group=group)
+        return hist, pk
+    dev = (torch.device("cuda", torch.cuda.current_device())
+           if dist.get_backend(group) == "nccl" else torch.device("cpu"))
+    h = torch.as_tensor(np.asarray(hist, dtype=np.int64), device=dev)
+    p = torch.tensor([float(peak)], dtype=torch.float64, device=dev)
+    dist.all_reduce(h, op=dist.ReduceOp.SUM, group=group)
+    dist.all_reduce(p, op=dist.ReduceOp.MAX, group=group)
+    return h.cpu().numpy().astype(np.uint64), float(p.item())
 
 
 def batch_gains(pcm_i32, tracks, n_albums):

@@ -210,10 +210,8 @@ static int ensure_decoder(void)
 {
     if (g_dec)
         return 0;
-    const char *v = getenv("ATG_DEVICE");
-    if (!v)
-        v = getenv("LOCAL_RANK");
-    if (atg_decoder_create(v ? atoi(v) : 0, &g_dec) != ATG_OK) {
+    /* ATG_DEVICE, LOCAL_RANK, else the node-wide round robin */
+    if (atg_decoder_create(atg_pick_device(), &g_dec) != ATG_OK) {
         PyErr_SetString(PyExc_RuntimeError, atg_decoder_last_error());
         return -1;
     }

@@ -82,12 +82,11 @@ static atg_engine *g_eng;      /* this process's own engine (no service) */
 static atg_service *g_svc;     /* the encoder service (atgpu-encoderd) */
 static int g_svc_mode = -1;    /* -1 undecided, 0 own engine, 1 service */
 
+/* ATG_DEVICE, LOCAL_RANK, else a node-wide round robin over the visible
+   GPUs (atg_pick_device): track2track's processes spread over the node */
 static int engine_device(void)
 {
-    const char *v = getenv("ATG_DEVICE");
-    if (!v)
-        v = getenv("LOCAL_RANK");
-    return v ? atoi(v) : 0;
+    return atg_pick_device();
 }
 
 static PyObject *raise_atg(atg_status st)
