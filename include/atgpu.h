@@ -343,6 +343,12 @@ atg_status atg_device_free(atg_engine *eng, void *d_ptr);
 atg_status atg_copy_to_device(atg_engine *eng, void *d_dst, const void *src,
                               uint64_t bytes);
 atg_status atg_copy_device(atg_engine *eng, void *d_dst, const void *d_src, uint64_t bytes);
+/* Host-side gather: n host buffers (srcs[i], bytes[i]) copied back to back
+   into dst on `threads` host threads (0 = the library's default, at most
+   16) -- the reads of a batch of PCMReaders laid out in a (pinned) staging
+   buffer in one call at memory bandwidth. */
+atg_status atg_host_gather(void *dst, const void *const *srcs, const uint64_t *bytes,
+                           uint64_t n, uint32_t threads);
 atg_status atg_copy_to_host(atg_engine *eng, void *dst, const void *d_src,
                             uint64_t bytes);
 

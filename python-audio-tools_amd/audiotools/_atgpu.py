@@ -757,6 +757,22 @@ class Engine(object):
             dst.nbytes))
         return dst
 
+    def copy_to_device(self, d_dst, src):
+        """the numpy array src (its full size) -> device bytes at d_dst"""
+        src = np.ascontiguousarray(src)
+        _check(self.lib, self.lib.atg_copy_to_device(
+            self.handle, ctypes.c_void_p(d_dst), src.ctypes.data_as(ctypes.c_void_p), src.nbytes))
+
+    def device_alloc(self, nbytes):
+        """device memory on this engine's device -> pointer (device_free)"""
+        p = ctypes.c_void_p()
+        _check(self.lib, self.lib.atg_device_alloc(self.handle, max(4, int(nbytes)),
+                                                   ctypes.byref(p)))
+        return p.value
+
+    def device_free(self, d_ptr):
+        _check(self.lib, self.lib.atg_device_free(self.handle, ctypes.c_void_p(d_ptr)))
+
 
 def stream_header(options, channels, bits_per_sample, sample_rate, total_samples=0,
                   min_frame_bytes=0xFFFFFF, max_frame_bytes=0, md5=b"\0" * 16):
@@ -788,6 +804,35 @@ def pinned_empty(shape, dtype=np.uint8):
     # DMAs into must outlive the engine; at exit the process takes it back
     weakref.finalize(buf, lib.atg_host_free, p.value).atexit = False
     return np.frombuffer(buf, dtype=dtype, count=count).reshape(shape)
+
+
+_staging = {}
+_staging_lock = threading.Lock()
+
+
+def staging(key, nbytes):
+    """a page-locked host buffer of at least nbytes, one per key, kept for
+    the process's lifetime (grown on demand): uploads from it run at DMA
+    rate without a pinning cost per call"""
+    with _staging_lock:
+        b = _staging.get(key)
+        if b is None or b.nbytes < nbytes:
+            b = pinned_empty(max(int(nbytes), 1 << 20), np.uint8)
+            _staging[key] = b
+        return b
+
+
+_upool = None
+
+
+def upload_pool():
+    """a thread for host-to-device copies beside the host threads' fills"""
+    global _upool
+    with _staging_lock:
+        if _upool is None:
+            import concurrent.futures
+            _upool = concurrent.futures.ThreadPoolExecutor(4)
+        return _upool
 
 
 def read_metadata(data, sp_cap=4096):

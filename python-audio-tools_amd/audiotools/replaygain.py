@@ -12,11 +12,18 @@ No CPU path.
 
 import math
 import os
+import time
 
 import numpy as np
 
 from . import _atgpu
+from . import _encoders_c
 from . import pcm
+
+# album_scan's last call: host seconds per phase (summed over shards)
+_last_phases = {}
+# bytes per upload chunk of album_scan (pinned staging, per shard)
+STAGE_BYTES = 256 << 20
 
 RATES = (48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000, 18900,
          37800, 56000, 64000, 88200, 96000, 112000, 128000, 144000, 176400, 192000)
@@ -25,7 +32,9 @@ RATES = (48000, 44100, 32000, 24000, 22050, 16000, 12000, 11025, 8000, 18900,
 def _read_title(pcmreader, sample_rate):
     """drain one title the way ReplayGain.title_gain reads it (read(4096)
     until an empty FrameList, replaygain.c:210-305) -> (int32 samples, read
-    sizes, channels, bits) or None when nothing was read"""
+    sizes, channels, bits) or None when nothing was read; the samples are
+    the reads' arrays, not concatenated (album_scan copies them once, into
+    the upload staging)"""
     if pcmreader.sample_rate != sample_rate:
         raise ValueError("pcmreader's sample rate doesn't match")
     parts, sizes = [], []
@@ -37,14 +46,14 @@ def _read_title(pcmreader, sample_rate):
             break
         if fl.channels not in (1, 2):
             raise ValueError("FrameList must contain only 1 or 2 channels")
-        parts.append(fl.samples)
+        parts.append(np.ascontiguousarray(fl.samples, dtype=np.int32))
         sizes.append(fl.frames)
     bps, ch = pcmreader.bits_per_sample, pcmreader.channels
     if parts and bps not in (8, 16, 24):
         raise ValueError("unsupported bits per sample")
     if not parts:
         return None
-    return np.concatenate(parts), sizes, ch, bps
+    return parts, sizes, ch, bps
 
 
 def _rg_track(offset, frames, sizes, ch, bps, rate):
@@ -74,7 +83,8 @@ class ReplayGain(object):
         title = _read_title(pcmreader, self.sample_rate)
         if title is None:
             return (0.0, 0.0)  # nothing read: no window, peak 0.0
-        samples, sizes, ch, bps = title
+        parts, sizes, ch, bps = title
+        samples = np.concatenate(parts)
         track = _rg_track(0, len(samples) // ch, sizes, ch, bps, self.sample_rate)
         (res,), peaks, _, hist = _atgpu.replaygain_host(samples, [track], 1,
                                                         return_hist=True)
@@ -110,8 +120,8 @@ def album_scan(titles, sample_rate):
     """ReplayGain of a whole album in one GPU call per device.
 
     titles: one entry per track, in album order: None (nothing read) or
-    (int32 samples, read sizes, channels, bits_per_sample) as _read_title
-    gives.  The non-empty titles are sharded over the node's GPUs
+    (int32 samples -- one array or the list of the reads' arrays --, read
+    sizes, channels, bits_per_sample) as _read_title gives.  The non-empty titles are sharded over the node's GPUs
     (_atgpu.batch_devices, contiguous groups balanced by frames); each
     shard is one atg_replaygain_device batch whose album histogram and peak
     come back with the titles' gains; the shards' histograms are summed and
@@ -126,28 +136,79 @@ def album_scan(titles, sample_rate):
     peak = 0.0
     if not idx:
         return out, hist, peak
+    nsamp = {i: sum(len(p) for p in _parts(titles[i][0])) for i in idx}
     devs = _atgpu.batch_devices()
-    frames = [len(titles[i][0]) // titles[i][2] for i in idx]
+    frames = [nsamp[i] // titles[i][2] for i in idx]
     ranges = _atgpu.shard_ranges(frames, len(devs)) if len(devs) > 1 else [(0, len(idx))]
+    _last_phases.update(fill_s=0.0, upload_wait_s=0.0, gpu_s=0.0)
 
     def shard(k):
         t0, t1 = ranges[k]
-        # one buffer; a title's pcm_offset counts frames of its own channel
-        # count (sample pcm_offset * channels), so mono and stereo titles
-        # are placed at disjoint sample ranges
-        parts, tracks, spos = [], [], 0
+        eng = (_atgpu.engine() if len(ranges) == 1
+               else _atgpu.shard_object("engine", k, devs[k]))
+        # one device buffer; a title's pcm_offset counts frames of its own
+        # channel count (sample pcm_offset * channels), so mono and stereo
+        # titles sit at disjoint sample ranges
+        tracks, starts, spos = [], [], 0
         for i in idx[t0:t1]:
-            samples, sizes, ch, bps = titles[i]
+            parts, sizes, ch, bps = titles[i]
             off = -(-spos // ch)
-            tracks.append(_rg_track(off, len(samples) // ch, sizes, ch, bps, sample_rate))
-            parts.append(np.asarray(samples, dtype=np.int32))
-            spos = off * ch + len(samples)
-        buf = np.zeros(max(1, spos), dtype=np.int32)
-        for p, tr in zip(parts, tracks):
-            buf[tr.pcm_offset * tr.channels:tr.pcm_offset * tr.channels + len(p)] = p
-        eng = None if len(ranges) == 1 else _atgpu.shard_object("engine", k, devs[k])
-        res, peaks, _, h = _atgpu.replaygain_host(buf, tracks, 1, return_hist=True, eng=eng)
-        return res, peaks[0], h[0]
+            tracks.append(_rg_track(off, nsamp[i] // ch, sizes, ch, bps, sample_rate))
+            starts.append(off * ch)
+            spos = off * ch + nsamp[i]
+        d_pcm = eng.device_alloc(4 * spos)
+        d_hist = eng.device_alloc(4 * 12000)
+        try:
+            # the titles' reads copied once, by host threads, into pinned
+            # staging (two buffers), each chunk uploaded by a thread of its
+            # own while the next chunk is filled
+            cap = max(STAGE_BYTES, 4 * max(nsamp[i] for i in idx[t0:t1]))
+            stages = [_atgpu.staging(("rg", k, b), cap).view(np.int32) for b in (0, 1)]
+            titles_k = idx[t0:t1]
+            chunks, j = [], 0
+            while j < len(titles_k):
+                m = j
+                while m < len(titles_k) and starts[m] + nsamp[titles_k[m]] - starts[j] <= \
+                        len(stages[0]):
+                    m += 1
+                chunks.append((j, m))
+                j = m
+            pending = [None, None]
+            for c, (j, m) in enumerate(chunks):
+                a = starts[j]
+                b = starts[m - 1] + nsamp[titles_k[m - 1]]
+                if pending[c % 2] is not None:
+                    pending[c % 2].result()  # that buffer's upload is done
+                view = stages[c % 2][:b - a]
+
+                # the chunk's reads in one threaded host gather (GIL
+                # released); a mono/stereo alignment gap is zeroed
+                segs = []
+                for q in range(j, m):
+                    i = titles_k[q]
+                    end = starts[q + 1] if q + 1 < m else b
+                    segs.extend(_parts(titles[i][0]))
+                    if end > starts[q] + nsamp[i]:
+                        segs.append(np.zeros(end - starts[q] - nsamp[i], dtype=np.int32))
+                tf = time.perf_counter()
+                _encoders_c.gather_into(view, segs)
+                _last_phases["fill_s"] += time.perf_counter() - tf
+                pending[c % 2] = _atgpu.upload_pool().submit(
+                    eng.copy_to_device, d_pcm + 4 * a, view)
+            tw = time.perf_counter()
+            for f in pending:
+                if f is not None:
+                    f.result()
+            _last_phases["upload_wait_s"] += time.perf_counter() - tw
+            tg = time.perf_counter()
+            res, peaks = _atgpu.replaygain_device(d_pcm, tracks, 1, d_hist)
+            h = np.empty(12000, dtype=np.uint32)
+            eng.copy_to_host(h, d_hist)
+            _last_phases["gpu_s"] += time.perf_counter() - tg
+        finally:
+            eng.device_free(d_pcm)
+            eng.device_free(d_hist)
+        return res, peaks[0], h
 
     for (t0, t1), (res, pk, h) in zip(ranges, _atgpu.run_shards(shard, len(ranges))):
         for i, r in zip(idx[t0:t1], res):
@@ -155,6 +216,11 @@ def album_scan(titles, sample_rate):
         hist += h.astype(np.uint64)
         peak = max(peak, pk)
     return out, hist, peak
+
+
+def _parts(samples):
+    """a title's samples: the list of its reads' arrays, or one array"""
+    return samples if isinstance(samples, (list, tuple)) else [samples]
 
 
 def album_allreduce(hist, peak, group=None):

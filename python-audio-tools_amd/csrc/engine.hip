@@ -2353,6 +2353,41 @@ atg_status atg_copy_device(atg_engine *e, void *d_dst, const void *d_src, uint64
     return ATG_OK;
 }
 
+atg_status atg_host_gather(void *dst, const void *const *srcs, const uint64_t *bytes,
+                           uint64_t n, uint32_t threads)
+{
+    if ((!dst || !srcs || !bytes) && n)
+        return fail(ATG_ERR_INVALID, "NULL argument");
+    std::vector<uint64_t> off(n + 1, 0);
+    for (uint64_t i = 0; i < n; ++i)
+        off[i + 1] = off[i] + bytes[i];
+    const uint64_t total = off[n];
+    const unsigned nt = (unsigned)std::max<uint64_t>(
+        1, std::min<uint64_t>({threads ? threads : host_threads(), n, total / (4u << 20) + 1}));
+    auto run = [&](unsigned k) {
+        // parts whose first byte falls in thread k's share of the bytes
+        const uint64_t lo = total * k / nt, hi = total * (k + 1) / nt;
+        uint64_t i = (uint64_t)(std::upper_bound(off.begin(), off.end(), lo) - off.begin()) - 1;
+        if (k == 0)
+            i = 0;
+        else if (off[i] < lo)
+            ++i;
+        for (; i < n && off[i] < hi; ++i)
+            std::memcpy((uint8_t *)dst + off[i], srcs[i], bytes[i]);
+    };
+    if (nt == 1) {
+        run(0);
+        return ATG_OK;
+    }
+    std::vector<std::thread> th;
+    for (unsigned k = 1; k < nt; ++k)
+        th.emplace_back(run, k);
+    run(0);
+    for (auto &t : th)
+        t.join();
+    return ATG_OK;
+}
+
 atg_status atg_copy_to_host(atg_engine *e, void *dst, const void *d_src, uint64_t bytes)
 {
     ATG_HANDLE_LOCK(e);

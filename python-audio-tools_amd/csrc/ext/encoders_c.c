@@ -437,7 +437,75 @@ static PyObject *set_segment_frames(PyObject *self, PyObject *arg)
     return PyLong_FromLong(old);
 }
 
+/* gather_into(dst, parts, offset=0) -> bytes written: the parts (objects
+   with the buffer protocol, e.g. the int32 sample arrays of a title's
+   FrameList reads) copied back to back into the writable buffer dst from
+   byte `offset` on, by host threads with the GIL released
+   (atg_host_gather) -- album_scan's upload staging (replaygain.py) */
+static PyObject *gather_into(PyObject *self, PyObject *args)
+{
+    (void)self;
+    PyObject *dst_o, *parts_o;
+    unsigned long long offset = 0;
+    if (!PyArg_ParseTuple(args, "OO|K", &dst_o, &parts_o, &offset))
+        return NULL;
+    PyObject *seq = PySequence_Fast(parts_o, "parts must be a sequence");
+    if (!seq)
+        return NULL;
+    const Py_ssize_t n = PySequence_Fast_GET_SIZE(seq);
+    Py_buffer dst;
+    if (PyObject_GetBuffer(dst_o, &dst, PyBUF_WRITABLE | PyBUF_C_CONTIGUOUS) < 0) {
+        Py_DECREF(seq);
+        return NULL;
+    }
+    Py_buffer *views = (Py_buffer *)PyMem_Calloc((size_t)(n ? n : 1), sizeof(Py_buffer));
+    const void **srcs = (const void **)PyMem_Calloc((size_t)(n ? n : 1), sizeof(void *));
+    uint64_t *bytes = (uint64_t *)PyMem_Calloc((size_t)(n ? n : 1), sizeof(uint64_t));
+    Py_ssize_t got = 0;
+    unsigned long long total = 0;
+    PyObject *ret = NULL;
+    if (!views || !srcs || !bytes) {
+        PyErr_NoMemory();
+        goto done;
+    }
+    for (; got < n; ++got) {
+        if (PyObject_GetBuffer(PySequence_Fast_GET_ITEM(seq, got), &views[got],
+                               PyBUF_C_CONTIGUOUS) < 0)
+            goto done;
+        srcs[got] = views[got].buf;
+        bytes[got] = (uint64_t)views[got].len;
+        total += (unsigned long long)views[got].len;
+    }
+    if (offset > (unsigned long long)dst.len || total > (unsigned long long)dst.len - offset) {
+        PyErr_SetString(PyExc_ValueError, "parts do not fit the destination");
+        goto done;
+    }
+    {
+        atg_status st;
+        Py_BEGIN_ALLOW_THREADS
+        st = atg_host_gather((uint8_t *)dst.buf + offset, srcs, bytes, (uint64_t)n, 0);
+        Py_END_ALLOW_THREADS
+        if (st != ATG_OK) {
+            raise_atg(st);
+            goto done;
+        }
+    }
+    ret = PyLong_FromUnsignedLongLong(total);
+done:
+    for (Py_ssize_t i = 0; i < got; ++i)
+        PyBuffer_Release(&views[i]);
+    PyMem_Free(views);
+    PyMem_Free(srcs);
+    PyMem_Free(bytes);
+    PyBuffer_Release(&dst);
+    Py_DECREF(seq);
+    return ret;
+}
+
 static PyMethodDef methods[] = {
+    {"gather_into", gather_into, METH_VARARGS,
+     "gather_into(dst, parts, offset=0) -> bytes: the parts' bytes back to back into dst "
+     "(host threads, GIL released)"},
     {"encode_flac", (PyCFunction)(void (*)(void))encode_flac, METH_VARARGS | METH_KEYWORDS,
      "encode_flac(filename, pcmreader, block_size, max_lpc_order, "
      "min_residual_partition_order, max_residual_partition_order, ...) -> "

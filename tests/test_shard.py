@@ -53,32 +53,71 @@ def _titles():
         ch = 1 if k % 3 == 1 else 2
         n = 44100 // 4 + 911 * k
         x = signals.make("tone", n, ch, 16, seed=40 + k).astype(np.int32)
-        out.append((x, [4096] * (n // 4096) + ([n % 4096] if n % 4096 else []), ch, 16))
+        sizes = [4096] * (n // 4096) + ([n % 4096] if n % 4096 else [])
+        # the reads' arrays, as replaygain._read_title keeps them
+        parts = np.split(x, np.cumsum(sizes)[:-1] * ch) if k % 2 else x
+        out.append((parts, sizes, ch, 16))
     out.insert(3, None)  # a title that read nothing
     return out
 
 
-def _oracle_host(buf, tracks, n_albums, return_hist=False, eng=None):
-    """replaygain_host's contract, computed by the CPU oracle per title"""
-    class R(object):
-        pass
-    res, hist, peak = [], np.zeros(12000, dtype=np.uint64), 0.0
-    for t in tracks:
-        a = t.pcm_offset * t.channels
-        A, pk = oracle_port.rg_title(buf[a:a + t.pcm_frames * t.channels], t.channels,
-                                     t.bits_per_sample, t.sample_rate)
-        r = R()
-        r.title_gain, r.title_peak = oracle_port.rg_gain(A), pk
-        res.append(r)
-        hist += A
-        peak = max(peak, pk)
-    return res, [peak], [], hist.astype(np.uint32)[None, :]
+class _FakeDevice(object):
+    """device memory and replaygain_device's contract on the host: the GPU
+    call is the CPU oracle (oracle/replaygain_port.c) per title"""
+
+    def __init__(self):
+        self.mem, self.next = {}, 1 << 40
+
+    def _find(self, p):
+        base = max(b for b in self.mem if b <= p)
+        return self.mem[base], p - base
+
+    def device_alloc(self, n):
+        p = self.next
+        self.mem[p] = np.zeros(max(4, int(n)), dtype=np.uint8)
+        self.next += 1 << 36
+        return p
+
+    def device_free(self, p):
+        del self.mem[p]
+
+    def copy_to_device(self, d, src):
+        buf, o = self._find(d)
+        b = np.ascontiguousarray(src).view(np.uint8).reshape(-1)
+        buf[o:o + len(b)] = b
+
+    def copy_to_host(self, dst, d):
+        buf, o = self._find(d)
+        dst.view(np.uint8).reshape(-1)[:] = buf[o:o + dst.nbytes]
+        return dst
+
+    def replaygain_device(self, d_pcm, tracks, n_albums=0, d_album_hist=None):
+        class R(object):
+            pass
+        buf, o = self._find(d_pcm)
+        x = buf[o:].view(np.int32)
+        res, hist, peak = [], np.zeros(12000, dtype=np.uint64), 0.0
+        for t in tracks:
+            a = t.pcm_offset * t.channels
+            A, pk = oracle_port.rg_title(x[a:a + t.pcm_frames * t.channels], t.channels,
+                                         t.bits_per_sample, t.sample_rate)
+            r = R()
+            r.title_gain, r.title_peak = oracle_port.rg_gain(A), pk
+            res.append(r)
+            hist += A
+            peak = max(peak, pk)
+        self.copy_to_device(d_album_hist, hist.astype(np.uint32))
+        return res, [peak]
 
 
 def test_album_scan_sharded_matches_oracle(monkeypatch):
-    monkeypatch.setattr(_atgpu, "replaygain_host", _oracle_host)
+    dev = _FakeDevice()
+    monkeypatch.setattr(_atgpu, "replaygain_device", dev.replaygain_device)
     monkeypatch.setattr(_atgpu, "batch_devices", lambda: [0, 1, 2])
-    monkeypatch.setattr(_atgpu, "shard_object", lambda kind, i, dev: None)
+    monkeypatch.setattr(_atgpu, "shard_object", lambda kind, i, d: dev)
+    # small staging buffers: the titles are uploaded over several chunks
+    monkeypatch.setattr(_atgpu, "staging", lambda key, n: np.zeros(n, dtype=np.uint8))
+    monkeypatch.setattr(replaygain, "STAGE_BYTES", 1)
     titles = _titles()
     gains, hist, peak = replaygain.album_scan(titles, 44100)
     want_hist, want_peak = np.zeros(12000, dtype=np.uint64), 0.0
@@ -86,7 +125,7 @@ def test_album_scan_sharded_matches_oracle(monkeypatch):
         if t is None:
             assert g == (0.0, 0.0)
             continue
-        A, pk = oracle_port.rg_title(t[0], t[2], 16, 44100)
+        A, pk = oracle_port.rg_title(np.concatenate(replaygain._parts(t[0])), t[2], 16, 44100)
         assert g == (oracle_port.rg_gain(A), pk)
         want_hist += A
         want_peak = max(want_peak, pk)
@@ -109,7 +148,7 @@ def _rank(rank, world, port, q):
         titles = [t for t in _titles() if t is not None][rank::world]
         hist, peak = np.zeros(12000, dtype=np.uint64), 0.0
         for x, _, ch, bps in titles:
-            A, pk = oracle_port.rg_title(x, ch, bps, 44100)
+            A, pk = oracle_port.rg_title(np.concatenate(replaygain._parts(x)), ch, bps, 44100)
             hist += A
             peak = max(peak, pk)
         h, p = replaygain.album_allreduce(hist, peak)
@@ -135,7 +174,7 @@ def test_album_allreduce_two_ranks_gloo():
         assert p.exitcode == 0
     want_hist, want_peak = np.zeros(12000, dtype=np.uint64), 0.0
     for x, _, ch, bps in [t for t in _titles() if t is not None]:
-        A, pk = oracle_port.rg_title(x, ch, bps, 44100)
+        A, pk = oracle_port.rg_title(np.concatenate(replaygain._parts(x)), ch, bps, 44100)
         want_hist += A
         want_peak = max(want_peak, pk)
     for _, h, p, th, tp in got:
