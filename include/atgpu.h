@@ -466,8 +466,11 @@ atg_status atg_flac_decode_device(atg_decoder *dec, const void *d_data, uint64_t
    .. 16.  A batch's STREAMINFO MD5 checks are serial hashes (~12 ms per 1 MB
    of decoded PCM whatever the batch width); from 4 on, the hashes of every
    batch in flight advance together, one launch per enqueue on one stream,
-   each batch's in n - 2 slices.  Fails while a batch is unwaited; the last
-   waited batch's buffers are no longer fetchable afterwards. */
+   each batch's in n - 2 slices.  Each slot holds its batch's PCM, restore
+   scratch and MD5 byte image (~5 GB for a 1024-track config-2 batch);
+   lowering the depth frees the slots past it.  Fails while a batch is
+   unwaited; the last waited batch's buffers are no longer fetchable
+   afterwards. */
 atg_status atg_decoder_set_inflight(atg_decoder *dec, uint32_t n);
 
 /* The parse's frame-end hypothesis (flac_decode.hip k_dec_spec): 1 (default)
@@ -476,21 +479,28 @@ atg_status atg_decoder_set_inflight(atg_decoder *dec, uint32_t n);
    subframe; the restore checks every such frame on the subframe it walks
    anyway, and a batch with a failed check is redone with every subframe
    walked inside atg_flac_decode_wait -- results are those of the full parse
-   (src/decoders/flac.c:174-285) either way.  0: every subframe walked by the
-   parse.  2: as 1, and every batch redone (self-check of the redo path). */
+   (src/decoders/flac.c:174-285) either way; after four redone batches in a
+   row the decoder switches itself to 0 (a stream of input the hypothesis
+   keeps failing on would pay two decodes per batch) until the mode is set
+   again.  0: every subframe walked by the parse.  2: as 1, and every batch
+   redone (self-check of the redo path). */
 atg_status atg_decoder_set_frame_hypothesis(atg_decoder *dec, int mode);
 
 /* Batches this decoder redid with the full parse (mode 1: failed checks). */
 uint64_t atg_decoder_frame_hypothesis_redos(atg_decoder *dec);
 
-/* Asynchronous form of atg_flac_decode_device (three batches in flight):
-   the scan, parse and frame walk run on the decoder's stream (two host
-   round trips for the counts), then the restore, emit and per-track MD5 on
-   the batch's own slot stream with its own buffers, so batch k's back half
-   runs under batch k+1's scan and parse.  Returns once everything is
-   queued.  d_data must stay valid until the wait; the PCM pointer the wait
-   returns stays valid until the slot is reused (the third enqueue after
-   it).  A fourth enqueue before a wait fails with ATG_ERR_INVALID. */
+/* Asynchronous form of atg_flac_decode_device, D batches in flight (D = 3
+   unless atg_decoder_set_inflight says otherwise, each slot with its own
+   buffers): the scan, parse and frame walk run on the decoder's stream
+   (two host round trips for the counts), then the restore, emit and
+   per-track MD5 on the batch's slot stream, so batch k's back half runs
+   under batch k+1's scan and parse.  Returns once everything is queued.
+   d_data must stay valid and unchanged until the batch is waited: when a
+   frame-end hypothesis fails its check, atg_flac_decode_wait re-reads
+   d_data to redo the batch with the full parse.  The PCM pointer the wait
+   returns stays valid until the slot is reused, D enqueues later.  An
+   enqueue while D batches are unwaited fails with ATG_ERR_INVALID; an
+   enqueue that fails leaves nothing of its batch queued. */
 atg_status atg_flac_decode_device_async(atg_decoder *dec, const void *d_data, uint64_t len,
                                         const atg_flac_dec_track *tracks, uint32_t n_tracks,
                                         uint64_t *ticket);
@@ -577,9 +587,14 @@ atg_status atg_replaygain_device(const int32_t *d_pcm, const atg_rg_track *track
    out[2] R_b the rounding sums into the state and the output, out[3]
    1 / (1 - ||A^L||_inf), out[4] L the segment length in frames, out[5] G_L
    = max over lags >= L (see replaygain.hip k_rg_seg).  A warm segment's
-   outputs err by at most G m + G_L (m + R_s) out[3] + 2 R_b for the
+   outputs err by at most G m + G_L (m + R_s) out[3] + 1.5 R_b for the
    largest measured seam state difference m. */
 atg_status atg_replaygain_bound(uint32_t sample_rate, double *out);
+/* The multiple of R_b the kernels use in that bound: 1.5 -- R_b is two
+   trajectories' rounding, and the bound counts three trajectories once
+   each (warm, predecessor, and the serial one at disjoint times; the
+   derivation is in replaygain.hip). */
+double atg_replaygain_rb_factor(void);
 /* windows whose histogram bin the host's log10 moved (lifetime count; a
    window within 1e-9 of a bin edge is binned with the C library's log10) */
 uint64_t atg_replaygain_rebinned_windows(void);

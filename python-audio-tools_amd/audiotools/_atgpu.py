@@ -36,6 +36,7 @@ EXPORTS = (
     "atg_flac_encode_device", "atg_flac_encode_device_async", "atg_flac_encode_wait",
     "atg_engine_kernel_times", "atg_engine_set_host_chunk_bytes", "atg_engine_set_inflight",
     "atg_engine_inflight", "atg_pick_device", "atg_visible_devices",
+    "atg_host_gather", "atg_replaygain_rb_factor",
     "atg_flac_encode_frames",
     "atg_flac_max_frames_bytes", "atg_flac_stream_header", "atg_host_alloc",
     "atg_flac_encode_frames_batch", "atg_service_connect", "atg_service_close",

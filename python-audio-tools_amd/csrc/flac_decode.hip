@@ -1791,6 +1791,7 @@ struct DBuf {
 // flight no longer queue their chains behind one another on shared hardware
 // queues (the 13.4 ms at four slots above).
 constexpr int kDecSlots = 3;
+constexpr uint32_t kSpecStreak = 4; // redone batches in a row before mode 0
 constexpr int kDecMaxSlots = 16;
 struct DecSlot {
     DBuf pcm, bytes, md5, md5meta;
@@ -1830,6 +1831,7 @@ struct atg_decoder {
     DBuf cbits, spec; // the frame-end hypothesis: candidate bitmap, lengths
     int spec_mode = 1; // atg_decoder_set_frame_hypothesis
     uint64_t spec_redos = 0; // batches redone with the full parse
+    uint32_t spec_streak = 0; // consecutive batches redone
     bool spec_off = false; // set while a batch is redone with the full parse
     std::vector<ScanSeg> segs_h; // the scan's segments (upload source)
     DecSlot slot[kDecMaxSlots];
@@ -2091,6 +2093,24 @@ static hipError_t dec_results_d2h(DecSlot &sl, uint32_t n, hipStream_t q)
         e = hipMemcpyAsync(sl.md5_h + 16 * (size_t)n, (uint8_t *)sl.md5.p + 16 * (size_t)n, 16,
                            hipMemcpyDeviceToHost, q);
     return e;
+}
+
+// a batch whose enqueue failed part-way: nothing of it may run on or be
+// waited for -- out of the rolled queue (its slices would otherwise keep
+// advancing a stale entry, and a reuse of the slot would queue it twice),
+// its streams drained, the slot free
+static void dec_abort(atg_decoder *d, DecSlot &sl)
+{
+    auto it = std::find(d->roll_q.begin(), d->roll_q.end(), &sl);
+    if (it != d->roll_q.end())
+        d->roll_q.erase(it);
+    sl.roll_done = sl.roll_parts = 0;
+    (void)hipStreamSynchronize(d->s);
+    if (d->s_roll)
+        (void)hipStreamSynchronize(d->s_roll);
+    if (sl.s_md5)
+        (void)hipStreamSynchronize(sl.s_md5);
+    sl.busy = false;
 }
 
 // the tail of a rolled batch on s_roll: tails + padding + digests, the
@@ -2438,13 +2458,25 @@ static atg_status finish_decode(atg_decoder *d, DecSlot &sl, atg_flac_dec_result
         d->spec_off = true;
         atg_status st = enqueue_decode(d, sl, sl.data, sl.len, want.data(), (uint32_t)want.size());
         d->spec_off = false;
-        if (st != ATG_OK)
+        if (st != ATG_OK) {
+            dec_abort(d, sl);
             return st;
+        }
         while (sl.rolled && sl.roll_done < sl.roll_parts)
-            if ((st = dec_roll_step(d, nullptr)) != ATG_OK)
+            if ((st = dec_roll_step(d, nullptr)) != ATG_OK) {
+                dec_abort(d, sl);
                 return st;
+            }
         DHIP(hipEventSynchronize(sl.ev_done));
         ++d->spec_redos;
+        // a stream of inputs the hypothesis keeps failing on (junk after
+        // frames, damaged files) would pay two decodes per batch: after
+        // kSpecStreak redone batches in a row the parse walks every
+        // subframe (mode 0) until the caller sets the mode again
+        if (++d->spec_streak >= kSpecStreak && d->spec_mode == 1)
+            d->spec_mode = 0;
+    } else if (sl.spec) {
+        d->spec_streak = 0;
     }
     // timings: scan, parse, chain (both passes + the host prefix), subframe,
     // emit, md5, total (scan start -> md5 end)
@@ -2525,8 +2557,10 @@ atg_status atg_flac_decode_device_async(atg_decoder *d, const void *d_data, uint
     if (st != ATG_OK)
         return st;
     st = enqueue_decode(d, *sl, (const uint8_t *)d_data, len, tracks, n);
-    if (st != ATG_OK)
+    if (st != ATG_OK) {
+        dec_abort(d, *sl);
         return st;
+    }
     sl->busy = true;
     *ticket = sl->ticket;
     return ATG_OK;
@@ -2648,6 +2682,16 @@ atg_status atg_decoder_set_inflight(atg_decoder *d, uint32_t n)
     for (DecSlot &sl : d->slot)
         if (sl.busy)
             return dfail(ATG_ERR_INVALID, "a decode batch is in flight: wait for it first");
+    // a lower depth gives the workspaces of the slots past it back (a
+    // config-2 slot holds ~5 GB: PCM, rows, byte image)
+    for (int k = (int)n; k < kDecMaxSlots; ++k) {
+        DecSlot &sl = d->slot[k];
+        if (sl.s_md5)
+            (void)hipStreamSynchronize(sl.s_md5);
+        for (DBuf *b : {&sl.pcm, &sl.bytes, &sl.md5, &sl.md5meta, &sl.tracks, &sl.frames, &sl.jobs,
+                        &sl.warm, &sl.rows, &sl.meta})
+            b->release();
+    }
     d->depth = (int)n;
     d->last = -1; // the oldest-slot rotation starts over
     return ATG_OK;
@@ -2659,6 +2703,7 @@ atg_status atg_decoder_set_frame_hypothesis(atg_decoder *d, int mode)
     if (!d || mode < 0 || mode > 2)
         return dfail(ATG_ERR_INVALID, "frame hypothesis mode must be 0, 1 or 2");
     d->spec_mode = mode;
+    d->spec_streak = 0;
     return ATG_OK;
 }
 

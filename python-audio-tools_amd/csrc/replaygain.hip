@@ -142,7 +142,15 @@ __device__ __forceinline__ double filt_r(Chan &s, double x, const double *ky, co
 //     after its L counted frames) plus its accumulated rounding sum_k A^k E r;
 //     so a counted output n frames into the warm segment errs by at most
 //       |C A^n (measured)| + |C A^(n+L) D_prev| + |sum_k C A^(n+k) E r|
-//       + its own rounding  <=  G m + G_L D_prev + R_b + R_b
+//       + its own rounding  <=  G m + G_L D_prev + 1.5 R_b
+//     -- the rounding terms count three trajectories, each once: rho (and
+//     so R_b = sum_n |C A^n E| rho) is two trajectories' worth, i.e. one
+//     trajectory's rounding over ANY set of distinct sample times
+//     propagates to the output with at most R_b / 2.  The predecessor's
+//     rounding (before the seam) and the warm segment's own (after it)
+//     give R_b / 2 each, and the serial trajectory's rounding enters both
+//     terms but at disjoint times (before and after the seam), so R_b / 2
+//     in all: 1.5 R_b (kRgRbFactor)
 //     with G = max_n ||C A^n||_1, G_L = max_{n >= L} ||C A^n||_1, R_b =
 //     sum_n |C A^n E| rho (C picks the Butterworth output, E the rounding
 //     injection), and D_prev <= (m + R_s) / (1 - ||A^L||_inf) over the track
@@ -163,6 +171,9 @@ constexpr uint32_t kRgSegWindows = 4;   // windows per segment (rounded to 10-fr
 // the C library's log10 (the reference's): the device log10 is accurate to
 // a few ulp, ~1e-12 at values below 12000, not correctly rounded.
 constexpr double kRgLogGuard = 1e-9;
+// the multiple of R_b in the certification bound (G m + G_L D_prev + 1.5
+// R_b above; atg_replaygain_rb_factor reports it)
+constexpr double kRgRbFactor = 1.5;
 
 struct RgSeg {
     uint64_t fw, f0, f1; // warm-up start, first counted frame, end (track frames)
@@ -402,11 +413,11 @@ __global__ __launch_bounds__(256) void k_rg_bin(const RgTrack *__restrict__ trac
     const double rho_y = 2.0 * g22 * (1e-10 + X * T.sb + Y * T.sa);
     const double rho_b = 2.0 * g6 * (T.ke * Y + T.ko * Bv);
     const double Rb = T.py * rho_y + T.pb * rho_b, Rs = T.qy * rho_y + T.qb * rho_b;
-    // the bound on a counted output sample's error in the warm segments:
-    // measured seam difference, the predecessor's decayed start error, three
-    // trajectories' rounding (warm, predecessor, serial: 1.5 Rb, rho being
-    // two trajectories' worth)
-    const double delta = T.gmax * dm + T.gl * (dm + Rs) * T.ginv + 1.5 * Rb;
+    // the bound on a counted output sample's error in the warm segments
+    // (the derivation above): measured seam difference, the predecessor's
+    // decayed start error, and kRgRbFactor = 1.5 R_b of rounding (three
+    // trajectories' worth, see the derivation)
+    const double delta = T.gmax * dm + T.gl * (dm + Rs) * T.ginv + kRgRbFactor * Rb;
     const uint32_t ww = warm_win ? warm_win[t] : 0xFFFFFFFFu;
     bool unsure = warm_win && ww != 0xFFFFFFFFu && !(T.ginv > 0.0 && delta < 1e300);
     // rounding of the window's own sum of n squares (both trajectories)
@@ -964,6 +975,8 @@ extern "C" {
 void atg_replaygain_set_warmup(int frames) { g_rg_warm_override = frames; }
 
 uint32_t atg_replaygain_fallback_tracks(void) { return g_rg_fallback_tracks; }
+
+double atg_replaygain_rb_factor(void) { return kRgRbFactor; }
 
 uint64_t atg_replaygain_rebinned_windows(void) { return g_rg_rebinned; }
 

@@ -169,3 +169,34 @@ def test_redo_inside_a_pipeline(gpu_engine, depth):
     # one redo per batch holding the junk stream
     assert dec.frame_hypothesis_redos() == (depth + 5) // 2
     dec.close()
+
+
+def test_redo_streak_falls_back_to_full_parse(gpu_engine):
+    """batch after batch of input the hypothesis fails on: the decoder redoes
+    four in a row, then walks every subframe (mode 0, flac_decode.hip
+    kSpecStreak) -- every batch's results equal the full parse's, and only
+    four redos are paid"""
+    from audiotools import _atgpu
+    opts = _atgpu.make_options(**oracle_port.PRESETS["8"])
+    pcm = signals.make("tone", 4096 * 6 + 55, 2, 16, seed=13)
+    out, res, _, _ = gpu_engine.encode(opts, pcm.astype(np.int16), [(0, len(pcm) // 2)], 2, 16,
+                                       44100)
+    img = out[res[0].out_offset:res[0].out_offset + res[0].bytes].tobytes()
+    rc, si, _ = _atgpu.read_metadata(img)
+    tracks, blob = _batch([img])
+    _, _, offs, _ = _atgpu.Decoder(0).decode(blob, tracks)
+    cut = si.frames_offset + int(offs[1])
+    bad = img[:cut] + b"\0\0" + img[cut:]
+    tracks, blob = _batch([bad, img])
+    ref = _atgpu.Decoder(0)
+    ref.set_frame_hypothesis(0)
+    want = [_key(r) for r in ref.decode(blob, tracks)[1]]
+    ref.close()
+    dec = _atgpu.Decoder(0)
+    for _ in range(7):
+        assert [_key(r) for r in dec.decode(blob, tracks)[1]] == want
+    assert dec.frame_hypothesis_redos() == 4
+    dec.set_frame_hypothesis(1)  # the caller's setting starts a new streak
+    assert [_key(r) for r in dec.decode(blob, tracks)[1]] == want
+    assert dec.frame_hypothesis_redos() == 5
+    dec.close()

@@ -110,3 +110,16 @@ def test_bound_holds_for_two_trajectories(rate):
                   [a + c for a, c in zip(bh, b0)])
     err = np.abs(b_w - b_r).max()
     assert 0 < err <= g * d0 + rb, (err, g * d0 + rb)
+
+
+def test_rb_factor_pinned():
+    """the kernels' bound takes 1.5 R_b (three trajectories' rounding,
+    each once; R_b is two trajectories' worth), the constant the derivation
+    in replaygain.hip and the header state (they said 2 R_b
+    while the code used 1.5)"""
+    lib = _atgpu.load_library()
+    lib.atg_replaygain_rb_factor.argtypes = []
+    lib.atg_replaygain_rb_factor.restype = ctypes.c_double
+    assert lib.atg_replaygain_rb_factor() == 1.5
+    hdr = open(os.path.join(ROOT, "include", "atgpu.h")).read()
+    assert "+ 1.5 R_b" in hdr
