@@ -46,6 +46,9 @@
 // wave were slower (17.6 -> 23.4 ms, 12.6 -> 17.1 ms; 8 and 16 slower
 // still), their waves already cover the SIMDs' latency
 constexpr uint32_t kAdecParseLpw = 64, kAdecChainLpw = 1, kAdecChannelLpw = 64;
+// device bytes the parse may fill with a batch's residuals (config 5: 30 k
+// framesets x 6 channels x 4096 x 4 B = 2.9 GB)
+constexpr uint64_t kResidMax = 12ull << 30;
 
 namespace {
 
@@ -79,11 +82,14 @@ struct AElem {
 };
 
 struct AFs {
+    uint64_t res_base;   // residuals stored by the parse: channel k at
+                         // res + res_base + k * stride (~0: not stored)
     uint64_t start;      // absolute byte
     uint32_t bytes;      // frameset length (byte aligned)
     int32_t status;
     uint32_t nelem, nch, n0, track;
     uint64_t pcm_start;  // pass 2: first interleaved output sample
+    uint64_t job0;       // pass 2: the frameset's first channel job (its planar slots)
     AElem e[8];
 };
 
@@ -91,14 +97,49 @@ struct ACount {
     uint64_t pcm_frames;
     uint32_t n_fs;
     int32_t status;
+    uint32_t max_n0; // the track's longest frameset (the planar slot stride)
+    uint32_t pad;
 };
 
 // one frameset at absolute byte `start` (read_frame x elements, alac.c:204-233)
-__device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AFs &F)
+// a lane's values to its own 16-byte aligned region, four per store (the
+// lanes of a wave write different regions: four values fill a quarter
+// line per store instead of one word)
+struct Out4 {
+    int32_t *p;
+    int4 b;
+    __device__ __forceinline__ void put(uint32_t i, int32_t v)
+    {
+        const uint32_t q = i & 3u;
+        b.x = q == 0u ? v : b.x;
+        b.y = q == 1u ? v : b.y;
+        b.z = q == 2u ? v : b.z;
+        b.w = q == 3u ? v : b.w;
+        if (q == 3u)
+            *(int4 *)(p + i - 3u) = b;
+    }
+    // the samples of the last, partial group (i = samples written)
+    __device__ __forceinline__ void flush(uint32_t i)
+    {
+        const uint32_t q = i & 3u, a = i - q;
+        if (q > 0u)
+            p[a] = b.x;
+        if (q > 1u)
+            p[a + 1u] = b.y;
+        if (q > 2u)
+            p[a + 2u] = b.z;
+    }
+};
+
+// res: where this frameset's residuals go (channel k at res + k * stride,
+// at most stride values each), or null
+__device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AFs &F,
+                         int32_t *res = nullptr, uint32_t stride = 0)
 {
     ABitRC r;
     const uint64_t b0 = start * 8;
     r.init(w, b0, T.end * 8);
+    F.res_base = ~0ull;
     F.start = start;
     F.bytes = 0;
     F.status = AD_OK;
@@ -173,8 +214,24 @@ __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AF
                 g.init(N, ss, T.ih, T.hm, T.mk);
                 uint32_t n = 0;
                 int32_t v;
-                while (g.next(r, v))
-                    ++n;
+                if (res) {
+                    // the values too, for the channel restore (k_adec_channel
+                    // then runs the adaptive filter without decoding again)
+                    Out4 q;
+                    q.p = res + (uint64_t)(F.nch + c) * stride;
+                    q.b = make_int4(0, 0, 0, 0);
+                    while (g.next(r, v)) {
+                        if (n < stride)
+                            q.put(n, v);
+                        ++n;
+                    }
+                    q.flush(n < stride ? n : stride);
+                    if (n > stride)
+                        res = nullptr; // a channel longer than the slot: not stored
+                } else {
+                    while (g.next(r, v))
+                        ++n;
+                }
                 E.nres[c] = n;
             }
         }
@@ -205,7 +262,9 @@ __global__ __launch_bounds__(64) void k_adec_parse(const uint32_t *__restrict__ 
                                                    const ADTrack *__restrict__ tr,
                                                    const uint32_t *__restrict__ pred_track,
                                                    const uint64_t *__restrict__ pred_start,
-                                                   uint64_t npred, AFs *__restrict__ recs)
+                                                   uint64_t npred, AFs *__restrict__ recs,
+                                                   int32_t *__restrict__ resid, uint64_t res_fs,
+                                                   uint32_t res_stride)
 {
     if (threadIdx.x >= kAdecParseLpw)
         return;
@@ -214,9 +273,21 @@ __global__ __launch_bounds__(64) void k_adec_parse(const uint32_t *__restrict__ 
         return;
     const ADTrack T = tr[pred_track[i]];
     AFs F;
-    parse_fs(w, T, pred_start[i], F);
+    int32_t *res = resid ? resid + i * res_fs : nullptr;
+    parse_fs(w, T, pred_start[i], F, res, res_stride);
+    // every channel's residuals stored (parse_fs drops res on a channel
+    // longer than the slot; a failed parse is never restored)
+    if (res && F.status == AD_OK) {
+        bool fit = F.nch * (uint64_t)res_stride <= res_fs;
+        for (uint32_t k = 0; k < F.nelem; ++k)
+            for (uint32_t c = 0; c < F.e[k].cc; ++c)
+                fit = fit && F.e[k].nres[c] <= res_stride;
+        if (fit)
+            F.res_base = i * res_fs;
+    }
     F.track = pred_track[i];
     F.pcm_start = 0;
+    F.job0 = 0;
     recs[i] = F;
 }
 
@@ -236,7 +307,7 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
         return;
     const ADTrack T = tr[t];
     uint64_t pos = T.start, remaining = T.remaining, pcm = 0;
-    uint32_t nfs = 0, k = 0, njob = 0;
+    uint32_t nfs = 0, k = 0, njob = 0, max_n0 = 0;
     int32_t status = AD_OK;
     while (remaining) {
         // the prediction for this position, if any (predictions ascend)
@@ -258,6 +329,7 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
         if (pass == 2) {
             F.track = t;
             F.pcm_start = T.pcm_base + pcm * T.channels;
+            F.job0 = T.job_base + njob;
             dense[T.fs_base + nfs] = F;
             for (uint32_t c = 0; c < F.nch; ++c)
                 jobs[T.job_base + njob + c] = make_uint2((uint32_t)(T.fs_base + nfs), c);
@@ -265,6 +337,7 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
         njob += F.nch;
         ++nfs;
         pcm += F.n0;
+        max_n0 = F.n0 > max_n0 ? F.n0 : max_n0;
         pos = F.start + F.bytes;
     }
     if (pass == 1) {
@@ -272,14 +345,16 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
         c.pcm_frames = pcm;
         c.n_fs = nfs;
         c.status = status;
+        c.max_n0 = max_n0;
+        c.pad = 0;
         counts[t] = c;
     }
 }
 
 // decode_subframe (alac.c:1147-1235) for one channel, ORDER coefficients in
-// registers; out[i] for i < n
-template <int ORDER, class R>
-__device__ __forceinline__ void restore_fixed(R &r, AResidualReader &g, const int32_t *coef_in,
+// registers; out[i] for i < n (16-byte aligned)
+template <int ORDER, class R, class G>
+__device__ __forceinline__ void restore_fixed(R &r, G &g, const int32_t *coef_in,
                               uint32_t qshift, uint32_t ss, uint32_t n, int32_t *out)
 {
     int32_t c[ORDER], h[ORDER + 1]; // h[0] newest
@@ -289,10 +364,15 @@ __device__ __forceinline__ void restore_fixed(R &r, AResidualReader &g, const in
 #pragma unroll
     for (int j = 0; j <= ORDER; ++j)
         h[j] = 0;
+    Out4 ob;
+    ob.p = out;
+    ob.b = make_int4(0, 0, 0, 0);
     for (uint32_t i = 0; i < n; ++i) {
         int32_t res;
-        if (!g.next(r, res))
+        if (!g.next(r, res)) {
+            ob.flush(i);
             return;
+        }
         int32_t s;
         if (i == 0) {
             s = res;
@@ -322,17 +402,18 @@ __device__ __forceinline__ void restore_fixed(R &r, AResidualReader &g, const in
                 live = live && (pos ? e > 0 : e < 0);
             }
         }
-        out[i] = s;
+        ob.put(i, s);
 #pragma unroll
         for (int j = ORDER; j > 0; --j)
             h[j] = h[j - 1];
         h[0] = s;
     }
+    ob.flush(n);
 }
 
 // any other order (the encoder writes only 4 and 8): history in the output
-template <class R>
-__device__ __forceinline__ void restore_generic(R &r, AResidualReader &g, int32_t *c, uint32_t order,
+template <class R, class G>
+__device__ __forceinline__ void restore_generic(R &r, G &g, int32_t *c, uint32_t order,
                                 uint32_t qshift, uint32_t ss, uint32_t n, int32_t *out)
 {
     if (order >= 31) { // the reference's verbatim branch advances i twice
@@ -394,12 +475,67 @@ __device__ __forceinline__ void restore_generic(R &r, AResidualReader &g, int32_
     }
 }
 
-// K3: one channel of one frameset -> planar[pcm_start * nch + ch * n0 + i]
+// The residuals the parse stored, as AResidualReader hands them out: four
+// per 16-byte load, the next four loaded while these are used
+struct StoredRes {
+    const int32_t *p;
+    uint32_t i, n;
+    int4 cur, nxt;
+    __device__ __forceinline__ void init(const int32_t *base, uint32_t count)
+    {
+        p = base;
+        i = 0;
+        n = count;
+        cur = n ? *(const int4 *)p : make_int4(0, 0, 0, 0);
+        nxt = n > 4u ? *(const int4 *)(p + 4) : make_int4(0, 0, 0, 0);
+    }
+    template <class R>
+    __device__ __forceinline__ bool next(R &, int32_t &out)
+    {
+        if (i >= n)
+            return false;
+        const uint32_t q = i & 3u;
+        out = q == 0u ? cur.x : q == 1u ? cur.y : q == 2u ? cur.z : cur.w;
+        ++i;
+        if (q == 3u) {
+            cur = nxt;
+            if (i + 4u < n)
+                nxt = *(const int4 *)(p + i + 4u);
+        }
+        return true;
+    }
+};
+
+// decode_subframe for one channel from a residual source G (the bitstream
+// reader or the parse's stored values)
+template <class R, class G>
+__device__ __forceinline__ void restore_channel(R &r, G &g, int32_t *coef, uint32_t order,
+                                                uint32_t qshift, uint32_t ss, uint32_t n,
+                                                int32_t *out)
+{
+    if (order == 4 && qshift >= 1) {
+        int32_t c4[4] = {coef[0], coef[1], coef[2], coef[3]};
+        restore_fixed<4>(r, g, c4, qshift, ss, n, out);
+    } else if (order == 8 && qshift >= 1) {
+        int32_t c8[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            c8[k] = coef[k];
+        restore_fixed<8>(r, g, c8, qshift, ss, n, out);
+    } else {
+        restore_generic(r, g, coef, order, qshift, ss, n, out);
+    }
+}
+
+// K3: one channel of one frameset -> its planar slot, planar[job * pstride + i]
 __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict__ w,
                                                      const ADTrack *__restrict__ tr,
                                                      const AFs *__restrict__ dense,
                                                      const uint2 *__restrict__ jobs,
-                                                     uint64_t njobs, int32_t *__restrict__ planar)
+                                                     uint64_t njobs, int32_t *__restrict__ planar,
+                                                     uint32_t pstride,
+                                                     const int32_t *__restrict__ resid,
+                                                     uint32_t res_stride)
 {
     if (threadIdx.x >= kAdecChannelLpw)
         return;
@@ -417,7 +553,7 @@ __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict_
     }
     const AElem E = F.e[e];
     const uint64_t b0 = F.start * 8;
-    int32_t *out = planar + F.pcm_start + (uint64_t)jb.y * F.n0;
+    int32_t *out = planar + j * pstride; // the job's slot (= (F.job0 + jb.y) * pstride)
     ABitR r;
     if (E.uncompressed) {
         const uint64_t stride = (uint64_t)E.cc * T.bps;
@@ -436,23 +572,19 @@ __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict_
     for (uint32_t k = 0; k < order; ++k)
         coef[k] = r.get_signed(16);
     const uint32_t ss = T.bps - E.lsbs * 8u + (E.cc - 1u);
+    const uint32_t n = E.nres[c];
+    if (F.res_base != ~0ull) { // the parse stored this channel's residuals
+        ABitRC none;
+        StoredRes g;
+        g.init(resid + F.res_base + (uint64_t)jb.y * res_stride, n);
+        restore_channel(none, g, coef, order, qshift, ss, n, out);
+        return;
+    }
     ABitRC rc;
     rc.init(w, b0 + E.res_bit[c], T.end * 8);
     AResidualReader g;
     g.init(E.N, ss, T.ih, T.hm, T.mk);
-    const uint32_t n = E.nres[c];
-    if (order == 4 && qshift >= 1) {
-        int32_t c4[4] = {coef[0], coef[1], coef[2], coef[3]};
-        restore_fixed<4>(rc, g, c4, qshift, ss, n, out);
-    } else if (order == 8 && qshift >= 1) {
-        int32_t c8[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-            c8[k] = coef[k];
-        restore_fixed<8>(rc, g, c8, qshift, ss, n, out);
-    } else {
-        restore_generic(rc, g, coef, order, qshift, ss, n, out);
-    }
+    restore_channel(rc, g, coef, order, qshift, ss, n, out);
 }
 
 // K4: decorrelate (alac.c:1237-1259), prepend LSBs (:930-941), wave order
@@ -461,6 +593,7 @@ __global__ __launch_bounds__(256) void k_adec_interleave(const uint32_t *__restr
                                                          const ADTrack *__restrict__ tr,
                                                          const AFs *__restrict__ dense,
                                                          const int32_t *__restrict__ planar,
+                                                         uint32_t pstride,
                                                          int32_t *__restrict__ pcm)
 {
     const AFs &F = dense[blockIdx.x];
@@ -469,7 +602,7 @@ __global__ __launch_bounds__(256) void k_adec_interleave(const uint32_t *__restr
     static const uint8_t M[9][8] = {{0}, {0}, {0, 1}, {1, 2, 0}, {1, 2, 0, 3}, {1, 2, 0, 3, 4},
                                     {1, 2, 0, 5, 3, 4}, {1, 2, 0, 6, 3, 4, 5},
                                     {3, 4, 0, 7, 5, 6, 1, 2}};
-    const int32_t *src = planar + F.pcm_start;
+    const int32_t *src = planar + F.job0 * pstride; // channel k at src + k * pstride
     int32_t *dst = pcm + F.pcm_start;
     const uint64_t b0 = F.start * 8;
     for (uint32_t i = threadIdx.x; i < n0; i += blockDim.x) {
@@ -477,8 +610,8 @@ __global__ __launch_bounds__(256) void k_adec_interleave(const uint32_t *__restr
         uint32_t ch = 0;
         for (uint32_t e = 0; e < F.nelem; ++e) {
             const AElem E = F.e[e];
-            int32_t a = src[(uint64_t)ch * n0 + i];
-            int32_t b = E.cc == 2 ? src[(uint64_t)(ch + 1) * n0 + i] : 0;
+            int32_t a = src[(uint64_t)ch * pstride + i];
+            int32_t b = E.cc == 2 ? src[(uint64_t)(ch + 1) * pstride + i] : 0;
             if (!E.uncompressed) {
                 if (E.cc == 2 && E.lw > 0) {
                     int64_t t = (int64_t)(b * (int32_t)E.lw);
@@ -601,6 +734,7 @@ struct atg_alac_decoder {
     float times[kADTimed] = {};
     bool have_times = false;
     DBufA data, tracks, ptrack, pstart, recs, counts, dense, jobs, planar, pcm;
+    DBufA resid; // the parse's stored residuals (k_adec_channel reads them)
     std::vector<ADTrack> tr;
     std::vector<ACount> cnt;
     uint64_t total_samples = 0, total_fs = 0;
@@ -755,7 +889,7 @@ void atg_alac_decoder_destroy(atg_alac_decoder *d)
     (void)hipSetDevice(d->device);
     (void)hipStreamSynchronize(d->s);
     for (DBufA *b : {&d->data, &d->tracks, &d->ptrack, &d->pstart, &d->recs, &d->counts,
-                     &d->dense, &d->jobs, &d->planar, &d->pcm})
+                     &d->dense, &d->jobs, &d->planar, &d->pcm, &d->resid})
         b->release();
     for (auto &e : d->ev)
         (void)hipEventDestroy(e);
@@ -806,6 +940,19 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
         b.pred_n = (uint32_t)pstart.size() - b.pred_first;
     }
     const uint64_t np = pstart.size();
+    // a slot per predicted frameset for its residuals: channels x the
+    // largest frame (rounded to 16 bytes per channel), when the whole batch
+    // fits kResidMax; otherwise the restore decodes the residuals again
+    uint32_t res_stride = 0, res_ch = 0;
+    for (const ADTrack &b : d->tr) {
+        res_stride = std::max(res_stride, b.maxn);
+        res_ch = std::max(res_ch, b.channels);
+    }
+    res_stride = (res_stride + 3u) & ~3u;
+    uint64_t res_fs = (uint64_t)res_ch * res_stride;
+    const bool store_res = np && res_stride && np * res_fs * 4u <= kResidMax;
+    if (store_res)
+        ADHIP(d->resid.ensure(sizeof(int32_t) * np * res_fs));
     ADHIP(d->tracks.ensure(sizeof(ADTrack) * std::max<uint32_t>(n, 1)));
     ADHIP(d->ptrack.ensure(sizeof(uint32_t) * std::max<uint64_t>(np, 1)));
     ADHIP(d->pstart.ensure(sizeof(uint64_t) * std::max<uint64_t>(np, 1)));
@@ -828,7 +975,8 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
                            dim3((unsigned)((np + kAdecParseLpw - 1) / kAdecParseLpw)),
                            dim3(64), 0, s, w, dtr,
                            (const uint32_t *)d->ptrack.p, (const uint64_t *)d->pstart.p, np,
-                           (AFs *)d->recs.p);
+                           (AFs *)d->recs.p, store_res ? (int32_t *)d->resid.p : nullptr,
+                           res_fs, res_stride);
     ADHIP(hipGetLastError());
     ADHIP(hipEventRecord(d->ev[1], s));
     const dim3 tg((n + kAdecChainLpw - 1) / kAdecChainLpw);
@@ -846,6 +994,10 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
     // walk stopped with AD_CHANNEL_MISMATCH): tracks' interleaved samples
     // back to back, pcm_base = the track's first sample
     uint64_t fb = 0, samples = 0, jb = 0;
+    uint32_t pstride = 0; // planar slot per channel job: the longest frameset, 16-byte rounded
+    for (uint32_t t = 0; t < n; ++t)
+        pstride = std::max(pstride, d->cnt[t].max_n0);
+    pstride = (pstride + 3u) & ~3u;
     for (uint32_t t = 0; t < n; ++t) {
         ADTrack &b = d->tr[t];
         b.fs_base = fb;
@@ -859,7 +1011,7 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
     d->total_fs = fb;
     ADHIP(d->dense.ensure(sizeof(AFs) * std::max<uint64_t>(fb, 1)));
     ADHIP(d->jobs.ensure(sizeof(uint2) * std::max<uint64_t>(jb, 1)));
-    ADHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(samples, 1)));
+    ADHIP(d->planar.ensure(sizeof(int32_t) * std::max<uint64_t>(jb * pstride, 1)));
     ADHIP(d->pcm.ensure(sizeof(int32_t) * std::max<uint64_t>(samples, 1)));
     if (n)
         ADHIP(hipMemcpyAsync(d->tracks.p, d->tr.data(), sizeof(ADTrack) * n,
@@ -875,12 +1027,13 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
                            dim3((unsigned)((jb + kAdecChannelLpw - 1) / kAdecChannelLpw)),
                            dim3(64), 0, s, w,
                            dtr, (const AFs *)d->dense.p, (const uint2 *)d->jobs.p, jb,
-                           (int32_t *)d->planar.p);
+                           (int32_t *)d->planar.p, pstride, (const int32_t *)d->resid.p,
+                           res_stride);
     ADHIP(hipGetLastError());
     ADHIP(hipEventRecord(d->ev[3], s));
     if (fb)
         hipLaunchKernelGGL(k_adec_interleave, dim3((unsigned)fb), dim3(256), 0, s, w, dtr,
-                           (const AFs *)d->dense.p, (const int32_t *)d->planar.p,
+                           (const AFs *)d->dense.p, (const int32_t *)d->planar.p, pstride,
                            (int32_t *)d->pcm.p);
     ADHIP(hipGetLastError());
     ADHIP(hipEventRecord(d->ev[4], s));
