@@ -10,6 +10,7 @@ over the node's GPUs, and ReplayGain's album reduce.
   and peak MAX every rank gets equal the single-process album."""
 import os
 import socket
+import threading
 
 import numpy as np
 import pytest
@@ -67,19 +68,23 @@ class _FakeDevice(object):
 
     def __init__(self):
         self.mem, self.next = {}, 1 << 40
+        self.lock = threading.Lock()  # the shards run on threads of their own
 
     def _find(self, p):
-        base = max(b for b in self.mem if b <= p)
-        return self.mem[base], p - base
+        with self.lock:
+            base = max(b for b in self.mem if b <= p)
+            return self.mem[base], p - base
 
     def device_alloc(self, n):
-        p = self.next
-        self.mem[p] = np.zeros(max(4, int(n)), dtype=np.uint8)
-        self.next += 1 << 36
-        return p
+        with self.lock:
+            p = self.next
+            self.mem[p] = np.zeros(max(4, int(n)), dtype=np.uint8)
+            self.next += 1 << 36
+            return p
 
     def device_free(self, p):
-        del self.mem[p]
+        with self.lock:
+            del self.mem[p]
 
     def copy_to_device(self, d, src):
         buf, o = self._find(d)
