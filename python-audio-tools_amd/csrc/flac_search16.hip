@@ -159,6 +159,65 @@ __device__ __forceinline__ void sad_acc(uint32_t &sa, uint32_t x, uint32_t b)
     asm("v_sad_u32 %0, %1, %2, %0" : "+v"(sa) : "v"(x), "v"(b));
 }
 
+// Where pass 1 puts its per-sample x (every pass-1 form below takes one).
+// PkStore keeps x's low 16 bits, two samples per register (v_perm): the
+// low 16 bits of n = x - B (B's low half is 0 for shv <= 15), which are n
+// itself whenever |r| < 2^15 -- checked after pass 1 from the lane sums
+// (every |r| <= sum |r|).  32 registers instead of 64: what pass 1 and the
+// partition search keep live no longer spills.  ReSum is pass 2 by
+// recomputation, for a wave with a larger residual: the same tap chains,
+// summing v >> kv (v = n ^ (n >> 31)) per sample instead of keeping x; its
+// chunk loop is rolled (rare path, small code).
+struct PkStore {
+    static constexpr bool kStore = true;
+    static constexpr int kUnroll = ATG_RUN / 8;
+    uint32_t up[ATG_RUN / 2];
+    uint32_t sel; // v_perm selector: bits 0..15 of both x (quiet lane) or 8..23 (loud)
+    __device__ __forceinline__ void put2(int i, uint32_t x0, uint32_t x1)
+    {
+        up[i >> 1] = __builtin_amdgcn_perm(x1, x0, sel);
+    }
+};
+// a lane whose last finished job of the candidate coded with k >= 9 keeps
+// bits 8..23 of x instead (the same v_perm, another selector): n >> 8,
+// exact for |r| < 2^23, and v >> kv = (v >> 8) >> (kv - 8) for kv >= 8
+constexpr uint32_t kSelQuiet = 0x05040100u, kSelLoud = 0x06050201u;
+struct ReSum {
+    static constexpr bool kStore = false;
+    static constexpr int kUnroll = 1;
+    uint32_t kv, bias, s;
+    __device__ __forceinline__ void put2(int, uint32_t x0, uint32_t x1)
+    {
+        const int n0 = (int)(x0 - bias), n1 = (int)(x1 - bias);
+        s = s + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
+    }
+};
+
+typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
+
+// Pass 2 on PkStore's words: sum over the run of v >> kv, two samples per
+// word: n = q - B_lo (v_pk_sub_u16), v = n ^ (n >> 15), v >> kv (kv >= 15
+// gives 0 as v < 2^15; the 16-bit shift reads 4 bits of its amount), both
+// halves summed by one v_dot2_u32_u16 -- 5 VALU per two samples where the
+// 32-bit form takes 9.
+__device__ __forceinline__ uint32_t packed_vsum(const uint32_t (&up)[ATG_RUN / 2], uint32_t kv,
+                                                uint32_t b_lo)
+{
+    const unsigned short kk = (unsigned short)(kv < 15u ? kv : 15u);
+    const ushort2_t kk2 = {kk, kk};
+    const ushort2_t bb = {(unsigned short)b_lo, (unsigned short)b_lo};
+    const ushort2_t one = {1, 1};
+    uint32_t s = 0;
+#pragma unroll
+    for (int t = 0; t < ATG_RUN / 2; ++t) {
+        const ushort2_t q = __builtin_bit_cast(ushort2_t, up[t]) - bb;
+        const short2_t sg = __builtin_bit_cast(short2_t, q) >> (short)15;
+        const uint32_t v = __builtin_bit_cast(uint32_t, q) ^ __builtin_bit_cast(uint32_t, sg);
+        s = __builtin_amdgcn_udot2(__builtin_bit_cast(ushort2_t, v) >> kk2, one, s, false);
+    }
+    return s;
+}
+
 // packed int16 L - R per half word (v_pk_sub_u16): the side channel's
 // packed words, exact when every |L - R| fits int16
 __device__ __forceinline__ uint32_t pk_sub16(uint32_t a, uint32_t b)
@@ -225,9 +284,9 @@ __device__ __forceinline__ uint32_t win_pair(const Win &x, int ii, int j)
 // operand issues at half the rate on gfx950, tools/int_rate.hip).
 // subr: run is the L image and the samples are L - R (the side channel
 // of a frame whose |S| fits int16), packed on the fly from the R image
-template <int D>
+template <int D, class Sink>
 __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const int (&cp)[14],
-                                      int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                      int c0acc, int shv, bool lane0, int order, Sink &u,
                                       uint32_t &sabs, bool subr)
 {
     int tap0 = cp[0];
@@ -238,7 +297,7 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
     // chunk c + 1's words are read while chunk c is computed
     uint4 n0 = load_run4(run, subr), n1 = load_run4(run + 4, subr);
     uint32_t sa = 0;
-#pragma unroll
+#pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
         // keep each chunk's loads inside the chunk (bounds live registers)
         asm volatile("" ::: "memory");
@@ -261,15 +320,17 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                     acc[h] = dot2(win_pair(A, ii + h, j), cp[j], acc[h]);
+            uint32_t x[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 16 * c + ii + h;
-                uint32_t x = (uint32_t)acc[h] >> shv;
+                x[h] = (uint32_t)acc[h] >> shv;
                 if (i < ATG_FAST_ORDER)
-                    x = (lane0 && i < order) ? bm1 : x;
-                u[i] = x;
-                sad_acc(sa, x, bm1);
+                    x[h] = (lane0 && i < order) ? bm1 : x[h];
+                if (Sink::kStore)
+                    sad_acc(sa, x[h], bm1);
             }
+            u.put2(16 * c + ii, x[0], x[1]);
         }
     }
     sabs = sa;
@@ -292,9 +353,9 @@ __device__ __forceinline__ void lr_words(const uint4 &l, const uint4 &r, uint32_
 
 // DBL (shift 15): the fold tap 2^15 does not fit int16, so tap 0 is
 // (-2^14, 2^14) and is applied twice
-template <int D, bool DBL = false>
+template <int D, bool DBL, class Sink>
 __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const int (&cl)[14],
-                                         int c0acc, int shv, bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                         int c0acc, int shv, bool lane0, int order, Sink &u,
                                          uint32_t &sabs)
 {
     constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
@@ -315,7 +376,7 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
     // chunk c + 1's words are read while chunk c is computed
     uint4 nl = *(const uint4 *)run, nr = *(const uint4 *)runR;
     uint32_t sa = 0;
-#pragma unroll
+#pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 8; ++c) {
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -340,15 +401,17 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 #pragma unroll
                 for (int h = 0; h < 2; ++h)
                     accs[h] = dot2(W[12 + ii + h - k], cl[k], accs[h]);
+            uint32_t x[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 8 * c + ii + h;
-                uint32_t x = (uint32_t)accs[h] >> shv;
+                x[h] = (uint32_t)accs[h] >> shv;
                 if (i < ATG_FAST_ORDER)
-                    x = (lane0 && i < order) ? bm1 : x;
-                u[i] = x;
-                sad_acc(sa, x, bm1);
+                    x[h] = (lane0 && i < order) ? bm1 : x[h];
+                if (Sink::kStore)
+                    sad_acc(sa, x[h], bm1);
             }
+            u.put2(8 * c + ii, x[0], x[1]);
         }
     }
     sabs = sa;
@@ -383,9 +446,109 @@ struct Eval16 {
     PartSel sel;
 };
 
+// After pass 1 (every predictor form): the lower-bound pruning and the
+// partition search; false: pruned (ev says so)
+__device__ __forceinline__ bool eval_select(uint32_t lane_sum, const RunCtx &c, int order, int warm,
+                                            uint32_t thr, Eval16 &ev)
+{
+#if ATG_K2F_TRUNC == 3
+    ev.bits = lane_sum;
+    ev.sel.porder = 0;
+    ev.sel.method = 0;
+    ev.sel.k_lane = 0;
+    ev.sel.k_own = 0;
+    ev.sel.hdr_bits = 0;
+    return false;
+#endif
+    if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
+        // cannot beat a finished LPC job: no partition search, no exact bits
+        K2_COUNT(c.lane, K2C_PRUNED);
+        ev.bits = K2F_PRUNED;
+        ev.sel.porder = 0;
+        ev.sel.method = 0;
+        ev.sel.k_lane = 0;
+        ev.sel.k_own = 0;
+        ev.sel.hdr_bits = 0;
+        return false;
+    }
+#if ATG_K2F_EXP == 3
+    ev.sel.porder = 6; ev.sel.method = 0; ev.sel.k_own = ev.sel.k_lane = (lane_sum >> 6) & 7u;
+    ev.sel.hdr_bits = 262;
+    if (0)
+#endif
+    if (wave_all(lane_sum < (1u << 25))) {
+        K2_COUNT(c.lane, K2C_FAST32);
+        ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
+    } else {
+        K2_COUNT(c.lane, K2C_PARTS);
+        ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
+    }
+    return true;
+}
+
+// the exact residual-section bits from sh2 = sum of v >> (k - 1) (sum v
+// for k = 0) over the lane's codes
+__device__ __forceinline__ uint32_t eval_bits(const Eval16 &ev, uint32_t lane_sum, uint32_t sh2,
+                                              int warm)
+{
+    const uint32_t k = ev.sel.k_lane;
+    const uint32_t cnt = (uint32_t)(ATG_RUN - warm);
+    // k = 0: sum u = 2 sum v + #neg = sum v + sum |r| (sh2 = sum v)
+    const uint32_t lb = cnt * (1u + k) + (k ? sh2 : sh2 + lane_sum);
+    return dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
+}
+
+// pass 2: the sum of v >> kv over the run, from PkStore's words when every
+// |r| of the wave fits 15 bits, else by recomputation (redo fills a ReSum)
+template <class Redo>
+__device__ __forceinline__ uint32_t pass2_sum(const PkStore &st, uint32_t lane_sum, uint32_t kv,
+                                              uint32_t bias, Redo &&redo)
+{
+#if ATG_K2F_EXP == 2
+    return st.up[kv & 31];
+#endif
+    // loud lanes: |r| < 2^23, kv >= 8, and B (2^(31 - shv)) a multiple of 2^8
+    const bool loud = st.sel == kSelLoud;
+    const bool ok = loud ? lane_sum < (1u << 23) && kv >= 8u && (bias & 0xFFu) == 0u
+                         : lane_sum < 32768u;
+    if (wave_all(ok)) {
+        const uint32_t s0 = loud ? 8u : 0u;
+        return packed_vsum(st.up, kv - s0, (bias >> s0) & 0xFFFFu);
+    }
+    ReSum rs{kv, bias, 0u};
+    redo(rs);
+    return rs.s;
+}
+
+// the lanes whose next job of the candidate should keep bits 8..23 (a
+// hint; any choice is exact or falls back to ReSum)
+__device__ __forceinline__ void set_loud_hint(uint64_t *hint, int lane, uint32_t kv)
+{
+    const uint64_t m = __ballot(kv >= 9u);
+    if (lane == 0)
+        __atomic_store_n(hint, m, __ATOMIC_RELAXED);
+}
+
+// the same after a pass 1 that kept every x in 32 bits (the hi/lo kernel)
 __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
                                             const RunCtx &c, int order, int warm, uint32_t thr,
-                                            uint32_t bias);
+                                            uint32_t bias)
+{
+    Eval16 ev;
+    if (!eval_select(lane_sum, c, order, warm, thr, ev))
+        return ev;
+    const uint32_t kv = ev.sel.k_lane ? ev.sel.k_lane - 1u : 0u;
+    uint32_t sh2 = 0;
+    // v >> kv = (n >> kv) ^ (n >> 31) for n = x - B (arithmetic shifts)
+#pragma unroll
+    for (int t = 0; t < ATG_RUN; t += 2) {
+        const int n0 = (int)(u[t] - bias), n1 = (int)(u[t + 1] - bias);
+        sh2 = sh2 + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
+    }
+    ev.bits = eval_bits(ev, lane_sum, sh2, warm);
+    return ev;
+}
+
 
 // One predictor with the folded 32-bit arithmetic (caller checked the
 // bounds): pass 1, partition search, exact bits.  run: the lane's run in a
@@ -424,22 +587,12 @@ __device__ __forceinline__ void make_taps(const uint32_t (&cw)[7], int sh, bool 
     }
 }
 
-// One predictor with the folded 32-bit arithmetic from its tap words
-// (make_taps): pass 1, partition search, exact bits
-template <bool TWO>
-__device__ __forceinline__ Eval16 eval_fold_q(const uint32_t *__restrict__ run, const RunCtx &c,
-                                              const int (&cq)[14], int order, int sh, uint32_t w,
-                                              uint32_t thr, bool lr, bool dbl)
+// pass 1 of one predictor on the folded 32-bit arithmetic, any form
+template <bool TWO, class Sink>
+__device__ __forceinline__ void pass1_fold_any(const uint32_t *__restrict__ run, const int (&cq)[14],
+                                               int c0acc, int shv, bool lane0, int order, bool lr,
+                                               bool dbl, Sink &u, uint32_t &lane_sum)
 {
-    const int c0acc = (int)(0x80000000u - (1u << (sh + (int)w)));
-    int shv = sh + (int)w;
-    asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
-    // lane 0's first `order` samples are warm-up: (lane0 && i < order) is a
-    // lane mask and a scalar compare, so one v_cndmask per masked sample
-    const bool lane0 = c.lane == 0;
-    const int warm = lane0 ? order : 0;
-    uint32_t u[ATG_RUN];
-    uint32_t lane_sum; // sum |r| of the run
     if (lr) {
         if (dbl) {
             switch (order / 2 + 1) {
@@ -453,13 +606,13 @@ __device__ __forceinline__ Eval16 eval_fold_q(const uint32_t *__restrict__ run, 
             }
         } else
         switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
-        case 1: pass1_lr<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 2: pass1_lr<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 3: pass1_lr<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 4: pass1_lr<4>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 5: pass1_lr<5>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        case 6: pass1_lr<6>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
-        default: pass1_lr<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 1: pass1_lr<1, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 2: pass1_lr<2, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 3: pass1_lr<3, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 4: pass1_lr<4, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 5: pass1_lr<5, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        case 6: pass1_lr<6, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
+        default: pass1_lr<7, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         }
     } else {
         switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
@@ -472,13 +625,43 @@ __device__ __forceinline__ Eval16 eval_fold_q(const uint32_t *__restrict__ run, 
         default: pass1<7>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         }
     }
-    return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u >> shv);
+}
+
+// One predictor with the folded 32-bit arithmetic from its tap words
+// (make_taps): pass 1, partition search, exact bits
+template <bool TWO>
+__device__ __forceinline__ Eval16 eval_fold_q(const uint32_t *__restrict__ run, const RunCtx &c,
+                                              const int (&cq)[14], int order, int sh, uint32_t w,
+                                              uint32_t thr, bool lr, bool dbl, uint64_t *hint)
+{
+    const int c0acc = (int)(0x80000000u - (1u << (sh + (int)w)));
+    int shv = sh + (int)w;
+    asm volatile("v_mov_b32 %0, %0" : "+v"(shv)); // keep the shift in a VGPR
+    // lane 0's first `order` samples are warm-up: (lane0 && i < order) is a
+    // lane mask and a scalar compare, so one v_cndmask per masked sample
+    const bool lane0 = c.lane == 0;
+    const int warm = lane0 ? order : 0;
+    PkStore st;
+    st.sel = ((__atomic_load_n(hint, __ATOMIC_RELAXED) >> c.lane) & 1u) ? kSelLoud : kSelQuiet;
+    uint32_t lane_sum; // sum |r| of the run
+    pass1_fold_any<TWO>(run, cq, c0acc, shv, lane0, order, lr, dbl, st, lane_sum);
+    Eval16 ev;
+    if (!eval_select(lane_sum, c, order, warm, thr, ev))
+        return ev;
+    const uint32_t kv = ev.sel.k_lane ? ev.sel.k_lane - 1u : 0u;
+    set_loud_hint(hint, c.lane, kv);
+    const uint32_t sh2 = pass2_sum(st, lane_sum, kv, 0x80000000u >> shv, [&](ReSum &rs) {
+        uint32_t unused;
+        pass1_fold_any<TWO>(run, cq, c0acc, shv, lane0, order, lr, dbl, rs, unused);
+    });
+    ev.bits = eval_bits(ev, lane_sum, sh2, warm);
+    return ev;
 }
 
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, const RunCtx &c,
                                             const uint32_t (&cw)[7], int order, int sh,
-                                            uint32_t w, uint32_t thr, bool s16)
+                                            uint32_t w, uint32_t thr, bool s16, uint64_t *hint)
 {
     // s16 (side channel, every |S| <= 32767): the packed path on L - R
     // words formed on the fly -- 2 taps per v_dot2 instead of 1
@@ -486,7 +669,7 @@ __device__ __forceinline__ Eval16 eval_fold(const uint32_t *__restrict__ run, co
     const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
     int cq[14];
     make_taps(cw, sh, lr, dbl, cq);
-    return eval_fold_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl);
+    return eval_fold_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl, hint);
 }
 
 // ---- split fold: the 32-bit fold for predictors whose worst-case sum
@@ -517,10 +700,10 @@ __device__ __forceinline__ int split_n(int a, int b, int sa_v, int sb_v)
     return BIG ? (a + (b >> 8)) >> sa_v : (a << sa_v) + (b >> sb_v);
 }
 
-template <int D, bool BIG>
+template <int D, bool BIG, class Sink>
 __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, const int (&cp)[14],
                                             int seed_h, int seed_l, int sa_v, int sb_v,
-                                            bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                            bool lane0, int order, Sink &u,
                                             uint32_t &sabs, bool subr)
 {
     int tap0 = cp[0];
@@ -546,7 +729,7 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
     }
     uint4 n0 = load_run4(run, subr), n1 = load_run4(run + 4, subr);
     uint32_t sa = 0;
-#pragma unroll
+#pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
         asm volatile("" ::: "memory");
         const uint4 a0 = n0, a1 = n1;
@@ -571,26 +754,28 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
                     ah[h] = dot2(win_pair(A, ii + h, j), cp[j], ah[h]);
                     al[h] = dot2(win_pair(B, ii + h, j), cp[j], al[h]);
                 }
+            uint32_t x[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 16 * c + ii + h;
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
-                const uint32_t x = (uint32_t)n ^ 0x80000000u;
-                u[i] = x;
-                sad_acc(sa, x, bm1);
+                x[h] = (uint32_t)n ^ 0x80000000u;
+                if (Sink::kStore)
+                    sad_acc(sa, x[h], bm1);
             }
+            u.put2(16 * c + ii, x[0], x[1]);
         }
     }
     sabs = sa;
 }
 
 // the side channel on (L, R) words, split: TAPS = min(2D, 13) as pass1_lr
-template <int D, bool BIG, bool DBL = false>
+template <int D, bool BIG, bool DBL, class Sink>
 __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run, const int (&cl)[14],
                                                int seed_h, int seed_l, int sa_v, int sb_v,
-                                               bool lane0, int order, uint32_t (&u)[ATG_RUN],
+                                               bool lane0, int order, Sink &u,
                                                uint32_t &sabs)
 {
     constexpr int TAPS = 2 * D < 13 ? 2 * D : 13;
@@ -612,7 +797,7 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
     }
     uint4 nl = *(const uint4 *)run, nr = *(const uint4 *)runR;
     uint32_t sa = 0;
-#pragma unroll
+#pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 8; ++c) {
         asm volatile("" ::: "memory");
 #pragma unroll
@@ -652,26 +837,28 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
                     ah[h] = dot2(WH[12 + ii + h - k], cl[k], ah[h]);
                     al[h] = dot2(WL[12 + ii + h - k], cl[k], al[h]);
                 }
+            uint32_t x[2];
 #pragma unroll
             for (int h = 0; h < 2; ++h) {
                 const int i = 8 * c + ii + h;
                 int n = split_n<BIG>(ah[h], al[h], sa_v, sb_v);
                 if (i < ATG_FAST_ORDER)
                     n = (lane0 && i < order) ? -1 : n;
-                const uint32_t x = (uint32_t)n ^ 0x80000000u;
-                u[i] = x;
-                sad_acc(sa, x, bm1);
+                x[h] = (uint32_t)n ^ 0x80000000u;
+                if (Sink::kStore)
+                    sad_acc(sa, x[h], bm1);
             }
+            u.put2(8 * c + ii, x[0], x[1]);
         }
     }
     sabs = sa;
 }
 
-template <bool BIG>
+template <bool BIG, class Sink>
 __device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run, bool lr,
                                                 const int (&cq)[14], int seed_h, int seed_l,
                                                 int sa_v, int sb_v, bool lane0, int order,
-                                                uint32_t (&u)[ATG_RUN], uint32_t &sabs, bool subr,
+                                                Sink &u, uint32_t &sabs, bool subr,
                                                 bool dbl)
 {
     if (lr && dbl) {
@@ -686,13 +873,13 @@ __device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run
         }
     } else if (lr) {
         switch (order / 2 + 1) {
-        case 1: pass1_lr_split<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        case 2: pass1_lr_split<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        case 3: pass1_lr_split<3, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        case 4: pass1_lr_split<4, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        case 5: pass1_lr_split<5, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        case 6: pass1_lr_split<6, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-        default: pass1_lr_split<7, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 1: pass1_lr_split<1, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 2: pass1_lr_split<2, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 3: pass1_lr_split<3, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 4: pass1_lr_split<4, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 5: pass1_lr_split<5, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        case 6: pass1_lr_split<6, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+        default: pass1_lr_split<7, BIG, false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
         }
     } else {
         switch (order / 2 + 1) {
@@ -712,7 +899,7 @@ __device__ __forceinline__ void pass1_split_any(const uint32_t *__restrict__ run
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_split_q(const uint32_t *__restrict__ run, const RunCtx &c,
                                                const int (&cq)[14], int order, int sh, uint32_t w,
-                                               uint32_t thr, bool lr, bool dbl)
+                                               uint32_t thr, bool lr, bool dbl, uint64_t *hint)
 {
     const int shv = sh + (int)w;
     const bool big = shv >= 8;
@@ -723,86 +910,43 @@ __device__ __forceinline__ Eval16 eval_split_q(const uint32_t *__restrict__ run,
     asm volatile("v_mov_b32 %0, %0" : "+v"(sb_v));
     const bool lane0 = c.lane == 0;
     const int warm = lane0 ? order : 0;
-    uint32_t u[ATG_RUN];
+    PkStore st;
+    st.sel = ((__atomic_load_n(hint, __ATOMIC_RELAXED) >> c.lane) & 1u) ? kSelLoud : kSelQuiet;
     uint32_t lane_sum;
     if (big)
-        pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+        pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, st, lane_sum,
                               TWO, dbl);
     else
-        pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+        pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, st, lane_sum,
                                TWO, dbl);
-    return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u);
+    Eval16 ev;
+    if (!eval_select(lane_sum, c, order, warm, thr, ev))
+        return ev;
+    const uint32_t kv = ev.sel.k_lane ? ev.sel.k_lane - 1u : 0u;
+    set_loud_hint(hint, c.lane, kv);
+    const uint32_t sh2 = pass2_sum(st, lane_sum, kv, 0x80000000u, [&](ReSum &rs) {
+        uint32_t unused;
+        if (big)
+            pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, rs, unused,
+                                  TWO, dbl);
+        else
+            pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, rs,
+                                   unused, TWO, dbl);
+    });
+    ev.bits = eval_bits(ev, lane_sum, sh2, warm);
+    return ev;
 }
 
 template <bool TWO>
 __device__ __forceinline__ Eval16 eval_split(const uint32_t *__restrict__ run, const RunCtx &c,
                                              const uint32_t (&cw)[7], int order, int sh, uint32_t w,
-                                             uint32_t thr, bool s16)
+                                             uint32_t thr, bool s16, uint64_t *hint)
 {
     const bool lr = TWO && !s16;
     const bool dbl = lr && sh == 15; // tap 0 (-2^14, 2^14) twice
     int cq[14];
     make_taps(cw, sh, lr, dbl, cq);
-    return eval_split_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl);
-}
-
-// After pass 1 (every predictor form): the lower-bound pruning, the
-// partition search and the exact bit count from the kept v = |r| - [r < 0]
-__device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&u)[ATG_RUN],
-                                            const RunCtx &c, int order, int warm, uint32_t thr,
-                                            uint32_t bias)
-{
-    Eval16 ev;
-#if ATG_K2F_TRUNC == 3
-    ev.bits = lane_sum;
-    ev.sel.porder = 0;
-    ev.sel.method = 0;
-    ev.sel.k_lane = 0;
-    ev.sel.k_own = 0;
-    ev.sel.hdr_bits = 0;
-    return ev;
-#endif
-    if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
-        // cannot beat a finished LPC job: no partition search, no exact bits
-        K2_COUNT(c.lane, K2C_PRUNED);
-        ev.bits = K2F_PRUNED;
-        ev.sel.porder = 0;
-        ev.sel.method = 0;
-        ev.sel.k_lane = 0;
-        ev.sel.k_own = 0;
-        ev.sel.hdr_bits = 0;
-        return ev;
-    }
-#if ATG_K2F_EXP == 3
-    ev.sel.porder = 6; ev.sel.method = 0; ev.sel.k_own = ev.sel.k_lane = (lane_sum >> 6) & 7u;
-    ev.sel.hdr_bits = 262;
-    if (0)
-#endif
-    if (wave_all(lane_sum < (1u << 25))) {
-        K2_COUNT(c.lane, K2C_FAST32);
-        ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
-    } else {
-        K2_COUNT(c.lane, K2C_PARTS);
-        ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
-    }
-    const uint32_t k = ev.sel.k_lane;
-    const uint32_t cnt = (uint32_t)(ATG_RUN - warm);
-    const uint32_t kv = k ? k - 1u : 0u;
-    uint32_t sh2 = 0;
-#if ATG_K2F_EXP == 2
-    sh2 = u[kv & 63];
-#else
-    // v >> kv = (n >> kv) ^ (n >> 31) for n = x - B (arithmetic shifts)
-#pragma unroll
-    for (int t = 0; t < ATG_RUN; t += 2) {
-        const int n0 = (int)(u[t] - bias), n1 = (int)(u[t + 1] - bias);
-        sh2 = sh2 + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
-    }
-#endif
-    // k = 0: sum u = 2 sum v + #neg = sum v + sum |r| (sh2 = sum v)
-    const uint32_t lb = cnt * (1u + k) + (k ? sh2 : sh2 + lane_sum);
-    ev.bits = dpp_wave_sum<uint32_t>(lb) + ev.sel.hdr_bits;
-    return ev;
+    return eval_split_q<TWO>(run, c, cq, order, sh, w, thr, lr, dbl, hint);
 }
 
 // Any predictor (order <= 12): 64-bit accumulation on the shifted samples,
@@ -954,6 +1098,7 @@ struct CandInfo {
 // (partition header included), partition order, coding method and every
 // lane's Rice parameter
 struct PredRes {
+    uint64_t loud;     // lanes that coded with k >= 9 in a finished job (PkStore hint)
     uint32_t best_lpc; // smallest LPC subframe total of the finished jobs
     uint32_t bits[K2F_MAXPRED];
     uint8_t porder[K2F_MAXPRED];
@@ -1187,10 +1332,10 @@ __device__ __forceinline__ void pred_job(const FlacParams &p, uint32_t N,
     Eval16 ev;
     if (j.fold)
         ev = eval_fold<TWO>(run_of(img, lane), c, j.cw, (int)j.o, j.shift, ci.w, thr,
-                            TWO && ci.amax <= 32767u);
+                            TWO && ci.amax <= 32767u, &res->loud);
     else if (j.split)
         ev = eval_split<TWO>(run_of(img, lane), c, j.cw, (int)j.o, j.shift, ci.w, thr,
-                             TWO && ci.amax <= 32767u);
+                             TWO && ci.amax <= 32767u, &res->loud);
     else
         ev = eval_wide<TWO>(img, c, j.cw, (int)j.o, j.shift, ci.w);
     job_store(res, pi, lane, j.is_fixed, j.hdr, ev);
@@ -1279,9 +1424,9 @@ __device__ __forceinline__ void pred_job_d(const FlacParams &p, uint32_t N,
                 cq[m] = 0;
         }
         if (path == 0u)
-            ev = eval_fold_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl);
+            ev = eval_fold_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl, &res->loud);
         else
-            ev = eval_split_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl);
+            ev = eval_split_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl, &res->loud);
     } else {
         const JobSetup j = job_setup<TWO>(p, load_info(info), pi, lq, ls);
         ev = eval_wide<TWO>(img, c, j.cw, o, shift, w);
@@ -1589,8 +1734,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
         else
             cand_prepare<false>(p, unit, sbps, img + cand * PK_WORDS, cs, lane, est_tab,
                                 out + unit, &info[cand]);
-        if (lane == 0)
+        if (lane == 0) {
             res[cand].best_lpc = 0xFFFFFFFFu;
+            res[cand].loud = 0u;
+        }
     }
     __syncthreads();
 #if ATG_K2F_COUNT
@@ -1754,8 +1901,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK2fWavesPer
     }
     __syncthreads();
     cand_prepare<false>(p, unit, sbps, pk, cs, lane, est_tab, out + unit, &info);
-    if (lane == 0)
+    if (lane == 0) {
         res.best_lpc = 0xFFFFFFFFu;
+        res.loud = 0u;
+    }
     __syncthreads();
     const CandInfo ci = load_info(&info);
     if (!ci.active)
@@ -2134,8 +2283,10 @@ __global__ __launch_bounds__(128) void k_subframe_search_hl(
     }
     if (wave == 0) {
         cand_prepare<false, true>(p, unit, sbps, pk, cs, lane, est_tab, out + unit, &info);
-        if (lane == 0)
+        if (lane == 0) {
             res.best_lpc = 0xFFFFFFFFu;
+            res.loud = 0u;
+        }
     }
     __syncthreads();
     const CandInfo ci = load_info(&info);
