@@ -159,6 +159,17 @@ __device__ __forceinline__ void sad_acc(uint32_t &sa, uint32_t x, uint32_t b)
     asm("v_sad_u32 %0, %1, %2, %0" : "+v"(sa) : "v"(x), "v"(b));
 }
 
+// the lane index from an opaque instruction pair: a value the compiler can
+// neither hoist nor share with the kernel's own, so the rare paths (split
+// fold) derive their run addresses where they run instead of keeping them
+// live -- or spilled to scratch, one write per thread -- across the job loop
+__device__ __forceinline__ int opaque_lane()
+{
+    int l;
+    asm volatile("v_mbcnt_lo_u32_b32 %0, -1, 0\n\tv_mbcnt_hi_u32_b32 %0, -1, %0" : "=v"(l));
+    return l;
+}
+
 // Where pass 1 puts its per-sample x (every pass-1 form below takes one).
 // PkStore keeps x's low 16 bits, two samples per register (v_perm): the
 // low 16 bits of n = x - B (B's low half is 0 for shv <= 15), which are n
@@ -192,6 +203,19 @@ struct ReSum {
         s = s + (uint32_t)((n0 >> kv) ^ (n0 >> 31)) + (uint32_t)((n1 >> kv) ^ (n1 >> 31));
     }
 };
+
+// the chunk index a pass-1 loop addresses its next words with: in a rolled
+// (ReSum) loop an opaque copy, so no address of the loop is strength-reduced
+// into a value live -- or spilled, one scratch write per thread -- across
+// the whole job loop
+template <class Sink>
+__device__ __forceinline__ int chunk_index(int c)
+{
+    int cc = c;
+    if constexpr (!Sink::kStore)
+        asm volatile("" : "+s"(cc));
+    return cc;
+}
 
 typedef unsigned short ushort2_t __attribute__((ext_vector_type(2)));
 
@@ -301,10 +325,11 @@ __device__ __forceinline__ void pass1(const uint32_t *__restrict__ run, const in
     for (int c = 0; c < ATG_RUN / 16; ++c) {
         // keep each chunk's loads inside the chunk (bounds live registers)
         asm volatile("" ::: "memory");
+        const int cc = chunk_index<Sink>(c);
         const uint4 a0 = n0, a1 = n1;
         if (c + 1 < ATG_RUN / 16) {
-            n0 = load_run4(run + 8 * (c + 1), subr);
-            n1 = load_run4(run + 8 * (c + 1) + 4, subr);
+            n0 = load_run4(run + 8 * (cc + 1), subr);
+            n1 = load_run4(run + 8 * (cc + 1) + 4, subr);
         }
         win_next(a0, a1, A);
         // two samples' tap chains interleaved: no dependent-issue bubble
@@ -379,13 +404,14 @@ __device__ __forceinline__ void pass1_lr(const uint32_t *__restrict__ run, const
 #pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 8; ++c) {
         asm volatile("" ::: "memory");
+        const int cc = chunk_index<Sink>(c);
 #pragma unroll
         for (int k = 0; k < 12; ++k)
             W[k] = W[8 + k];
         lr_words(nl, nr, W + 12);
         if (c + 1 < ATG_RUN / 8) {
-            nl = *(const uint4 *)(run + 4 * (c + 1));
-            nr = *(const uint4 *)(runR + 4 * (c + 1));
+            nl = *(const uint4 *)(run + 4 * (cc + 1));
+            nr = *(const uint4 *)(runR + 4 * (cc + 1));
         }
 #pragma unroll
         for (int ii = 0; ii < 8; ii += 2) {
@@ -732,10 +758,11 @@ __device__ __forceinline__ void pass1_split(const uint32_t *__restrict__ run, co
 #pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 16; ++c) {
         asm volatile("" ::: "memory");
+        const int cc = chunk_index<Sink>(c);
         const uint4 a0 = n0, a1 = n1;
         if (c + 1 < ATG_RUN / 16) {
-            n0 = load_run4(run + 8 * (c + 1), subr);
-            n1 = load_run4(run + 8 * (c + 1) + 4, subr);
+            n0 = load_run4(run + 8 * (cc + 1), subr);
+            n1 = load_run4(run + 8 * (cc + 1) + 4, subr);
         }
         win_next(split4(a0, true), split4(a1, true), A);
         win_next(split4(a0, false), split4(a1, false), B);
@@ -800,6 +827,7 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
 #pragma unroll Sink::kUnroll
     for (int c = 0; c < ATG_RUN / 8; ++c) {
         asm volatile("" ::: "memory");
+        const int cc = chunk_index<Sink>(c);
 #pragma unroll
         for (int k = 0; k < 12; ++k) {
             WH[k] = WH[8 + k];
@@ -815,8 +843,8 @@ __device__ __forceinline__ void pass1_lr_split(const uint32_t *__restrict__ run,
             }
         }
         if (c + 1 < ATG_RUN / 8) {
-            nl = *(const uint4 *)(run + 4 * (c + 1));
-            nr = *(const uint4 *)(runR + 4 * (c + 1));
+            nl = *(const uint4 *)(run + 4 * (cc + 1));
+            nr = *(const uint4 *)(runR + 4 * (cc + 1));
         }
 #pragma unroll
         for (int ii = 0; ii < 8; ii += 2) {
@@ -927,8 +955,8 @@ __device__ __forceinline__ Eval16 eval_split_q(const uint32_t *__restrict__ run,
     const uint32_t sh2 = pass2_sum(st, lane_sum, kv, 0x80000000u, [&](ReSum &rs) {
         uint32_t unused;
         if (big)
-            pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, rs, unused,
-                                  TWO, dbl);
+            pass1_split_any<true>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, rs,
+                                  unused, TWO, dbl);
         else
             pass1_split_any<false>(run, lr, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, rs,
                                    unused, TWO, dbl);
@@ -1115,6 +1143,7 @@ __device__ __forceinline__ const uint32_t *run_of(const uint32_t *__restrict__ i
 {
     return img + PK_PRE + 36 * lane;
 }
+
 
 // Phase 1 of a candidate (one wave): CONSTANT (written here), wasted bits,
 // the FIXED order (flac.c:856-916, 1578-1620) and the LPC orders to try
@@ -1426,7 +1455,8 @@ __device__ __forceinline__ void pred_job_d(const FlacParams &p, uint32_t N,
         if (path == 0u)
             ev = eval_fold_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl, &res->loud);
         else
-            ev = eval_split_q<TWO>(run_of(img, lane), c, cq, o, shift, w, thr, lr, dbl, &res->loud);
+            ev = eval_split_q<TWO>(run_of(img, opaque_lane()), c, cq, o, shift, w, thr, lr, dbl,
+                                   &res->loud);
     } else {
         const JobSetup j = job_setup<TWO>(p, load_info(info), pi, lq, ls);
         ev = eval_wide<TWO>(img, c, j.cw, o, shift, w);
@@ -1648,7 +1678,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
     if (f >= p.n_frames)
         return;
     const int tid = threadIdx.x;
-    const int wave = tid >> 6, lane = tid & 63;
+    // the wave index in an SGPR: the candidate's table addresses are scalar
+    const int wave = __builtin_amdgcn_readfirstlane(tid >> 6), lane = tid & 63;
     const FrameInfo fi = frames[f];
     const uint32_t N = fi.n;
     if (N != ATG_MAX_BLOCK) {
