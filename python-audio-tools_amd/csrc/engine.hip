@@ -31,11 +31,6 @@
 #include "launch.h"
 #include "md5_cpu.h"
 
-// timing experiments only (tools/gpu_exp.sh); 0 in every product build
-#ifndef ATG_EXP
-#define ATG_EXP 0
-#endif
-
 namespace {
 
 thread_local std::string g_err;
@@ -1203,9 +1198,6 @@ atg_status finish_batch(atg_engine *e, EncSlot &sl)
         return fail(ATG_ERR_UNSUPPORTED, "frame longer than the GPU block limit");
     if (err_h & 4u)
         return fail(ATG_ERR_CAPACITY, "a frame exceeds its track's output slot");
-#if ATG_EXP != 0
-    err_h = 0; // timing experiments do not produce valid streams
-#endif
     if (err_h)
         return fail(ATG_ERR_DEVICE, "GPU consistency check failed (code " +
                                         std::to_string(err_h) + ")");

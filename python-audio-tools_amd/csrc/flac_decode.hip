@@ -49,10 +49,6 @@
 #include "launch.h"
 #include "wave.h"
 
-#ifndef ATG_DEC_EXP
-#define ATG_DEC_EXP 0 // timing experiments only (exp/ builds); 0 in the product
-#endif
-
 namespace {
 
 enum {
@@ -350,11 +346,6 @@ struct WinPred {
     __device__ __forceinline__ void step(int32_t rv, bool commit)
     {
         int32_t p;
-#if ATG_DEC_EXP == 7 // timing experiment: no prediction (residuals only)
-        if (true) {
-            p = 0;
-        } else
-#endif
         if (fast) {
             int32_t acc = 0;
 #pragma unroll
@@ -1125,11 +1116,9 @@ __global__ __launch_bounds__(64) void k_dec_parse(const uint32_t *__restrict__ w
         const uint64_t p = cand_pos[i];
         const DecTrack t = tr[cand_trk[i]];
         ParseRec rec;
-        // (the frame's CRC-16 is k_dec_crc's; 6: timing experiment, residual
-        // words straight from global memory)
-        parse_frame<ATG_DEC_EXP != 6, false>(w, nw, p, t, ~0ull, nullptr, rec,
-                                             ring + threadIdx.x * kRingStride,
-                                             spec ? spec[i] : 0u);
+        // (the frame's CRC-16 is k_dec_crc's)
+        parse_frame<true, false>(w, nw, p, t, ~0ull, nullptr, rec, ring + threadIdx.x * kRingStride,
+                                 spec ? spec[i] : 0u);
         recs[i] = rec;
     }
 }
@@ -1233,7 +1222,7 @@ __device__ uint32_t wave_crc16(const uint32_t *__restrict__ w, uint64_t nw, uint
 // K2b: CRC-16 of every parsed candidate frame whose length the parse walked
 // (a wave per frame, wave_crc16; frames the speculative pass measured are
 // checked already).  The serial per-lane CRC in k_dec_parse cost 0.8 of its
-// 4.7 ms (profiles/r04_h_dec_probe.jsonl, ATG_DEC_EXP 3).
+// 4.7 ms (profiles/r04_h_dec_probe.jsonl).
 __global__ __launch_bounds__(256) void k_dec_crc(const uint32_t *__restrict__ w, uint64_t nw,
                                                  const uint32_t *__restrict__ ncand,
                                                  const uint64_t *__restrict__ cand_pos,
@@ -1451,9 +1440,6 @@ __device__ __forceinline__ bool restore_win(BitR &r, uint32_t N, uint32_t bps, u
     // int32 is exact while every sample is inside the bps range (see WinPred)
     p.half = bps >= 1 && bps <= 24 ? 1u << (bps - 1) : 0u;
     p.fast = allow_fast && p.half && (uint64_t)sum_abs * p.half < 0x80000000ull;
-#if ATG_DEC_EXP == 2 // timing experiment: int64 sums only
-    p.fast = false;
-#endif
     if ((((uintptr_t)r.w) & 15u) == 0 && r.last >= kWalkInit * kRingB)
         rc = walk_residual<true>(r, order, N, p, ring);
     else
@@ -1678,7 +1664,7 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
         for (uint32_t k = wv; k < NF; k += 4) {
             const uint32_t n = fn[k];
             const uint32_t left = n > i0 ? min(n - i0, kEmitTile) : 0u;
-            if (lane >= left || ATG_DEC_EXP == 4) // 4: timing experiment, no writes
+            if (lane >= left)
                 continue;
             const uint32_t ch = fch[k], as = fas[k], l = fj[k], bb = fbb[k], x = lane;
             const int32_t hi = fhi[k], lo = -hi - 1;
@@ -1701,8 +1687,7 @@ __global__ __launch_bounds__(256) void k_dec_emit(const DecTrack *__restrict__ t
                 // (src/pcm.c:1826-1948): only a corrupt stream can produce them
                 const int32_t v0 = o0 > hi ? hi : (o0 < lo ? lo : o0);
                 const int32_t v1 = o1 > hi ? hi : (o1 < lo ? lo : o1);
-                if (ATG_DEC_EXP == 8) { // timing experiment: no MD5 byte image
-                } else if (bb == 2) {
+                if (bb == 2) {
                     *(uint32_t *)bdst = ((uint32_t)v0 & 0xFFFFu) | ((uint32_t)v1 << 16);
                 } else {
                     for (uint32_t q = 0; q < bb; ++q) {

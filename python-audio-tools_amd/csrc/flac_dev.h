@@ -13,19 +13,6 @@
 //   TrackInfo  per track: output placement, STREAMINFO inputs
 #pragma once
 
-// Experiment switches (ATG_EXP, ATG_K2F_EXP, ATG_K2F_TRUNC, ATG_K2F_COUNT,
-// ATG_DEC_EXP) remove, replace or instrument
-// work to time it and produce WRONG bytes.  Only tools/build_exp.sh may set
-// them, and it also defines ATG_EXPERIMENT_BUILD and writes exp/ libraries;
-// a product build that sees one fails here.
-#if !defined(ATG_EXPERIMENT_BUILD) &&                                   \
-    ((defined(ATG_EXP) && ATG_EXP != 0) ||                              \
-     (defined(ATG_K2F_EXP) && ATG_K2F_EXP != 0) ||                      \
-     (defined(ATG_K2F_TRUNC) && ATG_K2F_TRUNC != 0) ||                  \
-     (defined(ATG_K2F_COUNT) && ATG_K2F_COUNT != 0) ||                  \
-     (defined(ATG_DEC_EXP) && ATG_DEC_EXP != 0))
-#error "ATG_*EXP experiment switches are for tools/build_exp.sh builds only"
-#endif
 #include <stdint.h>
 
 #define ATG_MAX_LPC 32        // widest LPC order accepted

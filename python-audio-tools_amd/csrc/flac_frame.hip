@@ -20,10 +20,6 @@
 #include "residual.h"
 #include "wave.h"
 
-// timing experiments only (tools/gpu_exp.sh); 0 in every product build
-#ifndef ATG_EXP
-#define ATG_EXP 0
-#endif
 
 __constant__ uint16_t c_crc_adv[24][16]; // advance CRC-16 state by 2^m zero bytes
 __constant__ uint32_t c_crc16[4][256]; // slicing tables: byte + k zero bytes
@@ -584,9 +580,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
                                        : rs + pbits * (jp + (part_head ? 0u : 1u)) + excl);
                     if (part_head)
                         wr.put(0, pbits, k);
-#if ATG_EXP != 8
                     emit_codes<REG>(wr, u, warm, len, k);
-#endif
                 } else {
                     // any order <= 32 / wide samples: 64-bit accumulator
                     const int i0 = max((int)ra, (int)order);
@@ -659,9 +653,6 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
                 q += 4;
             }
         }
-#if ATG_EXP == 7
-        q = qe;
-#endif
         for (; q < qe; q += 4) {
             const uint32_t t = fb_be32(fb, (uint32_t)q) ^ (crc << 16);
             crc = crc_tab[3][t >> 24] ^ crc_tab[2][(t >> 16) & 0xFFu] ^
@@ -689,10 +680,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
         dst[lane] = (uint8_t)fb_byte(fb, lane);
     const uint32_t body = (nb - h) / 4u;
     uint32_t *dw = (uint32_t *)(dst + h);
-#if ATG_EXP != 9
     for (uint32_t i = lane; i < body; i += 64)
         dw[i] = __builtin_bswap32(fb_be32(fb, h + 4u * i));
-#endif
     const uint32_t tail0 = h + 4u * body;
     if (tail0 + (uint32_t)lane < nb)
         dst[tail0 + lane] = (uint8_t)fb_byte(fb, tail0 + lane);

@@ -359,12 +359,7 @@ __device__ __forceinline__ void search_unit(const FlacParams &p, const T *__rest
 
     // ---- FIXED order by |residual| sums over samples [4,N) (flac.c:856-916)
     uint32_t fixed_order = 0;
-#if ATG_EXP == 1
-    fixed_order = 2;
-    if (0) {
-#else
     if (p.try_fixed) {
-#endif
         uint64_t s5[5] = {0, 0, 0, 0, 0};
         if (N == ATG_MAX_BLOCK && maxabs < (1u << 21)) {
             // the lane's 64 samples from LDS, differences carried in
@@ -465,14 +460,7 @@ __device__ __forceinline__ void search_unit(const FlacParams &p, const T *__rest
     uint32_t lpc_bits = 0xFFFFFFFFu, lpc_order = 0, lpc_prec = 0;
     int lpc_shift = 0;
     PartSel lpc_sel = {};
-#if ATG_EXP == 3
-    lo = hi = M;
-#endif
-#if ATG_EXP == 6
-    const uint32_t n_pred = 0;
-#else
     const uint32_t n_pred = (p.try_fixed ? 1u : 0u) + (p.try_lpc ? hi - lo + 1u : 0u);
-#endif
     for (uint32_t pi = 0; pi < n_pred; ++pi) {
         const bool is_fixed = p.try_fixed && pi == 0;
         const uint32_t o = is_fixed ? fixed_order : lo + pi - (p.try_fixed ? 1u : 0u);

@@ -46,43 +46,6 @@
 #include "rice.h"
 #include "wave.h"
 
-// timing experiments only (tools/gpu_exp.sh), 0 in every product build:
-// 1 FIXED predictor only, 2 no pass 2, 3 trivial partition choice, 4 no FIXED sums,
-// 5 no lower-bound pruning, 6 one tap pair per residual (prediction cost),
-// 7 no 64-bit fallback (every predictor on the folded 32-bit path)
-#ifndef ATG_K2F_EXP
-#define ATG_K2F_EXP 0
-#endif
-// instruction-ledger builds only (tools/gpu_k2ledger.sh, DESIGN 4a''), 0 in
-// every product build.  ATG_K2F_TRUNC n ends k_frame_search_ms after
-// 1 staging, 2 phase 1, 3 phase 2 with pass 1 only (no pruning, partition
-// search or pass 2), 4 phase 2; each writes VERBATIM descriptors so the
-// kernels after K2 still run on valid input.  ATG_K2F_COUNT counts the
-// kernel's dynamic events (jobs per order and path, pruned jobs, partition
-// searches) into k2_counts, read by atg_k2_counters.
-#ifndef ATG_K2F_TRUNC
-#define ATG_K2F_TRUNC 0
-#endif
-#ifndef ATG_K2F_COUNT
-#define ATG_K2F_COUNT 0
-#endif
-#if ATG_K2F_COUNT
-enum { K2C_FRAMES, K2C_ACTIVE, K2C_FIXED, K2C_LPC, K2C_ORDER0, K2C_FOLD = K2C_ORDER0 + 13,
-       K2C_SPLIT, K2C_WIDE, K2C_PRUNED, K2C_FAST32, K2C_PARTS, K2C_LR, K2C_SUBR, K2C_SLOW,
-       K2C_N };
-__device__ unsigned long long k2_counts[K2C_N];
-__device__ __forceinline__ void k2_count(int lane, int k)
-{
-    if (lane == 0)
-        atomicAdd(&k2_counts[k], 1ull);
-}
-#define K2_COUNT(lane, k) k2_count(lane, k)
-#else
-#define K2_COUNT(lane, k) ((void)0)
-#endif
-// 1: three residual-loop variants instead of seven (smaller code image)
-// 1: predictors that fail the 32-bit fold's bound take the split fold
-// (eval_split) instead of the 64-bit loop
 // waves per SIMD the register allocation targets
 constexpr int kK2fWavesPerEu = 4;
 
@@ -477,18 +440,8 @@ struct Eval16 {
 __device__ __forceinline__ bool eval_select(uint32_t lane_sum, const RunCtx &c, int order, int warm,
                                             uint32_t thr, Eval16 &ev)
 {
-#if ATG_K2F_TRUNC == 3
-    ev.bits = lane_sum;
-    ev.sel.porder = 0;
-    ev.sel.method = 0;
-    ev.sel.k_lane = 0;
-    ev.sel.k_own = 0;
-    ev.sel.hdr_bits = 0;
-    return false;
-#endif
     if (thr != 0xFFFFFFFFu && residual_lb(lane_sum, (uint32_t)(ATG_RUN - warm)) > thr) {
         // cannot beat a finished LPC job: no partition search, no exact bits
-        K2_COUNT(c.lane, K2C_PRUNED);
         ev.bits = K2F_PRUNED;
         ev.sel.porder = 0;
         ev.sel.method = 0;
@@ -497,18 +450,10 @@ __device__ __forceinline__ bool eval_select(uint32_t lane_sum, const RunCtx &c, 
         ev.sel.hdr_bits = 0;
         return false;
     }
-#if ATG_K2F_EXP == 3
-    ev.sel.porder = 6; ev.sel.method = 0; ev.sel.k_own = ev.sel.k_lane = (lane_sum >> 6) & 7u;
-    ev.sel.hdr_bits = 262;
-    if (0)
-#endif
-    if (wave_all(lane_sum < (1u << 25))) {
-        K2_COUNT(c.lane, K2C_FAST32);
+    if (wave_all(lane_sum < (1u << 25)))
         ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
-    } else {
-        K2_COUNT(c.lane, K2C_PARTS);
+    else
         ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
-    }
     return true;
 }
 
@@ -530,9 +475,6 @@ template <class Redo>
 __device__ __forceinline__ uint32_t pass2_sum(const PkStore &st, uint32_t lane_sum, uint32_t kv,
                                               uint32_t bias, Redo &&redo)
 {
-#if ATG_K2F_EXP == 2
-    return st.up[kv & 31];
-#endif
     // loud lanes: |r| < 2^23, kv >= 8, and B (2^(31 - shv)) a multiple of 2^8
     const bool loud = st.sel == kSelLoud;
     const bool ok = loud ? lane_sum < (1u << 23) && kv >= 8u && (bias & 0xFFu) == 0u
@@ -631,7 +573,7 @@ __device__ __forceinline__ void pass1_fold_any(const uint32_t *__restrict__ run,
             default: pass1_lr<7, true>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
             }
         } else
-        switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
+        switch (order / 2 + 1) {
         case 1: pass1_lr<1, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         case 2: pass1_lr<2, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         case 3: pass1_lr<3, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
@@ -641,7 +583,7 @@ __device__ __forceinline__ void pass1_fold_any(const uint32_t *__restrict__ run,
         default: pass1_lr<7, false>(run, cq, c0acc, shv, lane0, order, u, lane_sum); break;
         }
     } else {
-        switch (ATG_K2F_EXP == 6 ? 1 : order / 2 + 1) {
+        switch (order / 2 + 1) {
         case 1: pass1<1>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         case 2: pass1<2>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
         case 3: pass1<3>(run, cq, c0acc, shv, lane0, order, u, lane_sum, TWO); break;
@@ -1184,13 +1126,9 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
         return;
     }
     const uint32_t w = cs.orv ? (uint32_t)__builtin_ctz(cs.orv) : 0u;
-#if ATG_K2F_EXP == 4
-    const uint32_t fixed_order = 2u;
-#else
     const uint32_t fixed_order = !p.try_fixed ? 0u
                                : HL ? fixed_order_hl(run_of(img, lane), lane)
                                     : fixed_order_of<TWO>(run_of(img, lane), lane);
-#endif
     uint32_t lo = 1, hi = 0;
     if (p.try_lpc) {
         if (p.exhaustive) {
@@ -1200,10 +1138,6 @@ __device__ __forceinline__ void cand_prepare(const FlacParams &p, uint32_t unit,
             lo = hi = est_tab[unit];
         }
     }
-#if ATG_K2F_EXP == 1
-    lo = 1;
-    hi = 0;
-#endif
     if (lane == 0) {
         ci->active = 1;
         ci->w = w;
@@ -1304,7 +1238,7 @@ __device__ __forceinline__ JobSetup job_setup(const FlacParams &p, const CandInf
     const bool split_ok = shift <= 15 && hsum + (1ull << shv) < (1ull << 30) &&
                           (shv >= 8 || (hsum << (8 - shv)) < (1ull << 30));
     const bool codes_ok = 2u * rbound + 1u < (1ull << 26);
-    j.fold = (fold_ok && codes_ok) || ATG_K2F_EXP == 7;
+    j.fold = fold_ok && codes_ok;
     j.split = !j.fold && split_ok && codes_ok;
     return j;
 }
@@ -1312,13 +1246,8 @@ __device__ __forceinline__ JobSetup job_setup(const FlacParams &p, const CandInf
 // the pruning threshold of a job from the candidate's best finished LPC total
 __device__ __forceinline__ uint32_t job_threshold(const PredRes *__restrict__ res, uint32_t hh)
 {
-    uint32_t thr = 0xFFFFFFFFu;
-    if (ATG_K2F_EXP != 5) {
-        const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
-        if (best != 0xFFFFFFFFu)
-            thr = best > hh ? best - hh : 0u;
-    }
-    return thr;
+    const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
+    return best == 0xFFFFFFFFu ? 0xFFFFFFFFu : best > hh ? best - hh : 0u;
 }
 
 __device__ __forceinline__ RunCtx job_ctx(const FlacParams &p, uint32_t N, int lane)
@@ -1431,13 +1360,6 @@ __device__ __forceinline__ void pred_job_d(const FlacParams &p, uint32_t N,
     const RunCtx c = job_ctx(p, N, lane);
     const uint32_t thr = job_threshold(res, uniform_u32(jd->hh));
     Eval16 ev;
-#if ATG_K2F_COUNT
-    K2_COUNT(lane, is_fixed ? K2C_FIXED : K2C_LPC);
-    K2_COUNT(lane, K2C_ORDER0 + (is_fixed ? 0 : o));
-    if (TWO)
-        K2_COUNT(lane, lr ? K2C_LR : K2C_SUBR);
-    K2_COUNT(lane, path == 0u ? K2C_FOLD : path == 1u ? K2C_SPLIT : K2C_WIDE);
-#endif
     if (path < 2u) {
         int cq[14];
 #pragma unroll
@@ -1629,33 +1551,6 @@ __device__ __forceinline__ void stage_ms(const T *__restrict__ src, int tid, uin
     }
 }
 
-#if ATG_K2F_TRUNC
-// ledger builds: a VERBATIM descriptor for wave `cand`'s candidate
-__device__ __forceinline__ void trunc_verbatim(const FlacParams &p, uint32_t N, uint32_t unit,
-                                               uint32_t cand, int lane, SubDesc *__restrict__ d)
-{
-    if (lane == 0) {
-        const uint32_t sbps = p.bps + (cand == 3u ? 1u : 0u);
-        d->bits = 8u + sbps * N;
-        d->type = SF_VERBATIM;
-        d->order = 0;
-        d->wasted = 0;
-        d->porder = 0;
-        d->method = 0;
-        d->precision = 0;
-        d->shift = 0;
-        d->sbps = (uint8_t)sbps;
-        d->amax = (1u << (sbps - 1u)) - 1u;
-    }
-}
-#define K2_TRUNC_AT(n)                                                                    \
-    if (ATG_K2F_TRUNC == (n)) {                                                           \
-        trunc_verbatim(p, N, f * 4u + (uint32_t)wave, (uint32_t)wave, lane, out + f * 4u + wave); \
-        return;                                                                           \
-    }
-#else
-#define K2_TRUNC_AT(n)
-#endif
 
 template <typename T>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPerEu))) void k_frame_search_ms(
@@ -1687,7 +1582,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
             const uint32_t slot = atomicAdd(slow_count, 1u);
             slow_list[slot] = f * 4u + (uint32_t)tid;
         }
-        K2_COUNT(tid, K2C_SLOW);
         return;
     }
     if (tid < 3 * PK_PRE)
@@ -1742,11 +1636,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
             const uint32_t slot = atomicAdd(slow_count, 1u);
             slow_list[slot] = f * 4u + (uint32_t)tid;
         }
-        K2_COUNT(tid, K2C_SLOW);
         return;
     }
-    K2_COUNT(tid, K2C_FRAMES);
-    K2_TRUNC_AT(1)
 
     // phase 1: wave c prepares candidate c
     const uint32_t cand = (uint32_t)wave;
@@ -1771,10 +1662,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
         }
     }
     __syncthreads();
-#if ATG_K2F_COUNT
-    if (load_info(&info[cand]).active)
-        K2_COUNT(lane, K2C_ACTIVE);
-#endif
     // phase 1b: wave c forms candidate c's job descriptors, a lane per job
     {
         const CandInfo ci = load_info(&info[cand]);
@@ -1786,7 +1673,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
             jobs_prepare<false>(p, ci, lane, lq, ls, jdesc[cand]);
     }
     __syncthreads();
-    K2_TRUNC_AT(2)
 
     // phase 2: the (candidate, predictor) jobs, dynamically shared by the 4
     // waves, the costliest first (highest orders, side channel first): the
@@ -1814,8 +1700,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kK2fWavesPe
                               &res[jc]);
     }
     __syncthreads();
-    K2_TRUNC_AT(3)
-    K2_TRUNC_AT(4)
 
     // phase 3: wave c writes candidate c
     cand_finish(p, N, load_info(&info[cand]), &res[cand], lane,
@@ -2199,7 +2083,7 @@ __device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
     // rules it out the same way; its header is 7 + wf + o (sbps - w)
     const uint32_t hdr_f = 7u + wf + o * (ci.sbps - ci.w);
     uint32_t thr = 0xFFFFFFFFu;
-    if (ATG_K2F_EXP != 5) {
+    {
         const uint32_t best = uniform_u32(__atomic_load_n(&res->best_lpc, __ATOMIC_RELAXED));
         const uint32_t hh = is_fixed ? hdr_f : hdr;
         if (best != 0xFFFFFFFFu)
@@ -2394,21 +2278,4 @@ hipError_t launch_subframe_search16(const FlacParams &p, const void *pcm, int fm
     return hipGetLastError();
 }
 
-#if ATG_K2F_COUNT
-// ledger builds: read (and with reset != 0 clear) the K2 event counters
-extern "C" __attribute__((visibility("default"))) int atg_k2_counters(uint64_t *out, int n,
-                                                                       int reset)
-{
-    unsigned long long h[K2C_N] = {};
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(k2_counts), sizeof(h)) != hipSuccess)
-        return -1;
-    for (int k = 0; k < n && k < K2C_N; ++k)
-        out[k] = h[k];
-    if (reset) {
-        const unsigned long long z[K2C_N] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(k2_counts), z, sizeof(z)) != hipSuccess)
-            return -1;
-    }
-    return K2C_N;
-}
-#endif
+

@@ -12,11 +12,6 @@
 #include "rice.h"
 #include "wave.h"
 
-// timing experiments only (tools/gpu_exp.sh); 0 in every product build
-#ifndef ATG_EXP
-#define ATG_EXP 0
-#endif
-// partition-order search: DPP butterflies (1) or lane shuffles (0)
 
 struct RunCtx {
     int lane;
@@ -148,10 +143,6 @@ __device__ __forceinline__ PartSel select_partitions_t(S lane_sum, uint32_t orde
 __device__ __forceinline__ PartSel select_partitions(uint64_t lane_sum, uint32_t order,
                                                      const RunCtx &c, bool small = false)
 {
-#if ATG_EXP == 2
-    { PartSel r; r.porder = 6; r.method = 0; r.k_own = r.k_lane = (uint32_t)(lane_sum >> 6) & 7u;
-      r.hdr_bits = 6u + 64u * 4u; return r; }
-#endif
     if (small)
         return select_partitions_t<uint32_t>((uint32_t)lane_sum, order, c);
     return select_partitions_t<uint64_t>(lane_sum, order, c);
