@@ -1,7 +1,9 @@
 /* k2_prune_sim.c — development tool: how often K2's LPC jobs survive the
  * residual lower-bound pruning (flac_search16.hip residual_lb) on config-2
  * shaped frames, i.e. how many predictors per candidate pay for pass 2
- * (the exact bit count) and the partition search.  Jobs are simulated in
+ * (the exact bit count) and the partition search; and how many a bound
+ * checked after 16, 32 or 48 of a lane's 64 samples would prune there
+ * (what ending pass 1 early could save).  Jobs are simulated in
  * the kernel's order: FIXED always evaluated, LPC orders 12 .. 1, a job
  * pruned when its lane-sum bound exceeds (best finished LPC total - hdr).
  *
@@ -50,6 +52,7 @@ int main(int argc, char **argv)
     static int32_t L[4096], R[4096], C[4][4096], res[4096];
     long jobs = 0, pass2 = 0, subfr = 0;
     long per_order_pass2[13] = {0};
+    long early[3] = {0, 0, 0}; double cost_all = 0, cost_saved[3] = {0, 0, 0};
     for (int f = 0; f < n_frames; ++f) {
         const double f1 = 100 + 1900 * urand(), f2 = 2000 + 10000 * urand();
         const double a1 = 0.05 + 0.55 * urand(), a2 = 0.3 * urand();
@@ -122,6 +125,28 @@ int main(int argc, char **argv)
                     lb += lb_lane(sum, lane ? 64 : 64 - order);
                 }
                 jobs++;
+                {
+                    const int D = order / 2 + 1;
+                    const double cpl = (double)(D + 3) * 64; /* pass-1 VALU per lane-run */
+                    cost_all += cpl;
+                    const int cuts[3] = {16, 32, 48};
+                    for (int q = 0; q < 3; ++q) {
+                        float lbp = 0;
+                        for (int lane = 0; lane < 64; ++lane) {
+                            uint32_t sum = 0;
+                            int a = lane * 64 - order, b = lane * 64 - order + cuts[q];
+                            int cnt = cuts[q];
+                            if (a < 0) { cnt += a; a = 0; }
+                            for (int i = a; i < b; ++i)
+                                sum += (uint32_t)abs(res[i]);
+                            lbp += lb_lane(sum, cnt);
+                        }
+                        if (thr != 0xFFFFFFFFu && (uint32_t)lbp > thr) {
+                            early[q]++;
+                            cost_saved[q] += cpl * (64 - cuts[q]) / 64.0;
+                        }
+                    }
+                }
                 if (thr != 0xFFFFFFFFu && (uint32_t)lb > thr)
                     continue;
                 pass2++;
@@ -135,6 +160,9 @@ int main(int argc, char **argv)
     }
     printf("subframes %ld  LPC jobs %ld  pass2 %ld (%.2f per subframe, %.1f %%)\n", subfr, jobs,
            pass2, (double)pass2 / subfr, 100.0 * pass2 / jobs);
+    for (int q = 0; q < 3; ++q)
+        printf("check after %d of 64: %.1f %% of jobs pruned there, pass-1 cost saved %.1f %%\n",
+               16 * (q + 1), 100.0 * early[q] / jobs, 100.0 * cost_saved[q] / cost_all);
     for (int o2 = 12; o2 >= 1; --o2)
         printf("order %2d: pass2 in %.1f %% of subframes\n", o2, 100.0 * per_order_pass2[o2] / subfr);
     return 0;
