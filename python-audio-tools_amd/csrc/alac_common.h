@@ -340,3 +340,177 @@ struct AResidualReader {
         return true;
     }
 };
+
+// The residual walk's reader (k_adec_parse, ~24 k codes per lane and
+// frameset): a 64-bit window W of the next bits, MSB first, topped up by a
+// 32-bit word whenever fewer than 32 bits are left, the words taken in
+// order from a 16-byte chunk in registers with the next chunk's load in
+// flight (as ABitRC).  A code is one leading-ones count, one field
+// extraction and a window shift, with no end-of-data test: the walk uses
+// it only while at least 128 bits remain before `end` (two codes per
+// residual step, 41 bits each at most), and hands the rest to the exact
+// reader.
+struct AFastBits {
+    const uint32_t *w;
+    uint64_t W;          // the next nb bits, MSB first
+    uint32_t nb;         // valid bits in W (>= 32 between codes)
+    uint64_t ci;         // chunk index of a0..a3
+    uint32_t k;          // words of the chunk already in W
+    uint64_t lim;        // last readable word (one past `end`, as ABitRC)
+    uint32_t a0, a1, a2, a3, b0, b1, b2, b3; // current and next chunk
+    uint32_t used, room; // bits consumed since init; bits usable before the careful path
+
+    __device__ __forceinline__ uint32_t ld(uint64_t i) const { return w[i < lim ? i : lim]; }
+    __device__ __forceinline__ void load_chunk(uint64_t ch)
+    {
+        const uint64_t i = ch * 4u;
+        if (i + 3u <= lim && (((uintptr_t)w & 15u) == 0u)) {
+            const uint4 v = *(const uint4 *)(w + i);
+            b0 = v.x;
+            b1 = v.y;
+            b2 = v.z;
+            b3 = v.w;
+        } else {
+            b0 = ld(i);
+            b1 = ld(i + 1);
+            b2 = ld(i + 2);
+            b3 = ld(i + 3);
+        }
+    }
+    // the next word in stream order, big-endian to host order
+    __device__ __forceinline__ uint32_t next_word()
+    {
+        if (k == 4u) {
+            a0 = b0;
+            a1 = b1;
+            a2 = b2;
+            a3 = b3;
+            ci += 1u;
+            load_chunk(ci + 1u);
+            k = 0u;
+        }
+        const uint32_t v = a0;
+        a0 = a1;
+        a1 = a2;
+        a2 = a3;
+        k += 1u;
+        return __builtin_bswap32(v);
+    }
+    __device__ __forceinline__ void top_up()
+    {
+        if (nb < 32u) {
+            W |= (uint64_t)next_word() << (32u - nb);
+            nb += 32u;
+        }
+    }
+    __device__ __forceinline__ void init(const uint32_t *words, uint64_t pos, uint64_t end)
+    {
+        w = words;
+        lim = (end >> 5) + 1u;
+        const uint64_t wi = pos >> 5;
+        ci = wi >> 2;
+        load_chunk(ci);
+        a0 = b0;
+        a1 = b1;
+        a2 = b2;
+        a3 = b3;
+        load_chunk(ci + 1u);
+        k = 0u;
+        // skip to the word holding pos, then to its bit
+        for (uint32_t s = (uint32_t)(wi & 3u); s > 0u; --s)
+            next_word();
+        W = (uint64_t)next_word() << 32;
+        nb = 32u;
+        top_up();
+        const uint32_t sh = (uint32_t)(pos & 31u);
+        W <<= sh;
+        nb -= sh;
+        top_up();
+        used = 0u;
+        const uint64_t avail = end > pos ? end - pos : 0u;
+        room = avail > 128u + 0x7FFFFFFFull ? 0x7FFFFFFFu
+                                            : (avail > 128u ? (uint32_t)(avail - 128u) : 0u);
+    }
+    __device__ __forceinline__ uint32_t top32() const { return (uint32_t)(W >> 32); }
+    __device__ __forceinline__ void skip(uint32_t n) // n <= 32
+    {
+        W <<= n;
+        nb -= n;
+        used += n;
+        top_up();
+    }
+    // the next n bits (1 <= n <= 32)
+    __device__ __forceinline__ uint32_t take(uint32_t n)
+    {
+        const uint32_t v = top32() >> (32u - n);
+        skip(n);
+        return v;
+    }
+    __device__ __forceinline__ bool careful() const { return used > room; }
+};
+
+// alac_read_residual on AFastBits, with at least 41 bits before `end`
+// (no end-of-data case can arise)
+__device__ __forceinline__ uint32_t alac_read_residual_fast(AFastBits &f, uint32_t k, uint32_t ss)
+{
+    const uint32_t x = f.top32();
+    const uint32_t ones = (uint32_t)__clz(~x);
+    if (ones >= 9u) { // escape: a raw ss-bit value
+        f.skip(9u);
+        return ss ? f.take(ss) : 0u;
+    }
+    if (k == 0u) {
+        f.skip(ones + 1u);
+        return ones;
+    }
+    const uint32_t m = (1u << k) - 1u;
+    uint32_t lsb;
+    if (ones + 1u + k <= 32u) {
+        lsb = (x << (ones + 1u)) >> (32u - k);
+        const bool big = lsb > 1u;
+        f.skip(ones + k + (big ? 1u : 0u));
+        return ones * m + (big ? lsb - 1u : 0u);
+    }
+    f.skip(ones + 1u);
+    lsb = f.top32() >> (32u - k);
+    const bool big = lsb > 1u;
+    f.skip(k - (big ? 0u : 1u));
+    return ones * m + (big ? lsb - 1u : 0u);
+}
+
+// AResidualReader::next on AFastBits (caller checked !f.careful())
+__device__ __forceinline__ bool alac_next_fast(AResidualReader &g, AFastBits &f, int32_t &out)
+{
+    if (g.run_left) {
+        --g.run_left;
+        out = 0;
+        return true;
+    }
+    if (g.i >= (int32_t)g.count)
+        return false;
+    const int32_t kk = alac_log2s((g.history >> 9) + 3);
+    const uint32_t k = (uint32_t)kk < g.mk ? (uint32_t)kk : g.mk;
+    const uint32_t u = alac_read_residual_fast(f, k, g.ss) + g.sign_mod;
+    g.sign_mod = 0;
+    out = (u & 1u) ? -(int32_t)((u + 1u) >> 1) : (int32_t)(u >> 1);
+    if (u > 0xFFFFu)
+        g.history = 0xFFFF;
+    else
+        g.history = (int32_t)((uint32_t)g.history + (u * g.hm - (((uint32_t)g.history * g.hm) >> 9)));
+    if (g.history < 128 && (g.i + 1) < (int32_t)g.count) {
+        const int32_t lz = alac_log2s(g.history);
+        const int32_t kz = 7 - lz + ((g.history + 16) / 64);
+        const uint32_t k2 = (uint32_t)kz < g.mk ? (uint32_t)kz : g.mk;
+        uint32_t z = alac_read_residual_fast(f, k2, 16);
+        if (z > 0) {
+            const uint32_t cap = g.count - (uint32_t)g.i;
+            z = z < cap ? z : cap;
+            g.run_left = z;
+            g.i += (int32_t)z;
+        }
+        g.history = 0;
+        g.sign_mod = z <= 0xFFFFu ? 1u : 0u;
+    }
+    ++g.i;
+    return true;
+}

@@ -214,13 +214,30 @@ __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AF
                 g.init(N, ss, T.ih, T.hm, T.mk);
                 uint32_t n = 0;
                 int32_t v;
+                // the walk on the windowed reader while 128 bits remain
+                // before the end, then on the exact one (field widths the
+                // window cannot take go to the exact reader at once)
+                bool fast = ss <= 32u && T.mk <= 32u;
+                AFastBits fb;
+                if (fast)
+                    fb.init(w, r.pos, r.end);
+                const uint64_t p0 = r.pos;
+                auto step = [&](int32_t &x) -> bool {
+                    if (fast) {
+                        if (!fb.careful())
+                            return alac_next_fast(g, fb, x);
+                        r.pos = p0 + fb.used;
+                        fast = false;
+                    }
+                    return g.next(r, x);
+                };
                 if (res) {
                     // the values too, for the channel restore (k_adec_channel
                     // then runs the adaptive filter without decoding again)
                     Out4 q;
                     q.p = res + (uint64_t)(F.nch + c) * stride;
                     q.b = make_int4(0, 0, 0, 0);
-                    while (g.next(r, v)) {
+                    while (step(v)) {
                         if (n < stride)
                             q.put(n, v);
                         ++n;
@@ -229,9 +246,11 @@ __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AF
                     if (n > stride)
                         res = nullptr; // a channel longer than the slot: not stored
                 } else {
-                    while (g.next(r, v))
+                    while (step(v))
                         ++n;
                 }
+                if (fast)
+                    r.pos = p0 + fb.used;
                 E.nres[c] = n;
             }
         }
