@@ -215,21 +215,29 @@ __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AF
                 uint32_t n = 0;
                 int32_t v;
                 // the walk on the windowed reader while 128 bits remain
-                // before the end, then on the exact one (field widths the
-                // window cannot take go to the exact reader at once)
-                bool fast = ss <= 32u && T.mk <= 32u;
-                AFastBits fb;
-                if (fast)
-                    fb.init(w, r.pos, r.end);
-                const uint64_t p0 = r.pos;
-                auto step = [&](int32_t &x) -> bool {
+                // before the end, then on the exact one from the same
+                // position (field widths the window cannot take go to the
+                // exact reader at once); two loops, so the hot one holds
+                // only the windowed step
+                const bool fast = ss <= 32u && T.mk <= 32u;
+                auto walk = [&](auto &&use) {
+                    bool done = false;
                     if (fast) {
-                        if (!fb.careful())
-                            return alac_next_fast(g, fb, x);
+                        AFastBits fb;
+                        fb.init(w, r.pos, r.end);
+                        const uint64_t p0 = r.pos;
+                        while (!fb.careful()) {
+                            if (!alac_next_fast(g, fb, v)) {
+                                done = true;
+                                break;
+                            }
+                            use(v);
+                        }
                         r.pos = p0 + fb.used;
-                        fast = false;
                     }
-                    return g.next(r, x);
+                    if (!done)
+                        while (g.next(r, v))
+                            use(v);
                 };
                 if (res) {
                     // the values too, for the channel restore (k_adec_channel
@@ -237,20 +245,17 @@ __device__ void parse_fs(const uint32_t *w, const ADTrack &T, uint64_t start, AF
                     Out4 q;
                     q.p = res + (uint64_t)(F.nch + c) * stride;
                     q.b = make_int4(0, 0, 0, 0);
-                    while (step(v)) {
+                    walk([&](int32_t x) {
                         if (n < stride)
-                            q.put(n, v);
+                            q.put(n, x);
                         ++n;
-                    }
+                    });
                     q.flush(n < stride ? n : stride);
                     if (n > stride)
                         res = nullptr; // a channel longer than the slot: not stored
                 } else {
-                    while (step(v))
-                        ++n;
+                    walk([&](int32_t) { ++n; });
                 }
-                if (fast)
-                    r.pos = p0 + fb.used;
                 E.nres[c] = n;
             }
         }
