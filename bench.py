@@ -91,6 +91,9 @@ def parse_args(argv=None):
     ap.add_argument("--chain-inflight", type=int, default=4,
                     help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
                          "hashes are rolled)")
+    ap.add_argument("--chain-md5", choices=("auto", "gpu", "host"), default="auto",
+                    help="config-5 chain leg: where the FLAC batches' MD5 runs (the engine's "
+                         "choice, rolled GPU chains, or host threads)")
     ap.add_argument("--no-chain", action="store_true")
     ap.add_argument("--no-host", action="store_true", help="skip the host-to-host leg")
     ap.add_argument("--no-t2t", action="store_true", help="skip the track2track leg")
@@ -744,7 +747,7 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     depth = max(3, args.chain_inflight)
     ys = [torch.empty(n_out * n_tracks * ch, dtype=torch.int32, device=device)
           for _ in range(depth)]
-    eng = _atgpu.Engine(local)
+    eng = _atgpu.Engine(local, md5=args.chain_md5)
     eng.set_inflight(depth)
     fopts = _atgpu.make_options(**FLAC8)
     ftracks = [(k * n_out, n_out) for k in range(n_tracks)]
