@@ -403,6 +403,28 @@ struct AFastBits {
             nb += 32u;
         }
     }
+    // top_up with selects: no divergent branch for the word itself, only
+    // for a chunk change (every fourth word)
+    __device__ __forceinline__ void top_up_sel()
+    {
+        if (k == 4u) { // the chunk is used up (next_word's lazy change)
+            a0 = b0;
+            a1 = b1;
+            a2 = b2;
+            a3 = b3;
+            ci += 1u;
+            load_chunk(ci + 1u);
+            k = 0u;
+        }
+        const bool t = nb < 32u;
+        const uint64_t wd = (uint64_t)__builtin_bswap32(a0);
+        W |= t ? wd << ((32u - nb) & 63u) : 0ull;
+        nb += t ? 32u : 0u;
+        a0 = t ? a1 : a0;
+        a1 = t ? a2 : a1;
+        a2 = t ? a3 : a2;
+        k += t ? 1u : 0u;
+    }
     __device__ __forceinline__ void init(const uint32_t *words, uint64_t pos, uint64_t end)
     {
         w = words;
@@ -447,6 +469,13 @@ struct AFastBits {
         return v;
     }
     __device__ __forceinline__ bool careful() const { return used > room; }
+    __device__ __forceinline__ void skip_sel(uint32_t n) // n <= 32
+    {
+        W <<= n;
+        nb -= n;
+        used += n;
+        top_up_sel();
+    }
 };
 
 // alac_read_residual on AFastBits, with at least 41 bits before `end`
@@ -459,23 +488,25 @@ __device__ __forceinline__ uint32_t alac_read_residual_fast(AFastBits &f, uint32
         f.skip(9u);
         return ss ? f.take(ss) : 0u;
     }
-    if (k == 0u) {
+    if (k > 23u) { // ones + 1 + k may pass the 32 bits in view
+        if (k == 0u) {
+            f.skip(ones + 1u);
+            return ones;
+        }
+        const uint32_t m = (1u << k) - 1u;
         f.skip(ones + 1u);
-        return ones;
-    }
-    const uint32_t m = (1u << k) - 1u;
-    uint32_t lsb;
-    if (ones + 1u + k <= 32u) {
-        lsb = (x << (ones + 1u)) >> (32u - k);
+        const uint32_t lsb = f.top32() >> (32u - k);
         const bool big = lsb > 1u;
-        f.skip(ones + k + (big ? 1u : 0u));
+        f.skip(k - (big ? 0u : 1u));
         return ones * m + (big ? lsb - 1u : 0u);
     }
-    f.skip(ones + 1u);
-    lsb = f.top32() >> (32u - k);
+    // ones <= 8, k <= 23: both fields in x, no branch (k = 0: the unary
+    // value alone)
+    const uint32_t lsb = k ? (x << (ones + 1u)) >> ((32u - k) & 31u) : 0u;
+    const uint32_t m = (1u << k) - 1u;
     const bool big = lsb > 1u;
-    f.skip(k - (big ? 0u : 1u));
-    return ones * m + (big ? lsb - 1u : 0u);
+    f.skip_sel(k ? ones + k + (big ? 1u : 0u) : ones + 1u);
+    return k ? ones * m + (big ? lsb - 1u : 0u) : ones;
 }
 
 // AResidualReader::next on AFastBits (caller checked !f.careful())
