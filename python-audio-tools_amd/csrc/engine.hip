@@ -11,6 +11,7 @@
 #include <sched.h>
 
 #include <algorithm>
+#include <array>
 #include <cmath>
 #include <condition_variable>
 #include <cstdio>
@@ -177,8 +178,9 @@ struct EncSlot {
     // host-MD5 mode (want_host_md5): the PCM goes to pinned host memory and
     // the pool's threads hash it; the digests go back before the headers
     bool md5_host = false;
-    uint8_t *hpcm = nullptr;         // pinned: the tracks' PCM containers
+    uint8_t *hpcm = nullptr;         // pinned: the tracks' MD5 byte streams
     size_t hpcm_cap = 0;
+    DevBuf dpack;                    // the same streams packed on the device
     uint8_t *hmd5 = nullptr;         // pinned: 16 bytes per track
     size_t hmd5_cap = 0;
     DevBuf md5in;                    // the digests on the device
@@ -815,11 +817,15 @@ unsigned host_hash_threads()
 
 // Host or GPU for this batch's MD5.  A GPU chain hashes one 64-byte block
 // per ~0.8 us (one wave per track, md5.hip), so the batch's MD5 ends when
-// its longest track's chain does; host threads hash ~450 MB/s each after a
-// D2H copy (~40 GB/s pinned).  The host side wins only for few, long tracks
-// whose chains would outlast the GPU work they overlap (config 5: 8.6 MB
-// tracks, ~110 ms chains); the GPU otherwise (config 2: 1 MiB tracks, ~13 ms
-// chains under the next batches' search kernels).
+// its longest track's chain does; on the host a core hashes 16 tracks at
+// once at ~6 GB/s with AVX-512 (md5_cpu.h hash_bytes_multi; ~0.45 GB/s per
+// thread without), after the packed streams' download (~40 GB/s pinned).
+// The host side wins only for few, long tracks whose chains would outlast
+// the GPU work they overlap (config 5: 8.6 MB tracks, ~110 ms chains); the
+// GPU otherwise (config 2: 1 MiB tracks, ~13 ms chains under the next
+// batches' search kernels).
+constexpr size_t kHashGroup = md5cpu::kMultiLanes; // tracks per host hash task
+
 bool want_host_md5(atg_engine *e, const Plan &pl, int fmt, bool md5_early)
 {
     const FlacParams &p = pl.p;
@@ -836,9 +842,14 @@ bool want_host_md5(atg_engine *e, const Plan &pl, int fmt, bool md5_early)
         maxb = std::max(maxb, b);
         tot += b;
     }
+    (void)cs;
     const double gpu_ms = (double)maxb / 64.0 * 0.8e-3;
-    const double host_ms = (double)tot / (host_hash_threads() * 450e3) +
-                           (double)tot / bb * cs / 40e6;
+    const unsigned th = host_hash_threads();
+    const uint64_t groups = (pl.tracks.size() + kHashGroup - 1) / kHashGroup;
+    const double hash_ms = md5cpu::multi_simd()
+                               ? (double)tot / (double)std::min<uint64_t>(th, groups) / 6e6
+                               : (double)tot / (th * 450e3);
+    const double host_ms = hash_ms + (double)tot / 40e6;
     return gpu_ms > 40.0 && host_ms < gpu_ms;
 }
 
@@ -850,45 +861,50 @@ atg_status start_host_md5(atg_engine *e, EncSlot &sl, const Plan &pl, const void
     const FlacParams &p = pl.p;
     const size_t nt = pl.tracks.size();
     const uint64_t cs = fmt == ATG_PCM_S16 ? 2 : 4;
+    const uint32_t bb = p.bps / 8;
     for (std::future<void> &f : sl.hash_jobs) // a failed earlier batch's tasks
         f.wait();
     sl.hash_jobs.clear();
+    // each track's byte stream at a 16-byte aligned offset
+    std::vector<uint64_t> off(nt), len(nt);
     uint64_t total = 0;
-    for (const TrackInfo &t : pl.tracks)
-        total += t.pcm_frames * p.channels * cs;
+    for (size_t t = 0; t < nt; ++t) {
+        len[t] = pl.tracks[t].pcm_frames * p.channels * bb;
+        off[t] = total;
+        total += (len[t] + 15u) & ~15ull;
+    }
     HIP_TRY(ensure_pinned(sl.hpcm, sl.hpcm_cap, (size_t)std::max<uint64_t>(total, 1)));
     HIP_TRY(ensure_pinned(sl.hmd5, sl.hmd5_cap, 16 * nt));
     HIP_TRY(sl.md5in.ensure(16 * nt));
+    HIP_TRY(sl.dpack.ensure((size_t)std::max<uint64_t>(total, 1)));
     if (!sl.ev_hpcm)
         HIP_TRY(hipEventCreateWithFlags(&sl.ev_hpcm, hipEventDisableTiming));
-    std::vector<uint64_t> off(nt);
-    uint64_t o = 0;
     for (size_t t = 0; t < nt; ++t) {
         const TrackInfo &ti = pl.tracks[t];
-        const uint64_t nb = ti.pcm_frames * p.channels * cs;
-        off[t] = o;
-        if (nb)
-            HIP_TRY(hipMemcpyAsync(sl.hpcm + o,
-                                   (const uint8_t *)d_pcm + ti.pcm_start * p.channels * cs, nb,
-                                   hipMemcpyDeviceToHost, sl.s_aux));
-        o += nb;
+        HIP_TRY(launch_md5_pack((const uint8_t *)d_pcm + ti.pcm_start * p.channels * cs,
+                                fmt == ATG_PCM_S16, ti.pcm_frames * p.channels, bb,
+                                (uint8_t *)sl.dpack.p + off[t], sl.s_aux));
     }
+    if (total)
+        HIP_TRY(hipMemcpyAsync(sl.hpcm, sl.dpack.p, total, hipMemcpyDeviceToHost, sl.s_aux));
     HIP_TRY(hipEventRecord(sl.ev_hpcm, sl.s_aux));
     if (!e->pool)
         e->pool.reset(new HashPool(host_hash_threads()));
-    sl.hash_jobs.clear();
     const hipEvent_t ev = sl.ev_hpcm;
-    const uint32_t bb = p.bps / 8;
-    for (size_t t = 0; t < nt; ++t) {
-        const uint8_t *src = sl.hpcm + off[t];
-        const uint64_t n = pl.tracks[t].pcm_frames * p.channels;
-        uint8_t *dst = sl.hmd5 + 16 * t;
+    // one pool task per group of kHashGroup tracks: their chains side by
+    // side in one core's vector registers
+    for (size_t g0 = 0; g0 < nt; g0 += kHashGroup) {
+        const int n = (int)std::min<size_t>(kHashGroup, nt - g0);
+        std::array<const uint8_t *, kHashGroup> src{};
+        std::array<uint64_t, kHashGroup> bytes{};
+        for (int i = 0; i < n; ++i) {
+            src[i] = sl.hpcm + off[g0 + i];
+            bytes[i] = len[g0 + i];
+        }
+        uint8_t(*dst)[16] = (uint8_t(*)[16])(sl.hmd5 + 16 * g0);
         sl.hash_jobs.push_back(e->pool->submit([=] {
             (void)hipEventSynchronize(ev);
-            if (cs == 2)
-                md5cpu::hash_s16((const int16_t *)src, n, bb, dst);
-            else
-                md5cpu::hash_s32((const int32_t *)src, n, bb, dst);
+            md5cpu::hash_bytes_multi(src.data(), bytes.data(), n, dst);
         }));
     }
     return ATG_OK;
@@ -1627,7 +1643,7 @@ void set_depth(atg_engine *e, uint64_t n)
         EncSlot &sl = e->slot[k];
         for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
                           &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch,
-                          &sl.slow, &sl.md5in})
+                          &sl.slow, &sl.md5in, &sl.dpack})
             b->release();
         sl.uploaded = nullptr;
         sl.plan.reset();
@@ -1752,7 +1768,7 @@ void atg_engine_destroy(atg_engine *e)
             (void)hipStreamSynchronize(sl.s_aux);
         for (DevBuf *b : {&sl.frames, &sl.tracks, &sl.order, &sl.coef, &sl.shift, &sl.est,
                           &sl.sub, &sl.fdesc, &sl.tout, &sl.err, &sl.rice_big, &sl.scratch,
-                          &sl.md5in})
+                          &sl.md5in, &sl.dpack})
             b->release();
         for (void *q : {(void *)sl.hpcm, (void *)sl.hmd5})
             if (q)

@@ -63,6 +63,10 @@ hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
                              uint8_t *out, uint32_t *err, hipStream_t s);
 // md5.hip: host-hashed digests into TrackOut (engine host-MD5 mode)
 hipError_t launch_put_md5(TrackOut *tout, const uint8_t *md5, uint32_t n, hipStream_t s);
+// md5.hip: the MD5 byte stream of n samples (low bb bytes of each int16 /
+// int32 container) at dst, 16-byte aligned
+hipError_t launch_md5_pack(const void *src, int s16, uint64_t n, uint32_t bb, uint8_t *dst,
+                           hipStream_t s);
 hipError_t launch_stream_header(const FlacParams &p, const TrackInfo *tracks,
                                 const TrackOut *tout, uint8_t *out,
                                 hipStream_t s);

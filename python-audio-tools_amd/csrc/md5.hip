@@ -986,6 +986,57 @@ __global__ __launch_bounds__(64) void k_put_md5(TrackOut *__restrict__ tout,
         tout[t].md5[i] = md5[16u * t + i];
 }
 
+// engine host-MD5 mode: a track's MD5 byte stream -- the low bb bytes of
+// each container, little-endian (FrameList.to_bytes, src/pcm.c) -- packed
+// on the device, so the download carries only those bytes and the host
+// threads hash them as they are (md5_cpu.h hash_bytes_multi).  A lane per
+// four samples: 4 bb bytes, whole dwords (dst is 16-byte aligned).
+template <typename T>
+__global__ __launch_bounds__(256) void k_md5_pack(const T *__restrict__ src, uint64_t n, uint32_t bb,
+                                                  uint8_t *__restrict__ dst)
+{
+    const uint64_t i = 4u * ((uint64_t)blockIdx.x * 256u + threadIdx.x);
+    if (i >= n)
+        return;
+    if (i + 4u <= n) {
+        const uint32_t v0 = (uint32_t)src[i], v1 = (uint32_t)src[i + 1];
+        const uint32_t v2 = (uint32_t)src[i + 2], v3 = (uint32_t)src[i + 3];
+        uint32_t *o = (uint32_t *)(dst + i * bb);
+        if (bb == 1u) {
+            o[0] = (v0 & 0xFFu) | ((v1 & 0xFFu) << 8) | ((v2 & 0xFFu) << 16) | (v3 << 24);
+        } else if (bb == 2u) {
+            *(uint2 *)o = make_uint2((v0 & 0xFFFFu) | (v1 << 16), (v2 & 0xFFFFu) | (v3 << 16));
+        } else if (bb == 3u) {
+            o[0] = (v0 & 0xFFFFFFu) | (v1 << 24);
+            o[1] = ((v1 >> 8) & 0xFFFFu) | (v2 << 16);
+            o[2] = ((v2 >> 16) & 0xFFu) | (v3 << 8);
+        } else {
+            *(uint4 *)o = make_uint4(v0, v1, v2, v3);
+        }
+    } else {
+        for (uint64_t q = i; q < n; ++q) {
+            const uint32_t v = (uint32_t)src[q];
+            for (uint32_t b = 0; b < bb; ++b)
+                dst[q * bb + b] = (uint8_t)(v >> (8u * b));
+        }
+    }
+}
+
+hipError_t launch_md5_pack(const void *src, int s16, uint64_t n, uint32_t bb, uint8_t *dst,
+                           hipStream_t s)
+{
+    if (!n)
+        return hipSuccess;
+    const dim3 grid((unsigned)((n + 1023u) / 1024u));
+    if (s16)
+        hipLaunchKernelGGL((k_md5_pack<int16_t>), grid, dim3(256), 0, s, (const int16_t *)src, n,
+                           bb, dst);
+    else
+        hipLaunchKernelGGL((k_md5_pack<int32_t>), grid, dim3(256), 0, s, (const int32_t *)src, n,
+                           bb, dst);
+    return hipGetLastError();
+}
+
 hipError_t launch_put_md5(TrackOut *tout, const uint8_t *md5, uint32_t n, hipStream_t s)
 {
     if (!n)

@@ -7,11 +7,15 @@
 //
 // Few long tracks (config 5: 64 tracks of 8.6 MB of 24-bit 5.1 PCM) give the
 // GPU one serial MD5 chain per track, ~0.8 us per 64-byte block on one wave
-// (md5.hip), i.e. ~110 ms per batch whatever the GPU's width; host cores
-// hash the same bytes at ~0.6 GB/s each, all tracks at once.
+// (md5.hip), i.e. ~110 ms per batch whatever the GPU's width; a host core
+// hashes one stream at ~0.6-1 GB/s, or sixteen side by side at ~6 GB/s
+// (hash_bytes_multi, AVX-512; the engine packs the streams on the device).
 #pragma once
 #include <stdint.h>
 #include <string.h>
+#if defined(__x86_64__)
+#include <immintrin.h>
+#endif
 
 namespace md5cpu {
 
@@ -211,6 +215,161 @@ static inline void hash_s16(const int16_t *s, uint64_t n, uint32_t bb, uint8_t o
         }
     }
     c.final(out);
+}
+
+// ---- many streams at once: 16 MD5 chains in the 32-bit lanes of AVX-512
+// registers (one chain per track, the tracks of a batch side by side).  A
+// chain is serial -- each step needs the last -- so one core runs one
+// scalar chain at ~1 GB/s whatever its width; sixteen side by side cost
+// about what one does (the same dependent adds, rotates and `vpternlogd`
+// F functions, one lane each).  The streams' common whole blocks run here;
+// each stream's remaining bytes and padding finish on its own Ctx.
+
+#if defined(__x86_64__)
+// 16 x 16 32-bit transpose: row l (lane l's 16 words) -> register w holds
+// word w of every lane
+__attribute__((target("avx512f"))) static inline void transpose16(__m512i (&r)[16])
+{
+    __m512i t[16];
+    for (int i = 0; i < 16; i += 2) {
+        t[i] = _mm512_unpacklo_epi32(r[i], r[i + 1]);
+        t[i + 1] = _mm512_unpackhi_epi32(r[i], r[i + 1]);
+    }
+    for (int i = 0; i < 16; i += 4) {
+        r[i] = _mm512_unpacklo_epi64(t[i], t[i + 2]);
+        r[i + 1] = _mm512_unpackhi_epi64(t[i], t[i + 2]);
+        r[i + 2] = _mm512_unpacklo_epi64(t[i + 1], t[i + 3]);
+        r[i + 3] = _mm512_unpackhi_epi64(t[i + 1], t[i + 3]);
+    }
+    for (int i = 0; i < 16; i += 8)
+        for (int j = 0; j < 4; ++j) {
+            t[i + j] = _mm512_shuffle_i32x4(r[i + j], r[i + j + 4], 0x88);
+            t[i + j + 4] = _mm512_shuffle_i32x4(r[i + j], r[i + j + 4], 0xDD);
+        }
+    for (int j = 0; j < 8; ++j) {
+        r[j] = _mm512_shuffle_i32x4(t[j], t[j + 8], 0x88);
+        r[j + 8] = _mm512_shuffle_i32x4(t[j], t[j + 8], 0xDD);
+    }
+}
+
+__attribute__((target("avx512f"))) static inline void mb16_blocks(uint32_t (&h)[4][16],
+                                                                const uint8_t *const *p,
+                                                                uint64_t nblocks)
+{
+    __m512i A = _mm512_loadu_si512(h[0]), B = _mm512_loadu_si512(h[1]);
+    __m512i C = _mm512_loadu_si512(h[2]), D = _mm512_loadu_si512(h[3]);
+    static const uint32_t K[64] = {
+        0xd76aa478, 0xe8c7b756, 0x242070db, 0xc1bdceee, 0xf57c0faf, 0x4787c62a, 0xa8304613,
+        0xfd469501, 0x698098d8, 0x8b44f7af, 0xffff5bb1, 0x895cd7be, 0x6b901122, 0xfd987193,
+        0xa679438e, 0x49b40821, 0xf61e2562, 0xc040b340, 0x265e5a51, 0xe9b6c7aa, 0xd62f105d,
+        0x02441453, 0xd8a1e681, 0xe7d3fbc8, 0x21e1cde6, 0xc33707d6, 0xf4d50d87, 0x455a14ed,
+        0xa9e3e905, 0xfcefa3f8, 0x676f02d9, 0x8d2a4c8a, 0xfffa3942, 0x8771f681, 0x6d9d6122,
+        0xfde5380c, 0xa4beea44, 0x4bdecfa9, 0xf6bb4b60, 0xbebfbc70, 0x289b7ec6, 0xeaa127fa,
+        0xd4ef3085, 0x04881d05, 0xd9d4d039, 0xe6db99e5, 0x1fa27cf8, 0xc4ac5665, 0xf4292244,
+        0x432aff97, 0xab9423a7, 0xfc93a039, 0x655b59c3, 0x8f0ccc92, 0xffeff47d, 0x85845dd1,
+        0x6fa87e4f, 0xfe2ce6e0, 0xa3014314, 0x4e0811a1, 0xf7537e82, 0xbd3af235, 0x2ad7d2bb,
+        0xeb86d391};
+    for (uint64_t j = 0; j < nblocks; ++j) {
+        __m512i r[16];
+        for (int l = 0; l < 16; ++l)
+            r[l] = _mm512_loadu_si512(p[l] + 64 * j);
+        transpose16(r); // r[w] = message word w of every lane
+        const __m512i *X = r;
+        const __m512i a0 = A, b0 = B, c0 = C, d0 = D;
+#define MB_STEP(imm, a, b, c, d, x, i, s)                                                      \
+    a = _mm512_add_epi32(                                                                   \
+        b, _mm512_rol_epi32(_mm512_add_epi32(_mm512_add_epi32(                              \
+                                a, _mm512_ternarylogic_epi32(b, c, d, imm)),                \
+                                             _mm512_add_epi32(x, _mm512_set1_epi32((int)K[i]))), \
+                            s))
+        for (int i = 0; i < 16; i += 4) {
+            MB_STEP(0xCA, A, B, C, D, X[i], i, 7);
+            MB_STEP(0xCA, D, A, B, C, X[i + 1], i + 1, 12);
+            MB_STEP(0xCA, C, D, A, B, X[i + 2], i + 2, 17);
+            MB_STEP(0xCA, B, C, D, A, X[i + 3], i + 3, 22);
+        }
+        for (int i = 16; i < 32; i += 4) {
+            MB_STEP(0xE4, A, B, C, D, X[(5 * i + 1) & 15], i, 5);
+            MB_STEP(0xE4, D, A, B, C, X[(5 * (i + 1) + 1) & 15], i + 1, 9);
+            MB_STEP(0xE4, C, D, A, B, X[(5 * (i + 2) + 1) & 15], i + 2, 14);
+            MB_STEP(0xE4, B, C, D, A, X[(5 * (i + 3) + 1) & 15], i + 3, 20);
+        }
+        for (int i = 32; i < 48; i += 4) {
+            MB_STEP(0x96, A, B, C, D, X[(3 * i + 5) & 15], i, 4);
+            MB_STEP(0x96, D, A, B, C, X[(3 * (i + 1) + 5) & 15], i + 1, 11);
+            MB_STEP(0x96, C, D, A, B, X[(3 * (i + 2) + 5) & 15], i + 2, 16);
+            MB_STEP(0x96, B, C, D, A, X[(3 * (i + 3) + 5) & 15], i + 3, 23);
+        }
+        for (int i = 48; i < 64; i += 4) {
+            MB_STEP(0x39, A, B, C, D, X[(7 * i) & 15], i, 6);
+            MB_STEP(0x39, D, A, B, C, X[(7 * (i + 1)) & 15], i + 1, 10);
+            MB_STEP(0x39, C, D, A, B, X[(7 * (i + 2)) & 15], i + 2, 15);
+            MB_STEP(0x39, B, C, D, A, X[(7 * (i + 3)) & 15], i + 3, 21);
+        }
+#undef MB_STEP
+        A = _mm512_add_epi32(A, a0);
+        B = _mm512_add_epi32(B, b0);
+        C = _mm512_add_epi32(C, c0);
+        D = _mm512_add_epi32(D, d0);
+    }
+    _mm512_storeu_si512(h[0], A);
+    _mm512_storeu_si512(h[1], B);
+    _mm512_storeu_si512(h[2], C);
+    _mm512_storeu_si512(h[3], D);
+}
+
+static inline bool have_avx512()
+{
+    static const bool ok = __builtin_cpu_supports("avx512f");
+    return ok;
+}
+#endif
+
+// streams hash_bytes_multi takes at once, and whether this CPU runs them
+// side by side (otherwise one after another on the scalar path)
+constexpr int kMultiLanes = 16;
+static inline bool multi_simd()
+{
+#if defined(__x86_64__)
+    return have_avx512();
+#else
+    return false;
+#endif
+}
+
+// MD5 of n byte streams (n <= 16): p[i] / len[i] -> out[i]
+static inline void hash_bytes_multi(const uint8_t *const *p, const uint64_t *len, int n,
+                                    uint8_t (*out)[16], bool allow_simd = true)
+{
+    Ctx c[16];
+    uint64_t common = 0;
+#if defined(__x86_64__)
+    if (allow_simd && n > 1 && have_avx512()) {
+        common = ~0ull;
+        for (int i = 0; i < n; ++i)
+            common = len[i] / 64 < common ? len[i] / 64 : common;
+        if (common) {
+            uint32_t h[4][16];
+            const uint8_t *q[16];
+            for (int l = 0; l < 16; ++l) {
+                const int i = l < n ? l : 0; // idle lanes repeat stream 0
+                q[l] = p[i];
+                for (int k = 0; k < 4; ++k)
+                    h[k][l] = c[0].h[k];
+            }
+            mb16_blocks(h, q, common);
+            for (int i = 0; i < n; ++i) {
+                for (int k = 0; k < 4; ++k)
+                    c[i].h[k] = h[k][i];
+                c[i].len = common * 64;
+            }
+        }
+    }
+#endif
+    for (int i = 0; i < n; ++i) {
+        c[i].update(p[i] + common * 64, (size_t)(len[i] - common * 64));
+        c[i].final(out[i]);
+    }
 }
 
 } // namespace md5cpu
