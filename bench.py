@@ -91,6 +91,9 @@ def parse_args(argv=None):
     ap.add_argument("--chain-inflight", type=int, default=4,
                     help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
                          "hashes are rolled)")
+    ap.add_argument("--chain-decoders", type=int, default=2,
+                    help="config-5 chain leg: ALAC decoders (PCM buffers) the decode thread "
+                         "cycles through")
     ap.add_argument("--chain-md5", choices=("auto", "gpu", "host"), default="auto",
                     help="config-5 chain leg: where the FLAC batches' MD5 runs (the engine's "
                          "choice, rolled GPU chains, or host threads)")
@@ -735,7 +738,7 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
     # releases the GIL inside every library call, so the GPU sees the ALAC
     # kernels beside the resampler's and the encoder's.  A decoder is handed
     # back once the (synchronous) resample has read its buffer.
-    n_dec = 2
+    n_dec = max(2, args.chain_decoders)
     adecs = [_atgpu.AlacDecoder(local) for _ in range(n_dec)]
     rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
     n_out = _atgpu.resample_output_frames(n_in, ch, rin, rout)
@@ -847,8 +850,8 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
                       "channels": ch, "bits": bps, "rates": "%d -> %d" % (rin, rout),
                       "alac_bytes": alac_bytes, "flac_bytes": flac_bytes,
                       "flac_frames": n_flac,
-                      "pipeline": "decode thread (2 ALAC decoders) beside resample + FLAC "
-                                  "encode, %d FLAC batches in flight" % depth},
+                      "pipeline": "decode thread (%d ALAC decoders) beside resample + FLAC "
+                                  "encode, %d FLAC batches in flight" % (n_dec, depth)},
            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
            "verified_alac_lossless": bool(dec_ok and lossless),
            "alac_decode_status": sorted({int(r.status) for r in dres}),
