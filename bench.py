@@ -91,7 +91,7 @@ def parse_args(argv=None):
     ap.add_argument("--chain-inflight", type=int, default=4,
                     help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
                          "hashes are rolled)")
-    ap.add_argument("--chain-decoders", type=int, default=2,
+    ap.add_argument("--chain-decoders", type=int, default=3,
                     help="config-5 chain leg: ALAC decoders (PCM buffers) the decode thread "
                          "cycles through")
     ap.add_argument("--chain-md5", choices=("auto", "gpu", "host"), default="auto",
