@@ -732,12 +732,13 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
             frameset_bytes=fsb[r.first_frameset:r.first_frameset + r.n_framesets]))
     alac_bytes = sum(int(r.bytes) for r in ares)
     nbytes = max(int(r.out_offset + r.bytes) for r in ares)
-    # the pipeline: a decode thread runs batch k + 1's
-    # ALAC decode on one of two decoders (each owns its PCM buffer) while the
-    # main thread resamples batch k and enqueues its FLAC encode; ctypes
-    # releases the GIL inside every library call, so the GPU sees the ALAC
-    # kernels beside the resampler's and the encoder's.  A decoder is handed
-    # back once the (synchronous) resample has read its buffer.
+    # the pipeline: a decode thread runs the next
+    # batches' ALAC decodes on n_dec decoders (each owns its PCM buffer; three
+    # let it run two batches ahead) while the main thread resamples batch k
+    # and enqueues its FLAC encode; ctypes releases the GIL inside every
+    # library call, so the GPU sees the ALAC kernels beside the resampler's
+    # and the encoder's.  A decoder is handed back once the (synchronous)
+    # resample has read its buffer.
     n_dec = max(2, args.chain_decoders)
     adecs = [_atgpu.AlacDecoder(local) for _ in range(n_dec)]
     rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
