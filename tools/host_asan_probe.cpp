@@ -128,6 +128,28 @@ static int md5_check(std::mt19937_64 &rng)
             }
             ++cases;
         }
+    // the multi-stream hash (16 chains side by side) on streams of unequal
+    // lengths, exact-size heap buffers so a read past a stream is reported
+    for (int t = 0; t < 40; ++t) {
+        const int n = 1 + (int)(rng() % 16);
+        std::vector<std::vector<uint8_t>> st(n);
+        const uint8_t *p[16];
+        uint64_t len[16];
+        for (int i = 0; i < n; ++i) {
+            st[i].resize(t % 2 ? (size_t)(rng() % 3000) : (size_t)(64 * (rng() % 40)));
+            for (uint8_t &b : st[i])
+                b = (uint8_t)rng();
+            p[i] = st[i].empty() ? nullptr : st[i].data();
+            len[i] = st[i].size();
+        }
+        uint8_t got[16][16], want[16];
+        md5cpu::hash_bytes_multi(p, len, n, got);
+        for (int i = 0; i < n; ++i) {
+            md5_ref(p[i], (size_t)len[i], want);
+            CHECK(std::memcmp(want, got[i], 16) == 0);
+        }
+        ++cases;
+    }
     return cases;
 }
 
