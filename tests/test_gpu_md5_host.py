@@ -89,3 +89,22 @@ def test_auto_picks_host_for_long_tracks_and_matches_gpu():
         want, _ = oracle_port.encode(p, ch, bps, rate, **FLAC8)
         assert img == want
     assert "track_md5" in auto_kt
+
+
+@pytest.mark.parametrize("ch,bps", [(2, 16), (6, 24)])
+def test_host_md5_groups_of_sixteen(ch, bps):
+    """more tracks than one host task takes (16 per task, hashed side by
+    side): 37 tracks of uneven lengths, so the groups differ in size and
+    every stream ends at its own byte"""
+    import torch
+    from audiotools import _atgpu
+    pcms = [signals.make("tone" if k % 3 else "noise", 700 + 311 * k, ch, bps, seed=20 + k)
+            for k in range(37)]
+    eng = _atgpu.Engine(0, md5="host")
+    try:
+        (batch,) = _encode(eng, torch, pcms, ch, bps, 44100)
+    finally:
+        eng.close()
+    for p, img in zip(pcms, batch):
+        want, _ = oracle_port.encode(p, ch, bps, 44100, **FLAC8)
+        assert img == want
