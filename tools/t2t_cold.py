@@ -10,9 +10,11 @@ GPU, and breaks the per-process time into phases; the reference encoder
 (oracle/_ref/flacenc, one process per file, J at a time) runs the same files
 beside it when present.
 
-  python tools/t2t_cold.py J [N] [--frames F] [--fork] [--own-engine]  -> JSON line
+  python tools/t2t_cold.py J [N] [--frames F] [--fork] [--own-engine] [--warm]  -> JSON line
     --fork: the parent imports audiotools and forks a process per file
     (multiprocessing, as track2track); default: a fresh interpreter each
+    --warm (with --fork): the same files converted a second time, timed
+    apart, with the encoder service the first run started still up
     --own-engine: ATG_ENCODER_SERVICE=off (every process its own engine)
   python tools/t2t_cold.py --one in.wav out.flac   (a child)
 """
@@ -182,11 +184,26 @@ def main():
             from audiotools import encoders  # noqa: F401
             wall, done = run_forks(files, gdir, j)
             keys = ["hip_init", "encode"]
+            warm = None
+            if "--warm" in sys.argv:
+                # the same files again with the encoder service the first
+                # run started still up (a session's later conversions)
+                wdir = os.path.join(d, "gpu_warm")
+                os.mkdir(wdir)
+                wwall, _ = run_forks(files, wdir, j)
+                same_w = all(open(os.path.join(wdir, os.path.basename(f)[:-4] + ".flac"),
+                                  "rb").read() ==
+                             open(os.path.join(gdir, os.path.basename(f)[:-4] + ".flac"),
+                                  "rb").read() for f in files)
+                warm = {"wall_s": round(wwall, 3),
+                        "frames_per_s": round(n_files * frames / wwall, 1),
+                        "files_identical_to_first_run": same_w}
         else:
             cmds = [[sys.executable, os.path.abspath(__file__), "--one", fn,
                      os.path.join(gdir, os.path.basename(fn)[:-4] + ".flac")] for fn in files]
             wall, done = run_pool(cmds, j)
             keys = ["numpy", "audiotools", "hip_init", "encode"]
+            warm = None
         phases = {}
         for ts, out in done:
             t = json.loads(out.strip().splitlines()[-1])["t"]
@@ -204,6 +221,8 @@ def main():
                "per_process_ms_mean": {k: round(1e3 * sum(v) / len(v), 1)
                                        for k, v in phases.items()},
                "per_process_ms_max": {k: round(1e3 * max(v), 1) for k, v in phases.items()}}
+        if warm:
+            res["warm"] = warm
         ref = os.path.join(ROOT, "oracle", "_ref", "flacenc")
         if os.path.exists(ref):
             rdir = os.path.join(d, "ref")
