@@ -157,7 +157,23 @@ __global__ __launch_bounds__(64) void k_rs_positions(const RsTrack *__restrict__
 // fused multiply-add: fraction (12 bits) times the float difference (24
 // bits) is exact in fp64, so the FMA rounds once exactly where the
 // reference's separate multiply and add do.
-template <int CH, bool LEFT, bool HOIST, typename XT>
+// k_rs_phase's window index for more than two channels: one pad word after
+// every 16 floats.  A wave's lanes read frames `lspan x ratio` apart (8
+// frames = 48 floats for 192 -> 48 kHz 5.1), which without the pad land on
+// a few LDS banks (16-way conflicts, the kernel's largest stall); padded,
+// the lane bases are 51 words apart, coprime with the bank count.
+template <bool PAD>
+__device__ __forceinline__ uint32_t xpad(uint32_t i)
+{
+    return PAD ? i + (i >> 4) : i;
+}
+// floats a window of n floats occupies
+__host__ __device__ inline size_t xpad_floats(size_t n, int channels)
+{
+    return channels > 2 ? n + n / 16 + 1 : n;
+}
+
+template <int CH, bool LEFT, bool HOIST, typename XT, bool PAD = false>
 __device__ __forceinline__ void half_filter(const float *__restrict__ C, const XT *__restrict__ X,
                                             int32_t fi, int32_t inc, int32_t di,
                                             double (&acc)[CH])
@@ -173,7 +189,7 @@ __device__ __forceinline__ void half_filter(const float *__restrict__ C, const X
         const double icoeff = __builtin_fma(fraction, (double)(c1 - c0), (double)c0);
 #pragma unroll
         for (int k = 0; k < CH; ++k)
-            acc[k] = acc[k] + icoeff * (double)X[di * CH + k];
+            acc[k] = acc[k] + icoeff * (double)X[xpad<PAD>((uint32_t)(di * CH + k))];
         fi -= inc;
         di += LEFT ? 1 : -1;
     }
@@ -447,6 +463,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                                                   uint64_t tab_stride)
 {
     extern __shared__ double lds_d[];
+    constexpr bool PAD = CH > 2; // the window's layout (xpad)
     const uint32_t wave = threadIdx.x >> 6, lane = threadIdx.x & 63, nwaves = blockDim.x >> 6;
     double *cL = lds_d + (size_t)wave * 2 * M * wmax; // [wmax][M] left, then right
     double *cR = cL + (size_t)M * wmax;
@@ -486,7 +503,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
             for (uint32_t b = 0; b < kStage; ++b) {
                 const uint32_t i = i0 + b * blockDim.x;
                 if (i < nx)
-                    X[i] = (PhaseX)((float)v[b] * P.inv_q);
+                    X[xpad<PAD>(i)] = (PhaseX)((float)v[b] * P.inv_q);
             }
         }
         __syncthreads();
@@ -573,13 +590,13 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                 WL = __builtin_amdgcn_readfirstlane(WL);
                 WR = __builtin_amdgcn_readfirstlane(WR);
                 wave_lds_sync();
-                const PhaseX *xl = X + (int64_t)(c[0] + sl0 - w0) * CH;
+                const uint32_t bl = (uint32_t)((int64_t)(c[0] + sl0 - w0) * CH);
 #pragma unroll 2
                 for (int32_t k = 0; k < WL; ++k) {
                     double x[CH];
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
-                        x[q] = (double)xl[k * CH + q];
+                        x[q] = (double)X[xpad<PAD>(bl + (uint32_t)(k * CH + q))];
                     double ic[M];
                     load_coefs<M>(cL + k * M, ic);
 #pragma unroll
@@ -589,13 +606,13 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                             left[m][q] = left[m][q] + ic[m] * x[q];
                     }
                 }
-                const PhaseX *xr = X + (int64_t)(c[0] + sr1 - w0) * CH;
+                const uint32_t br = (uint32_t)((int64_t)(c[0] + sr1 - w0) * CH);
 #pragma unroll 2
                 for (int32_t k = 0; k < WR; ++k) {
                     double x[CH];
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
-                        x[q] = (double)xr[-k * CH + q];
+                        x[q] = (double)X[xpad<PAD>(br - (uint32_t)(k * CH) + (uint32_t)q)];
                     double ic[M];
                     load_coefs<M>(cR + k * M, ic);
 #pragma unroll
@@ -612,11 +629,11 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                     if (!valid[m])
                         continue;
                     const int32_t ccl = (max_fi - sfi[m]) / inc;
-                    half_filter<CH, true, false>(Cg, X, sfi[m] + ccl * inc, inc,
+                    half_filter<CH, true, false, PhaseX, PAD>(Cg, X, sfi[m] + ccl * inc, inc,
                                                  (int32_t)(c[m] - ccl - w0), left[m]);
                     const int32_t fr = inc - sfi[m];
                     const int32_t ccr = (max_fi - fr) / inc;
-                    half_filter<CH, false, false>(Cg, X, fr + ccr * inc, inc,
+                    half_filter<CH, false, false, PhaseX, PAD>(Cg, X, fr + ccr * inc, inc,
                                                   (int32_t)(c[m] + 1 + ccr - w0), right[m]);
                 }
             }
@@ -1076,8 +1093,9 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             uint64_t r = 0;
             for (uint64_t R = 1; R <= 64; R *= 2) {
                 const size_t win =
-                    (size_t)(64 * (L / p_out) * q_in * R + 2 * reach + 8 + (pm - 1) * step + 2) *
-                    channels * kPhaseXBytes;
+                    xpad_floats((size_t)(64 * (L / p_out) * q_in * R + 2 * reach + 8 +
+                                         (pm - 1) * step + 2) * channels, (int)channels) *
+                    kPhaseXBytes;
                 if (coef + win > kLds)
                     break;
                 r = R;
@@ -1182,9 +1200,11 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             const uint64_t g = std::gcd((uint64_t)a.in_rate, (uint64_t)a.out_rate);
             const uint64_t reach = (uint64_t)(max_fi / v.increment) + 2;
             lds_phase = std::max(lds_phase, waves * 2 * pm * wmax * sizeof(double) +
-                                                (size_t)(64 * (lspan[t] / per[t]) * (a.in_rate / g) *
-                                                         rows[t] + 2 * reach + 8 + T.wext) *
-                                                    channels * kPhaseXBytes);
+                                                xpad_floats((size_t)(64 * (lspan[t] / per[t]) *
+                                                                         (a.in_rate / g) * rows[t] +
+                                                                     2 * reach + 8 + T.wext) *
+                                                                channels, (int)channels) *
+                                                    kPhaseXBytes);
         } else {
             for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)
                 chunk_track.push_back(t);
