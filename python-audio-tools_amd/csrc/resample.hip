@@ -157,20 +157,22 @@ __global__ __launch_bounds__(64) void k_rs_positions(const RsTrack *__restrict__
 // fused multiply-add: fraction (12 bits) times the float difference (24
 // bits) is exact in fp64, so the FMA rounds once exactly where the
 // reference's separate multiply and add do.
-// k_rs_phase's window index for more than two channels: one pad word after
-// every 16 floats.  A wave's lanes read frames `lspan x ratio` apart (8
-// frames = 48 floats for 192 -> 48 kHz 5.1), which without the pad land on
-// a few LDS banks (16-way conflicts, the kernel's largest stall); padded,
-// the lane bases are 51 words apart, coprime with the bank count.
-template <bool PAD>
-__device__ __forceinline__ uint32_t xpad(uint32_t i)
+// k_rs_phase's window layout for more than two channels: frame f's CH
+// floats at f CH + f / 8 (one pad word after every 8 frames).  A wave's
+// lanes read frames `lspan x ratio` apart (8 frames = 48 floats for 192 ->
+// 48 kHz 5.1), which unpadded land on a few LDS banks (16-way conflicts,
+// the kernel's largest stall); padded, the lane bases are 49 words apart,
+// coprime with the bank count, and a frame's channels stay contiguous (one
+// base per tap, the channels at immediate offsets).
+template <int CH, bool PAD>
+__device__ __forceinline__ uint32_t xframe(uint32_t f)
 {
-    return PAD ? i + (i >> 4) : i;
+    return f * CH + (PAD ? f >> 3 : 0u);
 }
-// floats a window of n floats occupies
-__host__ __device__ inline size_t xpad_floats(size_t n, int channels)
+// floats a window of `frames` frames occupies
+__host__ __device__ inline size_t xpad_floats(size_t frames, int channels)
 {
-    return channels > 2 ? n + n / 16 + 1 : n;
+    return frames * channels + (channels > 2 ? frames / 8 + 1 : 0);
 }
 
 template <int CH, bool LEFT, bool HOIST, typename XT, bool PAD = false>
@@ -189,7 +191,7 @@ __device__ __forceinline__ void half_filter(const float *__restrict__ C, const X
         const double icoeff = __builtin_fma(fraction, (double)(c1 - c0), (double)c0);
 #pragma unroll
         for (int k = 0; k < CH; ++k)
-            acc[k] = acc[k] + icoeff * (double)X[xpad<PAD>((uint32_t)(di * CH + k))];
+            acc[k] = acc[k] + icoeff * (double)X[xframe<CH, PAD>((uint32_t)di) + k];
         fi -= inc;
         di += LEFT ? 1 : -1;
     }
@@ -503,7 +505,7 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
             for (uint32_t b = 0; b < kStage; ++b) {
                 const uint32_t i = i0 + b * blockDim.x;
                 if (i < nx)
-                    X[xpad<PAD>(i)] = (PhaseX)((float)v[b] * P.inv_q);
+                    X[i + (PAD ? (i / CH) >> 3 : 0u)] = (PhaseX)((float)v[b] * P.inv_q);
             }
         }
         __syncthreads();
@@ -590,13 +592,14 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                 WL = __builtin_amdgcn_readfirstlane(WL);
                 WR = __builtin_amdgcn_readfirstlane(WR);
                 wave_lds_sync();
-                const uint32_t bl = (uint32_t)((int64_t)(c[0] + sl0 - w0) * CH);
+                const uint32_t fl = (uint32_t)(c[0] + sl0 - w0);
 #pragma unroll 2
                 for (int32_t k = 0; k < WL; ++k) {
                     double x[CH];
+                    const PhaseX *xk = X + xframe<CH, PAD>(fl + (uint32_t)k);
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
-                        x[q] = (double)X[xpad<PAD>(bl + (uint32_t)(k * CH + q))];
+                        x[q] = (double)xk[q];
                     double ic[M];
                     load_coefs<M>(cL + k * M, ic);
 #pragma unroll
@@ -606,13 +609,14 @@ __global__ __launch_bounds__(1024) void k_rs_phase(RsParams P, const RsTrack *__
                             left[m][q] = left[m][q] + ic[m] * x[q];
                     }
                 }
-                const uint32_t br = (uint32_t)((int64_t)(c[0] + sr1 - w0) * CH);
+                const uint32_t fr0 = (uint32_t)(c[0] + sr1 - w0);
 #pragma unroll 2
                 for (int32_t k = 0; k < WR; ++k) {
                     double x[CH];
+                    const PhaseX *xk = X + xframe<CH, PAD>(fr0 - (uint32_t)k);
 #pragma unroll
                     for (int q = 0; q < CH; ++q)
-                        x[q] = (double)X[xpad<PAD>(br - (uint32_t)(k * CH) + (uint32_t)q)];
+                        x[q] = (double)xk[q];
                     double ic[M];
                     load_coefs<M>(cR + k * M, ic);
 #pragma unroll
@@ -1094,7 +1098,7 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             for (uint64_t R = 1; R <= 64; R *= 2) {
                 const size_t win =
                     xpad_floats((size_t)(64 * (L / p_out) * q_in * R + 2 * reach + 8 +
-                                         (pm - 1) * step + 2) * channels, (int)channels) *
+                                         (pm - 1) * step + 2), (int)channels) *
                     kPhaseXBytes;
                 if (coef + win > kLds)
                     break;
@@ -1202,8 +1206,8 @@ atg_status atg_resample_device(const atg_rs_track *tracks, uint32_t n, uint32_t 
             lds_phase = std::max(lds_phase, waves * 2 * pm * wmax * sizeof(double) +
                                                 xpad_floats((size_t)(64 * (lspan[t] / per[t]) *
                                                                          (a.in_rate / g) * rows[t] +
-                                                                     2 * reach + 8 + T.wext) *
-                                                                channels, (int)channels) *
+                                                                     2 * reach + 8 + T.wext),
+                                                            (int)channels) *
                                                     kPhaseXBytes);
         } else {
             for (uint64_t k = 0; k < (T.out_frames + chunk - 1) / chunk; ++k)

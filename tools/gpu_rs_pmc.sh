@@ -9,4 +9,4 @@ cd /tmp && export TMPDIR=/tmp
 timeout -s KILL 240 rocprofv3 --pmc SQ_INSTS_LDS SQ_ACTIVE_INST_LDS SQ_LDS_BANK_CONFLICT \
     SQ_WAIT_INST_LDS SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES \
     -d "$OUT/sq" -o run --output-format csv -- python3 $R/bench.py --steps 2 --warmup 1 \
-    --no-cpu-baseline --no-verify --no-host --no-t2t --no-rg4 --narrow= --no-decode > "$OUT/sq.log" 2>&1
+    --no-cpu-baseline --no-verify --no-host --no-t2t --no-rg4 --narrow= > "$OUT/sq.log" 2>&1
