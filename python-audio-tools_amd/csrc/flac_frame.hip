@@ -251,6 +251,14 @@ __device__ __forceinline__ void put_bits(uint32_t *fb, uint32_t pos, uint32_t n,
         atomicOr(&fb[w + 1], lo);
 }
 
+// LDS written by some lanes of a wave, then read by others of the same wave
+__device__ __forceinline__ void wave_lds_sync()
+{
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+}
+
 // per-lane MSB-first bit stream into the zeroed LDS image.  A lane's bit
 // range [begin, end) shares at most its first and last words with the
 // neighbouring lanes: those two are OR-ed in by end() (the first is held
@@ -356,38 +364,54 @@ __device__ __forceinline__ void emit_codes(LaneWriter &w, const uint32_t (&u)[AT
 // pairs with 16-byte loads: no sample LDS, twice the occupancy.  Used for
 // the leading full-length (4096) frames of a 16-bit mid/side batch whose
 // frame starts are 16-byte aligned (engine.hip counts them: n_reg_frames).
+// NW waves per frame (REG: 1): wave w packs subframes w, w + NW, ... into
+// the shared image, each from its own sample staging; a subframe's first bit
+// is the header plus the searched sizes (SubDesc.bits) of the ones before
+// it, and neighbouring subframes meet only in OR-ed words.  A 6-channel
+// 24-bit frame's image (75 KB) leaves LDS for one frame per CU: one wave
+// per CU before, three now.
 // waves per SIMD the pack kernel's registers are budgeted for
 constexpr int kK5WavesPerEu = 2;
-template <typename T, bool REG>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerEu))) void k_frame_pack(
+template <typename T, bool REG, int NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(kK5WavesPerEu))) void k_frame_pack(
     FlacParams p, uint32_t f0, const T *__restrict__ pcm, const FrameInfo *__restrict__ frames,
     const TrackInfo *__restrict__ tracks, const SubDesc *__restrict__ sub,
     const FrameDesc *__restrict__ fdesc, uint8_t *__restrict__ out, uint32_t *__restrict__ err)
 {
+    static_assert(!REG || NW == 1, "the register-staged pack is one wave per frame");
     extern __shared__ __attribute__((aligned(16))) uint32_t fb[];
-    __shared__ __attribute__((aligned(16))) int32_t sl[REG ? 4 : SL_WORDS];
-    __shared__ int32_t cfs[ATG_MAX_LPC];
+    __shared__ __attribute__((aligned(16))) int32_t sl_all[REG ? 4 : NW * SL_WORDS];
+    __shared__ int32_t cfs_all[NW][ATG_MAX_LPC];
     __shared__ uint16_t crc_tab[4][256];
 
     const uint32_t f = f0 + blockIdx.x;
-    const int lane = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wave = NW == 1 ? 0 : __builtin_amdgcn_readfirstlane(tid >> 6);
+    int32_t *sl = sl_all + (REG ? 0 : wave * SL_WORDS);
+    int32_t *cfs = cfs_all[wave];
     const FrameInfo fi = frames[f];
     const FrameDesc &fd = fdesc[f]; // by reference: hdr[]/sub[] indexed per lane
     const uint32_t N = fi.n;
     const bool ms = (p.n_cand == 4u) && (p.channels == 2u);
     const uint32_t words = (fd.bytes + 3u) / 4u + 1u;
 
-    for (uint32_t i = lane; i < words; i += 64)
+    for (uint32_t i = tid; i < words; i += 64 * NW)
         fb[i] = 0;
-    for (uint32_t i = lane; i < 1024u; i += 64)
+    for (uint32_t i = tid; i < 1024u; i += 64 * NW)
         (&crc_tab[0][0])[i] = (uint16_t)(&c_crc16[0][0])[i];
     if (!REG)
         for (int i = lane; i < SL_PRE; i += 64)
             sl[i] = 0;
     __syncthreads();
-    if (lane < fd.hdr_len)
-        put_bits(fb, 8u * lane, 8, fd.hdr[lane]);
-    uint32_t pos = 8u * fd.hdr_len;
+    if (tid < fd.hdr_len)
+        put_bits(fb, 8u * tid, 8, fd.hdr[tid]);
+    // the sample staging and coefficients are the wave's own
+    auto sync = [] {
+        if (NW == 1)
+            __syncthreads();
+        else
+            wave_lds_sync();
+    };
 
     // lane run mapping (same as the search kernel; REG: N = 4096 -> 64l..64l+63)
     const uint32_t tz = N ? (uint32_t)__builtin_ctz(N) : 0u;
@@ -400,7 +424,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
     ra = ra < re ? ra : re;
     const int len = (int)(re - ra);
 
-    for (uint32_t si = 0; si < fd.nsub; ++si) {
+    for (uint32_t si = (uint32_t)wave; si < fd.nsub; si += NW) {
+        uint32_t pos = 8u * fd.hdr_len;
+        for (uint32_t s0 = 0; s0 < si; ++s0)
+            pos += sub[(size_t)f * p.n_cand + fd.sub[s0]].bits;
         // REG: the frame's 16-bit stereo pairs for samples [ra - 16, ra + 64),
         // (re)loaded per subframe so they are not live across the emission
         uint32_t pr[80];
@@ -451,7 +478,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
                   : (lane == 0 ? 4 : lane == 1 ? -6 : lane == 2 ? 4 : -1);
             cfs[lane] = c;
         }
-        __syncthreads();
+        sync();
         const uint32_t rb = sbps - w;
         const uint32_t rmask = rb >= 32u ? 0xFFFFFFFFu : (1u << rb) - 1u;
         if (type == SF_CONSTANT) {
@@ -621,7 +648,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
         }
         if (pos - start != d.bits && lane == 0)
             atomicOr(err, 2u);
-        __syncthreads();
+        sync();
     }
     __syncthreads();
 
@@ -632,6 +659,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
     // 256 kCrcQ bytes (fewer than 256 prefix bytes: every lane has work),
     // else the power of two 2^m >= L / 64
     const uint32_t L = fd.bytes - 2u;
+    if (wave == 0) {
     const uint32_t cq = (L + 255u) >> 8;
     const bool qlen = cq >= 1u && cq <= (uint32_t)kCrcQ;
     uint32_t lc_log = 2;
@@ -667,6 +695,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
     }
     if (lane == 0)
         put_bits(fb, 8u * L, 16, crc);
+    }
     __syncthreads();
 
     // copy the image to its place: aligned dwords inside, bytes at the ends
@@ -676,15 +705,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kK5WavesPerE
     const uint32_t head = (uint32_t)((4u - (d0 & 3u)) & 3u);
     const uint32_t nb = fd.bytes;
     const uint32_t h = head < nb ? head : nb;
-    if ((uint32_t)lane < h)
-        dst[lane] = (uint8_t)fb_byte(fb, lane);
+    if ((uint32_t)tid < h)
+        dst[tid] = (uint8_t)fb_byte(fb, tid);
     const uint32_t body = (nb - h) / 4u;
     uint32_t *dw = (uint32_t *)(dst + h);
-    for (uint32_t i = lane; i < body; i += 64)
+    for (uint32_t i = tid; i < body; i += 64 * NW)
         dw[i] = __builtin_bswap32(fb_be32(fb, h + 4u * i));
     const uint32_t tail0 = h + 4u * body;
-    if (tail0 + (uint32_t)lane < nb)
-        dst[tail0 + lane] = (uint8_t)fb_byte(fb, tail0 + lane);
+    if (tid < 64 && tail0 + (uint32_t)tid < nb)
+        dst[tail0 + tid] = (uint8_t)fb_byte(fb, tail0 + tid);
 }
 
 // ---------------------------------------------------------------- K6
@@ -776,17 +805,37 @@ hipError_t launch_frame_pack(const FlacParams &p, const void *pcm, int fmt,
     const size_t lds = (size_t)p.frame_lds_words * 4u;
     const uint32_t nreg = fmt == 0 ? p.n_reg_frames : 0u;
     if (nreg)
-        hipLaunchKernelGGL((k_frame_pack<int16_t, true>), dim3(nreg), dim3(64), lds, s, p, 0u,
+        hipLaunchKernelGGL((k_frame_pack<int16_t, true, 1>), dim3(nreg), dim3(64), lds, s, p, 0u,
                            (const int16_t *)pcm, frames, tracks, sub, fd, out, err);
     const uint32_t rest = p.n_frames - nreg;
     if (rest == 0)
         return hipGetLastError();
-    if (fmt == 0)
-        hipLaunchKernelGGL((k_frame_pack<int16_t, false>), dim3(rest), dim3(64), lds, s, p, nreg,
-                           (const int16_t *)pcm, frames, tracks, sub, fd, out, err);
-    else
-        hipLaunchKernelGGL((k_frame_pack<int32_t, false>), dim3(rest), dim3(64), lds, s, p, nreg,
-                           (const int32_t *)pcm, frames, tracks, sub, fd, out, err);
+    // waves per frame: the subframes (one per channel) in as few rounds as
+    // four waves take them, spread evenly (6 -> 3 x 2, 5 -> 3, 8 -> 4 x 2),
+    // fewer while the image and the waves' staging exceed the CU's LDS
+    const uint32_t nsub = p.channels > 8u ? 8u : (p.channels ? p.channels : 1u);
+    const uint32_t rounds = (nsub + 3u) / 4u;
+    uint32_t nw = (nsub + rounds - 1u) / rounds;
+    const size_t per_wave = (size_t)(SL_WORDS + ATG_MAX_LPC) * 4u;
+    while (nw > 1u && lds + 2048u + nw * per_wave > 160u * 1024u)
+        --nw;
+#define ATG_PACK(TT, W)                                                                            \
+    hipLaunchKernelGGL((k_frame_pack<TT, false, W>), dim3(rest), dim3(64 * W), lds, s, p, nreg,    \
+                       (const TT *)pcm, frames, tracks, sub, fd, out, err)
+#define ATG_PACK_T(TT)                                                                             \
+    switch (nw) {                                                                                  \
+    case 4: ATG_PACK(TT, 4); break;                                                                \
+    case 3: ATG_PACK(TT, 3); break;                                                                \
+    case 2: ATG_PACK(TT, 2); break;                                                                \
+    default: ATG_PACK(TT, 1); break;                                                               \
+    }
+    if (fmt == 0) {
+        ATG_PACK_T(int16_t)
+    } else {
+        ATG_PACK_T(int32_t)
+    }
+#undef ATG_PACK_T
+#undef ATG_PACK
     return hipGetLastError();
 }
 
