@@ -1859,10 +1859,13 @@ __device__ __forceinline__ uint2 pack4_lo(const int32_t (&s)[4])
     return pack4(l);
 }
 
-template <int D, bool BIG>
+// CHK: the codes' range is not bounded in advance; the biased ~r (x) are
+// kept in [xmn, xmx] for the caller's check (max3 / min3, one op a sample)
+template <int D, bool BIG, bool CHK>
 __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const int (&cp)[14],
                                          int seed_h, int seed_l, int sa_v, int sb_v, bool lane0,
-                                         int order, uint32_t (&u)[ATG_RUN], uint32_t &sabs)
+                                         int order, uint32_t (&u)[ATG_RUN], uint32_t &sabs,
+                                         uint32_t &xmx, uint32_t &xmn)
 {
     int tap0 = cp[0];
     asm volatile("v_mov_b32 %0, %0" : "+v"(tap0));
@@ -1911,32 +1914,45 @@ __device__ __forceinline__ void pass1_hl(const uint32_t *__restrict__ run, const
                 u[i] = x;
                 sad_acc(sa, x, bm1);
             }
+            if (CHK) {
+                const int i = 16 * c + ii;
+                xmx = max(xmx, max(u[i], u[i + 1]));
+                xmn = min(xmn, min(u[i], u[i + 1]));
+            }
         }
     }
     sabs = sa;
 }
 
-template <bool BIG>
+template <bool BIG, bool CHK>
 __device__ __forceinline__ void pass1_hl_any(const uint32_t *__restrict__ run, const int (&cq)[14],
                                              int seed_h, int seed_l, int sa_v, int sb_v,
                                              bool lane0, int order, uint32_t (&u)[ATG_RUN],
-                                             uint32_t &sabs)
+                                             uint32_t &sabs, uint32_t &xmx, uint32_t &xmn)
 {
+#define ATG_P1HL(D)                                                                                \
+    pass1_hl<D, BIG, CHK>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs, xmx, xmn)
     switch (order / 2 + 1) {
-    case 1: pass1_hl<1, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    case 2: pass1_hl<2, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    case 3: pass1_hl<3, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    case 4: pass1_hl<4, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    case 5: pass1_hl<5, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    case 6: pass1_hl<6, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
-    default: pass1_hl<7, BIG>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, sabs); break;
+    case 1: ATG_P1HL(1); break;
+    case 2: ATG_P1HL(2); break;
+    case 3: ATG_P1HL(3); break;
+    case 4: ATG_P1HL(4); break;
+    case 5: ATG_P1HL(5); break;
+    case 6: ATG_P1HL(6); break;
+    default: ATG_P1HL(7); break;
     }
+#undef ATG_P1HL
 }
 
-// one predictor on the hi/lo images (caller checked the bounds)
+// one predictor on the hi/lo images (caller checked that A and B are
+// exact).  CHK: the caller could not bound the codes below 2^26 in advance
+// (loud 24-bit audio: the bound |s| (1 + sum|c| / 2^sh) is far above the
+// residuals a predictor leaves); pass 1 checks every ~r instead, and
+// *wide = true (nothing evaluated) when one lies outside [-2^25, 2^25)
+template <bool CHK>
 __device__ __forceinline__ Eval16 eval_fold_hl(const uint32_t *__restrict__ run, const RunCtx &c,
                                                const uint32_t (&cw)[7], int order, int sh,
-                                               uint32_t w, uint32_t thr)
+                                               uint32_t w, uint32_t thr, bool *wide)
 {
     int cq[14];
     cq[0] = (int)((cw[0] & 0xFFFFu) | ((uint32_t)(-(1 << sh)) << 16));
@@ -1956,11 +1972,20 @@ __device__ __forceinline__ Eval16 eval_fold_hl(const uint32_t *__restrict__ run,
     const bool lane0 = c.lane == 0;
     const int warm = lane0 ? order : 0;
     uint32_t u[ATG_RUN];
-    uint32_t lane_sum;
+    uint32_t lane_sum, xmx = 0u, xmn = 0xFFFFFFFFu;
     if (big)
-        pass1_hl_any<true>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
+        pass1_hl_any<true, CHK>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+                                xmx, xmn);
     else
-        pass1_hl_any<false>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum);
+        pass1_hl_any<false, CHK>(run, cq, seed_h, seed_l, sa_v, sb_v, lane0, order, u, lane_sum,
+                                 xmx, xmn);
+    // x = ~r + 2^31: ~r in [-2^25, 2^25) <=> x - (2^31 - 2^25) < 2^26, so
+    // every zig-zag code is below 2^26 as eval_tail's sums need
+    if (CHK && __ballot(xmx - 0x7E000000u >= (1u << 26) || xmn < 0x7E000000u) != 0ull) {
+        *wide = true;
+        Eval16 ev;
+        return ev;
+    }
     return eval_tail(lane_sum, u, c, order, warm, thr, 0x80000000u);
 }
 
@@ -2090,9 +2115,12 @@ __device__ __forceinline__ void pred_job_hl(const FlacParams &p, uint32_t N,
             thr = best > hh ? best - hh : 0u;
     }
     Eval16 ev;
+    bool wide = !fold_ok;
     if (fold_ok && 2u * rbound + 1u < (1ull << 26))
-        ev = eval_fold_hl(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr);
-    else
+        ev = eval_fold_hl<false>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr, &wide);
+    else if (fold_ok)
+        ev = eval_fold_hl<true>(run_of(img, lane), c, cw, (int)o, shift, ci.w, thr, &wide);
+    if (wide)
         ev = eval_wide<2>(img, c, cw, (int)o, shift, ci.w);
     if (!is_fixed && ev.bits != K2F_PRUNED && lane == 0)
         atomicMin(&res->best_lpc, hdr + ev.bits);

@@ -231,7 +231,11 @@ __device__ __forceinline__ PartSel select_fast32(uint32_t lane_sum, uint32_t ord
     }
     r.k_own = ko;
     r.k_lane = ko; // N = 4096: no partition is shorter than the order
-    r.method = 0;  // max_rice <= 14 on this path
-    r.hdr_bits = 6u + (1u << best_p) * 4u;
+    // RICE2 (5-bit parameters) once a chosen k passes 14, after the choice,
+    // as select_partitions_t (wide samples: the 16-bit paths cap k at 14)
+    r.method = 0;
+    if (c.max_rice > 14u)
+        r.method = wave_max_u32(ko) > 14u ? 1u : 0u;
+    r.hdr_bits = 6u + (1u << best_p) * (r.method ? 5u : 4u);
     return r;
 }

@@ -1,6 +1,14 @@
+#!/bin/bash
+# GPU-box recipe: A/B of the encoder on config-5-shaped batches
+# (tools/pack_probe.py: synchronous kernel times, image digest) between the
+# product library and abl/libatgpu_old.so (the previous commit's objects,
+# linked here), then the wide-sample parity suites.
 set -e -o pipefail
-mkdir -p gpurun_out/r6az
+OUT=gpurun_out/${1:-packab}
+mkdir -p $OUT
 for cfg in "--channels 6 --bits 24" "--channels 2 --bits 24" "--channels 8 --bits 16"; do
-  timeout -k 10 240 python -u tools/pack_probe.py $cfg >> gpurun_out/r6az/probe.jsonl 2>>gpurun_out/r6az/err.log
-  ATGPU_LIB=abl/libatgpu_old.so timeout -k 10 240 python -u tools/pack_probe.py $cfg >> gpurun_out/r6az/probe.jsonl 2>>gpurun_out/r6az/err.log
+  timeout -k 10 240 python -u tools/pack_probe.py $cfg >> $OUT/probe.jsonl 2>>$OUT/err.log
+  ATGPU_LIB=abl/libatgpu_old.so timeout -k 10 240 python -u tools/pack_probe.py $cfg >> $OUT/probe.jsonl 2>>$OUT/err.log
 done
+timeout -k 10 600 python -u -m pytest -x -q --timeout 120 --timeout-method thread -m gpu \
+    tests/test_gpu_hl_range.py tests/test_gpu_flac.py tests/test_gpu_flac_big.py > $OUT/pytest.log 2>&1
