@@ -437,6 +437,7 @@ struct Eval16 {
 
 // After pass 1 (every predictor form): the lower-bound pruning and the
 // partition search; false: pruned (ev says so)
+template <bool RICE2 = false>
 __device__ __forceinline__ bool eval_select(uint32_t lane_sum, const RunCtx &c, int order, int warm,
                                             uint32_t thr, Eval16 &ev)
 {
@@ -451,7 +452,7 @@ __device__ __forceinline__ bool eval_select(uint32_t lane_sum, const RunCtx &c, 
         return false;
     }
     if (wave_all(lane_sum < (1u << 25)))
-        ev.sel = select_fast32(lane_sum, (uint32_t)order, c);
+        ev.sel = select_fast32<RICE2>(lane_sum, (uint32_t)order, c);
     else
         ev.sel = select_partitions((uint64_t)lane_sum, (uint32_t)order, c, false);
     return true;
@@ -503,7 +504,7 @@ __device__ __forceinline__ Eval16 eval_tail(uint32_t lane_sum, const uint32_t (&
                                             uint32_t bias)
 {
     Eval16 ev;
-    if (!eval_select(lane_sum, c, order, warm, thr, ev))
+    if (!eval_select<true>(lane_sum, c, order, warm, thr, ev)) // wide samples: RICE2
         return ev;
     const uint32_t kv = ev.sel.k_lane ? ev.sel.k_lane - 1u : 0u;
     uint32_t sh2 = 0;

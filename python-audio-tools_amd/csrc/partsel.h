@@ -174,6 +174,9 @@ __device__ __forceinline__ uint32_t est32(uint32_t plen, uint32_t bl, uint32_t s
     return 4u + ((sum << 1) >> k) + (k + 1u) * plen - (plen >> 1);
 }
 
+// RICE2: the caller's samples may be wider than 16 bits (max_rice 30); the
+// 16-bit searches (max_rice 14) leave the method test out
+template <bool RICE2 = false>
 __device__ __forceinline__ PartSel select_fast32(uint32_t lane_sum, uint32_t order, const RunCtx &c)
 {
     const int lane = c.lane;
@@ -232,9 +235,9 @@ __device__ __forceinline__ PartSel select_fast32(uint32_t lane_sum, uint32_t ord
     r.k_own = ko;
     r.k_lane = ko; // N = 4096: no partition is shorter than the order
     // RICE2 (5-bit parameters) once a chosen k passes 14, after the choice,
-    // as select_partitions_t (wide samples: the 16-bit paths cap k at 14)
+    // as select_partitions_t
     r.method = 0;
-    if (c.max_rice > 14u)
+    if (RICE2 && c.max_rice > 14u)
         r.method = wave_max_u32(ko) > 14u ? 1u : 0u;
     r.hdr_bits = 6u + (1u << best_p) * (r.method ? 5u : 4u);
     return r;
