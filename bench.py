@@ -92,8 +92,12 @@ def parse_args(argv=None):
                     help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
                          "hashes are rolled)")
     ap.add_argument("--chain-decoders", type=int, default=3,
-                    help="config-5 chain leg: ALAC decoders (PCM buffers) the decode thread "
+                    help="config-5 chain leg: ALAC decoders (PCM buffers) each decode thread "
                          "cycles through")
+    ap.add_argument("--chain-decode-threads", type=int, default=1,
+                    help="config-5 chain leg: decode threads, batch k on thread k mod T (T "
+                         "decodes at once; 2 and 3 measured 34.7-35.1 and 32.9 ms per step "
+                         "against 33.4 for 1: the device is already full)")
     ap.add_argument("--chain-md5", choices=("auto", "gpu", "host"), default="auto",
                     help="config-5 chain leg: where the FLAC batches' MD5 runs (the engine's "
                          "choice, rolled GPU chains, or host threads)")
@@ -732,15 +736,17 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
             frameset_bytes=fsb[r.first_frameset:r.first_frameset + r.n_framesets]))
     alac_bytes = sum(int(r.bytes) for r in ares)
     nbytes = max(int(r.out_offset + r.bytes) for r in ares)
-    # the pipeline: a decode thread runs the next
-    # batches' ALAC decodes on n_dec decoders (each owns its PCM buffer; three
-    # let it run two batches ahead) while the main thread resamples batch k
-    # and enqueues its FLAC encode; ctypes releases the GIL inside every
-    # library call, so the GPU sees the ALAC kernels beside the resampler's
-    # and the encoder's.  A decoder is handed back once the (synchronous)
-    # resample has read its buffer.
+    # the pipeline: n_thr decode threads run the next
+    # batches' ALAC decodes (batch k on thread k mod n_thr), each on n_dec
+    # decoders of its own (each owns its PCM buffer; three let a thread run
+    # two of its batches ahead), while the main thread resamples batch k and
+    # enqueues its FLAC encode; ctypes releases the GIL inside every library
+    # call, so the GPU sees the ALAC kernels of n_thr batches beside the
+    # resampler's and the encoder's.  A decoder is handed back once the
+    # (synchronous) resample has read its buffer.
     n_dec = max(2, args.chain_decoders)
-    adecs = [_atgpu.AlacDecoder(local) for _ in range(n_dec)]
+    n_thr = max(1, args.chain_decode_threads)
+    adecs = [_atgpu.AlacDecoder(local) for _ in range(n_dec * n_thr)]
     rtracks = [(k * n_in, n_in, rin, rout) for k in range(n_tracks)]
     n_out = _atgpu.resample_output_frames(n_in, ch, rin, rout)
     # `depth` resampled-PCM and FLAC buffers: batch k is waited once batch
@@ -766,28 +772,35 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
 
     torch.cuda.synchronize()
 
-    def decode_thread(first, count, free, ready):
+    def decode_thread(ks, free, ready):
         try:
-            for k in range(first, first + count):
+            for k in ks:
                 i = free.get()
+                if i is None:  # the main thread gave up
+                    return
                 dres, d_pcm, nsamp = adecs[i].decode_device(alac.data_ptr(), nbytes, dtracks)
                 ready.put((k, i, dres, d_pcm, nsamp))
         except BaseException as e:  # re-raised on the main thread
             ready.put(e)
 
     def run(first, count, timed):
-        free, ready = queue.Queue(), queue.Queue()
-        for i in range(n_dec):
-            free.put(i)
-        th = threading.Thread(target=decode_thread, args=(first, count, free, ready),
-                              daemon=True)
-        th.start()
+        frees = [queue.Queue() for _ in range(n_thr)]
+        readies = [queue.Queue() for _ in range(n_thr)]
+        for j in range(n_thr):
+            for i in range(j * n_dec, (j + 1) * n_dec):
+                frees[j].put(i)
+        ths = [threading.Thread(target=decode_thread,
+                                args=(range(first + j, first + count, n_thr), frees[j],
+                                      readies[j]), daemon=True) for j in range(n_thr)]
+        for th in ths:
+            th.start()
         try:
-            for _ in range(count):
-                item = ready.get()
+            for kk in range(count):
+                item = readies[kk % n_thr].get()
                 if isinstance(item, BaseException):
                     raise item
                 k, i, dres, d_pcm, nsamp = item
+                free = frees[kk % n_thr]
                 # the resampler reads n_in frames per track at fixed offsets:
                 # only a complete decode may feed it
                 if nsamp != src.numel() or any(r.status or r.pcm_frames != n_in for r in dres):
@@ -821,7 +834,10 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
                         key = name if name.startswith("flac_") else "flac_" + name
                         kt[key] = kt.get(key, 0.0) + v / args.steps
         finally:
-            th.join()
+            for f in frees:
+                f.put(None)  # a thread still waiting for a decoder stops
+            for th in ths:
+                th.join()
 
     if args.warmup:
         run(0, args.warmup, False)
@@ -851,8 +867,8 @@ def chain_leg(args, torch, dist, world, device, barrier, threads, verify):
                       "channels": ch, "bits": bps, "rates": "%d -> %d" % (rin, rout),
                       "alac_bytes": alac_bytes, "flac_bytes": flac_bytes,
                       "flac_frames": n_flac,
-                      "pipeline": "decode thread (%d ALAC decoders) beside resample + FLAC "
-                                  "encode, %d FLAC batches in flight" % (n_dec, depth)},
+                      "pipeline": "%d decode threads (%d ALAC decoders each) beside resample + "
+                                  "FLAC encode, %d FLAC batches in flight" % (n_thr, n_dec, depth)},
            "kernel_ms": {k: round(v, 4) for k, v in kt.items()},
            "verified_alac_lossless": bool(dec_ok and lossless),
            "alac_decode_status": sorted({int(r.status) for r in dres}),
