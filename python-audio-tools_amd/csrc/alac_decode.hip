@@ -16,8 +16,9 @@
 //                      blocks (counting, no prediction) -- and records where
 //                      each channel's data lies, the frameset length and
 //                      status.
-//   K2 k_adec_chain    lane per track, twice: the read() walk from the
-//                      start position with remaining_frames; a frameset
+//   K2 k_adec_chain    wave per track, twice: the read() walk from the
+//                      start position with remaining_frames (64 chained
+//                      predictions a step, then serially); a frameset
 //                      whose position the prediction missed (a damaged or
 //                      absent stsz) is parsed inline, so the walk is always
 //                      the reference's.  Pass 1 counts, a host prefix places
@@ -40,12 +41,12 @@
 #include "alac_common.h"
 
 // Active lanes per 64-thread block of the walk kernels.  The read() chain
-// walk (one lane per track: 64 lanes for config 5) runs one track per wave:
-// 3.6 -> 1.5 ms, the lanes no longer wait on each other's branches.  The
+// walk runs one track per wave (it was one track per lane: 3.6 -> 1.5 ms,
+// then a wave's lanes check 64 chained predictions at once).  The
 // frameset parse and the channel restore stay at 64: 16 and 32 lanes a
 // wave were slower (17.6 -> 23.4 ms, 12.6 -> 17.1 ms; 8 and 16 slower
 // still), their waves already cover the SIMDs' latency
-constexpr uint32_t kAdecParseLpw = 64, kAdecChainLpw = 1, kAdecChannelLpw = 64;
+constexpr uint32_t kAdecParseLpw = 64, kAdecChannelLpw = 64;
 // device bytes the parse may fill with a batch's residuals (config 5: 30 k
 // framesets x 6 channels x 4096 x 4 B = 2.9 GB)
 constexpr uint64_t kResidMax = 12ull << 30;
@@ -315,7 +316,29 @@ __global__ __launch_bounds__(64) void k_adec_parse(const uint32_t *__restrict__ 
     recs[i] = F;
 }
 
-// K2: the read() walk per track (alac.c:183-254, remaining_frames)
+// exclusive prefix sum over the wave
+template <typename V>
+__device__ __forceinline__ V wave_excl_sum(V v, int lane)
+{
+    V x = v;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const V y = __shfl_up(x, d, 64);
+        x += lane >= d ? y : (V)0;
+    }
+    return x - v;
+}
+
+// K2: the read() walk per track (alac.c:183-254, remaining_frames), a wave
+// per track.  While the predictions chain -- each starts where the one
+// before it ends and parsed without error -- the wave takes 64 framesets a
+// step: a lane per frameset checks its link and its share of
+// remaining_frames, prefix sums place the counts (and in pass 2 the dense
+// records and channel jobs), and the walk advances past the first lane
+// that does not qualify.  From there lane 0 walks on serially, as before
+// (a missed prediction is parsed inline, a status stops the track).  The
+// serial walk alone was a chain of dependent loads per frameset (its
+// position comes from the record before), ~1.7 ms per pass for config 5.
 __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ w,
                                                    const ADTrack *__restrict__ tr, uint32_t nt,
                                                    const uint64_t *__restrict__ pred_start,
@@ -324,15 +347,67 @@ __global__ __launch_bounds__(64) void k_adec_chain(const uint32_t *__restrict__ 
                                                    AFs *__restrict__ dense,
                                                    uint2 *__restrict__ jobs)
 {
-    if (threadIdx.x >= kAdecChainLpw)
-        return;
-    const uint32_t t = blockIdx.x * kAdecChainLpw + threadIdx.x;
+    const uint32_t t = blockIdx.x;
+    const int lane = (int)threadIdx.x;
     if (t >= nt)
         return;
     const ADTrack T = tr[t];
     uint64_t pos = T.start, remaining = T.remaining, pcm = 0;
     uint32_t nfs = 0, k = 0, njob = 0, max_n0 = 0;
     int32_t status = AD_OK;
+    while (remaining && k < T.pred_n) {
+        const uint32_t idx = k + (uint32_t)lane;
+        const bool valid = idx < T.pred_n;
+        uint64_t ps = ~0ull, fend = 0;
+        uint32_t n0 = 0, nch = 0;
+        int32_t st = AD_IO_ERROR;
+        if (valid) {
+            const AFs &R = recs[T.pred_first + idx];
+            ps = pred_start[T.pred_first + idx];
+            st = R.status;
+            n0 = R.n0;
+            nch = R.nch;
+            fend = R.start + R.bytes;
+        }
+        uint64_t at = __shfl_up(fend, 1, 64);
+        at = lane == 0 ? pos : at;
+        const uint64_t before = wave_excl_sum<uint64_t>((uint64_t)n0, lane);
+        const uint32_t jbefore = wave_excl_sum<uint32_t>(nch, lane);
+        const bool take = valid && ps == at && st == AD_OK && before < remaining;
+        const uint64_t bad = __ballot(!take);
+        const uint32_t m = bad ? (uint32_t)__ffsll((long long)bad) - 1u : 64u;
+        if (pass == 2 && (uint32_t)lane < m) {
+            AFs F = recs[T.pred_first + idx];
+            F.track = t;
+            F.pcm_start = T.pcm_base + (pcm + before) * T.channels;
+            F.job0 = T.job_base + njob + jbefore;
+            dense[T.fs_base + nfs + (uint32_t)lane] = F;
+            for (uint32_t c = 0; c < F.nch; ++c)
+                jobs[T.job_base + njob + jbefore + c] =
+                    make_uint2((uint32_t)(T.fs_base + nfs + (uint32_t)lane), c);
+        }
+        if (m == 0u)
+            break;
+        // the state after lanes [0, m), from lane m - 1
+        const uint64_t s_n0 = __shfl(before + n0, (int)m - 1, 64);
+        const uint32_t s_nch = __shfl(jbefore + nch, (int)m - 1, 64);
+        const uint64_t end_m = __shfl(fend, (int)m - 1, 64);
+        uint32_t mx = (uint32_t)lane < m ? n0 : 0u;
+#pragma unroll
+        for (int d = 32; d >= 1; d >>= 1)
+            mx = max(mx, (uint32_t)__shfl_xor((int)mx, d, 64));
+        max_n0 = max(max_n0, mx);
+        remaining = remaining > s_n0 ? remaining - s_n0 : 0u;
+        pcm += s_n0;
+        njob += s_nch;
+        nfs += m;
+        pos = end_m;
+        k += m;
+        if (m < 64u)
+            break;
+    }
+    if (lane != 0)
+        return;
     while (remaining) {
         // the prediction for this position, if any (predictions ascend)
         while (k < T.pred_n && pred_start[T.pred_first + k] < pos)
@@ -1003,7 +1078,7 @@ static atg_status run_adecode(atg_alac_decoder *d, const uint8_t *d_data, uint64
                            res_fs, res_stride);
     ADHIP(hipGetLastError());
     ADHIP(hipEventRecord(d->ev[1], s));
-    const dim3 tg((n + kAdecChainLpw - 1) / kAdecChainLpw);
+    const dim3 tg(n); // a wave per track
     if (n)
         hipLaunchKernelGGL(k_adec_chain, tg, dim3(64), 0, s, w, dtr, n,
                            (const uint64_t *)d->pstart.p, (const AFs *)d->recs.p,
