@@ -88,9 +88,10 @@ def parse_args(argv=None):
     ap.add_argument("--chain-tracks", type=int, default=64,
                     help="config-5 chain leg: 192 kHz 5.1 tracks per GPU")
     ap.add_argument("--chain-seconds", type=int, default=10)
-    ap.add_argument("--chain-inflight", type=int, default=4,
-                    help="config-5 chain leg: FLAC batches in flight (from 4 on the MD5 "
-                         "hashes are rolled)")
+    ap.add_argument("--chain-inflight", type=int, default=3,
+                    help="config-5 chain leg: FLAC batches in flight (3: 31.7-32.0 ms per "
+                         "step, 4: 33.0-33.1, 5-6 slower; with the MD5 on the host no "
+                         "GPU chains need hiding; from 4 on GPU chains are rolled)")
     ap.add_argument("--chain-decoders", type=int, default=3,
                     help="config-5 chain leg: ALAC decoders (PCM buffers) each decode thread "
                          "cycles through")
