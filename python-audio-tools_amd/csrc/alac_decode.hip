@@ -687,7 +687,14 @@ __global__ __launch_bounds__(64) void k_adec_channel(const uint32_t *__restrict_
 }
 
 // K4: decorrelate (alac.c:1237-1259), prepend LSBs (:930-941), wave order
-// (:709-816), interleave
+// (:709-816), interleave.  Per 1024 samples of the frameset: a thread takes
+// four consecutive samples of every channel (16-byte loads from the planar
+// slots), writes them in output order into an LDS tile, and the block
+// copies the tile out as one contiguous run of the interleaved PCM
+// (consecutive threads, consecutive words), whatever the frameset's
+// alignment.
+constexpr uint32_t kIlvTile = 1024; // samples per tile (x 8 channels x 4 bytes = 32 KB)
+
 __global__ __launch_bounds__(256) void k_adec_interleave(const uint32_t *__restrict__ w,
                                                          const ADTrack *__restrict__ tr,
                                                          const AFs *__restrict__ dense,
@@ -695,49 +702,73 @@ __global__ __launch_bounds__(256) void k_adec_interleave(const uint32_t *__restr
                                                          uint32_t pstride,
                                                          int32_t *__restrict__ pcm)
 {
+    __shared__ int32_t tile[kIlvTile * 8];
+    __shared__ uint8_t inv[16]; // ALAC channel -> output position
     const AFs &F = dense[blockIdx.x];
     const ADTrack T = tr[F.track];
-    const uint32_t nch = F.nch, n0 = F.n0;
+    const uint32_t nch = F.nch, n0 = F.n0, tid = threadIdx.x;
     static const uint8_t M[9][8] = {{0}, {0}, {0, 1}, {1, 2, 0}, {1, 2, 0, 3}, {1, 2, 0, 3, 4},
                                     {1, 2, 0, 5, 3, 4}, {1, 2, 0, 6, 3, 4, 5},
                                     {3, 4, 0, 7, 5, 6, 1, 2}};
+    if (tid < 16)
+        inv[tid] = (uint8_t)tid;
+    __syncthreads();
+    if (nch <= 8 && tid < nch)
+        inv[M[nch][tid]] = (uint8_t)tid;
+    __syncthreads();
     const int32_t *src = planar + F.job0 * pstride; // channel k at src + k * pstride
     int32_t *dst = pcm + F.pcm_start;
     const uint64_t b0 = F.start * 8;
-    for (uint32_t i = threadIdx.x; i < n0; i += blockDim.x) {
-        int32_t v[8];
-        uint32_t ch = 0;
-        for (uint32_t e = 0; e < F.nelem; ++e) {
-            const AElem E = F.e[e];
-            int32_t a = src[(uint64_t)ch * pstride + i];
-            int32_t b = E.cc == 2 ? src[(uint64_t)(ch + 1) * pstride + i] : 0;
-            if (!E.uncompressed) {
-                if (E.cc == 2 && E.lw > 0) {
-                    int64_t t = (int64_t)(b * (int32_t)E.lw);
-                    t >>= (E.shift & 63u); // x86 sar count masking (the reference build)
-                    const int32_t rs = a - (int32_t)t;
-                    a = b + rs;
-                    b = rs;
-                }
-                if (E.lsbs && i < E.N) {
-                    const uint32_t lb = E.lsbs * 8u;
-                    ABitR r;
-                    r.init(w, b0 + E.lsb_bit + ((uint64_t)i * E.cc) * lb, T.end * 8);
-                    const int32_t la = (int32_t)r.get(lb);
-                    a = (int32_t)((uint32_t)a << lb) | la;
-                    if (E.cc == 2) {
-                        const int32_t lb2 = (int32_t)r.get(lb);
-                        b = (int32_t)((uint32_t)b << lb) | lb2;
+    for (uint32_t base = 0; base < n0; base += kIlvTile) {
+        const uint32_t cnt = min(kIlvTile, n0 - base);
+        const uint32_t i0 = base + 4u * tid; // this thread's samples i0 .. i0 + 3
+        if (4u * tid < cnt) {
+            uint32_t ch = 0;
+            for (uint32_t e = 0; e < F.nelem; ++e) {
+                const AElem E = F.e[e];
+                // a slot holds pstride (a multiple of 4, >= n0) values: the
+                // 16-byte loads stay inside it past n0
+                const int4 A = *(const int4 *)(src + (uint64_t)ch * pstride + i0);
+                const int4 Bv = E.cc == 2 ? *(const int4 *)(src + (uint64_t)(ch + 1) * pstride + i0)
+                                          : make_int4(0, 0, 0, 0);
+                int32_t a[4] = {A.x, A.y, A.z, A.w}, b[4] = {Bv.x, Bv.y, Bv.z, Bv.w};
+                const uint32_t oa = inv[ch], ob = inv[ch + 1u];
+#pragma unroll
+                for (uint32_t q = 0; q < 4; ++q) {
+                    const uint32_t i = i0 + q;
+                    if (!E.uncompressed) {
+                        if (E.cc == 2 && E.lw > 0) {
+                            int64_t t = (int64_t)(b[q] * (int32_t)E.lw);
+                            t >>= (E.shift & 63u); // x86 sar count masking (the reference build)
+                            const int32_t rs = a[q] - (int32_t)t;
+                            a[q] = b[q] + rs;
+                            b[q] = rs;
+                        }
+                        if (E.lsbs && i < E.N) {
+                            const uint32_t lb = E.lsbs * 8u;
+                            ABitR r;
+                            r.init(w, b0 + E.lsb_bit + ((uint64_t)i * E.cc) * lb, T.end * 8);
+                            const int32_t la = (int32_t)r.get(lb);
+                            a[q] = (int32_t)((uint32_t)a[q] << lb) | la;
+                            if (E.cc == 2) {
+                                const int32_t lb2 = (int32_t)r.get(lb);
+                                b[q] = (int32_t)((uint32_t)b[q] << lb) | lb2;
+                            }
+                        }
                     }
+                    const uint32_t row = (4u * tid + q) * nch;
+                    tile[row + oa] = a[q];
+                    if (E.cc == 2)
+                        tile[row + ob] = b[q];
                 }
+                ch += E.cc;
             }
-            v[ch] = a;
-            if (E.cc == 2)
-                v[ch + 1] = b;
-            ch += E.cc;
         }
-        for (uint32_t c = 0; c < nch; ++c)
-            dst[(uint64_t)i * nch + c] = v[nch <= 8 ? M[nch][c] : c];
+        __syncthreads();
+        int32_t *__restrict__ out = dst + (uint64_t)base * nch;
+        for (uint32_t q = tid; q < cnt * nch; q += blockDim.x)
+            out[q] = tile[q];
+        __syncthreads();
     }
 }
 
