@@ -207,7 +207,8 @@ def test_reference_fixture():
     assert hashlib.md5(b).hexdigest() == f["pcm_md5"]
 
 
-@pytest.mark.parametrize("ch,bps", [(2, 16), (1, 24), (6, 24), (8, 16), (5, 16)])
+@pytest.mark.parametrize("ch,bps", [(2, 16), (1, 24), (6, 24), (8, 16), (5, 16), (3, 24), (4, 16),
+                                    (7, 24), (8, 24)])
 def test_round_trip_gpu_encode_decode(ch, bps):
     from audiotools import decoders, m4a
     pcms = [signals.make(k, 4096 * (2 + i) + 13 * i, ch, bps, seed=i)
