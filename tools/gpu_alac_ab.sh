@@ -1,6 +1,8 @@
 #!/bin/bash
 # GPU-box recipe: ALAC A/B between the product library and abl/libatgpu_{A,B}.so
-# (variants linked from the product's objects), suites then chain runs.
+# (variants: a modified alac_decode.hip compiled here and linked with the
+# product's other objects, python-audio-tools_amd/csrc/obj/*.o), suites
+# then chain runs.
 set -e -o pipefail
 OUT=gpurun_out/r6bu
 mkdir -p $OUT

@@ -1,8 +1,11 @@
 #!/bin/bash
 # GPU-box recipe: A/B of the encoder on config-5-shaped batches
 # (tools/pack_probe.py: synchronous kernel times, image digest) between the
-# product library and abl/libatgpu_old.so (the previous commit's objects,
-# linked here), then the wide-sample parity suites.
+# product library and abl/libatgpu_old.so, then the wide-sample parity
+# suites.  Build the baseline in this container before the call, e.g. from
+# the previous commit's objects:
+#   hipcc --offload-arch=gfx950 -shared -fPIC -o abl/libatgpu_old.so \
+#       python-audio-tools_amd/csrc/obj/*.o   (before rebuilding the product)
 set -e -o pipefail
 OUT=gpurun_out/${1:-packab}
 mkdir -p $OUT
